@@ -1,0 +1,53 @@
+// Shared helpers for the gfx950 kernels of libsgg.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include "../../include/sgg.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace sgg {
+
+constexpr int kWave = 64;      // CDNA wavefront
+constexpr int kHidden = 512;   // pooling MLP hidden width (hard-coded, models.py:473)
+
+// last error, per calling host thread
+void set_error(const char* fmt, ...);
+
+#define SGG_CHECK_ARG(cond, ...)            \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::sgg::set_error(__VA_ARGS__);        \
+      return SGG_E_ARG;                     \
+    }                                       \
+  } while (0)
+
+#define SGG_RETURN_LAUNCH(name)                                          \
+  do {                                                                   \
+    hipError_t e_ = hipGetLastError();                                   \
+    if (e_ != hipSuccess) {                                              \
+      ::sgg::set_error("%s: launch failed: %s", name, hipGetErrorString(e_)); \
+      return (int)e_;                                                    \
+    }                                                                    \
+    return 0;                                                            \
+  } while (0)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ float elu(float x) { return x > 0.f ? x : expm1f(x); }
+// derivative of ELU(alpha = 1) from its input
+__device__ __forceinline__ float elu_grad(float x) { return x > 0.f ? 1.f : expf(x); }
+
+}  // namespace sgg

@@ -1,0 +1,106 @@
+// Dense node-feature transform Y = act(X @ W (+ bias)) on fp32 MFMA.
+//
+// v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fmaf chain, no xf32):
+//   A lane map: A[l & 15][l >> 4]    (16 rows x 4 k)
+//   B lane map: B[l >> 4][l & 15]    (4 k x 16 cols)
+//   C/D map   : row = (l >> 4) * 4 + r, col = l & 15   (r = 0..3)
+// Workgroup = 4 waves = 64 rows x 64 cols of Y; each wave owns 16 rows x 64
+// cols (4 accumulator tiles).  K is small on this path (32..144, 512 for the
+// pooling backward), so operands are read straight from L1/L2: the X row
+// fragment is reused across the 4 column tiles in registers, the W fragment
+// is shared by the 4 waves through L1.
+#include "sgg_common.h"
+
+namespace sgg {
+
+template <bool TRANS_W>
+__device__ __forceinline__ float load_w(const float* __restrict__ W, int k, int n, int K, int N) {
+  if (k >= K || n >= N) return 0.f;
+  return TRANS_W ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
+}
+
+template <bool TRANS_W>
+__global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, int ldx,
+                                                 const float* __restrict__ W,
+                                                 const float* __restrict__ bias, float* __restrict__ Y,
+                                                 int ldy, int M, int K, int N, int act) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * 64 + wave * 16;
+  const int col0 = blockIdx.y * 64;
+  const int ar = lane & 15;   // A row / B col within the 16x16 tile
+  const int kq = lane >> 4;   // k within the 4-deep step
+  const int arow = row0 + ar;
+  const bool arow_ok = arow < M;
+  const float* xrow = X + (size_t)(arow_ok ? arow : 0) * ldx;
+
+  floatx4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const bool full_n = col0 + 64 <= N;
+  int k0 = 0;
+  // main loop: 4 MFMA k-steps (16 k) per iteration, no k bounds checks
+  for (; k0 + 16 <= K; k0 += 16) {
+    float a[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a[s] = arow_ok ? xrow[k0 + 4 * s + kq] : 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = k0 + 4 * s + kq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = col0 + 16 * t + ar;
+        float b;
+        if (full_n) b = TRANS_W ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
+        else b = load_w<TRANS_W>(W, k, n, K, N);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b, acc[t], 0, 0, 0);
+      }
+    }
+  }
+  // tail: k bounds-checked
+  for (; k0 < K; k0 += 4) {
+    const int k = k0 + kq;
+    const float a = (arow_ok && k < K) ? xrow[k] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float b = load_w<TRANS_W>(W, k, col0 + 16 * t + ar, K, N);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+    }
+  }
+
+  // epilogue
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n = col0 + 16 * t + ar;
+    if (n >= N) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = row0 + kq * 4 + r;
+      if (m < M) {
+        float v = acc[t][r] + bv;
+        if (act == 1) v = v > 0.f ? v : 0.f;
+        Y[(size_t)m * ldy + n] = v;
+      }
+    }
+  }
+}
+
+}  // namespace sgg
+
+extern "C" int sgg_xw(const float* X, int ldx, const float* W, int trans_w, const float* bias,
+                      float* Y, int ldy, int M, int K, int N, int act, void* stream) {
+  SGG_CHECK_ARG(X && W && Y, "sgg_xw: null pointer");
+  SGG_CHECK_ARG(M >= 0 && K > 0 && N > 0, "sgg_xw: bad sizes M=%d K=%d N=%d", M, K, N);
+  SGG_CHECK_ARG(ldx >= K && ldy >= N, "sgg_xw: bad leading dims ldx=%d ldy=%d", ldx, ldy);
+  SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw: act must be 0 or 1");
+  if (M == 0) return 0;
+  dim3 grid((M + 63) / 64, (N + 63) / 64);
+  hipStream_t s = (hipStream_t)stream;
+  if (trans_w)
+    hipLaunchKernelGGL(sgg::xw_kernel<true>, grid, dim3(256), 0, s, X, ldx, W, bias, Y, ldy, M, K, N, act);
+  else
+    hipLaunchKernelGGL(sgg::xw_kernel<false>, grid, dim3(256), 0, s, X, ldx, W, bias, Y, ldy, M, K, N, act);
+  SGG_RETURN_LAUNCH("sgg_xw");
+}

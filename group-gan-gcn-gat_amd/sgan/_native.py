@@ -1,0 +1,82 @@
+"""ctypes binding of libsgg.so (include/sgg.h).
+
+The product path has NO CPU fallback: if the library is missing, or the
+process has no GPU, every entry point raises.  `torch` is imported first so
+libsgg.so binds to the HIP runtime torch already loaded (same SONAME
+libamdhip64.so.7): one runtime, torch's caching allocator and streams are
+ours.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libsgg.so")
+
+_i = ctypes.c_int
+_f = ctypes.c_float
+_p = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); must mirror include/sgg.h exactly
+SIGNATURES = {
+    "sgg_version": (_i, []),
+    "sgg_last_error": (ctypes.c_char_p, []),
+    "sgg_xw": (_i, [_p, _i, _p, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "sgg_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]),
+    "sgg_pool_bwd_grid": (_i, [_i]),
+    "sgg_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]),
+    "sgg_gat_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _i, _p]),
+    "sgg_gat_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _p, _i, _p, _p, _p, _p]),
+    "sgg_group_index_ws": (_sz, [_i, _i]),
+    "sgg_group_index": (_i, [_p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
+    "sgg_seg_reduce": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i, _p]),
+    "sgg_seg_gather": (_i, [_p, _i, _i, _p, _p, _p, _i, _p, _i, _p]),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib_path():
+    return _LIB_PATH
+
+
+def load(require_gpu=True):
+    """Load libsgg.so (once).  Raises NativeError when it is missing or, with
+    require_gpu, when no HIP device is visible: there is no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise NativeError("libsgg.so not built at %s -- run group-gan-gcn-gat_amd/build_native.py "
+                              "(or __graft_entry__.build())" % _LIB_PATH)
+        lib = ctypes.CDLL(_LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_gpu and not torch.cuda.is_available():
+        raise NativeError("sgan: no HIP device visible; the MI355X kernels have no CPU fallback")
+    return _lib
+
+
+def check(rc, name):
+    if rc != 0:
+        msg = _lib.sgg_last_error().decode(errors="replace")
+        raise NativeError("%s failed (rc=%d): %s" % (name, rc, msg))
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  Asserts device + contiguity
+    of the innermost dim; callers pass explicit leading dimensions."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())

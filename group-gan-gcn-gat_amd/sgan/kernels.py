@@ -1,0 +1,270 @@
+"""Autograd wrappers around the libsgg.so C ABI (include/sgg.h).
+
+Every op launches on torch's current stream through ctypes; forward and
+backward are hand-written HIP kernels, except the parameter-gradient
+reductions over all nodes (X^T dY, column sums), which are plain GEMMs /
+reductions left to rocBLAS via torch.  No op has a CPU path.
+"""
+import torch
+
+from . import _native as N
+
+
+def _lib():
+    return N.load()
+
+
+def _req(t, name, dtype=torch.float32):
+    if not t.is_cuda:
+        raise N.NativeError("%s must be a device tensor (no CPU path)" % name)
+    if t.dtype != dtype:
+        raise N.NativeError("%s must be %s, got %s" % (name, dtype, t.dtype))
+    return t
+
+
+def _rows(t, name):
+    """2-D with unit column stride (row stride is passed as leading dim)."""
+    _req(t, name)
+    if t.dim() != 2 or t.stride(1) != 1:
+        t = t.contiguous()
+    return t
+
+
+# ---------------------------------------------------------------------------
+# dense node transform
+# ---------------------------------------------------------------------------
+def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None):
+    x = _rows(x, "x")
+    w = _req(w, "w").contiguous()
+    M, K = x.shape
+    Nn = w.shape[0] if trans_w else w.shape[1]
+    assert (w.shape[1] if trans_w else w.shape[0]) == K, (x.shape, w.shape, trans_w)
+    if bias is not None:
+        bias = _req(bias, "bias").contiguous()
+        assert bias.numel() == Nn
+    y = out if out is not None else torch.empty(M, Nn, device=x.device, dtype=torch.float32)
+    N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(w), int(bool(trans_w)), N.ptr(bias), N.ptr(y), y.stride(0),
+                          M, K, Nn, int(act), N.stream_ptr()), "sgg_xw")
+    return y
+
+
+class _XW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, trans_w, act):
+        y = xw_raw(x, w, bias, trans_w, act)
+        ctx.trans_w, ctx.act, ctx.has_bias = trans_w, act, bias is not None
+        ctx.save_for_backward(x, w, y if act else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        if ctx.act:
+            dy = dy * (y > 0)
+        dy = dy.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = xw_raw(dy, w, None, not ctx.trans_w, 0)
+        if ctx.needs_input_grad[1]:
+            dw = dy.t().mm(x) if ctx.trans_w else x.t().mm(dy)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(0)
+        return dx, dw, db, None, None
+
+
+def xw(x, w, bias=None, trans_w=False, act=0):
+    """act(x @ w + bias) (trans_w: w stored (N, K), i.e. nn.Linear layout)."""
+    return _XW.apply(x, w, bias, trans_w, act)
+
+
+def linear(x, lin, act=0):
+    """nn.Linear through the MFMA node transform (weight is (out, in))."""
+    return _XW.apply(x, lin.weight, lin.bias, True, act)
+
+
+# ---------------------------------------------------------------------------
+# social pooling
+# ---------------------------------------------------------------------------
+class _Pool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, pos, W1h, A, c, W2, b2, scenes):
+        lib = _lib()
+        h = _rows(h, "h")
+        pos = _req(pos, "pos").contiguous()
+        B = h.shape[0]
+        bn = W2.shape[0]
+        assert pos.shape == (B, 2) and scenes.B == B, (pos.shape, B, scenes.B)
+        W1h = W1h.contiguous()
+        U = xw_raw(h, W1h, c, trans_w=True)                       # B x 512
+        out = torch.empty(B, bn, device=h.device, dtype=torch.float32)
+        am = torch.empty(B, bn, device=h.device, dtype=torch.int32)
+        W2T = W2.t().contiguous()
+        A = A.contiguous()
+        b2 = b2.contiguous()
+        N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2T), N.ptr(b2), N.ptr(scenes.scene_off),
+                                 scenes.S, B, bn, scenes.max_n, N.ptr(out), N.ptr(am), N.stream_ptr()),
+                "sgg_pool_fwd")
+        ctx.scenes = scenes
+        ctx.save_for_backward(h, pos, W1h, A, W2, U, out, am)
+        ctx.mark_non_differentiable(am)
+        return out, am
+
+    @staticmethod
+    def backward(ctx, dout, _dam):
+        lib = _lib()
+        h, pos, W1h, A, W2, U, out, am = ctx.saved_tensors
+        sc = ctx.scenes
+        B, bn = out.shape
+        dout = dout.contiguous()
+        grid = lib.sgg_pool_bwd_grid(sc.S)
+        dU = torch.empty(B, 512, device=h.device, dtype=torch.float32)
+        dW2p = torch.empty(grid, bn, 512, device=h.device, dtype=torch.float32)
+        dAp = torch.empty(grid, 512, 2, device=h.device, dtype=torch.float32)
+        W2c = W2.contiguous()
+        N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2c), N.ptr(out), N.ptr(am), N.ptr(dout),
+                                 N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(dW2p), N.ptr(dAp),
+                                 N.stream_ptr()), "sgg_pool_bwd")
+        dh = xw_raw(dU, W1h, None, trans_w=False) if ctx.needs_input_grad[0] else None
+        dW1h = dU.t().mm(h)
+        dc = dU.sum(0)
+        db2 = (dout * (out > 0)).sum(0)
+        return dh, None, dW1h, dAp.sum(0), dc, dW2p.sum(0), db2, None
+
+
+def social_pool(h, pos, W1h, A, c, W2, b2, scenes):
+    """PoolHiddenNet core (models.py:497-549) -> (B, bn); see sgg_pool_fwd."""
+    out, _ = _Pool.apply(h, pos, W1h, A, c, W2, b2, scenes)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# graph attention
+# ---------------------------------------------------------------------------
+class _GatAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, wh, a, labels, seg_off, nseg, max_seg, alpha, mode, epi):
+        lib = _lib()
+        wh = _req(wh, "wh").contiguous()
+        n, F = wh.shape
+        a = a.contiguous().view(-1)
+        y = torch.zeros(n, F, device=wh.device, dtype=torch.float32)
+        hp = torch.zeros(n, F, device=wh.device, dtype=torch.float32) if epi else None
+        N.check(lib.sgg_gat_fwd(N.ptr(wh), N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, float(alpha), mode,
+                                epi, max_seg, N.ptr(hp), N.ptr(y), F, N.stream_ptr()), "sgg_gat_fwd")
+        ctx.meta = (labels, seg_off, nseg, max_seg, float(alpha), mode, epi)
+        ctx.save_for_backward(wh, a, hp, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib()
+        wh, a, hp, y = ctx.saved_tensors
+        labels, seg_off, nseg, max_seg, alpha, mode, epi = ctx.meta
+        n, F = wh.shape
+        dy = dy.contiguous()
+        dWh = torch.zeros(n, F, device=wh.device, dtype=torch.float32)
+        ds = torch.zeros(n, device=wh.device, dtype=torch.float32)
+        dt = torch.zeros(n, device=wh.device, dtype=torch.float32)
+        N.check(lib.sgg_gat_bwd(N.ptr(wh), N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, alpha, mode, epi,
+                                max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), F, N.ptr(dWh), N.ptr(ds), N.ptr(dt),
+                                N.stream_ptr()), "sgg_gat_bwd")
+        da = torch.cat([wh.t().mv(ds), wh.t().mv(dt)]).view(2 * F, 1)
+        return dWh, da, None, None, None, None, None, None, None
+
+
+def gat_attention(wh, a, alpha, graph, epilogue):
+    """Masked-softmax attention + aggregation + epilogue over `graph`
+    (a SegmentGraph).  epilogue: 0 none, 1 ELU, 2 log_softmax(ELU)."""
+    return _GatAttn.apply(wh, a, graph.labels, graph.seg_off, graph.nseg, graph.max_seg, alpha, graph.mode, epilogue)
+
+
+class SegmentGraph:
+    """Node segments for the attention kernel: mode 0 = label mask inside each
+    scene (intra-group graph), mode 1 = complete graph (inter-group graph)."""
+
+    def __init__(self, seg_off, nseg, max_seg, mode, labels=None):
+        self.seg_off, self.nseg, self.max_seg, self.mode, self.labels = seg_off, nseg, max_seg, mode, labels
+
+
+# ---------------------------------------------------------------------------
+# segmented reduce / gather (group pool, un-pool, GCN aggregation)
+# ---------------------------------------------------------------------------
+def _seg_reduce_raw(x, seg_of_row, row_scale, range_off, seg_range, nseg_dev, cap, mean):
+    x = _rows(x, "x")
+    F = x.shape[1]
+    out = torch.empty(cap, F, device=x.device, dtype=torch.float32)
+    N.check(_lib().sgg_seg_reduce(N.ptr(x), x.stride(0), F, N.ptr(seg_of_row), N.ptr(row_scale), N.ptr(range_off),
+                                  N.ptr(seg_range), N.ptr(nseg_dev), cap, int(mean), N.ptr(out), F, N.stream_ptr()),
+            "sgg_seg_reduce")
+    return out
+
+
+def _seg_gather_raw(src, seg_of_row, row_scale, nrow_dev, n):
+    src = _rows(src, "src")
+    F = src.shape[1]
+    out = torch.empty(n, F, device=src.device, dtype=torch.float32)
+    N.check(_lib().sgg_seg_gather(N.ptr(src), src.stride(0), F, N.ptr(seg_of_row), N.ptr(row_scale),
+                                  N.ptr(nrow_dev), n, N.ptr(out), F, N.stream_ptr()), "sgg_seg_gather")
+    return out
+
+
+class _SegReduce(torch.autograd.Function):
+    """out[k] = post_k * sum_{rows of k} scale_i x_i ; backward gathers with
+    bwd_scale_i = scale_i * post_{seg(i)} (given by the caller)."""
+
+    @staticmethod
+    def forward(ctx, x, seg_of_row, row_scale, range_off, seg_range, nseg_dev, cap, mean, bwd_scale, nrow_dev):
+        ctx.meta = (seg_of_row, bwd_scale, nrow_dev, x.shape[0])
+        return _seg_reduce_raw(x, seg_of_row, row_scale, range_off, seg_range, nseg_dev, cap, mean)
+
+    @staticmethod
+    def backward(ctx, dout):
+        seg_of_row, bwd_scale, nrow_dev, n = ctx.meta
+        dx = _seg_gather_raw(dout, seg_of_row, bwd_scale, nrow_dev, n)
+        return dx, None, None, None, None, None, None, None, None, None
+
+
+class _SegGather(torch.autograd.Function):
+    """out[i] = scale_i * src[seg(i)] ; backward = segment sum of scale_i dout_i."""
+
+    @staticmethod
+    def forward(ctx, src, seg_of_row, row_scale, nrow_dev, n, range_off, seg_range, nseg_dev):
+        ctx.meta = (seg_of_row, row_scale, range_off, seg_range, nseg_dev, src.shape[0])
+        return _seg_gather_raw(src, seg_of_row, row_scale, nrow_dev, n)
+
+    @staticmethod
+    def backward(ctx, dout):
+        seg_of_row, row_scale, range_off, seg_range, nseg_dev, cap = ctx.meta
+        dsrc = _seg_reduce_raw(dout, seg_of_row, row_scale, range_off, seg_range, nseg_dev, cap, 0)
+        return dsrc, None, None, None, None, None, None, None
+
+
+def group_mean(x, groups):
+    """R @ X with R the row-normalised distinct rows of M_intra
+    (models.py:271-280): per-group mean of its members -> (cap, F), rows >= G zero."""
+    sc = groups.scenes
+    return _SegReduce.apply(x, groups.ped_gid, None, sc.scene_off, groups.group_scene, groups.n_groups_dev,
+                            groups.cap, True, groups.ped_inv_size, None)
+
+
+def group_unpool(gx, groups, scale=True):
+    """R^T @ G (models.py:286): ped i receives G[g(i)] / |g(i)| (scale=True) or
+    G[g(i)] (scale=False, the broadcast of the GCN's A @ H)."""
+    sc = groups.scenes
+    rs = groups.ped_inv_size if scale else None
+    return _SegGather.apply(gx, groups.ped_gid, rs, None, sc.B, sc.scene_off, groups.group_scene,
+                            groups.n_groups_dev)
+
+
+def scene_mean_over_groups(gx, groups):
+    """Complete-graph row-normalised A @ H over each scene's groups
+    (models.py:688-694 with A = ones/M): every group row gets the mean of its
+    scene's group rows.  Rows >= G stay zero."""
+    sc = groups.scenes
+    if not hasattr(groups, "_group_inv_ng"):
+        ng = (groups.group_off[1:] - groups.group_off[:-1]).float().clamp(min=1)
+        groups._group_inv_ng = ng.index_select(0, groups.group_scene.long()).reciprocal()
+    sm = _SegReduce.apply(gx, groups.group_scene, None, groups.group_off, None, None, sc.S, True,
+                          groups._group_inv_ng, groups.n_groups_dev)
+    return _SegGather.apply(sm, groups.group_scene, None, groups.n_groups_dev, groups.cap, groups.group_off, None,
+                            None)

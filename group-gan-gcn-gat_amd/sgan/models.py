@@ -1,0 +1,421 @@
+"""sgan.models for MI355X: drop-in TrajectoryGenerator / TrajectoryDiscriminator.
+
+Same classes, constructor keywords, forward() signatures and state-dict keys
+as the reference's sgan/models.py (so scripts/train.py, scripts/evaluate_model.py
+and reference checkpoints work unchanged), but the hot path runs on the
+libsgg.so HIP kernels (sgan/kernels.py):
+
+  - social pooling (PoolHiddenNet)        -> sgg_pool_fwd / sgg_pool_bwd
+  - GAT attention + softmax + aggregate   -> sgg_gat_fwd / sgg_gat_bwd
+  - GCN / GAT node transforms X W, Linear -> sgg_xw (fp32 MFMA)
+  - group structure, R / R^T pooling       -> sgg_group_index, sgg_seg_reduce/gather
+
+Scene bookkeeping is an int32 CSR built once per batch (sgan/scene.py)
+instead of a `.item()` per scene per module.  The LSTMs of the encoder and
+decoder stay on torch (MIOpen) for now.
+
+Extra keyword-only arguments beyond the reference's are optional and default
+to the reference behaviour:
+  TrajectoryGenerator(..., graph='gat'|'gcn')  selects the message-passing
+      module the forward calls ('gat' = the committed forward,
+      models.py:903-905; 'gcn' = the sgan-g-p checkpoint family, :902).
+  forward(..., scenes=SceneIndex)  reuses a precomputed scene index.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import kernels as K
+from .scene import SceneIndex
+
+# ---------------------------------------------------------------------------
+# batch bookkeeping
+# ---------------------------------------------------------------------------
+_SCENE_CACHE = {"sse": None, "ver": None, "dev": None, "idx": None}
+
+
+def scene_index(seq_start_end, device):
+    """SceneIndex of a batch, cached on the identity of the seq_start_end
+    tensor (generator_step calls G best_k times with the same one).  The
+    cache holds a reference to the tensor so its memory cannot be recycled
+    into a different batch while cached."""
+    c = _SCENE_CACHE
+    if c["sse"] is seq_start_end and c["ver"] == seq_start_end._version and c["dev"] == device:
+        return c["idx"]
+    idx = SceneIndex.from_seq_start_end(seq_start_end, device)
+    c.update(sse=seq_start_end, ver=seq_start_end._version, dev=device, idx=idx)
+    return idx
+
+
+def _scenes(seq_start_end, device, scenes):
+    if scenes is not None:
+        return scenes
+    return scene_index(seq_start_end, device)
+
+
+def make_mlp(dim_list, activation="relu", batch_norm=True, dropout=0):
+    """Same layer layout as the reference (models.py:7-20) so state-dict keys
+    (`.0.weight`, `.2.weight`, ...) match; executed by run_mlp."""
+    layers = []
+    for dim_in, dim_out in zip(dim_list[:-1], dim_list[1:]):
+        layers.append(nn.Linear(dim_in, dim_out))
+        if batch_norm:
+            layers.append(nn.BatchNorm1d(dim_out))
+        if activation == "relu":
+            layers.append(nn.ReLU())
+        elif activation == "leakyrelu":
+            layers.append(nn.LeakyReLU())
+        if dropout > 0:
+            layers.append(nn.Dropout(p=dropout))
+    return nn.Sequential(*layers)
+
+
+def run_mlp(seq, x):
+    """Run a make_mlp Sequential with every Linear on the MFMA node transform
+    (ReLU fused into its epilogue)."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.Linear):
+            fuse = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+            x = K.linear(x, m, act=1 if fuse else 0)
+            i += 2 if fuse else 1
+            continue
+        if isinstance(m, nn.BatchNorm1d):
+            x = m(x)
+        else:
+            x = m(x)
+        i += 1
+    return x
+
+
+def get_noise(shape, noise_type):
+    """models.py:23-29: drawn from the HOST torch RNG (same stream as the
+    reference, which draws on the CPU and copies)."""
+    if noise_type == "gaussian":
+        return torch.randn(*shape)
+    if noise_type == "uniform":
+        return torch.rand(*shape).sub_(0.5).mul_(2.0)
+    raise ValueError('Unrecognized noise type "%s"' % noise_type)
+
+
+# ---------------------------------------------------------------------------
+# encoder / decoder (torch LSTM; models.py:32-178)
+# ---------------------------------------------------------------------------
+class Encoder(nn.Module):
+    def __init__(self, embedding_dim=64, h_dim=64, mlp_dim=1024, num_layers=1, dropout=0.0):
+        super().__init__()
+        self.mlp_dim = 1024
+        self.h_dim = h_dim
+        self.embedding_dim = embedding_dim
+        self.num_layers = num_layers
+        self.spatial_embedding = nn.Linear(2, embedding_dim)
+        self.encoder = nn.LSTM(embedding_dim, h_dim, num_layers, dropout=dropout)
+
+    def forward(self, obs_traj):
+        T, B = obs_traj.shape[:2]
+        emb = K.linear(obs_traj.reshape(-1, 2), self.spatial_embedding).view(T, B, self.embedding_dim)
+        z = torch.zeros(self.num_layers, B, self.h_dim, device=obs_traj.device)
+        _, (h, _) = self.encoder(emb, (z, z))
+        return h
+
+
+class Decoder(nn.Module):
+    def __init__(self, seq_len, embedding_dim=64, h_dim=128, mlp_dim=1024, num_layers=1,
+                 pool_every_timestep=True, dropout=0.0, bottleneck_dim=1024, activation="relu",
+                 batch_norm=True, pooling_type="pool_net", neighborhood_size=2.0, grid_size=8):
+        super().__init__()
+        self.seq_len = seq_len
+        self.mlp_dim = mlp_dim
+        self.h_dim = h_dim
+        self.embedding_dim = embedding_dim
+        self.pool_every_timestep = pool_every_timestep
+        self.spatial_embedding = nn.Linear(2, embedding_dim)
+        self.decoder = nn.LSTM(embedding_dim, h_dim, num_layers, dropout=dropout)
+        self.hidden2pos = nn.Linear(h_dim, 2)
+        if pool_every_timestep:
+            if pooling_type == "pool_net":
+                self.pool_net = PoolHiddenNet(embedding_dim=embedding_dim, h_dim=h_dim, mlp_dim=mlp_dim,
+                                              bottleneck_dim=bottleneck_dim, activation=activation,
+                                              batch_norm=batch_norm, dropout=dropout)
+            self.mlp = make_mlp([h_dim + bottleneck_dim, mlp_dim, h_dim], activation=activation,
+                                batch_norm=batch_norm, dropout=dropout)
+
+    def forward(self, last_pos, last_pos_rel, state_tuple, seq_start_end, scenes=None):
+        B = last_pos.size(0)
+        x = K.linear(last_pos_rel, self.spatial_embedding).view(1, B, self.embedding_dim)
+        outs = []
+        for _ in range(self.seq_len):
+            y, state_tuple = self.decoder(x, state_tuple)
+            rel = K.linear(y.view(-1, self.h_dim), self.hidden2pos)
+            curr = rel + last_pos
+            if self.pool_every_timestep:
+                h = state_tuple[0]
+                pool_h = self.pool_net(h, seq_start_end, curr, scenes=scenes)
+                h = run_mlp(self.mlp, torch.cat([h.view(-1, self.h_dim), pool_h], dim=1))
+                state_tuple = (h.unsqueeze(0), state_tuple[1])
+            x = K.linear(rel, self.spatial_embedding).view(1, B, self.embedding_dim)
+            outs.append(rel.view(B, -1))
+            last_pos = curr
+        return torch.stack(outs, dim=0), state_tuple[0]
+
+
+# ---------------------------------------------------------------------------
+# social pooling (models.py:458-549) -> sgg_pool_*
+# ---------------------------------------------------------------------------
+class PoolHiddenNet(nn.Module):
+    """Pooling module as proposed in Social-GAN.  The pair MLP runs fused in
+    sgg_pool_fwd; the spatial embedding is folded into the first layer
+    (A = W1e We, c = W1e be + b1) so autograd carries its gradients."""
+
+    def __init__(self, embedding_dim=64, h_dim=64, mlp_dim=1024, bottleneck_dim=1024, activation="relu",
+                 batch_norm=True, dropout=0.0):
+        super().__init__()
+        self.mlp_dim = 1024
+        self.h_dim = h_dim
+        self.bottleneck_dim = bottleneck_dim
+        self.embedding_dim = embedding_dim
+        self.activation, self.batch_norm, self.dropout = activation, batch_norm, dropout
+        self.spatial_embedding = nn.Linear(2, embedding_dim)
+        self.mlp_pre_pool = make_mlp([embedding_dim + h_dim, 512, bottleneck_dim], activation=activation,
+                                     batch_norm=batch_norm, dropout=dropout)
+
+    def forward(self, h_states, seq_start_end, end_pos, scenes=None):
+        if self.batch_norm or self.activation != "relu" or self.dropout > 0:
+            raise NotImplementedError("the fused pooling kernel implements the reference configs "
+                                      "(batch_norm=0, relu, dropout=0)")
+        sc = _scenes(seq_start_end, end_pos.device, scenes)
+        E = self.embedding_dim
+        l1, l2 = self.mlp_pre_pool[0], self.mlp_pre_pool[2]
+        W1e, W1h = l1.weight[:, :E], l1.weight[:, E:]
+        A = W1e.mm(self.spatial_embedding.weight)                   # 512 x 2
+        c = torch.addmv(l1.bias, W1e, self.spatial_embedding.bias)  # 512
+        return K.social_pool(h_states.reshape(-1, self.h_dim), end_pos, W1h, A, c, l2.weight, l2.bias, sc)
+
+
+# ---------------------------------------------------------------------------
+# GAT (models.py:184-294) -> sgg_xw + sgg_gat_*
+# ---------------------------------------------------------------------------
+class GraphAttentionLayer(nn.Module):
+    def __init__(self, in_features, out_features, dropout, alpha, concat=True):
+        super().__init__()
+        self.dropout = dropout
+        self.in_features = in_features
+        self.out_features = out_features
+        self.alpha = alpha
+        self.concat = concat
+        self.W = nn.Parameter(torch.empty(size=(in_features, out_features)))
+        nn.init.xavier_uniform_(self.W.data, gain=1.414)
+        self.a = nn.Parameter(torch.empty(size=(2 * out_features, 1)))
+        nn.init.xavier_uniform_(self.a.data, gain=1.414)
+
+    def forward(self, h, graph, epilogue=None):
+        """graph: kernels.SegmentGraph.  epilogue defaults to ELU when concat
+        (models.py:207-210); GAT passes 2 to fuse its ELU + log_softmax."""
+        if self.dropout > 0 and self.training:
+            raise NotImplementedError("attention dropout is not implemented in the fused kernel (dropout1=0)")
+        wh = K.xw(h, self.W)
+        epi = (1 if self.concat else 0) if epilogue is None else epilogue
+        return K.gat_attention(wh, self.a, self.alpha, graph, epi)
+
+
+class GAT(nn.Module):
+    def __init__(self, nfeat, nhid, nclass, dropout, alpha, nheads):
+        super().__init__()
+        self.dropout = dropout
+        self.attentions = [GraphAttentionLayer(nfeat, nhid, dropout=dropout, alpha=alpha, concat=True)
+                           for _ in range(nheads)]
+        for i, attention in enumerate(self.attentions):
+            self.add_module("attention_{}".format(i), attention)
+        self.out_att = GraphAttentionLayer(nhid * nheads, nclass, dropout=dropout, alpha=alpha, concat=False)
+
+    def forward(self, x, graph):
+        """models.py:231-237: heads (ELU) concatenated -> out_att -> ELU ->
+        log_softmax(dim=1); the last two fused into the kernel epilogue."""
+        heads = [att(x, graph) for att in self.attentions]
+        x = heads[0] if len(heads) == 1 else torch.cat(heads, dim=1)
+        return self.out_att(x, graph, epilogue=2)
+
+
+class GATEncoder(nn.Module):
+    def __init__(self, n_units, n_heads, dropout, alpha):
+        super().__init__()
+        self.gat_intra = GAT(40, 72, 16, dropout, alpha, n_heads)
+        self.gat_inter = GAT(16, 72, 16, dropout, alpha, n_heads)
+        self.out_embedding = nn.Linear(16 * 2, 24)
+
+    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None):
+        sc = _scenes(seq_start_end, h_states.device, scenes)
+        if sc.max_n > 128:
+            raise ValueError("GAT kernels hold <= 128 peds per scene (got %d)" % sc.max_n)
+        g = sc.groups(end_group.reshape(-1))
+        intra_graph = K.SegmentGraph(sc.scene_off, sc.S, sc.max_n, 0, g.labels)
+        inter_graph = K.SegmentGraph(g.group_off, sc.S, sc.max_n, 1, None)
+        intra = self.gat_intra(h_states, intra_graph)                 # B x 16
+        gin = K.group_mean(intra, g)                                   # R @ intra  (cap x 16)
+        gout = self.gat_inter(gin, inter_graph)                        # cap x 16
+        inter = K.group_unpool(gout, g, scale=True)                    # R^T @ gout (B x 16)
+        return K.linear(torch.cat([intra, inter], dim=1), self.out_embedding)
+
+
+# ---------------------------------------------------------------------------
+# GCN (models.py:552-712) -> sgg_seg_* + sgg_xw (ReLU fused)
+# ---------------------------------------------------------------------------
+class GCN(nn.Module):
+    def __init__(self, input_dim=48, hidden_dim=72, out_dim=8, gcn_layers=2):
+        super().__init__()
+        self.X_dim = input_dim
+        self.hidden_dim = hidden_dim
+        self.out_dim = out_dim
+        self.gcn_layers = gcn_layers
+        self.W = torch.nn.ParameterList()
+        for i in range(self.gcn_layers):
+            if i == 0:
+                self.W.append(nn.Parameter(torch.randn(self.X_dim, self.hidden_dim)))
+            elif i == self.gcn_layers - 1:
+                self.W.append(nn.Parameter(torch.randn(self.hidden_dim, self.out_dim)))
+            else:
+                self.W.append(nn.Parameter(torch.randn(self.hidden_dim, self.hidden_dim)))
+
+    def forward(self, aggregate, X):
+        """H <- ReLU((A H) W_l); `aggregate` applies the row-normalised A."""
+        H = X
+        for w in self.W:
+            H = K.xw(aggregate(H), w, act=1)
+        return H
+
+
+class GCNModule(nn.Module):
+    def __init__(self, input_dim=40, hidden_dim=72, out_dim=16, gcn_layers=2, final_dim=24):
+        super().__init__()
+        self.gcn_intra = GCN(input_dim=input_dim, hidden_dim=hidden_dim, out_dim=out_dim, gcn_layers=gcn_layers)
+        self.gcn_inter = GCN(input_dim=16, hidden_dim=hidden_dim, out_dim=out_dim, gcn_layers=gcn_layers)
+        self.out_embedding = nn.Linear(out_dim * 2, final_dim)
+
+    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None):
+        sc = _scenes(seq_start_end, h_states.device, scenes)
+        g = sc.groups(end_group.reshape(-1))
+        # A_intra = D^-1 M: row i averages its group (models.py:658-665)
+        intra = self.gcn_intra(lambda H: K.group_unpool(K.group_mean(H, g), g, scale=False), h_states)
+        gin = K.group_mean(intra, g)                                           # R @ intra
+        gout = self.gcn_inter(lambda H: K.scene_mean_over_groups(H, g), gin)   # A_inter = 1/M
+        inter = K.group_unpool(gout, g, scale=True)                            # R^T @ gout
+        return K.linear(torch.cat([intra, inter], dim=1), self.out_embedding)
+
+
+# ---------------------------------------------------------------------------
+# generator / discriminator
+# ---------------------------------------------------------------------------
+class TrajectoryGenerator(nn.Module):
+    def __init__(self, obs_len, pred_len, embedding_dim=64, encoder_h_dim=64, decoder_h_dim=128,
+                 mlp_dim=1024, num_layers=1, noise_dim=(0,), noise_type="gaussian", noise_mix_type="ped",
+                 pooling_type=None, pool_every_timestep=True, dropout=0.0, bottleneck_dim=1024,
+                 activation="relu", batch_norm=True, neighborhood_size=2.0, grid_size=8,
+                 n_units=[32, 16, 32], n_heads=4, dropout1=0, alpha=0.2, *, graph="gat"):
+        super().__init__()
+        if pooling_type and pooling_type.lower() == "none":
+            pooling_type = None
+        if graph not in ("gat", "gcn"):
+            raise ValueError("graph must be 'gat' or 'gcn'")
+        self.obs_len = obs_len
+        self.pred_len = pred_len
+        self.mlp_dim = mlp_dim
+        self.encoder_h_dim = encoder_h_dim
+        self.decoder_h_dim = decoder_h_dim
+        self.embedding_dim = embedding_dim
+        self.noise_dim = noise_dim
+        self.num_layers = num_layers
+        self.noise_type = noise_type
+        self.noise_mix_type = noise_mix_type
+        self.pooling_type = pooling_type
+        self.noise_first_dim = 0
+        self.pool_every_timestep = pool_every_timestep
+        self.bottleneck_dim = 1024
+        self.graph = graph
+
+        self.encoder = Encoder(embedding_dim=embedding_dim, h_dim=encoder_h_dim, mlp_dim=mlp_dim,
+                               num_layers=num_layers, dropout=dropout)
+        self.decoder = Decoder(pred_len, embedding_dim=embedding_dim, h_dim=decoder_h_dim, mlp_dim=mlp_dim,
+                               num_layers=num_layers, pool_every_timestep=pool_every_timestep, dropout=dropout,
+                               bottleneck_dim=bottleneck_dim, activation=activation, batch_norm=batch_norm,
+                               pooling_type=pooling_type, grid_size=grid_size,
+                               neighborhood_size=neighborhood_size)
+        if pooling_type == "pool_net":
+            self.pool_net = PoolHiddenNet(embedding_dim=self.embedding_dim, h_dim=encoder_h_dim, mlp_dim=mlp_dim,
+                                          bottleneck_dim=bottleneck_dim, activation=activation,
+                                          batch_norm=batch_norm)
+        if self.noise_dim is None:
+            self.noise_dim = None
+        elif self.noise_dim[0] == 0:
+            self.noise_dim = None
+        else:
+            self.noise_first_dim = noise_dim[0]
+        self.gatencoder = GATEncoder(n_units=n_units, n_heads=n_heads, dropout=dropout1, alpha=alpha)
+        input_dim = encoder_h_dim + bottleneck_dim if pooling_type else encoder_h_dim
+        self.gcn_module = GCNModule(input_dim=input_dim, hidden_dim=72, out_dim=16, gcn_layers=2,
+                                    final_dim=decoder_h_dim - self.noise_first_dim)
+
+    def add_noise(self, _input, seq_start_end, user_noise=None, scenes=None):
+        """models.py:814-850 (noise drawn on the host, one draw per call)."""
+        if not self.noise_dim:
+            return _input
+        sc = _scenes(seq_start_end, _input.device, scenes)
+        if self.noise_mix_type == "global":
+            noise_shape = (sc.S,) + tuple(self.noise_dim)
+        else:
+            noise_shape = (_input.size(0),) + tuple(self.noise_dim)
+        z = user_noise if user_noise is not None else get_noise(noise_shape, self.noise_type)
+        z = z.to(_input.device, non_blocking=True)
+        if self.noise_mix_type == "global":
+            z = z.index_select(0, sc.ped_scene_long())
+        return torch.cat([_input, z], dim=1)
+
+    def mlp_decoder_needed(self):
+        return bool(self.noise_dim or self.pooling_type or self.encoder_h_dim != self.decoder_h_dim)
+
+    def forward(self, obs_traj, obs_traj_rel, seq_start_end, obs_traj_g, user_noise=None, *, scenes=None):
+        batch = obs_traj_rel.size(1)
+        sc = _scenes(seq_start_end, obs_traj.device, scenes)
+        final_encoder_h = self.encoder(obs_traj_rel)
+        ctx = final_encoder_h.view(-1, self.encoder_h_dim)
+        end_pos = obs_traj[-1]
+        if self.pooling_type:
+            pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc)
+            ctx = torch.cat([ctx, pool_h], dim=1)
+        if self.mlp_decoder_needed():
+            mod = self.gatencoder if self.graph == "gat" else self.gcn_module
+            noise_input = mod(ctx, seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
+        else:
+            noise_input = ctx
+        decoder_h = self.add_noise(noise_input, seq_start_end, user_noise=user_noise, scenes=sc).unsqueeze(0)
+        decoder_c = torch.zeros(self.num_layers, batch, self.decoder_h_dim, device=obs_traj.device)
+        out, _ = self.decoder(obs_traj[-1], obs_traj_rel[-1], (decoder_h, decoder_c), seq_start_end, scenes=sc)
+        return out
+
+
+class TrajectoryDiscriminator(nn.Module):
+    def __init__(self, obs_len, pred_len, embedding_dim=64, h_dim=64, mlp_dim=1024, num_layers=1,
+                 activation="relu", batch_norm=True, dropout=0.0, d_type="local"):
+        super().__init__()
+        self.obs_len = obs_len
+        self.pred_len = pred_len
+        self.seq_len = obs_len + pred_len
+        self.h_dim = h_dim
+        self.d_type = d_type
+        self.encoder = Encoder(embedding_dim=embedding_dim, h_dim=h_dim, mlp_dim=mlp_dim, num_layers=num_layers,
+                               dropout=dropout)
+        if d_type == "global":
+            mlp_pool_dims = [h_dim + embedding_dim, mlp_dim, h_dim]
+            self.pool_net = PoolHiddenNet(embedding_dim=embedding_dim, h_dim=h_dim, mlp_dim=mlp_pool_dims,
+                                          bottleneck_dim=h_dim, activation=activation, batch_norm=batch_norm)
+        self.real_classifier = make_mlp([h_dim, mlp_dim, 1], activation=activation, batch_norm=batch_norm,
+                                        dropout=dropout)
+
+    def forward(self, traj, traj_rel, seq_start_end=None, *, scenes=None):
+        final_h = self.encoder(traj_rel)
+        if self.d_type == "local":
+            x = final_h.squeeze()
+        else:
+            x = self.pool_net(final_h.squeeze(), seq_start_end, traj[0], scenes=scenes)
+        return run_mlp(self.real_classifier, x)

@@ -1,0 +1,152 @@
+/*
+ * sgg.h -- C ABI of libsgg.so, the MI355X (gfx950) kernels behind the
+ * group-aware Social-GAN hot path (reference: peaceminusones/Group-GAN-GCN-GAT).
+ *
+ * The reference has no native boundary: its "operator API" is the PyTorch
+ * module code in sgan/models.py.  Each entry point below replaces a sequence
+ * of ATen ops inside one of those modules; the replaced reference lines are
+ * cited per function (paths relative to the reference root).
+ *
+ * Conventions (every function):
+ *   - all pointers are DEVICE pointers owned by the caller (the library never
+ *     allocates); fp32 tensors are row-major and contiguous unless an explicit
+ *     leading dimension is given;
+ *   - scenes / segments are CSR ranges: `off[k] .. off[k+1]` (int32, off[0] = 0);
+ *   - launches go on `stream` (a hipStream_t passed as void*); nothing blocks,
+ *     nothing synchronises, so every call is hipGraph-capturable;
+ *   - return 0 on success, SGG_E_ARG (-1) for a bad argument (nothing
+ *     launched), or a positive hipError_t from the launch.  sgg_last_error()
+ *     describes the last failure of the calling thread.
+ */
+#ifndef SGG_H
+#define SGG_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGG_E_ARG (-1)
+
+/* Library version / self description. */
+int sgg_version(void);
+const char* sgg_last_error(void);
+
+/* Upper bounds the kernels are built for (checked on every call). */
+#define SGG_POOL_MAX_PEDS 64   /* peds per scene held LDS-resident by the pooling kernel      */
+#define SGG_GAT_MAX_NODES 128  /* nodes per segment held LDS-resident by the attention kernel */
+
+/* ------------------------------------------------------------------------
+ * Dense node-feature transform on MFMA (v_mfma_f32_16x16x4_f32, exact fp32):
+ *   Y[m, n] = act( sum_k X[m, k] * Wop[k, n] + bias[n] )
+ * Wop = W (K x N row-major) when trans_w = 0, or W^T for a W stored N x K when
+ * trans_w = 1.  act: 0 none, 1 ReLU.  bias may be NULL.  ldx / ldy are the
+ * row strides of X and Y (elements).
+ * Replaces the per-node `torch.mm(h, W)` / nn.Linear calls of
+ * models.py:199 (GAT Wh = hW), :576 ((AH)W of the GCN), :289 / :706
+ * (out_embedding), and the h_j half of the pooling MLP's first layer :538.
+ */
+int sgg_xw(const float* X, int ldx, const float* W, int trans_w, const float* bias,
+           float* Y, int ldy, int M, int K, int N, int act, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Social pooling (PoolHiddenNet.forward, models.py:497-549), factored:
+ *   hidden(i,j,k) = ReLU( U[j,k] + A[k,0]*(p_j - p_i)_x + A[k,1]*(p_j - p_i)_y )
+ *   out[i,c]      = max_j ReLU( sum_k W2[c,k] * hidden(i,j,k) + b2[c] )
+ * where U = h W1h^T + (W1e be + b1) (one sgg_xw) and A = W1e We, i.e. the
+ * reference's Linear(2,E) -> cat[., h_j] -> Linear(E+H,512) with the
+ * embedding folded into the first layer.  The (N^2 x 512) pair tensor is
+ * never materialised.  argmax[i,c] receives the GLOBAL ped index j that
+ * attains the max (smallest j on ties) for the backward.
+ *   U: B x 512, pos: B x 2, A: 512 x 2, W2T: 512 x bn (= W2^T), b2: bn
+ *   out: B x bn, argmax: B x bn (int32).  bn in {8, 16, 32, 48, 64}.
+ *   max_n = largest scene size in the batch (<= SGG_POOL_MAX_PEDS).
+ */
+int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2T,
+                 const float* b2, const int32_t* scene_off, int S, int B, int bn, int max_n,
+                 float* out, int32_t* argmax, void* stream);
+
+/* Backward of sgg_pool_fwd.  Only the (i, argmax[i,c]) pairs carry gradient
+ * (torch.max(dim) backward, models.py:541).  Writes dU (B x 512, every row),
+ * and per-workgroup partial sums of dW2 (grid x bn x 512) and dA
+ * (grid x 512 x 2), `grid` = sgg_pool_bwd_grid(S); the caller sums the
+ * partial slabs over their first axis (fixed order => deterministic).
+ * pos gets no gradient (it is an input trajectory in every caller). */
+int sgg_pool_bwd_grid(int S);
+int sgg_pool_bwd(const float* U, const float* pos, const float* A, const float* W2,
+                 const float* out, const int32_t* argmax, const float* dout,
+                 const int32_t* scene_off, int S, int B, int bn, int max_n,
+                 float* dU, float* dW2_part, float* dA_part, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Graph attention over the nodes of each segment (GraphAttentionLayer,
+ * models.py:198-220, and the ELU / log_softmax of GAT.forward :236-237):
+ *   s_i = Wh_i . a[:F],  t_j = Wh_j . a[F:]
+ *   e_ij = LeakyReLU_alpha(s_i + t_j) on the mask, softmax over j,
+ *   hp_i = sum_j att_ij Wh_j
+ *   y_i  = epilogue(hp_i): 0 identity, 1 ELU, 2 log_softmax(ELU(.)) over F
+ * mask_mode 0: (i == j) or (lab_i == lab_j and lab_i != 0)   (models.py:263-267)
+ * mask_mode 1: complete graph                                (models.py:282-283)
+ * Wh: n x F (ld F); y is written with row stride ldy (so heads can be written
+ * straight into their concat slot, models.py:234); hp (n x F) is written when
+ * epilogue != 0 (needed by the backward; epilogue 2 requires ldy == F).  Segments larger than
+ * SGG_GAT_MAX_NODES are rejected.
+ */
+int sgg_gat_fwd(const float* Wh, const float* a, const float* labels, const int32_t* seg_off,
+                int nseg, int n, int F, float alpha, int mask_mode, int epilogue, int max_seg,
+                float* hp, float* y, int ldy, void* stream);
+
+/* Backward of sgg_gat_fwd.  dy: n x F (row stride lddy), y / hp as written by
+ * the forward.  Writes dWh (n x F), ds, dt (n): the caller finishes
+ * da = [Wh^T ds ; Wh^T dt], dX = dWh W^T, dW = X^T dWh (plain GEMMs). */
+int sgg_gat_bwd(const float* Wh, const float* a, const float* labels, const int32_t* seg_off,
+                int nseg, int n, int F, float alpha, int mask_mode, int epilogue, int max_seg,
+                const float* hp, const float* y, const float* dy, int lddy,
+                float* dWh, float* ds, float* dt, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Group structure of each scene from the last observed group labels
+ * (models.py:263-278 / 654-680: M_intra, torch.unique rows, R = D^-1 rows):
+ * group = one non-zero label value of the scene, label 0 = singleton.
+ * Groups are numbered scene by scene, in order of their first member.
+ * Outputs (device):
+ *   ped_gid[B]        global group index of each ped
+ *   ped_scene[B]      scene of each ped
+ *   group_off[S+1]    CSR of groups per scene (group_off[S] = total groups G)
+ *   group_scene[B]    scene of group g        (valid for g < G)
+ *   group_count[B]    members of group g      (valid for g < G)
+ * max_n = largest scene (<= 1024).  workspace: >= sgg_group_index_ws(S, B) bytes.
+ */
+size_t sgg_group_index_ws(int S, int B);
+int sgg_group_index(const float* labels, const int32_t* scene_off, int S, int B, int max_n,
+                    int32_t* ped_gid, int32_t* ped_scene, int32_t* group_off,
+                    int32_t* group_scene, int32_t* group_count, void* workspace, void* stream);
+
+/* Segmented reduction with deterministic (row-ascending) order:
+ *   out[k, f] = post_k * sum_{i in [lo_k, hi_k), seg_of_row[i] == k} row_scale_i * x[i, f]
+ * lo_k = range_off[r_k], hi_k = range_off[r_k + 1], r_k = seg_range ? seg_range[k] : k.
+ * post_k = 1 / count_k when mean != 0 (count = matching rows), else 1.
+ * row_scale may be NULL (= 1).  Rows k >= nseg_valid(*) are zero-filled up to
+ * nseg_cap, where nseg_valid is read on the DEVICE from *nseg_dev (no host sync).
+ * Replaces R @ X (group mean-pool, models.py:280 / :683), the row-normalised
+ * A @ H aggregations of the GCN (:576), and (with mean = 0, row_scale = 1/|g|)
+ * the backward of R^T (:286 / :699). */
+int sgg_seg_reduce(const float* x, int ldx, int F, const int32_t* seg_of_row,
+                   const float* row_scale, const int32_t* range_off, const int32_t* seg_range,
+                   const int32_t* nseg_dev, int nseg_cap, int mean, float* out, int ldo,
+                   void* stream);
+
+/* out[i, f] = src[seg_of_row[i], f] * (row_scale ? row_scale[i] : 1) for
+ * i < nvalid, 0 for nvalid <= i < n, nvalid = nrow_dev ? *nrow_dev : n (read on
+ * the device).  Replaces R^T @ G (un-pool, models.py:286 / :699) and the
+ * broadcast half of the GCN's A @ H (:576). */
+int sgg_seg_gather(const float* src, int lds, int F, const int32_t* seg_of_row,
+                   const float* row_scale, const int32_t* nrow_dev, int n, float* out, int ldo,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGG_H */

@@ -1,0 +1,427 @@
+"""Generate the golden fixtures under tests/golden/ from the REAL reference.
+
+Test infrastructure only.  Runs in the build container (CPU), where the
+reference checkout lives read-only at /root/reference.  It never runs on the
+GPU box and nothing in the product imports it; only the .npz / .json files it
+writes travel.
+
+The reference hard-codes `.cuda()` (sgan/models.py:26,28,58-59,267,278,283,
+661,680,690,912), so we map `Tensor.cuda` / `Module.cuda` to identity before
+importing it, and stub the `attrdict` package that scripts/evaluate_model.py:11
+imports (absent here).  Nothing of the reference is copied: we call its
+functions and record inputs/outputs.
+
+Usage:  python tests/golden/make_golden.py [--only NAME ...] [--skip-eval]
+"""
+import argparse
+import importlib.util
+import json
+import os
+import random
+import shutil
+import sys
+import time
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+SPLITS = ["eth", "hotel", "univ", "zara1", "zara2"]
+
+
+# ----------------------------------------------------------------------------
+# reference import shim
+# ----------------------------------------------------------------------------
+def _import_reference():
+    sys.dont_write_bytecode = True
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    ad = types.ModuleType("attrdict")
+
+    class AttrDict(dict):
+        def __getattr__(self, k):
+            try:
+                return self[k]
+            except KeyError:
+                raise AttributeError(k)
+
+    ad.AttrDict = AttrDict
+    sys.modules["attrdict"] = ad
+    sys.path.insert(0, REF)
+    import sgan.models as m  # noqa
+    import sgan.losses as l  # noqa
+    import sgan.utils as u  # noqa
+    import sgan.data.loader as dl  # noqa
+
+    saved_argv = sys.argv
+    sys.argv = ["train.py"]
+    spec = importlib.util.spec_from_file_location("ref_train", os.path.join(REF, "scripts/train.py"))
+    tr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tr)
+    spec = importlib.util.spec_from_file_location("ref_eval", os.path.join(REF, "scripts/evaluate_model.py"))
+    ev = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ev)
+    sys.argv = saved_argv
+    return m, l, u, dl, tr, ev
+
+
+M, L, U, DL, TR, EV = _import_reference()
+ARGS = TR.parser.parse_args([])  # train.py defaults (GAT config)
+ARGS.loader_num_workers = 0
+
+
+def build_models(seed=0):
+    """Generator / discriminator exactly as scripts/train.py:173-220 builds them."""
+    torch.manual_seed(seed)
+    a = ARGS
+    n_units = [40] + [int(x) for x in a.hidden_units.strip().split(",")] + [40]
+    g = M.TrajectoryGenerator(
+        obs_len=a.obs_len, pred_len=a.pred_len, embedding_dim=a.embedding_dim,
+        encoder_h_dim=a.encoder_h_dim_g, decoder_h_dim=a.decoder_h_dim_g, mlp_dim=a.mlp_dim,
+        num_layers=a.num_layers, noise_dim=a.noise_dim, noise_type=a.noise_type,
+        noise_mix_type=a.noise_mix_type, pooling_type=a.pooling_type,
+        pool_every_timestep=a.pool_every_timestep, dropout=a.dropout,
+        bottleneck_dim=a.bottleneck_dim, neighborhood_size=a.neighborhood_size,
+        grid_size=a.grid_size, batch_norm=a.batch_norm, n_units=n_units,
+        n_heads=a.n_heads, dropout1=a.dropout1, alpha=a.alpha)
+    g.apply(TR.init_weights)
+    g.train()
+    d = M.TrajectoryDiscriminator(
+        obs_len=a.obs_len, pred_len=a.pred_len, embedding_dim=a.embedding_dim,
+        h_dim=a.encoder_h_dim_d, mlp_dim=a.mlp_dim, num_layers=a.num_layers,
+        dropout=a.dropout, batch_norm=a.batch_norm, d_type=a.d_type)
+    d.apply(TR.init_weights)
+    d.train()
+    return g, d
+
+
+def sd_arrays(module, prefix):
+    return {prefix + k: v.detach().numpy().astype(np.float32).copy() for k, v in module.state_dict().items()}
+
+
+def grad_arrays(module, prefix):
+    out = {}
+    for k, p in module.named_parameters():
+        if p.grad is not None:
+            out[prefix + k] = p.grad.detach().numpy().astype(np.float32).copy()
+    return out
+
+
+# ----------------------------------------------------------------------------
+# synthetic scenes (SURVEY.md §8d recipe)
+# ----------------------------------------------------------------------------
+def synth_batch(sizes, seed, n_labels=5, obs_len=8, pred_len=12):
+    rng = np.random.default_rng(seed)
+    T = obs_len + pred_len
+    B = int(sum(sizes))
+    start = rng.uniform(0, 15, size=(B, 2))
+    vel = rng.normal(0, 0.3, size=(B, 2))
+    jit = rng.normal(0, 0.05, size=(T, B, 2))
+    steps = vel[None] + jit
+    steps[0] = 0.0
+    abs_ = start[None] + np.cumsum(steps, axis=0)
+    rel = np.zeros_like(abs_)
+    rel[1:] = abs_[1:] - abs_[:-1]
+    lab = rng.integers(0, n_labels, size=(B,)).astype(np.float64)
+    g = np.broadcast_to(lab[None, :, None], (T, B, 1)).copy()
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    sse = np.stack([off[:-1], off[1:]], axis=1).astype(np.int64)
+    f = lambda x: torch.from_numpy(np.ascontiguousarray(x)).float()
+    return dict(
+        obs_traj=f(abs_[:obs_len]), pred_traj=f(abs_[obs_len:]),
+        obs_traj_rel=f(rel[:obs_len]), pred_traj_rel=f(rel[obs_len:]),
+        obs_traj_g=f(g[:obs_len]), pred_traj_g=f(g[obs_len:]),
+        non_linear_ped=torch.zeros(B), loss_mask=torch.ones(B, T),
+        seq_start_end=torch.from_numpy(sse))
+
+
+def label_patterns(sizes, seed):
+    """Group-label patterns covering all-singletons, one big group, mixed."""
+    rng = np.random.default_rng(seed)
+    labs = []
+    for s, n in enumerate(sizes):
+        kind = s % 4
+        if kind == 0:
+            l = np.zeros(n)                              # everybody ungrouped
+        elif kind == 1:
+            l = np.full(n, 3.0)                          # one big group
+        elif kind == 2:
+            l = rng.integers(0, 5, size=n).astype(float)  # mixed with label 0
+        else:
+            l = rng.integers(1, 1 + max(1, n // 2), size=n).astype(float)  # many small groups
+        labs.append(l)
+    return np.concatenate(labs)
+
+
+def sse_of(sizes):
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    return torch.from_numpy(np.stack([off[:-1], off[1:]], 1).astype(np.int64))
+
+
+def save(name, arrs):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print("wrote", path, "%.1f KB" % (os.path.getsize(path) / 1024))
+
+
+# ----------------------------------------------------------------------------
+# fixtures
+# ----------------------------------------------------------------------------
+POOL_SIZES = [1, 2, 5, 20, 57, 64, 3, 20]
+
+
+def fx_weights():
+    g, d = build_models(0)
+    arr = {}
+    arr.update(sd_arrays(g, "g/"))
+    arr.update(sd_arrays(d, "d/"))
+    save("weights.npz", arr)
+
+
+def fx_pool():
+    """PoolHiddenNet fwd + bwd, models.py:497-549, for G (h32->8) and D (h48->48)."""
+    g, d = build_models(0)
+    out = {}
+    for tag, net, hd in (("g", g.pool_net, 32), ("d", d.pool_net, 48)):
+        torch.manual_seed(11 if tag == "g" else 12)
+        B = sum(POOL_SIZES)
+        h = torch.randn(1, B, hd, requires_grad=True)
+        pos = (torch.rand(B, 2) * 15.0)
+        sse = sse_of(POOL_SIZES)
+        y = net(h, sse, pos)
+        dy = torch.randn_like(y)
+        net.zero_grad()
+        (y * dy).sum().backward()
+        out[tag + "/h"] = h.detach().numpy()[0]
+        out[tag + "/pos"] = pos.numpy()
+        out[tag + "/sse"] = sse.numpy()
+        out[tag + "/out"] = y.detach().numpy()
+        out[tag + "/dout"] = dy.numpy()
+        out[tag + "/dh"] = h.grad.numpy()[0]
+        for k, p in net.named_parameters():
+            out[tag + "/w/" + k] = p.detach().numpy()
+            out[tag + "/dw/" + k] = p.grad.numpy()
+    save("pool.npz", out)
+
+
+GRAPH_SIZES = [1, 2, 5, 20, 20, 33, 57, 64, 7, 12, 20, 20]
+
+
+def _graph_module_fixture(name, build_mod, seed):
+    torch.manual_seed(seed)
+    mod = build_mod()
+    B = sum(GRAPH_SIZES)
+    x = torch.randn(B, 40, requires_grad=True)
+    lab = torch.from_numpy(label_patterns(GRAPH_SIZES, seed)).float().view(B, 1)
+    sse = sse_of(GRAPH_SIZES)
+    end_pos = torch.zeros(B, 2)
+    y = mod(x, sse, end_pos, lab)
+    dy = torch.randn_like(y)
+    mod.zero_grad()
+    (y * dy).sum().backward()
+    out = dict(x=x.detach().numpy(), labels=lab.numpy()[:, 0], sse=sse.numpy(), out=y.detach().numpy(),
+               dout=dy.numpy(), dx=x.grad.numpy())
+    for k, p in mod.named_parameters():
+        out["w/" + k] = p.detach().numpy()
+        if p.grad is not None:
+            out["dw/" + k] = p.grad.numpy()
+    save(name, out)
+
+
+def fx_gat():
+    # GATEncoder, models.py:239-294 (dims hard-coded 40->72->16, 16->72->16, 32->24)
+    _graph_module_fixture("gat_encoder.npz", lambda: M.GATEncoder(n_units=[40, 16, 40], n_heads=1, dropout=0, alpha=0.2), 21)
+    # n_heads=2 variant exercises concat of heads (models.py:226-234)
+    _graph_module_fixture("gat_encoder_h2.npz", lambda: M.GATEncoder(n_units=[40, 16, 40], n_heads=2, dropout=0, alpha=0.2), 22)
+
+
+def fx_gcn():
+    # GCNModule, models.py:583-712 (input 40, hidden 72, out 16, final 24)
+    def mk():
+        m = M.GCNModule(input_dim=40, hidden_dim=72, out_dim=16, gcn_layers=2, final_dim=24)
+        # randn init (models.py:567-571) blows activations up by ~x50 per layer;
+        # keep it, it is what the reference trains from.
+        return m
+    _graph_module_fixture("gcn_module.npz", mk, 31)
+
+
+def _gen_forward(g, batch, noise, mode):
+    """TrajectoryGenerator.forward, models.py:862-927; mode 'gcn' swaps in the
+    commented call at models.py:902 (the sgan-g-p checkpoint family)."""
+    if mode == "gat":
+        return g(batch["obs_traj"], batch["obs_traj_rel"], batch["seq_start_end"], batch["obs_traj_g"], user_noise=noise)
+    obs_traj, obs_rel, sse, obs_g = batch["obs_traj"], batch["obs_traj_rel"], batch["seq_start_end"], batch["obs_traj_g"]
+    Bn = obs_rel.size(1)
+    h = g.encoder(obs_rel)
+    end_pos = obs_traj[-1]
+    pool_h = g.pool_net(h, sse, end_pos)
+    ctx = torch.cat([h.view(-1, g.encoder_h_dim), pool_h], dim=1)
+    ni = g.gcn_module(ctx, sse, end_pos, obs_g[-1])
+    dh = g.add_noise(ni, sse, user_noise=noise).unsqueeze(0)
+    dc = torch.zeros(g.num_layers, Bn, g.decoder_h_dim)
+    out, _ = g.decoder(obs_traj[-1], obs_rel[-1], (dh, dc), sse)
+    return out
+
+
+def real_batch(split="zara1", dset_type="test", n_scenes=16):
+    path = os.path.join(REF, "datasets_group", split, dset_type)
+    dset = DL.TrajectoryDataset(path, obs_len=8, pred_len=12, skip=1, delim="tab")
+    from sgan.data.trajectories_GCN import seq_collate
+    items = [dset[i] for i in range(min(n_scenes, len(dset)))]
+    t = seq_collate(items)
+    keys = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel",
+            "obs_traj_g", "pred_traj_g", "non_linear_ped", "loss_mask", "seq_start_end"]
+    return dict(zip(keys, t))
+
+
+def fx_gen():
+    g, d = build_models(0)
+    batches = {"synth": synth_batch([20] * 6 + [2, 5, 33], seed=5), "zara1": real_batch("zara1", "test", 16)}
+    for mode in ("gat", "gcn"):
+        out = {}
+        for bname, b in batches.items():
+            S = b["seq_start_end"].size(0)
+            torch.manual_seed(77)
+            noise = torch.randn(S, 8)
+            g.zero_grad()
+            y = _gen_forward(g, b, noise, mode)
+            dy = torch.randn_like(y)
+            (y * dy).sum().backward()
+            pre = bname + "/"
+            for k in ("obs_traj", "obs_traj_rel", "obs_traj_g", "seq_start_end", "pred_traj", "pred_traj_rel"):
+                out[pre + k] = b[k].numpy()
+            out[pre + "noise"] = noise.numpy()
+            out[pre + "out"] = y.detach().numpy()
+            out[pre + "dout"] = dy.numpy()
+            for k, v in grad_arrays(g, pre + "dw/").items():
+                out[k] = v
+        save("gen_fwd_%s.npz" % mode, out)
+
+
+def fx_disc():
+    g, d = build_models(0)
+    b = synth_batch([20] * 4 + [2, 9], seed=6)
+    traj = torch.cat([b["obs_traj"], b["pred_traj"]], 0)
+    traj_rel = torch.cat([b["obs_traj_rel"], b["pred_traj_rel"]], 0).requires_grad_(True)
+    d.zero_grad()
+    s = d(traj, traj_rel, b["seq_start_end"])
+    ds = torch.randn_like(s)
+    (s * ds).sum().backward()
+    # also the pre-classifier features (trailing ReLU zeroes most scores)
+    feat = d.pool_net(d.encoder(traj_rel).squeeze(), b["seq_start_end"], traj[0])
+    out = dict(traj=traj.numpy(), traj_rel=traj_rel.detach().numpy(), sse=b["seq_start_end"].numpy(),
+               scores=s.detach().numpy(), dscores=ds.numpy(), dtraj_rel=traj_rel.grad.numpy(),
+               feat=feat.detach().numpy())
+    out.update(grad_arrays(d, "dw/"))
+    save("disc_fwd.npz", out)
+
+
+def fx_train_step():
+    """discriminator_step + generator_step (scripts/train.py:395-484), 2 iterations,
+    fresh Adam, seeded host RNGs (noise: torch CPU RNG, label smoothing: random)."""
+    g, d = build_models(0)
+    opt_g = torch.optim.Adam(g.parameters(), lr=ARGS.g_learning_rate)
+    opt_d = torch.optim.Adam(d.parameters(), lr=ARGS.d_learning_rate)
+    out = {}
+    batches = [synth_batch([20] * 5 + [7], seed=41), synth_batch([20] * 4 + [3, 12], seed=42)]
+    torch.manual_seed(1234)
+    random.seed(1234)
+    keys = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel",
+            "obs_traj_g", "pred_traj_g", "non_linear_ped", "loss_mask", "seq_start_end"]
+    for it, b in enumerate(batches):
+        b = dict(b)
+        b["obs_vel"] = b["obs_traj_rel"] * 2.5
+        b["pred_vel"] = b["pred_traj_rel"] * 2.5
+        tup = [b[k] for k in keys]
+        for k in keys:
+            out["b%d/%s" % (it, k)] = b[k].numpy()
+        ld = TR.discriminator_step(ARGS, tup, g, d, TR.gan_d_loss, opt_d)
+        lg = TR.generator_step(ARGS, tup, g, d, TR.gan_g_loss, opt_g)
+        for k, v in ld.items():
+            out["it%d/D/%s" % (it, k)] = np.float64(v)
+        for k, v in lg.items():
+            out["it%d/G/%s" % (it, k)] = np.float64(v)
+        out.update(sd_arrays(g, "it%d/g/" % it))
+        out.update(sd_arrays(d, "it%d/d/" % it))
+    save("train_step.npz", out)
+
+
+def fx_eval(splits):
+    """scripts/evaluate_model.py:72-99 on the test split, 20 samples, seeded host RNG,
+    seeded random-init weights (trained checkpoints are not loadable with the
+    safe loader: they hold collections.defaultdict)."""
+    res = {}
+    for mode in ("gat", "gcn"):
+        for split in splits:
+            g, _ = build_models(0)
+            if mode == "gcn":
+                g.forward = types.MethodType(
+                    lambda self, ot, orl, sse, og, user_noise=None: _gen_forward(
+                        self, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse, obs_traj_g=og), user_noise, "gcn"), g)
+            path = os.path.join(REF, "datasets_group", split, "test")
+            a = EV.AttrDict(dict(vars(ARGS)))
+            _, loader = DL.data_loader(a, path)
+            torch.manual_seed(0)
+            t0 = time.time()
+            ade, fde = EV.evaluate(a, loader, g, 20)
+            res["%s/%s" % (mode, split)] = dict(ade=float(ade), fde=float(fde), seconds=time.time() - t0,
+                                                 num_seq=len(loader.dataset))
+            print(mode, split, res["%s/%s" % (mode, split)], flush=True)
+    with open(os.path.join(HERE, "evaluate.json"), "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+
+
+def copy_test_data():
+    for split in SPLITS:
+        src = os.path.join(REF, "datasets_group", split, "test")
+        dst = os.path.join(HERE, "datasets_group", split, "test")
+        os.makedirs(dst, exist_ok=True)
+        for f in os.listdir(src):
+            shutil.copyfile(os.path.join(src, f), os.path.join(dst, f))
+
+
+def fx_cpu_timing():
+    """Reference CPU train-iteration timing on this host, used to
+    validate the oracle's reference-formulation timing (ratio check)."""
+    g, d = build_models(0)
+    opt_g = torch.optim.Adam(g.parameters(), lr=ARGS.g_learning_rate)
+    opt_d = torch.optim.Adam(d.parameters(), lr=ARGS.d_learning_rate)
+    keys = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel",
+            "obs_traj_g", "pred_traj_g", "non_linear_ped", "loss_mask", "seq_start_end"]
+    b = synth_batch([20] * 16, seed=0)
+    b["obs_vel"] = b["obs_traj_rel"] * 2.5
+    b["pred_vel"] = b["pred_traj_rel"] * 2.5
+    tup = [b[k] for k in keys]
+    TR.discriminator_step(ARGS, tup, g, d, TR.gan_d_loss, opt_d)
+    t0 = time.time()
+    n = 2
+    for _ in range(n):
+        TR.discriminator_step(ARGS, tup, g, d, TR.gan_d_loss, opt_d)
+        TR.generator_step(ARGS, tup, g, d, TR.gan_g_loss, opt_g)
+    dt = (time.time() - t0) / n
+    res = dict(scenes_per_s=16 / dt, threads=torch.get_num_threads(), batch=16, n_peds=20)
+    print("reference cpu timing", res)
+    with open(os.path.join(HERE, "ref_cpu_timing.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+ALL = dict(weights=fx_weights, pool=fx_pool, gat=fx_gat, gcn=fx_gcn, gen=fx_gen, disc=fx_disc,
+           train=fx_train_step, data=copy_test_data, timing=fx_cpu_timing)
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--skip-eval", action="store_true")
+    ap.add_argument("--splits", nargs="*", default=SPLITS)
+    a = ap.parse_args()
+    names = a.only if a.only else list(ALL)
+    for n in names:
+        if n == "eval":
+            continue
+        t0 = time.time()
+        ALL[n]()
+        print("[%s] %.1fs" % (n, time.time() - t0), flush=True)
+    if (a.only is None and not a.skip_eval) or (a.only and "eval" in a.only):
+        fx_eval(a.splits)

@@ -1,0 +1,144 @@
+"""Pin the CPU oracle (oracle/sgan_oracle.py) against fixtures produced by the
+real reference (tests/golden/make_golden.py).  CPU only."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sgan_oracle as O
+
+from conftest import GOLDEN
+
+RTOL = 2e-5
+
+
+def npz(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def T(a):
+    return torch.from_numpy(np.asarray(a)).clone()
+
+
+def close(a, b, rtol=RTOL, atol=None, floor=1e-6):
+    """max |a-b| relative to max |b| (or to `floor` when the reference tensor is
+    ~0, e.g. a gradient that cancels analytically)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    scale = max(np.abs(b).max(), floor)
+    err = np.abs(a - b).max() / scale
+    assert err <= (rtol if atol is None else atol), "max rel err %.3e" % err
+
+
+def grad_floor(f, prefix):
+    """1e-2 of the largest reference parameter gradient of the module: a tensor
+    whose gradient is analytically ~0 (the inter-group out_att.a, whose source
+    half cancels under the row softmax) is compared on that scale."""
+    return 1e-2 * max(np.abs(f[k]).max() for k in f.files if k.startswith(prefix))
+
+
+def load_models(prefix_g="g/", prefix_d="d/", graph="gat", w=None):
+    w = w if w is not None else npz("weights.npz")
+    g, d = O.build_default(graph)
+    g.load_state_dict({k[len(prefix_g):]: T(w[k]) for k in w.files if k.startswith(prefix_g)})
+    d.load_state_dict({k[len(prefix_d):]: T(w[k]) for k in w.files if k.startswith(prefix_d)})
+    return g, d
+
+
+@pytest.mark.parametrize("tag", ["g", "d"])
+def test_pool_fixture(tag):
+    f = npz("pool.npz")
+    hd = f[tag + "/h"].shape[1]
+    bn = f[tag + "/out"].shape[1]
+    net = O.PoolHiddenNet(16, hd, 64, bn, "relu", False)
+    net.load_state_dict({k[len(tag) + 3:]: T(f[k]) for k in f.files if k.startswith(tag + "/w/")})
+    h = T(f[tag + "/h"]).unsqueeze(0).requires_grad_(True)
+    y = net(h, T(f[tag + "/sse"]), T(f[tag + "/pos"]))
+    close(y.detach(), f[tag + "/out"])
+    (y * T(f[tag + "/dout"])).sum().backward()
+    close(h.grad[0], f[tag + "/dh"])
+    for k, p in net.named_parameters():
+        close(p.grad, f[tag + "/dw/" + k], floor=grad_floor(f, tag + "/dw/"))
+
+
+@pytest.mark.parametrize("name,heads", [("gat_encoder.npz", 1), ("gat_encoder_h2.npz", 2), ("gcn_module.npz", 0)])
+def test_graph_module_fixture(name, heads):
+    f = npz(name)
+    if heads:
+        mod = O.GATEncoder([40, 16, 40], heads, 0.0, 0.2)
+    else:
+        mod = O.GCNModule(40, 72, 16, 2, 24)
+    mod.load_state_dict({k[2:]: T(f[k]) for k in f.files if k.startswith("w/")})
+    x = T(f["x"]).requires_grad_(True)
+    y = mod(x, T(f["sse"]), None, T(f["labels"]).view(-1, 1))
+    close(y.detach(), f["out"])
+    (y * T(f["dout"])).sum().backward()
+    close(x.grad, f["dx"])
+    for k, p in mod.named_parameters():
+        if "dw/" + k in f.files:
+            close(p.grad, f["dw/" + k], rtol=1e-4, floor=grad_floor(f, "dw/"))
+
+
+@pytest.mark.parametrize("graph", ["gat", "gcn"])
+def test_generator_fixture(graph):
+    f = npz("gen_fwd_%s.npz" % graph)
+    g, _ = load_models(graph=graph)
+    for b in ("synth", "zara1"):
+        g.zero_grad()
+        y = g(T(f[b + "/obs_traj"]), T(f[b + "/obs_traj_rel"]), T(f[b + "/seq_start_end"]),
+              T(f[b + "/obs_traj_g"]), user_noise=T(f[b + "/noise"]))
+        close(y.detach(), f[b + "/out"])
+        (y * T(f[b + "/dout"])).sum().backward()
+        for k, p in g.named_parameters():
+            key = b + "/dw/" + k
+            if key in f.files:
+                close(p.grad, f[key], rtol=1e-4, floor=grad_floor(f, b + "/dw/"))
+
+
+def test_discriminator_fixture():
+    f = npz("disc_fwd.npz")
+    _, d = load_models()
+    tr = T(f["traj_rel"]).requires_grad_(True)
+    s = d(T(f["traj"]), tr, T(f["sse"]))
+    close(s.detach(), f["scores"])
+    feat = d.pool_net(d.encoder(tr).squeeze(), T(f["sse"]), T(f["traj"])[0])
+    close(feat.detach(), f["feat"])
+    (s * T(f["dscores"])).sum().backward()
+    close(tr.grad, f["dtraj_rel"], atol=1e-5)
+    for k, p in d.named_parameters():
+        if "dw/" + k in f.files:
+            close(p.grad, f["dw/" + k], rtol=1e-4, floor=grad_floor(f, "dw/"))
+
+
+@pytest.mark.slow
+def test_train_step_fixture():
+    path = os.path.join(GOLDEN, "train_step.npz")
+    if not os.path.exists(path):
+        pytest.skip("train_step fixture not generated")
+    f = np.load(path)
+    g, d = load_models()
+    og = torch.optim.Adam(g.parameters(), lr=O.Args.g_learning_rate)
+    od = torch.optim.Adam(d.parameters(), lr=O.Args.d_learning_rate)
+    torch.manual_seed(1234)
+    random.seed(1234)
+    keys = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel",
+            "obs_traj_g", "pred_traj_g", "non_linear_ped", "loss_mask", "seq_start_end"]
+    for it in range(2):
+        b = [T(f["b%d/%s" % (it, k)]) for k in keys]
+        ld = O.discriminator_step(O.Args, b, g, d, od)
+        lg = O.generator_step(O.Args, b, g, d, og)
+        for k, v in ld.items():
+            assert abs(v - float(f["it%d/D/%s" % (it, k)])) <= 1e-4 * max(1.0, abs(v))
+        for k, v in lg.items():
+            assert abs(v - float(f["it%d/G/%s" % (it, k)])) <= 1e-4 * max(1.0, abs(v))
+        # Adam's first steps move each weight by ~lr * sign(grad); weights whose
+        # gradient is rounding noise (the attention vectors `a`, whose source
+        # half cancels in the row softmax) may flip sign: allow 2*lr per step.
+        for mod, tag, lr in ((g, "g", O.Args.g_learning_rate), (d, "d", O.Args.d_learning_rate)):
+            for k, v in mod.state_dict().items():
+                ref = f["it%d/%s/%s" % (it, tag, k)]
+                err = np.abs(v.numpy().astype(np.float64) - ref).max()
+                assert err <= 2 * lr * (it + 1) + 1e-5 * np.abs(ref).max(), (tag, k, err)
