@@ -1,0 +1,173 @@
+"""Benchmark: train-scenes/s of the group-aware Social-GAN hot path on MI355X.
+
+One step = one reference training iteration (scripts/train.py defaults, GAT
+generator): D-step + G-step (best_k = 20) with Adam updates, on a batch of
+`--batch` synthetic 20-ped scenes per GPU (obs 8 / pred 12), inputs resident
+in HBM before the timed region.  Multi-GPU: one process per GPU launched by
+torch.distributed.run, scenes sharded (weak scaling), RCCL all-reduce of the
+G/D gradients once per optimizer step.
+
+Prints ONE JSON line (rank 0).  Extra objects:
+  roofline     the dominant kernel (by summed device time over the timed
+               steps, measured with HIP events on its launch stream) against
+               the fp32 peak; `achieved` = algorithmic FLOP per launch / avg
+               launch time (FLOP model in DESIGN.md);
+  cpu_baseline the CPU oracle (reference formulation, per-scene loops) timed
+               on this host for a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "group-gan-gcn-gat_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "scenes/sec (obs8/pred12, 20 peds) at 1/2/4/8 GPUs; ADE/FDE vs ref"
+FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 dense (vector == f32 MFMA), MI355X_MICROARCH.md
+
+
+def build_models(seed, graph="gat"):
+    from sgan.models import TrajectoryDiscriminator, TrajectoryGenerator
+    torch.manual_seed(seed)
+    g = TrajectoryGenerator(8, 12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32, mlp_dim=64, num_layers=1,
+                            noise_dim=(8,), noise_type="gaussian", noise_mix_type="global", pooling_type="pool_net",
+                            pool_every_timestep=False, dropout=0.0, bottleneck_dim=8, batch_norm=False,
+                            n_units=[40, 16, 40], n_heads=1, dropout1=0.0, alpha=0.2, graph=graph)
+    d = TrajectoryDiscriminator(8, 12, embedding_dim=16, h_dim=48, mlp_dim=64, num_layers=1, batch_norm=False,
+                                dropout=0.0, d_type="global")
+    for m in list(g.modules()) + list(d.modules()):   # train.py:127-130 init_weights
+        if isinstance(m, torch.nn.Linear):
+            torch.nn.init.kaiming_normal_(m.weight)
+    return g, d
+
+
+def cpu_baseline(batch_scenes, n_peds, iters=2, threads=None):
+    """Oracle (reference formulation) D-step + G-step on the host cores."""
+    from oracle import sgan_oracle as O
+    from sgan.data.synthetic import synthetic_batch
+    threads = threads or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    g, d = O.build_default("gat")
+    og = torch.optim.Adam(g.parameters(), lr=1e-4)
+    od = torch.optim.Adam(d.parameters(), lr=1e-3)
+    b = synthetic_batch([n_peds] * batch_scenes, seed=123)
+    O.discriminator_step(O.Args, b, g, d, od)          # warm-up (not timed)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        O.discriminator_step(O.Args, b, g, d, od)
+        O.generator_step(O.Args, b, g, d, og)
+    dt = time.perf_counter() - t0
+    return {"value": round(batch_scenes * iters / dt, 3), "unit": "scenes/s", "cores": threads, "kind": "port",
+            "sample": "%d train iterations (D-step + G-step, best_k=20) on %d x %d-ped synthetic scenes, oracle/"
+                      "sgan_oracle.py reference formulation, torch CPU fp32, %d threads (%.1f s)"
+                      % (iters, batch_scenes, n_peds, threads, dt)}
+
+
+def pool_flops(sc, bn):
+    """Algorithmic FLOP of one sgg_pool_fwd launch: per (i, j) pair 512 hidden
+    units x (2 FMA for A.r + bn FMA for layer 2) = 512 * (4 + 2 bn)."""
+    sizes = np.diff(sc.host_off)
+    return float((sizes.astype(np.float64) ** 2).sum()) * 512.0 * (4 + 2 * bn)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="scenes per GPU")
+    ap.add_argument("--peds", type=int, default=20)
+    ap.add_argument("--graph", default="gat", choices=["gat", "gcn"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from sgan import kernels as K
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import DataParallel, GanTrainer
+
+    g, d = build_models(0, args.graph)
+    g, d = g.to(dev), d.to(dev)
+    trainer = GanTrainer(g, d, dp=DataParallel())
+    batch = synthetic_batch([args.peds] * args.batch, seed=1000 + rank, device=dev)
+    sc = SceneIndex.from_seq_start_end(batch[-1], dev)
+    S_glob, B_glob = sc.S * world, sc.B * world
+    kw = dict(S_global=S_glob, B_global=B_glob, shard=(rank * sc.S, (rank + 1) * sc.S))
+
+    for _ in range(args.warmup):
+        trainer.step(batch, sc, **kw)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    K.pool_timer.start()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step(batch, sc, **kw)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    launches = K.pool_timer.stop()
+
+    if rank == 0:
+        # dominant kernel: the pooling forward variant with the most device time
+        by_bn = {}
+        for bn, flops, ms in launches:
+            a = by_bn.setdefault(bn, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += flops
+            a[2] += ms
+        bn_dom = max(by_bn, key=lambda b: by_bn[b][2])
+        n, fl, ms = by_bn[bn_dom]
+        achieved = (fl / n) / (ms / n * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                    "kernel": "sgg::pool_fwd_kernel<%d>" % bn_dom, "launches": n,
+                    "avg_launch_us": round(ms / n * 1e3, 2),
+                    "note": "fp32 (VALU FMA, same peak as f32 MFMA); all pool variants: %s" % {
+                        "bn%d" % b: {"launches": v[0], "ms": round(v[2], 3)} for b, v in by_bn.items()}}
+        ms_step = elapsed / args.steps * 1e3
+        value = world * args.batch / (elapsed / args.steps)
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.batch, args.peds, iters=args.cpu_iters)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "scenes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights, SURVEY.md 8d recipe)",
+            "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam) of the GAT generator "
+                                   "(scripts/train.py defaults)", "scenes_per_gpu": args.batch,
+                       "global_batch": args.batch * world, "peds_per_scene": args.peds, "obs_len": 8, "pred_len": 12,
+                       "graph": args.graph, "parallelism": "dp%d" % world},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -85,6 +85,34 @@ def linear(x, lin, act=0):
 # ---------------------------------------------------------------------------
 # social pooling
 # ---------------------------------------------------------------------------
+class _PoolTimer:
+    """Optional HIP-event timing of every sgg_pool_fwd launch (bench.py's
+    roofline): events are recorded on the launch stream around the kernel."""
+
+    def __init__(self):
+        self.active = False
+        self.rec = []
+
+    def start(self):
+        self.active, self.rec = True, []
+
+    def stop(self):
+        self.active = False
+        torch.cuda.synchronize()
+        out = [(bn, fl, e0.elapsed_time(e1)) for bn, fl, e0, e1 in self.rec]
+        self.rec = []
+        return out
+
+
+pool_timer = _PoolTimer()
+
+
+def _pool_flops(scenes, bn):
+    import numpy as np
+    sz = np.diff(scenes.host_off).astype(np.float64)
+    return float((sz * sz).sum()) * 512.0 * (4 + 2 * bn)
+
+
 class _Pool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, pos, W1h, A, c, W2, b2, scenes):
@@ -101,9 +129,16 @@ class _Pool(torch.autograd.Function):
         W2T = W2.t().contiguous()
         A = A.contiguous()
         b2 = b2.contiguous()
+        timed = pool_timer.active
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2T), N.ptr(b2), N.ptr(scenes.scene_off),
                                  scenes.S, B, bn, scenes.max_n, N.ptr(out), N.ptr(am), N.stream_ptr()),
                 "sgg_pool_fwd")
+        if timed:
+            e1.record()
+            pool_timer.rec.append((bn, _pool_flops(scenes, bn), e0, e1))
         ctx.scenes = scenes
         ctx.save_for_backward(h, pos, W1h, A, W2, U, out, am)
         ctx.mark_non_differentiable(am)

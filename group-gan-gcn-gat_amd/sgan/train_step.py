@@ -1,0 +1,245 @@
+"""Fast GAN training iteration (reference scripts/train.py:395-484), with
+scene-sharded data parallelism over RCCL.
+
+Same maths and the same host RNG streams as the reference's
+discriminator_step / generator_step:
+  D-step: fake = G(batch) (1 noise draw), D on fake and real, gan_d_loss
+          (2 random.uniform draws), backward, [clip], Adam.
+  G-step: best_k G samples (best_k noise draws, in order), per-scene
+          min_k sum_peds l2 / sum(mask) summed over scenes, + gan_g_loss on
+          D(last sample) (1 random.uniform draw), backward, clip 2.0, Adam.
+
+What differs is the execution plan, all results-neutral:
+  * D on fake and real runs as ONE call over the two batches stacked.
+  * The D-step's G forward runs without autograd: its gradients are
+    discarded by the reference (optimizer_g.zero_grad() precedes the G
+    backward, train.py:478).
+  * The best_k G samples run as ONE no-grad call over a k-times replicated
+    batch; the per-scene argmin picks each scene's best sample, and only
+    that sample and the last one (the D input) are recomputed with autograd.
+    The gradient of min_k and of the D term flows only through those two, so
+    the gradients equal the reference's (every other sample's contribution
+    is exactly zero).  `selective_backward=False` keeps all k in the graph.
+  * The G-step's D forward backpropagates to G only (its D parameter
+    gradients are discarded by the reference, train.py:397-427).
+  * Loss values come back as device tensors (no per-step host sync).
+
+Data parallelism (one process per GPU, torch.distributed, backend nccl=RCCL):
+every rank holds S_local whole scenes of the global batch; all ranks draw the
+GLOBAL noise tensors from identically seeded host generators and slice their
+own rows, and draw the same label-smoothing numbers; local losses are scaled
+so that the SUM over ranks is the global loss (the l2 term is a sum over
+scenes, the BCE terms are means over the B_global peds); one flat bucket
+all-reduce per optimizer step (grads + loss values), then clip and Adam.
+The result equals single-GPU training on the global batch up to summation
+order.
+"""
+import random
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .losses import bce_loss
+from .models import get_noise
+from .scene import SceneIndex
+from .utils import relative_to_abs
+
+
+class TrainArgs:
+    """scripts/train.py:29-124 defaults of the fields the steps read."""
+
+    def __init__(self, **kw):
+        self.obs_len = 8
+        self.pred_len = 12
+        self.best_k = 20
+        self.l2_loss_weight = 1.0
+        self.clipping_threshold_g = 2.0
+        self.clipping_threshold_d = 0.0
+        self.g_learning_rate = 1e-4
+        self.d_learning_rate = 1e-3
+        self.__dict__.update(kw)
+
+
+def _rep(t, k):
+    return t.repeat(1, k, 1) if k > 1 else t
+
+
+def _sse_of(sc):
+    return torch.from_numpy(np.stack([sc.host_off[:-1], sc.host_off[1:]], 1))
+
+
+class DataParallel:
+    """Scene-sharded DP context (world 1 = plain single-GPU)."""
+
+    def __init__(self, group=None):
+        self.on = dist.is_available() and dist.is_initialized()
+        self.group = group
+        self.world = dist.get_world_size(group) if self.on else 1
+        self.rank = dist.get_rank(group) if self.on else 0
+
+    def shard(self, S_global):
+        """Contiguous scene range [s0, s1) of this rank."""
+        per = (S_global + self.world - 1) // self.world
+        s0 = min(self.rank * per, S_global)
+        return s0, min(s0 + per, S_global)
+
+    def allreduce_(self, tensors):
+        """SUM-all-reduce a list of tensors through one flat bucket."""
+        if not self.on or self.world == 1 or not tensors:
+            return
+        flat = torch.cat([t.reshape(-1) for t in tensors])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        o = 0
+        for t in tensors:
+            n = t.numel()
+            t.copy_(flat[o:o + n].view_as(t))
+            o += n
+
+
+class GanTrainer:
+    def __init__(self, G, D, args=None, dp=None, selective_backward=True):
+        self.G, self.D = G, D
+        self.args = args or TrainArgs()
+        self.dp = dp or DataParallel()
+        self.selective_backward = selective_backward
+        self.opt_g = torch.optim.Adam(G.parameters(), lr=self.args.g_learning_rate)
+        self.opt_d = torch.optim.Adam(D.parameters(), lr=self.args.d_learning_rate)
+        skip = "gcn_module." if getattr(G, "graph", "gat") == "gat" else "gatencoder."
+        self.g_params = [p for n, p in G.named_parameters() if not n.startswith(skip)]
+        self.d_params = list(D.parameters())
+
+    # -- helpers -----------------------------------------------------------
+    def _noise(self, S_global, s0, s1):
+        G = self.G
+        if not G.noise_dim:
+            return None
+        if G.noise_mix_type != "global":
+            raise NotImplementedError("GanTrainer shards scenes; per-ped noise ('ped' mix) is not sharded yet")
+        z = get_noise((S_global,) + tuple(G.noise_dim), G.noise_type)   # host RNG, global draw
+        return z[s0:s1]
+
+    def _finish(self, params, opt, loss_terms, clip):
+        """all-reduce grads (+ loss values), clip, step."""
+        grads = [p.grad for p in params if p.grad is not None]
+        vals = torch.stack([t.detach().reshape(()) for t in loss_terms])
+        self.dp.allreduce_(grads + [vals])
+        if clip > 0:
+            torch.nn.utils.clip_grad_norm_(params, clip)
+        opt.step()
+        return vals
+
+    # -- steps ---------------------------------------------------------------
+    def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None)):
+        """discriminator_step (train.py:395-429). `batch` holds this rank's
+        scenes (device tensors), `sc` their SceneIndex."""
+        a = self.args
+        (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, _lm, sse) = batch
+        S_global = S_global or sc.S
+        B_global = B_global or sc.B
+        s0 = shard[0]
+        z = self._noise(S_global, s0, s0 + sc.S)
+        with torch.no_grad():
+            fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
+        fake = relative_to_abs(fake_rel, obs[-1])
+        traj = torch.cat([torch.cat([obs, fake], 0), torch.cat([obs, pred_gt], 0)], 1)
+        traj_rel = torch.cat([torch.cat([obs_rel, fake_rel], 0), torch.cat([obs_rel, pred_gt_rel], 0)], 1)
+        sc2 = sc.repeat(2)
+        scores = self.D(traj, traj_rel, _sse_of(sc2), scenes=sc2)
+        s_fake, s_real = scores[:sc.B], scores[sc.B:]
+        y_real = random.uniform(0.7, 1.2)
+        y_fake = random.uniform(0, 0.3)
+        w = sc.B / B_global
+        loss = w * (bce_loss(s_real, torch.ones_like(s_real) * y_real) +
+                    bce_loss(s_fake, torch.zeros_like(s_fake) * y_fake))
+        self.opt_d.zero_grad(set_to_none=True)
+        loss.backward()
+        vals = self._finish(self.d_params, self.opt_d, [loss], a.clipping_threshold_d)
+        return {"D_data_loss": vals[0], "D_total_loss": vals[0]}
+
+    def g_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None)):
+        """generator_step (train.py:432-484)."""
+        a = self.args
+        G, D = self.G, self.D
+        (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, loss_mask, sse) = batch
+        S_global = S_global or sc.S
+        B_global = B_global or sc.B
+        s0 = shard[0]
+        S, B, k = sc.S, sc.B, a.best_k
+        mask = loss_mask[:, a.obs_len:]                                   # (B, pred_len)
+        zs = [self._noise(S_global, s0, s0 + S) for _ in range(k)]        # k draws, reference order
+        seg = sc.ped_scene_long()
+        mask_sum = torch.zeros(S, device=obs.device).index_add_(0, seg, mask.sum(1))
+
+        def l2_raw(pred_rel):   # losses.py:52-71 mode='raw', per ped
+            return (mask.unsqueeze(2) * (pred_gt_rel.permute(1, 0, 2) - pred_rel.permute(1, 0, 2)) ** 2).sum(2).sum(1)
+
+        use_l2 = a.l2_loss_weight > 0
+        if self.selective_backward and k > 1:
+            z_all = torch.cat(zs, 0) if zs[0] is not None else None
+            sck = sc.repeat(k)
+            with torch.no_grad():
+                pred_all = G(_rep(obs, k), _rep(obs_rel, k), _sse_of(sck), _rep(obs_g, k), user_noise=z_all,
+                             scenes=sck).view(a.pred_len, k, B, 2)
+                if use_l2:
+                    l2k = ((pred_gt_rel.unsqueeze(1) - pred_all) ** 2).sum(3) * mask.t().unsqueeze(1)
+                    l2k = l2k.sum(0)                                          # (k, B)
+                    scene_l2 = torch.zeros(k, S, device=obs.device).index_add_(1, seg, l2k)
+                    best = scene_l2.argmin(0)                                 # (S,)
+            copies = 2 if use_l2 else 1
+            zc = None
+            if z_all is not None:
+                zk = z_all.view(k, S, -1).to(obs.device)
+                parts = ([zk[best, torch.arange(S, device=obs.device)]] if use_l2 else []) + [zk[k - 1]]
+                zc = torch.cat(parts, 0)
+            scc = sc.repeat(copies)
+            out = G(_rep(obs, copies), _rep(obs_rel, copies), _sse_of(scc), _rep(obs_g, copies), user_noise=zc,
+                    scenes=scc)
+            fake_rel_last = out[:, (copies - 1) * B:]
+            fake_rel_best = out[:, :B] if use_l2 else None
+        else:
+            outs = [G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc) for z in zs]
+            fake_rel_last = outs[-1]
+            fake_rel_best = None
+            if use_l2:
+                l2s = torch.stack([l2_raw(o) for o in outs], 0)                # (k, B)
+                scene_l2 = torch.zeros(k, S, device=obs.device).index_add_(1, seg, l2s)
+        terms = []
+        if use_l2:
+            if fake_rel_best is not None:
+                sl2 = torch.zeros(S, device=obs.device).index_add_(0, seg, a.l2_loss_weight * l2_raw(fake_rel_best))
+            else:
+                sl2 = a.l2_loss_weight * scene_l2.min(0)[0]
+            g_l2 = (sl2 / mask_sum).sum()
+            terms.append(g_l2)
+        fake_last = relative_to_abs(fake_rel_last, obs[-1])
+        scores = D(torch.cat([obs, fake_last], 0), torch.cat([obs_rel, fake_rel_last], 0), sse, scenes=sc)
+        y = random.uniform(0.7, 1.2)
+        adv = (sc.B / B_global) * bce_loss(scores, torch.ones_like(scores) * y)
+        loss = adv + (terms[0] if terms else 0.0)
+        self.opt_g.zero_grad(set_to_none=True)
+        torch.autograd.backward(loss, inputs=self.g_params)
+        vals = self._finish(self.g_params, self.opt_g, [terms[0] if terms else adv * 0, adv, loss],
+                            a.clipping_threshold_g)
+        out = {"G_discriminator_loss": vals[1], "G_total_loss": vals[2]}
+        if use_l2:
+            out["G_l2_loss_rel"] = vals[0]
+        return out
+
+    def step(self, batch, sc, **kw):
+        """One reference iteration (d_steps = g_steps = 1) on one batch."""
+        ld = self.d_step(batch, sc, **kw)
+        lg = self.g_step(batch, sc, **kw)
+        return ld, lg
+
+
+def shard_batch(batch, sc, s0, s1):
+    """Rows of scenes [s0, s1) of a global batch + their re-based SceneIndex."""
+    p0, p1 = int(sc.host_off[s0]), int(sc.host_off[s1])
+    (obs, pred, obs_rel, pred_rel, ov, pv, obs_g, pg, nl, lm, sse) = batch
+    t = lambda x: x[:, p0:p1]
+    off = sc.host_off[s0:s1 + 1] - p0
+    local = SceneIndex(off, sc.device)
+    sse_l = _sse_of(local)
+    return (t(obs), t(pred), t(obs_rel), t(pred_rel), t(ov), t(pv), t(obs_g), t(pg), nl[p0:p1], lm[p0:p1],
+            sse_l), local

@@ -199,3 +199,34 @@ def test_evaluate_ade_fde_all_splits():
             ref = ev["%s/%s" % (graph, split)]
             assert abs(ade - ref["ade"]) <= 1e-3 * ref["ade"], (graph, split, ade, ref)
             assert abs(fde - ref["fde"]) <= 1e-3 * ref["fde"], (graph, split, fde, ref)
+
+
+KEYS = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel", "obs_traj_g",
+        "pred_traj_g", "non_linear_ped", "loss_mask", "seq_start_end"]
+
+
+@pytest.mark.parametrize("selective", [True, False])
+def test_train_step_vs_reference_fixture(selective):
+    """Two reference iterations (discriminator_step + generator_step, fresh
+    Adam, seeded host RNGs) reproduced by GanTrainer: losses within 1e-4 rel,
+    weights within Adam's sign-flip bound on noise-level gradients."""
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer
+    g, d = build_models()
+    tr = GanTrainer(g, d, selective_backward=selective)
+    f = npz("train_step.npz")
+    torch.manual_seed(1234)
+    random.seed(1234)
+    for it in range(2):
+        b = [T(f["b%d/%s" % (it, k)]) for k in KEYS]
+        sc = SceneIndex.from_seq_start_end(b[-1], DEV)
+        ld, lg = tr.step(b, sc)
+        for k, v in list(ld.items()) + list(lg.items()):
+            tag = "D" if k.startswith("D") else "G"
+            ref = float(f["it%d/%s/%s" % (it, tag, k)])
+            assert abs(float(v) - ref) <= 1e-4 * max(1.0, abs(ref)), (it, k, float(v), ref)
+        for mod, tag, lr in ((g, "g", 1e-4), (d, "d", 1e-3)):
+            for k, v in mod.state_dict().items():
+                ref = f["it%d/%s/%s" % (it, tag, k)]
+                err = np.abs(v.detach().cpu().numpy().astype(np.float64) - ref).max()
+                assert err <= 2 * lr * (it + 1) + 1e-5 * np.abs(ref).max(), (it, tag, k, err)
