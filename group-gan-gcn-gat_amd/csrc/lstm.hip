@@ -1,0 +1,244 @@
+// Fused LSTM sequences: the Encoder (reference sgan/models.py:32-92) and the
+// autoregressive Decoder rollout (models.py:142-178), forward and backward,
+// one launch each instead of one MIOpen RNN call (plus Linear/cat kernels)
+// per time step.
+//
+// Folding (exact up to fp32 reassociation): the input of every step is a
+// 2-d relative displacement r embedded by Linear(2, E), so
+//   W_ih (We r + be) + b_ih + b_hh = A r + b'    with A = W_ih We (4H x 2),
+//                                                b' = W_ih be + b_ih + b_hh
+// (A and b' are formed by the caller with torch ops, so autograd carries
+// their gradients back to W_ih, We, be, b_ih, b_hh).  Decoder: r_0 is the
+// last observed displacement, r_t = Wp h_t + bp (hidden2pos) feeds step t+1.
+//
+// Layout: one workgroup = P = 4 peds x 4H gate rows (16 H threads); thread
+// (ped, r) owns gate row r: its W_hh row lives in registers, h_{t-1} is read
+// from LDS as a per-ped broadcast, so a step is H register FMAs per thread +
+// one LDS exchange of the gate activations; the H "cell" threads of a ped
+// keep c_t in a register.  The backward uses the column layout (thread
+// (ped, g, k) owns column k of gate block g of W_hh) so dh_{t-1} = W_hh^T dG_t
+// is H register FMAs + a 4-way LDS reduction.  Parameter gradients are sums
+// over (t, ped) of outer products -> the caller's GEMMs on the saved dG.
+#include "sgg_common.h"
+
+namespace sgg {
+
+constexpr int kLstmPeds = 4;
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int H>
+__global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(
+    const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
+    const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
+    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
+    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out) {
+  constexpr int G4 = 4 * H;
+  __shared__ float hbuf[kLstmPeds][H];
+  __shared__ float gbuf[kLstmPeds][G4];
+  __shared__ float relb[kLstmPeds][2];
+  const int pl = threadIdx.x / G4, r = threadIdx.x - pl * G4;
+  const int ped = blockIdx.x * kLstmPeds + pl;
+  const bool valid = ped < B;
+  float w[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) w[k] = Whh[r * H + k];
+  const float a0 = A[2 * r], a1 = A[2 * r + 1], bb = bias[r];
+  const bool is_g = r >= 2 * H && r < 3 * H;
+  float c = 0.f;
+  if (r < H) {
+    const float hv = (valid && h0) ? h0[(size_t)ped * H + r] : 0.f;
+    c = (valid && c0) ? c0[(size_t)ped * H + r] : 0.f;
+    hbuf[pl][r] = hv;
+    if (valid) {
+      h_all[(size_t)ped * H + r] = hv;
+      c_all[(size_t)ped * H + r] = c;
+    }
+  }
+  if (decoder && r < 2) relb[pl][r] = valid ? rel[(size_t)ped * 2 + r] : 0.f;
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    float x0, x1;
+    if (decoder) {
+      x0 = relb[pl][0];
+      x1 = relb[pl][1];
+    } else {
+      x0 = valid ? rel[((size_t)t * B + ped) * 2] : 0.f;
+      x1 = valid ? rel[((size_t)t * B + ped) * 2 + 1] : 0.f;
+    }
+    float acc = fmaf(a1, x1, fmaf(a0, x0, bb));
+#pragma unroll
+    for (int k = 0; k < H; k += 4) {
+      const float4 hv = *reinterpret_cast<const float4*>(&hbuf[pl][k]);
+      acc = fmaf(w[k], hv.x, acc);
+      acc = fmaf(w[k + 1], hv.y, acc);
+      acc = fmaf(w[k + 2], hv.z, acc);
+      acc = fmaf(w[k + 3], hv.w, acc);
+    }
+    const float act = is_g ? tanhf(acc) : sigm(acc);
+    if (act_all && valid) act_all[((size_t)t * B + ped) * G4 + r] = act;
+    gbuf[pl][r] = act;
+    __syncthreads();
+    if (r < H) {
+      const float ig = gbuf[pl][r], fg = gbuf[pl][H + r], gg = gbuf[pl][2 * H + r], og = gbuf[pl][3 * H + r];
+      c = fmaf(fg, c, ig * gg);
+      const float h = og * tanhf(c);
+      hbuf[pl][r] = h;
+      if (valid) {
+        const size_t o = ((size_t)(t + 1) * B + ped) * H + r;
+        h_all[o] = h;
+        c_all[o] = c;
+      }
+    }
+    __syncthreads();
+    if (decoder) {
+      if (r < 2) {
+        float s = bp[r];
+#pragma unroll
+        for (int k = 0; k < H; ++k) s = fmaf(Wp[r * H + k], hbuf[pl][k], s);
+        relb[pl][r] = s;
+        if (valid) rel_out[((size_t)t * B + ped) * 2 + r] = s;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int H>
+__global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
+    const float* __restrict__ A, const float* __restrict__ Whh, const float* __restrict__ Wp,
+    const float* __restrict__ c_all, const float* __restrict__ act_all, const float* __restrict__ dh_last,
+    const float* __restrict__ dout, int T, int B, int decoder, float* __restrict__ dG, float* __restrict__ dh0,
+    float* __restrict__ drel_in, float* __restrict__ drel_tot) {
+  constexpr int G4 = 4 * H;
+  __shared__ float dgb[kLstmPeds][G4];
+  __shared__ float pb[kLstmPeds][4][H];
+  __shared__ float drelb[kLstmPeds][2];
+  const int pl = threadIdx.x / G4, q = threadIdx.x - pl * G4;
+  const int g = q / H, k = q - g * H;
+  const int ped = blockIdx.x * kLstmPeds + pl;
+  const bool valid = ped < B;
+  float wcol[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) wcol[j] = Whh[(g * H + j) * H + k];
+  float a_d = 0.f;  // A[:, d] column is read from global in the q < 2 threads
+  (void)a_d;
+  float dh = 0.f, dc = 0.f, fb = 0.f;
+  const float wp0 = decoder ? Wp[q < H ? q : 0] : 0.f;
+  const float wp1 = decoder ? Wp[H + (q < H ? q : 0)] : 0.f;
+  if (q < H && !decoder && valid && dh_last) dh = dh_last[(size_t)ped * H + q];
+  for (int t = T - 1; t >= 0; --t) {
+    if (decoder) {
+      if (q < 2) {
+        const float v = (valid ? dout[((size_t)t * B + ped) * 2 + q] : 0.f) + fb;
+        drelb[pl][q] = v;
+        if (valid) drel_tot[((size_t)t * B + ped) * 2 + q] = v;
+      }
+      __syncthreads();
+      if (q < H) dh = fmaf(wp0, drelb[pl][0], fmaf(wp1, drelb[pl][1], dh));
+    }
+    if (q < H) {
+      float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, ct = 0.f, cp = 0.f;
+      if (valid) {
+        const size_t ab = ((size_t)t * B + ped) * G4;
+        ig = act_all[ab + q];
+        fg = act_all[ab + H + q];
+        gg = act_all[ab + 2 * H + q];
+        og = act_all[ab + 3 * H + q];
+        ct = c_all[((size_t)(t + 1) * B + ped) * H + q];
+        cp = c_all[((size_t)t * B + ped) * H + q];
+      }
+      const float tc = tanhf(ct);
+      const float d_o = dh * tc;
+      const float dct = fmaf(dh * og, 1.f - tc * tc, dc);
+      const float di = dct * gg, dgg = dct * ig, df = dct * cp;
+      dc = dct * fg;
+      const float vi = di * ig * (1.f - ig), vf = df * fg * (1.f - fg);
+      const float vg = dgg * (1.f - gg * gg), vo = d_o * og * (1.f - og);
+      dgb[pl][q] = vi;
+      dgb[pl][H + q] = vf;
+      dgb[pl][2 * H + q] = vg;
+      dgb[pl][3 * H + q] = vo;
+      if (valid) {
+        const size_t ob = ((size_t)t * B + ped) * G4;
+        dG[ob + q] = vi;
+        dG[ob + H + q] = vf;
+        dG[ob + 2 * H + q] = vg;
+        dG[ob + 3 * H + q] = vo;
+      }
+    }
+    __syncthreads();
+    float p = 0.f;
+#pragma unroll
+    for (int j = 0; j < H; ++j) p = fmaf(wcol[j], dgb[pl][g * H + j], p);
+    pb[pl][g][k] = p;
+    if (q < 2) {
+      float s = 0.f;
+      for (int rr = 0; rr < G4; ++rr) s = fmaf(A[2 * rr + q], dgb[pl][rr], s);
+      fb = s;
+      if (valid) drel_in[((size_t)t * B + ped) * 2 + q] = s;
+    }
+    __syncthreads();
+    if (q < H) dh = pb[pl][0][q] + pb[pl][1][q] + pb[pl][2][q] + pb[pl][3][q];
+    __syncthreads();
+  }
+  if (q < H && valid && dh0) dh0[(size_t)ped * H + q] = dh;
+}
+
+template <int H>
+static int launch_lstm_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
+                           const float* c0, const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all,
+                           float* act_all, float* rel_out, hipStream_t st) {
+  const int grid = (B + kLstmPeds - 1) / kLstmPeds;
+  hipLaunchKernelGGL(lstm_fwd_kernel<H>, dim3(grid), dim3(16 * H), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T,
+                     B, decoder, h_all, c_all, act_all, rel_out);
+  SGG_RETURN_LAUNCH("sgg_lstm_fwd");
+}
+
+template <int H>
+static int launch_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all,
+                           const float* act_all, const float* dh_last, const float* dout, int T, int B, int decoder,
+                           float* dG, float* dh0, float* drel_in, float* drel_tot, hipStream_t st) {
+  const int grid = (B + kLstmPeds - 1) / kLstmPeds;
+  hipLaunchKernelGGL(lstm_bwd_kernel<H>, dim3(grid), dim3(16 * H), 0, st, A, Whh, Wp, c_all, act_all, dh_last, dout,
+                     T, B, decoder, dG, dh0, drel_in, drel_tot);
+  SGG_RETURN_LAUNCH("sgg_lstm_bwd");
+}
+
+}  // namespace sgg
+
+using namespace sgg;
+
+extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
+                            const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
+                            float* c_all, float* act_all, float* rel_out, void* stream) {
+  SGG_CHECK_ARG(rel && A && Whh && bias && h_all && c_all, "sgg_lstm_fwd: null pointer");
+  SGG_CHECK_ARG(!decoder || (Wp && bp && rel_out), "sgg_lstm_fwd: decoder needs Wp, bp, rel_out");
+  SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_fwd: bad sizes T=%d B=%d", T, B);
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (H) {
+    case 16: return launch_lstm_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    case 32: return launch_lstm_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    case 48: return launch_lstm_fwd<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    case 64: return launch_lstm_fwd<64>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    default: SGG_CHECK_ARG(false, "sgg_lstm_fwd: hidden size %d not built (16/32/48/64)", H);
+  }
+}
+
+extern "C" int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all,
+                            const float* act_all, const float* dh_last, const float* dout, int T, int B, int H,
+                            int decoder, float* dG, float* dh0, float* drel_in, float* drel_tot, void* stream) {
+  SGG_CHECK_ARG(A && Whh && c_all && act_all && dG && drel_in, "sgg_lstm_bwd: null pointer");
+  SGG_CHECK_ARG(!decoder || (Wp && dout && drel_tot), "sgg_lstm_bwd: decoder needs Wp, dout, drel_tot");
+  SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_bwd: bad sizes");
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (H) {
+    case 16: return launch_lstm_bwd<16>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    case 32: return launch_lstm_bwd<32>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    case 48: return launch_lstm_bwd<48>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    case 64: return launch_lstm_bwd<64>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    default: SGG_CHECK_ARG(false, "sgg_lstm_bwd: hidden size %d not built (16/32/48/64)", H);
+  }
+}

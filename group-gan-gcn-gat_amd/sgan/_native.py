@@ -32,6 +32,8 @@ SIGNATURES = {
     "sgg_group_index": (_i, [_p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "sgg_seg_reduce": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i, _p]),
     "sgg_seg_gather": (_i, [_p, _i, _i, _p, _p, _p, _i, _p, _i, _p]),
+    "sgg_lstm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
 }
 
 _lib = None

@@ -303,3 +303,85 @@ def scene_mean_over_groups(gx, groups):
                           groups._group_inv_ng, groups.n_groups_dev)
     return _SegGather.apply(sm, groups.group_scene, None, groups.n_groups_dev, groups.cap, groups.group_off, None,
                             None)
+
+
+# ---------------------------------------------------------------------------
+# fused LSTM sequences (encoder / decoder rollout)
+# ---------------------------------------------------------------------------
+class _LSTMSeq(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rel, A, Whh, bias, h0, c0, Wp, bp, decoder, T, save):
+        lib = _lib()
+        rel = _req(rel, "rel").contiguous()
+        H = Whh.shape[1]
+        B = rel.shape[-2]
+        dev = rel.device
+        h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
+        c_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
+        act = torch.empty(T, B, 4 * H, device=dev, dtype=torch.float32) if save else None
+        rel_out = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
+        A, Whh, bias = A.contiguous(), Whh.contiguous(), bias.contiguous()
+        h0c = h0.contiguous() if h0 is not None else None
+        c0c = c0.contiguous() if c0 is not None else None
+        Wpc = Wp.contiguous() if Wp is not None else None
+        N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), N.ptr(Wpc), N.ptr(bp),
+                                 T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out),
+                                 N.stream_ptr()), "sgg_lstm_fwd")
+        ctx.meta = (decoder, T, B, H, h0 is not None)
+        if save:
+            ctx.save_for_backward(rel, A, Whh, Wpc, h_all, c_all, act, rel_out)
+        h_last = h_all[T]
+        if decoder:
+            return h_last, rel_out
+        return h_last, h_last.new_empty(0)
+
+    @staticmethod
+    def backward(ctx, dh_last, drel_out):
+        lib = _lib()
+        decoder, T, B, H, has_h0 = ctx.meta
+        rel, A, Whh, Wp, h_all, c_all, act, rel_out = ctx.saved_tensors
+        dev = rel.device
+        dG = torch.empty(T, B, 4 * H, device=dev, dtype=torch.float32)
+        drel_in = torch.empty(T, B, 2, device=dev, dtype=torch.float32)
+        dh0 = torch.empty(B, H, device=dev, dtype=torch.float32)
+        drel_tot = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
+        if decoder:
+            dout = drel_out.contiguous() if drel_out is not None else torch.zeros(T, B, 2, device=dev)
+            dhl = None
+            # dL/dh_T from a consumer of the final state (unused by the generator)
+            if dh_last is not None and bool(dh_last.abs().sum() > 0):
+                raise NotImplementedError("gradient through the decoder's final hidden state")
+        else:
+            dout = None
+            dhl = dh_last.contiguous() if dh_last is not None else None
+        N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(c_all), N.ptr(act), N.ptr(dhl), N.ptr(dout),
+                                 T, B, H, int(decoder), N.ptr(dG), N.ptr(dh0), N.ptr(drel_in), N.ptr(drel_tot),
+                                 N.stream_ptr()), "sgg_lstm_bwd")
+        dGf = dG.view(T * B, 4 * H)
+        dWhh = dGf.t().mm(h_all[:T].reshape(T * B, H))
+        if decoder:
+            rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0)
+        else:
+            rel_in = rel
+        dA = dGf.t().mm(rel_in.reshape(T * B, 2))
+        dbias = dGf.sum(0)
+        dWp = dbp = None
+        if decoder:
+            dr = drel_tot.view(T * B, 2)
+            dWp = dr.t().mm(h_all[1:].reshape(T * B, H))
+            dbp = dr.sum(0)
+            drel = drel_in[0]
+        else:
+            drel = drel_in
+        return drel, dA, dWhh, dbias, (dh0 if has_h0 else None), None, dWp, dbp, None, None, None
+
+
+def lstm_sequence(rel, A, Whh, bias, h0=None, c0=None, Wp=None, bp=None, decoder=False, T=None):
+    """Fused LSTM over T steps (see sgg_lstm_fwd).  Returns (h_last, rel_out)."""
+    T = T if T is not None else rel.shape[0]
+    save = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad for t in (rel, A, Whh, bias, h0, Wp, bp))
+    if c0 is not None and c0.requires_grad and torch.is_grad_enabled():
+        raise NotImplementedError("gradient w.r.t. the initial cell state")
+    h_last, rel_out = _LSTMSeq.apply(rel, A, Whh, bias, h0, c0, Wp, bp, bool(decoder), T, save)
+    return h_last, (rel_out if decoder else None)

@@ -11,8 +11,8 @@ libsgg.so HIP kernels (sgan/kernels.py):
   - group structure, R / R^T pooling       -> sgg_group_index, sgg_seg_reduce/gather
 
 Scene bookkeeping is an int32 CSR built once per batch (sgan/scene.py)
-instead of a `.item()` per scene per module.  The LSTMs of the encoder and
-decoder stay on torch (MIOpen) for now.
+instead of a `.item()` per scene per module.  The encoder LSTM and the 12-step
+decoder rollout are single fused launches (sgg_lstm_fwd / sgg_lstm_bwd).
 
 Extra keyword-only arguments beyond the reference's are optional and default
 to the reference behaviour:
@@ -101,8 +101,16 @@ def get_noise(shape, noise_type):
 
 
 # ---------------------------------------------------------------------------
-# encoder / decoder (torch LSTM; models.py:32-178)
+# encoder / decoder (models.py:32-178) -> sgg_lstm_fwd / sgg_lstm_bwd
 # ---------------------------------------------------------------------------
+def _fold_embedding(lstm, emb):
+    """Input weights of a 1-layer LSTM fed by Linear(2, E): A = W_ih We (4H x 2),
+    b = W_ih be + b_ih + b_hh (torch ops: autograd carries their gradients)."""
+    W_ih = lstm.weight_ih_l0
+    A = W_ih.mm(emb.weight)
+    b = torch.addmv(lstm.bias_ih_l0 + lstm.bias_hh_l0, W_ih, emb.bias)
+    return A, b
+
 class Encoder(nn.Module):
     def __init__(self, embedding_dim=64, h_dim=64, mlp_dim=1024, num_layers=1, dropout=0.0):
         super().__init__()
@@ -114,11 +122,13 @@ class Encoder(nn.Module):
         self.encoder = nn.LSTM(embedding_dim, h_dim, num_layers, dropout=dropout)
 
     def forward(self, obs_traj):
-        T, B = obs_traj.shape[:2]
-        emb = K.linear(obs_traj.reshape(-1, 2), self.spatial_embedding).view(T, B, self.embedding_dim)
-        z = torch.zeros(self.num_layers, B, self.h_dim, device=obs_traj.device)
-        _, (h, _) = self.encoder(emb, (z, z))
-        return h
+        """Fused sgg_lstm_fwd over all T steps; the Linear(2, E) embedding is
+        folded into the input weights (A = W_ih We, b = W_ih be + b_ih + b_hh)."""
+        if self.num_layers != 1:
+            raise NotImplementedError("fused LSTM kernel: num_layers must be 1 (all reference configs)")
+        A, b = _fold_embedding(self.encoder, self.spatial_embedding)
+        h, _ = K.lstm_sequence(obs_traj, A, self.encoder.weight_hh_l0, b)
+        return h.unsqueeze(0)
 
 
 class Decoder(nn.Module):
@@ -143,6 +153,15 @@ class Decoder(nn.Module):
                                 batch_norm=batch_norm, dropout=dropout)
 
     def forward(self, last_pos, last_pos_rel, state_tuple, seq_start_end, scenes=None):
+        if not self.pool_every_timestep:
+            # the whole 12-step rollout (LSTM step -> hidden2pos -> embedding
+            # of the predicted displacement) is one sgg_lstm_fwd launch
+            A, b = _fold_embedding(self.decoder, self.spatial_embedding)
+            h0, c0 = state_tuple
+            h, rel = K.lstm_sequence(last_pos_rel, A, self.decoder.weight_hh_l0, b, h0=h0[0], c0=c0[0],
+                                     Wp=self.hidden2pos.weight, bp=self.hidden2pos.bias, decoder=True,
+                                     T=self.seq_len)
+            return rel, h.unsqueeze(0)
         B = last_pos.size(0)
         x = K.linear(last_pos_rel, self.spatial_embedding).view(1, B, self.embedding_dim)
         outs = []

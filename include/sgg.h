@@ -146,6 +146,35 @@ int sgg_seg_gather(const float* src, int lds, int F, const int32_t* seg_of_row,
                    const float* row_scale, const int32_t* nrow_dev, int n, float* out, int ldo,
                    void* stream);
 
+/* ------------------------------------------------------------------------
+ * Fused LSTM sequence (Encoder.forward models.py:62-92; Decoder.forward
+ * :142-178 with pool_every_timestep = 0), one launch for all T steps:
+ *   gates_t = A r_t + W_hh h_{t-1} + bias   (A = W_ih We, bias = W_ih be + b_ih + b_hh:
+ *                                           the Linear(2, E) input embedding folded in)
+ *   i, f, o = sigmoid, g = tanh;  c_t = f c_{t-1} + i g;  h_t = o tanh(c_t)
+ * encoder (decoder = 0): r_t = rel[t] (T x B x 2); h_{-1} = h0, c_{-1} = c0 (NULL = 0).
+ * decoder (decoder = 1): r_0 = rel (B x 2), r_t = Wp h_{t-1} + bp (hidden2pos) for
+ *   t >= 1; rel_out[t] = Wp h_t + bp (T x B x 2) is the predicted displacement.
+ * H in {16, 32, 48, 64}.  Outputs h_all, c_all: (T+1) x B x H with index 0 the
+ * initial state; act_all (T x B x 4H, gate activations i|f|g|o) may be NULL
+ * (inference) and is required by the backward. */
+int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float* bias,
+                 const float* h0, const float* c0, const float* Wp, const float* bp, int T, int B, int H,
+                 int decoder, float* h_all, float* c_all, float* act_all, float* rel_out,
+                 void* stream);
+
+/* Backward of sgg_lstm_fwd (BPTT).  encoder: dh_last = dL/dh_{T-1} (B x H, may
+ * be NULL); decoder: dout = dL/drel_out (T x B x 2) (the decoder feedback
+ * r_t -> step t+1 is included).  Writes dG (T x B x 4H, gradient of the gate
+ * pre-activations), drel_in (T x B x 2, dL/dr_t of the step inputs), dh0
+ * (B x H, may be NULL; no gradient is produced for c0) and, for the decoder, drel_tot (T x B x 2, total
+ * dL/d rel_out[t]).  Parameter gradients are outer-product sums over (t, ped)
+ * of these and the saved states -- plain GEMMs left to the caller. */
+int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all,
+                 const float* act_all, const float* dh_last, const float* dout, int T, int B,
+                 int H, int decoder, float* dG, float* dh0, float* drel_in, float* drel_tot,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

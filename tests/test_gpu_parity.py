@@ -230,3 +230,43 @@ def test_train_step_vs_reference_fixture(selective):
                 ref = f["it%d/%s/%s" % (it, tag, k)]
                 err = np.abs(v.detach().cpu().numpy().astype(np.float64) - ref).max()
                 assert err <= 2 * lr * (it + 1) + 1e-5 * np.abs(ref).max(), (it, tag, k, err)
+
+
+@pytest.mark.parametrize("H,T,decoder", [(32, 8, False), (48, 20, False), (32, 12, True), (16, 5, True), (64, 3, False)])
+def test_fused_lstm_vs_oracle(H, T, decoder):
+    """sgg_lstm_fwd/bwd (Encoder / Decoder rollout) against the oracle's
+    torch-CPU modules: outputs and every parameter / input gradient."""
+    from oracle import sgan_oracle as O
+    from sgan import models as M
+    torch.manual_seed(H + T)
+    B = 37
+    if decoder:
+        ref, mod = O.Decoder(T, 16, H, 64, 1, False), M.Decoder(T, 16, H, 64, 1, False)
+    else:
+        ref, mod = O.Encoder(16, H), M.Encoder(16, H)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(DEV)
+    if decoder:
+        last_pos, last_rel = torch.randn(B, 2), torch.randn(B, 2) * 0.3
+        h0 = (torch.randn(1, B, H) * 0.5).requires_grad_(True)
+        c0 = torch.zeros(1, B, H)
+        y_ref, _ = ref(last_pos, last_rel, (h0, c0), None)
+        h0d = h0.detach().to(DEV).requires_grad_(True)
+        y, _ = mod(last_pos.to(DEV), last_rel.to(DEV), (h0d, c0.to(DEV)), None)
+        dy = torch.randn_like(y_ref)
+        (y_ref * dy).sum().backward()
+        (y * dy.to(DEV)).sum().backward()
+        close(y, y_ref.detach().numpy(), rtol=1e-5, what="decoder out")
+        close(h0d.grad, h0.grad.numpy(), rtol=1e-4, what="decoder dh0")
+    else:
+        rel = (torch.randn(T, B, 2) * 0.3).requires_grad_(True)
+        y_ref = ref(rel)
+        reld = rel.detach().to(DEV).requires_grad_(True)
+        y = mod(reld)
+        dy = torch.randn_like(y_ref)
+        (y_ref * dy).sum().backward()
+        (y * dy.to(DEV)).sum().backward()
+        close(y, y_ref.detach().numpy(), rtol=1e-5, what="encoder h")
+        close(reld.grad, rel.grad.numpy(), rtol=1e-4, what="encoder drel")
+    for (k, p), (_, q) in zip(ref.named_parameters(), mod.named_parameters()):
+        close(q.grad, p.grad.numpy(), rtol=1e-4, floor=1e-6, what="lstm d" + k)
