@@ -27,71 +27,184 @@
 
 namespace sgg {
 
-constexpr int kURow = kHidden + 4;  // padded LDS row (floats)
+
+// ---- forward: MFMA layer 2 ---------------------------------------------------
+// Work unit = a chunk of whole i-rows [i0, i1) of one scene (host plan,
+// sgg_pool_plan): every pair (i, j) of those rows, j fastest, cut into 16-pair
+// MFMA groups, GPW groups per wave (the tail groups of a chunk are padding).
+// Keeping whole i-rows in one workgroup makes max_j complete there (LDS
+// atomics only).  The 512 hidden units are walked in k-tiles of 64 staged in
+// LDS (U rows of the scene, W2^T tile, A tile); per 4-deep k-step a lane builds
+// ONE hidden value per group (pair l&15, unit l>>4: 2 FMA + max) -- the A
+// operand of v_mfma_f32_16x16x4_f32 against the W2^T fragment, NT = bn/16
+// column tiles.  fp32 in, fp32 accumulate (exact fmaf chains).  The next
+// k-step's LDS operands are loaded before the current step's MFMAs.
+constexpr int kKT = 64;          // hidden units per LDS k-tile
+constexpr int kKTP = kKT + 2;    // U tile row stride: (2j + k) mod 32 -> conflict-free b32 reads
+constexpr int kPoolWaves = 4;
 
 template <int BN>
+struct PoolCfg {
+  static constexpr int NT = (BN + 15) / 16;                      // 16-wide column tiles
+  static constexpr int BNP = NT * 16 + ((NT % 2 == 0) ? 16 : 0); // odd multiple of 16: conflict-free B reads
+};
+
+template <int BN, int GPW>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2T /* 512 x BN */, const float* __restrict__ b2,
-    const int32_t* __restrict__ scene_off, int S, float* __restrict__ out, int32_t* __restrict__ argmax) {
+    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+  using C = PoolCfg<BN>;
+  constexpr int NT = C::NT, BNP = C::BNP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int max_n = SGG_POOL_MAX_PEDS;
-  (void)max_n;
-  for (int s = blockIdx.x; s < S; s += gridDim.x) {
+  float* Us = reinterpret_cast<float*>(smem);                              // 64 x kKTP
+  float* W2s = Us + SGG_POOL_MAX_PEDS * kKTP;                              // kKT x BNP
+  float* As = W2s + kKT * BNP;                                             // kKT x 2
+  float2* ps = reinterpret_cast<float2*>(As + 2 * kKT);                    // scene positions (<= 64)
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // 64 x BN
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kq = lane >> 4;
+
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int4 cd = chunks[ch];
+    const int s = cd.x, i0 = cd.y, i1 = cd.z;
     const int o = scene_off[s];
     const int n = scene_off[s + 1] - o;
-    float* Us = reinterpret_cast<float*>(smem);
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(Us + (size_t)n * kURow);
-    float2* ps = reinterpret_cast<float2*>(keys + (size_t)n * BN);
+    const int rows = i1 - i0;
+    const int npairs = rows * n;
 
-    // stage U rows (float4 granules) and positions
-    const float4* Ug = reinterpret_cast<const float4*>(U + (size_t)o * kHidden);
-    for (int q = threadIdx.x; q < n * (kHidden / 4); q += blockDim.x) {
-      const int r = q / (kHidden / 4), c4 = q - r * (kHidden / 4);
-      *reinterpret_cast<float4*>(Us + (size_t)r * kURow + 4 * c4) = Ug[q];
-    }
     for (int q = threadIdx.x; q < n; q += blockDim.x) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
-    for (int q = threadIdx.x; q < n * BN; q += blockDim.x) keys[q] = 0ull;
-    __syncthreads();
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) keys[q] = 0ull;
+    __syncthreads();  // ps visible for the per-lane pair set-up below
 
-    const int npairs = n * n;
-    for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
-      const int j = p / n;
-      const int i = p - j * n;
-      const float rx = ps[j].x - ps[i].x;
-      const float ry = ps[j].y - ps[i].y;
-      const float* ur = Us + (size_t)j * kURow;
-      float acc[BN];
+    // per-lane A-row pair of each group (padding pairs -> j = 0, r = 0)
+    int uoff[GPW];
+    float rx[GPW], ry[GPW];
+    floatx4 acc[GPW][NT];
 #pragma unroll
-      for (int c = 0; c < BN; ++c) acc[c] = 0.f;
-      for (int k4 = 0; k4 < kHidden; k4 += 4) {
-        const float4 u = *reinterpret_cast<const float4*>(ur + k4);
-        const float uu[4] = {u.x, u.y, u.z, u.w};
+    for (int g = 0; g < GPW; ++g) {
+      const int p = (wave * GPW + g) * 16 + c16;
+      int il = 0, j = 0;
+      if (p < npairs) { il = p / n; j = p - il * n; }
+      uoff[g] = j * kKTP + kq;
+      const float2 pj = ps[j], pi = ps[i0 + il];
+      rx[g] = p < npairs ? pj.x - pi.x : 0.f;
+      ry[g] = p < npairs ? pj.y - pi.y : 0.f;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int k = k4 + q;
-          float h = fmaf(A[2 * k + 1], ry, fmaf(A[2 * k], rx, uu[q]));
-          h = h > 0.f ? h : 0.f;
+      for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    // k-tiles of 64 hidden units, register-staged one tile ahead (the next
+    // tile's global loads are in flight while the current tile computes)
+    constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + 255) / 256;   // float4 of U per thread
+    constexpr int kWQ = (kKT * BNP + 255) / 256;                       // W2^T floats per thread
+    float4 ureg[kUQ];
+    float wreg[kWQ];
+    float areg = 0.f;
+    auto load_tile = [&](int k0) {
 #pragma unroll
-          for (int c = 0; c < BN; ++c) acc[c] = fmaf(W2T[k * BN + c], h, acc[c]);
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n) ureg[e] = *reinterpret_cast<const float4*>(U + (size_t)(o + r) * kHidden + k0 + 4 * c4);
+      }
+#pragma unroll
+      for (int e = 0; e < kWQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int kk = q / BNP, cc = q - kk * BNP;
+        wreg[e] = (kk < kKT && cc < BN) ? W2T[(size_t)(k0 + kk) * BN + cc] : 0.f;
+      }
+      if (threadIdx.x < 2 * kKT) areg = A[2 * k0 + threadIdx.x];
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n) {
+          float* d = Us + r * kKTP + 4 * c4;
+          d[0] = ureg[e].x; d[1] = ureg[e].y; d[2] = ureg[e].z; d[3] = ureg[e].w;
         }
       }
-      const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
 #pragma unroll
-      for (int c = 0; c < BN; ++c) {
-        float v = acc[c] + b2[c];
-        v = v > 0.f ? v : 0.f;
-        const unsigned long long key = ((unsigned long long)__float_as_uint(v) << 32) | jkey;
-        atomicMax(&keys[i * BN + c], key);
+      for (int e = 0; e < kWQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        if (q < kKT * BNP) W2s[q] = wreg[e];
+      }
+      if (threadIdx.x < 2 * kKT) As[threadIdx.x] = areg;
+    };
+    load_tile(0);
+    __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
+    store_tile();
+    __syncthreads();
+    for (int k0 = 0; k0 < kHidden; k0 += kKT) {
+      if (k0 + kKT < kHidden) load_tile(k0 + kKT);
+      float b[NT], u[GPW];
+      float2 a;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[t] = W2s[kq * BNP + 16 * t + c16];
+      a = *reinterpret_cast<const float2*>(As + 2 * kq);
+#pragma unroll
+      for (int g = 0; g < GPW; ++g) u[g] = Us[uoff[g]];
+#pragma unroll 2
+      for (int s4 = 0; s4 < kKT / 4; ++s4) {
+        float h[GPW], bc[NT];
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) h[g] = fmaxf(fmaf(a.y, ry[g], fmaf(a.x, rx[g], u[g])), 0.f);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bc[t] = b[t];
+        if (s4 + 1 < kKT / 4) {  // prefetch the next k-step's operands
+          const int kn = 4 * (s4 + 1);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) b[t] = W2s[(kn + kq) * BNP + 16 * t + c16];
+          a = *reinterpret_cast<const float2*>(As + 2 * (kn + kq));
+#pragma unroll
+          for (int g = 0; g < GPW; ++g) u[g] = Us[uoff[g] + kn];
+        }
+#pragma unroll
+        for (int g = 0; g < GPW; ++g)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(h[g], bc[t], acc[g][t], 0, 0, 0);
+      }
+      __syncthreads();  // tile consumed
+      if (k0 + kKT < kHidden) {
+        store_tile();
+        __syncthreads();
+      }
+    }
+
+    // epilogue: bias, ReLU, max over j (LDS atomic max on (bits << 32 | ~j))
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int grp = wave * GPW + g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = grp * 16 + kq * 4 + r;
+        if (p < npairs) {
+          const int il = p / n, j = p - il * n;
+          const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int cc = 16 * t + c16;
+            if (cc < BN) {
+              float v = acc[g][t][r] + b2[cc];
+              v = v > 0.f ? v : 0.f;
+              atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
+            }
+          }
+        }
       }
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < n * BN; q += blockDim.x) {
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) {
       const unsigned long long key = keys[q];
-      out[(size_t)o * BN + q] = __uint_as_float((unsigned)(key >> 32));
-      argmax[(size_t)o * BN + q] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+      const size_t oi = (size_t)(o + i0) * BN + q;
+      out[oi] = __uint_as_float((unsigned)(key >> 32));
+      argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
     }
-    __syncthreads();  // LDS reused by the next scene
+    __syncthreads();
   }
 }
 
@@ -177,8 +290,20 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
   dA_part[((size_t)blockIdx.x * kHidden + k) * 2 + 1] = dA1;
 }
 
-static size_t pool_fwd_lds(int bn, int max_n) {
-  return (size_t)max_n * kURow * 4 + (size_t)max_n * bn * 8 + (size_t)max_n * 8 + 16;
+template <int BN>
+static size_t pool_fwd_lds(int max_rows) {
+  using C = PoolCfg<BN>;
+  return sizeof(float) * ((size_t)SGG_POOL_MAX_PEDS * kKTP + (size_t)kKT * C::BNP + 2 * kKT) +
+         sizeof(float2) * SGG_POOL_MAX_PEDS + sizeof(unsigned long long) * (size_t)max_rows * BN;
+}
+
+template <int BN, int GPW>
+static void launch_fwd_g(const float* U, const float* pos, const float* A, const float* W2T, const float* b2,
+                         const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, float* out,
+                         int32_t* am, hipStream_t st) {
+  const int grid = nchunks < 65536 ? nchunks : 65536;
+  hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW>), dim3(grid), dim3(256), pool_fwd_lds<BN>(max_rows), st, U, pos, A,
+                     W2T, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, out, am);
 }
 static size_t pool_bwd_lds(int bn, int max_n) {
   return (size_t)bn * kHidden * 4 + (size_t)max_n * bn * 12 + (size_t)(((max_n + 2) & ~1) * 4) +
@@ -187,10 +312,14 @@ static size_t pool_bwd_lds(int bn, int max_n) {
 
 template <int BN>
 static int launch_fwd(const float* U, const float* pos, const float* A, const float* W2T, const float* b2,
-                      const int32_t* off, int S, int max_n, float* out, int32_t* am, hipStream_t st) {
-  const size_t lds = pool_fwd_lds(BN, max_n);
-  const int grid = S < 8192 ? S : 8192;
-  hipLaunchKernelGGL(pool_fwd_kernel<BN>, dim3(grid), dim3(256), lds, st, U, pos, A, W2T, b2, off, S, out, am);
+                      const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, int gpw, float* out,
+                      int32_t* am, hipStream_t st) {
+  switch (gpw) {
+    case 1: launch_fwd_g<BN, 1>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    case 2: launch_fwd_g<BN, 2>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    case 4: launch_fwd_g<BN, 4>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    default: launch_fwd_g<BN, 8>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+  }
   SGG_RETURN_LAUNCH("sgg_pool_fwd");
 }
 
@@ -210,22 +339,75 @@ using namespace sgg;
 
 static bool pool_bn_ok(int bn) { return bn == 8 || bn == 16 || bn == 32 || bn == 48 || bn == 64; }
 
+static int plan_rows(int n, int gpw) {
+  int rows = (16 * kPoolWaves * gpw) / n;
+  if (rows > 64) rows = 64;
+  return rows < 1 ? 1 : rows;
+}
+
+extern "C" int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int target_chunks, int max_gpw,
+                             int32_t* chunks, int cap, int* max_rows, int* gpw_out) {
+  // host helper: pick the widest per-wave group count whose chunking still
+  // yields >= target_chunks workgroups, then split every scene into chunks
+  // of whole i-rows (see pool_fwd_kernel).
+  if (!host_scene_off || !chunks || !max_rows || !gpw_out || S < 0 || cap < 0) {
+    sgg::set_error("sgg_pool_plan: bad argument");
+    return SGG_E_ARG;
+  }
+  int gpw = bn > 16 ? 4 : 8;  // register budget: GPW x NT accumulator tiles
+  if (max_gpw > 0) {
+    while (gpw > max_gpw && gpw > 1) gpw >>= 1;
+  }
+  for (; gpw > 1; gpw >>= 1) {
+    long nc = 0;
+    for (int s = 0; s < S; ++s) {
+      const int n = host_scene_off[s + 1] - host_scene_off[s];
+      if (n > 0) nc += (n + plan_rows(n, gpw) - 1) / plan_rows(n, gpw);
+    }
+    if (nc >= target_chunks) break;
+  }
+  int nc = 0, mr = 1;
+  for (int s = 0; s < S; ++s) {
+    const int n = host_scene_off[s + 1] - host_scene_off[s];
+    if (n <= 0) continue;
+    const int rows = plan_rows(n, gpw);
+    for (int i0 = 0; i0 < n; i0 += rows) {
+      const int i1 = i0 + rows < n ? i0 + rows : n;
+      if (nc >= cap) {
+        sgg::set_error("sgg_pool_plan: chunk table capacity %d exceeded", cap);
+        return SGG_E_ARG;
+      }
+      chunks[4 * nc + 0] = s;
+      chunks[4 * nc + 1] = i0;
+      chunks[4 * nc + 2] = i1;
+      chunks[4 * nc + 3] = gpw;
+      if (i1 - i0 > mr) mr = i1 - i0;
+      ++nc;
+    }
+  }
+  *max_rows = mr;
+  *gpw_out = gpw;
+  return nc;
+}
+
 extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2T, const float* b2,
-                            const int32_t* scene_off, int S, int B, int bn, int max_n, float* out,
-                            int32_t* argmax, void* stream) {
-  SGG_CHECK_ARG(U && pos && A && W2T && b2 && scene_off && out && argmax, "sgg_pool_fwd: null pointer");
+                            const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
+                            int B, int bn, int max_n, float* out, int32_t* argmax, void* stream) {
+  SGG_CHECK_ARG(U && pos && A && W2T && b2 && scene_off && chunks && out && argmax, "sgg_pool_fwd: null pointer");
   SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_fwd: bottleneck %d not built (8/16/32/48/64)", bn);
-  SGG_CHECK_ARG(S >= 0 && B >= 0, "sgg_pool_fwd: bad sizes");
+  SGG_CHECK_ARG(nchunks >= 0 && B >= 0, "sgg_pool_fwd: bad sizes");
   SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "sgg_pool_fwd: max scene size %d outside [1, %d]",
                 max_n, SGG_POOL_MAX_PEDS);
-  if (S == 0) return 0;
+  SGG_CHECK_ARG(max_rows >= 1 && max_rows <= 64, "sgg_pool_fwd: chunk rows %d outside [1, 64]", max_rows);
+  SGG_CHECK_ARG(gpw == 1 || gpw == 2 || gpw == 4 || gpw == 8, "sgg_pool_fwd: gpw %d not in {1,2,4,8}", gpw);
+  if (nchunks == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (bn) {
-    case 8: return launch_fwd<8>(U, pos, A, W2T, b2, scene_off, S, max_n, out, argmax, st);
-    case 16: return launch_fwd<16>(U, pos, A, W2T, b2, scene_off, S, max_n, out, argmax, st);
-    case 32: return launch_fwd<32>(U, pos, A, W2T, b2, scene_off, S, max_n, out, argmax, st);
-    case 48: return launch_fwd<48>(U, pos, A, W2T, b2, scene_off, S, max_n, out, argmax, st);
-    default: return launch_fwd<64>(U, pos, A, W2T, b2, scene_off, S, max_n, out, argmax, st);
+    case 8: return launch_fwd<8>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 16: return launch_fwd<16>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 32: return launch_fwd<32>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 48: return launch_fwd<48>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    default: return launch_fwd<64>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
   }
 }
 

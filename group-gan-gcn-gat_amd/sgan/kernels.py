@@ -133,9 +133,10 @@ class _Pool(torch.autograd.Function):
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+        chunks, nchunks, max_rows, gpw = scenes.pool_plan(bn)
         N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2T), N.ptr(b2), N.ptr(scenes.scene_off),
-                                 scenes.S, B, bn, scenes.max_n, N.ptr(out), N.ptr(am), N.stream_ptr()),
-                "sgg_pool_fwd")
+                                 N.ptr(chunks), nchunks, max_rows, gpw, B, bn, scenes.max_n, N.ptr(out), N.ptr(am),
+                                 N.stream_ptr()), "sgg_pool_fwd")
         if timed:
             e1.record()
             pool_timer.rec.append((bn, _pool_flops(scenes, bn), e0, e1))

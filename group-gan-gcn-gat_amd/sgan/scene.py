@@ -53,6 +53,30 @@ class SceneIndex:
                 self.device, non_blocking=True)
         return self._ped_scene
 
+    POOL_TARGET_CHUNKS = 512
+    POOL_MAX_GPW = int(__import__("os").environ.get("SGG_POOL_MAX_GPW", "0"))
+
+    def pool_plan(self, bn, target_chunks=None):
+        """Device chunk table for sgg_pool_fwd (built on the host by
+        sgg_pool_plan, cached per bottleneck width)."""
+        target_chunks = target_chunks or self.POOL_TARGET_CHUNKS
+        plans = self.__dict__.setdefault("_pool_plans", {})
+        key = (bn > 16, target_chunks, self.POOL_MAX_GPW)
+        if key not in plans:
+            import ctypes
+            lib = N.load()
+            off = np.ascontiguousarray(self.host_off.astype(np.int32))
+            cap = int(self.B) + self.S + 1
+            tab = np.zeros((cap, 4), dtype=np.int32)
+            mr, gpw = ctypes.c_int(0), ctypes.c_int(0)
+            nc = lib.sgg_pool_plan(off.ctypes.data_as(ctypes.c_void_p), self.S, bn, target_chunks, self.POOL_MAX_GPW,
+                                   tab.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(mr), ctypes.byref(gpw))
+            if nc < 0:
+                N.check(nc, "sgg_pool_plan")
+            dev = torch.from_numpy(tab[:max(nc, 1)].copy()).to(self.device, non_blocking=True)
+            plans[key] = (dev, int(nc), int(mr.value), int(gpw.value))
+        return plans[key]
+
     # -- groups ---------------------------------------------------------------
     def groups(self, labels):
         """Group structure from last-observation labels (B,) float on device."""

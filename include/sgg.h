@@ -58,15 +58,28 @@ int sgg_xw(const float* X, int ldx, const float* W, int trans_w, const float* bi
  * where U = h W1h^T + (W1e be + b1) (one sgg_xw) and A = W1e We, i.e. the
  * reference's Linear(2,E) -> cat[., h_j] -> Linear(E+H,512) with the
  * embedding folded into the first layer.  The (N^2 x 512) pair tensor is
- * never materialised.  argmax[i,c] receives the GLOBAL ped index j that
- * attains the max (smallest j on ties) for the backward.
+ * never materialised; the 512 -> bn layer runs on fp32 MFMA.  argmax[i,c]
+ * receives the GLOBAL ped index j that attains the max (smallest j on ties)
+ * for the backward.
  *   U: B x 512, pos: B x 2, A: 512 x 2, W2T: 512 x bn (= W2^T), b2: bn
  *   out: B x bn, argmax: B x bn (int32).  bn in {8, 16, 32, 48, 64}.
  *   max_n = largest scene size in the batch (<= SGG_POOL_MAX_PEDS).
+ * Work is split into chunks of whole i-rows of one scene; the chunk table
+ * (int32 x 4 per chunk: scene, i0, i1, gpw) is built on the HOST by
+ * sgg_pool_plan from the host copy of scene_off and copied to the device by
+ * the caller (once per batch).  sgg_pool_plan returns the number of chunks
+ * (<= cap) or SGG_E_ARG, the largest chunk height in *max_rows and the
+ * 16-pair groups per wave in *gpw (1, 2, 4 or 8: the widest that still gives
+ * >= target_chunks workgroups, capped by max_gpw when > 0; ~2-4x the CU
+ * count keeps small batches busy).
+ * Pass max_rows and gpw unchanged to sgg_pool_fwd.
  */
+int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int target_chunks, int max_gpw,
+                  int32_t* host_chunks, int cap, int* max_rows, int* gpw);
 int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2T,
-                 const float* b2, const int32_t* scene_off, int S, int B, int bn, int max_n,
-                 float* out, int32_t* argmax, void* stream);
+                 const float* b2, const int32_t* scene_off, const int32_t* chunks, int nchunks,
+                 int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,
+                 void* stream);
 
 /* Backward of sgg_pool_fwd.  Only the (i, argmax[i,c]) pairs carry gradient
  * (torch.max(dim) backward, models.py:541).  Writes dU (B x 512, every row),

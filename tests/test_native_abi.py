@@ -49,3 +49,37 @@ def test_product_path_has_no_cpu_fallback():
     from sgan import kernels
     with pytest.raises(_native.NativeError):
         kernels.xw(torch.ones(4, 4), torch.ones(4, 4))
+
+
+def test_pool_plan_covers_every_row_once():
+    """sgg_pool_plan (host function of the C ABI): chunks are whole i-rows of
+    one scene, cover every (scene, row) exactly once, respect the pair cap."""
+    import ctypes
+    import numpy as np
+    from sgan import _native
+    if not os.path.exists(_native.lib_path()):
+        pytest.skip("libsgg.so not built")
+    lib = _native.load(require_gpu=False)
+    rng = np.random.default_rng(0)
+    for bn in (8, 48):
+        for sizes in ([20] * 64, [1, 2, 64, 57, 3, 20, 0, 5], list(rng.integers(1, 65, size=300))):
+            off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+            S = len(sizes)
+            for target in (1, 64, 1024, 100000):
+                cap = int(off[-1]) + S + 1
+                tab = np.zeros((cap, 4), np.int32)
+                mr, gpw = ctypes.c_int(0), ctypes.c_int(0)
+                nc = lib.sgg_pool_plan(off.ctypes.data_as(ctypes.c_void_p), S, bn, target, 0,
+                                       tab.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(mr), ctypes.byref(gpw))
+                assert nc > 0 and gpw.value in (1, 2, 4, 8)
+                cap_pairs = max(64 * gpw.value, 64)
+                seen = {}
+                for s, i0, i1, _ in tab[:nc]:
+                    n = sizes[s]
+                    assert 0 <= i0 < i1 <= n and i1 - i0 <= 64
+                    assert (i1 - i0) * n <= cap_pairs or i1 - i0 == 1
+                    assert i1 - i0 <= mr.value
+                    for i in range(i0, i1):
+                        assert (s, i) not in seen
+                        seen[(s, i)] = 1
+                assert len(seen) == int(off[-1])
