@@ -354,7 +354,7 @@ extern "C" int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int t
     sgg::set_error("sgg_pool_plan: bad argument");
     return SGG_E_ARG;
   }
-  int gpw = bn > 16 ? 4 : 8;  // register budget: GPW x NT accumulator tiles
+  int gpw = bn > 16 ? 4 : 2;  // measured best caps (register budget vs LDS re-staging)
   if (max_gpw > 0) {
     while (gpw > max_gpw && gpw > 1) gpw >>= 1;
   }

@@ -1,0 +1,108 @@
+"""Scene-sharded data parallelism (sgan/train_step.py) on CPU with gloo,
+world_size 2: one D-step + G-step on a global batch split across ranks must
+equal the single-process step on the whole batch (losses and weights).  The
+models are the CPU oracle's behind a thin adapter: this checks the host-side
+DP logic (sharding, global noise draw and slicing, loss scaling, the one
+flat all-reduce, clipping after the reduce), not the kernels."""
+import os
+import random
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+
+SIZES = [20, 7, 13, 2, 20, 9]
+
+
+class _Adapt(torch.nn.Module):
+    """Oracle module with the product's keyword-only `scenes=` argument."""
+
+    def __init__(self, m):
+        super().__init__()
+        self.m = m
+
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(self.m, name)
+
+    def forward(self, *a, scenes=None, **k):
+        return self.m(*a, **k)
+
+
+def _models():
+    from oracle import sgan_oracle as O
+    w = np.load(os.path.join(GOLDEN, "weights.npz"))
+    g, d = O.build_default("gat")
+    g.load_state_dict({k[2:]: torch.from_numpy(w[k]) for k in w.files if k.startswith("g/")})
+    d.load_state_dict({k[2:]: torch.from_numpy(w[k]) for k in w.files if k.startswith("d/")})
+    return _Adapt(g), _Adapt(d)
+
+
+def _run(rank, world, port, out):
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import DataParallel, GanTrainer, shard_batch
+    torch.set_num_threads(1)
+    if world > 1:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    g, d = _models()
+    tr = GanTrainer(g, d, dp=DataParallel())
+    batch = synthetic_batch(SIZES, seed=11)
+    sc = SceneIndex(np.concatenate([[0], np.cumsum(SIZES)]), "cpu")
+    s0, s1 = tr.dp.shard(sc.S)
+    local, lsc = shard_batch(batch, sc, s0, s1)
+    torch.manual_seed(5)
+    random.seed(5)
+    losses = []
+    for _ in range(2):
+        ld, lg = tr.step(local, lsc, S_global=sc.S, B_global=sc.B, shard=(s0, s1))
+        losses.append([float(v) for v in list(ld.values()) + list(lg.values())])
+    if rank == 0:
+        torch.save({"g": g.m.state_dict(), "d": d.m.state_dict(), "losses": losses}, out)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.slow
+def test_two_rank_step_equals_single_process():
+    with tempfile.TemporaryDirectory() as td:
+        single, multi = os.path.join(td, "single.pt"), os.path.join(td, "multi.pt")
+        _run(0, 1, 0, single)
+        mp.spawn(_run, args=(2, _free_port(), multi), nprocs=2, join=True)
+        a = torch.load(single, weights_only=True)
+        b = torch.load(multi, weights_only=True)
+    for la, lb in zip(a["losses"], b["losses"]):
+        np.testing.assert_allclose(la, lb, rtol=1e-5, atol=1e-6)
+    for key, lr in (("g", 1e-4), ("d", 1e-3)):
+        for k, v in a[key].items():
+            err = (v - b[key][k]).abs().max().item()
+            # Adam sign flips on noise-level gradients bound the difference (2 lr / step)
+            assert err <= 4 * lr + 1e-5 * v.abs().max().item(), (key, k, err)
+
+
+def test_shard_covers_scenes():
+    from sgan.train_step import DataParallel
+    dp = DataParallel()
+    dp.world, dp.rank = 3, 0
+    spans = []
+    for r in range(3):
+        dp.rank = r
+        spans.append(dp.shard(8))
+    assert spans == [(0, 3), (3, 6), (6, 8)]
