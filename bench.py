@@ -85,8 +85,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="scenes per GPU")
     ap.add_argument("--peds", type=int, default=20)
-    ap.add_argument("--graph", default="gat", choices=["gat", "gcn"])
+    ap.add_argument("--graph-kind", dest="graph_kind", default="gat", choices=["gat", "gcn"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", type=int, default=1, help="capture the iteration in a HIP graph (1) or run eager (0)")
     ap.add_argument("--cpu-iters", type=int, default=2)
     args = ap.parse_args()
 
@@ -101,26 +102,37 @@ def main():
     from sgan import kernels as K
     from sgan.data.synthetic import synthetic_batch
     from sgan.scene import SceneIndex
-    from sgan.train_step import DataParallel, GanTrainer
+    from sgan.train_step import DataParallel, GanTrainer, GraphedTrainer
 
-    g, d = build_models(0, args.graph)
+    g, d = build_models(0, args.graph_kind)
     g, d = g.to(dev), d.to(dev)
-    trainer = GanTrainer(g, d, dp=DataParallel())
+    trainer = GanTrainer(g, d, dp=DataParallel(), capturable=bool(args.graph))
     batch = synthetic_batch([args.peds] * args.batch, seed=1000 + rank, device=dev)
     sc = SceneIndex.from_seq_start_end(batch[-1], dev)
     S_glob, B_glob = sc.S * world, sc.B * world
     kw = dict(S_global=S_glob, B_global=B_glob, shard=(rank * sc.S, (rank + 1) * sc.S))
 
+    graphed = False
+    if args.graph:
+        try:
+            gt = GraphedTrainer(trainer, batch, sc, warmup=2, **kw)
+            step = gt.step
+            graphed = True
+        except Exception as e:  # capture unsupported (e.g. a collective): eager
+            print("bench: graph capture failed (%s: %s); running eager" % (type(e).__name__, e), file=sys.stderr)
+            torch.cuda.synchronize()
+    if not graphed:
+        step = lambda: trainer.step(batch, sc, **kw)
+
     for _ in range(args.warmup):
-        trainer.step(batch, sc, **kw)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    K.pool_timer.start()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.step(batch, sc, **kw)
+        step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -130,6 +142,13 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    # roofline of the pooling kernel: HIP events around every sgg_pool_fwd
+    # launch of instrumented iterations on the same inputs (the graph replays
+    # carry no events); rocprofv3's kernel trace of the same command is the
+    # cross-check (profiles/)
+    K.pool_timer.start()
+    for _ in range(max(1, min(args.steps, 3))):
+        trainer.step(batch, sc, **kw)
     launches = K.pool_timer.stop()
 
     if rank == 0:
@@ -161,7 +180,7 @@ def main():
             "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam) of the GAT generator "
                                    "(scripts/train.py defaults)", "scenes_per_gpu": args.batch,
                        "global_batch": args.batch * world, "peds_per_scene": args.peds, "obs_len": 8, "pred_len": 12,
-                       "graph": args.graph, "parallelism": "dp%d" % world},
+                       "generator": args.graph_kind, "hip_graph": graphed, "parallelism": "dp%d" % world},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -33,10 +33,12 @@ __global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
     const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
     float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out) {
+  const bool save_states = act_all != nullptr;  // inference: only the final state is stored
   constexpr int G4 = 4 * H;
   __shared__ float hbuf[kLstmPeds][H];
   __shared__ float gbuf[kLstmPeds][G4];
   __shared__ float relb[kLstmPeds][2];
+  __shared__ float redb[kLstmPeds][2][H];
   const int pl = threadIdx.x / G4, r = threadIdx.x - pl * G4;
   const int ped = blockIdx.x * kLstmPeds + pl;
   const bool valid = ped < B;
@@ -45,12 +47,14 @@ __global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(
   for (int k = 0; k < H; ++k) w[k] = Whh[r * H + k];
   const float a0 = A[2 * r], a1 = A[2 * r + 1], bb = bias[r];
   const bool is_g = r >= 2 * H && r < 3 * H;
+  const float wp0 = (decoder && r < H) ? Wp[r] : 0.f, wp1 = (decoder && r < H) ? Wp[H + r] : 0.f;
+  const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
   float c = 0.f;
   if (r < H) {
     const float hv = (valid && h0) ? h0[(size_t)ped * H + r] : 0.f;
     c = (valid && c0) ? c0[(size_t)ped * H + r] : 0.f;
     hbuf[pl][r] = hv;
-    if (valid) {
+    if (valid && save_states) {
       h_all[(size_t)ped * H + r] = hv;
       c_all[(size_t)ped * H + r] = c;
     }
@@ -84,18 +88,23 @@ __global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(
       c = fmaf(fg, c, ig * gg);
       const float h = og * tanhf(c);
       hbuf[pl][r] = h;
-      if (valid) {
-        const size_t o = ((size_t)(t + 1) * B + ped) * H + r;
+      if (decoder) {
+        redb[pl][0][r] = wp0 * h;
+        redb[pl][1][r] = wp1 * h;
+      }
+      if (valid && (save_states || t == T - 1)) {
+        const size_t o = ((size_t)(save_states ? t + 1 : T) * B + ped) * H + r;
         h_all[o] = h;
         c_all[o] = c;
       }
     }
     __syncthreads();
     if (decoder) {
-      if (r < 2) {
-        float s = bp[r];
+      if (r < 2) {  // rel_t = Wp h_t + bp  (H-term sum from LDS, same order for every ped)
+        float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < H; ++k) s = fmaf(Wp[r * H + k], hbuf[pl][k], s);
+        for (int k = 0; k < H; ++k) s += redb[pl][r][k];
+        s += r ? bp1 : bp0;
         relb[pl][r] = s;
         if (valid) rel_out[((size_t)t * B + ped) * 2 + r] = s;
       }
@@ -114,6 +123,7 @@ __global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
   __shared__ float dgb[kLstmPeds][G4];
   __shared__ float pb[kLstmPeds][4][H];
   __shared__ float drelb[kLstmPeds][2];
+  __shared__ float fbp[kLstmPeds][2][G4 / 64 > 0 ? G4 / 64 : 1];
   const int pl = threadIdx.x / G4, q = threadIdx.x - pl * G4;
   const int g = q / H, k = q - g * H;
   const int ped = blockIdx.x * kLstmPeds + pl;
@@ -121,8 +131,9 @@ __global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
   float wcol[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) wcol[j] = Whh[(g * H + j) * H + k];
-  float a_d = 0.f;  // A[:, d] column is read from global in the q < 2 threads
-  (void)a_d;
+  const float aq0 = A[2 * q], aq1 = A[2 * q + 1];   // row q of A (gate q of this thread)
+  const int lane = threadIdx.x & 63;
+  const int wq = q >> 6;                             // wave index within the ped (G4 is a multiple of 64)
   float dh = 0.f, dc = 0.f, fb = 0.f;
   const float wp0 = decoder ? Wp[q < H ? q : 0] : 0.f;
   const float wp1 = decoder ? Wp[H + (q < H ? q : 0)] : 0.f;
@@ -172,14 +183,23 @@ __global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < H; ++j) p = fmaf(wcol[j], dgb[pl][g * H + j], p);
     pb[pl][g][k] = p;
-    if (q < 2) {
-      float s = 0.f;
-      for (int rr = 0; rr < G4; ++rr) s = fmaf(A[2 * rr + q], dgb[pl][rr], s);
-      fb = s;
-      if (valid) drel_in[((size_t)t * B + ped) * 2 + q] = s;
+    {  // drel_t = A^T dG_t: one product per gate thread, wave shuffle + LDS combine
+      const float dgq = dgb[pl][q];
+      const float r0 = wave_sum(aq0 * dgq), r1 = wave_sum(aq1 * dgq);
+      if (lane == 0) {
+        fbp[pl][0][wq] = r0;
+        fbp[pl][1][wq] = r1;
+      }
     }
     __syncthreads();
     if (q < H) dh = pb[pl][0][q] + pb[pl][1][q] + pb[pl][2][q] + pb[pl][3][q];
+    if (q < 2) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < G4 / 64; ++w) s += fbp[pl][q][w];
+      fb = s;
+      if (valid) drel_in[((size_t)t * B + ped) * 2 + q] = s;
+    }
     __syncthreads();
   }
   if (q < H && valid && dh0) dh0[(size_t)ped * H + q] = dh;

@@ -1,0 +1,142 @@
+// Parameter-gradient reductions  C = X^T Y  (X: R x M, Y: R x N, R >> M, N),
+// plus optional column sums of Y (bias gradients), on fp32 MFMA with split-K.
+//
+// Every weight gradient of the path is such a reduction over all nodes /
+// (time, ped) pairs: dW = X^T dY of a node transform, dW_hh = dG^T h_{t-1}
+// summed over T x B, dW1h = dU^T h of the pooling, da = Wh^T [ds dt] of the
+// attention.  R is 10^3..10^5 and M, N <= 512: a library GEMM sees a skinny
+// problem with a huge K and launches a handful of workgroups.  Here the rows
+// are split over enough workgroups to fill the chip; each writes its partial
+// 64 x 64 tile to a slab, and a second pass sums the slabs in split order
+// (deterministic).  v_mfma_f32_16x16x4_f32: A[m][k] = X[r0 + k][m] (lanes run
+// along m: coalesced), B[k][n] = Y[r0 + k][n].
+#include "sgg_common.h"
+
+namespace sgg {
+
+__global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restrict__ X, int ldx,
+                                                          const float* __restrict__ Y, int ldy, int R, int M,
+                                                          int N, int rows_per_split, float* __restrict__ slab,
+                                                          float* __restrict__ colslab) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, kq = lane >> 4;
+  const int m0 = blockIdx.x * 64 + wave * 16;
+  const int n0 = blockIdx.y * 64;
+  const int split = blockIdx.z;
+  const int r0 = split * rows_per_split;
+  const int r1 = min(R, r0 + rows_per_split);
+  const int m = m0 + c16;
+  const bool mok = m < M;
+  bool nok[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) nok[t] = n0 + 16 * t + c16 < N;
+  const bool do_col = colslab && blockIdx.x == 0 && wave == 0;
+  floatx4 acc[4];
+  float col[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // software pipeline: the next 16 rows' loads are in flight while the current
+  // 16 rows run through the MFMAs
+  float a[4], b[4][4], an[4], bnx[4][4];
+  auto load16 = [&](int r, float (&aa)[4], float (&bb)[4][4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int row = r + 4 * s + kq;
+      const bool rok = row < r1;
+      aa[s] = (rok && mok) ? X[(size_t)row * ldx + m] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bb[s][t] = (rok && nok[t]) ? Y[(size_t)row * ldy + n0 + 16 * t + c16] : 0.f;
+    }
+  };
+  if (r0 < r1) load16(r0, a, b);
+  for (int r = r0; r < r1; r += 16) {
+    const bool more = r + 16 < r1;
+    if (more) load16(r + 16, an, bnx);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
+        if (do_col) col[t] += b[s][t];
+      }
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        a[s] = an[s];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b[s][t] = bnx[s][t];
+      }
+    }
+  }
+  float* out = slab + (size_t)split * M * N;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n = n0 + 16 * t + c16;
+    if (n >= N) continue;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int mm = m0 + kq * 4 + rr;
+      if (mm < M) out[(size_t)mm * N + n] = acc[t][rr];
+    }
+  }
+  if (do_col) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {  // sum the 4 row phases (lanes c16, c16+16, +32, +48)
+      float v = col[t];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int n = n0 + 16 * t + c16;
+      if (kq == 0 && n < N) colslab[(size_t)split * N + n] = v;
+    }
+  }
+}
+
+// slab sum: block = 64 outputs x 4 split phases; fixed order -> deterministic
+__global__ void __launch_bounds__(256) xtw_reduce_kernel(const float* __restrict__ slab, int splits, int MN,
+                                                         float* __restrict__ C, int N, int ldc) {
+  __shared__ float part[4][64];
+  const int el = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
+  float s = 0.f;
+  if (e < MN)
+    for (int k = ph; k < splits; k += 4) s += slab[(size_t)k * MN + e];
+  part[ph][el] = s;
+  __syncthreads();
+  if (ph == 0 && e < MN) {
+    const float v = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
+    const int mm = e / N, n = e - mm * N;
+    C[(size_t)mm * ldc + n] = v;
+  }
+}
+
+}  // namespace sgg
+
+using namespace sgg;
+
+extern "C" int sgg_xtw_splits(int R, int M, int N) {
+  const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  int splits = (1024 + tiles - 1) / tiles;
+  const int max_by_rows = (R + 127) / 128;  // >= 128 rows per split
+  if (splits > max_by_rows) splits = max_by_rows;
+  return splits < 1 ? 1 : splits;
+}
+
+extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, int M, int N, float* C, int ldc,
+                       float* colsum, float* ws, size_t ws_bytes, void* stream) {
+  SGG_CHECK_ARG((R == 0 || (X && Y)) && C && ws, "sgg_xtw: null pointer");
+  SGG_CHECK_ARG(R >= 0 && M > 0 && N > 0 && ldx >= M && ldy >= N && ldc >= N, "sgg_xtw: bad sizes");
+  const int splits = sgg_xtw_splits(R, M, N);
+  const size_t need = sizeof(float) * (size_t)splits * ((size_t)M * N + N);
+  SGG_CHECK_ARG(ws_bytes >= need, "sgg_xtw: workspace %zu < %zu bytes", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  const int rps = ((R + splits - 1) / splits + 15) & ~15;
+  float* colslab = ws + (size_t)splits * M * N;
+  dim3 grid((M + 63) / 64, (N + 63) / 64, splits);
+  hipLaunchKernelGGL(xtw_partial_kernel, grid, dim3(256), 0, st, X, ldx, Y, ldy, R, M, N, rps, ws,
+                     colsum ? colslab : nullptr);
+  const int MN = M * N;
+  hipLaunchKernelGGL(xtw_reduce_kernel, dim3((MN + 63) / 64), dim3(256), 0, st, ws, splits, MN, C, N, ldc);
+  if (colsum)
+    hipLaunchKernelGGL(xtw_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, st, colslab, splits, N, colsum, N, N);
+  SGG_RETURN_LAUNCH("sgg_xtw");
+}

@@ -40,21 +40,38 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
 
   const bool full_n = col0 + 64 <= N;
   int k0 = 0;
-  // main loop: 4 MFMA k-steps (16 k) per iteration, no k bounds checks
-  for (; k0 + 16 <= K; k0 += 16) {
-    float a[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) a[s] = arow_ok ? xrow[k0 + 4 * s + kq] : 0.f;
+  // main loop: 4 MFMA k-steps (16 k) per iteration, no k bounds checks; the
+  // next 16 k of both operands are loaded while the current ones compute
+  auto load16 = [&](int kb, float (&aa)[4], float (&bb)[4][4]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int k = k0 + 4 * s + kq;
+      const int k = kb + 4 * s + kq;
+      aa[s] = arow_ok ? xrow[k] : 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int n = col0 + 16 * t + ar;
-        float b;
-        if (full_n) b = TRANS_W ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
-        else b = load_w<TRANS_W>(W, k, n, K, N);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b, acc[t], 0, 0, 0);
+        if (full_n) bb[s][t] = TRANS_W ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
+        else bb[s][t] = load_w<TRANS_W>(W, k, n, K, N);
+      }
+    }
+  };
+  if (K >= 16) {
+    float a[4], b[4][4], an[4], bn[4][4];
+    load16(0, a, b);
+    for (; k0 + 16 <= K; k0 += 16) {
+      const bool more = k0 + 32 <= K;
+      if (more) load16(k0 + 16, an, bn);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
+      if (more) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          a[s] = an[s];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) b[s][t] = bn[s][t];
+        }
       }
     }
   }

@@ -33,6 +33,8 @@ SIGNATURES = {
     "sgg_group_index": (_i, [_p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "sgg_seg_reduce": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i, _p]),
     "sgg_seg_gather": (_i, [_p, _i, _i, _p, _p, _p, _i, _p, _i, _p]),
+    "sgg_xtw_splits": (_i, [_i, _i, _i]),
+    "sgg_xtw": (_i, [_p, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _sz, _p]),
     "sgg_lstm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
 }

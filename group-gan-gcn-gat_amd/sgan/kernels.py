@@ -48,6 +48,27 @@ def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None):
     return y
 
 
+def xtw(X, Y, colsum=False):
+    """C = X^T Y (+ column sums of Y) with the split-K MFMA reduction
+    (sgg_xtw); X: R x M, Y: R x N, row-strided 2-D views allowed."""
+    lib = _lib()
+    X = _rows(X, "X")
+    Y = _rows(Y, "Y")
+    R, M = X.shape
+    Nn = Y.shape[1]
+    assert Y.shape[0] == R
+    if R == 0:
+        C = torch.zeros(M, Nn, device=X.device, dtype=torch.float32)
+        return (C, torch.zeros(Nn, device=X.device)) if colsum else C
+    splits = lib.sgg_xtw_splits(R, M, Nn)
+    ws = torch.empty(splits * (M * Nn + Nn), device=X.device, dtype=torch.float32)
+    C = torch.empty(M, Nn, device=X.device, dtype=torch.float32)
+    cs = torch.empty(Nn, device=X.device, dtype=torch.float32) if colsum else None
+    N.check(lib.sgg_xtw(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), R, M, Nn, N.ptr(C), Nn, N.ptr(cs), N.ptr(ws),
+                        ws.numel() * 4, N.stream_ptr()), "sgg_xtw")
+    return (C, cs) if colsum else C
+
+
 class _XW(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, trans_w, act):
@@ -65,10 +86,10 @@ class _XW(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = xw_raw(dy, w, None, not ctx.trans_w, 0)
-        if ctx.needs_input_grad[1]:
-            dw = dy.t().mm(x) if ctx.trans_w else x.t().mm(dy)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.sum(0)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            g, cs = xtw(x, dy, colsum=True)                 # (K x N) = X^T dY, colsum = sum dY
+            dw = g.t() if ctx.trans_w else g
+            db = cs if ctx.has_bias else None
         return dx, dw, db, None, None
 
 
@@ -161,8 +182,8 @@ class _Pool(torch.autograd.Function):
                                  N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(dW2p), N.ptr(dAp),
                                  N.stream_ptr()), "sgg_pool_bwd")
         dh = xw_raw(dU, W1h, None, trans_w=False) if ctx.needs_input_grad[0] else None
-        dW1h = dU.t().mm(h)
-        dc = dU.sum(0)
+        g, dc = xtw(h, dU, colsum=True)                     # (Hd x 512) = dW1h^T, dc = sum_j dU_j
+        dW1h = g.t()
         db2 = (dout * (out > 0)).sum(0)
         return dh, None, dW1h, dAp.sum(0), dc, dW2p.sum(0), db2, None
 
@@ -204,7 +225,7 @@ class _GatAttn(torch.autograd.Function):
         N.check(lib.sgg_gat_bwd(N.ptr(wh), N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, alpha, mode, epi,
                                 max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), F, N.ptr(dWh), N.ptr(ds), N.ptr(dt),
                                 N.stream_ptr()), "sgg_gat_bwd")
-        da = torch.cat([wh.t().mv(ds), wh.t().mv(dt)]).view(2 * F, 1)
+        da = xtw(wh, torch.stack([ds, dt], 1)).t().reshape(2 * F, 1)
         return dWh, da, None, None, None, None, None, None, None
 
 
@@ -348,10 +369,7 @@ class _LSTMSeq(torch.autograd.Function):
         drel_tot = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
         if decoder:
             dout = drel_out.contiguous() if drel_out is not None else torch.zeros(T, B, 2, device=dev)
-            dhl = None
-            # dL/dh_T from a consumer of the final state (unused by the generator)
-            if dh_last is not None and bool(dh_last.abs().sum() > 0):
-                raise NotImplementedError("gradient through the decoder's final hidden state")
+            dhl = None  # the decoder's final state feeds nothing in the generator (models.py:925)
         else:
             dout = None
             dhl = dh_last.contiguous() if dh_last is not None else None
@@ -359,18 +377,18 @@ class _LSTMSeq(torch.autograd.Function):
                                  T, B, H, int(decoder), N.ptr(dG), N.ptr(dh0), N.ptr(drel_in), N.ptr(drel_tot),
                                  N.stream_ptr()), "sgg_lstm_bwd")
         dGf = dG.view(T * B, 4 * H)
-        dWhh = dGf.t().mm(h_all[:T].reshape(T * B, H))
+        g, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True)      # (H x 4H), sum dG
+        dWhh = g.t()
         if decoder:
             rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0)
         else:
             rel_in = rel
-        dA = dGf.t().mm(rel_in.reshape(T * B, 2))
-        dbias = dGf.sum(0)
+        dA = xtw(rel_in.reshape(T * B, 2), dGf).t()
         dWp = dbp = None
         if decoder:
             dr = drel_tot.view(T * B, 2)
-            dWp = dr.t().mm(h_all[1:].reshape(T * B, H))
-            dbp = dr.sum(0)
+            g, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True)
+            dWp = g.t()
             drel = drel_in[0]
         else:
             drel = drel_in

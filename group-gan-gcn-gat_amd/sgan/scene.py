@@ -41,9 +41,13 @@ class SceneIndex:
 
     def repeat(self, k):
         """k back-to-back copies of the batch (sample-major): scene s of copy r
-        is scene r*S + s.  Used to batch the best-of-k samples."""
-        off = np.concatenate([[0]] + [self.host_off[1:] + r * self.B for r in range(k)])
-        return SceneIndex(off, self.device)
+        is scene r*S + s.  Used to batch the best-of-k samples.  Memoised, so
+        a captured graph never re-uploads the index."""
+        reps = self.__dict__.setdefault("_reps", {})
+        if k not in reps:
+            off = np.concatenate([[0]] + [self.host_off[1:] + r * self.B for r in range(k)])
+            reps[k] = SceneIndex(off, self.device)
+        return reps[k]
 
     def ped_scene_long(self):
         """Scene of every ped as an int64 device tensor (noise broadcast)."""

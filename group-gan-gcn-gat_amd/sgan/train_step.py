@@ -97,14 +97,23 @@ class DataParallel:
             o += n
 
 
+class StepInputs:
+    """Host-RNG draws of one iteration, in the reference's order, staged in
+    device tensors: noise of the D-step's G call, the best_k noises of the
+    G-step, and the three label-smoothing numbers (D real, D fake, G)."""
+
+    def __init__(self, z_d, z_g, y):
+        self.z_d, self.z_g, self.y = z_d, z_g, y
+
+
 class GanTrainer:
-    def __init__(self, G, D, args=None, dp=None, selective_backward=True):
+    def __init__(self, G, D, args=None, dp=None, selective_backward=True, capturable=False):
         self.G, self.D = G, D
         self.args = args or TrainArgs()
         self.dp = dp or DataParallel()
         self.selective_backward = selective_backward
-        self.opt_g = torch.optim.Adam(G.parameters(), lr=self.args.g_learning_rate)
-        self.opt_d = torch.optim.Adam(D.parameters(), lr=self.args.d_learning_rate)
+        self.opt_g = torch.optim.Adam(G.parameters(), lr=self.args.g_learning_rate, capturable=capturable)
+        self.opt_d = torch.optim.Adam(D.parameters(), lr=self.args.d_learning_rate, capturable=capturable)
         skip = "gcn_module." if getattr(G, "graph", "gat") == "gat" else "gatencoder."
         self.g_params = [p for n, p in G.named_parameters() if not n.startswith(skip)]
         self.d_params = list(D.parameters())
@@ -130,15 +139,16 @@ class GanTrainer:
         return vals
 
     # -- steps ---------------------------------------------------------------
-    def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None)):
+    def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """discriminator_step (train.py:395-429). `batch` holds this rank's
-        scenes (device tensors), `sc` their SceneIndex."""
+        scenes (device tensors), `sc` their SceneIndex.  `inputs` (StepInputs)
+        replaces the host RNG draws by pre-drawn device tensors (graph mode)."""
         a = self.args
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, _lm, sse) = batch
         S_global = S_global or sc.S
         B_global = B_global or sc.B
         s0 = shard[0]
-        z = self._noise(S_global, s0, s0 + sc.S)
+        z = inputs.z_d if inputs is not None else self._noise(S_global, s0, s0 + sc.S)
         with torch.no_grad():
             fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
         fake = relative_to_abs(fake_rel, obs[-1])
@@ -147,8 +157,11 @@ class GanTrainer:
         sc2 = sc.repeat(2)
         scores = self.D(traj, traj_rel, _sse_of(sc2), scenes=sc2)
         s_fake, s_real = scores[:sc.B], scores[sc.B:]
-        y_real = random.uniform(0.7, 1.2)
-        y_fake = random.uniform(0, 0.3)
+        if inputs is not None:
+            y_real, y_fake = inputs.y[0], inputs.y[1]
+        else:
+            y_real = random.uniform(0.7, 1.2)
+            y_fake = random.uniform(0, 0.3)
         w = sc.B / B_global
         loss = w * (bce_loss(s_real, torch.ones_like(s_real) * y_real) +
                     bce_loss(s_fake, torch.zeros_like(s_fake) * y_fake))
@@ -157,7 +170,7 @@ class GanTrainer:
         vals = self._finish(self.d_params, self.opt_d, [loss], a.clipping_threshold_d)
         return {"D_data_loss": vals[0], "D_total_loss": vals[0]}
 
-    def g_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None)):
+    def g_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """generator_step (train.py:432-484)."""
         a = self.args
         G, D = self.G, self.D
@@ -167,7 +180,10 @@ class GanTrainer:
         s0 = shard[0]
         S, B, k = sc.S, sc.B, a.best_k
         mask = loss_mask[:, a.obs_len:]                                   # (B, pred_len)
-        zs = [self._noise(S_global, s0, s0 + S) for _ in range(k)]        # k draws, reference order
+        if inputs is not None:
+            zs = [inputs.z_g[i] for i in range(k)] if inputs.z_g is not None else [None] * k
+        else:
+            zs = [self._noise(S_global, s0, s0 + S) for _ in range(k)]    # k draws, reference order
         seg = sc.ped_scene_long()
         mask_sum = torch.zeros(S, device=obs.device).index_add_(0, seg, mask.sum(1))
 
@@ -214,7 +230,7 @@ class GanTrainer:
             terms.append(g_l2)
         fake_last = relative_to_abs(fake_rel_last, obs[-1])
         scores = D(torch.cat([obs, fake_last], 0), torch.cat([obs_rel, fake_rel_last], 0), sse, scenes=sc)
-        y = random.uniform(0.7, 1.2)
+        y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)
         adv = (sc.B / B_global) * bce_loss(scores, torch.ones_like(scores) * y)
         loss = adv + (terms[0] if terms else 0.0)
         self.opt_g.zero_grad(set_to_none=True)
@@ -231,6 +247,87 @@ class GanTrainer:
         ld = self.d_step(batch, sc, **kw)
         lg = self.g_step(batch, sc, **kw)
         return ld, lg
+
+    def draw_inputs(self, S_global, s0, s1):
+        """The host draws one iteration makes, in the reference's order (torch
+        RNG: D-step noise, then best_k G-step noises; Python random: D real,
+        D fake, G label smoothing)."""
+        z_d = self._noise(S_global, s0, s1)
+        yr, yf = random.uniform(0.7, 1.2), random.uniform(0, 0.3)
+        z_g = [self._noise(S_global, s0, s1) for _ in range(self.args.best_k)]
+        yg = random.uniform(0.7, 1.2)
+        zg = torch.stack(z_g, 0) if z_g[0] is not None else None
+        return z_d, zg, torch.tensor([yr, yf, yg], dtype=torch.float32)
+
+
+class GraphedTrainer:
+    """One full iteration (D-step + G-step, both Adam updates and the DP
+    all-reduces) captured once into a HIP graph and replayed.
+
+    The batch lives in static device tensors (copy new data into
+    `self.batch` between replays for real training); each replay first draws
+    the host RNG numbers exactly as the eager step would (StepInputs) into
+    pinned buffers and copies them to the device inputs of the graph.  The
+    trainer must be built with capturable=True (Adam keeps its step on the
+    device)."""
+
+    def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2):
+        self.t = trainer
+        self.batch, self.sc = batch, sc
+        self.kw = dict(S_global=S_global or sc.S, B_global=B_global or sc.B, shard=shard)
+        dev = batch[0].device
+        s0 = shard[0]
+        self.span = (self.kw["S_global"], s0, s0 + sc.S)
+        G = trainer.G
+        nd = tuple(G.noise_dim) if G.noise_dim else None
+        k = trainer.args.best_k
+        # two pinned staging sets, alternated, each guarded by an event so the
+        # host never overwrites a buffer whose H2D copy is still pending
+        mk = lambda shape: torch.empty(shape, dtype=torch.float32).pin_memory() if nd else None
+        self.stage = [(mk((sc.S,) + (nd or ())), mk((k, sc.S) + (nd or ())), torch.empty(3).pin_memory())
+                      for _ in range(2)]
+        self.stage_ev = [None, None]
+        self.cur = 0
+        dv = lambda shape: torch.zeros(shape, device=dev) if nd else None
+        self.inp = StepInputs(dv((sc.S,) + (nd or ())), dv((k, sc.S) + (nd or ())), torch.zeros(3, device=dev))
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._load(*trainer.draw_inputs(*self.span))
+                trainer.step(batch, sc, inputs=self.inp, **self.kw)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        trainer.opt_g.zero_grad(set_to_none=True)
+        trainer.opt_d.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.losses = trainer.step(batch, sc, inputs=self.inp, **self.kw)
+
+    def _load(self, z_d, z_g, y):
+        i = self.cur
+        self.cur ^= 1
+        if self.stage_ev[i] is not None:
+            self.stage_ev[i].synchronize()        # that set's previous copies are done
+        h_zd, h_zg, h_y = self.stage[i]
+        if z_d is not None:
+            h_zd.copy_(z_d)
+            self.inp.z_d.copy_(h_zd, non_blocking=True)
+        if z_g is not None:
+            h_zg.copy_(z_g)
+            self.inp.z_g.copy_(h_zg, non_blocking=True)
+        h_y.copy_(y)
+        self.inp.y.copy_(h_y, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.stage_ev[i] = ev
+
+    def step(self):
+        """Draw this iteration's host RNG numbers, replay the graph; returns the
+        (device) loss dicts of the captured step."""
+        self._load(*self.t.draw_inputs(*self.span))
+        self.graph.replay()
+        return self.losses
 
 
 def shard_batch(batch, sc, s0, s1):

@@ -160,6 +160,18 @@ int sgg_seg_gather(const float* src, int lds, int F, const int32_t* seg_of_row,
                    void* stream);
 
 /* ------------------------------------------------------------------------
+ * Parameter-gradient reduction C = X^T Y over R rows (X: R x M, Y: R x N,
+ * row strides ldx / ldy; C: M x N, row stride ldc), and optionally colsum =
+ * sum_r Y[r, :] (bias gradient).  Split-K over sgg_xtw_splits(R, M, N)
+ * workgroup slabs summed in a fixed order (deterministic); ws must hold
+ * splits * (M*N + N) floats.  Replaces the library GEMMs of every weight
+ * gradient (dW = X^T dY of the node transforms, W_hh / W_ih / hidden2pos of the
+ * LSTMs summed over T x B, W1h of the pooling, `a` of the attention). */
+int sgg_xtw_splits(int R, int M, int N);
+int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, int M, int N, float* C,
+            int ldc, float* colsum, float* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * Fused LSTM sequence (Encoder.forward models.py:62-92; Decoder.forward
  * :142-178 with pool_every_timestep = 0), one launch for all T steps:
  *   gates_t = A r_t + W_hh h_{t-1} + bias   (A = W_ih We, bias = W_ih be + b_ih + b_hh:
@@ -170,7 +182,8 @@ int sgg_seg_gather(const float* src, int lds, int F, const int32_t* seg_of_row,
  *   t >= 1; rel_out[t] = Wp h_t + bp (T x B x 2) is the predicted displacement.
  * H in {16, 32, 48, 64}.  Outputs h_all, c_all: (T+1) x B x H with index 0 the
  * initial state; act_all (T x B x 4H, gate activations i|f|g|o) may be NULL
- * (inference) and is required by the backward. */
+ * (inference: then only h_all[T], c_all[T] are written) and is required by the
+ * backward. */
 int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float* bias,
                  const float* h0, const float* c0, const float* Wp, const float* bp, int T, int B, int H,
                  int decoder, float* h_all, float* c_all, float* act_all, float* rel_out,

@@ -270,3 +270,48 @@ def test_fused_lstm_vs_oracle(H, T, decoder):
         close(reld.grad, rel.grad.numpy(), rtol=1e-4, what="encoder drel")
     for (k, p), (_, q) in zip(ref.named_parameters(), mod.named_parameters()):
         close(q.grad, p.grad.numpy(), rtol=1e-4, floor=1e-6, what="lstm d" + k)
+
+
+def test_xtw_matches_torch():
+    from sgan import kernels as K
+    torch.manual_seed(1)
+    for (R, M, Nn) in [(0, 3, 4), (5, 3, 7), (1000, 32, 128), (51200, 48, 192), (25600, 32, 512), (300, 144, 2)]:
+        X = torch.randn(R, M, device=DEV)
+        Y = torch.randn(R, Nn, device=DEV)
+        C, cs = K.xtw(X, Y, colsum=True)
+        ref = (X.double().t() @ Y.double()).float()
+        close(C, ref.cpu(), rtol=5e-6, floor=1.0, what="xtw %s" % ((R, M, Nn),))
+        close(cs, Y.double().sum(0).float().cpu(), rtol=5e-6, floor=1.0, what="colsum")
+
+
+def test_graphed_trainer_equals_eager():
+    """The HIP-graph replay of a training iteration (GraphedTrainer) consumes
+    the host RNGs in the same order and produces the same updates as the eager
+    GanTrainer."""
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, GraphedTrainer
+    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
+    res = []
+    for graphed in (False, True):
+        g, d = build_models()
+        tr = GanTrainer(g, d, capturable=True)
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        torch.manual_seed(9)
+        random.seed(9)
+        if graphed:
+            gt = GraphedTrainer(tr, batch, sc, warmup=2)
+            for _ in range(2):
+                ld, lg = gt.step()
+        else:
+            for _ in range(4):
+                ld, lg = tr.step(batch, sc)
+        torch.cuda.synchronize()
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())},
+                    {k: v.detach().cpu().clone() for k, v in list(g.state_dict().items()) + list(d.state_dict().items())}))
+    (la, wa), (lb, wb) = res
+    for k in la:
+        assert abs(la[k] - lb[k]) <= 1e-5 * max(1.0, abs(la[k])), (k, la[k], lb[k])
+    for k in wa:
+        err = (wa[k] - wb[k]).abs().max().item()
+        assert err <= 1e-5 + 1e-5 * wa[k].abs().max().item(), (k, err)
