@@ -9,6 +9,13 @@
 // graph); Wh is LDS-resident with an odd row stride (F | 1) so column walks
 // across rows are bank-conflict free; one wave per attention row with lanes
 // over j: row max / row sum are wave shuffles (__shfl_xor over 64 lanes).
+//
+// Multi-head (the batched GAT of the sgangat family, sgan/GAT.py:6-55 text):
+// Wh holds all heads side by side (n x heads*F, the output of one X @ [w_0 |
+// .. | w_{H-1}] transform), `a` is heads x [a_src | a_dst], and the workgroup
+// grid runs over (segment, head) pairs; head h writes columns [hF, hF + F) of
+// y, so the concatenation of heads (GAT.py:86) is free.  `bias` (F, shared by
+// the heads, GAT.py:41) is added to the aggregate before the epilogue.
 #include "sgg_common.h"
 
 namespace sgg {
@@ -46,9 +53,9 @@ __device__ __forceinline__ void gat_row(int i, int n, int mode, const float* lab
 }
 
 __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
-    const float* __restrict__ Wh, const float* __restrict__ a, const float* __restrict__ labels,
-    const int32_t* __restrict__ seg_off, int nseg, int F, float alpha, int mode, int epi, int max_seg,
-    float* __restrict__ hp, float* __restrict__ y, int ldy) {
+    const float* __restrict__ Wh, int heads, const float* __restrict__ a_all, const float* __restrict__ bias,
+    const float* __restrict__ labels, const int32_t* __restrict__ seg_off, int nseg, int F, float alpha, int mode,
+    int epi, int max_seg, float* __restrict__ hp, float* __restrict__ y, int ldy) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int Fp = F | 1;
   float* Ws = reinterpret_cast<float*>(smem);       // max_seg x Fp
@@ -57,12 +64,16 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
   float* lab = ts + max_seg;                        // max_seg
   float* att = lab + max_seg;                       // kGatWaves x max_seg
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int g = blockIdx.x; g < nseg; g += gridDim.x) {
+  const int HF = heads * F;
+  for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
+    const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
     const int n = seg_off[g + 1] - o;
+    const float* a = a_all + 2 * F * hd;
+    const int c0 = hd * F;
     for (int q = threadIdx.x; q < n * F; q += blockDim.x) {
       const int r = q / F, f = q - r * F;
-      Ws[r * Fp + f] = Wh[(size_t)o * F + q];
+      Ws[r * Fp + f] = Wh[(size_t)(o + r) * HF + c0 + f];
     }
     __syncthreads();
     for (int r = threadIdx.x; r < n; r += blockDim.x) {
@@ -94,6 +105,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
         float acc = 0.f;
         if (f < F) {
           for (int j = 0; j < n; ++j) acc = fmaf(arow[j], Ws[j * Fp + f], acc);
+          if (bias) acc += bias[f];
         }
         hv[c] = acc;
         zv[c] = epi ? elu(acc) : acc;
@@ -113,8 +125,8 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
       for (int c = 0; c < 2; ++c) {
         const int f = lane + 64 * c;
         if (f < F) {
-          if (epi) hp[(size_t)(o + i) * F + f] = hv[c];
-          y[(size_t)(o + i) * ldy + f] = epi == 2 ? zv[c] - lse : zv[c];
+          if (epi) hp[(size_t)(o + i) * HF + c0 + f] = hv[c];
+          y[(size_t)(o + i) * ldy + c0 + f] = epi == 2 ? zv[c] - lse : zv[c];
         }
       }
     }
@@ -123,7 +135,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
 }
 
 __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
-    const float* __restrict__ Wh, const float* __restrict__ a, const float* __restrict__ labels,
+    const float* __restrict__ Wh, int heads, const float* __restrict__ a_all, const float* __restrict__ labels,
     const int32_t* __restrict__ seg_off, int nseg, int F, float alpha, int mode, int epi, int max_seg,
     const float* __restrict__ hp, const float* __restrict__ y, const float* __restrict__ dy, int lddy,
     float* __restrict__ dWh, float* __restrict__ ds_out, float* __restrict__ dt_out) {
@@ -139,12 +151,16 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
   float* dss = lab + max_seg;
   float* dts = dss + max_seg;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int g = blockIdx.x; g < nseg; g += gridDim.x) {
+  const int HF = heads * F;
+  for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
+    const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
     const int n = seg_off[g + 1] - o;
+    const float* a = a_all + 2 * F * hd;
+    const int c0 = hd * F;
     for (int q = threadIdx.x; q < n * F; q += blockDim.x) {
       const int r = q / F, f = q - r * F;
-      Ws[r * Fp + f] = Wh[(size_t)o * F + q];
+      Ws[r * Fp + f] = Wh[(size_t)(o + r) * HF + c0 + f];
     }
     __syncthreads();
     for (int r = threadIdx.x; r < n; r += blockDim.x) {
@@ -167,8 +183,8 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
         const int f = lane + 64 * c;
         d[c] = 0.f; h[c] = 0.f; sm[c] = 0.f;
         if (f < F) {
-          d[c] = dy[(size_t)(o + i) * lddy + f];
-          if (epi) h[c] = hp[(size_t)(o + i) * F + f];
+          d[c] = dy[(size_t)(o + i) * lddy + c0 + f];
+          if (epi) h[c] = hp[(size_t)(o + i) * HF + c0 + f];
           if (epi == 2) sm[c] = expf(y[(size_t)(o + i) * F + f]);
           sdy += d[c];
         }
@@ -193,7 +209,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
       const int j = q / F, f = q - j * F;
       float acc = 0.f;
       for (int i = 0; i < n; ++i) acc = fmaf(At[i * Np + j], Ds[i * Fp + f], acc);
-      dWh[(size_t)o * F + q] = acc;
+      dWh[(size_t)(o + j) * HF + c0 + f] = acc;
     }
     __syncthreads();
     // per row: datt_ij = dhp_i . Wh_j ; softmax + LeakyReLU backward -> dz (in place of att)
@@ -234,13 +250,13 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
       float acc = 0.f;
       for (int i = 0; i < n; ++i) acc += At[i * Np + j];
       dts[j] = acc;
-      ds_out[o + j] = dss[j];
-      dt_out[o + j] = acc;
+      ds_out[(size_t)(o + j) * heads + hd] = dss[j];
+      dt_out[(size_t)(o + j) * heads + hd] = acc;
     }
     __syncthreads();
     for (int q = threadIdx.x; q < n * F; q += blockDim.x) {
       const int j = q / F, f = q - j * F;
-      dWh[(size_t)o * F + q] += dss[j] * a[f] + dts[j] * a[F + f];
+      dWh[(size_t)(o + j) * HF + c0 + f] += dss[j] * a[f] + dts[j] * a[F + f];
     }
     __syncthreads();
   }
@@ -257,49 +273,56 @@ static size_t gat_bwd_lds(int F, int max_seg) {
 
 using namespace sgg;
 
-static int gat_args_ok(const char* who, const float* Wh, const float* a, const float* labels, const int32_t* off,
-                       int nseg, int n, int F, int mode, int epi, int max_seg) {
+static int gat_args_ok(const char* who, const float* Wh, int heads, const float* a, const float* labels,
+                       const int32_t* off, int nseg, int n, int F, int mode, int epi, int max_seg) {
   SGG_CHECK_ARG(Wh && a && off, "%s: null pointer", who);
   SGG_CHECK_ARG(mode == 1 || labels, "%s: mask_mode 0 needs labels", who);
   SGG_CHECK_ARG(nseg >= 0 && n >= 0, "%s: bad sizes", who);
   SGG_CHECK_ARG(F >= 1 && F <= 128, "%s: F=%d outside [1, 128]", who, F);
+  SGG_CHECK_ARG(heads >= 1 && heads <= 64, "%s: heads=%d outside [1, 64]", who, heads);
   SGG_CHECK_ARG(mode == 0 || mode == 1, "%s: bad mask_mode", who);
   SGG_CHECK_ARG(epi >= 0 && epi <= 2, "%s: bad epilogue", who);
+  SGG_CHECK_ARG(epi != 2 || heads == 1, "%s: the log_softmax epilogue is single-head", who);
   SGG_CHECK_ARG(max_seg >= 1 && max_seg <= SGG_GAT_MAX_NODES, "%s: max segment %d outside [1, %d]", who, max_seg,
                 SGG_GAT_MAX_NODES);
   return 0;
 }
 
-extern "C" int sgg_gat_fwd(const float* Wh, const float* a, const float* labels, const int32_t* seg_off, int nseg,
-                           int n, int F, float alpha, int mask_mode, int epilogue, int max_seg, float* hp, float* y,
-                           int ldy, void* stream) {
-  int rc = gat_args_ok("sgg_gat_fwd", Wh, a, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
+static int gat_grid(int nseg, int heads) {
+  const long long w = (long long)nseg * heads;
+  return w < 16384 ? (int)w : 16384;
+}
+
+extern "C" int sgg_gat_fwd(const float* Wh, int heads, const float* a, const float* bias, const float* labels,
+                           const int32_t* seg_off, int nseg, int n, int F, float alpha, int mask_mode, int epilogue,
+                           int max_seg, float* hp, float* y, int ldy, void* stream) {
+  int rc = gat_args_ok("sgg_gat_fwd", Wh, heads, a, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
   if (rc) return rc;
   SGG_CHECK_ARG(y && (epilogue == 0 || hp), "sgg_gat_fwd: null output");
-  SGG_CHECK_ARG(ldy >= F, "sgg_gat_fwd: ldy < F");
+  SGG_CHECK_ARG(ldy >= heads * F, "sgg_gat_fwd: ldy < heads * F");
   SGG_CHECK_ARG(epilogue != 2 || ldy == F, "sgg_gat_fwd: log_softmax epilogue needs a dense y (ldy == F)");
   if (nseg == 0) return 0;
-  const int grid = nseg < 16384 ? nseg : 16384;
-  hipLaunchKernelGGL(gat_fwd_kernel, dim3(grid), dim3(kGatThreads), gat_fwd_lds(F, max_seg), (hipStream_t)stream,
-                     Wh, a, labels, seg_off, nseg, F, alpha, mask_mode, epilogue, max_seg, hp, y, ldy);
+  hipLaunchKernelGGL(gat_fwd_kernel, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), gat_fwd_lds(F, max_seg),
+                     (hipStream_t)stream, Wh, heads, a, bias, labels, seg_off, nseg, F, alpha, mask_mode, epilogue,
+                     max_seg, hp, y, ldy);
   SGG_RETURN_LAUNCH("sgg_gat_fwd");
 }
 
-extern "C" int sgg_gat_bwd(const float* Wh, const float* a, const float* labels, const int32_t* seg_off, int nseg,
-                           int n, int F, float alpha, int mask_mode, int epilogue, int max_seg, const float* hp,
-                           const float* y, const float* dy, int lddy, float* dWh, float* ds, float* dt,
-                           void* stream) {
-  int rc = gat_args_ok("sgg_gat_bwd", Wh, a, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
+extern "C" int sgg_gat_bwd(const float* Wh, int heads, const float* a, const float* labels, const int32_t* seg_off,
+                           int nseg, int n, int F, float alpha, int mask_mode, int epilogue, int max_seg,
+                           const float* hp, const float* y, const float* dy, int lddy, float* dWh, float* ds,
+                           float* dt, void* stream) {
+  int rc = gat_args_ok("sgg_gat_bwd", Wh, heads, a, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
   if (rc) return rc;
   SGG_CHECK_ARG(dy && dWh && ds && dt, "sgg_gat_bwd: null pointer");
   SGG_CHECK_ARG(epilogue == 0 || hp, "sgg_gat_bwd: epilogue needs hp");
   SGG_CHECK_ARG(epilogue != 2 || y, "sgg_gat_bwd: log_softmax epilogue needs y");
-  SGG_CHECK_ARG(lddy >= F, "sgg_gat_bwd: lddy < F");
+  SGG_CHECK_ARG(lddy >= heads * F, "sgg_gat_bwd: lddy < heads * F");
   if (nseg == 0) return 0;
   const size_t lds = gat_bwd_lds(F, max_seg);
   SGG_CHECK_ARG(lds <= 160 * 1024, "sgg_gat_bwd: segment %d x F %d needs %zu B of LDS", max_seg, F, lds);
-  const int grid = nseg < 16384 ? nseg : 16384;
-  hipLaunchKernelGGL(gat_bwd_kernel, dim3(grid), dim3(kGatThreads), lds, (hipStream_t)stream, Wh, a, labels, seg_off,
-                     nseg, F, alpha, mask_mode, epilogue, max_seg, hp, y, dy, lddy, dWh, ds, dt);
+  hipLaunchKernelGGL(gat_bwd_kernel, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), lds, (hipStream_t)stream, Wh,
+                     heads, a, labels, seg_off, nseg, F, alpha, mask_mode, epilogue, max_seg, hp, y, dy, lddy, dWh,
+                     ds, dt);
   SGG_RETURN_LAUNCH("sgg_gat_bwd");
 }

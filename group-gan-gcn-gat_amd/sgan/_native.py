@@ -27,8 +27,10 @@ SIGNATURES = {
     "sgg_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_pool_bwd_grid": (_i, [_i]),
     "sgg_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]),
-    "sgg_gat_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _i, _p]),
-    "sgg_gat_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _p, _i, _p, _p, _p, _p]),
+    "sgg_gat_fwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _i, _p]),
+    "sgg_gat_bwd": (_i, [_p, _i, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _p, _i, _p, _p, _p, _p]),
+    "sgg_seg_norm_fwd": (_i, [_p, _i, _i, _p, _i, _f, _p, _i, _p, _p]),
+    "sgg_seg_norm_bwd": (_i, [_p, _i, _p, _i, _i, _p, _i, _p, _p, _i, _p]),
     "sgg_group_index_ws": (_sz, [_i, _i]),
     "sgg_group_index": (_i, [_p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "sgg_seg_reduce": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i, _p]),
@@ -37,6 +39,8 @@ SIGNATURES = {
     "sgg_xtw": (_i, [_p, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _sz, _p]),
     "sgg_lstm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p]),
+    "sgg_bce_bwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p]),
 }
 
 _lib = None

@@ -199,16 +199,24 @@ def social_pool(h, pos, W1h, A, c, W2, b2, scenes):
 # ---------------------------------------------------------------------------
 class _GatAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, wh, a, labels, seg_off, nseg, max_seg, alpha, mode, epi):
+    def forward(ctx, wh, a, bias, labels, seg_off, nseg, max_seg, alpha, mode, epi, heads):
         lib = _lib()
         wh = _req(wh, "wh").contiguous()
-        n, F = wh.shape
+        n, HF = wh.shape
+        F = HF // heads
+        ctx.a_shape = a.shape
         a = a.contiguous().view(-1)
-        y = torch.zeros(n, F, device=wh.device, dtype=torch.float32)
-        hp = torch.zeros(n, F, device=wh.device, dtype=torch.float32) if epi else None
-        N.check(lib.sgg_gat_fwd(N.ptr(wh), N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, float(alpha), mode,
-                                epi, max_seg, N.ptr(hp), N.ptr(y), F, N.stream_ptr()), "sgg_gat_fwd")
-        ctx.meta = (labels, seg_off, nseg, max_seg, float(alpha), mode, epi)
+        if bias is not None:
+            bias = bias.contiguous()
+        # the complete-graph mode runs over zero-padded group buffers whose
+        # pad rows no segment covers: keep them zero for the reductions after
+        alloc = torch.zeros if mode == 1 else torch.empty
+        y = alloc(n, HF, device=wh.device, dtype=torch.float32)
+        hp = torch.empty(n, HF, device=wh.device, dtype=torch.float32) if epi else None
+        N.check(lib.sgg_gat_fwd(N.ptr(wh), heads, N.ptr(a), N.ptr(bias), N.ptr(labels), N.ptr(seg_off), nseg, n, F,
+                                float(alpha), mode, epi, max_seg, N.ptr(hp), N.ptr(y), HF, N.stream_ptr()),
+                "sgg_gat_fwd")
+        ctx.meta = (labels, seg_off, nseg, max_seg, float(alpha), mode, epi, heads, bias is not None)
         ctx.save_for_backward(wh, a, hp, y)
         return y
 
@@ -216,23 +224,71 @@ class _GatAttn(torch.autograd.Function):
     def backward(ctx, dy):
         lib = _lib()
         wh, a, hp, y = ctx.saved_tensors
-        labels, seg_off, nseg, max_seg, alpha, mode, epi = ctx.meta
-        n, F = wh.shape
+        labels, seg_off, nseg, max_seg, alpha, mode, epi, heads, has_bias = ctx.meta
+        n, HF = wh.shape
+        F = HF // heads
         dy = dy.contiguous()
-        dWh = torch.zeros(n, F, device=wh.device, dtype=torch.float32)
-        ds = torch.zeros(n, device=wh.device, dtype=torch.float32)
-        dt = torch.zeros(n, device=wh.device, dtype=torch.float32)
-        N.check(lib.sgg_gat_bwd(N.ptr(wh), N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, alpha, mode, epi,
-                                max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), F, N.ptr(dWh), N.ptr(ds), N.ptr(dt),
+        alloc = torch.zeros if mode == 1 else torch.empty
+        dWh = alloc(n, HF, device=wh.device, dtype=torch.float32)
+        ds = alloc(n, heads, device=wh.device, dtype=torch.float32)
+        dt = alloc(n, heads, device=wh.device, dtype=torch.float32)
+        N.check(lib.sgg_gat_bwd(N.ptr(wh), heads, N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, alpha, mode,
+                                epi, max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), HF, N.ptr(dWh), N.ptr(ds), N.ptr(dt),
                                 N.stream_ptr()), "sgg_gat_bwd")
-        da = xtw(wh, torch.stack([ds, dt], 1)).t().reshape(2 * F, 1)
-        return dWh, da, None, None, None, None, None, None, None
+        dsdt = torch.cat([ds, dt], 1)                                       # n x [ds_h | dt_h]
+        if heads == 1:
+            da = xtw(wh, dsdt).t().reshape(ctx.a_shape)
+        else:
+            C = xtw(wh, dsdt).view(heads, F, 2, heads)                     # [h, f, src|dst, h']
+            hh = torch.arange(heads, device=wh.device)
+            da = C[hh, :, :, hh].permute(0, 2, 1).reshape(heads, 2 * F)    # diagonal blocks h == h'
+        dbias = None
+        if has_bias:
+            dpre = dy if epi == 0 else dy * torch.where(hp > 0, torch.ones_like(hp), torch.exp(hp))
+            dbias = dpre.view(n, heads, F).sum((0, 1))
+        return dWh, da, dbias, None, None, None, None, None, None, None, None
 
 
-def gat_attention(wh, a, alpha, graph, epilogue):
+def gat_attention(wh, a, alpha, graph, epilogue, heads=1, bias=None):
     """Masked-softmax attention + aggregation + epilogue over `graph`
-    (a SegmentGraph).  epilogue: 0 none, 1 ELU, 2 log_softmax(ELU)."""
-    return _GatAttn.apply(wh, a, graph.labels, graph.seg_off, graph.nseg, graph.max_seg, alpha, graph.mode, epilogue)
+    (a SegmentGraph).  epilogue: 0 none, 1 ELU, 2 log_softmax(ELU).
+    Multi-head: wh is n x heads*F, a is heads x 2F, bias (F) shared by the
+    heads and added before the epilogue (sgangat GAT, GAT.py:6-55 text)."""
+    return _GatAttn.apply(wh, a, bias, graph.labels, graph.seg_off, graph.nseg, graph.max_seg, alpha, graph.mode,
+                          epilogue, heads)
+
+
+class _SegNorm(torch.autograd.Function):
+    """Per-segment instance normalisation (sgg_seg_norm_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, seg_off, nseg, eps):
+        lib = _lib()
+        x = _rows(x, "x")
+        n, F = x.shape
+        y = torch.empty(n, F, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(nseg, F, device=x.device, dtype=torch.float32)
+        N.check(lib.sgg_seg_norm_fwd(N.ptr(x), x.stride(0), F, N.ptr(seg_off), nseg, float(eps), N.ptr(y), F,
+                                     N.ptr(rstd), N.stream_ptr()), "sgg_seg_norm_fwd")
+        ctx.meta = (seg_off, nseg)
+        ctx.save_for_backward(y, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, rstd = ctx.saved_tensors
+        seg_off, nseg = ctx.meta
+        dy = _rows(dy, "dy")
+        n, F = y.shape
+        dx = torch.empty(n, F, device=y.device, dtype=torch.float32)
+        N.check(_lib().sgg_seg_norm_bwd(N.ptr(y), F, N.ptr(dy), dy.stride(0), F, N.ptr(seg_off), nseg, N.ptr(rstd),
+                                        N.ptr(dx), F, N.stream_ptr()), "sgg_seg_norm_bwd")
+        return dx, None, None, None
+
+
+def seg_instance_norm(x, seg_off, nseg, eps=1e-5):
+    """InstanceNorm1d (affine=False) of each segment's rows, per feature."""
+    return _SegNorm.apply(x, seg_off, nseg, eps)
 
 
 class SegmentGraph:
@@ -404,3 +460,43 @@ def lstm_sequence(rel, A, Whh, bias, h0=None, c0=None, Wp=None, bp=None, decoder
         raise NotImplementedError("gradient w.r.t. the initial cell state")
     h_last, rel_out = _LSTMSeq.apply(rel, A, Whh, bias, h0, c0, Wp, bp, bool(decoder), T, save)
     return h_last, (rel_out if decoder else None)
+
+
+# ---------------------------------------------------------------------------
+# adversarial loss (losses.py:5-49) -> sgg_bce_fwd / sgg_bce_bwd
+# ---------------------------------------------------------------------------
+class _Bce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ya, yb, split, w):
+        ctx.shape = x.shape
+        x = _req(x, "scores").contiguous().view(-1)
+        loss = torch.empty((), device=x.device, dtype=torch.float32)
+        N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
+                                   N.stream_ptr()), "sgg_bce_fwd")
+        ctx.meta = (split, float(w))
+        ctx.save_for_backward(x, ya, yb)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, ya, yb = ctx.saved_tensors
+        split, w = ctx.meta
+        g = g.contiguous()
+        dx = torch.empty_like(x)
+        N.check(_lib().sgg_bce_bwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), w, N.ptr(g), N.ptr(dx),
+                                   N.stream_ptr()), "sgg_bce_bwd")
+        return dx.view(ctx.shape), None, None, None, None
+
+
+def _scalar_dev(y, device):
+    if torch.is_tensor(y):
+        return y.to(device=device, dtype=torch.float32).reshape(())
+    # a fill kernel, not a host->device copy: stays legal inside graph capture
+    return torch.full((), float(y), device=device, dtype=torch.float32)
+
+
+def bce_pair(scores, split, y_a, y_b, w=1.0):
+    """w * (bce_loss(scores[:split], y_a) + bce_loss(scores[split:], y_b)) with
+    scalar targets (python floats or device scalars); split = len -> one term."""
+    dev = scores.device
+    return _Bce.apply(scores, _scalar_dev(y_a, dev), _scalar_dev(y_b, dev), int(split), w)

@@ -16,9 +16,12 @@ decoder rollout are single fused launches (sgg_lstm_fwd / sgg_lstm_bwd).
 
 Extra keyword-only arguments beyond the reference's are optional and default
 to the reference behaviour:
-  TrajectoryGenerator(..., graph='gat'|'gcn')  selects the message-passing
-      module the forward calls ('gat' = the committed forward,
-      models.py:903-905; 'gcn' = the sgan-g-p checkpoint family, :902).
+  TrajectoryGenerator(..., graph='gat'|'gcn'|'sgangat')  selects the
+      message-passing module the forward calls ('gat' = the committed forward,
+      models.py:903-905; 'gcn' = the sgan-g(-p) checkpoint families, :902;
+      'sgangat' = the sgangat-g-p family: the batched multi-head GAT of the
+      commented sgan/GAT.py:6-106 text, then gcn_module; n_heads is then the
+      per-layer head list, e.g. [4, 1]).
   forward(..., scenes=SceneIndex)  reuses a precomputed scene index.
 """
 import torch
@@ -279,6 +282,89 @@ class GATEncoder(nn.Module):
 
 
 # ---------------------------------------------------------------------------
+# batched multi-head GAT of the sgangat checkpoint family (the commented-out
+# BatchMultiHeadGraphAttention / GAT / GATEncoder text of sgan/GAT.py:6-106)
+# -> sgg_seg_norm_* + sgg_xw + multi-head sgg_gat_*
+# ---------------------------------------------------------------------------
+class BatchMultiHeadGraphAttention(nn.Module):
+    """GAT.py:6-55 text: per head h, h'_h = x w_h; e_ij = LeakyReLU_0.2(
+    h'_i.a_src + h'_j.a_dst) over the complete scene graph (no adjacency);
+    softmax over j; out_h = att h'_h + bias.  All heads in one kernel launch;
+    the (n, heads*F_out) output is the transpose(1, 2).view concat of :86."""
+
+    def __init__(self, n_head, f_in, f_out, attn_dropout, bias=True):
+        super().__init__()
+        self.n_head, self.f_in, self.f_out = n_head, f_in, f_out
+        self.w = nn.Parameter(torch.Tensor(n_head, f_in, f_out))
+        self.a_src = nn.Parameter(torch.Tensor(n_head, f_out, 1))
+        self.a_dst = nn.Parameter(torch.Tensor(n_head, f_out, 1))
+        self.leaky_relu = nn.LeakyReLU(negative_slope=0.2)
+        self.softmax = nn.Softmax(dim=-1)
+        self.dropout = nn.Dropout(attn_dropout)
+        if bias:
+            self.bias = nn.Parameter(torch.Tensor(f_out))
+            nn.init.constant_(self.bias, 0)
+        else:
+            self.register_parameter("bias", None)
+        nn.init.xavier_uniform_(self.w, gain=1.414)
+        nn.init.xavier_uniform_(self.a_src, gain=1.414)
+        nn.init.xavier_uniform_(self.a_dst, gain=1.414)
+
+    def forward(self, x, graph, epilogue):
+        if self.dropout.p > 0 and self.training:
+            raise NotImplementedError("attention dropout is not implemented in the fused kernel (dropout1=0)")
+        H, Fi, Fo = self.n_head, self.f_in, self.f_out
+        w_all = self.w.permute(1, 0, 2).reshape(Fi, H * Fo)                 # [w_0 | .. | w_{H-1}]
+        wh = K.xw(x, w_all)                                                  # n x H*Fo
+        a_all = torch.cat([self.a_src.view(H, Fo), self.a_dst.view(H, Fo)], dim=1)
+        return K.gat_attention(wh, a_all, 0.2, graph, epilogue, heads=H, bias=self.bias)
+
+    def __repr__(self):
+        return "%s (%d -> %d -> %d)" % (self.__class__.__name__, self.n_head, self.f_in, self.f_out)
+
+
+class BatchGAT(nn.Module):
+    """GAT.py:58-89 text: per layer InstanceNorm1d over the scene's peds, the
+    multi-head attention, then ELU (all but the last layer, whose single head
+    is squeezed).  The reference's norm_list modules hold no parameters."""
+
+    def __init__(self, n_units, n_heads, dropout=0.2, alpha=0.2):
+        super().__init__()
+        self.n_layer = len(n_units) - 1
+        self.dropout = dropout
+        self.layer_stack = nn.ModuleList()
+        for i in range(self.n_layer):
+            f_in = n_units[i] * n_heads[i - 1] if i else n_units[i]
+            self.layer_stack.append(BatchMultiHeadGraphAttention(n_heads[i], f_in=f_in, f_out=n_units[i + 1],
+                                                                 attn_dropout=dropout))
+        if n_heads[self.n_layer - 1] != 1:
+            raise ValueError("the last batched GAT layer must have one head (GAT.py:83 squeezes it)")
+
+    def forward(self, x, graph):
+        if self.dropout > 0 and self.training:
+            raise NotImplementedError("dropout between GAT layers is not implemented (dropout1=0)")
+        for i, layer in enumerate(self.layer_stack):
+            x = K.seg_instance_norm(x, graph.seg_off, graph.nseg)
+            x = layer(x, graph, 0 if i + 1 == self.n_layer else 1)          # ELU fused into the kernel
+        return x
+
+
+class BatchGATEncoder(nn.Module):
+    """GAT.py:92-106 text: the batched GAT run over each scene's peds
+    (complete graph); (B, n_units[0]) -> (B, n_units[-1])."""
+
+    def __init__(self, n_units, n_heads, dropout, alpha):
+        super().__init__()
+        self.gat_net = BatchGAT(n_units, n_heads, dropout, alpha)
+
+    def forward(self, h_states, seq_start_end, scenes=None):
+        sc = _scenes(seq_start_end, h_states.device, scenes)
+        if sc.max_n > 128:
+            raise ValueError("GAT kernels hold <= 128 peds per scene (got %d)" % sc.max_n)
+        return self.gat_net(h_states, K.SegmentGraph(sc.scene_off, sc.S, sc.max_n, 1, None))
+
+
+# ---------------------------------------------------------------------------
 # GCN (models.py:552-712) -> sgg_seg_* + sgg_xw (ReLU fused)
 # ---------------------------------------------------------------------------
 class GCN(nn.Module):
@@ -335,8 +421,8 @@ class TrajectoryGenerator(nn.Module):
         super().__init__()
         if pooling_type and pooling_type.lower() == "none":
             pooling_type = None
-        if graph not in ("gat", "gcn"):
-            raise ValueError("graph must be 'gat' or 'gcn'")
+        if graph not in ("gat", "gcn", "sgangat"):
+            raise ValueError("graph must be 'gat', 'gcn' or 'sgangat'")
         self.obs_len = obs_len
         self.pred_len = pred_len
         self.mlp_dim = mlp_dim
@@ -370,8 +456,21 @@ class TrajectoryGenerator(nn.Module):
             self.noise_dim = None
         else:
             self.noise_first_dim = noise_dim[0]
-        self.gatencoder = GATEncoder(n_units=n_units, n_heads=n_heads, dropout=dropout1, alpha=alpha)
         input_dim = encoder_h_dim + bottleneck_dim if pooling_type else encoder_h_dim
+        # module set (and registration order, which fixes the optimizer-state
+        # order) of each checkpoint family:
+        #   gat     : committed models.py:800-812 -> gatencoder, gcn_module
+        #   gcn     : sgan-g(-p)-models            -> mlp_decoder_context, gcn_module
+        #   sgangat : sgangat-g-p-models           -> gatencoder.gat_net, mlp_decoder_context, gcn_module
+        # (mlp_decoder_context is carried by those checkpoints but not called)
+        if graph == "gat":
+            self.gatencoder = GATEncoder(n_units=n_units, n_heads=n_heads, dropout=dropout1, alpha=alpha)
+        elif graph == "sgangat":
+            heads = list(n_heads) if isinstance(n_heads, (list, tuple)) else [n_heads] * (len(n_units) - 2) + [1]
+            self.gatencoder = BatchGATEncoder(n_units=list(n_units), n_heads=heads, dropout=dropout1, alpha=alpha)
+        if graph != "gat":
+            self.mlp_decoder_context = make_mlp([input_dim, mlp_dim, decoder_h_dim - self.noise_first_dim],
+                                                activation=activation, batch_norm=batch_norm, dropout=dropout)
         self.gcn_module = GCNModule(input_dim=input_dim, hidden_dim=72, out_dim=16, gcn_layers=2,
                                     final_dim=decoder_h_dim - self.noise_first_dim)
 
@@ -403,8 +502,12 @@ class TrajectoryGenerator(nn.Module):
             pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc)
             ctx = torch.cat([ctx, pool_h], dim=1)
         if self.mlp_decoder_needed():
-            mod = self.gatencoder if self.graph == "gat" else self.gcn_module
-            noise_input = mod(ctx, seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
+            if self.graph == "gat":
+                noise_input = self.gatencoder(ctx, seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
+            else:
+                if self.graph == "sgangat":
+                    ctx = self.gatencoder(ctx, seq_start_end, scenes=sc)
+                noise_input = self.gcn_module(ctx, seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
         else:
             noise_input = ctx
         decoder_h = self.add_noise(noise_input, seq_start_end, user_noise=user_noise, scenes=sc).unsqueeze(0)

@@ -40,7 +40,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .losses import bce_loss
+from . import kernels as K
 from .models import get_noise
 from .scene import SceneIndex
 from .utils import relative_to_abs
@@ -107,13 +107,20 @@ class StepInputs:
 
 
 class GanTrainer:
-    def __init__(self, G, D, args=None, dp=None, selective_backward=True, capturable=False):
+    def __init__(self, G, D, args=None, dp=None, selective_backward=True, capturable=False, bce_pair=None):
+        """bce_pair(scores, split, y_a, y_b, w): the adversarial loss
+        (default: the fused kernel, kernels.bce_pair); the CPU DP tests plug
+        in a torch restatement together with the oracle's models."""
         self.G, self.D = G, D
+        self.bce_pair = bce_pair or K.bce_pair
         self.args = args or TrainArgs()
         self.dp = dp or DataParallel()
         self.selective_backward = selective_backward
-        self.opt_g = torch.optim.Adam(G.parameters(), lr=self.args.g_learning_rate, capturable=capturable)
-        self.opt_d = torch.optim.Adam(D.parameters(), lr=self.args.d_learning_rate, capturable=capturable)
+        # fused multi-tensor Adam: 2 launches per step instead of ~10 per tensor
+        self.opt_g = torch.optim.Adam(G.parameters(), lr=self.args.g_learning_rate, capturable=capturable,
+                                      fused=True)
+        self.opt_d = torch.optim.Adam(D.parameters(), lr=self.args.d_learning_rate, capturable=capturable,
+                                      fused=True)
         skip = "gcn_module." if getattr(G, "graph", "gat") == "gat" else "gatencoder."
         self.g_params = [p for n, p in G.named_parameters() if not n.startswith(skip)]
         self.d_params = list(D.parameters())
@@ -156,15 +163,13 @@ class GanTrainer:
         traj_rel = torch.cat([torch.cat([obs_rel, fake_rel], 0), torch.cat([obs_rel, pred_gt_rel], 0)], 1)
         sc2 = sc.repeat(2)
         scores = self.D(traj, traj_rel, _sse_of(sc2), scenes=sc2)
-        s_fake, s_real = scores[:sc.B], scores[sc.B:]
         if inputs is not None:
-            y_real, y_fake = inputs.y[0], inputs.y[1]
+            y_real = inputs.y[0]
         else:
             y_real = random.uniform(0.7, 1.2)
-            y_fake = random.uniform(0, 0.3)
-        w = sc.B / B_global
-        loss = w * (bce_loss(s_real, torch.ones_like(s_real) * y_real) +
-                    bce_loss(s_fake, torch.zeros_like(s_fake) * y_fake))
+            random.uniform(0, 0.3)   # the fake-label draw (losses.py:47): consumed, but zeros_like * y == 0
+        # gan_d_loss = bce(real, y_real) + bce(fake, 0); scores = [fake | real]
+        loss = self.bce_pair(scores, sc.B, 0.0, y_real, sc.B / B_global)
         self.opt_d.zero_grad(set_to_none=True)
         loss.backward()
         vals = self._finish(self.d_params, self.opt_d, [loss], a.clipping_threshold_d)
@@ -231,7 +236,7 @@ class GanTrainer:
         fake_last = relative_to_abs(fake_rel_last, obs[-1])
         scores = D(torch.cat([obs, fake_last], 0), torch.cat([obs_rel, fake_rel_last], 0), sse, scenes=sc)
         y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)
-        adv = (sc.B / B_global) * bce_loss(scores, torch.ones_like(scores) * y)
+        adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global)    # gan_g_loss
         loss = adv + (terms[0] if terms else 0.0)
         self.opt_g.zero_grad(set_to_none=True)
         torch.autograd.backward(loss, inputs=self.g_params)

@@ -102,22 +102,47 @@ int sgg_pool_bwd(const float* U, const float* pos, const float* A, const float* 
  *   y_i  = epilogue(hp_i): 0 identity, 1 ELU, 2 log_softmax(ELU(.)) over F
  * mask_mode 0: (i == j) or (lab_i == lab_j and lab_i != 0)   (models.py:263-267)
  * mask_mode 1: complete graph                                (models.py:282-283)
- * Wh: n x F (ld F); y is written with row stride ldy (so heads can be written
- * straight into their concat slot, models.py:234); hp (n x F) is written when
- * epilogue != 0 (needed by the backward; epilogue 2 requires ldy == F).  Segments larger than
- * SGG_GAT_MAX_NODES are rejected.
+ * Multi-head (the batched GAT of the sgangat family, sgan/GAT.py:6-55 text,
+ * attention over the complete scene graph = mask_mode 1): Wh is n x heads*F
+ * (heads side by side), a is heads x 2F ([a_src | a_dst] per head), head h
+ * writes columns [hF, hF + F) of y (the head concat of GAT.py:86), and bias
+ * (F, may be NULL) is added to every head's aggregate before the epilogue
+ * (GAT.py:41).  heads = 1, bias = NULL is the GraphAttentionLayer above.
+ * y is written with row stride ldy (>= heads*F; single-head layers of the
+ * group GAT write straight into their concat slot, models.py:234); hp
+ * (n x heads*F, pre-epilogue, bias included) is written when epilogue != 0
+ * (needed by the backward).  Epilogue 2 requires heads == 1 and ldy == F.
+ * Segments larger than SGG_GAT_MAX_NODES are rejected.
  */
-int sgg_gat_fwd(const float* Wh, const float* a, const float* labels, const int32_t* seg_off,
-                int nseg, int n, int F, float alpha, int mask_mode, int epilogue, int max_seg,
-                float* hp, float* y, int ldy, void* stream);
+int sgg_gat_fwd(const float* Wh, int heads, const float* a, const float* bias, const float* labels,
+                const int32_t* seg_off, int nseg, int n, int F, float alpha, int mask_mode,
+                int epilogue, int max_seg, float* hp, float* y, int ldy, void* stream);
 
-/* Backward of sgg_gat_fwd.  dy: n x F (row stride lddy), y / hp as written by
- * the forward.  Writes dWh (n x F), ds, dt (n): the caller finishes
- * da = [Wh^T ds ; Wh^T dt], dX = dWh W^T, dW = X^T dWh (plain GEMMs). */
-int sgg_gat_bwd(const float* Wh, const float* a, const float* labels, const int32_t* seg_off,
+/* Backward of sgg_gat_fwd (bias excluded: its gradient is the column sum of
+ * the pre-epilogue gradient, formed by the caller).  dy: head h at columns
+ * [hF, hF + F) of row stride lddy; y / hp as written by the forward.  Writes
+ * dWh (n x heads*F) and ds, dt (n x heads): the caller finishes
+ * da_h = [Wh_h^T ds_h ; Wh_h^T dt_h], dX = dWh W^T, dW = X^T dWh. */
+int sgg_gat_bwd(const float* Wh, int heads, const float* a, const float* labels, const int32_t* seg_off,
                 int nseg, int n, int F, float alpha, int mask_mode, int epilogue, int max_seg,
                 const float* hp, const float* y, const float* dy, int lddy,
                 float* dWh, float* ds, float* dt, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Instance normalisation over the rows of each segment (InstanceNorm1d,
+ * affine = False, of the sgangat GAT, GAT.py:71-74, 80: each scene's
+ * (1, F, N) view is normalised per feature over its N peds):
+ *   y_ij = (x_ij - mean_j) * rstd_j,  rstd_j = 1 / sqrt(var_j + eps)
+ * with the biased variance over the segment.  rstd (nseg x F) is saved for
+ * the backward.  A 1-row segment normalises to 0 (torch raises for it; the
+ * reference's loader never produces one-ped scenes, trajectories_GCN.py).
+ */
+int sgg_seg_norm_fwd(const float* x, int ldx, int F, const int32_t* seg_off, int nseg, float eps,
+                     float* y, int ldy, float* rstd, void* stream);
+
+/* dx = rstd * (dy - mean(dy) - y * mean(dy * y)) per segment and feature. */
+int sgg_seg_norm_bwd(const float* y, int ldy, const float* dy, int lddy, int F, const int32_t* seg_off,
+                     int nseg, const float* rstd, float* dx, int lddx, void* stream);
 
 /* ------------------------------------------------------------------------
  * Group structure of each scene from the last observed group labels
@@ -200,6 +225,21 @@ int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float*
                  const float* act_all, const float* dh_last, const float* dout, int T, int B,
                  int H, int decoder, float* dG, float* dh0, float* drel_in, float* drel_tot,
                  void* stream);
+
+/* ------------------------------------------------------------------------
+ * Adversarial loss (losses.py:5-21 bce_loss; gan_d_loss :36-49 sums two of
+ * them, gan_g_loss :24-33 is one), shard-weighted:
+ *   loss = w * (mean_{i < split} f(x_i, *ya) + mean_{i >= split} f(x_i, *yb))
+ *   f(x, y) = max(x, 0) - x y + log(1 + exp(-|x|))
+ * An empty range contributes 0.  ya, yb are device scalars (graph-capturable
+ * label smoothing); loss is one device float. */
+int sgg_bce_fwd(const float* x, int n, int split, const float* ya, const float* yb, float w, float* loss,
+                void* stream);
+
+/* dx_i = *gout * w / |range(i)| * df/dx(x_i, y_range(i)) with torch's
+ * subgradients at 0 (clamp passes x >= 0, d|x| = sign(x) = 0 at 0). */
+int sgg_bce_bwd(const float* x, int n, int split, const float* ya, const float* yb, float w,
+                const float* gout, float* dx, void* stream);
 
 #ifdef __cplusplus
 }

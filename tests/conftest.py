@@ -20,3 +20,17 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+def load_family(model, sd):
+    """Load a reference-built generator state (committed GAT layout:
+    gatencoder.gat_intra/inter + gcn_module) into a model of any checkpoint
+    family.  Keys the family lacks (the group GAT for 'gcn') are dropped;
+    the only keys allowed to stay at init are mlp_decoder_context.*, which
+    those families carry but never call."""
+    own = model.state_dict()
+    take = {k: v for k, v in sd.items() if k in own}
+    missing = [k for k in own if k not in take]
+    assert all(k.startswith("mlp_decoder_context.") for k in missing), missing
+    model.load_state_dict(take, strict=False)
+    return model

@@ -300,6 +300,118 @@ def fx_gen():
         save("gen_fwd_%s.npz" % mode, out)
 
 
+# ----------------------------------------------------------------------------
+# sgangat family: the commented batched-GAT text of sgan/GAT.py:6-106
+# ----------------------------------------------------------------------------
+def _ref_sgat_classes():
+    """Un-comment sgan/GAT.py lines 6-106 (BatchMultiHeadGraphAttention, GAT,
+    GATEncoder) and execute that text in a private namespace.  Nothing is
+    written to the repo; the module is imported this way only to produce the
+    reference outputs for the sgangat checkpoint family."""
+    lines = open(os.path.join(REF, "sgan/GAT.py")).read().split("\n")[5:106]
+    src = "\n".join(l[2:] if l.startswith("# ") else "" for l in lines)
+    ns = dict(torch=torch, nn=torch.nn, F=torch.nn.functional, np=np)
+    exec(compile(src, "sgan/GAT.py:6-106 (commented text)", "exec"), ns)
+    return ns
+
+
+SGAT = None
+SGAT_SIZES = [2, 5, 20, 20, 33, 57, 64, 7, 12, 20, 20, 3]   # the instance norm needs >= 2 peds
+
+
+def build_sgangat(seed=0):
+    """Generator of the sgangat-g-p family: build_models(seed)'s G (encoder,
+    decoder, pool_net, gcn_module) + the batched GAT (heads 4,1; units
+    40,16,40 from the checkpoint args) + mlp_decoder_context [40, 64, 24]."""
+    global SGAT
+    if SGAT is None:
+        SGAT = _ref_sgat_classes()
+    g, _ = build_models(seed)
+    torch.manual_seed(seed + 500)
+    sg = SGAT["GATEncoder"]([40, 16, 40], [4, 1], 0.0, 0.2)
+    for layer in sg.gat_net.layer_stack:           # bias is zero-init (GAT.py:21); exercise it
+        layer.bias.data.normal_(0.0, 0.1)
+    mdc = M.make_mlp([40, 64, 24], activation="relu", batch_norm=False, dropout=0.0)
+    return g, sg, mdc
+
+
+def _sgat_call(sg, x, sse):
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):      # GAT.py:101-102 print per scene
+        return sg(x.unsqueeze(0), sse)[0]
+
+
+def _sgangat_forward(g, sg, batch, noise):
+    obs_traj, obs_rel, sse, obs_g = batch["obs_traj"], batch["obs_traj_rel"], batch["seq_start_end"], batch["obs_traj_g"]
+    Bn = obs_rel.size(1)
+    h = g.encoder(obs_rel)
+    end_pos = obs_traj[-1]
+    ctx = torch.cat([h.view(-1, g.encoder_h_dim), g.pool_net(h, sse, end_pos)], dim=1)
+    ctx = _sgat_call(sg, ctx, sse)
+    ni = g.gcn_module(ctx, sse, end_pos, obs_g[-1])
+    dh = g.add_noise(ni, sse, user_noise=noise).unsqueeze(0)
+    dc = torch.zeros(g.num_layers, Bn, g.decoder_h_dim)
+    out, _ = g.decoder(obs_traj[-1], obs_rel[-1], (dh, dc), sse)
+    return out
+
+
+def _sgangat_state(g, sg, mdc, grads=False):
+    """State dict (or grads) under the sgangat checkpoint's key names."""
+    out = {}
+    for prefix, mod in (("", g), ("gatencoder.", sg), ("mlp_decoder_context.", mdc)):
+        for k, p in mod.named_parameters():
+            if prefix == "" and k.startswith("gatencoder."):
+                continue
+            if grads:
+                if p.grad is not None:
+                    out[prefix + k] = p.grad.detach().numpy().copy()
+            else:
+                out[prefix + k] = p.detach().numpy().copy()
+    return out
+
+
+def fx_sgangat():
+    # batched GAT module alone: fwd + bwd over scenes of 2..64 peds
+    g, sg, mdc = build_sgangat(0)
+    torch.manual_seed(61)
+    B = sum(SGAT_SIZES)
+    x = torch.randn(B, 40, requires_grad=True)
+    sse = sse_of(SGAT_SIZES)
+    y = _sgat_call(sg, x, sse)
+    dy = torch.randn_like(y)
+    sg.zero_grad()
+    (y * dy).sum().backward()
+    out = dict(x=x.detach().numpy(), sse=sse.numpy(), out=y.detach().numpy(), dout=dy.numpy(), dx=x.grad.numpy())
+    for k, p in sg.named_parameters():
+        out["w/" + k] = p.detach().numpy()
+        out["dw/" + k] = p.grad.numpy()
+    save("sgangat_gat.npz", out)
+    # the whole generator
+    batches = {"synth": synth_batch([20] * 6 + [2, 5, 33], seed=5), "zara1": real_batch("zara1", "test", 16)}
+    out = {}
+    for k, v in _sgangat_state(g, sg, mdc).items():
+        out["w/" + k] = v
+    for bname, b in batches.items():
+        S = b["seq_start_end"].size(0)
+        torch.manual_seed(77)
+        noise = torch.randn(S, 8)
+        g.zero_grad()
+        sg.zero_grad()
+        y = _sgangat_forward(g, sg, b, noise)
+        dy = torch.randn_like(y)
+        (y * dy).sum().backward()
+        pre = bname + "/"
+        for k in ("obs_traj", "obs_traj_rel", "obs_traj_g", "seq_start_end", "pred_traj", "pred_traj_rel"):
+            out[pre + k] = b[k].numpy()
+        out[pre + "noise"] = noise.numpy()
+        out[pre + "out"] = y.detach().numpy()
+        out[pre + "dout"] = dy.numpy()
+        for k, v in _sgangat_state(g, sg, mdc, grads=True).items():
+            out[pre + "dw/" + k] = v
+    save("gen_fwd_sgangat.npz", out)
+
+
 def fx_disc():
     g, d = build_models(0)
     b = synth_batch([20] * 4 + [2, 9], seed=6)
@@ -353,9 +465,15 @@ def fx_eval(splits):
     seeded random-init weights (trained checkpoints are not loadable with the
     safe loader: they hold collections.defaultdict)."""
     res = {}
-    for mode in ("gat", "gcn"):
+    for mode in ("gat", "gcn", "sgangat"):
         for split in splits:
             g, _ = build_models(0)
+            if mode == "sgangat":
+                g, sg, _ = build_sgangat(0)
+                g.forward = types.MethodType(
+                    lambda self, ot, orl, sse, og, user_noise=None, sg=sg: _sgangat_forward(
+                        self, sg, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse, obs_traj_g=og), user_noise),
+                    g)
             if mode == "gcn":
                 g.forward = types.MethodType(
                     lambda self, ot, orl, sse, og, user_noise=None: _gen_forward(
@@ -407,7 +525,8 @@ def fx_cpu_timing():
         json.dump(res, f, indent=1)
 
 
-ALL = dict(weights=fx_weights, pool=fx_pool, gat=fx_gat, gcn=fx_gcn, gen=fx_gen, disc=fx_disc,
+ALL = dict(weights=fx_weights, pool=fx_pool, gat=fx_gat, gcn=fx_gcn, gen=fx_gen, sgangat=fx_sgangat,
+           disc=fx_disc,
            train=fx_train_step, data=copy_test_data, timing=fx_cpu_timing)
 
 if __name__ == "__main__":

@@ -46,6 +46,15 @@ def _models():
     return _Adapt(g), _Adapt(d)
 
 
+def _bce_pair(scores, split, y_a, y_b, w=1.0):
+    """Torch restatement of kernels.bce_pair over the oracle's bce_loss."""
+    from oracle import sgan_oracle as O
+    x = scores.reshape(-1)
+    a, b = x[:split], x[split:]
+    terms = [O.bce_loss(t, torch.ones_like(t) * y) for t, y in ((a, y_a), (b, y_b)) if t.numel()]
+    return w * sum(terms)
+
+
 def _run(rank, world, port, out):
     from sgan.data.synthetic import synthetic_batch
     from sgan.scene import SceneIndex
@@ -54,7 +63,7 @@ def _run(rank, world, port, out):
     if world > 1:
         dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     g, d = _models()
-    tr = GanTrainer(g, d, dp=DataParallel())
+    tr = GanTrainer(g, d, dp=DataParallel(), bce_pair=_bce_pair)
     batch = synthetic_batch(SIZES, seed=11)
     sc = SceneIndex(np.concatenate([[0], np.cumsum(SIZES)]), "cpu")
     s0, s1 = tr.dp.shard(sc.S)

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import GOLDEN, load_family
 
 pytestmark = pytest.mark.gpu
 
@@ -41,12 +41,16 @@ def build_models(graph="gat"):
     g = TrajectoryGenerator(8, 12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32, mlp_dim=64, num_layers=1,
                             noise_dim=(8,), noise_type="gaussian", noise_mix_type="global",
                             pooling_type="pool_net", pool_every_timestep=False, dropout=0.0, bottleneck_dim=8,
-                            batch_norm=False, n_units=[40, 16, 40], n_heads=1, dropout1=0.0, alpha=0.2,
-                            graph=graph)
+                            batch_norm=False, n_units=[40, 16, 40], n_heads=[4, 1] if graph == "sgangat" else 1,
+                            dropout1=0.0, alpha=0.2, graph=graph)
     d = TrajectoryDiscriminator(8, 12, embedding_dim=16, h_dim=48, mlp_dim=64, num_layers=1, batch_norm=False,
                                 dropout=0.0, d_type="global")
     w = npz("weights.npz")
-    g.load_state_dict({k[2:]: torch.from_numpy(w[k]) for k in w.files if k.startswith("g/")})
+    if graph == "sgangat":   # the family's full state (batched GAT + mlp_decoder_context) is in its fixture
+        f = npz("gen_fwd_sgangat.npz")
+        g.load_state_dict({k[2:]: torch.from_numpy(f[k]) for k in f.files if k.startswith("w/")})
+    else:
+        load_family(g, {k[2:]: torch.from_numpy(w[k]) for k in w.files if k.startswith("g/")})
     d.load_state_dict({k[2:]: torch.from_numpy(w[k]) for k in w.files if k.startswith("d/")})
     return g.to(DEV), d.to(DEV)
 
@@ -108,7 +112,75 @@ def test_graph_module_vs_reference_fixture(name, kind):
             close(p.grad, f["dw/" + k], rtol=2e-4, floor=fl, what=name + " d" + k)
 
 
-@pytest.mark.parametrize("graph", ["gat", "gcn"])
+def test_seg_instance_norm_matches_torch():
+    """sgg_seg_norm_fwd/bwd vs torch's InstanceNorm1d (affine=False) per
+    scene, F in {40, 64, 100}; a one-ped scene normalises to 0."""
+    from sgan import kernels as K
+    torch.manual_seed(5)
+    sizes = [2, 3, 20, 64, 128, 7, 1]
+    off = torch.tensor(np.concatenate([[0], np.cumsum(sizes)]), dtype=torch.int32, device=DEV)
+    for F in (40, 64, 100):
+        x = (torch.randn(sum(sizes), F, device=DEV) * 3 + 1).requires_grad_(True)
+        y = K.seg_instance_norm(x, off, len(sizes))
+        dy = torch.randn_like(y)
+        (y * dy).sum().backward()
+        o = 0
+        for n in sizes:
+            xs = x.detach()[o:o + n].double().cpu().requires_grad_(True)
+            if n == 1:
+                assert float(y[o:o + n].abs().max()) == 0.0
+                o += n
+                continue
+            ref = torch.nn.functional.instance_norm(xs.t().unsqueeze(0), eps=1e-5)[0].t()
+            (ref * dy[o:o + n].double().cpu()).sum().backward()
+            close(y[o:o + n], ref.detach().numpy(), rtol=2e-5, what="norm y n=%d F=%d" % (n, F))
+            if n > 2:   # a 2-row segment normalises to +-1 whatever x is: its dx is pure rounding noise
+                close(x.grad[o:o + n], xs.grad.numpy(), rtol=1e-4, floor=1e-3, what="norm dx n=%d F=%d" % (n, F))
+            o += n
+
+
+def test_bce_pair_matches_reference_formula():
+    """sgg_bce_fwd/bwd vs losses.py:5-21 under torch autograd, incl. the
+    scores D's trailing ReLU pins at exactly 0, and an empty range."""
+    from sgan import kernels as K
+    from sgan.losses import bce_loss
+    torch.manual_seed(2)
+    for n, split in ((1280 * 2, 1280), (1000, 1000), (37, 0), (5, 2)):
+        x = torch.randn(n, 1, device=DEV) * 3
+        x[::3] = 0.0
+        ya, yb = 0.0, 0.93
+        for w in (1.0, 0.25):
+            xa = x.clone().requires_grad_(True)
+            loss = K.bce_pair(xa, split, ya, torch.tensor(yb, device=DEV), w)
+            loss.backward(torch.tensor(1.7, device=DEV))
+            xr = x.double().clone().requires_grad_(True)
+            parts = [bce_loss(t, torch.ones_like(t) * y) for t, y in ((xr[:split], ya), (xr[split:], yb)) if t.numel()]
+            ref = w * sum(parts)
+            (ref * 1.7).backward()
+            close(loss, np.array(float(ref)), rtol=2e-6, what="bce loss n=%d" % n)
+            close(xa.grad, xr.grad.cpu().numpy(), rtol=2e-6, what="bce grad n=%d" % n)
+
+
+def test_sgangat_module_vs_reference_fixture():
+    """Batched multi-head GAT of the sgangat family (GAT.py:6-106 text, heads
+    4,1, instance norm) against the reference's own output."""
+    from sgan.models import BatchGATEncoder
+    f = npz("sgangat_gat.npz")
+    mod = BatchGATEncoder([40, 16, 40], [4, 1], 0.0, 0.2)
+    mod.load_state_dict({k[2:]: torch.from_numpy(f[k]) for k in f.files if k.startswith("w/")})
+    mod = mod.to(DEV)
+    x = T(f["x"]).requires_grad_(True)
+    y = mod(x, T(f["sse"]))
+    close(y, f["out"], rtol=1e-5, what="sgat out")
+    (y * T(f["dout"])).sum().backward()
+    close(x.grad, f["dx"], rtol=1e-4, what="sgat dx")
+    fl = grad_floor(f, "dw/")
+    for k, p in mod.named_parameters():
+        # layer 0's bias gradient nearly cancels in the next layer's norm
+        close(p.grad, f["dw/" + k], rtol=1e-3 if k.endswith("0.bias") else 2e-4, floor=fl, what="sgat d" + k)
+
+
+@pytest.mark.parametrize("graph", ["gat", "gcn", "sgangat"])
 def test_generator_vs_reference_fixture(graph):
     g, _ = build_models(graph)
     f = npz("gen_fwd_%s.npz" % graph)
@@ -191,7 +263,7 @@ def test_evaluate_ade_fde_all_splits():
     reference run on CPU (tests/golden/evaluate.json)."""
     from sgan.evaluate import evaluate_split
     ev = json.load(open(os.path.join(GOLDEN, "evaluate.json")))
-    for graph in ("gat", "gcn"):
+    for graph in ("gat", "gcn", "sgangat"):
         g, _ = build_models(graph)
         for split in ("eth", "hotel", "univ", "zara1", "zara2"):
             torch.manual_seed(0)
