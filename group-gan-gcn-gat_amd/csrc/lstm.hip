@@ -237,6 +237,8 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_fwd: bad sizes T=%d B=%d", T, B);
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (lstm_fwd_mfma_ok(H, B))
+    return lstm_fwd_mfma(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
   switch (H) {
     case 16: return launch_lstm_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
     case 32: return launch_lstm_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);

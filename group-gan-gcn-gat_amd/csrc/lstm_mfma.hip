@@ -1,0 +1,172 @@
+// Fused LSTM sequence forward on v_mfma_f32_16x16x4_f32 (Encoder,
+// reference sgan/models.py:62-92; Decoder rollout :142-178).  Same contract
+// as lstm_fwd_kernel (lstm.hip, sgg_lstm_fwd in include/sgg.h); used for the
+// large batches of the training step, where the per-step gate GEMM
+// (4H x H per ped) dominates and the VALU form is FMA-bound.
+//
+// One wave = 16 peds and the whole recurrence stays in its registers:
+//   G^T (4H x 16 peds) = W_ext (4H x (H + 4)) . X^T ((H + 4) x 16 peds)
+// with X = [h_{t-1} | r_x r_y 1 0]: the folded input projection A r + b'
+// rides along as one extra 4-deep k-step.  16x16x4 lane maps (A[row][k]:
+// lane (k<<4 | row); B[k][col]: lane (k<<4 | col); D[row][col]: lane
+// (row>>2 << 4 | col), register row & 3), so lane l = (q = l >> 4, ped = l & 15)
+// ends a step holding gate rows 16 mt + 4q + r of its ped: the i, f, g and o
+// rows of unit u = 16 mu + 4q + r sit in tiles mu, mu + H/16, mu + 2H/16,
+// mu + 3H/16 of the SAME lane and register, so the cell update is lane-local.
+// The k order of the next step's GEMM is permuted so that k-step ks, lane q
+// supplies unit 16 (ks >> 2) + 4q + (ks & 3) -- exactly the h value that lane
+// just produced (h[ks]); W_ext's columns are loaded into registers in the
+// same permuted order once.  No LDS, no barriers: waves are independent.
+// Decoder: rel_t = Wp h_t + bp is a lane partial over its H/4 units plus two
+// cross-q shuffles, and feeds the next step's input k-step in registers.
+#include "sgg_common.h"
+
+namespace sgg {
+
+namespace {
+
+// v_exp_f32 / v_rcp_f32 forms (~2 ulp): the 5H transcendentals per ped and
+// step are the VALU side of this kernel
+__device__ __forceinline__ float sigm_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f); }
+
+template <int H>
+__global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
+    const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
+    const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
+    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
+    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out) {
+  constexpr int G4 = 4 * H;
+  constexpr int MT = G4 / 16;     // gate-row tiles
+  constexpr int MU = H / 16;      // unit tiles (i/f/g/o blocks are MU tiles apart)
+  constexpr int KSH = H / 4;      // k-steps over h_{t-1}
+  constexpr int NU = H / 4;       // units per lane
+  const bool save = act_all != nullptr;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, c16 = lane & 15;
+  const int ped = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + c16;
+  const bool valid = ped < B;
+
+  // W_ext in registers, columns in the permuted k order
+  float w[MT][KSH + 1];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = 16 * mt + c16;
+#pragma unroll
+    for (int ks = 0; ks < KSH; ++ks) w[mt][ks] = Whh[row * H + 16 * (ks >> 2) + 4 * q + (ks & 3)];
+    w[mt][KSH] = q == 0 ? A[2 * row] : q == 1 ? A[2 * row + 1] : q == 2 ? bias[row] : 0.f;
+  }
+  float wp0[NU], wp1[NU];
+#pragma unroll
+  for (int k = 0; k < NU; ++k) {
+    const int u = 16 * (k >> 2) + 4 * q + (k & 3);
+    wp0[k] = decoder ? Wp[u] : 0.f;
+    wp1[k] = decoder ? Wp[H + u] : 0.f;
+  }
+  const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
+
+  // state of the lane's NU units (k = 4 mu + r  <->  unit 16 mu + 4q + r)
+  float h[NU], c[NU];
+#pragma unroll
+  for (int mu = 0; mu < MU; ++mu) {
+    const size_t o = (size_t)ped * H + 16 * mu + 4 * q;
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f), cv = hv;
+    if (valid && h0) hv = *reinterpret_cast<const float4*>(h0 + o);
+    if (valid && c0) cv = *reinterpret_cast<const float4*>(c0 + o);
+    h[4 * mu] = hv.x; h[4 * mu + 1] = hv.y; h[4 * mu + 2] = hv.z; h[4 * mu + 3] = hv.w;
+    c[4 * mu] = cv.x; c[4 * mu + 1] = cv.y; c[4 * mu + 2] = cv.z; c[4 * mu + 3] = cv.w;
+    if (valid && save) {
+      *reinterpret_cast<float4*>(h_all + o) = hv;
+      *reinterpret_cast<float4*>(c_all + o) = cv;
+    }
+  }
+  // input k-step operand: r_x (q = 0), r_y (q = 1), 1 (q = 2), 0 (q = 3)
+  auto load_in = [&](int t) -> float {
+    if (q >= 2) return q == 2 ? 1.f : 0.f;
+    if (!valid) return 0.f;
+    return decoder ? rel[(size_t)ped * 2 + q] : rel[((size_t)t * B + ped) * 2 + q];
+  };
+  float xin = load_in(0);
+
+  for (int t = 0; t < T; ++t) {
+    const float xnext = (!decoder && t + 1 < T) ? load_in(t + 1) : 0.f;   // prefetch
+    floatx4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KSH; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][ks], h[ks], acc[mt], 0, 0, 0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][KSH], xin, acc[mt], 0, 0, 0);
+
+    // gate activations (i, f, o sigmoid; g tanh) and the cell update
+    float px = 0.f, py = 0.f;
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu) {
+      float ai[4], af[4], ag[4], ao[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ai[r] = sigm_fast(acc[mu][r]);
+        af[r] = sigm_fast(acc[MU + mu][r]);
+        ag[r] = tanh_fast(acc[2 * MU + mu][r]);
+        ao[r] = sigm_fast(acc[3 * MU + mu][r]);
+        const int k = 4 * mu + r;
+        c[k] = fmaf(af[r], c[k], ai[r] * ag[r]);
+        h[k] = ao[r] * tanh_fast(c[k]);
+        px = fmaf(wp0[k], h[k], px);
+        py = fmaf(wp1[k], h[k], py);
+      }
+      if (valid && save) {
+        const size_t ab = ((size_t)t * B + ped) * G4 + 16 * mu + 4 * q;
+        *reinterpret_cast<float4*>(act_all + ab) = make_float4(ai[0], ai[1], ai[2], ai[3]);
+        *reinterpret_cast<float4*>(act_all + ab + H) = make_float4(af[0], af[1], af[2], af[3]);
+        *reinterpret_cast<float4*>(act_all + ab + 2 * H) = make_float4(ag[0], ag[1], ag[2], ag[3]);
+        *reinterpret_cast<float4*>(act_all + ab + 3 * H) = make_float4(ao[0], ao[1], ao[2], ao[3]);
+      }
+      if (valid && (save || t == T - 1)) {
+        const size_t o = ((size_t)(save ? t + 1 : T) * B + ped) * H + 16 * mu + 4 * q;
+        *reinterpret_cast<float4*>(h_all + o) = make_float4(h[4 * mu], h[4 * mu + 1], h[4 * mu + 2], h[4 * mu + 3]);
+        *reinterpret_cast<float4*>(c_all + o) = make_float4(c[4 * mu], c[4 * mu + 1], c[4 * mu + 2], c[4 * mu + 3]);
+      }
+    }
+    if (decoder) {   // rel_t = Wp h_t + bp: sum the 4 q-lanes of the ped
+      px += __shfl_xor(px, 16);
+      px += __shfl_xor(px, 32);
+      py += __shfl_xor(py, 16);
+      py += __shfl_xor(py, 32);
+      px += bp0;
+      py += bp1;
+      if (valid && q == 0) *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + ped) * 2) = make_float2(px, py);
+      xin = q == 0 ? px : q == 1 ? py : xin;
+    } else {
+      xin = xnext;
+    }
+  }
+}
+
+template <int H>
+int launch(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0, const float* c0,
+           const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
+           float* rel_out, hipStream_t st) {
+  const int grid = (B + 63) / 64;
+  hipLaunchKernelGGL(lstm_fwd_mfma_kernel<H>, dim3(grid), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B,
+                     decoder, h_all, c_all, act_all, rel_out);
+  SGG_RETURN_LAUNCH("sgg_lstm_fwd");
+}
+
+}  // namespace
+
+// measured crossover vs the VALU kernel (tools/bench_kernels.py lstm)
+// (H = 48 at B <= 2560 -- the discriminator -- is slower than the VALU kernel:
+// 156 MFMAs per step at one wave per SIMD (233 VGPRs))
+bool lstm_fwd_mfma_ok(int H, int B) { return H == 32 && B >= kLstmMfmaMinPeds; }
+
+int lstm_fwd_mfma(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
+                  const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
+                  float* c_all, float* act_all, float* rel_out, hipStream_t st) {
+  if (H == 32) return launch<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+  return launch<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+}
+
+}  // namespace sgg

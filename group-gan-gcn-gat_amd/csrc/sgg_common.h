@@ -46,6 +46,16 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// lstm_mfma.hip: MFMA form of the LSTM sequence forward for large batches,
+// dispatched by sgg_lstm_fwd (lstm.hip); internal, not part of the C ABI
+constexpr int kLstmMfmaMinPeds = 4096;
+__attribute__((visibility("hidden"))) bool lstm_fwd_mfma_ok(int H, int B);
+__attribute__((visibility("hidden"))) int lstm_fwd_mfma(const float* rel, const float* A, const float* Whh,
+                                                        const float* bias, const float* h0, const float* c0,
+                                                        const float* Wp, const float* bp, int T, int B, int H,
+                                                        int decoder, float* h_all, float* c_all, float* act_all,
+                                                        float* rel_out, hipStream_t st);
+
 __device__ __forceinline__ float elu(float x) { return x > 0.f ? x : expm1f(x); }
 // derivative of ELU(alpha = 1) from its input
 __device__ __forceinline__ float elu_grad(float x) { return x > 0.f ? 1.f : expf(x); }

@@ -65,7 +65,7 @@ class SceneIndex:
         sgg_pool_plan, cached per bottleneck width)."""
         target_chunks = target_chunks or self.POOL_TARGET_CHUNKS
         plans = self.__dict__.setdefault("_pool_plans", {})
-        key = (bn > 16, target_chunks, self.POOL_MAX_GPW)
+        key = (bn, target_chunks, self.POOL_MAX_GPW)
         if key not in plans:
             import ctypes
             lib = N.load()

@@ -304,14 +304,16 @@ def test_train_step_vs_reference_fixture(selective):
                 assert err <= 2 * lr * (it + 1) + 1e-5 * np.abs(ref).max(), (it, tag, k, err)
 
 
-@pytest.mark.parametrize("H,T,decoder", [(32, 8, False), (48, 20, False), (32, 12, True), (16, 5, True), (64, 3, False)])
-def test_fused_lstm_vs_oracle(H, T, decoder):
+@pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (48, 20, False, 37), (32, 12, True, 37),
+                                            (16, 5, True, 37), (64, 3, False, 37),
+                                            # batches that take the MFMA forward (lstm_mfma.hip)
+                                            (32, 8, False, 4133), (32, 12, True, 4133), (48, 20, False, 2085)])
+def test_fused_lstm_vs_oracle(H, T, decoder, B):
     """sgg_lstm_fwd/bwd (Encoder / Decoder rollout) against the oracle's
     torch-CPU modules: outputs and every parameter / input gradient."""
     from oracle import sgan_oracle as O
     from sgan import models as M
     torch.manual_seed(H + T)
-    B = 37
     if decoder:
         ref, mod = O.Decoder(T, 16, H, 64, 1, False), M.Decoder(T, 16, H, 64, 1, False)
     else:

@@ -1,0 +1,104 @@
+"""Micro-benchmarks of single kernels on the training shapes (HIP events on
+the launch stream).  Usage: python tools/bench_kernels.py [pool|big|lstm]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "group-gan-gcn-gat_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from sgan import _native as N  # noqa: E402
+from sgan import kernels as K  # noqa: E402
+from sgan.scene import SceneIndex  # noqa: E402
+
+
+def run(S, n, hd, bn, gpws=(0,), reps=20):
+    torch.manual_seed(0)
+    dev = "cuda"
+    B = S * n
+    sc = SceneIndex(np.arange(0, B + 1, n), dev)
+    h = torch.randn(B, hd, device=dev)
+    pos = torch.rand(B, 2, device=dev) * 15
+    W1h = torch.randn(512, hd, device=dev) * 0.1
+    A = torch.randn(512, 2, device=dev) * 0.3
+    c = torch.randn(512, device=dev) * 0.1
+    W2 = torch.randn(bn, 512, device=dev) * 0.05
+    b2 = torch.randn(bn, device=dev) * 0.1
+    U = K.xw_raw(h, W1h, c, trans_w=True)
+    W2T = W2.t().contiguous()
+    lib = N.load()
+    flops = float(S * n * n) * 512 * (4 + 2 * bn)
+    for gpw in gpws:
+        sc.POOL_MAX_GPW = gpw
+        sc.__dict__.pop("_pool_plans", None)
+        chunks, nchunks, max_rows, g = sc.pool_plan(bn)
+        out = torch.empty(B, bn, device=dev)
+        am = torch.empty(B, bn, device=dev, dtype=torch.int32)
+        call = lambda: N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2T), N.ptr(b2),
+                                                N.ptr(sc.scene_off), N.ptr(chunks), nchunks, max_rows, g, B, bn,
+                                                sc.max_n, N.ptr(out), N.ptr(am), N.stream_ptr()), "pool")
+        for _ in range(3):
+            call()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / reps * 1e3
+        print("pool_fwd S=%5d n=%2d bn=%2d chunks=%5d gpw=%d  %8.1f us  %6.1f TF/s" % (
+            S, n, bn, nchunks, g, us, flops / us / 1e6), flush=True)
+
+
+def lstm(B, T, H, decoder, reps=10, save=False):
+    torch.manual_seed(0)
+    dev = "cuda"
+    lib = N.load()
+    rel = torch.randn(1 if decoder else T, B, 2, device=dev).squeeze(0) * 0.3
+    A = torch.randn(4 * H, 2, device=dev) * 0.3
+    Whh = torch.randn(4 * H, H, device=dev) * 0.2
+    bias = torch.randn(4 * H, device=dev) * 0.1
+    h0 = torch.randn(B, H, device=dev) * 0.5
+    Wp = torch.randn(2, H, device=dev) * 0.2
+    bp = torch.randn(2, device=dev) * 0.1
+    h_all = torch.empty(T + 1, B, H, device=dev)
+    c_all = torch.empty(T + 1, B, H, device=dev)
+    act = torch.empty(T, B, 4 * H, device=dev)
+    rel_out = torch.empty(T, B, 2, device=dev)
+    call = lambda: N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0), None,
+                                            N.ptr(Wp), N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all),
+                                            N.ptr(act) if save else None, N.ptr(rel_out), N.stream_ptr()), "lstm")
+    for _ in range(3):
+        call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    flops = 2.0 * T * B * 4 * H * (H + 2)
+    print("lstm_fwd B=%6d T=%2d H=%2d dec=%d save=%d  %8.1f us  %6.1f TF/s (gate GEMM)" % (
+        B, T, H, decoder, save, us, flops / us / 1e6), flush=True)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "pool"
+    if what == "big":     # one config (profiling)
+        run(1280, 20, 32, 8, reps=5)
+        sys.exit(0)
+    if what == "lstm":
+        for B in (1280, 2560, 4096, 25600):
+            for save in (False, True):
+                lstm(B, 8, 32, False, save=save)
+                lstm(B, 12, 32, True, save=save)
+        for B in (1280, 2560):
+            lstm(B, 20, 48, False, save=True)
+        sys.exit(0)
+    run(1280, 20, 32, 8, gpws=(0, 1, 2, 4))
+    run(64, 20, 32, 8, gpws=(0, 1, 2))
+    run(128, 20, 32, 8)
+    run(128, 20, 48, 48)
+    run(256, 57, 32, 8)
