@@ -181,7 +181,10 @@ class _Pool(torch.autograd.Function):
         N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2c), N.ptr(out), N.ptr(am), N.ptr(dout),
                                  N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(dW2p), N.ptr(dAp),
                                  N.stream_ptr()), "sgg_pool_bwd")
-        dh = xw_raw(dU, W1h, None, trans_w=False) if ctx.needs_input_grad[0] else None
+        need = ctx.needs_input_grad
+        dh = xw_raw(dU, W1h, None, trans_w=False) if need[0] else None
+        if not any(need[2:7]):       # weights frozen (the G-step's discriminator): input gradient only
+            return dh, None, None, None, None, None, None, None
         g, dc = xtw(h, dU, colsum=True)                     # (Hd x 512) = dW1h^T, dc = sum_j dU_j
         dW1h = g.t()
         db2 = (dout * (out > 0)).sum(0)
@@ -235,6 +238,8 @@ class _GatAttn(torch.autograd.Function):
         N.check(lib.sgg_gat_bwd(N.ptr(wh), heads, N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, alpha, mode,
                                 epi, max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), HF, N.ptr(dWh), N.ptr(ds), N.ptr(dt),
                                 N.stream_ptr()), "sgg_gat_bwd")
+        if not ctx.needs_input_grad[1] and not has_bias:
+            return dWh, None, None, None, None, None, None, None, None, None, None
         dsdt = torch.cat([ds, dt], 1)                                       # n x [ds_h | dt_h]
         if heads == 1:
             da = xtw(wh, dsdt).t().reshape(ctx.a_shape)
@@ -433,18 +438,22 @@ class _LSTMSeq(torch.autograd.Function):
                                  T, B, H, int(decoder), N.ptr(dG), N.ptr(dh0), N.ptr(drel_in), N.ptr(drel_tot),
                                  N.stream_ptr()), "sgg_lstm_bwd")
         dGf = dG.view(T * B, 4 * H)
-        g, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True)      # (H x 4H), sum dG
-        dWhh = g.t()
+        need = ctx.needs_input_grad
+        dWhh = dbias = dA = dWp = dbp = None
+        if need[2] or need[3]:
+            g, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True)      # (H x 4H), sum dG
+            dWhh = g.t()
+        if need[1]:
+            if decoder:
+                rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0)
+            else:
+                rel_in = rel
+            dA = xtw(rel_in.reshape(T * B, 2), dGf).t()
         if decoder:
-            rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0)
-        else:
-            rel_in = rel
-        dA = xtw(rel_in.reshape(T * B, 2), dGf).t()
-        dWp = dbp = None
-        if decoder:
-            dr = drel_tot.view(T * B, 2)
-            g, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True)
-            dWp = g.t()
+            if need[6] or need[7]:
+                dr = drel_tot.view(T * B, 2)
+                g, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True)
+                dWp = g.t()
             drel = drel_in[0]
         else:
             drel = drel_in

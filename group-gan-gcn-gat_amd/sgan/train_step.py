@@ -234,7 +234,16 @@ class GanTrainer:
             g_l2 = (sl2 / mask_sum).sum()
             terms.append(g_l2)
         fake_last = relative_to_abs(fake_rel_last, obs[-1])
-        scores = D(torch.cat([obs, fake_last], 0), torch.cat([obs_rel, fake_rel_last], 0), sse, scenes=sc)
+        # the reference back-propagates into D's weights here and discards the
+        # result (optimizer_d never sees it, train.py:478-482): freeze them for
+        # this forward so D's backward produces input gradients only
+        for p in self.d_params:
+            p.requires_grad_(False)
+        try:
+            scores = D(torch.cat([obs, fake_last], 0), torch.cat([obs_rel, fake_rel_last], 0), sse, scenes=sc)
+        finally:
+            for p in self.d_params:
+                p.requires_grad_(True)
         y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)
         adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global)    # gan_g_loss
         loss = adv + (terms[0] if terms else 0.0)
