@@ -1,0 +1,97 @@
+// Input-embedding fold of the path's first layers (one launch each way).
+//
+// Every Linear(2, E) embedding of a displacement feeds a linear layer
+// straight away: the LSTM input weights of Encoder/Decoder (reference
+// sgan/models.py:52-59, 121-125; W_ih (4H x E), biases b_ih + b_hh) and the
+// first pooling layer (models.py:477-481, 530-538: W1[:, :E], b1).  Folding
+//   W (We r + be) + b1 (+ b2)  =  A r + bias,   A = W We (R x 2),
+//                                              bias = W be + b1 (+ b2)
+// turns the per-(ped, step) / per-pair embedding into two FMAs.  The fold
+// runs once per forward; its backward maps (dA, dbias) back to
+//   dW = dA We^T + dbias be^T,  dWe = W^T dA,  dbe = W^T dbias,
+//   db1 = db2 = dbias (left to the caller: no copy needed).
+// R <= 512, E <= 128: one workgroup, latency-bound -- the point is one
+// launch instead of the ~3 forward / ~5 backward BLAS + elementwise launches
+// autograd would issue for the same algebra.
+#include "sgg_common.h"
+
+namespace sgg {
+
+__global__ void __launch_bounds__(512) fold_fwd_kernel(const float* __restrict__ W, int ldw, int R, int E,
+                                                       const float* __restrict__ We, const float* __restrict__ be,
+                                                       const float* __restrict__ b1, const float* __restrict__ b2,
+                                                       float* __restrict__ A, float* __restrict__ bias) {
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f, bb = 0.f;
+    const float* w = W + (size_t)r * ldw;
+#pragma unroll 8
+    for (int e = 0; e < E; ++e) {
+      const float we = w[e];
+      a0 = fmaf(we, We[2 * e], a0);
+      a1 = fmaf(we, We[2 * e + 1], a1);
+      bb = fmaf(we, be[e], bb);
+    }
+    A[2 * r] = a0;
+    A[2 * r + 1] = a1;
+    bias[r] = bb + b1[r] + (b2 ? b2[r] : 0.f);
+  }
+}
+
+__global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__ W, int ldw, int R, int E,
+                                                       const float* __restrict__ We, const float* __restrict__ be,
+                                                       const float* __restrict__ dA, const float* __restrict__ dbias,
+                                                       float* __restrict__ dW, int lddw, float* __restrict__ dWe,
+                                                       float* __restrict__ dbe) {
+  // dW: one (r, e) element per thread-iteration
+  for (int q = threadIdx.x; q < R * E; q += blockDim.x) {
+    const int r = q / E, e = q - r * E;
+    dW[(size_t)r * lddw + e] = fmaf(dA[2 * r], We[2 * e], fmaf(dA[2 * r + 1], We[2 * e + 1], dbias[r] * be[e]));
+  }
+  // dWe, dbe: 3E column sums over R rows.  Thread t takes output o = t % 3E
+  // and every rg-th row from t / 3E (rg = blockDim / 3E row groups), then
+  // the row groups are summed in LDS in a fixed order.
+  __shared__ float part[512];
+  const int no = 3 * E;
+  const int rg = blockDim.x / no;
+  if (threadIdx.x < no * rg) {
+    const int o = threadIdx.x % no, g = threadIdx.x / no;
+    const int e = o / 3, j = o - 3 * e;
+    float s = 0.f;
+#pragma unroll 8
+    for (int r = g; r < R; r += rg) {
+      const float gv = j < 2 ? dA[2 * r + j] : dbias[r];
+      s = fmaf(W[(size_t)r * ldw + e], gv, s);
+    }
+    part[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < no) {
+    const int e = threadIdx.x / 3, j = threadIdx.x - 3 * e;
+    float s = 0.f;
+    for (int g = 0; g < rg; ++g) s += part[g * no + threadIdx.x];
+    if (j < 2) dWe[2 * e + j] = s;
+    else dbe[e] = s;
+  }
+}
+
+}  // namespace sgg
+
+using namespace sgg;
+
+extern "C" int sgg_fold_fwd(const float* W, int ldw, int R, int E, const float* We, const float* be, const float* b1,
+                            const float* b2, float* A, float* bias, void* stream) {
+  SGG_CHECK_ARG(W && We && be && b1 && A && bias, "sgg_fold_fwd: null pointer");
+  SGG_CHECK_ARG(R >= 1 && E >= 1 && ldw >= E, "sgg_fold_fwd: bad sizes R=%d E=%d ldw=%d", R, E, ldw);
+  hipLaunchKernelGGL(fold_fwd_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, W, ldw, R, E, We, be, b1, b2, A,
+                     bias);
+  SGG_RETURN_LAUNCH("sgg_fold_fwd");
+}
+
+extern "C" int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be, const float* dA,
+                            const float* dbias, float* dW, int lddw, float* dWe, float* dbe, void* stream) {
+  SGG_CHECK_ARG(W && We && be && dA && dbias && dW && dWe && dbe, "sgg_fold_bwd: null pointer");
+  SGG_CHECK_ARG(R >= 1 && E >= 1 && E <= 128 && ldw >= E && lddw >= E, "sgg_fold_bwd: bad sizes");
+  hipLaunchKernelGGL(fold_bwd_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, W, ldw, R, E, We, be, dA, dbias,
+                     dW, lddw, dWe, dbe);
+  SGG_RETURN_LAUNCH("sgg_fold_bwd");
+}

@@ -52,7 +52,7 @@ struct PoolCfg {
 template <int BN, int GPW>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
-    const float* __restrict__ W2T /* 512 x BN */, const float* __restrict__ b2,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
     const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
     float* __restrict__ out, int32_t* __restrict__ argmax) {
   using C = PoolCfg<BN>;
@@ -111,10 +111,10 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
         if (r < n) ureg[e] = *reinterpret_cast<const float4*>(U + (size_t)(o + r) * kHidden + k0 + 4 * c4);
       }
 #pragma unroll
-      for (int e = 0; e < kWQ; ++e) {
-        const int q = threadIdx.x + 256 * e;
+      for (int e = 0; e < kWQ; ++e) {   // W2 (BN x 512, nn.Linear layout), read transposed:
+        const int q = threadIdx.x + 256 * e;   // c fastest, so the LDS stores below are conflict-free
         const int kk = q / BNP, cc = q - kk * BNP;
-        wreg[e] = (kk < kKT && cc < BN) ? W2T[(size_t)(k0 + kk) * BN + cc] : 0.f;
+        wreg[e] = (kk < kKT && cc < BN) ? W2[(size_t)cc * kHidden + k0 + kk] : 0.f;
       }
       if (threadIdx.x < 2 * kKT) areg = A[2 * k0 + threadIdx.x];
     };
@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
         }
       }
 #pragma unroll
-      for (int e = 0; e < kWQ; ++e) {
+      for (int e = 0; e < kWQ; ++e) {   // the W2^T tile
         const int q = threadIdx.x + 256 * e;
         if (q < kKT * BNP) W2s[q] = wreg[e];
       }
@@ -298,12 +298,12 @@ static size_t pool_fwd_lds(int max_rows) {
 }
 
 template <int BN, int GPW>
-static void launch_fwd_g(const float* U, const float* pos, const float* A, const float* W2T, const float* b2,
+static void launch_fwd_g(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
                          const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, float* out,
                          int32_t* am, hipStream_t st) {
   const int grid = nchunks < 65536 ? nchunks : 65536;
   hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW>), dim3(grid), dim3(256), pool_fwd_lds<BN>(max_rows), st, U, pos, A,
-                     W2T, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, out, am);
+                     W2, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, out, am);
 }
 static size_t pool_bwd_lds(int bn, int max_n) {
   return (size_t)bn * kHidden * 4 + (size_t)max_n * bn * 12 + (size_t)(((max_n + 2) & ~1) * 4) +
@@ -311,14 +311,14 @@ static size_t pool_bwd_lds(int bn, int max_n) {
 }
 
 template <int BN>
-static int launch_fwd(const float* U, const float* pos, const float* A, const float* W2T, const float* b2,
+static int launch_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
                       const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, int gpw, float* out,
                       int32_t* am, hipStream_t st) {
   switch (gpw) {
-    case 1: launch_fwd_g<BN, 1>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
-    case 2: launch_fwd_g<BN, 2>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
-    case 4: launch_fwd_g<BN, 4>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
-    default: launch_fwd_g<BN, 8>(U, pos, A, W2T, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    case 1: launch_fwd_g<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    case 2: launch_fwd_g<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    case 4: launch_fwd_g<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    default: launch_fwd_g<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
   }
   SGG_RETURN_LAUNCH("sgg_pool_fwd");
 }
@@ -390,10 +390,10 @@ extern "C" int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int t
   return nc;
 }
 
-extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2T, const float* b2,
+extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
                             const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
                             int B, int bn, int max_n, float* out, int32_t* argmax, void* stream) {
-  SGG_CHECK_ARG(U && pos && A && W2T && b2 && scene_off && chunks && out && argmax, "sgg_pool_fwd: null pointer");
+  SGG_CHECK_ARG(U && pos && A && W2 && b2 && scene_off && chunks && out && argmax, "sgg_pool_fwd: null pointer");
   SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_fwd: bottleneck %d not built (8/16/32/48/64)", bn);
   SGG_CHECK_ARG(nchunks >= 0 && B >= 0, "sgg_pool_fwd: bad sizes");
   SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "sgg_pool_fwd: max scene size %d outside [1, %d]",
@@ -403,11 +403,11 @@ extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, co
   if (nchunks == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (bn) {
-    case 8: return launch_fwd<8>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    case 16: return launch_fwd<16>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    case 32: return launch_fwd<32>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    case 48: return launch_fwd<48>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    default: return launch_fwd<64>(U, pos, A, W2T, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 8: return launch_fwd<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 16: return launch_fwd<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 32: return launch_fwd<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 48: return launch_fwd<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    default: return launch_fwd<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
   }
 }
 

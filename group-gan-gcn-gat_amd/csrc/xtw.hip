@@ -91,21 +91,33 @@ __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restric
   }
 }
 
-// slab sum: block = 64 outputs x 4 split phases; fixed order -> deterministic
+// slab sum: block = 64 outputs x 4 split phases; fixed order -> deterministic.
+// The split loop is unrolled 8-wide so its loads are in flight together (the
+// partial slabs were just written: L2 hits, latency- not bandwidth-bound).
 __global__ void __launch_bounds__(256) xtw_reduce_kernel(const float* __restrict__ slab, int splits, int MN,
-                                                         float* __restrict__ C, int N, int ldc) {
+                                                         float* __restrict__ C, int N, int ldc, int trans_c) {
   __shared__ float part[4][64];
   const int el = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + el;
   float s = 0.f;
-  if (e < MN)
-    for (int k = ph; k < splits; k += 4) s += slab[(size_t)k * MN + e];
+  if (e < MN) {
+    int k = ph;
+    for (; k + 28 < splits; k += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(size_t)(k + 4 * u) * MN + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < splits; k += 4) s += slab[(size_t)k * MN + e];
+  }
   part[ph][el] = s;
   __syncthreads();
   if (ph == 0 && e < MN) {
     const float v = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
     const int mm = e / N, n = e - mm * N;
-    C[(size_t)mm * ldc + n] = v;
+    if (trans_c) C[(size_t)n * ldc + mm] = v;
+    else C[(size_t)mm * ldc + n] = v;
   }
 }
 
@@ -114,17 +126,24 @@ __global__ void __launch_bounds__(256) xtw_reduce_kernel(const float* __restrict
 using namespace sgg;
 
 extern "C" int sgg_xtw_splits(int R, int M, int N) {
+  // ~32 rows per split (two 16-row MFMA steps: the partial kernel is one or
+  // two load latencies long), capped by the grid (<= 4096 workgroups) and
+  // by the slab (<= 2^21 floats, so the reduce stays an L2-resident pass)
   const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
-  int splits = (1024 + tiles - 1) / tiles;
-  const int max_by_rows = (R + 127) / 128;  // >= 128 rows per split
-  if (splits > max_by_rows) splits = max_by_rows;
-  return splits < 1 ? 1 : splits;
+  const long long mn = (long long)M * N;
+  long long splits = (R + 31) / 32;
+  const long long by_grid = 4096 / tiles > 0 ? 4096 / tiles : 1;
+  const long long by_slab = (1ll << 21) / mn > 0 ? (1ll << 21) / mn : 1;
+  if (splits > by_grid) splits = by_grid;
+  if (splits > by_slab) splits = by_slab;
+  return splits < 1 ? 1 : (int)splits;
 }
 
 extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, int M, int N, float* C, int ldc,
-                       float* colsum, float* ws, size_t ws_bytes, void* stream) {
+                       int trans_c, float* colsum, float* ws, size_t ws_bytes, void* stream) {
   SGG_CHECK_ARG((R == 0 || (X && Y)) && C && ws, "sgg_xtw: null pointer");
-  SGG_CHECK_ARG(R >= 0 && M > 0 && N > 0 && ldx >= M && ldy >= N && ldc >= N, "sgg_xtw: bad sizes");
+  SGG_CHECK_ARG(R >= 0 && M > 0 && N > 0 && ldx >= M && ldy >= N && ldc >= (trans_c ? M : N),
+                "sgg_xtw: bad sizes");
   const int splits = sgg_xtw_splits(R, M, N);
   const size_t need = sizeof(float) * (size_t)splits * ((size_t)M * N + N);
   SGG_CHECK_ARG(ws_bytes >= need, "sgg_xtw: workspace %zu < %zu bytes", ws_bytes, need);
@@ -135,8 +154,8 @@ extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, 
   hipLaunchKernelGGL(xtw_partial_kernel, grid, dim3(256), 0, st, X, ldx, Y, ldy, R, M, N, rps, ws,
                      colsum ? colslab : nullptr);
   const int MN = M * N;
-  hipLaunchKernelGGL(xtw_reduce_kernel, dim3((MN + 63) / 64), dim3(256), 0, st, ws, splits, MN, C, N, ldc);
+  hipLaunchKernelGGL(xtw_reduce_kernel, dim3((MN + 63) / 64), dim3(256), 0, st, ws, splits, MN, C, N, ldc, trans_c);
   if (colsum)
-    hipLaunchKernelGGL(xtw_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, st, colslab, splits, N, colsum, N, N);
+    hipLaunchKernelGGL(xtw_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, st, colslab, splits, N, colsum, N, N, 0);
   SGG_RETURN_LAUNCH("sgg_xtw");
 }

@@ -5,23 +5,18 @@
 //   B lane map: B[l >> 4][l & 15]    (4 k x 16 cols)
 //   C/D map   : row = (l >> 4) * 4 + r, col = l & 15   (r = 0..3)
 // Workgroup = 4 waves = 64 rows x 64 cols of Y; each wave owns 16 rows x 64
-// cols (4 accumulator tiles).  K is small on this path (32..144, 512 for the
+// cols (4 accumulator tiles).  K is small on this path (2..144, 512 for the
 // pooling backward), so operands are read straight from L1/L2: the X row
 // fragment is reused across the 4 column tiles in registers, the W fragment
-// is shared by the 4 waves through L1.
+// is shared by the 4 waves through L1.  These launches are latency-bound
+// (a few dozen workgroups), hence the deep register prefetch below.
 #include "sgg_common.h"
 
 namespace sgg {
 
 template <bool TRANS_W>
-__device__ __forceinline__ float load_w(const float* __restrict__ W, int k, int n, int K, int N) {
-  if (k >= K || n >= N) return 0.f;
-  return TRANS_W ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
-}
-
-template <bool TRANS_W>
 __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, int ldx,
-                                                 const float* __restrict__ W,
+                                                 const float* __restrict__ W, int ldw,
                                                  const float* __restrict__ bias, float* __restrict__ Y,
                                                  int ldy, int M, int K, int N, int act) {
   const int lane = threadIdx.x & 63;
@@ -38,55 +33,42 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const bool full_n = col0 + 64 <= N;
-  int k0 = 0;
-  // main loop: 4 MFMA k-steps (16 k) per iteration, no k bounds checks; the
-  // next 16 k of both operands are loaded while the current ones compute
-  auto load16 = [&](int kb, float (&aa)[4], float (&bb)[4][4]) {
+  // K is walked in 32-deep chunks (8 MFMA k-steps), double-buffered in
+  // registers: the next chunk's loads are all in flight while the current
+  // chunk computes, so a K <= 144 transform costs ~K/32 load latencies
+  // instead of one per 4-deep step.  Out-of-range k / n read as 0 (adds 0).
+  constexpr int KC = 32, S4 = KC / 4;
+  auto load_chunk = [&](int kb, float (&aa)[S4], float (&bb)[S4][4]) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < S4; ++s) {
       const int k = kb + 4 * s + kq;
-      aa[s] = arow_ok ? xrow[k] : 0.f;
+      const bool kok = k < K;
+      aa[s] = (arow_ok && kok) ? xrow[k] : 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int n = col0 + 16 * t + ar;
-        if (full_n) bb[s][t] = TRANS_W ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
-        else bb[s][t] = load_w<TRANS_W>(W, k, n, K, N);
+        bb[s][t] = (kok && n < N) ? (TRANS_W ? W[(size_t)n * ldw + k] : W[(size_t)k * ldw + n]) : 0.f;
       }
     }
   };
-  if (K >= 16) {
-    float a[4], b[4][4], an[4], bn[4][4];
-    load16(0, a, b);
-    for (; k0 + 16 <= K; k0 += 16) {
-      const bool more = k0 + 32 <= K;
-      if (more) load16(k0 + 16, an, bn);
+  float a0[S4], b0[S4][4], a1[S4], b1[S4][4];
+  load_chunk(0, a0, b0);
+  for (int k0 = 0; k0 < K; k0 += 2 * KC) {
+    if (k0 + KC < K) load_chunk(k0 + KC, a1, b1);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < S4; ++s)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
-      if (more) {
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b0[s][t], acc[t], 0, 0, 0);
+    if (k0 + KC >= K) break;
+    if (k0 + 2 * KC < K) load_chunk(k0 + 2 * KC, a0, b0);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          a[s] = an[s];
+    for (int s = 0; s < S4; ++s)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) b[s][t] = bn[s][t];
-        }
-      }
-    }
-  }
-  // tail: k bounds-checked
-  for (; k0 < K; k0 += 4) {
-    const int k = k0 + kq;
-    const float a = (arow_ok && k < K) ? xrow[k] : 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float b = load_w<TRANS_W>(W, k, col0 + 16 * t + ar, K, N);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
-    }
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], b1[s][t], acc[t], 0, 0, 0);
   }
 
-  // epilogue
+  // epilogue (direct stores: an LDS-staged full-row variant measured slower,
+  // 67 vs 42 us on the 25600 x 512 pooling U -- L2 merges the 64-B pieces)
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int n = col0 + 16 * t + ar;
@@ -106,18 +88,19 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
 
 }  // namespace sgg
 
-extern "C" int sgg_xw(const float* X, int ldx, const float* W, int trans_w, const float* bias,
+extern "C" int sgg_xw(const float* X, int ldx, const float* W, int ldw, int trans_w, const float* bias,
                       float* Y, int ldy, int M, int K, int N, int act, void* stream) {
   SGG_CHECK_ARG(X && W && Y, "sgg_xw: null pointer");
   SGG_CHECK_ARG(M >= 0 && K > 0 && N > 0, "sgg_xw: bad sizes M=%d K=%d N=%d", M, K, N);
-  SGG_CHECK_ARG(ldx >= K && ldy >= N, "sgg_xw: bad leading dims ldx=%d ldy=%d", ldx, ldy);
+  SGG_CHECK_ARG(ldx >= K && ldy >= N && ldw >= (trans_w ? K : N), "sgg_xw: bad leading dims ldx=%d ldw=%d ldy=%d",
+                ldx, ldw, ldy);
   SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw: act must be 0 or 1");
   if (M == 0) return 0;
   dim3 grid((M + 63) / 64, (N + 63) / 64);
   hipStream_t s = (hipStream_t)stream;
   if (trans_w)
-    hipLaunchKernelGGL(sgg::xw_kernel<true>, grid, dim3(256), 0, s, X, ldx, W, bias, Y, ldy, M, K, N, act);
+    hipLaunchKernelGGL(sgg::xw_kernel<true>, grid, dim3(256), 0, s, X, ldx, W, ldw, bias, Y, ldy, M, K, N, act);
   else
-    hipLaunchKernelGGL(sgg::xw_kernel<false>, grid, dim3(256), 0, s, X, ldx, W, bias, Y, ldy, M, K, N, act);
+    hipLaunchKernelGGL(sgg::xw_kernel<false>, grid, dim3(256), 0, s, X, ldx, W, ldw, bias, Y, ldy, M, K, N, act);
   SGG_RETURN_LAUNCH("sgg_xw");
 }

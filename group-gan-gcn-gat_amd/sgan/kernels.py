@@ -34,8 +34,10 @@ def _rows(t, name):
 # dense node transform
 # ---------------------------------------------------------------------------
 def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None):
+    """act(x @ W + bias); W = w (K x N) or w^T (w stored N x K, trans_w).  w
+    may be a row-strided column block (e.g. W1[:, E:]), passed in place."""
     x = _rows(x, "x")
-    w = _req(w, "w").contiguous()
+    w = _rows(w, "w")
     M, K = x.shape
     Nn = w.shape[0] if trans_w else w.shape[1]
     assert (w.shape[1] if trans_w else w.shape[0]) == K, (x.shape, w.shape, trans_w)
@@ -43,30 +45,65 @@ def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None):
         bias = _req(bias, "bias").contiguous()
         assert bias.numel() == Nn
     y = out if out is not None else torch.empty(M, Nn, device=x.device, dtype=torch.float32)
-    N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(w), int(bool(trans_w)), N.ptr(bias), N.ptr(y), y.stride(0),
-                          M, K, Nn, int(act), N.stream_ptr()), "sgg_xw")
+    N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(w), w.stride(0), int(bool(trans_w)), N.ptr(bias), N.ptr(y),
+                          y.stride(0), M, K, Nn, int(act), N.stream_ptr()), "sgg_xw")
     return y
 
 
-def xtw(X, Y, colsum=False):
-    """C = X^T Y (+ column sums of Y) with the split-K MFMA reduction
-    (sgg_xtw); X: R x M, Y: R x N, row-strided 2-D views allowed."""
+def xtw(X, Y, colsum=False, trans_c=False, out=None):
+    """C = X^T Y (M x N), or C^T (N x M) with trans_c, plus the column sums of
+    Y, with the split-K MFMA reduction (sgg_xtw).  X: R x M, Y: R x N,
+    row-strided 2-D views allowed; `out` (row-strided, unit column stride)
+    receives C in place."""
     lib = _lib()
     X = _rows(X, "X")
     Y = _rows(Y, "Y")
     R, M = X.shape
     Nn = Y.shape[1]
     assert Y.shape[0] == R
+    shape = (Nn, M) if trans_c else (M, Nn)
+    if out is None:
+        C = torch.empty(shape, device=X.device, dtype=torch.float32)
+    else:
+        assert tuple(out.shape) == shape and out.stride(1) == 1, (out.shape, shape)
+        C = out
     if R == 0:
-        C = torch.zeros(M, Nn, device=X.device, dtype=torch.float32)
+        C.zero_()
         return (C, torch.zeros(Nn, device=X.device)) if colsum else C
     splits = lib.sgg_xtw_splits(R, M, Nn)
     ws = torch.empty(splits * (M * Nn + Nn), device=X.device, dtype=torch.float32)
-    C = torch.empty(M, Nn, device=X.device, dtype=torch.float32)
     cs = torch.empty(Nn, device=X.device, dtype=torch.float32) if colsum else None
-    N.check(lib.sgg_xtw(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), R, M, Nn, N.ptr(C), Nn, N.ptr(cs), N.ptr(ws),
-                        ws.numel() * 4, N.stream_ptr()), "sgg_xtw")
+    N.check(lib.sgg_xtw(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), R, M, Nn, N.ptr(C), C.stride(0), int(trans_c),
+                        N.ptr(cs), N.ptr(ws), ws.numel() * 4, N.stream_ptr()), "sgg_xtw")
     return (C, cs) if colsum else C
+
+
+# ---------------------------------------------------------------------------
+# input-embedding fold (sgg_fold_fwd / sgg_fold_bwd)
+# ---------------------------------------------------------------------------
+def fold_fwd(W, We, be, b1, b2=None):
+    """A = W We (R x 2), bias = W be + b1 (+ b2); W may be a column block."""
+    W = _rows(W, "W")
+    R, E = W.shape
+    A = torch.empty(R, 2, device=W.device, dtype=torch.float32)
+    bias = torch.empty(R, device=W.device, dtype=torch.float32)
+    N.check(_lib().sgg_fold_fwd(N.ptr(W), W.stride(0), R, E, N.ptr(We.contiguous()), N.ptr(be.contiguous()),
+                                N.ptr(b1.contiguous()), N.ptr(b2.contiguous() if b2 is not None else None), N.ptr(A),
+                                N.ptr(bias), N.stream_ptr()), "sgg_fold_fwd")
+    return A, bias
+
+
+def fold_bwd(W, We, be, dA, dbias, dW=None):
+    """(dW, dWe, dbe) of fold_fwd; dW may be a preallocated column block."""
+    W = _rows(W, "W")
+    R, E = W.shape
+    dW = dW if dW is not None else torch.empty(R, E, device=W.device, dtype=torch.float32)
+    dWe = torch.empty(E, 2, device=W.device, dtype=torch.float32)
+    dbe = torch.empty(E, device=W.device, dtype=torch.float32)
+    N.check(_lib().sgg_fold_bwd(N.ptr(W), W.stride(0), R, E, N.ptr(We.contiguous()), N.ptr(be.contiguous()),
+                                N.ptr(dA.contiguous()), N.ptr(dbias.contiguous()), N.ptr(dW), dW.stride(0), N.ptr(dWe),
+                                N.ptr(dbe), N.stream_ptr()), "sgg_fold_bwd")
+    return dW, dWe, dbe
 
 
 class _XW(torch.autograd.Function):
@@ -87,8 +124,8 @@ class _XW(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = xw_raw(dy, w, None, not ctx.trans_w, 0)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            g, cs = xtw(x, dy, colsum=True)                 # (K x N) = X^T dY, colsum = sum dY
-            dw = g.t() if ctx.trans_w else g
+            # X^T dY (K x N); nn.Linear-layout weights take it transposed (N x K)
+            dw, cs = xtw(x, dy, colsum=True, trans_c=ctx.trans_w)
             db = cs if ctx.has_bias else None
         return dx, dw, db, None, None
 
@@ -135,65 +172,75 @@ def _pool_flops(scenes, bn):
 
 
 class _Pool(torch.autograd.Function):
+    """PoolHiddenNet on raw parameters: W1 (512 x (E + Hd)) = [W1e | W1h], the
+    spatial embedding (We, be), b1, W2 (bn x 512), b2.  Forward: one fold
+    launch (A = W1e We, c = W1e be + b1), U = h W1h^T + c (sgg_xw on the W1h
+    block in place), the fused pooling kernel.  Backward: the pooling
+    backward, dW1 assembled in place (fold backward -> left block, X^T dU
+    transposed -> right block)."""
+
     @staticmethod
-    def forward(ctx, h, pos, W1h, A, c, W2, b2, scenes):
+    def forward(ctx, h, pos, W1, We, be, b1, W2, b2, scenes):
         lib = _lib()
         h = _rows(h, "h")
         pos = _req(pos, "pos").contiguous()
-        B = h.shape[0]
+        B, Hd = h.shape
+        E = We.shape[0]
         bn = W2.shape[0]
         assert pos.shape == (B, 2) and scenes.B == B, (pos.shape, B, scenes.B)
-        W1h = W1h.contiguous()
-        U = xw_raw(h, W1h, c, trans_w=True)                       # B x 512
+        assert W1.shape == (512, E + Hd), (W1.shape, E, Hd)
+        W1 = W1.contiguous()
+        W2 = W2.contiguous()
+        b2 = b2.contiguous()
+        A, c = fold_fwd(W1[:, :E], We, be, b1)
+        U = xw_raw(h, W1[:, E:], c, trans_w=True)                 # B x 512
         out = torch.empty(B, bn, device=h.device, dtype=torch.float32)
         am = torch.empty(B, bn, device=h.device, dtype=torch.int32)
-        W2T = W2.t().contiguous()
-        A = A.contiguous()
-        b2 = b2.contiguous()
         timed = pool_timer.active
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         chunks, nchunks, max_rows, gpw = scenes.pool_plan(bn)
-        N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2T), N.ptr(b2), N.ptr(scenes.scene_off),
+        N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(scenes.scene_off),
                                  N.ptr(chunks), nchunks, max_rows, gpw, B, bn, scenes.max_n, N.ptr(out), N.ptr(am),
                                  N.stream_ptr()), "sgg_pool_fwd")
         if timed:
             e1.record()
             pool_timer.rec.append((bn, _pool_flops(scenes, bn), e0, e1))
         ctx.scenes = scenes
-        ctx.save_for_backward(h, pos, W1h, A, W2, U, out, am)
+        ctx.E = E
+        ctx.save_for_backward(h, pos, W1, We, be, A, W2, U, out, am)
         ctx.mark_non_differentiable(am)
         return out, am
 
     @staticmethod
     def backward(ctx, dout, _dam):
         lib = _lib()
-        h, pos, W1h, A, W2, U, out, am = ctx.saved_tensors
-        sc = ctx.scenes
+        h, pos, W1, We, be, A, W2, U, out, am = ctx.saved_tensors
+        sc, E = ctx.scenes, ctx.E
         B, bn = out.shape
         dout = dout.contiguous()
         grid = lib.sgg_pool_bwd_grid(sc.S)
         dU = torch.empty(B, 512, device=h.device, dtype=torch.float32)
         dW2p = torch.empty(grid, bn, 512, device=h.device, dtype=torch.float32)
         dAp = torch.empty(grid, 512, 2, device=h.device, dtype=torch.float32)
-        W2c = W2.contiguous()
-        N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2c), N.ptr(out), N.ptr(am), N.ptr(dout),
+        N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(out), N.ptr(am), N.ptr(dout),
                                  N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(dW2p), N.ptr(dAp),
                                  N.stream_ptr()), "sgg_pool_bwd")
         need = ctx.needs_input_grad
-        dh = xw_raw(dU, W1h, None, trans_w=False) if need[0] else None
-        if not any(need[2:7]):       # weights frozen (the G-step's discriminator): input gradient only
-            return dh, None, None, None, None, None, None, None
-        g, dc = xtw(h, dU, colsum=True)                     # (Hd x 512) = dW1h^T, dc = sum_j dU_j
-        dW1h = g.t()
+        dh = xw_raw(dU, W1[:, E:], None, trans_w=False) if need[0] else None
+        if not any(need[2:8]):       # weights frozen (the G-step's discriminator): input gradient only
+            return dh, None, None, None, None, None, None, None, None
+        dW1 = torch.empty_like(W1)
+        _, dc = xtw(h, dU, colsum=True, trans_c=True, out=dW1[:, E:])   # dW1h = dU^T h, dc = sum_j dU_j
+        _, dWe, dbe = fold_bwd(W1[:, :E], We, be, dAp.sum(0), dc, dW=dW1[:, :E])
         db2 = (dout * (out > 0)).sum(0)
-        return dh, None, dW1h, dAp.sum(0), dc, dW2p.sum(0), db2, None
+        return dh, None, dW1, dWe, dbe, dc, dW2p.sum(0), db2, None
 
 
-def social_pool(h, pos, W1h, A, c, W2, b2, scenes):
+def social_pool(h, pos, W1, We, be, b1, W2, b2, scenes):
     """PoolHiddenNet core (models.py:497-549) -> (B, bn); see sgg_pool_fwd."""
-    out, _ = _Pool.apply(h, pos, W1h, A, c, W2, b2, scenes)
+    out, _ = _Pool.apply(h, pos, W1, We, be, b1, W2, b2, scenes)
     return out
 
 
@@ -392,27 +439,34 @@ def scene_mean_over_groups(gx, groups):
 # fused LSTM sequences (encoder / decoder rollout)
 # ---------------------------------------------------------------------------
 class _LSTMSeq(torch.autograd.Function):
+    """Fused LSTM sequence on the raw parameters of Linear(2, E) + LSTM(E, H)
+    (+ hidden2pos for the decoder): the embedding fold is one launch
+    (sgg_fold_fwd), the T-step recurrence another; the backward returns
+    the raw parameters' gradients (sgg_fold_bwd maps dA, dbias back)."""
+
     @staticmethod
-    def forward(ctx, rel, A, Whh, bias, h0, c0, Wp, bp, decoder, T, save):
+    def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save):
         lib = _lib()
         rel = _req(rel, "rel").contiguous()
-        H = Whh.shape[1]
+        H = W_hh.shape[1]
         B = rel.shape[-2]
         dev = rel.device
+        A, bias = fold_fwd(W_ih, We, be, b_ih, b_hh)
         h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
         c_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
         act = torch.empty(T, B, 4 * H, device=dev, dtype=torch.float32) if save else None
         rel_out = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
-        A, Whh, bias = A.contiguous(), Whh.contiguous(), bias.contiguous()
+        Whh = W_hh.contiguous()
         h0c = h0.contiguous() if h0 is not None else None
         c0c = c0.contiguous() if c0 is not None else None
         Wpc = Wp.contiguous() if Wp is not None else None
-        N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), N.ptr(Wpc), N.ptr(bp),
-                                 T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out),
-                                 N.stream_ptr()), "sgg_lstm_fwd")
+        N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), N.ptr(Wpc),
+                                 N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
+                                 N.ptr(rel_out), N.stream_ptr()), "sgg_lstm_fwd")
         ctx.meta = (decoder, T, B, H, h0 is not None)
+        ctx.set_materialize_grads(False)   # unused outputs (the decoder's h_last) get None, not a zero fill
         if save:
-            ctx.save_for_backward(rel, A, Whh, Wpc, h_all, c_all, act, rel_out)
+            ctx.save_for_backward(rel, W_ih, We, be, A, Whh, Wpc, h_all, c_all, act, rel_out)
         h_last = h_all[T]
         if decoder:
             return h_last, rel_out
@@ -422,7 +476,7 @@ class _LSTMSeq(torch.autograd.Function):
     def backward(ctx, dh_last, drel_out):
         lib = _lib()
         decoder, T, B, H, has_h0 = ctx.meta
-        rel, A, Whh, Wp, h_all, c_all, act, rel_out = ctx.saved_tensors
+        rel, W_ih, We, be, A, Whh, Wp, h_all, c_all, act, rel_out = ctx.saved_tensors
         dev = rel.device
         dG = torch.empty(T, B, 4 * H, device=dev, dtype=torch.float32)
         drel_in = torch.empty(T, B, 2, device=dev, dtype=torch.float32)
@@ -439,35 +493,38 @@ class _LSTMSeq(torch.autograd.Function):
                                  N.stream_ptr()), "sgg_lstm_bwd")
         dGf = dG.view(T * B, 4 * H)
         need = ctx.needs_input_grad
-        dWhh = dbias = dA = dWp = dbp = None
-        if need[2] or need[3]:
-            g, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True)      # (H x 4H), sum dG
-            dWhh = g.t()
-        if need[1]:
-            if decoder:
-                rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0)
-            else:
-                rel_in = rel
-            dA = xtw(rel_in.reshape(T * B, 2), dGf).t()
+        dW_ih = dW_hh = db_ih = db_hh = dWe = dbe = dWp = dbp = None
+        if any(need[1:7]):
+            # dW_hh = dG^T h_{t-1} (4H x H, transposed reduction), dbias = sum dG
+            dW_hh, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True, trans_c=True)
+            rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0) if decoder else rel
+            dA = xtw(rel_in.reshape(T * B, 2), dGf, trans_c=True)                   # 4H x 2
+            dW_ih, dWe, dbe = fold_bwd(W_ih, We, be, dA, dbias)
+            db_ih, db_hh = dbias, dbias.clone()     # two leaves: no shared gradient storage
         if decoder:
-            if need[6] or need[7]:
+            if need[9] or need[10]:
                 dr = drel_tot.view(T * B, 2)
-                g, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True)
-                dWp = g.t()
+                dWp, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True, trans_c=True)
             drel = drel_in[0]
         else:
             drel = drel_in
-        return drel, dA, dWhh, dbias, (dh0 if has_h0 else None), None, dWp, dbp, None, None, None
+        return (drel, dW_ih, dW_hh, db_ih, db_hh, dWe, dbe, (dh0 if has_h0 else None), None, dWp, dbp,
+                None, None, None)
 
 
-def lstm_sequence(rel, A, Whh, bias, h0=None, c0=None, Wp=None, bp=None, decoder=False, T=None):
-    """Fused LSTM over T steps (see sgg_lstm_fwd).  Returns (h_last, rel_out)."""
+def lstm_sequence(rel, lstm, emb, h0=None, c0=None, proj=None, decoder=False, T=None):
+    """Fused Linear(2, E) + 1-layer LSTM over T steps (see sgg_lstm_fwd);
+    `proj` is the decoder's hidden2pos.  Returns (h_last, rel_out)."""
     T = T if T is not None else rel.shape[0]
-    save = torch.is_grad_enabled() and any(
-        t is not None and t.requires_grad for t in (rel, A, Whh, bias, h0, Wp, bp))
+    W_ih, W_hh, b_ih, b_hh = lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0
+    Wp = proj.weight if proj is not None else None
+    bp = proj.bias if proj is not None else None
+    ins = (rel, W_ih, W_hh, b_ih, b_hh, emb.weight, emb.bias, h0, Wp, bp)
+    save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ins)
     if c0 is not None and c0.requires_grad and torch.is_grad_enabled():
         raise NotImplementedError("gradient w.r.t. the initial cell state")
-    h_last, rel_out = _LSTMSeq.apply(rel, A, Whh, bias, h0, c0, Wp, bp, bool(decoder), T, save)
+    h_last, rel_out = _LSTMSeq.apply(rel, W_ih, W_hh, b_ih, b_hh, emb.weight, emb.bias, h0, c0, Wp, bp,
+                                     bool(decoder), T, save)
     return h_last, (rel_out if decoder else None)
 
 

@@ -106,14 +106,6 @@ def get_noise(shape, noise_type):
 # ---------------------------------------------------------------------------
 # encoder / decoder (models.py:32-178) -> sgg_lstm_fwd / sgg_lstm_bwd
 # ---------------------------------------------------------------------------
-def _fold_embedding(lstm, emb):
-    """Input weights of a 1-layer LSTM fed by Linear(2, E): A = W_ih We (4H x 2),
-    b = W_ih be + b_ih + b_hh (torch ops: autograd carries their gradients)."""
-    W_ih = lstm.weight_ih_l0
-    A = W_ih.mm(emb.weight)
-    b = torch.addmv(lstm.bias_ih_l0 + lstm.bias_hh_l0, W_ih, emb.bias)
-    return A, b
-
 class Encoder(nn.Module):
     def __init__(self, embedding_dim=64, h_dim=64, mlp_dim=1024, num_layers=1, dropout=0.0):
         super().__init__()
@@ -129,8 +121,7 @@ class Encoder(nn.Module):
         folded into the input weights (A = W_ih We, b = W_ih be + b_ih + b_hh)."""
         if self.num_layers != 1:
             raise NotImplementedError("fused LSTM kernel: num_layers must be 1 (all reference configs)")
-        A, b = _fold_embedding(self.encoder, self.spatial_embedding)
-        h, _ = K.lstm_sequence(obs_traj, A, self.encoder.weight_hh_l0, b)
+        h, _ = K.lstm_sequence(obs_traj, self.encoder, self.spatial_embedding)
         return h.unsqueeze(0)
 
 
@@ -159,11 +150,10 @@ class Decoder(nn.Module):
         if not self.pool_every_timestep:
             # the whole 12-step rollout (LSTM step -> hidden2pos -> embedding
             # of the predicted displacement) is one sgg_lstm_fwd launch
-            A, b = _fold_embedding(self.decoder, self.spatial_embedding)
             h0, c0 = state_tuple
-            h, rel = K.lstm_sequence(last_pos_rel, A, self.decoder.weight_hh_l0, b, h0=h0[0], c0=c0[0],
-                                     Wp=self.hidden2pos.weight, bp=self.hidden2pos.bias, decoder=True,
-                                     T=self.seq_len)
+            h, rel = K.lstm_sequence(last_pos_rel, self.decoder, self.spatial_embedding, h0=h0[0],
+                                     c0=c0[0] if c0 is not None else None,
+                                     proj=self.hidden2pos, decoder=True, T=self.seq_len)
             return rel, h.unsqueeze(0)
         B = last_pos.size(0)
         x = K.linear(last_pos_rel, self.spatial_embedding).view(1, B, self.embedding_dim)
@@ -189,7 +179,8 @@ class Decoder(nn.Module):
 class PoolHiddenNet(nn.Module):
     """Pooling module as proposed in Social-GAN.  The pair MLP runs fused in
     sgg_pool_fwd; the spatial embedding is folded into the first layer
-    (A = W1e We, c = W1e be + b1) so autograd carries its gradients."""
+    (A = W1e We, c = W1e be + b1, sgg_fold_fwd) inside the autograd op, which
+    returns the raw parameters' gradients."""
 
     def __init__(self, embedding_dim=64, h_dim=64, mlp_dim=1024, bottleneck_dim=1024, activation="relu",
                  batch_norm=True, dropout=0.0):
@@ -208,12 +199,10 @@ class PoolHiddenNet(nn.Module):
             raise NotImplementedError("the fused pooling kernel implements the reference configs "
                                       "(batch_norm=0, relu, dropout=0)")
         sc = _scenes(seq_start_end, end_pos.device, scenes)
-        E = self.embedding_dim
         l1, l2 = self.mlp_pre_pool[0], self.mlp_pre_pool[2]
-        W1e, W1h = l1.weight[:, :E], l1.weight[:, E:]
-        A = W1e.mm(self.spatial_embedding.weight)                   # 512 x 2
-        c = torch.addmv(l1.bias, W1e, self.spatial_embedding.bias)  # 512
-        return K.social_pool(h_states.reshape(-1, self.h_dim), end_pos, W1h, A, c, l2.weight, l2.bias, sc)
+        emb = self.spatial_embedding
+        return K.social_pool(h_states.reshape(-1, self.h_dim), end_pos, l1.weight, emb.weight, emb.bias, l1.bias,
+                             l2.weight, l2.bias, sc)
 
 
 # ---------------------------------------------------------------------------
@@ -511,7 +500,10 @@ class TrajectoryGenerator(nn.Module):
         else:
             noise_input = ctx
         decoder_h = self.add_noise(noise_input, seq_start_end, user_noise=user_noise, scenes=sc).unsqueeze(0)
-        decoder_c = torch.zeros(self.num_layers, batch, self.decoder_h_dim, device=obs_traj.device)
+        # c0 = 0 (models.py:912): the fused decoder takes a NULL initial cell
+        # state as zeros; the per-step fallback needs the tensor
+        decoder_c = (torch.zeros(self.num_layers, batch, self.decoder_h_dim, device=obs_traj.device)
+                     if self.pool_every_timestep else None)
         out, _ = self.decoder(obs_traj[-1], obs_traj_rel[-1], (decoder_h, decoder_c), seq_start_end, scenes=sc)
         return out
 

@@ -42,13 +42,14 @@ const char* sgg_last_error(void);
  * Dense node-feature transform on MFMA (v_mfma_f32_16x16x4_f32, exact fp32):
  *   Y[m, n] = act( sum_k X[m, k] * Wop[k, n] + bias[n] )
  * Wop = W (K x N row-major) when trans_w = 0, or W^T for a W stored N x K when
- * trans_w = 1.  act: 0 none, 1 ReLU.  bias may be NULL.  ldx / ldy are the
- * row strides of X and Y (elements).
+ * trans_w = 1.  act: 0 none, 1 ReLU.  bias may be NULL.  ldx / ldw / ldy are
+ * the row strides of X, W (as stored) and Y (elements); a column block of a
+ * wider weight (the h-half W1[:, E:] of the pooling layer) is passed in place.
  * Replaces the per-node `torch.mm(h, W)` / nn.Linear calls of
  * models.py:199 (GAT Wh = hW), :576 ((AH)W of the GCN), :289 / :706
  * (out_embedding), and the h_j half of the pooling MLP's first layer :538.
  */
-int sgg_xw(const float* X, int ldx, const float* W, int trans_w, const float* bias,
+int sgg_xw(const float* X, int ldx, const float* W, int ldw, int trans_w, const float* bias,
            float* Y, int ldy, int M, int K, int N, int act, void* stream);
 
 /* ------------------------------------------------------------------------
@@ -61,7 +62,7 @@ int sgg_xw(const float* X, int ldx, const float* W, int trans_w, const float* bi
  * never materialised; the 512 -> bn layer runs on fp32 MFMA.  argmax[i,c]
  * receives the GLOBAL ped index j that attains the max (smallest j on ties)
  * for the backward.
- *   U: B x 512, pos: B x 2, A: 512 x 2, W2T: 512 x bn (= W2^T), b2: bn
+ *   U: B x 512, pos: B x 2, A: 512 x 2, W2: bn x 512 (nn.Linear layout), b2: bn
  *   out: B x bn, argmax: B x bn (int32).  bn in {8, 16, 32, 48, 64}.
  *   max_n = largest scene size in the batch (<= SGG_POOL_MAX_PEDS).
  * Work is split into chunks of whole i-rows of one scene; the chunk table
@@ -76,7 +77,7 @@ int sgg_xw(const float* X, int ldx, const float* W, int trans_w, const float* bi
  */
 int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int target_chunks, int max_gpw,
                   int32_t* host_chunks, int cap, int* max_rows, int* gpw);
-int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2T,
+int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2,
                  const float* b2, const int32_t* scene_off, const int32_t* chunks, int nchunks,
                  int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,
                  void* stream);
@@ -186,15 +187,30 @@ int sgg_seg_gather(const float* src, int lds, int F, const int32_t* seg_of_row,
 
 /* ------------------------------------------------------------------------
  * Parameter-gradient reduction C = X^T Y over R rows (X: R x M, Y: R x N,
- * row strides ldx / ldy; C: M x N, row stride ldc), and optionally colsum =
- * sum_r Y[r, :] (bias gradient).  Split-K over sgg_xtw_splits(R, M, N)
+ * row strides ldx / ldy; C: M x N, or C^T (N x M) when trans_c = 1, row
+ * stride ldc -- nn.Linear-layout weights take their gradient transposed, so
+ * it lands in place), and optionally colsum = sum_r Y[r, :] (bias gradient).  Split-K over sgg_xtw_splits(R, M, N)
  * workgroup slabs summed in a fixed order (deterministic); ws must hold
  * splits * (M*N + N) floats.  Replaces the library GEMMs of every weight
  * gradient (dW = X^T dY of the node transforms, W_hh / W_ih / hidden2pos of the
  * LSTMs summed over T x B, W1h of the pooling, `a` of the attention). */
 int sgg_xtw_splits(int R, int M, int N);
 int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, int M, int N, float* C,
-            int ldc, float* colsum, float* ws, size_t ws_bytes, void* stream);
+            int ldc, int trans_c, float* colsum, float* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Input-embedding fold (a Linear(2, E) displacement embedding feeding a
+ * linear layer: the LSTM input weights, models.py:52-59 / 121-125, and the
+ * pooling MLP's first layer, :477-481 / 530-538):
+ *   A = W We (R x 2),  bias = W be + b1 (+ b2; b2 may be NULL)
+ * W: R x E with row stride ldw (W1[:, :E] in place), We: E x 2, be, b1, b2.
+ * Backward: dW = dA We^T + dbias be^T (R x E, row stride lddw),
+ * dWe = W^T dA (E x 2), dbe = W^T dbias (E); db1 = db2 = dbias. */
+int sgg_fold_fwd(const float* W, int ldw, int R, int E, const float* We, const float* be,
+                 const float* b1, const float* b2, float* A, float* bias, void* stream);
+int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be,
+                 const float* dA, const float* dbias, float* dW, int lddw, float* dWe, float* dbe,
+                 void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused LSTM sequence (Encoder.forward models.py:62-92; Decoder.forward

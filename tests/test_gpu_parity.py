@@ -356,6 +356,43 @@ def test_xtw_matches_torch():
         ref = (X.double().t() @ Y.double()).float()
         close(C, ref.cpu(), rtol=5e-6, floor=1.0, what="xtw %s" % ((R, M, Nn),))
         close(cs, Y.double().sum(0).float().cpu(), rtol=5e-6, floor=1.0, what="colsum")
+        Ct = K.xtw(X, Y, trans_c=True)                               # transposed output
+        close(Ct, ref.t().cpu(), rtol=5e-6, floor=1.0, what="xtw^T %s" % ((R, M, Nn),))
+        big = torch.full((Nn, M + 5), 7.0, device=DEV)               # in place into a column block
+        K.xtw(X, Y, trans_c=True, out=big[:, 3:3 + M])
+        close(big[:, 3:3 + M], ref.t().cpu(), rtol=5e-6, floor=1.0, what="xtw^T in place")
+        assert float(big[:, :3].sub(7).abs().max()) == 0 and float(big[:, 3 + M:].sub(7).abs().max()) == 0
+
+
+def test_xw_strided_weight_block():
+    """sgg_xw on a column block of a wider weight (the pooling layer's h-half
+    W1[:, E:], models.py:538) read in place through its row stride."""
+    from sgan import kernels as K
+    torch.manual_seed(4)
+    W1 = torch.randn(512, 16 + 48, device=DEV)
+    h = torch.randn(300, 48, device=DEV)
+    c = torch.randn(512, device=DEV)
+    ref = (h.double() @ W1[:, 16:].double().t() + c.double()).float()
+    close(K.xw_raw(h, W1[:, 16:], c, trans_w=True), ref.cpu(), rtol=2e-6, what="xw strided")
+
+
+def test_fold_matches_torch():
+    """sgg_fold_fwd / sgg_fold_bwd against the autograd of W (We r + be) + b1 + b2."""
+    from sgan import kernels as K
+    torch.manual_seed(6)
+    for R, E, ld in ((128, 16, 16), (512, 16, 64), (192, 16, 16)):
+        Wfull = torch.randn(R, ld, device=DEV, dtype=torch.float64)
+        W = Wfull[:, :E]
+        We, be = torch.randn(E, 2, device=DEV, dtype=torch.float64), torch.randn(E, device=DEV, dtype=torch.float64)
+        b1, b2 = torch.randn(R, device=DEV, dtype=torch.float64), torch.randn(R, device=DEV, dtype=torch.float64)
+        A, bias = K.fold_fwd(W.float(), We.float(), be.float(), b1.float(), b2.float())
+        close(A, (W @ We).cpu().numpy(), rtol=2e-6, what="fold A")
+        close(bias, (W @ be + b1 + b2).cpu().numpy(), rtol=2e-6, what="fold bias")
+        dA, db = torch.randn(R, 2, device=DEV, dtype=torch.float64), torch.randn(R, device=DEV, dtype=torch.float64)
+        dW, dWe, dbe = K.fold_bwd(W.float(), We.float(), be.float(), dA.float(), db.float())
+        close(dW, (dA @ We.t() + db[:, None] * be[None, :]).cpu().numpy(), rtol=2e-6, what="fold dW")
+        close(dWe, (W.t() @ dA).cpu().numpy(), rtol=2e-6, what="fold dWe")
+        close(dbe, (W.t() @ db).cpu().numpy(), rtol=2e-6, what="fold dbe")
 
 
 def test_graphed_trainer_equals_eager():

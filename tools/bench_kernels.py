@@ -27,7 +27,7 @@ def run(S, n, hd, bn, gpws=(0,), reps=20):
     W2 = torch.randn(bn, 512, device=dev) * 0.05
     b2 = torch.randn(bn, device=dev) * 0.1
     U = K.xw_raw(h, W1h, c, trans_w=True)
-    W2T = W2.t().contiguous()
+    W2c = W2.contiguous()
     lib = N.load()
     flops = float(S * n * n) * 512 * (4 + 2 * bn)
     for gpw in gpws:
@@ -36,7 +36,7 @@ def run(S, n, hd, bn, gpws=(0,), reps=20):
         chunks, nchunks, max_rows, g = sc.pool_plan(bn)
         out = torch.empty(B, bn, device=dev)
         am = torch.empty(B, bn, device=dev, dtype=torch.int32)
-        call = lambda: N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2T), N.ptr(b2),
+        call = lambda: N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2c), N.ptr(b2),
                                                 N.ptr(sc.scene_off), N.ptr(chunks), nchunks, max_rows, g, B, bn,
                                                 sc.max_n, N.ptr(out), N.ptr(am), N.stream_ptr()), "pool")
         for _ in range(3):
@@ -84,10 +84,43 @@ def lstm(B, T, H, decoder, reps=10, save=False):
         B, T, H, decoder, save, us, flops / us / 1e6), flush=True)
 
 
+def timeit(call, reps=20):
+    for _ in range(3):
+        call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def dense():
+    """sgg_xw / sgg_xtw on the training step's shapes."""
+    dev = "cuda"
+    for (M, Kd, Nn, tw) in [(2560, 40, 72, False), (2560, 72, 16, False), (1280, 32, 512, True), (2560, 64, 48, True),
+                            (25600, 40, 72, False), (1280, 512, 32, False), (2560, 48, 64, True)]:
+        x = torch.randn(M, Kd, device=dev)
+        w = torch.randn(Nn, Kd, device=dev) if tw else torch.randn(Kd, Nn, device=dev)
+        us = timeit(lambda: K.xw_raw(x, w, None, trans_w=tw))
+        print("xw   M=%6d K=%4d N=%4d trans=%d  %7.1f us" % (M, Kd, Nn, tw, us), flush=True)
+    for (R, M, Nn) in [(1280, 32, 512), (2560, 48, 512), (51200, 48, 192), (20480, 32, 128), (2560, 40, 72),
+                       (1280, 64, 1), (2560, 2, 192)]:
+        X = torch.randn(R, M, device=dev)
+        Y = torch.randn(R, Nn, device=dev)
+        us = timeit(lambda: K.xtw(X, Y, colsum=True))
+        print("xtw  R=%6d M=%4d N=%4d  %7.1f us  (splits %d)" % (R, M, Nn, us, N.load().sgg_xtw_splits(R, M, Nn)),
+              flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "pool"
     if what == "big":     # one config (profiling)
         run(1280, 20, 32, 8, reps=5)
+        sys.exit(0)
+    if what == "dense":
+        dense()
         sys.exit(0)
     if what == "lstm":
         for B in (1280, 2560, 4096, 25600):
