@@ -56,6 +56,13 @@ __attribute__((visibility("hidden"))) int lstm_fwd_mfma(const float* rel, const 
                                                         int decoder, float* h_all, float* c_all, float* act_all,
                                                         float* rel_out, hipStream_t st);
 
+// v if keep else +0.f, as a bit mask: a plain `keep ? v : 0` lets the
+// compiler sink the load of v into an exec-masked branch that waits for it
+// (one memory latency per load); the mask keeps every load unconditional
+__device__ __forceinline__ float keep_if(float v, bool keep) {
+  return __int_as_float(__float_as_int(v) & (keep ? -1 : 0));
+}
+
 __device__ __forceinline__ float elu(float x) { return x > 0.f ? x : expm1f(x); }
 // derivative of ELU(alpha = 1) from its input
 __device__ __forceinline__ float elu_grad(float x) { return x > 0.f ? 1.f : expf(x); }

@@ -38,14 +38,31 @@ __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restric
   // software pipeline: the next 16 rows' loads are in flight while the current
   // 16 rows run through the MFMAs
   float a[4], b[4][4], an[4], bnx[4][4];
+  // Loads come from clamped addresses: columns >= M / >= N produce values
+  // that are never stored; only rows >= r1 must contribute zero, which
+  // concerns the last 16-row step alone -- a wave-uniform branch.
+  const int mcl = mok ? m : M - 1;
+  int ncl[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ncl[t] = nok[t] ? n0 + 16 * t + c16 : N - 1;
   auto load16 = [&](int r, float (&aa)[4], float (&bb)[4][4]) {
+    if (r + 16 <= r1) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int row = r + 4 * s + kq;
-      const bool rok = row < r1;
-      aa[s] = (rok && mok) ? X[(size_t)row * ldx + m] : 0.f;
+      for (int s = 0; s < 4; ++s) {
+        const size_t row = (size_t)(r + 4 * s + kq);
+        aa[s] = X[row * ldx + mcl];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bb[s][t] = (rok && nok[t]) ? Y[(size_t)row * ldy + n0 + 16 * t + c16] : 0.f;
+        for (int t = 0; t < 4; ++t) bb[s][t] = Y[row * ldy + ncl[t]];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int row = r + 4 * s + kq;
+        const size_t rc = (size_t)min(row, r1 - 1);
+        aa[s] = keep_if(X[rc * ldx + mcl], row < r1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bb[s][t] = keep_if(Y[rc * ldy + ncl[t]], row < r1);
+      }
     }
   };
   if (r0 < r1) load16(r0, a, b);

@@ -38,16 +38,31 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   // chunk computes, so a K <= 144 transform costs ~K/32 load latencies
   // instead of one per 4-deep step.  Out-of-range k / n read as 0 (adds 0).
   constexpr int KC = 32, S4 = KC / 4;
+  // Loads come from clamped (in-bounds) addresses: rows >= M and columns
+  // >= N compute values that the epilogue never stores, so they need no
+  // mask; only k >= K must contribute zero, which concerns the last chunk
+  // alone -- a wave-uniform branch.  (A per-load `cond ? v : 0` makes the
+  // compiler sink each load into an exec-masked branch that waits for it.)
+  int ncl[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ncl[t] = min(col0 + 16 * t + ar, N - 1);
   auto load_chunk = [&](int kb, float (&aa)[S4], float (&bb)[S4][4]) {
+    if (kb + KC <= K) {
 #pragma unroll
-    for (int s = 0; s < S4; ++s) {
-      const int k = kb + 4 * s + kq;
-      const bool kok = k < K;
-      aa[s] = (arow_ok && kok) ? xrow[k] : 0.f;
+      for (int s = 0; s < S4; ++s) {
+        const int k = kb + 4 * s + kq;
+        aa[s] = xrow[k];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int n = col0 + 16 * t + ar;
-        bb[s][t] = (kok && n < N) ? (TRANS_W ? W[(size_t)n * ldw + k] : W[(size_t)k * ldw + n]) : 0.f;
+        for (int t = 0; t < 4; ++t) bb[s][t] = TRANS_W ? W[ncl[t] * ldw + k] : W[k * ldw + ncl[t]];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < S4; ++s) {
+        const int k = kb + 4 * s + kq;
+        const int kc = min(k, K - 1);
+        aa[s] = keep_if(xrow[kc], k < K);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bb[s][t] = TRANS_W ? W[ncl[t] * ldw + kc] : W[kc * ldw + ncl[t]];
       }
     }
   };
