@@ -107,22 +107,26 @@ def main():
     g, d = build_models(0, args.graph_kind)
     g, d = g.to(dev), d.to(dev)
     trainer = GanTrainer(g, d, dp=DataParallel(), capturable=bool(args.graph))
+    # the reference feeds consecutive loader batches to the D-step and the
+    # G-step (scripts/train.py:279-297): two distinct synthetic batches
     batch = synthetic_batch([args.peds] * args.batch, seed=1000 + rank, device=dev)
+    batch_g = synthetic_batch([args.peds] * args.batch, seed=5000 + rank, device=dev)
     sc = SceneIndex.from_seq_start_end(batch[-1], dev)
+    sc_g = SceneIndex.from_seq_start_end(batch_g[-1], dev)
     S_glob, B_glob = sc.S * world, sc.B * world
     kw = dict(S_global=S_glob, B_global=B_glob, shard=(rank * sc.S, (rank + 1) * sc.S))
 
     graphed = False
     if args.graph:
         try:
-            gt = GraphedTrainer(trainer, batch, sc, warmup=2, **kw)
+            gt = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, **kw)
             step = gt.step
             graphed = True
         except Exception as e:  # capture unsupported (e.g. a collective): eager
             print("bench: graph capture failed (%s: %s); running eager" % (type(e).__name__, e), file=sys.stderr)
             torch.cuda.synchronize()
     if not graphed:
-        step = lambda: trainer.step(batch, sc, **kw)
+        step = lambda: trainer.step(batch, sc, batch_g, sc_g, **kw)
 
     for _ in range(args.warmup):
         step()
@@ -148,7 +152,7 @@ def main():
     # cross-check (profiles/)
     K.pool_timer.start()
     for _ in range(max(1, min(args.steps, 3))):
-        trainer.step(batch, sc, **kw)
+        trainer.step(batch, sc, batch_g, sc_g, **kw)
     launches = K.pool_timer.stop()
 
     if rank == 0:

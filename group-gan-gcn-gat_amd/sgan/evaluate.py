@@ -33,10 +33,14 @@ def sample_k(generator, batch, k, sc=None):
     B = obs_traj.size(1)
     sc = sc or SceneIndex.from_seq_start_end(sse, dev)
     z = draw_sample_noise(generator, sc, B, k)
-    sck = sc.repeat(k) if k > 1 else sc
-    rep = (lambda t: t.repeat(1, k, 1)) if k > 1 else (lambda t: t)
-    sse_k = torch.from_numpy(np.stack([sck.host_off[:-1], sck.host_off[1:]], 1)) if k > 1 else sse
-    out = generator(rep(obs_traj), rep(obs_traj_rel), sse_k, rep(obs_traj_g), user_noise=z, scenes=sck)
+    if generator.pool_every_timestep and k > 1:   # per-step pooling: replicate the whole batch
+        sck = sc.repeat(k)
+        rep = lambda t: t.repeat(1, k, 1)
+        sse_k = torch.from_numpy(np.stack([sck.host_off[:-1], sck.host_off[1:]], 1))
+        out = generator(rep(obs_traj), rep(obs_traj_rel), sse_k, rep(obs_traj_g), user_noise=z, scenes=sck)
+    else:   # the noise-independent context once, k decoder rollouts
+        ctx = generator.context(obs_traj, obs_traj_rel, sse, obs_traj_g, scenes=sc)
+        out = generator.decode(ctx, obs_traj, obs_traj_rel, sse, user_noise=z, scenes=sc, copies=k)
     return out.view(out.size(0), k, B, 2), sc
 
 

@@ -482,7 +482,17 @@ class TrajectoryGenerator(nn.Module):
         return bool(self.noise_dim or self.pooling_type or self.encoder_h_dim != self.decoder_h_dim)
 
     def forward(self, obs_traj, obs_traj_rel, seq_start_end, obs_traj_g, user_noise=None, *, scenes=None):
-        batch = obs_traj_rel.size(1)
+        sc = _scenes(seq_start_end, obs_traj.device, scenes)
+        noise_input = self.context(obs_traj, obs_traj_rel, seq_start_end, obs_traj_g, scenes=sc)
+        return self.decode(noise_input, obs_traj, obs_traj_rel, seq_start_end, user_noise=user_noise, scenes=sc)
+
+    def context(self, obs_traj, obs_traj_rel, seq_start_end, obs_traj_g, *, scenes=None):
+        """The noise-independent part of forward() (models.py:877-906):
+        encoder -> pooling -> GAT / GCN -> the decoder context (B, dec_h - noise).
+        best-of-k sampling (scripts/train.py:443-455, evaluate_model.py:85)
+        draws k samples that differ only in the noise appended after this
+        point, so it runs once per batch and `decode(copies=k)` rolls the k
+        samples out (the reference recomputes it k times, bit-identically)."""
         sc = _scenes(seq_start_end, obs_traj.device, scenes)
         final_encoder_h = self.encoder(obs_traj_rel)
         ctx = final_encoder_h.view(-1, self.encoder_h_dim)
@@ -499,12 +509,29 @@ class TrajectoryGenerator(nn.Module):
                 noise_input = self.gcn_module(ctx, seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
         else:
             noise_input = ctx
+        return noise_input
+
+    def decode(self, noise_input, obs_traj, obs_traj_rel, seq_start_end, user_noise=None, *, scenes=None,
+               copies=1):
+        """add_noise + decoder (models.py:909-925) for `copies` samples of the
+        batch laid out sample-major (scene s of copy r is scene r*S + s, as
+        SceneIndex.repeat builds it); user_noise then holds copies*S rows
+        (global mix).  -> pred_traj_fake_rel (pred_len, copies*B, 2)."""
+        sc = _scenes(seq_start_end, obs_traj.device, scenes)
+        last_pos, last_rel = obs_traj[-1], obs_traj_rel[-1]
+        if copies > 1:
+            if self.pool_every_timestep:
+                raise NotImplementedError("decode(copies>1) with per-step pooling: run forward() per sample")
+            sc = sc.repeat(copies)
+            noise_input = noise_input.repeat(copies, 1)
+            last_pos, last_rel = last_pos.repeat(copies, 1), last_rel.repeat(copies, 1)
+            seq_start_end = None
         decoder_h = self.add_noise(noise_input, seq_start_end, user_noise=user_noise, scenes=sc).unsqueeze(0)
         # c0 = 0 (models.py:912): the fused decoder takes a NULL initial cell
         # state as zeros; the per-step fallback needs the tensor
-        decoder_c = (torch.zeros(self.num_layers, batch, self.decoder_h_dim, device=obs_traj.device)
+        decoder_c = (torch.zeros(self.num_layers, sc.B, self.decoder_h_dim, device=obs_traj.device)
                      if self.pool_every_timestep else None)
-        out, _ = self.decoder(obs_traj[-1], obs_traj_rel[-1], (decoder_h, decoder_c), seq_start_end, scenes=sc)
+        out, _ = self.decoder(last_pos, last_rel, (decoder_h, decoder_c), seq_start_end, scenes=sc)
         return out
 
 

@@ -14,12 +14,16 @@ What differs is the execution plan, all results-neutral:
   * The D-step's G forward runs without autograd: its gradients are
     discarded by the reference (optimizer_g.zero_grad() precedes the G
     backward, train.py:478).
-  * The best_k G samples run as ONE no-grad call over a k-times replicated
-    batch; the per-scene argmin picks each scene's best sample, and only
-    that sample and the last one (the D input) are recomputed with autograd.
-    The gradient of min_k and of the D term flows only through those two, so
-    the gradients equal the reference's (every other sample's contribution
-    is exactly zero).  `selective_backward=False` keeps all k in the graph.
+  * The best_k G samples differ only in the noise appended after the graph
+    module (models.py:909), so the encoder / pooling / GAT context runs ONCE
+    per G-step, with autograd (G.context), and only the decoder rolls out
+    the k samples (G.decode): one no-grad rollout over the k-times
+    replicated context; the per-scene argmin picks each scene's best sample,
+    and only that sample and the last one (the D input) are rolled out again
+    with autograd.  The gradient of min_k and of the D term flows only
+    through those two, so the gradients equal the reference's (every other
+    sample's contribution is exactly zero).  `selective_backward=False`
+    keeps all k rollouts in the graph.
   * The G-step's D forward backpropagates to G only (its D parameter
     gradients are discarded by the reference, train.py:397-427).
   * Loss values come back as device tensors (no per-step host sync).
@@ -196,12 +200,15 @@ class GanTrainer:
             return (mask.unsqueeze(2) * (pred_gt_rel.permute(1, 0, 2) - pred_rel.permute(1, 0, 2)) ** 2).sum(2).sum(1)
 
         use_l2 = a.l2_loss_weight > 0
+        # the k samples differ only in the noise appended after the graph
+        # module: the encoder / pooling / GAT context runs once (with autograd)
+        # and only the decoder rolls out k times
+        ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
         if self.selective_backward and k > 1:
             z_all = torch.cat(zs, 0) if zs[0] is not None else None
-            sck = sc.repeat(k)
             with torch.no_grad():
-                pred_all = G(_rep(obs, k), _rep(obs_rel, k), _sse_of(sck), _rep(obs_g, k), user_noise=z_all,
-                             scenes=sck).view(a.pred_len, k, B, 2)
+                pred_all = G.decode(ctx.detach(), obs, obs_rel, sse, user_noise=z_all, scenes=sc,
+                                    copies=k).view(a.pred_len, k, B, 2)
                 if use_l2:
                     l2k = ((pred_gt_rel.unsqueeze(1) - pred_all) ** 2).sum(3) * mask.t().unsqueeze(1)
                     l2k = l2k.sum(0)                                          # (k, B)
@@ -213,13 +220,13 @@ class GanTrainer:
                 zk = z_all.view(k, S, -1).to(obs.device)
                 parts = ([zk[best, torch.arange(S, device=obs.device)]] if use_l2 else []) + [zk[k - 1]]
                 zc = torch.cat(parts, 0)
-            scc = sc.repeat(copies)
-            out = G(_rep(obs, copies), _rep(obs_rel, copies), _sse_of(scc), _rep(obs_g, copies), user_noise=zc,
-                    scenes=scc)
+            out = G.decode(ctx, obs, obs_rel, sse, user_noise=zc, scenes=sc, copies=copies)
             fake_rel_last = out[:, (copies - 1) * B:]
             fake_rel_best = out[:, :B] if use_l2 else None
         else:
-            outs = [G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc) for z in zs]
+            z_all = torch.cat(zs, 0) if zs[0] is not None else None
+            out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k)
+            outs = [out[:, i * B:(i + 1) * B] for i in range(k)]
             fake_rel_last = outs[-1]
             fake_rel_best = None
             if use_l2:
@@ -256,10 +263,14 @@ class GanTrainer:
             out["G_l2_loss_rel"] = vals[0]
         return out
 
-    def step(self, batch, sc, **kw):
-        """One reference iteration (d_steps = g_steps = 1) on one batch."""
+    def step(self, batch, sc, batch_g=None, sc_g=None, **kw):
+        """One reference iteration (d_steps = g_steps = 1): the D-step on
+        `batch`, the G-step on `batch_g` (default: the same batch).  The
+        reference's loop feeds consecutive loader batches to the two steps
+        (scripts/train.py:279-297); batch_g must have the same scene / ped
+        counts when S_global / B_global are given."""
         ld = self.d_step(batch, sc, **kw)
-        lg = self.g_step(batch, sc, **kw)
+        lg = self.g_step(batch if batch_g is None else batch_g, sc if sc_g is None else sc_g, **kw)
         return ld, lg
 
     def draw_inputs(self, S_global, s0, s1):
@@ -285,9 +296,13 @@ class GraphedTrainer:
     trainer must be built with capturable=True (Adam keeps its step on the
     device)."""
 
-    def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2):
+    def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2, batch_g=None,
+                 sc_g=None):
         self.t = trainer
         self.batch, self.sc = batch, sc
+        self.batch_g, self.sc_g = batch_g, sc_g
+        if batch_g is not None:
+            assert sc_g is not None and (sc_g.S, sc_g.B) == (sc.S, sc.B), "G-step batch must match the D-step's sizes"
         self.kw = dict(S_global=S_global or sc.S, B_global=B_global or sc.B, shard=shard)
         dev = batch[0].device
         s0 = shard[0]
@@ -309,14 +324,14 @@ class GraphedTrainer:
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self._load(*trainer.draw_inputs(*self.span))
-                trainer.step(batch, sc, inputs=self.inp, **self.kw)
+                trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         trainer.opt_g.zero_grad(set_to_none=True)
         trainer.opt_d.zero_grad(set_to_none=True)
         with torch.cuda.graph(self.graph):
-            self.losses = trainer.step(batch, sc, inputs=self.inp, **self.kw)
+            self.losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
 
     def _load(self, z_d, z_g, y):
         i = self.cur

@@ -36,6 +36,25 @@ class _Adapt(torch.nn.Module):
     def forward(self, *a, scenes=None, **k):
         return self.m(*a, **k)
 
+    # the product generator's context() / decode() split of forward(),
+    # restated over the oracle's submodules (models.py:877-925)
+    def context(self, obs_traj, obs_traj_rel, seq_start_end, obs_traj_g, scenes=None):
+        g = self.m
+        h = g.encoder(obs_traj_rel)
+        ctx = h.view(-1, g.encoder_h_dim)
+        if g.pooling_type:
+            ctx = torch.cat([ctx, g.pool_net(h, seq_start_end, obs_traj[-1])], 1)
+        return g.gatencoder(ctx, seq_start_end, obs_traj[-1], obs_traj_g[-1])
+
+    def decode(self, ni, obs_traj, obs_traj_rel, seq_start_end, user_noise=None, scenes=None, copies=1):
+        g = self.m
+        sc = scenes.repeat(copies)
+        sse = torch.from_numpy(np.stack([sc.host_off[:-1], sc.host_off[1:]], 1))
+        dh = g.add_noise(ni.repeat(copies, 1), sse, user_noise).unsqueeze(0)
+        dc = torch.zeros(1, sc.B, g.decoder_h_dim)
+        out, _ = g.decoder(obs_traj[-1].repeat(copies, 1), obs_traj_rel[-1].repeat(copies, 1), (dh, dc), sse)
+        return out
+
 
 def _models():
     from oracle import sgan_oracle as O
