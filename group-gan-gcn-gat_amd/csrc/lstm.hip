@@ -19,13 +19,19 @@
 // (ped, g, k) owns column k of gate block g of W_hh) so dh_{t-1} = W_hh^T dG_t
 // is H register FMAs + a 4-way LDS reduction.  Parameter gradients are sums
 // over (t, ped) of outer products -> the caller's GEMMs on the saved dG.
+#include <stdlib.h>
+
 #include "sgg_common.h"
 
 namespace sgg {
 
 constexpr int kLstmPeds = 4;
+constexpr int kLstmMaxT = 32;   // encoder inputs of up to this many steps are staged in LDS up front
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// v_exp_f32 / v_rcp_f32 forms (~2 ulp), as in lstm_mfma.hip: the gate
+// activations sit on the serial critical path of every step
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f); }
 
 template <int H>
 __global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(
@@ -35,10 +41,11 @@ __global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(
     float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out) {
   const bool save_states = act_all != nullptr;  // inference: only the final state is stored
   constexpr int G4 = 4 * H;
-  __shared__ float hbuf[kLstmPeds][H];
+  __shared__ __attribute__((aligned(16))) float hbuf[kLstmPeds][H];
   __shared__ float gbuf[kLstmPeds][G4];
   __shared__ float relb[kLstmPeds][2];
   __shared__ float redb[kLstmPeds][2][H];
+  __shared__ float relseq[kLstmPeds][kLstmMaxT][2];
   const int pl = threadIdx.x / G4, r = threadIdx.x - pl * G4;
   const int ped = blockIdx.x * kLstmPeds + pl;
   const bool valid = ped < B;
@@ -60,33 +67,42 @@ __global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(
     }
   }
   if (decoder && r < 2) relb[pl][r] = valid ? rel[(size_t)ped * 2 + r] : 0.f;
+  // encoder: the whole input sequence of the ped is loaded once, so no step
+  // waits on a global load
+  const bool staged = !decoder && T <= kLstmMaxT;
+  if (staged && r < 2 * T) relseq[pl][r >> 1][r & 1] = valid ? rel[((size_t)(r >> 1) * B + ped) * 2 + (r & 1)] : 0.f;
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     float x0, x1;
     if (decoder) {
       x0 = relb[pl][0];
       x1 = relb[pl][1];
+    } else if (staged) {
+      x0 = relseq[pl][t][0];
+      x1 = relseq[pl][t][1];
     } else {
       x0 = valid ? rel[((size_t)t * B + ped) * 2] : 0.f;
       x1 = valid ? rel[((size_t)t * B + ped) * 2 + 1] : 0.f;
     }
-    float acc = fmaf(a1, x1, fmaf(a0, x0, bb));
+    // four independent partial sums: the H-long FMA chain is the step's latency
+    float p0 = fmaf(a1, x1, fmaf(a0, x0, bb)), p1 = 0.f, p2 = 0.f, p3 = 0.f;
 #pragma unroll
     for (int k = 0; k < H; k += 4) {
       const float4 hv = *reinterpret_cast<const float4*>(&hbuf[pl][k]);
-      acc = fmaf(w[k], hv.x, acc);
-      acc = fmaf(w[k + 1], hv.y, acc);
-      acc = fmaf(w[k + 2], hv.z, acc);
-      acc = fmaf(w[k + 3], hv.w, acc);
+      p0 = fmaf(w[k], hv.x, p0);
+      p1 = fmaf(w[k + 1], hv.y, p1);
+      p2 = fmaf(w[k + 2], hv.z, p2);
+      p3 = fmaf(w[k + 3], hv.w, p3);
     }
-    const float act = is_g ? tanhf(acc) : sigm(acc);
+    const float acc = (p0 + p1) + (p2 + p3);
+    const float act = is_g ? tanh_f(acc) : sigm(acc);
     if (act_all && valid) act_all[((size_t)t * B + ped) * G4 + r] = act;
     gbuf[pl][r] = act;
     __syncthreads();
     if (r < H) {
       const float ig = gbuf[pl][r], fg = gbuf[pl][H + r], gg = gbuf[pl][2 * H + r], og = gbuf[pl][3 * H + r];
       c = fmaf(fg, c, ig * gg);
-      const float h = og * tanhf(c);
+      const float h = og * tanh_f(c);
       hbuf[pl][r] = h;
       if (decoder) {
         redb[pl][0][r] = wp0 * h;
@@ -120,7 +136,7 @@ __global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
     const float* __restrict__ dout, int T, int B, int decoder, float* __restrict__ dG, float* __restrict__ dh0,
     float* __restrict__ drel_in, float* __restrict__ drel_tot) {
   constexpr int G4 = 4 * H;
-  __shared__ float dgb[kLstmPeds][G4];
+  __shared__ __attribute__((aligned(16))) float dgb[kLstmPeds][G4];
   __shared__ float pb[kLstmPeds][4][H];
   __shared__ float drelb[kLstmPeds][2];
   __shared__ float fbp[kLstmPeds][2][G4 / 64 > 0 ? G4 / 64 : 1];
@@ -138,6 +154,20 @@ __global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
   const float wp0 = decoder ? Wp[q < H ? q : 0] : 0.f;
   const float wp1 = decoder ? Wp[H + (q < H ? q : 0)] : 0.f;
   if (q < H && !decoder && valid && dh_last) dh = dh_last[(size_t)ped * H + q];
+  // the saved activations of step t are loaded one step ahead (registers)
+  float nig = 0.f, nfg = 0.f, ngg = 0.f, nog = 0.f, nct = 0.f, ncp = 0.f;
+  auto load_step = [&](int t) {
+    if (q < H && valid) {
+      const size_t ab = ((size_t)t * B + ped) * G4;
+      nig = act_all[ab + q];
+      nfg = act_all[ab + H + q];
+      ngg = act_all[ab + 2 * H + q];
+      nog = act_all[ab + 3 * H + q];
+      nct = c_all[((size_t)(t + 1) * B + ped) * H + q];
+      ncp = c_all[((size_t)t * B + ped) * H + q];
+    }
+  };
+  load_step(T - 1);
   for (int t = T - 1; t >= 0; --t) {
     if (decoder) {
       if (q < 2) {
@@ -149,17 +179,9 @@ __global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
       if (q < H) dh = fmaf(wp0, drelb[pl][0], fmaf(wp1, drelb[pl][1], dh));
     }
     if (q < H) {
-      float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, ct = 0.f, cp = 0.f;
-      if (valid) {
-        const size_t ab = ((size_t)t * B + ped) * G4;
-        ig = act_all[ab + q];
-        fg = act_all[ab + H + q];
-        gg = act_all[ab + 2 * H + q];
-        og = act_all[ab + 3 * H + q];
-        ct = c_all[((size_t)(t + 1) * B + ped) * H + q];
-        cp = c_all[((size_t)t * B + ped) * H + q];
-      }
-      const float tc = tanhf(ct);
+      const float ig = nig, fg = nfg, gg = ngg, og = nog, ct = nct, cp = ncp;
+      if (t > 0) load_step(t - 1);   // in flight while this step computes
+      const float tc = tanh_f(ct);
       const float d_o = dh * tc;
       const float dct = fmaf(dh * og, 1.f - tc * tc, dc);
       const float di = dct * gg, dgg = dct * ig, df = dct * cp;
@@ -179,10 +201,16 @@ __global__ void __launch_bounds__(16 * H) lstm_bwd_kernel(
       }
     }
     __syncthreads();
-    float p = 0.f;
+    float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
 #pragma unroll
-    for (int j = 0; j < H; ++j) p = fmaf(wcol[j], dgb[pl][g * H + j], p);
-    pb[pl][g][k] = p;
+    for (int j = 0; j < H; j += 4) {
+      const float4 d4 = *reinterpret_cast<const float4*>(&dgb[pl][g * H + j]);
+      p0 = fmaf(wcol[j], d4.x, p0);
+      p1 = fmaf(wcol[j + 1], d4.y, p1);
+      p2 = fmaf(wcol[j + 2], d4.z, p2);
+      p3 = fmaf(wcol[j + 3], d4.w, p3);
+    }
+    pb[pl][g][k] = (p0 + p1) + (p2 + p3);
     {  // drel_t = A^T dG_t: one product per gate thread, wave shuffle + LDS combine
       const float dgq = dgb[pl][q];
       const float r0 = wave_sum(aq0 * dgq), r1 = wave_sum(aq1 * dgq);
@@ -237,8 +265,10 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_fwd: bad sizes T=%d B=%d", T, B);
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (lstm_fwd_mfma_ok(H, B))
+  if (lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
     return lstm_fwd_mfma(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
+  if (lstm_unit_ok(H, decoder) && !getenv("SGG_LSTM_ROWS"))
+    return lstm_unit_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
   switch (H) {
     case 16: return launch_lstm_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
     case 32: return launch_lstm_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
@@ -256,6 +286,8 @@ extern "C" int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, c
   SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_bwd: bad sizes");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (lstm_unit_ok(H, decoder) && !getenv("SGG_LSTM_ROWS"))
+    return lstm_unit_bwd(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, H, decoder, dG, dh0, drel_in, drel_tot, st);
   switch (H) {
     case 16: return launch_lstm_bwd<16>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
     case 32: return launch_lstm_bwd<32>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);

@@ -56,6 +56,19 @@ __attribute__((visibility("hidden"))) int lstm_fwd_mfma(const float* rel, const 
                                                         int decoder, float* h_all, float* c_all, float* act_all,
                                                         float* rel_out, hipStream_t st);
 
+// lstm_unit.hip: unit-per-thread LSTM sequence kernels (one barrier per
+// step), dispatched by sgg_lstm_fwd / sgg_lstm_bwd; internal
+__attribute__((visibility("hidden"))) bool lstm_unit_ok(int H, int decoder);
+__attribute__((visibility("hidden"))) int lstm_unit_fwd(const float* rel, const float* A, const float* Whh,
+                                                        const float* bias, const float* h0, const float* c0,
+                                                        const float* Wp, const float* bp, int T, int B, int H,
+                                                        int decoder, float* h_all, float* c_all, float* act_all,
+                                                        float* rel_out, hipStream_t st);
+__attribute__((visibility("hidden"))) int lstm_unit_bwd(const float* A, const float* Whh, const float* Wp,
+                                                        const float* c_all, const float* act_all, const float* dh_last,
+                                                        const float* dout, int T, int B, int H, int decoder, float* dG,
+                                                        float* dh0, float* drel_in, float* drel_tot, hipStream_t st);
+
 // v if keep else +0.f, as a bit mask: a plain `keep ? v : 0` lets the
 // compiler sink the load of v into an exec-masked branch that waits for it
 // (one memory latency per load); the mask keeps every load unconditional
