@@ -1,0 +1,654 @@
+// The whole group GAT encoder of a scene in one workgroup (GATEncoder,
+// reference sgan/models.py:254-294, with GAT :222-237 and
+// GraphAttentionLayer :184-220), forward and backward.
+//
+// Per scene (n <= 64 peds, the workgroup's LDS holds everything):
+//   groups      M_ij = (i == j) | (lab_i == lab_j != 0) on the last-observed
+//               labels (:263-266); group g(i) = index of i's first member
+//   intra GAT   per head h: Wh = X W_h (40 -> 72), masked softmax attention,
+//               ELU; heads concatenated; out layer (72 nh -> 16) + ELU +
+//               log_softmax over features                      (:269, :231-237)
+//   group mean  gin = R intra, R the row-normalised distinct rows of M
+//                                                               (:271-280)
+//   inter GAT   the same GAT (16 -> 72 -> 16) on the complete graph of the
+//               scene's groups                                  (:282-285)
+//   un-pool     inter_i = gout[g(i)] / |g(i)|  (R^T with R normalised, :286)
+//   out         Linear(32, 24)([intra, inter])                   (:288-289)
+//
+// One launch replaces the ~14 launches of the per-op path (sgg_xw +
+// sgg_gat_fwd per layer, group pooling kernels, concat, Linear).  The
+// backward recomputes the forward in LDS (it is ~0.3 MFLOP per 20-ped scene)
+// and back-propagates through every layer in the same workgroup; each
+// scene's parameter gradients go to its own row of a slab (no atomics) that
+// sgg_slab_reduce sums in scene order (deterministic).
+//
+// Attention: e_ij = LeakyReLU(a[:F].Wh_i + a[F:].Wh_j) (the s_i + t_j
+// decomposition of the reference's (N, N, 2F) concatenation), masked to
+// -inf outside the graph, softmax over j; one wavefront per attention row
+// with lane j (n <= 64), row max / sum by wave shuffles.
+#include "sgg_common.h"
+
+namespace sgg {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int FI = 40, FH = 72, FO = 16, FE = 24;   // GATEncoder dims (models.py:242-244)
+constexpr int P40 = FI + 1, P72 = FH + 1, P16 = FO + 1;
+
+struct Layout {
+  // float offsets into the workgroup's LDS
+  int X, H1, yI, preI, gin, G1, preG, gout, Wh, s, t, ds, dt, att;   // forward
+  int dWh, dH, dI, dG, dpre, attm;                                    // backward
+  int ints;       // int region: lab (float), gidl, grank, cnt, M
+  int total;      // floats
+  int PH, NP, NPP;
+};
+
+__host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
+  Layout L;
+  L.NP = np;
+  L.PH = FH * nh + 1;
+  L.NPP = np | 1;
+  int o = 0;
+  auto take = [&](int n) { const int r = o; o += (n + 3) & ~3; return r; };
+  L.X = take(np * P40);
+  L.H1 = take(np * L.PH);
+  L.yI = take(np * P16);
+  L.preI = take(np * P16);
+  L.gin = take(np * P16);
+  L.G1 = take(np * L.PH);
+  L.preG = take(np * P16);
+  L.gout = take(np * P16);
+  L.Wh = take(np * P72);
+  L.s = take(np);
+  L.t = take(np);
+  L.ds = take(np);
+  L.dt = take(np);
+  L.att = take(kWaves * 64);
+  if (bwd) {
+    L.dWh = take(np * P72);
+    L.dH = take(np * L.PH);
+    L.dI = take(np * P16);
+    L.dG = take(np * P16);
+    L.dpre = take(np * P16);
+    L.attm = take(np * L.NPP);
+  } else {
+    L.dWh = L.dH = L.dI = L.dG = L.dpre = L.attm = 0;
+  }
+  L.ints = take(5 * np + 4);
+  L.total = o;
+  return L;
+}
+
+// parameter-gradient slab layout (floats per scene)
+struct PLayout {
+  int Wi[kGatEncMaxHeads], ai[kGatEncMaxHeads], Wio, aio, Wg[kGatEncMaxHeads], ag[kGatEncMaxHeads], Wgo, ago, Woe,
+      boe, total;
+};
+
+__host__ __device__ inline PLayout make_playout(int nh) {
+  PLayout P;
+  int o = 0;
+  for (int h = 0; h < nh; ++h) {
+    P.Wi[h] = o; o += FI * FH;
+    P.ai[h] = o; o += 2 * FH;
+  }
+  P.Wio = o; o += FH * nh * FO;
+  P.aio = o; o += 2 * FO;
+  for (int h = 0; h < nh; ++h) {
+    P.Wg[h] = o; o += FO * FH;
+    P.ag[h] = o; o += 2 * FH;
+  }
+  P.Wgo = o; o += FH * nh * FO;
+  P.ago = o; o += 2 * FO;
+  P.Woe = o; o += FE * 2 * FO;
+  P.boe = o; o += FE;
+  P.total = o;
+  return P;
+}
+
+__device__ __forceinline__ float lrelu(float x, float a) { return x > 0.f ? x : a * x; }
+
+// out[r][c] = sum_k in[r][k] W[k][c]   (W: K x N row-major, global)
+__device__ void lin(const float* in, int ldi, int rows, int K, const float* __restrict__ W, int N, float* out,
+                    int ldo) {
+  for (int e = threadIdx.x; e < rows * N; e += kThreads) {
+    const int r = e / N, c = e - r * N;
+    const float* x = in + r * ldi;
+    float a0 = 0.f, a1 = 0.f;
+    int k = 0;
+    for (; k + 1 < K; k += 2) {
+      a0 = fmaf(x[k], W[k * N + c], a0);
+      a1 = fmaf(x[k + 1], W[(k + 1) * N + c], a1);
+    }
+    if (k < K) a0 = fmaf(x[k], W[k * N + c], a0);
+    out[r * ldo + c] = a0 + a1;
+  }
+}
+
+// out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin)
+__device__ void lin_t(const float* d, int ldd, int rows, int N, const float* __restrict__ W, int K, float* out,
+                      int ldo, bool acc) {
+  for (int e = threadIdx.x; e < rows * K; e += kThreads) {
+    const int r = e / K, k = e - r * K;
+    const float* dr = d + r * ldd;
+    const float* wr = W + k * N;
+    float a0 = 0.f, a1 = 0.f;
+    int c = 0;
+    for (; c + 1 < N; c += 2) {
+      a0 = fmaf(dr[c], wr[c], a0);
+      a1 = fmaf(dr[c + 1], wr[c + 1], a1);
+    }
+    if (c < N) a0 = fmaf(dr[c], wr[c], a0);
+    const float v = a0 + a1;
+    out[r * ldo + k] = acc ? out[r * ldo + k] + v : v;
+  }
+}
+
+// dst[k][c] = sum_r x[r][k] d[r][c]   (weight gradient of lin, to the slab)
+__device__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, int ldd, int N, float* dst) {
+  for (int e = threadIdx.x; e < K * N; e += kThreads) {
+    const int k = e / N, c = e - k * N;
+    float a0 = 0.f, a1 = 0.f;
+    int r = 0;
+    for (; r + 1 < rows; r += 2) {
+      a0 = fmaf(x[r * ldx + k], d[r * ldd + c], a0);
+      a1 = fmaf(x[(r + 1) * ldx + k], d[(r + 1) * ldd + c], a1);
+    }
+    if (r < rows) a0 = fmaf(x[r * ldx + k], d[r * ldd + c], a0);
+    dst[e] = a0 + a1;
+  }
+}
+
+// s_i = a[:F].Wh_i, t_i = a[F:].Wh_i
+__device__ void scores(const float* Wh, int ldw, int rows, int F, const float* __restrict__ a, float* s, float* t) {
+  for (int e = threadIdx.x; e < 2 * rows; e += kThreads) {
+    const int r = e >> 1, w = e & 1;
+    const float* av = a + w * F;
+    const float* x = Wh + r * ldw;
+    float a0 = 0.f, a1 = 0.f;
+    int f = 0;
+    for (; f + 1 < F; f += 2) {
+      a0 = fmaf(x[f], av[f], a0);
+      a1 = fmaf(x[f + 1], av[f + 1], a1);
+    }
+    if (f < F) a0 = fmaf(x[f], av[f], a0);
+    (w ? t : s)[r] = a0 + a1;
+  }
+}
+
+__device__ __forceinline__ bool edge(const int* gidl, int i, int j) { return gidl == nullptr || gidl[i] == gidl[j]; }
+
+// softmax row i of the attention, lane j (n <= 64)
+__device__ __forceinline__ float att_row(int i, int rows, const int* gidl, const float* s, const float* t, float alpha,
+                                         int lane) {
+  const bool ok = lane < rows && edge(gidl, i, lane);
+  const float e = ok ? lrelu(s[i] + t[lane], alpha) : -INFINITY;
+  const float m = wave_max(e);
+  const float p = ok ? __expf(e - m) : 0.f;
+  const float sum = wave_sum(p);
+  return p / sum;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// attention layer forward: out = epi(att . Wh); pre (optional) = att . Wh
+// epi: 1 ELU, 2 ELU + log_softmax over the F features
+__device__ void att_fwd(const float* Wh, int ldw, int rows, int F, const int* gidl, const float* s, const float* t,
+                        float alpha, int epi, float* out, int ldo, float* pre, int ldp, float* attw) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* aw = attw + wave * 64;
+  for (int i = wave; i < rows; i += kWaves) {
+    aw[lane] = att_row(i, rows, gidl, s, t, alpha, lane);
+    wave_lds_sync();
+    float hv[2], zv[2], zmax = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int f = lane + 64 * c;
+      float acc = 0.f;
+      if (f < F)
+        for (int j = 0; j < rows; ++j) acc = fmaf(aw[j], Wh[j * ldw + f], acc);
+      hv[c] = acc;
+      zv[c] = elu(acc);
+      if (f < F) zmax = fmaxf(zmax, zv[c]);
+    }
+    float lse = 0.f;
+    if (epi == 2) {
+      zmax = wave_max(zmax);
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (lane + 64 * c < F) se += __expf(zv[c] - zmax);
+      lse = zmax + __logf(wave_sum(se));
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int f = lane + 64 * c;
+      if (f < F) {
+        if (pre) pre[i * ldp + f] = hv[c];
+        out[i * ldo + f] = epi == 2 ? zv[c] - lse : zv[c];
+      }
+    }
+    wave_lds_sync();   // aw is rewritten by the wave's next row
+  }
+}
+
+// gradient through the epilogue: d (in: d out, out: d pre), one wave per row
+__device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, int F, int epi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = wave; i < rows; i += kWaves) {
+    float dv[2], hv[2], zv[2];
+    float zmax = -INFINITY, sdy = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int f = lane + 64 * c;
+      dv[c] = f < F ? d[i * ldd + f] : 0.f;
+      hv[c] = f < F ? pre[i * ldp + f] : 0.f;
+      zv[c] = elu(hv[c]);
+      if (f < F) {
+        zmax = fmaxf(zmax, zv[c]);
+        sdy += dv[c];
+      }
+    }
+    float lse = 0.f;
+    if (epi == 2) {
+      zmax = wave_max(zmax);
+      sdy = wave_sum(sdy);
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (lane + 64 * c < F) se += __expf(zv[c] - zmax);
+      lse = zmax + __logf(wave_sum(se));
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int f = lane + 64 * c;
+      if (f < F) {
+        float v = dv[c];
+        if (epi == 2) v -= __expf(zv[c] - lse) * sdy;
+        d[i * ldd + f] = v * elu_grad(hv[c]);
+      }
+    }
+  }
+}
+
+// attention layer backward.  dpre: gradient of the aggregate (rows x F);
+// writes dWh (rows x F) and the a-gradient (2F) to da; attm scratch rows x npp
+__device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gidl, float* s, float* t, float alpha,
+                        const float* __restrict__ a, const float* dpre, int ldd, float* dWh, int lddw, float* ds,
+                        float* dt, float* attm, int npp, float* da) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  scores(Wh, ldw, rows, F, a, s, t);
+  __syncthreads();
+  for (int i = wave; i < rows; i += kWaves) {
+    const float v = att_row(i, rows, gidl, s, t, alpha, lane);
+    if (lane < rows) attm[i * npp + lane] = v;
+  }
+  __syncthreads();
+  // attention-weighted part: dWh_j = sum_i att_ij dpre_i
+  for (int e = threadIdx.x; e < rows * F; e += kThreads) {
+    const int j = e / F, f = e - j * F;
+    float acc = 0.f;
+    for (int i = 0; i < rows; ++i) acc = fmaf(attm[i * npp + j], dpre[i * ldd + f], acc);
+    dWh[j * lddw + f] = acc;
+  }
+  __syncthreads();   // attm is overwritten with dz below
+  for (int i = wave; i < rows; i += kWaves) {
+    const int j = lane;
+    float datt = 0.f, at = 0.f;
+    if (j < rows) {
+      at = attm[i * npp + j];
+      for (int f = 0; f < F; ++f) datt = fmaf(dpre[i * ldd + f], Wh[j * ldw + f], datt);
+    }
+    const float dot = wave_sum(at * datt);
+    float dz = 0.f;
+    if (j < rows) {
+      const float de = at * (datt - dot);
+      dz = (s[i] + t[j]) > 0.f ? de : alpha * de;
+      attm[i * npp + j] = dz;
+    }
+    const float dsum = wave_sum(dz);
+    if (lane == 0) ds[i] = dsum;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < rows; j += kThreads) {
+    float acc = 0.f;
+    for (int i = 0; i < rows; ++i) acc += attm[i * npp + j];
+    dt[j] = acc;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < rows * F; e += kThreads) {
+    const int j = e / F, f = e - j * F;
+    dWh[j * lddw + f] += ds[j] * a[f] + dt[j] * a[F + f];
+  }
+  // da[f] = sum_i ds_i Wh_i[f], da[F + f] = sum_j dt_j Wh_j[f]
+  for (int e = threadIdx.x; e < 2 * F; e += kThreads) {
+    const int w = e / F, f = e - w * F;
+    const float* g = w ? dt : ds;
+    float acc = 0.f;
+    for (int r = 0; r < rows; ++r) acc = fmaf(g[r], Wh[r * ldw + f], acc);
+    da[e] = acc;
+  }
+  __syncthreads();
+}
+
+template <bool BWD>
+__global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const Layout L = make_layout(p.np, p.nh, BWD);
+  const PLayout PL = make_playout(p.nh);
+  const int nh = p.nh, PH = L.PH;
+  float* X = sm + L.X;
+  float* H1 = sm + L.H1;
+  float* yI = sm + L.yI;
+  float* preI = sm + L.preI;
+  float* gin = sm + L.gin;
+  float* G1 = sm + L.G1;
+  float* preG = sm + L.preG;
+  float* gout = sm + L.gout;
+  float* Wh = sm + L.Wh;
+  float* s = sm + L.s;
+  float* t = sm + L.t;
+  float* ds = sm + L.ds;
+  float* dt = sm + L.dt;
+  float* attw = sm + L.att;
+  float* lab = sm + L.ints;
+  int* gidl = reinterpret_cast<int*>(lab + L.NP);
+  int* grank = gidl + L.NP;
+  int* cnt = grank + L.NP;
+  float* ginv = reinterpret_cast<float*>(cnt + L.NP);
+  int* Mp = reinterpret_cast<int*>(ginv + L.NP);
+  const int tid = threadIdx.x;
+
+  for (int sc = blockIdx.x; sc < p.S; sc += gridDim.x) {
+    const int o = p.scene_off[sc];
+    const int n = p.scene_off[sc + 1] - o;
+    if (n <= 0) continue;   // uniform over the workgroup
+    // ---- inputs and group structure ------------------------------------
+    for (int e = tid; e < n * FI; e += kThreads) {
+      const int r = e / FI, k = e - r * FI;
+      X[r * P40 + k] = p.X[(size_t)(o + r) * p.ldx + k];
+    }
+    for (int i = tid; i < n; i += kThreads) lab[i] = p.labels[o + i];
+    __syncthreads();
+    for (int i = tid; i < n; i += kThreads) {
+      int g = i;
+      const float li = lab[i];
+      if (li != 0.f)
+        for (int j = 0; j < i; ++j)
+          if (lab[j] == li) { g = j; break; }
+      gidl[i] = g;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += kThreads) {
+      int r = 0;
+      for (int j = 0; j < gidl[i]; ++j) r += gidl[j] == j;
+      grank[i] = r;
+      int c = 0;
+      for (int j = 0; j < n; ++j) c += gidl[j] == gidl[i];
+      ginv[i] = 1.f / (float)c;
+      if (gidl[i] == i) cnt[r] = c;
+      if (i == n - 1) {
+        int m = 0;
+        for (int j = 0; j < n; ++j) m += gidl[j] == j;
+        *Mp = m;
+      }
+    }
+    __syncthreads();
+    const int M = *Mp;
+
+    // ---- intra GAT: heads (40 -> 72, ELU), out (72 nh -> 16, ELU, log_softmax)
+    for (int h = 0; h < nh; ++h) {
+      lin(X, P40, n, FI, p.w.Wi[h], FH, Wh, P72);
+      __syncthreads();
+      scores(Wh, P72, n, FH, p.w.ai[h], s, t);
+      __syncthreads();
+      att_fwd(Wh, P72, n, FH, gidl, s, t, p.alpha, 1, H1 + h * FH, PH, nullptr, 0, attw);
+      __syncthreads();
+    }
+    lin(H1, PH, n, FH * nh, p.w.Wio, FO, Wh, P72);
+    __syncthreads();
+    scores(Wh, P72, n, FO, p.w.aio, s, t);
+    __syncthreads();
+    att_fwd(Wh, P72, n, FO, gidl, s, t, p.alpha, 2, yI, P16, preI, P16, attw);
+    __syncthreads();
+    // ---- group mean (R intra) ------------------------------------------
+    for (int e = tid; e < M * FO; e += kThreads) {
+      const int g = e / FO, f = e - g * FO;
+      float acc = 0.f;
+      for (int i = 0; i < n; ++i)
+        if (grank[i] == g) acc = fmaf(ginv[i], yI[i * P16 + f], acc);
+      gin[g * P16 + f] = acc;
+    }
+    __syncthreads();
+    // ---- inter GAT on the complete graph of the M groups ----------------
+    for (int h = 0; h < nh; ++h) {
+      lin(gin, P16, M, FO, p.w.Wg[h], FH, Wh, P72);
+      __syncthreads();
+      scores(Wh, P72, M, FH, p.w.ag[h], s, t);
+      __syncthreads();
+      att_fwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, 1, G1 + h * FH, PH, nullptr, 0, attw);
+      __syncthreads();
+    }
+    lin(G1, PH, M, FH * nh, p.w.Wgo, FO, Wh, P72);
+    __syncthreads();
+    scores(Wh, P72, M, FO, p.w.ago, s, t);
+    __syncthreads();
+    att_fwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, 2, gout, P16, preG, P16, attw);
+    __syncthreads();
+
+    if (!BWD) {
+      // ---- out = Woe [intra, gout[g(i)] / |g(i)|] + boe ------------------
+      for (int e = tid; e < n * FE; e += kThreads) {
+        const int i = e / FE, c = e - i * FE;
+        const float* wr = p.w.Woe + c * 2 * FO;
+        const float* gi = gout + grank[i] * P16;
+        const float sc_i = ginv[i];
+        float a0 = p.w.boe[c], a1 = 0.f;
+        for (int f = 0; f < FO; ++f) {
+          a0 = fmaf(wr[f], yI[i * P16 + f], a0);
+          a1 = fmaf(wr[FO + f], gi[f] * sc_i, a1);
+        }
+        p.y[(size_t)(o + i) * p.ldy + c] = a0 + a1;
+      }
+      __syncthreads();
+      continue;
+    }
+
+    // ================= backward ===========================================
+    float* dWh = sm + L.dWh;
+    float* dH = sm + L.dH;
+    float* dI = sm + L.dI;
+    float* dG = sm + L.dG;
+    float* dpre = sm + L.dpre;
+    float* attm = sm + L.attm;
+    float* slab = p.slab + (size_t)sc * PL.total;
+    const float* dy = p.dy + (size_t)o * p.lddy;
+    // out embedding: d[intra | inter] = dy Woe; dWoe = dy^T [intra | inter]; dboe = sum dy
+    for (int e = tid; e < n * 2 * FO; e += kThreads) {
+      const int i = e / (2 * FO), c = e - i * 2 * FO;
+      float acc = 0.f;
+      for (int k = 0; k < FE; ++k) acc = fmaf(dy[i * p.lddy + k], p.w.Woe[k * 2 * FO + c], acc);
+      if (c < FO) dI[i * P16 + c] = acc;
+      else dpre[i * P16 + c - FO] = acc;   // d inter (scratch)
+    }
+    for (int e = tid; e < FE * 2 * FO; e += kThreads) {
+      const int k = e / (2 * FO), c = e - k * 2 * FO;
+      float acc = 0.f;
+      for (int i = 0; i < n; ++i) {
+        const float v = c < FO ? yI[i * P16 + c] : gout[grank[i] * P16 + c - FO] * ginv[i];
+        acc = fmaf(dy[i * p.lddy + k], v, acc);
+      }
+      slab[PL.Woe + e] = acc;
+    }
+    for (int k = tid; k < FE; k += kThreads) {
+      float acc = 0.f;
+      for (int i = 0; i < n; ++i) acc += dy[i * p.lddy + k];
+      slab[PL.boe + k] = acc;
+    }
+    __syncthreads();
+    // un-pool backward: d gout[g] = sum_{i in g} d inter_i / |g|
+    for (int e = tid; e < M * FO; e += kThreads) {
+      const int g = e / FO, f = e - g * FO;
+      float acc = 0.f;
+      for (int i = 0; i < n; ++i)
+        if (grank[i] == g) acc = fmaf(ginv[i], dpre[i * P16 + f], acc);
+      dG[g * P16 + f] = acc;
+    }
+    __syncthreads();
+    // ---- inter out layer ----
+    epi_bwd(dG, P16, preG, P16, M, FO, 2);
+    lin(G1, PH, M, FH * nh, p.w.Wgo, FO, Wh, P72);
+    __syncthreads();
+    att_bwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, p.w.ago, dG, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.ago);
+    wgrad(G1, PH, M, FH * nh, dWh, P72, FO, slab + PL.Wgo);
+    lin_t(dWh, P72, M, FO, p.w.Wgo, FH * nh, dH, PH, false);
+    __syncthreads();
+    // ---- inter heads ----
+    for (int e = tid; e < M * FO; e += kThreads) dG[(e / FO) * P16 + e % FO] = 0.f;   // becomes d gin
+    for (int h = 0; h < nh; ++h) {
+      // ELU backward from the stored output: elu'(x) = 1 (y > 0) | y + 1
+      for (int e = tid; e < M * FH; e += kThreads) {
+        const int r = e / FH, f = e - r * FH;
+        const float yv = G1[r * PH + h * FH + f];
+        dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
+      }
+      lin(gin, P16, M, FO, p.w.Wg[h], FH, Wh, P72);
+      __syncthreads();
+      att_bwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, p.w.ag[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
+              slab + PL.ag[h]);
+      wgrad(gin, P16, M, FO, dWh, P72, FH, slab + PL.Wg[h]);
+      lin_t(dWh, P72, M, FH, p.w.Wg[h], FO, dG, P16, true);
+      __syncthreads();
+    }
+    // group-mean backward: d intra_i += d gin[g(i)] / |g(i)|
+    for (int e = tid; e < n * FO; e += kThreads) {
+      const int i = e / FO, f = e - i * FO;
+      dI[i * P16 + f] = fmaf(ginv[i], dG[grank[i] * P16 + f], dI[i * P16 + f]);
+    }
+    __syncthreads();
+    // ---- intra out layer ----
+    epi_bwd(dI, P16, preI, P16, n, FO, 2);
+    lin(H1, PH, n, FH * nh, p.w.Wio, FO, Wh, P72);
+    __syncthreads();
+    att_bwd(Wh, P72, n, FO, gidl, s, t, p.alpha, p.w.aio, dI, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.aio);
+    wgrad(H1, PH, n, FH * nh, dWh, P72, FO, slab + PL.Wio);
+    lin_t(dWh, P72, n, FO, p.w.Wio, FH * nh, dH, PH, false);
+    __syncthreads();
+    // ---- intra heads ----
+    float* dXo = p.dX + (size_t)o * p.lddx;
+    for (int h = 0; h < nh; ++h) {
+      for (int e = tid; e < n * FH; e += kThreads) {
+        const int r = e / FH, f = e - r * FH;
+        const float yv = H1[r * PH + h * FH + f];
+        dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
+      }
+      lin(X, P40, n, FI, p.w.Wi[h], FH, Wh, P72);
+      __syncthreads();
+      att_bwd(Wh, P72, n, FH, gidl, s, t, p.alpha, p.w.ai[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
+              slab + PL.ai[h]);
+      wgrad(X, P40, n, FI, dWh, P72, FH, slab + PL.Wi[h]);
+      // dX (global) accumulates over heads in a fixed order
+      for (int e = tid; e < n * FI; e += kThreads) {
+        const int r = e / FI, k = e - r * FI;
+        const float* dr = dWh + r * P72;
+        const float* wr = p.w.Wi[h] + k * FH;
+        float a0 = 0.f, a1 = 0.f;
+        for (int c = 0; c < FH; c += 2) {
+          a0 = fmaf(dr[c], wr[c], a0);
+          a1 = fmaf(dr[c + 1], wr[c + 1], a1);
+        }
+        float* dst = dXo + (size_t)r * p.lddx + k;
+        *dst = h ? *dst + (a0 + a1) : a0 + a1;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// out[c] = sum_s slab[s][c] in scene order (deterministic)
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, int rows, int cols,
+                                                         float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int r = 0;
+  for (; r + 3 < rows; r += 4) {
+    a0 += slab[(size_t)r * cols + c];
+    a1 += slab[(size_t)(r + 1) * cols + c];
+    a2 += slab[(size_t)(r + 2) * cols + c];
+    a3 += slab[(size_t)(r + 3) * cols + c];
+  }
+  for (; r < rows; ++r) a0 += slab[(size_t)r * cols + c];
+  out[c] = (a0 + a1) + (a2 + a3);
+}
+
+}  // namespace
+
+}  // namespace sgg
+
+using namespace sgg;
+
+extern "C" int sgg_gatenc_param_size(int nh) {
+  if (nh < 1 || nh > kGatEncMaxHeads) return -1;
+  return make_playout(nh).total;
+}
+
+extern "C" long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd) {
+  if (max_n < 1 || nh < 1 || nh > kGatEncMaxHeads) return -1;
+  return 4ll * make_layout(max_n, nh, bwd != 0).total;
+}
+
+static int gatenc_check(const char* who, const GatEncArgs* a, int bwd) {
+  SGG_CHECK_ARG(a, "%s: null args", who);
+  SGG_CHECK_ARG(a->X && a->labels && a->scene_off, "%s: null input", who);
+  SGG_CHECK_ARG(a->nh >= 1 && a->nh <= kGatEncMaxHeads, "%s: heads %d outside [1, %d]", who, a->nh, kGatEncMaxHeads);
+  SGG_CHECK_ARG(a->np >= 1 && a->np <= 64, "%s: max scene size %d outside [1, 64]", who, a->np);
+  SGG_CHECK_ARG(a->S >= 0 && a->ldx >= FI, "%s: bad sizes", who);
+  for (int h = 0; h < a->nh; ++h)
+    SGG_CHECK_ARG(a->w.Wi[h] && a->w.ai[h] && a->w.Wg[h] && a->w.ag[h], "%s: null head weight %d", who, h);
+  SGG_CHECK_ARG(a->w.Wio && a->w.aio && a->w.Wgo && a->w.ago && a->w.Woe && a->w.boe, "%s: null weight", who);
+  if (bwd) {
+    SGG_CHECK_ARG(a->dy && a->dX && a->slab && a->lddy >= FE && a->lddx >= FI, "%s: null / bad gradient buffer", who);
+  } else {
+    SGG_CHECK_ARG(a->y && a->ldy >= FE, "%s: null / bad output", who);
+  }
+  const long long lds = sgg_gatenc_lds_bytes(a->np, a->nh, bwd);
+  SGG_CHECK_ARG(lds <= 160 * 1024, "%s: %d peds x %d heads need %lld B of LDS (> 160 KiB)", who, a->np, a->nh, lds);
+  return 0;
+}
+
+extern "C" int sgg_gatenc_fwd(const GatEncArgs* args, void* stream) {
+  const int rc = gatenc_check("sgg_gatenc_fwd", args, 0);
+  if (rc) return rc;
+  if (args->S == 0) return 0;
+  const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 0);
+  hipLaunchKernelGGL(gatenc_kernel<false>, dim3(args->S < 65536 ? args->S : 65536), dim3(kThreads), lds,
+                     (hipStream_t)stream, *args);
+  SGG_RETURN_LAUNCH("sgg_gatenc_fwd");
+}
+
+extern "C" int sgg_gatenc_bwd(const GatEncArgs* args, void* stream) {
+  const int rc = gatenc_check("sgg_gatenc_bwd", args, 1);
+  if (rc) return rc;
+  if (args->S == 0) return 0;
+  const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 1);
+  hipLaunchKernelGGL(gatenc_kernel<true>, dim3(args->S < 65536 ? args->S : 65536), dim3(kThreads), lds,
+                     (hipStream_t)stream, *args);
+  SGG_RETURN_LAUNCH("sgg_gatenc_bwd");
+}
+
+extern "C" int sgg_slab_reduce(const float* slab, int rows, int cols, float* out, void* stream) {
+  SGG_CHECK_ARG(slab && out, "sgg_slab_reduce: null pointer");
+  SGG_CHECK_ARG(rows >= 0 && cols >= 0, "sgg_slab_reduce: bad sizes");
+  if (cols == 0) return 0;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((cols + 255) / 256), dim3(256), 0, (hipStream_t)stream, slab, rows, cols,
+                     out);
+  SGG_RETURN_LAUNCH("sgg_slab_reduce");
+}

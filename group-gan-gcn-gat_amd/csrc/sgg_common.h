@@ -11,6 +11,8 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 namespace sgg {
 
 constexpr int kWave = 64;      // CDNA wavefront
+constexpr int kGatEncMaxHeads = SGG_GATENC_MAX_HEADS;
+using GatEncArgs = SggGatEncArgs;
 constexpr int kHidden = 512;   // pooling MLP hidden width (hard-coded, models.py:473)
 
 // last error, per calling host thread

@@ -18,6 +18,24 @@ _f = ctypes.c_float
 _p = ctypes.c_void_p
 _sz = ctypes.c_size_t
 
+MAX_HEADS = 4   # SGG_GATENC_MAX_HEADS
+
+
+class GatEncWeights(ctypes.Structure):
+    """SggGatEncWeights (include/sgg.h)."""
+    _fields_ = [("Wi", _p * MAX_HEADS), ("ai", _p * MAX_HEADS), ("Wio", _p), ("aio", _p),
+                ("Wg", _p * MAX_HEADS), ("ag", _p * MAX_HEADS), ("Wgo", _p), ("ago", _p), ("Woe", _p), ("boe", _p)]
+
+
+class GatEncArgs(ctypes.Structure):
+    """SggGatEncArgs (include/sgg.h)."""
+    _fields_ = [("X", _p), ("ldx", _i), ("labels", _p), ("scene_off", _p), ("S", _i), ("np", _i), ("nh", _i),
+                ("alpha", _f), ("w", GatEncWeights), ("y", _p), ("ldy", _i), ("dy", _p), ("lddy", _i), ("dX", _p),
+                ("lddx", _i), ("slab", _p)]
+
+
+_pargs = ctypes.POINTER(GatEncArgs)
+
 # name -> (restype, argtypes); must mirror include/sgg.h exactly
 SIGNATURES = {
     "sgg_version": (_i, []),
@@ -43,6 +61,11 @@ SIGNATURES = {
     "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p]),
     "sgg_bce_bwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p]),
+    "sgg_gatenc_param_size": (_i, [_i]),
+    "sgg_gatenc_lds_bytes": (ctypes.c_longlong, [_i, _i, _i]),
+    "sgg_gatenc_fwd": (_i, [_pargs, _p]),
+    "sgg_gatenc_bwd": (_i, [_pargs, _p]),
+    "sgg_slab_reduce": (_i, [_p, _i, _i, _p, _p]),
 }
 
 _lib = None

@@ -5,9 +5,14 @@ backward are hand-written HIP kernels, except the parameter-gradient
 reductions over all nodes (X^T dY, column sums), which are plain GEMMs /
 reductions left to rocBLAS via torch.  No op has a CPU path.
 """
+import os
+
 import torch
 
 from . import _native as N
+
+# the one-launch GATEncoder (sgg_gatenc_*); "0" forces the per-layer kernels
+GATENC_FUSED = os.environ.get("SGG_GATENC_FUSED", "1") != "0"
 
 
 def _lib():
@@ -308,6 +313,80 @@ def gat_attention(wh, a, alpha, graph, epilogue, heads=1, bias=None):
     heads and added before the epilogue (sgangat GAT, GAT.py:6-55 text)."""
     return _GatAttn.apply(wh, a, bias, graph.labels, graph.seg_off, graph.nseg, graph.max_seg, alpha, graph.mode,
                           epilogue, heads)
+
+
+class _GatEnc(torch.autograd.Function):
+    """The whole GATEncoder of every scene in one launch (sgg_gatenc_fwd);
+    backward = one recompute + back-propagation launch (sgg_gatenc_bwd) + the
+    scene-ordered slab sum of the parameter gradients (sgg_slab_reduce).
+    params: [W_h, a_h for each intra head], W_out, a_out (intra), the same for
+    the inter GAT, out_embedding weight, bias -- the slab order of sgg.h."""
+
+    @staticmethod
+    def forward(ctx, x, labels, scenes, nh, alpha, *params):
+        lib = _lib()
+        x = _rows(x, "x")
+        B = x.shape[0]
+        y = torch.empty(B, 24, device=x.device, dtype=torch.float32)
+        ps = [_req(q, "gat weight").contiguous() for q in params]
+        a = _gatenc_args(x, labels, scenes, nh, alpha, ps)
+        a.y, a.ldy = N.ptr(y), 24
+        N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_fwd")
+        ctx.meta = (labels, scenes, nh, alpha)
+        ctx.save_for_backward(x, *ps)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib()
+        x, *ps = ctx.saved_tensors
+        labels, scenes, nh, alpha = ctx.meta
+        dy = _rows(dy, "dy")
+        B = x.shape[0]
+        P = lib.sgg_gatenc_param_size(nh)
+        dx = torch.empty(B, 40, device=x.device, dtype=torch.float32)
+        slab = torch.empty(max(scenes.S, 1), P, device=x.device, dtype=torch.float32)
+        a = _gatenc_args(x, labels, scenes, nh, alpha, ps)
+        a.dy, a.lddy = N.ptr(dy), dy.stride(0)
+        a.dX, a.lddx = N.ptr(dx), 40
+        a.slab = N.ptr(slab)
+        N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_bwd")
+        flat = torch.empty(P, device=x.device, dtype=torch.float32)
+        N.check(lib.sgg_slab_reduce(N.ptr(slab), scenes.S, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+        grads, o = [], 0
+        for q in ps:
+            grads.append(flat[o:o + q.numel()].view_as(q))
+            o += q.numel()
+        return (dx, None, None, None, None) + tuple(grads)
+
+
+def _gatenc_args(x, labels, scenes, nh, alpha, ps):
+    a = N.GatEncArgs()
+    a.X, a.ldx = N.ptr(x), x.stride(0)
+    a.labels, a.scene_off = N.ptr(labels), N.ptr(scenes.scene_off)
+    a.S, a.np, a.nh, a.alpha = scenes.S, max(scenes.max_n, 1), nh, float(alpha)
+    it = iter(ps)
+    for h in range(nh):
+        a.w.Wi[h], a.w.ai[h] = N.ptr(next(it)), N.ptr(next(it))
+    a.w.Wio, a.w.aio = N.ptr(next(it)), N.ptr(next(it))
+    for h in range(nh):
+        a.w.Wg[h], a.w.ag[h] = N.ptr(next(it)), N.ptr(next(it))
+    a.w.Wgo, a.w.ago = N.ptr(next(it)), N.ptr(next(it))
+    a.w.Woe, a.w.boe = N.ptr(next(it)), N.ptr(next(it))
+    return a
+
+
+def gat_encoder_fused_ok(scenes, nh, need_grad):
+    """The fused GATEncoder path holds a scene in one workgroup's LDS."""
+    if not GATENC_FUSED or nh < 1 or nh > N.MAX_HEADS or scenes.max_n > 64:
+        return False
+    return _lib().sgg_gatenc_lds_bytes(max(scenes.max_n, 1), nh, int(bool(need_grad))) <= 160 * 1024
+
+
+def gat_encoder(x, labels, scenes, nh, alpha, params):
+    """GATEncoder.forward (models.py:254-294) for all scenes: (B, 40) -> (B, 24)."""
+    lab = _req(labels, "labels").contiguous().view(-1)
+    return _GatEnc.apply(x, lab, scenes, nh, alpha, *params)
 
 
 class _SegNorm(torch.autograd.Function):

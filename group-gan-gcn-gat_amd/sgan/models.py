@@ -256,10 +256,25 @@ class GATEncoder(nn.Module):
         self.gat_inter = GAT(16, 72, 16, dropout, alpha, n_heads)
         self.out_embedding = nn.Linear(16 * 2, 24)
 
+    def fused_params(self):
+        """The parameters in the order of the fused kernel's slab (sgg.h)."""
+        ps = []
+        for gat in (self.gat_intra, self.gat_inter):
+            for att in gat.attentions:
+                ps += [att.W, att.a]
+            ps += [gat.out_att.W, gat.out_att.a]
+        return ps + [self.out_embedding.weight, self.out_embedding.bias]
+
     def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None):
         sc = _scenes(seq_start_end, h_states.device, scenes)
         if sc.max_n > 128:
             raise ValueError("GAT kernels hold <= 128 peds per scene (got %d)" % sc.max_n)
+        nh = len(self.gat_intra.attentions)
+        params = self.fused_params()
+        need_grad = torch.is_grad_enabled() and (h_states.requires_grad or any(p.requires_grad for p in params))
+        if (self.gat_intra.dropout == 0 or not self.training) and K.gat_encoder_fused_ok(sc, nh, need_grad):
+            # one launch per direction for the whole module (sgg_gatenc_fwd / _bwd)
+            return K.gat_encoder(h_states, end_group, sc, nh, self.gat_intra.attentions[0].alpha, params)
         g = sc.groups(end_group.reshape(-1))
         intra_graph = K.SegmentGraph(sc.scene_off, sc.S, sc.max_n, 0, g.labels)
         inter_graph = K.SegmentGraph(g.group_off, sc.S, sc.max_n, 1, None)

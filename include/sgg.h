@@ -257,6 +257,69 @@ int sgg_bce_fwd(const float* x, int n, int split, const float* ya, const float* 
 int sgg_bce_bwd(const float* x, int n, int split, const float* ya, const float* yb, float w,
                 const float* gout, float* dx, void* stream);
 
+/* ------------------------------------------------------------------------
+ * The group GAT encoder of every scene in ONE launch (GATEncoder.forward,
+ * models.py:254-294, with GAT.forward :231-237 and GraphAttentionLayer
+ * :198-220): per scene (workgroup) the group mask of the last-observed labels
+ * (:263-266), the intra-group GAT 40 -> 72 (x nh heads, ELU) -> 16 (ELU,
+ * log_softmax), the group mean R.intra (:271-280), the inter-group GAT
+ * 16 -> 72 -> 16 on the complete graph of the scene's groups (:282-285), the
+ * un-pool R^T (:286) and out_embedding Linear(32, 24) (:288-289), all in LDS.
+ * Replaces the per-op sequence sgg_xw / sgg_gat_fwd / sgg_group_index /
+ * sgg_seg_reduce / sgg_seg_gather / concat / Linear (~14 launches).
+ *
+ * Weights are the module's own tensors: Wi[h] (40 x 72), ai[h] (144),
+ * Wio (72 nh x 16), aio (32) of gat_intra; Wg[h] (16 x 72), ag[h], Wgo, ago of
+ * gat_inter; Woe (24 x 32, nn.Linear layout), boe (24).  X: B x 40 rows
+ * (stride ldx), labels: B floats, scene_off: S + 1, np = the largest scene
+ * (<= 64; the LDS plan is sized by it, sgg_gatenc_lds_bytes <= 160 KiB).
+ * Forward writes y (B x 24, stride ldy).  Backward (recomputes the forward)
+ * reads dy and writes dX (B x 40, stride lddx) and, per scene s, the
+ * parameter gradients into slab row s (sgg_gatenc_param_size(nh) floats, in
+ * the order Wi[0], ai[0], .., Wio, aio, Wg[0], ag[0], .., Wgo, ago, Woe, boe);
+ * sgg_slab_reduce sums the rows in scene order.
+ */
+#define SGG_GATENC_MAX_HEADS 4
+typedef struct {
+  const float* Wi[SGG_GATENC_MAX_HEADS];
+  const float* ai[SGG_GATENC_MAX_HEADS];
+  const float* Wio;
+  const float* aio;
+  const float* Wg[SGG_GATENC_MAX_HEADS];
+  const float* ag[SGG_GATENC_MAX_HEADS];
+  const float* Wgo;
+  const float* ago;
+  const float* Woe;
+  const float* boe;
+} SggGatEncWeights;
+
+typedef struct {
+  const float* X;
+  int ldx;
+  const float* labels;
+  const int32_t* scene_off;
+  int S;
+  int np;
+  int nh;
+  float alpha;
+  SggGatEncWeights w;
+  float* y;
+  int ldy;
+  const float* dy;
+  int lddy;
+  float* dX;
+  int lddx;
+  float* slab;
+} SggGatEncArgs;
+
+int sgg_gatenc_param_size(int nh);
+long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd);
+int sgg_gatenc_fwd(const SggGatEncArgs* args, void* stream);
+int sgg_gatenc_bwd(const SggGatEncArgs* args, void* stream);
+
+/* out[c] = sum_r slab[r][c] (rows x cols, row-major), rows summed in order. */
+int sgg_slab_reduce(const float* slab, int rows, int cols, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -426,3 +426,43 @@ def test_graphed_trainer_equals_eager():
     for k in wa:
         err = (wa[k] - wb[k]).abs().max().item()
         assert err <= 1e-5 + 1e-5 * wa[k].abs().max().item(), (k, err)
+
+
+@pytest.mark.parametrize("nh,sizes", [(1, [1, 2, 20, 64, 13, 5]), (2, [20, 7, 40, 1]), (3, [3, 20, 33])])
+def test_gat_encoder_fused_equals_per_layer(nh, sizes):
+    """The one-launch GATEncoder (sgg_gatenc_fwd / _bwd + sgg_slab_reduce)
+    against the per-layer kernels on the same module: outputs, input and
+    parameter gradients; label patterns with singletons (label 0), one big
+    group, mixed groups, one-ped scenes."""
+    from sgan import kernels as K
+    from sgan.models import GATEncoder
+    from sgan.scene import SceneIndex
+    torch.manual_seed(nh)
+    mod = GATEncoder([40, 16, 40], nh, 0.0, 0.2).to(DEV)
+    B = sum(sizes)
+    sc = SceneIndex(np.concatenate([[0], np.cumsum(sizes)]), DEV)
+    labs = []
+    for k, n in enumerate(sizes):
+        pat = k % 3
+        labs.append(np.zeros(n) if pat == 0 else np.full(n, 3.0) if pat == 1 else np.random.RandomState(k).randint(0, 4, n))
+    lab = torch.from_numpy(np.concatenate(labs).astype(np.float32)).to(DEV).view(-1, 1)
+    x = torch.randn(B, 40, device=DEV)
+    dy = torch.randn(B, 24, device=DEV)
+    res = []
+    for fused in (True, False):
+        K.GATENC_FUSED = fused
+        try:
+            assert K.gat_encoder_fused_ok(sc, nh, True) == fused
+            mod.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            y = mod(xi, None, None, lab, scenes=sc)
+            (y * dy).sum().backward()
+            res.append((y.detach(), xi.grad, {k: p.grad.clone() for k, p in mod.named_parameters()}))
+        finally:
+            K.GATENC_FUSED = True
+    (yf, dxf, gf), (yr, dxr, gr) = res
+    close(yf, yr.cpu().numpy(), rtol=2e-5, what="fused out")
+    close(dxf, dxr.cpu().numpy(), rtol=1e-4, what="fused dx")
+    fl = 1e-2 * max(float(g.abs().max()) for g in gr.values())
+    for k in gr:
+        close(gf[k], gr[k].cpu().numpy(), rtol=2e-4, floor=fl, what="fused d" + k)
