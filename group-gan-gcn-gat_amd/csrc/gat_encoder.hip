@@ -32,16 +32,54 @@ namespace sgg {
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
+// forward 1024 threads (16 waves: attention rows and output elements of a
+// 20-ped scene are ~1 per wave / thread, so the dependent chains overlap);
+// the same for the backward
+constexpr int kFwdThreads = 1024, kBwdThreads = 1024;
+constexpr int kMaxWaves = kFwdThreads / 64;
 constexpr int FI = 40, FH = 72, FO = 16, FE = 24;   // GATEncoder dims (models.py:242-244)
 constexpr int P40 = FI + 1, P72 = FH + 1, P16 = FO + 1;
+
+// LDS image of the weights: W (K x N) rows at pitch N + 1 (odd: a column walk
+// across rows, lane = row, is bank-conflict free; a row walk is contiguous)
+constexpr int PW72 = FH + 1, PW16 = FO + 1, PWE = 2 * FO + 1;
+__host__ __device__ inline int weights_floats(int nh) {
+  return nh * (FI * PW72 + 2 * FH) + (FH * nh * PW16 + 2 * FO) + nh * (FO * PW72 + 2 * FH) + (FH * nh * PW16 + 2 * FO) +
+         FE * PWE + FE;
+}
+
+struct LW {
+  const float* Wi[kGatEncMaxHeads];
+  const float* ai[kGatEncMaxHeads];
+  const float* Wio;
+  const float* aio;
+  const float* Wg[kGatEncMaxHeads];
+  const float* ag[kGatEncMaxHeads];
+  const float* Wgo;
+  const float* ago;
+  const float* Woe;
+  const float* boe;
+};
+
+// copy a K x N row-major global matrix to LDS at pitch N + 1
+__device__ inline float* stage_mat(float* dst, const float* __restrict__ src, int K, int N, int nthreads) {
+  for (int e = threadIdx.x; e < K * N; e += nthreads) {
+    const int k = e / N, c = e - k * N;
+    dst[k * (N + 1) + c] = src[e];
+  }
+  return dst + K * (N + 1);
+}
+__device__ inline float* stage_vec(float* dst, const float* __restrict__ src, int n, int nthreads) {
+  for (int e = threadIdx.x; e < n; e += nthreads) dst[e] = src[e];
+  return dst + n;
+}
 
 struct Layout {
   // float offsets into the workgroup's LDS
   int X, H1, yI, preI, gin, G1, preG, gout, Wh, s, t, ds, dt, att;   // forward
   int dWh, dH, dI, dG, dpre, attm;                                    // backward
   int ints;       // int region: lab (float), gidl, grank, cnt, M
+  int wts;        // the module's weights, staged once per workgroup (odd row pitches)
   int total;      // floats
   int PH, NP, NPP;
 };
@@ -66,7 +104,7 @@ __host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
   L.t = take(np);
   L.ds = take(np);
   L.dt = take(np);
-  L.att = take(kWaves * 64);
+  L.att = take(kMaxWaves * 64);
   if (bwd) {
     L.dWh = take(np * P72);
     L.dH = take(np * L.PH);
@@ -78,6 +116,7 @@ __host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
     L.dWh = L.dH = L.dI = L.dG = L.dpre = L.attm = 0;
   }
   L.ints = take(5 * np + 4);
+  L.wts = take(weights_floats(nh));
   L.total = o;
   return L;
 }
@@ -111,45 +150,45 @@ __host__ __device__ inline PLayout make_playout(int nh) {
 
 __device__ __forceinline__ float lrelu(float x, float a) { return x > 0.f ? x : a * x; }
 
-// out[r][c] = sum_k in[r][k] W[k][c]   (W: K x N row-major, global)
-__device__ void lin(const float* in, int ldi, int rows, int K, const float* __restrict__ W, int N, float* out,
-                    int ldo) {
-  for (int e = threadIdx.x; e < rows * N; e += kThreads) {
+// out[r][c] = sum_k in[r][k] W[k][c]   (W: K x N in LDS at pitch ldw, K % 4 == 0)
+__device__ void lin(const float* in, int ldi, int rows, int K, const float* W, int ldw, int N, float* out, int ldo) {
+  for (int e = threadIdx.x; e < rows * N; e += blockDim.x) {
     const int r = e / N, c = e - r * N;
     const float* x = in + r * ldi;
-    float a0 = 0.f, a1 = 0.f;
-    int k = 0;
-    for (; k + 1 < K; k += 2) {
-      a0 = fmaf(x[k], W[k * N + c], a0);
-      a1 = fmaf(x[k + 1], W[(k + 1) * N + c], a1);
+    const float* w = W + c;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int k = 0; k < K; k += 4) {
+      a0 = fmaf(x[k], w[k * ldw], a0);
+      a1 = fmaf(x[k + 1], w[(k + 1) * ldw], a1);
+      a2 = fmaf(x[k + 2], w[(k + 2) * ldw], a2);
+      a3 = fmaf(x[k + 3], w[(k + 3) * ldw], a3);
     }
-    if (k < K) a0 = fmaf(x[k], W[k * N + c], a0);
-    out[r * ldo + c] = a0 + a1;
+    out[r * ldo + c] = (a0 + a1) + (a2 + a3);
   }
 }
 
-// out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin)
-__device__ void lin_t(const float* d, int ldd, int rows, int N, const float* __restrict__ W, int K, float* out,
-                      int ldo, bool acc) {
-  for (int e = threadIdx.x; e < rows * K; e += kThreads) {
+// out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin; N % 4 == 0)
+__device__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, int ldw, int K, float* out, int ldo,
+                      bool acc) {
+  for (int e = threadIdx.x; e < rows * K; e += blockDim.x) {
     const int r = e / K, k = e - r * K;
     const float* dr = d + r * ldd;
-    const float* wr = W + k * N;
-    float a0 = 0.f, a1 = 0.f;
-    int c = 0;
-    for (; c + 1 < N; c += 2) {
+    const float* wr = W + k * ldw;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int c = 0; c < N; c += 4) {
       a0 = fmaf(dr[c], wr[c], a0);
       a1 = fmaf(dr[c + 1], wr[c + 1], a1);
+      a2 = fmaf(dr[c + 2], wr[c + 2], a2);
+      a3 = fmaf(dr[c + 3], wr[c + 3], a3);
     }
-    if (c < N) a0 = fmaf(dr[c], wr[c], a0);
-    const float v = a0 + a1;
+    const float v = (a0 + a1) + (a2 + a3);
     out[r * ldo + k] = acc ? out[r * ldo + k] + v : v;
   }
 }
 
 // dst[k][c] = sum_r x[r][k] d[r][c]   (weight gradient of lin, to the slab)
 __device__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, int ldd, int N, float* dst) {
-  for (int e = threadIdx.x; e < K * N; e += kThreads) {
+  for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
     const int k = e / N, c = e - k * N;
     float a0 = 0.f, a1 = 0.f;
     int r = 0;
@@ -163,8 +202,8 @@ __device__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, 
 }
 
 // s_i = a[:F].Wh_i, t_i = a[F:].Wh_i
-__device__ void scores(const float* Wh, int ldw, int rows, int F, const float* __restrict__ a, float* s, float* t) {
-  for (int e = threadIdx.x; e < 2 * rows; e += kThreads) {
+__device__ void scores(const float* Wh, int ldw, int rows, int F, const float* a, float* s, float* t) {
+  for (int e = threadIdx.x; e < 2 * rows; e += blockDim.x) {
     const int r = e >> 1, w = e & 1;
     const float* av = a + w * F;
     const float* x = Wh + r * ldw;
@@ -204,16 +243,23 @@ __device__ void att_fwd(const float* Wh, int ldw, int rows, int F, const int* gi
                         float alpha, int epi, float* out, int ldo, float* pre, int ldp, float* attw) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* aw = attw + wave * 64;
-  for (int i = wave; i < rows; i += kWaves) {
+  for (int i = wave; i < rows; i += (int)(blockDim.x >> 6)) {
     aw[lane] = att_row(i, rows, gidl, s, t, alpha, lane);
     wave_lds_sync();
     float hv[2], zv[2], zmax = -INFINITY;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int f = lane + 64 * c;
-      float acc = 0.f;
-      if (f < F)
-        for (int j = 0; j < rows; ++j) acc = fmaf(aw[j], Wh[j * ldw + f], acc);
+      float acc = 0.f, acc2 = 0.f;
+      if (f < F) {
+        int j = 0;
+        for (; j + 1 < rows; j += 2) {
+          acc = fmaf(aw[j], Wh[j * ldw + f], acc);
+          acc2 = fmaf(aw[j + 1], Wh[(j + 1) * ldw + f], acc2);
+        }
+        if (j < rows) acc = fmaf(aw[j], Wh[j * ldw + f], acc);
+        acc += acc2;
+      }
       hv[c] = acc;
       zv[c] = elu(acc);
       if (f < F) zmax = fmaxf(zmax, zv[c]);
@@ -242,7 +288,7 @@ __device__ void att_fwd(const float* Wh, int ldw, int rows, int F, const int* gi
 // gradient through the epilogue: d (in: d out, out: d pre), one wave per row
 __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, int F, int epi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = wave; i < rows; i += kWaves) {
+  for (int i = wave; i < rows; i += (int)(blockDim.x >> 6)) {
     float dv[2], hv[2], zv[2];
     float zmax = -INFINITY, sdy = 0.f;
 #pragma unroll
@@ -281,25 +327,25 @@ __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, 
 // attention layer backward.  dpre: gradient of the aggregate (rows x F);
 // writes dWh (rows x F) and the a-gradient (2F) to da; attm scratch rows x npp
 __device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gidl, float* s, float* t, float alpha,
-                        const float* __restrict__ a, const float* dpre, int ldd, float* dWh, int lddw, float* ds,
+                        const float* a, const float* dpre, int ldd, float* dWh, int lddw, float* ds,
                         float* dt, float* attm, int npp, float* da) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   scores(Wh, ldw, rows, F, a, s, t);
   __syncthreads();
-  for (int i = wave; i < rows; i += kWaves) {
+  for (int i = wave; i < rows; i += (int)(blockDim.x >> 6)) {
     const float v = att_row(i, rows, gidl, s, t, alpha, lane);
     if (lane < rows) attm[i * npp + lane] = v;
   }
   __syncthreads();
   // attention-weighted part: dWh_j = sum_i att_ij dpre_i
-  for (int e = threadIdx.x; e < rows * F; e += kThreads) {
+  for (int e = threadIdx.x; e < rows * F; e += blockDim.x) {
     const int j = e / F, f = e - j * F;
     float acc = 0.f;
     for (int i = 0; i < rows; ++i) acc = fmaf(attm[i * npp + j], dpre[i * ldd + f], acc);
     dWh[j * lddw + f] = acc;
   }
   __syncthreads();   // attm is overwritten with dz below
-  for (int i = wave; i < rows; i += kWaves) {
+  for (int i = wave; i < rows; i += (int)(blockDim.x >> 6)) {
     const int j = lane;
     float datt = 0.f, at = 0.f;
     if (j < rows) {
@@ -317,18 +363,18 @@ __device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gi
     if (lane == 0) ds[i] = dsum;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < rows; j += kThreads) {
+  for (int j = threadIdx.x; j < rows; j += blockDim.x) {
     float acc = 0.f;
     for (int i = 0; i < rows; ++i) acc += attm[i * npp + j];
     dt[j] = acc;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < rows * F; e += kThreads) {
+  for (int e = threadIdx.x; e < rows * F; e += blockDim.x) {
     const int j = e / F, f = e - j * F;
     dWh[j * lddw + f] += ds[j] * a[f] + dt[j] * a[F + f];
   }
   // da[f] = sum_i ds_i Wh_i[f], da[F + f] = sum_j dt_j Wh_j[f]
-  for (int e = threadIdx.x; e < 2 * F; e += kThreads) {
+  for (int e = threadIdx.x; e < 2 * F; e += blockDim.x) {
     const int w = e / F, f = e - w * F;
     const float* g = w ? dt : ds;
     float acc = 0.f;
@@ -339,7 +385,7 @@ __device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gi
 }
 
 template <bool BWD>
-__global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
+__global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel(GatEncArgs p) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const Layout L = make_layout(p.np, p.nh, BWD);
   const PLayout PL = make_playout(p.nh);
@@ -365,19 +411,38 @@ __global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
   float* ginv = reinterpret_cast<float*>(cnt + L.NP);
   int* Mp = reinterpret_cast<int*>(ginv + L.NP);
   const int tid = threadIdx.x;
+  LW lw;
+  {
+    float* q = sm + L.wts;
+    for (int h = 0; h < nh; ++h) {
+      lw.Wi[h] = q; q = stage_mat(q, p.w.Wi[h], FI, FH, blockDim.x);
+      lw.ai[h] = q; q = stage_vec(q, p.w.ai[h], 2 * FH, blockDim.x);
+    }
+    lw.Wio = q; q = stage_mat(q, p.w.Wio, FH * nh, FO, blockDim.x);
+    lw.aio = q; q = stage_vec(q, p.w.aio, 2 * FO, blockDim.x);
+    for (int h = 0; h < nh; ++h) {
+      lw.Wg[h] = q; q = stage_mat(q, p.w.Wg[h], FO, FH, blockDim.x);
+      lw.ag[h] = q; q = stage_vec(q, p.w.ag[h], 2 * FH, blockDim.x);
+    }
+    lw.Wgo = q; q = stage_mat(q, p.w.Wgo, FH * nh, FO, blockDim.x);
+    lw.ago = q; q = stage_vec(q, p.w.ago, 2 * FO, blockDim.x);
+    lw.Woe = q; q = stage_mat(q, p.w.Woe, FE, 2 * FO, blockDim.x);
+    lw.boe = q; q = stage_vec(q, p.w.boe, FE, blockDim.x);
+  }
+  // (the first scene's input loads are followed by a barrier before any use)
 
   for (int sc = blockIdx.x; sc < p.S; sc += gridDim.x) {
     const int o = p.scene_off[sc];
     const int n = p.scene_off[sc + 1] - o;
     if (n <= 0) continue;   // uniform over the workgroup
     // ---- inputs and group structure ------------------------------------
-    for (int e = tid; e < n * FI; e += kThreads) {
+    for (int e = tid; e < n * FI; e += blockDim.x) {
       const int r = e / FI, k = e - r * FI;
       X[r * P40 + k] = p.X[(size_t)(o + r) * p.ldx + k];
     }
-    for (int i = tid; i < n; i += kThreads) lab[i] = p.labels[o + i];
+    for (int i = tid; i < n; i += blockDim.x) lab[i] = p.labels[o + i];
     __syncthreads();
-    for (int i = tid; i < n; i += kThreads) {
+    for (int i = tid; i < n; i += blockDim.x) {
       int g = i;
       const float li = lab[i];
       if (li != 0.f)
@@ -386,7 +451,7 @@ __global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
       gidl[i] = g;
     }
     __syncthreads();
-    for (int i = tid; i < n; i += kThreads) {
+    for (int i = tid; i < n; i += blockDim.x) {
       int r = 0;
       for (int j = 0; j < gidl[i]; ++j) r += gidl[j] == j;
       grank[i] = r;
@@ -405,21 +470,21 @@ __global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
 
     // ---- intra GAT: heads (40 -> 72, ELU), out (72 nh -> 16, ELU, log_softmax)
     for (int h = 0; h < nh; ++h) {
-      lin(X, P40, n, FI, p.w.Wi[h], FH, Wh, P72);
+      lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
       __syncthreads();
-      scores(Wh, P72, n, FH, p.w.ai[h], s, t);
+      scores(Wh, P72, n, FH, lw.ai[h], s, t);
       __syncthreads();
       att_fwd(Wh, P72, n, FH, gidl, s, t, p.alpha, 1, H1 + h * FH, PH, nullptr, 0, attw);
       __syncthreads();
     }
-    lin(H1, PH, n, FH * nh, p.w.Wio, FO, Wh, P72);
+    lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72);
     __syncthreads();
-    scores(Wh, P72, n, FO, p.w.aio, s, t);
+    scores(Wh, P72, n, FO, lw.aio, s, t);
     __syncthreads();
     att_fwd(Wh, P72, n, FO, gidl, s, t, p.alpha, 2, yI, P16, preI, P16, attw);
     __syncthreads();
     // ---- group mean (R intra) ------------------------------------------
-    for (int e = tid; e < M * FO; e += kThreads) {
+    for (int e = tid; e < M * FO; e += blockDim.x) {
       const int g = e / FO, f = e - g * FO;
       float acc = 0.f;
       for (int i = 0; i < n; ++i)
@@ -429,28 +494,28 @@ __global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
     __syncthreads();
     // ---- inter GAT on the complete graph of the M groups ----------------
     for (int h = 0; h < nh; ++h) {
-      lin(gin, P16, M, FO, p.w.Wg[h], FH, Wh, P72);
+      lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
       __syncthreads();
-      scores(Wh, P72, M, FH, p.w.ag[h], s, t);
+      scores(Wh, P72, M, FH, lw.ag[h], s, t);
       __syncthreads();
       att_fwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, 1, G1 + h * FH, PH, nullptr, 0, attw);
       __syncthreads();
     }
-    lin(G1, PH, M, FH * nh, p.w.Wgo, FO, Wh, P72);
+    lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72);
     __syncthreads();
-    scores(Wh, P72, M, FO, p.w.ago, s, t);
+    scores(Wh, P72, M, FO, lw.ago, s, t);
     __syncthreads();
     att_fwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, 2, gout, P16, preG, P16, attw);
     __syncthreads();
 
     if (!BWD) {
       // ---- out = Woe [intra, gout[g(i)] / |g(i)|] + boe ------------------
-      for (int e = tid; e < n * FE; e += kThreads) {
+      for (int e = tid; e < n * FE; e += blockDim.x) {
         const int i = e / FE, c = e - i * FE;
-        const float* wr = p.w.Woe + c * 2 * FO;
+        const float* wr = lw.Woe + c * PWE;
         const float* gi = gout + grank[i] * P16;
         const float sc_i = ginv[i];
-        float a0 = p.w.boe[c], a1 = 0.f;
+        float a0 = lw.boe[c], a1 = 0.f;
         for (int f = 0; f < FO; ++f) {
           a0 = fmaf(wr[f], yI[i * P16 + f], a0);
           a1 = fmaf(wr[FO + f], gi[f] * sc_i, a1);
@@ -471,14 +536,14 @@ __global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
     float* slab = p.slab + (size_t)sc * PL.total;
     const float* dy = p.dy + (size_t)o * p.lddy;
     // out embedding: d[intra | inter] = dy Woe; dWoe = dy^T [intra | inter]; dboe = sum dy
-    for (int e = tid; e < n * 2 * FO; e += kThreads) {
+    for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
       const int i = e / (2 * FO), c = e - i * 2 * FO;
       float acc = 0.f;
-      for (int k = 0; k < FE; ++k) acc = fmaf(dy[i * p.lddy + k], p.w.Woe[k * 2 * FO + c], acc);
+      for (int k = 0; k < FE; ++k) acc = fmaf(dy[i * p.lddy + k], lw.Woe[k * PWE + c], acc);
       if (c < FO) dI[i * P16 + c] = acc;
       else dpre[i * P16 + c - FO] = acc;   // d inter (scratch)
     }
-    for (int e = tid; e < FE * 2 * FO; e += kThreads) {
+    for (int e = tid; e < FE * 2 * FO; e += blockDim.x) {
       const int k = e / (2 * FO), c = e - k * 2 * FO;
       float acc = 0.f;
       for (int i = 0; i < n; ++i) {
@@ -487,14 +552,14 @@ __global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
       }
       slab[PL.Woe + e] = acc;
     }
-    for (int k = tid; k < FE; k += kThreads) {
+    for (int k = tid; k < FE; k += blockDim.x) {
       float acc = 0.f;
       for (int i = 0; i < n; ++i) acc += dy[i * p.lddy + k];
       slab[PL.boe + k] = acc;
     }
     __syncthreads();
     // un-pool backward: d gout[g] = sum_{i in g} d inter_i / |g|
-    for (int e = tid; e < M * FO; e += kThreads) {
+    for (int e = tid; e < M * FO; e += blockDim.x) {
       const int g = e / FO, f = e - g * FO;
       float acc = 0.f;
       for (int i = 0; i < n; ++i)
@@ -504,61 +569,61 @@ __global__ void __launch_bounds__(kThreads) gatenc_kernel(GatEncArgs p) {
     __syncthreads();
     // ---- inter out layer ----
     epi_bwd(dG, P16, preG, P16, M, FO, 2);
-    lin(G1, PH, M, FH * nh, p.w.Wgo, FO, Wh, P72);
+    lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72);
     __syncthreads();
-    att_bwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, p.w.ago, dG, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.ago);
+    att_bwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, lw.ago, dG, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.ago);
     wgrad(G1, PH, M, FH * nh, dWh, P72, FO, slab + PL.Wgo);
-    lin_t(dWh, P72, M, FO, p.w.Wgo, FH * nh, dH, PH, false);
+    lin_t(dWh, P72, M, FO, lw.Wgo, PW16, FH * nh, dH, PH, false);
     __syncthreads();
     // ---- inter heads ----
-    for (int e = tid; e < M * FO; e += kThreads) dG[(e / FO) * P16 + e % FO] = 0.f;   // becomes d gin
+    for (int e = tid; e < M * FO; e += blockDim.x) dG[(e / FO) * P16 + e % FO] = 0.f;   // becomes d gin
     for (int h = 0; h < nh; ++h) {
       // ELU backward from the stored output: elu'(x) = 1 (y > 0) | y + 1
-      for (int e = tid; e < M * FH; e += kThreads) {
+      for (int e = tid; e < M * FH; e += blockDim.x) {
         const int r = e / FH, f = e - r * FH;
         const float yv = G1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      lin(gin, P16, M, FO, p.w.Wg[h], FH, Wh, P72);
+      lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
       __syncthreads();
-      att_bwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, p.w.ag[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
+      att_bwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, lw.ag[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
               slab + PL.ag[h]);
       wgrad(gin, P16, M, FO, dWh, P72, FH, slab + PL.Wg[h]);
-      lin_t(dWh, P72, M, FH, p.w.Wg[h], FO, dG, P16, true);
+      lin_t(dWh, P72, M, FH, lw.Wg[h], PW72, FO, dG, P16, true);
       __syncthreads();
     }
     // group-mean backward: d intra_i += d gin[g(i)] / |g(i)|
-    for (int e = tid; e < n * FO; e += kThreads) {
+    for (int e = tid; e < n * FO; e += blockDim.x) {
       const int i = e / FO, f = e - i * FO;
       dI[i * P16 + f] = fmaf(ginv[i], dG[grank[i] * P16 + f], dI[i * P16 + f]);
     }
     __syncthreads();
     // ---- intra out layer ----
     epi_bwd(dI, P16, preI, P16, n, FO, 2);
-    lin(H1, PH, n, FH * nh, p.w.Wio, FO, Wh, P72);
+    lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72);
     __syncthreads();
-    att_bwd(Wh, P72, n, FO, gidl, s, t, p.alpha, p.w.aio, dI, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.aio);
+    att_bwd(Wh, P72, n, FO, gidl, s, t, p.alpha, lw.aio, dI, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.aio);
     wgrad(H1, PH, n, FH * nh, dWh, P72, FO, slab + PL.Wio);
-    lin_t(dWh, P72, n, FO, p.w.Wio, FH * nh, dH, PH, false);
+    lin_t(dWh, P72, n, FO, lw.Wio, PW16, FH * nh, dH, PH, false);
     __syncthreads();
     // ---- intra heads ----
     float* dXo = p.dX + (size_t)o * p.lddx;
     for (int h = 0; h < nh; ++h) {
-      for (int e = tid; e < n * FH; e += kThreads) {
+      for (int e = tid; e < n * FH; e += blockDim.x) {
         const int r = e / FH, f = e - r * FH;
         const float yv = H1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      lin(X, P40, n, FI, p.w.Wi[h], FH, Wh, P72);
+      lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
       __syncthreads();
-      att_bwd(Wh, P72, n, FH, gidl, s, t, p.alpha, p.w.ai[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
+      att_bwd(Wh, P72, n, FH, gidl, s, t, p.alpha, lw.ai[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
               slab + PL.ai[h]);
       wgrad(X, P40, n, FI, dWh, P72, FH, slab + PL.Wi[h]);
       // dX (global) accumulates over heads in a fixed order
-      for (int e = tid; e < n * FI; e += kThreads) {
+      for (int e = tid; e < n * FI; e += blockDim.x) {
         const int r = e / FI, k = e - r * FI;
         const float* dr = dWh + r * P72;
-        const float* wr = p.w.Wi[h] + k * FH;
+        const float* wr = lw.Wi[h] + k * PW72;
         float a0 = 0.f, a1 = 0.f;
         for (int c = 0; c < FH; c += 2) {
           a0 = fmaf(dr[c], wr[c], a0);
@@ -629,7 +694,7 @@ extern "C" int sgg_gatenc_fwd(const GatEncArgs* args, void* stream) {
   if (rc) return rc;
   if (args->S == 0) return 0;
   const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 0);
-  hipLaunchKernelGGL(gatenc_kernel<false>, dim3(args->S < 65536 ? args->S : 65536), dim3(kThreads), lds,
+  hipLaunchKernelGGL(gatenc_kernel<false>, dim3(args->S < 65536 ? args->S : 65536), dim3(kFwdThreads), lds,
                      (hipStream_t)stream, *args);
   SGG_RETURN_LAUNCH("sgg_gatenc_fwd");
 }
@@ -639,7 +704,7 @@ extern "C" int sgg_gatenc_bwd(const GatEncArgs* args, void* stream) {
   if (rc) return rc;
   if (args->S == 0) return 0;
   const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 1);
-  hipLaunchKernelGGL(gatenc_kernel<true>, dim3(args->S < 65536 ? args->S : 65536), dim3(kThreads), lds,
+  hipLaunchKernelGGL(gatenc_kernel<true>, dim3(args->S < 65536 ? args->S : 65536), dim3(kBwdThreads), lds,
                      (hipStream_t)stream, *args);
   SGG_RETURN_LAUNCH("sgg_gatenc_bwd");
 }
