@@ -1,0 +1,225 @@
+// The small data-movement and loss steps around the G / D modules of a
+// training iteration (reference scripts/train.py:395-484, sgan/losses.py,
+// sgan/models.py:814-850), one launch each instead of the 3..15 elementwise /
+// index / reduction launches the reference's torch expressions take:
+//
+//   sgg_traj_cat      the discriminator input traj_rel = cat(obs_rel, pred)
+//                     (train.py:409-415, 468-470), fake and real halves side
+//                     by side in one call (no relative_to_abs: the
+//                     discriminator reads only traj[0] and traj_rel)
+//   sgg_decoder_init  add_noise (models.py:814-850, 'global' mix) for
+//                     `copies` samples of the batch: h0 = [ctx | z_scene],
+//                     plus the decoder's first input (the last observed
+//                     displacement), replicated sample-major
+//   sgg_l2_select     best-of-k (train.py:443-464): per scene the sample
+//                     with the smallest sum over its peds of l2_loss(raw)
+//   sgg_l2_loss_fwd/bwd  sum over scenes of  l2_loss(raw) summed over the
+//                     scene's peds / sum(loss_mask) (train.py:459-464)
+// All sums run in a fixed order (deterministic).
+#include "sgg_common.h"
+
+namespace sgg {
+
+namespace {
+
+__global__ void __launch_bounds__(256) traj_cat_kernel(const float* __restrict__ head, int ldh, int T0,
+                                                       const float* __restrict__ a, int lda,
+                                                       const float* __restrict__ b, int ldb, int T1, int B,
+                                                       float* __restrict__ out) {
+  const int NB = b ? 2 * B : B;
+  const int total = (T0 + T1) * NB;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int t = e / NB, p = e - t * NB;
+    const float* src;
+    if (t < T0) {
+      src = head + (size_t)t * ldh + 2 * (p < B ? p : p - B);
+    } else if (p < B) {
+      src = a + (size_t)(t - T0) * lda + 2 * p;
+    } else {
+      src = b + (size_t)(t - T0) * ldb + 2 * (p - B);
+    }
+    reinterpret_cast<float2*>(out)[e] = *reinterpret_cast<const float2*>(src);
+  }
+}
+
+__global__ void __launch_bounds__(256) decoder_init_kernel(const float* __restrict__ ctx, int ldc, int Dc,
+                                                           const float* __restrict__ z, int nz,
+                                                           const int64_t* __restrict__ best, int first_k,
+                                                           int copies, const int32_t* __restrict__ ped_scene,
+                                                           int S, int B, const float* __restrict__ last_rel,
+                                                           float* __restrict__ h0, float* __restrict__ rel0) {
+  const int D = Dc + nz;
+  const int total = copies * B * D;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int row = e / D, c = e - row * D;
+    const int r = row / B, p = row - r * B;
+    float v;
+    if (c < Dc) {
+      v = ctx[(size_t)p * ldc + c];
+    } else {
+      const int s = ped_scene[p];
+      const int k = (best && r == 0) ? (int)best[s] : first_k + r - (best ? 1 : 0);
+      v = z[((size_t)k * S + s) * nz + (c - Dc)];
+    }
+    h0[e] = v;
+    if (c < 2) rel0[(size_t)row * 2 + c] = last_rel[(size_t)p * 2 + c];
+  }
+}
+
+// one workgroup per scene: sum over (sample, ped, step) of mask (gt - pred)^2,
+// argmin over the k samples (first minimum, as torch.argmin)
+__global__ void __launch_bounds__(256) l2_select_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                        const float* __restrict__ mask, int ldm,
+                                                        const int32_t* __restrict__ scene_off, int T, int B, int k,
+                                                        int64_t* __restrict__ best) {
+  __shared__ float part[4][64];
+  const int s = blockIdx.x;
+  const int o = scene_off[s], n = scene_off[s + 1] - o;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r = wave; r < k; r += 4) {
+    float acc = 0.f;
+    for (int e = lane; e < n * T; e += 64) {
+      const int i = e / T, t = e - i * T;
+      const int p = o + i;
+      const float2 g = reinterpret_cast<const float2*>(gt)[(size_t)t * B + p];
+      const float2 q = reinterpret_cast<const float2*>(pred)[((size_t)t * k + r) * B + p];
+      const float dx = g.x - q.x, dy = g.y - q.y;
+      acc = fmaf(mask[(size_t)p * ldm + t], fmaf(dx, dx, dy * dy), acc);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) part[r & 3][r >> 2] = acc;   // k <= 256
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int bi = 0;
+    float bv = part[0][0];
+    for (int r = 1; r < k; ++r) {
+      const float v = part[r & 3][r >> 2];
+      if (v < bv) { bv = v; bi = r; }
+    }
+    best[s] = bi;
+  }
+}
+
+// single workgroup: per scene (one wave each) sum of mask (gt - pred)^2 and of
+// the mask, term = w * l2 / msum, loss = sum of the terms in scene order
+__global__ void __launch_bounds__(1024) l2_loss_fwd_kernel(const float* __restrict__ pred, int ldp,
+                                                           const float* __restrict__ gt,
+                                                           const float* __restrict__ mask, int ldm,
+                                                           const int32_t* __restrict__ scene_off, int S, int T,
+                                                           int B, float w, float* __restrict__ loss,
+                                                           float* __restrict__ msum_out,
+                                                           float* __restrict__ term) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int s = wave; s < S; s += nw) {
+    const int o = scene_off[s], n = scene_off[s + 1] - o;
+    float acc = 0.f, ms = 0.f;
+    for (int e = lane; e < n * T; e += 64) {
+      const int i = e / T, t = e - i * T;
+      const int p = o + i;
+      const float m = mask[(size_t)p * ldm + t];
+      const float2 g = reinterpret_cast<const float2*>(gt)[(size_t)t * B + p];
+      const float2 q = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
+      const float dx = g.x - q.x, dy = g.y - q.y;
+      acc = fmaf(m, fmaf(dx, dx, dy * dy), acc);
+      ms += m;
+    }
+    acc = wave_sum(acc);
+    ms = wave_sum(ms);
+    if (lane == 0) {
+      msum_out[s] = ms;
+      term[s] = (w * acc) / ms;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int s = 0; s < S; ++s) tot += term[s];
+    *loss = tot;
+  }
+}
+
+__global__ void __launch_bounds__(256) l2_loss_bwd_kernel(const float* __restrict__ pred, int ldp,
+                                                          const float* __restrict__ gt,
+                                                          const float* __restrict__ mask, int ldm,
+                                                          const int32_t* __restrict__ ped_scene,
+                                                          const float* __restrict__ msum, int T, int B, float w,
+                                                          const float* __restrict__ gout, float* __restrict__ dpred,
+                                                          int ldd) {
+  const float g = *gout * w * -2.f;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < T * B; e += gridDim.x * blockDim.x) {
+    const int t = e / B, p = e - t * B;
+    const float m = mask[(size_t)p * ldm + t];
+    const float2 gv = reinterpret_cast<const float2*>(gt)[e];
+    const float2 q = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
+    const float c = g * m / msum[ped_scene[p]];
+    *reinterpret_cast<float2*>(dpred + (size_t)t * ldd + 2 * p) = make_float2(c * (gv.x - q.x), c * (gv.y - q.y));
+  }
+}
+
+int grid_for(long long n, int per) {
+  const long long g = (n + per - 1) / per;
+  return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+}  // namespace
+
+}  // namespace sgg
+
+using namespace sgg;
+
+extern "C" int sgg_traj_cat(const float* head, int ldh, int T0, const float* a, int lda, const float* b, int ldb,
+                            int T1, int B, float* out, void* stream) {
+  SGG_CHECK_ARG(head && a && out, "sgg_traj_cat: null pointer");
+  SGG_CHECK_ARG(T0 >= 0 && T1 >= 0 && B >= 0 && ldh >= 2 * B && lda >= 2 * B && (!b || ldb >= 2 * B),
+                "sgg_traj_cat: bad sizes");
+  const long long total = (long long)(T0 + T1) * (b ? 2 * B : B);
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(traj_cat_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, head, ldh, T0, a,
+                     lda, b, ldb, T1, B, out);
+  SGG_RETURN_LAUNCH("sgg_traj_cat");
+}
+
+extern "C" int sgg_decoder_init(const float* ctx, int ldc, int Dc, const float* z, int nz, const int64_t* best,
+                                int first_k, int copies, const int32_t* ped_scene, int S, int B,
+                                const float* last_rel, float* h0, float* rel0, void* stream) {
+  SGG_CHECK_ARG(ctx && ped_scene && last_rel && h0 && rel0 && (nz == 0 || z), "sgg_decoder_init: null pointer");
+  SGG_CHECK_ARG(Dc > 0 && nz >= 0 && ldc >= Dc && copies >= 1 && S >= 0 && B >= 0 && Dc + nz >= 2,
+                "sgg_decoder_init: bad sizes");
+  const long long total = (long long)copies * B * (Dc + nz);
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(decoder_init_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, ctx, ldc, Dc,
+                     z, nz, best, first_k, copies, ped_scene, S, B, last_rel, h0, rel0);
+  SGG_RETURN_LAUNCH("sgg_decoder_init");
+}
+
+extern "C" int sgg_l2_select(const float* pred, const float* gt, const float* mask, int ldm, const int32_t* scene_off,
+                             int S, int T, int B, int k, int64_t* best, void* stream) {
+  SGG_CHECK_ARG(pred && gt && mask && scene_off && best, "sgg_l2_select: null pointer");
+  SGG_CHECK_ARG(S >= 0 && T >= 1 && B >= 0 && k >= 1 && k <= 256 && ldm >= T, "sgg_l2_select: bad sizes");
+  if (S == 0) return 0;
+  hipLaunchKernelGGL(l2_select_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, pred, gt, mask, ldm, scene_off, T,
+                     B, k, best);
+  SGG_RETURN_LAUNCH("sgg_l2_select");
+}
+
+extern "C" int sgg_l2_loss_fwd(const float* pred, int ldp, const float* gt, const float* mask, int ldm,
+                               const int32_t* scene_off, int S, int T, int B, float w, float* loss, float* msum,
+                               float* term_ws, void* stream) {
+  SGG_CHECK_ARG(pred && gt && mask && scene_off && loss && msum && term_ws, "sgg_l2_loss_fwd: null pointer");
+  SGG_CHECK_ARG(S >= 0 && T >= 1 && B >= 0 && ldm >= T && ldp >= 2 * B, "sgg_l2_loss_fwd: bad sizes");
+  hipLaunchKernelGGL(l2_loss_fwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, pred, ldp, gt, mask, ldm,
+                     scene_off, S, T, B, w, loss, msum, term_ws);
+  SGG_RETURN_LAUNCH("sgg_l2_loss_fwd");
+}
+
+extern "C" int sgg_l2_loss_bwd(const float* pred, int ldp, const float* gt, const float* mask, int ldm,
+                               const int32_t* ped_scene, const float* msum, int T, int B, float w, const float* gout,
+                               float* dpred, int ldd, void* stream) {
+  SGG_CHECK_ARG(pred && gt && mask && ped_scene && msum && gout && dpred, "sgg_l2_loss_bwd: null pointer");
+  SGG_CHECK_ARG(T >= 1 && B >= 0 && ldm >= T && ldp >= 2 * B && ldd >= 2 * B, "sgg_l2_loss_bwd: bad sizes");
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(l2_loss_bwd_kernel, dim3(grid_for((long long)T * B, 256)), dim3(256), 0, (hipStream_t)stream,
+                     pred, ldp, gt, mask, ldm, ped_scene, msum, T, B, w, gout, dpred, ldd);
+  SGG_RETURN_LAUNCH("sgg_l2_loss_bwd");
+}

@@ -645,3 +645,112 @@ def bce_pair(scores, split, y_a, y_b, w=1.0):
     scalar targets (python floats or device scalars); split = len -> one term."""
     dev = scores.device
     return _Bce.apply(scores, _scalar_dev(y_a, dev), _scalar_dev(y_b, dev), int(split), w)
+
+
+# ---------------------------------------------------------------------------
+# training-step glue (glue.hip)
+# ---------------------------------------------------------------------------
+class _TrajCat(torch.autograd.Function):
+    """cat over time of head (T0 x B x 2, repeated for both halves when b is
+    given) and a | b (T1 x B x 2 each, side by side); a may be a batch slice
+    of a wider tensor.  Gradient flows to `a` only (the generator output)."""
+
+    @staticmethod
+    def forward(ctx, head, a, b):
+        T0, B = head.shape[0], head.shape[1]
+        T1 = a.shape[0]
+        for t, nm in ((head, "head"), (a, "a")) + (((b, "b"),) if b is not None else ()):
+            _req(t, nm)
+            assert t.shape[1:] == (B, 2) and t.stride(1) == 2 and t.stride(2) == 1, (nm, t.shape, t.stride())
+        NB = 2 * B if b is not None else B
+        out = torch.empty(T0 + T1, NB, 2, device=a.device, dtype=torch.float32)
+        N.check(_lib().sgg_traj_cat(N.ptr(head), head.stride(0), T0, N.ptr(a), a.stride(0), N.ptr(b),
+                                    b.stride(0) if b is not None else 0, T1, B, N.ptr(out), N.stream_ptr()),
+                "sgg_traj_cat")
+        ctx.dims = (T0, B)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        T0, B = ctx.dims
+        return None, dout[T0:, :B], None
+
+
+def traj_cat(head, a, b=None):
+    return _TrajCat.apply(head, a, b)
+
+
+class _DecoderInit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cvec, z, best, first_k, copies, scenes, last_rel):
+        cvec = _rows(cvec, "ctx")
+        B, Dc = cvec.shape
+        nz = z.shape[-1] if z is not None else 0
+        h0 = torch.empty(copies * B, Dc + nz, device=cvec.device, dtype=torch.float32)
+        rel0 = torch.empty(copies * B, 2, device=cvec.device, dtype=torch.float32)
+        zc = _req(z, "z").contiguous() if z is not None else None
+        N.check(_lib().sgg_decoder_init(N.ptr(cvec), cvec.stride(0), Dc, N.ptr(zc), nz, N.ptr(best), int(first_k),
+                                        int(copies), N.ptr(scenes.ped_scene_i32()), scenes.S, B,
+                                        N.ptr(_req(last_rel, "last_rel").contiguous()), N.ptr(h0), N.ptr(rel0),
+                                        N.stream_ptr()), "sgg_decoder_init")
+        ctx.dims = (copies, B, Dc)
+        ctx.mark_non_differentiable(rel0)
+        return h0, rel0
+
+    @staticmethod
+    def backward(ctx, dh0, _drel0):
+        copies, B, Dc = ctx.dims
+        d = dh0.view(copies, B, -1)[:, :, :Dc]
+        return (d[0] if copies == 1 else d.sum(0)), None, None, None, None, None, None
+
+
+def decoder_init(cvec, z, best, first_k, copies, scenes, last_rel):
+    """add_noise (global mix) + the decoder's first input for `copies` samples:
+    z is (K, S, nz); copy r takes sample best[s] (r = 0, when best is given)
+    or first_k + r (- 1 with best).  -> (h0 (copies*B, Dc+nz), rel0)."""
+    return _DecoderInit.apply(cvec, z, best, first_k, copies, scenes, last_rel)
+
+
+def l2_select(pred, gt, mask, scenes, k):
+    """best-of-k sample per scene (train.py:443-464) -> int64 (S,)."""
+    best = torch.empty(scenes.S, device=pred.device, dtype=torch.int64)
+    pred = _req(pred, "pred").contiguous()
+    N.check(_lib().sgg_l2_select(N.ptr(pred), N.ptr(_req(gt, "gt").contiguous()), N.ptr(mask), mask.stride(0),
+                                 N.ptr(scenes.scene_off), scenes.S, gt.shape[0], scenes.B, int(k), N.ptr(best),
+                                 N.stream_ptr()), "sgg_l2_select")
+    return best
+
+
+class _L2Loss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, gt, mask, scenes, w):
+        _req(pred, "pred")
+        assert pred.stride(1) == 2 and pred.stride(2) == 1 and mask.stride(1) == 1
+        gt = _req(gt, "gt").contiguous()
+        T, B = gt.shape[0], gt.shape[1]
+        loss = torch.empty((), device=pred.device, dtype=torch.float32)
+        msum = torch.empty(scenes.S, device=pred.device, dtype=torch.float32)
+        term = torch.empty(scenes.S, device=pred.device, dtype=torch.float32)
+        N.check(_lib().sgg_l2_loss_fwd(N.ptr(pred), pred.stride(0), N.ptr(gt), N.ptr(mask), mask.stride(0),
+                                       N.ptr(scenes.scene_off), scenes.S, T, B, float(w), N.ptr(loss), N.ptr(msum),
+                                       N.ptr(term), N.stream_ptr()), "sgg_l2_loss_fwd")
+        ctx.save_for_backward(pred, gt, mask, msum)
+        ctx.meta = (scenes, float(w))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, gt, mask, msum = ctx.saved_tensors
+        scenes, w = ctx.meta
+        T, B = gt.shape[0], gt.shape[1]
+        dpred = torch.empty(T, B, 2, device=pred.device, dtype=torch.float32)
+        N.check(_lib().sgg_l2_loss_bwd(N.ptr(pred), pred.stride(0), N.ptr(gt), N.ptr(mask), mask.stride(0),
+                                       N.ptr(scenes.ped_scene_i32()), N.ptr(msum), T, B, w, N.ptr(g.contiguous()),
+                                       N.ptr(dpred), 2 * B, N.stream_ptr()), "sgg_l2_loss_bwd")
+        return dpred, None, None, None, None
+
+
+def l2_loss(pred, gt, mask, scenes, w=1.0):
+    """sum_s w * l2_loss(pred, gt, mask, 'raw') summed over the peds of s /
+    sum(mask of s) (train.py:459-464 for the selected sample)."""
+    return _L2Loss.apply(pred, gt, mask, scenes, w)

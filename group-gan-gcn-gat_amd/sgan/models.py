@@ -527,12 +527,35 @@ class TrajectoryGenerator(nn.Module):
         return noise_input
 
     def decode(self, noise_input, obs_traj, obs_traj_rel, seq_start_end, user_noise=None, *, scenes=None,
-               copies=1):
+               copies=1, noise_index=None):
         """add_noise + decoder (models.py:909-925) for `copies` samples of the
         batch laid out sample-major (scene s of copy r is scene r*S + s, as
         SceneIndex.repeat builds it); user_noise then holds copies*S rows
-        (global mix).  -> pred_traj_fake_rel (pred_len, copies*B, 2)."""
+        (global mix).  noise_index = (best, first_k): user_noise is the
+        (K, S, nz) stack of K draws and copy r takes draw best[s] (r = 0, if
+        best is given) or first_k + r (- 1 with best).
+        -> pred_traj_fake_rel (pred_len, copies*B, 2)."""
         sc = _scenes(seq_start_end, obs_traj.device, scenes)
+        if (not self.pool_every_timestep and self.noise_dim and self.noise_mix_type == "global"
+                and user_noise is not None and self.num_layers == 1):
+            # one launch builds h0 = [ctx | z_scene] and the first input for all copies
+            nz = self.noise_first_dim
+            if noise_index is None:
+                z, best, first_k = user_noise.reshape(copies, sc.S, nz), None, 0
+            else:
+                (best, first_k), z = noise_index, user_noise
+            z = z.to(noise_input.device, non_blocking=True)
+            h0, rel0 = K.decoder_init(noise_input, z, best, first_k, copies, sc, obs_traj_rel[-1])
+            h, rel = K.lstm_sequence(rel0, self.decoder.decoder, self.decoder.spatial_embedding, h0=h0, c0=None,
+                                     proj=self.decoder.hidden2pos, decoder=True, T=self.pred_len)
+            return rel
+        if noise_index is not None and user_noise is not None:
+            best, first_k = noise_index
+            zk = user_noise.to(noise_input.device)
+            ar = torch.arange(sc.S, device=zk.device)
+            parts = [zk[best, ar]] if best is not None else []
+            parts += [zk[first_k + r] for r in range(copies - len(parts))]
+            user_noise = torch.cat(parts, 0)
         last_pos, last_rel = obs_traj[-1], obs_traj_rel[-1]
         if copies > 1:
             if self.pool_every_timestep:

@@ -57,6 +57,14 @@ class SceneIndex:
                 self.device, non_blocking=True)
         return self._ped_scene
 
+    def ped_scene_i32(self):
+        """Scene of every ped as an int32 device tensor."""
+        if getattr(self, "_ped_scene32", None) is None:
+            sizes = np.diff(self.host_off)
+            self._ped_scene32 = torch.from_numpy(np.repeat(np.arange(self.S, dtype=np.int32), sizes)).to(
+                self.device, non_blocking=True)
+        return self._ped_scene32
+
     POOL_TARGET_CHUNKS = 512
     POOL_MAX_GPW = int(__import__("os").environ.get("SGG_POOL_MAX_GPW", "0"))
 

@@ -47,7 +47,6 @@ import torch.distributed as dist
 from . import kernels as K
 from .models import get_noise
 from .scene import SceneIndex
-from .utils import relative_to_abs
 
 
 class TrainArgs:
@@ -63,10 +62,6 @@ class TrainArgs:
         self.g_learning_rate = 1e-4
         self.d_learning_rate = 1e-3
         self.__dict__.update(kw)
-
-
-def _rep(t, k):
-    return t.repeat(1, k, 1) if k > 1 else t
 
 
 def _sse_of(sc):
@@ -110,13 +105,23 @@ class StepInputs:
         self.z_d, self.z_g, self.y = z_d, z_g, y
 
 
+class KernelOps:
+    """The step's glue and loss ops on the HIP kernels (kernels.py); the CPU
+    data-parallel tests plug in a torch restatement of the same interface
+    together with the oracle's models."""
+    traj_cat = staticmethod(K.traj_cat)
+    l2_select = staticmethod(K.l2_select)
+    l2_loss = staticmethod(K.l2_loss)
+    bce_pair = staticmethod(K.bce_pair)
+
+
 class GanTrainer:
-    def __init__(self, G, D, args=None, dp=None, selective_backward=True, capturable=False, bce_pair=None):
-        """bce_pair(scores, split, y_a, y_b, w): the adversarial loss
-        (default: the fused kernel, kernels.bce_pair); the CPU DP tests plug
-        in a torch restatement together with the oracle's models."""
+    def __init__(self, G, D, args=None, dp=None, selective_backward=True, capturable=False, bce_pair=None, ops=None):
+        """ops: KernelOps-like (traj_cat, l2_select, l2_loss, bce_pair);
+        bce_pair(scores, split, y_a, y_b, w) overrides ops.bce_pair."""
         self.G, self.D = G, D
-        self.bce_pair = bce_pair or K.bce_pair
+        self.ops = ops or KernelOps()
+        self.bce_pair = bce_pair or self.ops.bce_pair
         self.args = args or TrainArgs()
         self.dp = dp or DataParallel()
         self.selective_backward = selective_backward
@@ -162,11 +167,12 @@ class GanTrainer:
         z = inputs.z_d if inputs is not None else self._noise(S_global, s0, s0 + sc.S)
         with torch.no_grad():
             fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
-        fake = relative_to_abs(fake_rel, obs[-1])
-        traj = torch.cat([torch.cat([obs, fake], 0), torch.cat([obs, pred_gt], 0)], 1)
-        traj_rel = torch.cat([torch.cat([obs_rel, fake_rel], 0), torch.cat([obs_rel, pred_gt_rel], 0)], 1)
+        # D reads traj[0] (the start positions, models.py:989) and traj_rel
+        # only: [fake | real] side by side, no relative_to_abs needed
+        traj_rel = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel)
+        start = obs[:1].repeat(1, 2, 1)
         sc2 = sc.repeat(2)
-        scores = self.D(traj, traj_rel, _sse_of(sc2), scenes=sc2)
+        scores = self.D(start, traj_rel, _sse_of(sc2), scenes=sc2)
         if inputs is not None:
             y_real = inputs.y[0]
         else:
@@ -182,72 +188,60 @@ class GanTrainer:
     def g_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """generator_step (train.py:432-484)."""
         a = self.args
-        G, D = self.G, self.D
+        G, D, ops = self.G, self.D, self.ops
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, loss_mask, sse) = batch
         S_global = S_global or sc.S
         B_global = B_global or sc.B
         s0 = shard[0]
         S, B, k = sc.S, sc.B, a.best_k
-        mask = loss_mask[:, a.obs_len:]                                   # (B, pred_len)
+        mask = loss_mask[:, a.obs_len:]                                   # (B, pred_len) view
         if inputs is not None:
-            zs = [inputs.z_g[i] for i in range(k)] if inputs.z_g is not None else [None] * k
+            z_all = inputs.z_g                                            # (k, S, nz) on the device
         else:
             zs = [self._noise(S_global, s0, s0 + S) for _ in range(k)]    # k draws, reference order
-        seg = sc.ped_scene_long()
-        mask_sum = torch.zeros(S, device=obs.device).index_add_(0, seg, mask.sum(1))
-
-        def l2_raw(pred_rel):   # losses.py:52-71 mode='raw', per ped
-            return (mask.unsqueeze(2) * (pred_gt_rel.permute(1, 0, 2) - pred_rel.permute(1, 0, 2)) ** 2).sum(2).sum(1)
-
+            z_all = torch.stack(zs, 0) if zs[0] is not None else None
         use_l2 = a.l2_loss_weight > 0
         # the k samples differ only in the noise appended after the graph
         # module: the encoder / pooling / GAT context runs once (with autograd)
         # and only the decoder rolls out k times
         ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
         if self.selective_backward and k > 1:
-            z_all = torch.cat(zs, 0) if zs[0] is not None else None
-            with torch.no_grad():
-                pred_all = G.decode(ctx.detach(), obs, obs_rel, sse, user_noise=z_all, scenes=sc,
-                                    copies=k).view(a.pred_len, k, B, 2)
-                if use_l2:
-                    l2k = ((pred_gt_rel.unsqueeze(1) - pred_all) ** 2).sum(3) * mask.t().unsqueeze(1)
-                    l2k = l2k.sum(0)                                          # (k, B)
-                    scene_l2 = torch.zeros(k, S, device=obs.device).index_add_(1, seg, l2k)
-                    best = scene_l2.argmin(0)                                 # (S,)
+            best = None
+            if use_l2:
+                with torch.no_grad():
+                    pred_all = G.decode(ctx.detach(), obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k,
+                                        noise_index=(None, 0))
+                    best = ops.l2_select(pred_all, pred_gt_rel, mask, sc, k)   # (S,) int64
             copies = 2 if use_l2 else 1
-            zc = None
-            if z_all is not None:
-                zk = z_all.view(k, S, -1).to(obs.device)
-                parts = ([zk[best, torch.arange(S, device=obs.device)]] if use_l2 else []) + [zk[k - 1]]
-                zc = torch.cat(parts, 0)
-            out = G.decode(ctx, obs, obs_rel, sse, user_noise=zc, scenes=sc, copies=copies)
+            out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=copies,
+                           noise_index=(best, k - 1))
             fake_rel_last = out[:, (copies - 1) * B:]
             fake_rel_best = out[:, :B] if use_l2 else None
         else:
-            z_all = torch.cat(zs, 0) if zs[0] is not None else None
-            out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k)
-            outs = [out[:, i * B:(i + 1) * B] for i in range(k)]
-            fake_rel_last = outs[-1]
+            out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k, noise_index=(None, 0))
+            fake_rel_last = out[:, (k - 1) * B:]
             fake_rel_best = None
-            if use_l2:
-                l2s = torch.stack([l2_raw(o) for o in outs], 0)                # (k, B)
+            if use_l2:   # every sample in the graph: min over k of the per-scene terms
+                seg = sc.ped_scene_long()
+                m = mask.t().unsqueeze(2)
+                l2s = torch.stack([(m * (pred_gt_rel - out[:, i * B:(i + 1) * B]) ** 2).sum((0, 2))
+                                   for i in range(k)], 0)                       # (k, B)
                 scene_l2 = torch.zeros(k, S, device=obs.device).index_add_(1, seg, l2s)
+                mask_sum = torch.zeros(S, device=obs.device).index_add_(0, seg, mask.sum(1))
         terms = []
         if use_l2:
             if fake_rel_best is not None:
-                sl2 = torch.zeros(S, device=obs.device).index_add_(0, seg, a.l2_loss_weight * l2_raw(fake_rel_best))
+                g_l2 = ops.l2_loss(fake_rel_best, pred_gt_rel, mask, sc, a.l2_loss_weight)
             else:
-                sl2 = a.l2_loss_weight * scene_l2.min(0)[0]
-            g_l2 = (sl2 / mask_sum).sum()
+                g_l2 = (a.l2_loss_weight * scene_l2.min(0)[0] / mask_sum).sum()
             terms.append(g_l2)
-        fake_last = relative_to_abs(fake_rel_last, obs[-1])
         # the reference back-propagates into D's weights here and discards the
         # result (optimizer_d never sees it, train.py:478-482): freeze them for
         # this forward so D's backward produces input gradients only
         for p in self.d_params:
             p.requires_grad_(False)
         try:
-            scores = D(torch.cat([obs, fake_last], 0), torch.cat([obs_rel, fake_rel_last], 0), sse, scenes=sc)
+            scores = D(obs[:1], ops.traj_cat(obs_rel, fake_rel_last), sse, scenes=sc)
         finally:
             for p in self.d_params:
                 p.requires_grad_(True)

@@ -320,6 +320,44 @@ int sgg_gatenc_bwd(const SggGatEncArgs* args, void* stream);
 /* out[c] = sum_r slab[r][c] (rows x cols, row-major), rows summed in order. */
 int sgg_slab_reduce(const float* slab, int rows, int cols, float* out, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Training-step glue (scripts/train.py:395-484, sgan/losses.py:52-71,
+ * sgan/models.py:814-850), one launch each.  Trajectory tensors are
+ * time-major rows of (x, y) pairs; ld* are floats per time step.
+ *
+ * sgg_traj_cat: out ((T0 + T1) x NB x 2, NB = B, or 2B when b != NULL) =
+ *   cat over time of head (T0 steps, B peds; repeated for both halves) and
+ *   a (T1 steps, B peds) | b (T1 steps, B peds) side by side -- the
+ *   discriminator input traj_rel of the fake and real trajectories
+ *   (train.py:409-415, 468-470).
+ */
+int sgg_traj_cat(const float* head, int ldh, int T0, const float* a, int lda, const float* b, int ldb, int T1, int B,
+                 float* out, void* stream);
+
+/* sgg_decoder_init: add_noise ('global' mix, models.py:827-850) for `copies`
+ * sample-major copies of the batch: h0[r*B + p] = [ctx[p] (Dc) | z[k, s(p)] (nz)]
+ * with k = best[s] for r = 0 when best != NULL (then k = first_k + r - 1
+ * for r > 0), else k = first_k + r; z is (K x S x nz).  rel0[r*B + p] =
+ * last_rel[p] (the decoder's first input, models.py:915). */
+int sgg_decoder_init(const float* ctx, int ldc, int Dc, const float* z, int nz, const int64_t* best, int first_k,
+                     int copies, const int32_t* ped_scene, int S, int B, const float* last_rel, float* h0,
+                     float* rel0, void* stream);
+
+/* sgg_l2_select: best-of-k (train.py:443-464): pred (T x k*B x 2, sample-major),
+ * gt (T x B x 2), mask (B rows of ldm floats, the pred_len steps); best[s] =
+ * argmin_k sum_{peds of s, t} mask (gt - pred)^2 (first minimum). */
+int sgg_l2_select(const float* pred, const float* gt, const float* mask, int ldm, const int32_t* scene_off, int S,
+                  int T, int B, int k, int64_t* best, void* stream);
+
+/* sgg_l2_loss_fwd: loss = sum_s w * sum_{i in s, t} mask (gt - pred)^2 / msum_s,
+ * msum_s = sum_{i in s, t} mask (train.py:459-464, losses.py:52-71 'raw');
+ * writes msum (S) and uses term_ws (S floats).  sgg_l2_loss_bwd: dpred =
+ * gout * w * -2 mask (gt - pred) / msum_{s(i)}. */
+int sgg_l2_loss_fwd(const float* pred, int ldp, const float* gt, const float* mask, int ldm, const int32_t* scene_off,
+                    int S, int T, int B, float w, float* loss, float* msum, float* term_ws, void* stream);
+int sgg_l2_loss_bwd(const float* pred, int ldp, const float* gt, const float* mask, int ldm, const int32_t* ped_scene,
+                    const float* msum, int T, int B, float w, const float* gout, float* dpred, int ldd, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

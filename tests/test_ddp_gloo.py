@@ -46,8 +46,14 @@ class _Adapt(torch.nn.Module):
             ctx = torch.cat([ctx, g.pool_net(h, seq_start_end, obs_traj[-1])], 1)
         return g.gatencoder(ctx, seq_start_end, obs_traj[-1], obs_traj_g[-1])
 
-    def decode(self, ni, obs_traj, obs_traj_rel, seq_start_end, user_noise=None, scenes=None, copies=1):
+    def decode(self, ni, obs_traj, obs_traj_rel, seq_start_end, user_noise=None, scenes=None, copies=1,
+               noise_index=None):
         g = self.m
+        if noise_index is not None and user_noise is not None:   # (K, S, nz) draws, picked per copy
+            best, first_k = noise_index
+            parts = [user_noise[best, torch.arange(scenes.S)]] if best is not None else []
+            parts += [user_noise[first_k + r] for r in range(copies - len(parts))]
+            user_noise = torch.cat(parts, 0)
         sc = scenes.repeat(copies)
         sse = torch.from_numpy(np.stack([sc.host_off[:-1], sc.host_off[1:]], 1))
         dh = g.add_noise(ni.repeat(copies, 1), sse, user_noise).unsqueeze(0)
@@ -74,6 +80,33 @@ def _bce_pair(scores, split, y_a, y_b, w=1.0):
     return w * sum(terms)
 
 
+class _TorchOps:
+    """Torch restatement of train_step.KernelOps (glue.hip / loss.hip)."""
+
+    @staticmethod
+    def traj_cat(head, a, b=None):
+        if b is None:
+            return torch.cat([head, a], 0)
+        return torch.cat([torch.cat([head, a], 0), torch.cat([head, b], 0)], 1)
+
+    @staticmethod
+    def l2_select(pred, gt, mask, scenes, k):
+        T, B = gt.shape[0], gt.shape[1]
+        l2 = ((gt.unsqueeze(1) - pred.view(T, k, B, 2)) ** 2).sum(3) * mask.t().unsqueeze(1)
+        seg = scenes.ped_scene_long()
+        return torch.zeros(k, scenes.S).index_add_(1, seg, l2.sum(0)).argmin(0)
+
+    @staticmethod
+    def l2_loss(pred, gt, mask, scenes, w=1.0):
+        seg = scenes.ped_scene_long()
+        l2 = (mask.t().unsqueeze(2) * (gt - pred) ** 2).sum((0, 2))
+        num = torch.zeros(scenes.S).index_add_(0, seg, w * l2)
+        den = torch.zeros(scenes.S).index_add_(0, seg, mask.sum(1))
+        return (num / den).sum()
+
+    bce_pair = staticmethod(_bce_pair)
+
+
 def _run(rank, world, port, out):
     from sgan.data.synthetic import synthetic_batch
     from sgan.scene import SceneIndex
@@ -82,7 +115,7 @@ def _run(rank, world, port, out):
     if world > 1:
         dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     g, d = _models()
-    tr = GanTrainer(g, d, dp=DataParallel(), bce_pair=_bce_pair)
+    tr = GanTrainer(g, d, dp=DataParallel(), ops=_TorchOps())
     batch = synthetic_batch(SIZES, seed=11)
     sc = SceneIndex(np.concatenate([[0], np.cumsum(SIZES)]), "cpu")
     s0, s1 = tr.dp.shard(sc.S)

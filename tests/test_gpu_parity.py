@@ -466,3 +466,54 @@ def test_gat_encoder_fused_equals_per_layer(nh, sizes):
     fl = 1e-2 * max(float(g.abs().max()) for g in gr.values())
     for k in gr:
         close(gf[k], gr[k].cpu().numpy(), rtol=2e-4, floor=fl, what="fused d" + k)
+
+
+def test_step_glue_kernels_match_torch():
+    """glue.hip (sgg_traj_cat, sgg_decoder_init, sgg_l2_select,
+    sgg_l2_loss_fwd/bwd) against the reference's torch expressions
+    (train.py:409-415, 443-470; losses.py:52-71; models.py:827-850)."""
+    from sgan import kernels as K
+    from sgan.scene import SceneIndex
+    torch.manual_seed(11)
+    sizes = [20, 1, 7, 13, 20, 2]
+    B, S, T, k = sum(sizes), len(sizes), 12, 5
+    sc = SceneIndex(np.concatenate([[0], np.cumsum(sizes)]), DEV)
+    seg = sc.ped_scene_long()
+    obs_rel, a, b = torch.randn(8, B, 2, device=DEV), torch.randn(T, B, 2, device=DEV), torch.randn(T, B, 2, device=DEV)
+    wide = torch.randn(T, 2 * B, 2, device=DEV)
+    close(K.traj_cat(obs_rel, a, b), torch.cat([torch.cat([obs_rel, a]), torch.cat([obs_rel, b])], 1).cpu().numpy(),
+          rtol=0, what="traj_cat")
+    ar = wide[:, B:].requires_grad_(False)
+    close(K.traj_cat(obs_rel, ar), torch.cat([obs_rel, ar]).cpu().numpy(), rtol=0, what="traj_cat slice")
+    # decoder init: copies with a best index
+    ctx = torch.randn(B, 24, device=DEV, requires_grad=True)
+    z = torch.randn(k, S, 8, device=DEV)
+    best = torch.randint(0, k, (S,), device=DEV)
+    last = torch.randn(B, 2, device=DEV)
+    h0, rel0 = K.decoder_init(ctx, z, best, k - 1, 2, sc, last)
+    zc = torch.cat([z[best, torch.arange(S, device=DEV)], z[k - 1]], 0)
+    ref = torch.cat([ctx.repeat(2, 1), zc.index_select(0, sc.repeat(2).ped_scene_long())], 1)
+    close(h0, ref.detach().cpu().numpy(), rtol=0, what="decoder_init h0")
+    close(rel0, last.repeat(2, 1).cpu().numpy(), rtol=0, what="decoder_init rel0")
+    g = torch.randn_like(h0)
+    (h0 * g).sum().backward()
+    close(ctx.grad, (g[:B, :24] + g[B:, :24]).cpu().numpy(), rtol=1e-6, what="decoder_init dctx")
+    # best-of-k selection and the selected sample's l2 term
+    gt = torch.randn(T, B, 2, device=DEV)
+    pred = torch.randn(T, k * B, 2, device=DEV)
+    lm = (torch.rand(B, 8 + T, device=DEV) > 0.2).float()
+    mask = lm[:, 8:]
+    l2 = ((gt.unsqueeze(1) - pred.view(T, k, B, 2)) ** 2).sum(3) * mask.t().unsqueeze(1)
+    ref_best = torch.zeros(k, S, device=DEV).index_add_(1, seg, l2.sum(0)).argmin(0)
+    assert torch.equal(K.l2_select(pred, gt, mask, sc, k), ref_best)
+    p = torch.randn(T, 2 * B, 2, device=DEV)
+    pv = p[:, :B].clone().requires_grad_(True)
+    loss = K.l2_loss(p[:, :B], gt, mask, sc, 1.0)
+    num = torch.zeros(S, device=DEV).index_add_(0, seg, (mask.t().unsqueeze(2) * (gt - pv) ** 2).sum((0, 2)))
+    den = torch.zeros(S, device=DEV).index_add_(0, seg, mask.sum(1))
+    ref_loss = (num / den).sum()
+    close(loss, ref_loss.detach().cpu().numpy(), rtol=1e-5, what="l2 loss")
+    ref_loss.backward()
+    pk = p[:, :B].clone().requires_grad_(True)
+    K.l2_loss(pk, gt, mask, sc, 1.0).backward()
+    close(pk.grad, pv.grad.cpu().numpy(), rtol=1e-5, what="l2 loss grad")
