@@ -41,7 +41,10 @@ __global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__
                                                        const float* __restrict__ We, const float* __restrict__ be,
                                                        const float* __restrict__ dA, const float* __restrict__ dbias,
                                                        float* __restrict__ dW, int lddw, float* __restrict__ dWe,
-                                                       float* __restrict__ dbe) {
+                                                       float* __restrict__ dbe, float* __restrict__ dbias_copy) {
+  // the second bias leaf (b_hh next to b_ih) gets its own copy of dbias
+  if (dbias_copy)
+    for (int r = threadIdx.x; r < R; r += blockDim.x) dbias_copy[r] = dbias[r];
   // dW: one (r, e) element per thread-iteration
   for (int q = threadIdx.x; q < R * E; q += blockDim.x) {
     const int r = q / E, e = q - r * E;
@@ -88,10 +91,11 @@ extern "C" int sgg_fold_fwd(const float* W, int ldw, int R, int E, const float* 
 }
 
 extern "C" int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be, const float* dA,
-                            const float* dbias, float* dW, int lddw, float* dWe, float* dbe, void* stream) {
+                            const float* dbias, float* dW, int lddw, float* dWe, float* dbe, float* dbias_copy,
+                            void* stream) {
   SGG_CHECK_ARG(W && We && be && dA && dbias && dW && dWe && dbe, "sgg_fold_bwd: null pointer");
   SGG_CHECK_ARG(R >= 1 && E >= 1 && E <= 128 && ldw >= E && lddw >= E, "sgg_fold_bwd: bad sizes");
   hipLaunchKernelGGL(fold_bwd_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, W, ldw, R, E, We, be, dA, dbias,
-                     dW, lddw, dWe, dbe);
+                     dW, lddw, dWe, dbe, dbias_copy);
   SGG_RETURN_LAUNCH("sgg_fold_bwd");
 }

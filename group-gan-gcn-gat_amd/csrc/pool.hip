@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ out,
     const int32_t* __restrict__ argmax, const float* __restrict__ dout, const int32_t* __restrict__ scene_off,
-    int S, int max_n, float* __restrict__ dU, float* __restrict__ dW2_part, float* __restrict__ dA_part) {
+    int S, int max_n, float* __restrict__ dU, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int k = threadIdx.x;  // hidden unit, blockDim.x == 512
   const int lane = k & 63;
@@ -229,6 +229,7 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
   for (int c = 0; c < BN; ++c) dW2s[c * kHidden + k] = 0.f;
   const float a0 = A[2 * k], a1 = A[2 * k + 1];
   float dA0 = 0.f, dA1 = 0.f;
+  float db2 = 0.f;   // thread c < BN: this workgroup's share of db2[c] = sum_i [out_ic > 0] dout_ic
 
   for (int s = blockIdx.x; s < S; s += gridDim.x) {
     const int o = scene_off[s];
@@ -241,6 +242,8 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
     }
     for (int q = k; q < n; q += blockDim.x) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
     __syncthreads();
+    if (k < BN)
+      for (int i = 0; i < n; ++i) db2 += gs[i * BN + k];
     if (wave == 0) {  // stable bucket of the selected (i, c) entries by j
       int cnt = 0;
       for (int j = 0; j < n; ++j) {
@@ -284,10 +287,13 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
     }
     __syncthreads();  // lists / gs reused by the next scene
   }
+  // this workgroup's row of the parameter-gradient slab: [dW2 (BN x 512) | dA (512 x 2) | db2 (BN)]
+  float* row = part + (size_t)blockIdx.x * (BN * kHidden + 2 * kHidden + BN);
 #pragma unroll
-  for (int c = 0; c < BN; ++c) dW2_part[((size_t)blockIdx.x * BN + c) * kHidden + k] = dW2s[c * kHidden + k];
-  dA_part[((size_t)blockIdx.x * kHidden + k) * 2 + 0] = dA0;
-  dA_part[((size_t)blockIdx.x * kHidden + k) * 2 + 1] = dA1;
+  for (int c = 0; c < BN; ++c) row[c * kHidden + k] = dW2s[c * kHidden + k];
+  row[BN * kHidden + 2 * k] = dA0;
+  row[BN * kHidden + 2 * k + 1] = dA1;
+  if (k < BN) row[BN * kHidden + 2 * kHidden + k] = db2;
 }
 
 template <int BN>
@@ -326,10 +332,10 @@ static int launch_fwd(const float* U, const float* pos, const float* A, const fl
 template <int BN>
 static int launch_bwd(const float* U, const float* pos, const float* A, const float* W2, const float* out,
                       const int32_t* am, const float* dout, const int32_t* off, int S, int max_n, float* dU,
-                      float* dW2p, float* dAp, hipStream_t st) {
+                      float* part, hipStream_t st) {
   const size_t lds = pool_bwd_lds(BN, max_n);
   hipLaunchKernelGGL(pool_bwd_kernel<BN>, dim3(sgg_pool_bwd_grid(S)), dim3(512), lds, st, U, pos, A, W2, out,
-                     am, dout, off, S, max_n, dU, dW2p, dAp);
+                     am, dout, off, S, max_n, dU, part);
   SGG_RETURN_LAUNCH("sgg_pool_bwd");
 }
 
@@ -415,8 +421,8 @@ extern "C" int sgg_pool_bwd_grid(int S) { return S < 1 ? 1 : (S < 256 ? S : 256)
 
 extern "C" int sgg_pool_bwd(const float* U, const float* pos, const float* A, const float* W2, const float* out,
                             const int32_t* argmax, const float* dout, const int32_t* scene_off, int S, int B,
-                            int bn, int max_n, float* dU, float* dW2_part, float* dA_part, void* stream) {
-  SGG_CHECK_ARG(U && pos && A && W2 && out && argmax && dout && scene_off && dU && dW2_part && dA_part,
+                            int bn, int max_n, float* dU, float* part, void* stream) {
+  SGG_CHECK_ARG(U && pos && A && W2 && out && argmax && dout && scene_off && dU && part,
                 "sgg_pool_bwd: null pointer");
   SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_bwd: bottleneck %d not built", bn);
   SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "sgg_pool_bwd: max scene size %d outside [1, %d]",
@@ -425,10 +431,10 @@ extern "C" int sgg_pool_bwd(const float* U, const float* pos, const float* A, co
   hipStream_t st = (hipStream_t)stream;
   if (S == 0) return 0;
   switch (bn) {
-    case 8: return launch_bwd<8>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, dW2_part, dA_part, st);
-    case 16: return launch_bwd<16>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, dW2_part, dA_part, st);
-    case 32: return launch_bwd<32>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, dW2_part, dA_part, st);
-    case 48: return launch_bwd<48>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, dW2_part, dA_part, st);
-    default: return launch_bwd<64>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, dW2_part, dA_part, st);
+    case 8: return launch_bwd<8>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, part, st);
+    case 16: return launch_bwd<16>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, part, st);
+    case 32: return launch_bwd<32>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, part, st);
+    case 48: return launch_bwd<48>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, part, st);
+    default: return launch_bwd<64>(U, pos, A, W2, out, argmax, dout, scene_off, S, max_n, dU, part, st);
   }
 }

@@ -15,7 +15,8 @@
 namespace sgg {
 
 __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restrict__ X, int ldx,
-                                                          const float* __restrict__ Y, int ldy, int R, int M,
+                                                          const float* __restrict__ Y, int ldy,
+                                                          const float* __restrict__ Ym, int ldm, int R, int M,
                                                           int N, int rows_per_split, float* __restrict__ slab,
                                                           float* __restrict__ colslab) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -52,7 +53,8 @@ __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restric
         const size_t row = (size_t)(r + 4 * s + kq);
         aa[s] = X[row * ldx + mcl];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) bb[s][t] = Y[row * ldy + ncl[t]];
+        for (int t = 0; t < 4; ++t)
+          bb[s][t] = Ym ? keep_if(Y[row * ldy + ncl[t]], Ym[row * ldm + ncl[t]] > 0.f) : Y[row * ldy + ncl[t]];
       }
     } else {
 #pragma unroll
@@ -61,7 +63,8 @@ __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restric
         const size_t rc = (size_t)min(row, r1 - 1);
         aa[s] = keep_if(X[rc * ldx + mcl], row < r1);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) bb[s][t] = keep_if(Y[rc * ldy + ncl[t]], row < r1);
+        for (int t = 0; t < 4; ++t)
+          bb[s][t] = keep_if(Y[rc * ldy + ncl[t]], row < r1 && (!Ym || Ym[rc * ldm + ncl[t]] > 0.f));
       }
     }
   };
@@ -156,19 +159,21 @@ extern "C" int sgg_xtw_splits(int R, int M, int N) {
   return splits < 1 ? 1 : (int)splits;
 }
 
-extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, int M, int N, float* C, int ldc,
-                       int trans_c, float* colsum, float* ws, size_t ws_bytes, void* stream) {
+extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const float* Ymask, int ldm, int R, int M,
+                       int N, float* C, int ldc, int trans_c, float* colsum, float* ws, size_t ws_bytes,
+                       void* stream) {
   SGG_CHECK_ARG((R == 0 || (X && Y)) && C && ws, "sgg_xtw: null pointer");
   SGG_CHECK_ARG(R >= 0 && M > 0 && N > 0 && ldx >= M && ldy >= N && ldc >= (trans_c ? M : N),
                 "sgg_xtw: bad sizes");
   const int splits = sgg_xtw_splits(R, M, N);
   const size_t need = sizeof(float) * (size_t)splits * ((size_t)M * N + N);
   SGG_CHECK_ARG(ws_bytes >= need, "sgg_xtw: workspace %zu < %zu bytes", ws_bytes, need);
+  SGG_CHECK_ARG(!Ymask || ldm >= N, "sgg_xtw: mask leading dim %d < N", ldm);
   hipStream_t st = (hipStream_t)stream;
   const int rps = ((R + splits - 1) / splits + 15) & ~15;
   float* colslab = ws + (size_t)splits * M * N;
   dim3 grid((M + 63) / 64, (N + 63) / 64, splits);
-  hipLaunchKernelGGL(xtw_partial_kernel, grid, dim3(256), 0, st, X, ldx, Y, ldy, R, M, N, rps, ws,
+  hipLaunchKernelGGL(xtw_partial_kernel, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws,
                      colsum ? colslab : nullptr);
   const int MN = M * N;
   hipLaunchKernelGGL(xtw_reduce_kernel, dim3((MN + 63) / 64), dim3(256), 0, st, ws, splits, MN, C, N, ldc, trans_c);

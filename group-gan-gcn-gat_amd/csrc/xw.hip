@@ -16,6 +16,7 @@ namespace sgg {
 
 template <bool TRANS_W>
 __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, int ldx,
+                                                 const float* __restrict__ Xmask, int ldm,
                                                  const float* __restrict__ W, int ldw,
                                                  const float* __restrict__ bias, float* __restrict__ Y,
                                                  int ldy, int M, int K, int N, int act) {
@@ -28,6 +29,8 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   const int arow = row0 + ar;
   const bool arow_ok = arow < M;
   const float* xrow = X + (size_t)(arow_ok ? arow : 0) * ldx;
+  // ReLU backward fused into the operand: X[m, k] counts where Xmask[m, k] > 0
+  const float* mrow = Xmask ? Xmask + (size_t)(arow_ok ? arow : 0) * ldm : nullptr;
 
   floatx4 acc[4];
 #pragma unroll
@@ -51,7 +54,7 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
 #pragma unroll
       for (int s = 0; s < S4; ++s) {
         const int k = kb + 4 * s + kq;
-        aa[s] = xrow[k];
+        aa[s] = mrow ? keep_if(xrow[k], mrow[k] > 0.f) : xrow[k];
 #pragma unroll
         for (int t = 0; t < 4; ++t) bb[s][t] = TRANS_W ? W[ncl[t] * ldw + k] : W[k * ldw + ncl[t]];
       }
@@ -60,7 +63,7 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
       for (int s = 0; s < S4; ++s) {
         const int k = kb + 4 * s + kq;
         const int kc = min(k, K - 1);
-        aa[s] = keep_if(xrow[kc], k < K);
+        aa[s] = keep_if(xrow[kc], k < K && (!mrow || mrow[kc] > 0.f));
 #pragma unroll
         for (int t = 0; t < 4; ++t) bb[s][t] = TRANS_W ? W[ncl[t] * ldw + kc] : W[kc * ldw + ncl[t]];
       }
@@ -103,19 +106,20 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
 
 }  // namespace sgg
 
-extern "C" int sgg_xw(const float* X, int ldx, const float* W, int ldw, int trans_w, const float* bias,
-                      float* Y, int ldy, int M, int K, int N, int act, void* stream) {
+extern "C" int sgg_xw(const float* X, int ldx, const float* Xmask, int ldm, const float* W, int ldw, int trans_w,
+                      const float* bias, float* Y, int ldy, int M, int K, int N, int act, void* stream) {
   SGG_CHECK_ARG(X && W && Y, "sgg_xw: null pointer");
   SGG_CHECK_ARG(M >= 0 && K > 0 && N > 0, "sgg_xw: bad sizes M=%d K=%d N=%d", M, K, N);
   SGG_CHECK_ARG(ldx >= K && ldy >= N && ldw >= (trans_w ? K : N), "sgg_xw: bad leading dims ldx=%d ldw=%d ldy=%d",
                 ldx, ldw, ldy);
   SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw: act must be 0 or 1");
+  SGG_CHECK_ARG(!Xmask || ldm >= K, "sgg_xw: mask leading dim %d < K", ldm);
   if (M == 0) return 0;
   dim3 grid((M + 63) / 64, (N + 63) / 64);
   hipStream_t s = (hipStream_t)stream;
   if (trans_w)
-    hipLaunchKernelGGL(sgg::xw_kernel<true>, grid, dim3(256), 0, s, X, ldx, W, ldw, bias, Y, ldy, M, K, N, act);
+    hipLaunchKernelGGL(sgg::xw_kernel<true>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy, M, K, N, act);
   else
-    hipLaunchKernelGGL(sgg::xw_kernel<false>, grid, dim3(256), 0, s, X, ldx, W, ldw, bias, Y, ldy, M, K, N, act);
+    hipLaunchKernelGGL(sgg::xw_kernel<false>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy, M, K, N, act);
   SGG_RETURN_LAUNCH("sgg_xw");
 }

@@ -40,11 +40,11 @@ _pargs = ctypes.POINTER(GatEncArgs)
 SIGNATURES = {
     "sgg_version": (_i, []),
     "sgg_last_error": (ctypes.c_char_p, []),
-    "sgg_xw": (_i, [_p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "sgg_xw": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
     "sgg_pool_plan": (_i, [_p, _i, _i, _i, _i, _p, _i, _p, _p]),
     "sgg_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_pool_bwd_grid": (_i, [_i]),
-    "sgg_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]),
+    "sgg_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_gat_fwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _i, _p]),
     "sgg_gat_bwd": (_i, [_p, _i, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _p, _i, _p, _p, _p, _p]),
     "sgg_seg_norm_fwd": (_i, [_p, _i, _i, _p, _i, _f, _p, _i, _p, _p]),
@@ -54,9 +54,9 @@ SIGNATURES = {
     "sgg_seg_reduce": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i, _p]),
     "sgg_seg_gather": (_i, [_p, _i, _i, _p, _p, _p, _i, _p, _i, _p]),
     "sgg_xtw_splits": (_i, [_i, _i, _i]),
-    "sgg_xtw": (_i, [_p, _i, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _sz, _p]),
+    "sgg_xtw": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _sz, _p]),
     "sgg_fold_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
-    "sgg_fold_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _p]),
+    "sgg_fold_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "sgg_lstm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p]),

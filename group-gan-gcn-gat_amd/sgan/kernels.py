@@ -38,10 +38,14 @@ def _rows(t, name):
 # ---------------------------------------------------------------------------
 # dense node transform
 # ---------------------------------------------------------------------------
-def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None):
+def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None, mask=None):
     """act(x @ W + bias); W = w (K x N) or w^T (w stored N x K, trans_w).  w
-    may be a row-strided column block (e.g. W1[:, E:]), passed in place."""
+    may be a row-strided column block (e.g. W1[:, E:]), passed in place.
+    mask (same shape as x): x counts only where mask > 0 (fused ReLU backward)."""
     x = _rows(x, "x")
+    if mask is not None:
+        mask = _rows(mask, "mask")
+        assert mask.shape == x.shape
     w = _rows(w, "w")
     M, K = x.shape
     Nn = w.shape[0] if trans_w else w.shape[1]
@@ -50,12 +54,13 @@ def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None):
         bias = _req(bias, "bias").contiguous()
         assert bias.numel() == Nn
     y = out if out is not None else torch.empty(M, Nn, device=x.device, dtype=torch.float32)
-    N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(w), w.stride(0), int(bool(trans_w)), N.ptr(bias), N.ptr(y),
+    N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(mask), mask.stride(0) if mask is not None else 0, N.ptr(w),
+                          w.stride(0), int(bool(trans_w)), N.ptr(bias), N.ptr(y),
                           y.stride(0), M, K, Nn, int(act), N.stream_ptr()), "sgg_xw")
     return y
 
 
-def xtw(X, Y, colsum=False, trans_c=False, out=None):
+def xtw(X, Y, colsum=False, trans_c=False, out=None, mask=None):
     """C = X^T Y (M x N), or C^T (N x M) with trans_c, plus the column sums of
     Y, with the split-K MFMA reduction (sgg_xtw).  X: R x M, Y: R x N,
     row-strided 2-D views allowed; `out` (row-strided, unit column stride)
@@ -63,6 +68,9 @@ def xtw(X, Y, colsum=False, trans_c=False, out=None):
     lib = _lib()
     X = _rows(X, "X")
     Y = _rows(Y, "Y")
+    if mask is not None:
+        mask = _rows(mask, "mask")
+        assert mask.shape == Y.shape
     R, M = X.shape
     Nn = Y.shape[1]
     assert Y.shape[0] == R
@@ -78,7 +86,8 @@ def xtw(X, Y, colsum=False, trans_c=False, out=None):
     splits = lib.sgg_xtw_splits(R, M, Nn)
     ws = torch.empty(splits * (M * Nn + Nn), device=X.device, dtype=torch.float32)
     cs = torch.empty(Nn, device=X.device, dtype=torch.float32) if colsum else None
-    N.check(lib.sgg_xtw(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), R, M, Nn, N.ptr(C), C.stride(0), int(trans_c),
+    N.check(lib.sgg_xtw(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), N.ptr(mask),
+                        mask.stride(0) if mask is not None else 0, R, M, Nn, N.ptr(C), C.stride(0), int(trans_c),
                         N.ptr(cs), N.ptr(ws), ws.numel() * 4, N.stream_ptr()), "sgg_xtw")
     return (C, cs) if colsum else C
 
@@ -98,8 +107,9 @@ def fold_fwd(W, We, be, b1, b2=None):
     return A, bias
 
 
-def fold_bwd(W, We, be, dA, dbias, dW=None):
-    """(dW, dWe, dbe) of fold_fwd; dW may be a preallocated column block."""
+def fold_bwd(W, We, be, dA, dbias, dW=None, dbias_copy=None):
+    """(dW, dWe, dbe) of fold_fwd; dW may be a preallocated column block;
+    dbias_copy (optional) receives a copy of dbias in the same launch."""
     W = _rows(W, "W")
     R, E = W.shape
     dW = dW if dW is not None else torch.empty(R, E, device=W.device, dtype=torch.float32)
@@ -107,7 +117,7 @@ def fold_bwd(W, We, be, dA, dbias, dW=None):
     dbe = torch.empty(E, device=W.device, dtype=torch.float32)
     N.check(_lib().sgg_fold_bwd(N.ptr(W), W.stride(0), R, E, N.ptr(We.contiguous()), N.ptr(be.contiguous()),
                                 N.ptr(dA.contiguous()), N.ptr(dbias.contiguous()), N.ptr(dW), dW.stride(0), N.ptr(dWe),
-                                N.ptr(dbe), N.stream_ptr()), "sgg_fold_bwd")
+                                N.ptr(dbe), N.ptr(dbias_copy), N.stream_ptr()), "sgg_fold_bwd")
     return dW, dWe, dbe
 
 
@@ -122,15 +132,14 @@ class _XW(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        if ctx.act:
-            dy = dy * (y > 0)
         dy = dy.contiguous()
+        m = y if ctx.act else None    # ReLU backward dy * (y > 0), fused into the operands
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = xw_raw(dy, w, None, not ctx.trans_w, 0)
+            dx = xw_raw(dy, w, None, not ctx.trans_w, 0, mask=m)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             # X^T dY (K x N); nn.Linear-layout weights take it transposed (N x K)
-            dw, cs = xtw(x, dy, colsum=True, trans_c=ctx.trans_w)
+            dw, cs = xtw(x, dy, colsum=True, trans_c=ctx.trans_w, mask=m)
             db = cs if ctx.has_bias else None
         return dx, dw, db, None, None
 
@@ -216,6 +225,7 @@ class _Pool(torch.autograd.Function):
         ctx.E = E
         ctx.save_for_backward(h, pos, W1, We, be, A, W2, U, out, am)
         ctx.mark_non_differentiable(am)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for the argmax output
         return out, am
 
     @staticmethod
@@ -226,21 +236,22 @@ class _Pool(torch.autograd.Function):
         B, bn = out.shape
         dout = dout.contiguous()
         grid = lib.sgg_pool_bwd_grid(sc.S)
+        P = bn * 512 + 1024 + bn
         dU = torch.empty(B, 512, device=h.device, dtype=torch.float32)
-        dW2p = torch.empty(grid, bn, 512, device=h.device, dtype=torch.float32)
-        dAp = torch.empty(grid, 512, 2, device=h.device, dtype=torch.float32)
+        part = torch.empty(grid, P, device=h.device, dtype=torch.float32)
         N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(out), N.ptr(am), N.ptr(dout),
-                                 N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(dW2p), N.ptr(dAp),
+                                 N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(part),
                                  N.stream_ptr()), "sgg_pool_bwd")
         need = ctx.needs_input_grad
         dh = xw_raw(dU, W1[:, E:], None, trans_w=False) if need[0] else None
         if not any(need[2:8]):       # weights frozen (the G-step's discriminator): input gradient only
             return dh, None, None, None, None, None, None, None, None
+        flat = torch.empty(P, device=h.device, dtype=torch.float32)     # [dW2 | dA | db2]
+        N.check(lib.sgg_slab_reduce(N.ptr(part), grid, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
         dW1 = torch.empty_like(W1)
         _, dc = xtw(h, dU, colsum=True, trans_c=True, out=dW1[:, E:])   # dW1h = dU^T h, dc = sum_j dU_j
-        _, dWe, dbe = fold_bwd(W1[:, :E], We, be, dAp.sum(0), dc, dW=dW1[:, :E])
-        db2 = (dout * (out > 0)).sum(0)
-        return dh, None, dW1, dWe, dbe, dc, dW2p.sum(0), db2, None
+        _, dWe, dbe = fold_bwd(W1[:, :E], We, be, flat[bn * 512:bn * 512 + 1024].view(512, 2), dc, dW=dW1[:, :E])
+        return dh, None, dW1, dWe, dbe, dc, flat[:bn * 512].view(bn, 512), flat[bn * 512 + 1024:], None
 
 
 def social_pool(h, pos, W1, We, be, b1, W2, b2, scenes):
@@ -578,8 +589,9 @@ class _LSTMSeq(torch.autograd.Function):
             dW_hh, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True, trans_c=True)
             rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0) if decoder else rel
             dA = xtw(rel_in.reshape(T * B, 2), dGf, trans_c=True)                   # 4H x 2
-            dW_ih, dWe, dbe = fold_bwd(W_ih, We, be, dA, dbias)
-            db_ih, db_hh = dbias, dbias.clone()     # two leaves: no shared gradient storage
+            db_hh = torch.empty_like(dbias)          # two leaves: no shared gradient storage
+            dW_ih, dWe, dbe = fold_bwd(W_ih, We, be, dA, dbias, dbias_copy=db_hh)
+            db_ih = dbias
         if decoder:
             if need[9] or need[10]:
                 dr = drel_tot.view(T * B, 2)
@@ -633,11 +645,23 @@ class _Bce(torch.autograd.Function):
         return dx.view(ctx.shape), None, None, None, None
 
 
+_CONST = {}
+
+
+def const(v, device):
+    """A cached device scalar (no fill launch per use; created on first use,
+    outside graph capture: the trainers warm up before capturing)."""
+    key = (str(device), float(v))
+    t = _CONST.get(key)
+    if t is None:
+        t = _CONST[key] = torch.full((), float(v), device=device, dtype=torch.float32)
+    return t
+
+
 def _scalar_dev(y, device):
     if torch.is_tensor(y):
         return y.to(device=device, dtype=torch.float32).reshape(())
-    # a fill kernel, not a host->device copy: stays legal inside graph capture
-    return torch.full((), float(y), device=device, dtype=torch.float32)
+    return const(y, device)
 
 
 def bce_pair(scores, split, y_a, y_b, w=1.0):
@@ -754,3 +778,26 @@ def l2_loss(pred, gt, mask, scenes, w=1.0):
     """sum_s w * l2_loss(pred, gt, mask, 'raw') summed over the peds of s /
     sum(mask of s) (train.py:459-464 for the selected sample)."""
     return _L2Loss.apply(pred, gt, mask, scenes, w)
+
+
+class _Split2(torch.autograd.Function):
+    """(x[:, :B], x[:, B:]) with ONE concatenating launch in the backward
+    (autograd's slice backward would zero-fill and copy per slice)."""
+
+    @staticmethod
+    def forward(ctx, x, B):
+        ctx.meta = (x.shape, B)
+        return x[:, :B], x[:, B:]
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        shape, B = ctx.meta
+        if ga is None:
+            ga = torch.zeros(shape[0], B, *shape[2:], device=gb.device, dtype=gb.dtype)
+        if gb is None:
+            gb = torch.zeros(shape[0], shape[1] - B, *shape[2:], device=ga.device, dtype=ga.dtype)
+        return torch.cat([ga, gb], 1), None
+
+
+def split2(x, B):
+    return _Split2.apply(x, B)

@@ -113,6 +113,8 @@ class KernelOps:
     l2_select = staticmethod(K.l2_select)
     l2_loss = staticmethod(K.l2_loss)
     bce_pair = staticmethod(K.bce_pair)
+    split2 = staticmethod(K.split2)
+    one = staticmethod(lambda device: K.const(1.0, device))
 
 
 class GanTrainer:
@@ -181,7 +183,7 @@ class GanTrainer:
         # gan_d_loss = bce(real, y_real) + bce(fake, 0); scores = [fake | real]
         loss = self.bce_pair(scores, sc.B, 0.0, y_real, sc.B / B_global)
         self.opt_d.zero_grad(set_to_none=True)
-        loss.backward()
+        torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device))
         vals = self._finish(self.d_params, self.opt_d, [loss], a.clipping_threshold_d)
         return {"D_data_loss": vals[0], "D_total_loss": vals[0]}
 
@@ -215,8 +217,10 @@ class GanTrainer:
             copies = 2 if use_l2 else 1
             out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=copies,
                            noise_index=(best, k - 1))
-            fake_rel_last = out[:, (copies - 1) * B:]
-            fake_rel_best = out[:, :B] if use_l2 else None
+            if use_l2:
+                fake_rel_best, fake_rel_last = ops.split2(out, B)
+            else:
+                fake_rel_best, fake_rel_last = None, out
         else:
             out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k, noise_index=(None, 0))
             fake_rel_last = out[:, (k - 1) * B:]
@@ -249,7 +253,7 @@ class GanTrainer:
         adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global)    # gan_g_loss
         loss = adv + (terms[0] if terms else 0.0)
         self.opt_g.zero_grad(set_to_none=True)
-        torch.autograd.backward(loss, inputs=self.g_params)
+        torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self.g_params)
         vals = self._finish(self.g_params, self.opt_g, [terms[0] if terms else adv * 0, adv, loss],
                             a.clipping_threshold_g)
         out = {"G_discriminator_loss": vals[1], "G_total_loss": vals[2]}

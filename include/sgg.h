@@ -48,9 +48,12 @@ const char* sgg_last_error(void);
  * Replaces the per-node `torch.mm(h, W)` / nn.Linear calls of
  * models.py:199 (GAT Wh = hW), :576 ((AH)W of the GCN), :289 / :706
  * (out_embedding), and the h_j half of the pooling MLP's first layer :538.
+ * Xmask (may be NULL, row stride ldm): X[m, k] enters only where
+ * Xmask[m, k] > 0 -- the ReLU backward dY * (Y > 0) of a transform with a
+ * fused ReLU, without materialising the masked gradient.
  */
-int sgg_xw(const float* X, int ldx, const float* W, int ldw, int trans_w, const float* bias,
-           float* Y, int ldy, int M, int K, int N, int act, void* stream);
+int sgg_xw(const float* X, int ldx, const float* Xmask, int ldm, const float* W, int ldw, int trans_w,
+           const float* bias, float* Y, int ldy, int M, int K, int N, int act, void* stream);
 
 /* ------------------------------------------------------------------------
  * Social pooling (PoolHiddenNet.forward, models.py:497-549), factored:
@@ -84,15 +87,16 @@ int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* 
 
 /* Backward of sgg_pool_fwd.  Only the (i, argmax[i,c]) pairs carry gradient
  * (torch.max(dim) backward, models.py:541).  Writes dU (B x 512, every row),
- * and per-workgroup partial sums of dW2 (grid x bn x 512) and dA
- * (grid x 512 x 2), `grid` = sgg_pool_bwd_grid(S); the caller sums the
- * partial slabs over their first axis (fixed order => deterministic).
+ * and one row per workgroup of the parameter-gradient slab `part`
+ * (grid x (bn*512 + 1024 + bn), grid = sgg_pool_bwd_grid(S)): the
+ * workgroup's partial sums of [dW2 (bn x 512) | dA (512 x 2) | db2 (bn)];
+ * sgg_slab_reduce sums the rows (fixed order => deterministic).
  * pos gets no gradient (it is an input trajectory in every caller). */
 int sgg_pool_bwd_grid(int S);
 int sgg_pool_bwd(const float* U, const float* pos, const float* A, const float* W2,
                  const float* out, const int32_t* argmax, const float* dout,
                  const int32_t* scene_off, int S, int B, int bn, int max_n,
-                 float* dU, float* dW2_part, float* dA_part, void* stream);
+                 float* dU, float* part, void* stream);
 
 /* ------------------------------------------------------------------------
  * Graph attention over the nodes of each segment (GraphAttentionLayer,
@@ -193,10 +197,12 @@ int sgg_seg_gather(const float* src, int lds, int F, const int32_t* seg_of_row,
  * workgroup slabs summed in a fixed order (deterministic); ws must hold
  * splits * (M*N + N) floats.  Replaces the library GEMMs of every weight
  * gradient (dW = X^T dY of the node transforms, W_hh / W_ih / hidden2pos of the
- * LSTMs summed over T x B, W1h of the pooling, `a` of the attention). */
+ * LSTMs summed over T x B, W1h of the pooling, `a` of the attention).
+ * Ymask (may be NULL, row stride ldm): Y[r, n] enters (C and colsum) only where
+ * Ymask[r, n] > 0 (the fused ReLU's backward). */
 int sgg_xtw_splits(int R, int M, int N);
-int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, int M, int N, float* C,
-            int ldc, int trans_c, float* colsum, float* ws, size_t ws_bytes, void* stream);
+int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const float* Ymask, int ldm, int R, int M, int N,
+            float* C, int ldc, int trans_c, float* colsum, float* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Input-embedding fold (a Linear(2, E) displacement embedding feeding a
@@ -208,9 +214,10 @@ int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, int R, int M, int 
  * dWe = W^T dA (E x 2), dbe = W^T dbias (E); db1 = db2 = dbias. */
 int sgg_fold_fwd(const float* W, int ldw, int R, int E, const float* We, const float* be,
                  const float* b1, const float* b2, float* A, float* bias, void* stream);
-int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be,
-                 const float* dA, const float* dbias, float* dW, int lddw, float* dWe, float* dbe,
-                 void* stream);
+/* dbias_copy (may be NULL) receives a copy of dbias: the LSTM's second bias
+ * leaf b_hh gets its own gradient tensor without an extra launch. */
+int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be, const float* dA,
+                 const float* dbias, float* dW, int lddw, float* dWe, float* dbe, float* dbias_copy, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused LSTM sequence (Encoder.forward models.py:62-92; Decoder.forward

@@ -105,6 +105,8 @@ class _TorchOps:
         return (num / den).sum()
 
     bce_pair = staticmethod(_bce_pair)
+    split2 = staticmethod(lambda x, B: (x[:, :B], x[:, B:]))
+    one = staticmethod(lambda device: torch.ones((), device=device))
 
 
 def _run(rank, world, port, out):
