@@ -46,6 +46,7 @@ __global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__
   if (dbias_copy)
     for (int r = threadIdx.x; r < R; r += blockDim.x) dbias_copy[r] = dbias[r];
   // dW: one (r, e) element per thread-iteration
+#pragma unroll 4
   for (int q = threadIdx.x; q < R * E; q += blockDim.x) {
     const int r = q / E, e = q - r * E;
     dW[(size_t)r * lddw + e] = fmaf(dA[2 * r], We[2 * e], fmaf(dA[2 * r + 1], We[2 * e + 1], dbias[r] * be[e]));

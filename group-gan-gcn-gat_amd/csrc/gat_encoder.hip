@@ -61,11 +61,23 @@ struct LW {
   const float* boe;
 };
 
-// copy a K x N row-major global matrix to LDS at pitch N + 1
+// copy a K x N row-major global matrix to LDS at pitch N + 1; each thread
+// issues its (up to 4 per round) loads before any store, so a matrix costs
+// one memory latency per 4 trips instead of one per trip
 __device__ inline float* stage_mat(float* dst, const float* __restrict__ src, int K, int N, int nthreads) {
-  for (int e = threadIdx.x; e < K * N; e += nthreads) {
-    const int k = e / N, c = e - k * N;
-    dst[k * (N + 1) + c] = src[e];
+  const int tot = K * N;
+  for (int e0 = threadIdx.x; e0 < tot; e0 += 4 * nthreads) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src[min(e0 + u * nthreads, tot - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * nthreads;
+      if (e < tot) {
+        const int k = e / N, c = e - k * N;
+        dst[k * (N + 1) + c] = v[u];
+      }
+    }
   }
   return dst + K * (N + 1);
 }
@@ -201,20 +213,19 @@ __device__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, 
   }
 }
 
-// s_i = a[:F].Wh_i, t_i = a[F:].Wh_i
+// s_i = a[:F].Wh_i, t_i = a[F:].Wh_i: one wavefront per dot product (lanes
+// over the F <= 128 features, a wave-shuffle sum) instead of an F-long
+// serial chain of LDS reads per thread
 __device__ void scores(const float* Wh, int ldw, int rows, int F, const float* a, float* s, float* t) {
-  for (int e = threadIdx.x; e < 2 * rows; e += blockDim.x) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int e = wave; e < 2 * rows; e += nw) {
     const int r = e >> 1, w = e & 1;
     const float* av = a + w * F;
     const float* x = Wh + r * ldw;
-    float a0 = 0.f, a1 = 0.f;
-    int f = 0;
-    for (; f + 1 < F; f += 2) {
-      a0 = fmaf(x[f], av[f], a0);
-      a1 = fmaf(x[f + 1], av[f + 1], a1);
-    }
-    if (f < F) a0 = fmaf(x[f], av[f], a0);
-    (w ? t : s)[r] = a0 + a1;
+    float v = lane < F ? x[lane] * av[lane] : 0.f;
+    if (lane + 64 < F) v = fmaf(x[lane + 64], av[lane + 64], v);
+    v = wave_sum(v);
+    if (lane == 0) (w ? t : s)[r] = v;
   }
 }
 
@@ -534,12 +545,37 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     float* dpre = sm + L.dpre;
     float* attm = sm + L.attm;
     float* slab = p.slab + (size_t)sc * PL.total;
-    const float* dy = p.dy + (size_t)o * p.lddy;
+    // the scene's dy rows to LDS first (the Wh scratch, pitch FE + 1): the
+    // loops below walk them n-deep, one memory latency per step from global
+    constexpr int PDY = FE + 1;
+    float* dy = Wh;
+    {
+      const float* dyg = p.dy + (size_t)o * p.lddy;
+      const int tot = n * FE;
+      for (int e0 = tid; e0 < tot; e0 += 4 * blockDim.x) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = min(e0 + u * (int)blockDim.x, tot - 1);
+          const int i = e / FE, k = e - i * FE;
+          v[u] = dyg[(size_t)i * p.lddy + k];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = e0 + u * (int)blockDim.x;
+          if (e < tot) {
+            const int i = e / FE, k = e - i * FE;
+            dy[i * PDY + k] = v[u];
+          }
+        }
+      }
+    }
+    __syncthreads();
     // out embedding: d[intra | inter] = dy Woe; dWoe = dy^T [intra | inter]; dboe = sum dy
     for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
       const int i = e / (2 * FO), c = e - i * 2 * FO;
       float acc = 0.f;
-      for (int k = 0; k < FE; ++k) acc = fmaf(dy[i * p.lddy + k], lw.Woe[k * PWE + c], acc);
+      for (int k = 0; k < FE; ++k) acc = fmaf(dy[i * PDY + k], lw.Woe[k * PWE + c], acc);
       if (c < FO) dI[i * P16 + c] = acc;
       else dpre[i * P16 + c - FO] = acc;   // d inter (scratch)
     }
@@ -548,13 +584,13 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       float acc = 0.f;
       for (int i = 0; i < n; ++i) {
         const float v = c < FO ? yI[i * P16 + c] : gout[grank[i] * P16 + c - FO] * ginv[i];
-        acc = fmaf(dy[i * p.lddy + k], v, acc);
+        acc = fmaf(dy[i * PDY + k], v, acc);
       }
       slab[PL.Woe + e] = acc;
     }
     for (int k = tid; k < FE; k += blockDim.x) {
       float acc = 0.f;
-      for (int i = 0; i < n; ++i) acc += dy[i * p.lddy + k];
+      for (int i = 0; i < n; ++i) acc += dy[i * PDY + k];
       slab[PL.boe + k] = acc;
     }
     __syncthreads();
@@ -637,21 +673,35 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
   }
 }
 
-// out[c] = sum_s slab[s][c] in scene order (deterministic)
-__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, int rows, int cols,
-                                                         float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int r = 0;
-  for (; r + 3 < rows; r += 4) {
-    a0 += slab[(size_t)r * cols + c];
-    a1 += slab[(size_t)(r + 1) * cols + c];
-    a2 += slab[(size_t)(r + 2) * cols + c];
-    a3 += slab[(size_t)(r + 3) * cols + c];
+// out[c] = sum_s slab[s][c] in a fixed order (deterministic): block = 64
+// columns x 16 row phases, phase p sums rows p, p + 16, ... with 4 loads in
+// flight, then the 16 phase sums in order
+__global__ void __launch_bounds__(1024) slab_reduce_kernel(const float* __restrict__ slab, int rows, int cols,
+                                                          float* __restrict__ out) {
+  __shared__ float part[16][64];
+  const int el = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + el;
+  float s = 0.f;
+  if (c < cols) {
+    int r = ph;
+    for (; r + 48 < rows; r += 64) {
+      const float v0 = slab[(size_t)r * cols + c], v1 = slab[(size_t)(r + 16) * cols + c];
+      const float v2 = slab[(size_t)(r + 32) * cols + c], v3 = slab[(size_t)(r + 48) * cols + c];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
+    }
+    for (; r < rows; r += 16) s += slab[(size_t)r * cols + c];
   }
-  for (; r < rows; ++r) a0 += slab[(size_t)r * cols + c];
-  out[c] = (a0 + a1) + (a2 + a3);
+  part[ph][el] = s;
+  __syncthreads();
+  if (ph == 0 && c < cols) {
+    float v = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) v += part[p][el];
+    out[c] = v;
+  }
 }
 
 }  // namespace
@@ -713,7 +763,7 @@ extern "C" int sgg_slab_reduce(const float* slab, int rows, int cols, float* out
   SGG_CHECK_ARG(slab && out, "sgg_slab_reduce: null pointer");
   SGG_CHECK_ARG(rows >= 0 && cols >= 0, "sgg_slab_reduce: bad sizes");
   if (cols == 0) return 0;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((cols + 255) / 256), dim3(256), 0, (hipStream_t)stream, slab, rows, cols,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((cols + 63) / 64), dim3(1024), 0, (hipStream_t)stream, slab, rows, cols,
                      out);
   SGG_RETURN_LAUNCH("sgg_slab_reduce");
 }

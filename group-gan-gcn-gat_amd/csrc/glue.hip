@@ -66,43 +66,54 @@ __global__ void __launch_bounds__(256) decoder_init_kernel(const float* __restri
   }
 }
 
-// one workgroup per scene: sum over (sample, ped, step) of mask (gt - pred)^2,
-// argmin over the k samples (first minimum, as torch.argmin)
-__global__ void __launch_bounds__(256) l2_select_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
+// one workgroup (8 waves) per scene: wave w takes samples w, w + 8, ...;
+// lane = ped (its sum over the T steps of mask (gt - pred)^2: independent
+// loads), the scene sum by a wave shuffle; argmin over the k samples (first
+// minimum, as torch.argmin)
+__global__ void __launch_bounds__(512) l2_select_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
                                                         const float* __restrict__ mask, int ldm,
                                                         const int32_t* __restrict__ scene_off, int T, int B, int k,
                                                         int64_t* __restrict__ best) {
-  __shared__ float part[4][64];
+  __shared__ float part[256];   // k <= 256
   const int s = blockIdx.x;
   const int o = scene_off[s], n = scene_off[s + 1] - o;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int r = wave; r < k; r += 4) {
+  const float2* g2 = reinterpret_cast<const float2*>(gt);
+  const float2* p2 = reinterpret_cast<const float2*>(pred);
+  for (int r = wave; r < k; r += 8) {
     float acc = 0.f;
-    for (int e = lane; e < n * T; e += 64) {
-      const int i = e / T, t = e - i * T;
+    for (int i = lane; i < n; i += 64) {
       const int p = o + i;
-      const float2 g = reinterpret_cast<const float2*>(gt)[(size_t)t * B + p];
-      const float2 q = reinterpret_cast<const float2*>(pred)[((size_t)t * k + r) * B + p];
-      const float dx = g.x - q.x, dy = g.y - q.y;
-      acc = fmaf(mask[(size_t)p * ldm + t], fmaf(dx, dx, dy * dy), acc);
+      float a = 0.f;
+#pragma unroll 4
+      for (int t = 0; t < T; ++t) {
+        const float2 g = g2[(size_t)t * B + p];
+        const float2 q = p2[((size_t)t * k + r) * B + p];
+        const float dx = g.x - q.x, dy = g.y - q.y;
+        a = fmaf(mask[(size_t)p * ldm + t], fmaf(dx, dx, dy * dy), a);
+      }
+      acc += a;
     }
     acc = wave_sum(acc);
-    if (lane == 0) part[r & 3][r >> 2] = acc;   // k <= 256
+    if (lane == 0) part[r] = acc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     int bi = 0;
-    float bv = part[0][0];
-    for (int r = 1; r < k; ++r) {
-      const float v = part[r & 3][r >> 2];
-      if (v < bv) { bv = v; bi = r; }
-    }
+    float bv = part[0];
+    for (int r = 1; r < k; ++r)
+      if (part[r] < bv) {
+        bv = part[r];
+        bi = r;
+      }
     best[s] = bi;
   }
 }
 
-// single workgroup: per scene (one wave each) sum of mask (gt - pred)^2 and of
-// the mask, term = w * l2 / msum, loss = sum of the terms in scene order
+// single workgroup: wave w takes scenes w, w + 16, ... (lane = ped: its sums
+// over the T steps of mask (gt - pred)^2 and of the mask, independent loads),
+// term_s = w * l2_s / msum_s; loss = the terms summed in a fixed order (per
+// wave in scene order, then the waves in order)
 __global__ void __launch_bounds__(1024) l2_loss_fwd_kernel(const float* __restrict__ pred, int ldp,
                                                            const float* __restrict__ gt,
                                                            const float* __restrict__ mask, int ldm,
@@ -110,31 +121,42 @@ __global__ void __launch_bounds__(1024) l2_loss_fwd_kernel(const float* __restri
                                                            int B, float w, float* __restrict__ loss,
                                                            float* __restrict__ msum_out,
                                                            float* __restrict__ term) {
+  __shared__ float wsum[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const float2* g2 = reinterpret_cast<const float2*>(gt);
+  float run = 0.f;
   for (int s = wave; s < S; s += nw) {
     const int o = scene_off[s], n = scene_off[s + 1] - o;
     float acc = 0.f, ms = 0.f;
-    for (int e = lane; e < n * T; e += 64) {
-      const int i = e / T, t = e - i * T;
+    for (int i = lane; i < n; i += 64) {
       const int p = o + i;
-      const float m = mask[(size_t)p * ldm + t];
-      const float2 g = reinterpret_cast<const float2*>(gt)[(size_t)t * B + p];
-      const float2 q = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
-      const float dx = g.x - q.x, dy = g.y - q.y;
-      acc = fmaf(m, fmaf(dx, dx, dy * dy), acc);
+      float a = 0.f, m = 0.f;
+#pragma unroll 4
+      for (int t = 0; t < T; ++t) {
+        const float mk = mask[(size_t)p * ldm + t];
+        const float2 g = g2[(size_t)t * B + p];
+        const float2 q = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
+        const float dx = g.x - q.x, dy = g.y - q.y;
+        a = fmaf(mk, fmaf(dx, dx, dy * dy), a);
+        m += mk;
+      }
+      acc += a;
       ms += m;
     }
     acc = wave_sum(acc);
     ms = wave_sum(ms);
     if (lane == 0) {
       msum_out[s] = ms;
-      term[s] = (w * acc) / ms;
+      const float tv = (w * acc) / ms;
+      term[s] = tv;
+      run += tv;
     }
   }
+  if (lane == 0) wsum[wave] = run;
   __syncthreads();
   if (threadIdx.x == 0) {
     float tot = 0.f;
-    for (int s = 0; s < S; ++s) tot += term[s];
+    for (int i = 0; i < nw; ++i) tot += wsum[i];
     *loss = tot;
   }
 }
@@ -198,7 +220,7 @@ extern "C" int sgg_l2_select(const float* pred, const float* gt, const float* ma
   SGG_CHECK_ARG(pred && gt && mask && scene_off && best, "sgg_l2_select: null pointer");
   SGG_CHECK_ARG(S >= 0 && T >= 1 && B >= 0 && k >= 1 && k <= 256 && ldm >= T, "sgg_l2_select: bad sizes");
   if (S == 0) return 0;
-  hipLaunchKernelGGL(l2_select_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, pred, gt, mask, ldm, scene_off, T,
+  hipLaunchKernelGGL(l2_select_kernel, dim3(S), dim3(512), 0, (hipStream_t)stream, pred, gt, mask, ldm, scene_off, T,
                      B, k, best);
   SGG_RETURN_LAUNCH("sgg_l2_select");
 }

@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ 
   __shared__ float red[2][4];
   const float a = *ya, b = *yb;
   float s0 = 0.f, s1 = 0.f;
+#pragma unroll 4
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     if (i < split) s0 += bce_term(x[i], a);
     else s1 += bce_term(x[i], b);

@@ -267,6 +267,8 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   hipStream_t st = (hipStream_t)stream;
   if (lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
     return lstm_fwd_mfma(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
+  if (lstm_mw_ok(H, B))
+    return lstm_mw_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
   if (lstm_unit_ok(H, decoder) && !getenv("SGG_LSTM_ROWS"))
     return lstm_unit_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
   switch (H) {
@@ -286,6 +288,8 @@ extern "C" int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, c
   SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_bwd: bad sizes");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (lstm_mw_ok(H, B))
+    return lstm_mw_bwd(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, H, decoder, dG, dh0, drel_in, drel_tot, st);
   if (lstm_unit_ok(H, decoder) && !getenv("SGG_LSTM_ROWS"))
     return lstm_unit_bwd(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, H, decoder, dG, dh0, drel_in, drel_tot, st);
   switch (H) {

@@ -1,0 +1,418 @@
+// Fused LSTM sequences on v_mfma_f32_16x16x4_f32, one workgroup of four
+// waves per 16 peds (Encoder, reference sgan/models.py:62-92; Decoder
+// rollout :142-178).  Same contract as sgg_lstm_fwd / sgg_lstm_bwd
+// (include/sgg.h), dispatched by lstm.hip for batches of a few thousand peds
+// (the discriminator's real+fake sequences): one workgroup per CU, where
+// every step of the recurrence is latency-bound and the per-ped gate GEMM
+// (4H x H) has to be spread over all four SIMDs of the CU.
+//
+// Forward step, wave g = gate block g (i | f | g | o):
+//   G_g^T (H x 16 peds) = [W_hh,g | A_g b_g] . [h_{t-1} | r_x r_y 1 0]^T
+// = MU = H / 16 tiles x (H / 4 + 1) k-steps of 16x16x4 per wave.  The D
+// layout puts (unit 16 mu + 4 q + r, ped c16) in lane (q << 4 | c16),
+// register r of tile mu: "slot" j = 4 mu + r of that lane.  The wave applies
+// its gate's activation and writes slot j to LDS gate[g][j][lane]; after a
+// barrier wave w runs the cell update of slots w MU .. w MU + MU - 1 (c in
+// registers) and writes h to hb[j][lane].  The next step's B operand for
+// k-step ks is h of unit 16 (ks >> 2) + 4 q + (ks & 3) -- exactly
+// hb[ks][lane], because W_hh's columns are loaded in that permuted order.
+// Two barriers per step; every LDS access is lane-linear (conflict-free).
+// Decoder: the hidden2pos feedback r_t = Wp h_t + bp into step t+1 is folded
+// into the weights before step 1 (W_hh + A Wp, b' + A bp; lstm_unit.hip), so
+// r_t is off the critical path: wave partials in LDS, summed by wave 0 after
+// the step's second barrier.
+//
+// Backward step t (reverse): the slot owners turn dh_t (four gate-block
+// partials of W^T dG_{t+1} from LDS, + Wp^T dout_t for the decoder) into dG_t
+// with the saved activations (loaded a step ahead), writing dG_t to LDS
+// dgb[g][j][lane]; after a barrier wave g stores its gate block of dG_t
+// (float4 per lane) and computes that block's share of dh_{t-1}:
+//   P_g (H x 16) = W_hh,g^T (H x H) . dG_g^T       (MU tiles x H / 4 k-steps)
+// written to LDS for the next step's owners; second barrier.  The decoder
+// uses the folded W' for t >= 1 (its input r_{t-1} depends on h_{t-1}) and
+// plain W_hh at t = 0 (dh0).  drel_in = A^T dG_t is a slot partial reduced
+// over the q lanes and the waves off the critical path.
+#include <stdlib.h>
+#include <string.h>
+
+#include "sgg_common.h"
+
+namespace sgg {
+
+namespace {
+
+constexpr int kMwThreads = 256;   // four waves: one per gate block, one per SIMD
+constexpr int kMwPeds = 16;       // MFMA columns
+constexpr int kMwMaxT = 32;       // encoder inputs of up to this many steps are staged in LDS
+
+// v_exp_f32 / v_rcp_f32 forms (~2 ulp), as the other LSTM kernels.
+// s = 1: sigmoid(x); s = 2: tanh(x) = 2 sigmoid(2x) - 1 (the same
+// expressions as lstm_unit.hip's sigm_u / tanh_u)
+__device__ __forceinline__ float gate_act(float x, float s) {
+  return fmaf(s, __builtin_amdgcn_rcpf(1.f + __expf(-(s * x))), 1.f - s);
+}
+__device__ __forceinline__ float tanh_m(float x) {
+  return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f);
+}
+
+// unit held by slot j of lane quarter q
+__device__ __forceinline__ int slot_unit(int j, int q) { return 16 * (j >> 2) + 4 * q + (j & 3); }
+
+template <int H>
+__global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
+    const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
+    const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
+    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
+    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out) {
+  constexpr int MU = H / 16, KS = H / 4, G4 = 4 * H;
+  __shared__ float gate[4][KS][64];
+  __shared__ float hb[KS][64];
+  __shared__ float2 rpart[4][kMwPeds];
+  __shared__ float relseq[kMwMaxT][kMwPeds][2];
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, c16 = lane & 15;
+  const int ped = blockIdx.x * kMwPeds + c16;
+  const bool valid = ped < B;
+  const int pc = valid ? ped : B - 1;   // clamped: every load unconditional and in bounds
+  const bool save = act_all != nullptr;
+
+  // [W_hh,g | A_g b_g] in registers, W_hh's columns in the permuted k order
+  float w[MU][KS + 1], ak0[MU], ak1[MU];
+#pragma unroll
+  for (int mu = 0; mu < MU; ++mu) {
+    const int row = g * H + 16 * mu + c16;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) w[mu][ks] = Whh[row * H + slot_unit(ks, q)];
+    ak0[mu] = A[2 * row];
+    ak1[mu] = A[2 * row + 1];
+    w[mu][KS] = q == 0 ? ak0[mu] : q == 1 ? ak1[mu] : q == 2 ? bias[row] : 0.f;
+  }
+  float c[MU], wp0[MU], wp1[MU];
+#pragma unroll
+  for (int i = 0; i < MU; ++i) {
+    const int j = g * MU + i, u = slot_unit(j, q);
+    const float hv = h0 ? h0[(size_t)pc * H + u] : 0.f;
+    c[i] = c0 ? c0[(size_t)pc * H + u] : 0.f;
+    hb[j][lane] = hv;
+    if (valid && save) {
+      h_all[(size_t)ped * H + u] = hv;
+      c_all[(size_t)ped * H + u] = c[i];
+    }
+    wp0[i] = decoder ? Wp[u] : 0.f;
+    wp1[i] = decoder ? Wp[H + u] : 0.f;
+  }
+  const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
+  const bool staged = !decoder && T <= kMwMaxT;
+  if (staged)
+    for (int e = threadIdx.x; e < 2 * kMwPeds * T; e += kMwThreads) {
+      const int t = e / (2 * kMwPeds), p = (e >> 1) & (kMwPeds - 1), k = e & 1;
+      const int pp = blockIdx.x * kMwPeds + p;
+      relseq[t][p][k] = pp < B ? rel[((size_t)t * B + pp) * 2 + k] : 0.f;
+    }
+  __syncthreads();
+
+  // input k-step operand: r_x (q = 0), r_y (q = 1), 1 (q = 2), 0 (q = 3)
+  auto input = [&](int t) -> float {
+    if (q >= 2) return q == 2 ? 1.f : 0.f;
+    if (decoder) return rel[(size_t)pc * 2 + q];
+    return staged ? relseq[t][c16][q] : rel[((size_t)t * B + pc) * 2 + q];
+  };
+  float xin = input(0);
+  const float s = g == 2 ? 2.f : 1.f;   // g: tanh, i f o: sigmoid
+
+  for (int t = 0; t < T; ++t) {
+    if (decoder && t == 1) {
+      // fold the hidden2pos feedback into the recurrence (see header)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int u = slot_unit(ks, q);
+        const float p0 = Wp[u], p1 = Wp[H + u];
+#pragma unroll
+        for (int mu = 0; mu < MU; ++mu) w[mu][ks] = fmaf(ak1[mu], p1, fmaf(ak0[mu], p0, w[mu][ks]));
+      }
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu)
+        if (q == 2) w[mu][KS] = fmaf(ak1[mu], bp1, fmaf(ak0[mu], bp0, w[mu][KS]));
+      xin = q == 2 ? 1.f : 0.f;
+    }
+    floatx4 acc[MU];
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu)
+      acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][KS], xin, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    float hk[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[ks][lane];
+    if (!decoder && t + 1 < T) xin = input(t + 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][ks], hk[ks], acc[mu], 0, 0, 0);
+
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu) {
+      float a[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = gate_act(acc[mu][r], s);
+        gate[g][4 * mu + r][lane] = a[r];
+      }
+      if (valid && save)
+        *reinterpret_cast<float4*>(act_all + ((size_t)t * B + ped) * G4 + g * H + 16 * mu + 4 * q) =
+            make_float4(a[0], a[1], a[2], a[3]);
+    }
+    lds_barrier();
+
+    // cell update of this wave's slots
+    float px = 0.f, py = 0.f;
+#pragma unroll
+    for (int i = 0; i < MU; ++i) {
+      const int j = g * MU + i;
+      const float ig = gate[0][j][lane], fg = gate[1][j][lane], gg = gate[2][j][lane], og = gate[3][j][lane];
+      c[i] = fmaf(fg, c[i], ig * gg);
+      const float h = og * tanh_m(c[i]);
+      hb[j][lane] = h;
+      if (valid && (save || t == T - 1)) {
+        const size_t o = ((size_t)(save ? t + 1 : T) * B + ped) * H + slot_unit(j, q);
+        h_all[o] = h;
+        c_all[o] = c[i];
+      }
+      px = fmaf(wp0[i], h, px);
+      py = fmaf(wp1[i], h, py);
+    }
+    if (decoder) {
+      px += __shfl_xor(px, 16);
+      px += __shfl_xor(px, 32);
+      py += __shfl_xor(py, 16);
+      py += __shfl_xor(py, 32);
+      if (q == 0) rpart[g][c16] = make_float2(px, py);
+    }
+    lds_barrier();
+    if (decoder && g == 0 && q == 0 && valid) {   // r_t = Wp h_t + bp
+      const float2 r0 = rpart[0][c16], r1 = rpart[1][c16], r2 = rpart[2][c16], r3 = rpart[3][c16];
+      *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + ped) * 2) =
+          make_float2(((r0.x + r1.x) + (r2.x + r3.x)) + bp0, ((r0.y + r1.y) + (r2.y + r3.y)) + bp1);
+    }
+  }
+}
+
+template <int H>
+__global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
+    const float* __restrict__ A, const float* __restrict__ Whh, const float* __restrict__ Wp,
+    const float* __restrict__ c_all, const float* __restrict__ act_all, const float* __restrict__ dh_last,
+    const float* __restrict__ dout, int T, int B, int decoder, float* __restrict__ dG, float* __restrict__ dh0,
+    float* __restrict__ drel_in, float* __restrict__ drel_tot) {
+  constexpr int MU = H / 16, KS = H / 4, G4 = 4 * H;
+  __shared__ float dgb[4][KS][64];
+  __shared__ float part[4][KS][64];
+  __shared__ float2 fbp[4][kMwPeds];
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, c16 = lane & 15;
+  const int ped = blockIdx.x * kMwPeds + c16;
+  const bool valid = ped < B;
+  const int pc = valid ? ped : B - 1;
+
+  // W_hh,g^T in registers: wt[mu][ks] = W_hh[g H + slot_unit(ks, q)][16 mu + c16]
+  // (decoder: the folded W' = W_hh + A Wp for t >= 1, plain W_hh kept for t = 0)
+  float wt[MU][KS], wt0[MU][KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int row = g * H + slot_unit(ks, q);
+    const float a0 = decoder ? A[2 * row] : 0.f, a1 = decoder ? A[2 * row + 1] : 0.f;
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu) {
+      const int col = 16 * mu + c16;
+      const float v = Whh[row * H + col];
+      wt0[mu][ks] = v;
+      wt[mu][ks] = decoder ? fmaf(a1, Wp[H + col], fmaf(a0, Wp[col], v)) : v;
+    }
+  }
+  // per owned slot: rows of A for the four gates (A^T dG), Wp columns, dc
+  float aa0[MU][4], aa1[MU][4], wp0[MU], wp1[MU], dc[MU], dh[MU];
+#pragma unroll
+  for (int i = 0; i < MU; ++i) {
+    const int u = slot_unit(g * MU + i, q);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      aa0[i][k] = A[2 * (k * H + u)];
+      aa1[i][k] = A[2 * (k * H + u) + 1];
+    }
+    wp0[i] = decoder ? Wp[u] : 0.f;
+    wp1[i] = decoder ? Wp[H + u] : 0.f;
+    dc[i] = 0.f;
+    dh[i] = (!decoder && dh_last) ? dh_last[(size_t)pc * H + u] : 0.f;
+  }
+
+  // saved activations and cells of the owned slots (and the decoder's output
+  // gradient), one step ahead
+  float ni[MU], nf[MU], ng[MU], no[MU], nc[MU], ncp[MU], nd0 = 0.f, nd1 = 0.f;
+  auto load_step = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < MU; ++i) {
+      const int u = slot_unit(g * MU + i, q);
+      const float* ab = act_all + ((size_t)t * B + pc) * G4 + u;
+      ni[i] = ab[0];
+      nf[i] = ab[H];
+      ng[i] = ab[2 * H];
+      no[i] = ab[3 * H];
+      nc[i] = c_all[((size_t)(t + 1) * B + pc) * H + u];
+      ncp[i] = c_all[((size_t)t * B + pc) * H + u];
+    }
+    if (decoder) {
+      const float2 dv = *reinterpret_cast<const float2*>(dout + ((size_t)t * B + pc) * 2);
+      nd0 = dv.x;
+      nd1 = dv.y;
+    }
+  };
+  load_step(T - 1);
+  float din_x = 0.f, din_y = 0.f;   // drel_in[t + 1] (wave 0, q = 0 lanes)
+
+  for (int t = T - 1; t >= 0; --t) {
+    const float d0 = nd0, d1 = nd1;
+    float ci[MU], cf[MU], cg[MU], co[MU], cc[MU], ccp[MU];
+#pragma unroll
+    for (int i = 0; i < MU; ++i) {
+      ci[i] = ni[i];
+      cf[i] = nf[i];
+      cg[i] = ng[i];
+      co[i] = no[i];
+      cc[i] = nc[i];
+      ccp[i] = ncp[i];
+    }
+    if (t > 0) load_step(t - 1);   // in flight while this step computes
+
+    float f0 = 0.f, f1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MU; ++i) {
+      const int j = g * MU + i;
+      float dhv = dh[i];
+      if (t < T - 1) dhv = (part[0][j][lane] + part[1][j][lane]) + (part[2][j][lane] + part[3][j][lane]);
+      if (decoder) dhv = fmaf(wp0[i], d0, fmaf(wp1[i], d1, dhv));
+      const float ig = ci[i], fg = cf[i], gg = cg[i], og = co[i];
+      const float tc = tanh_m(cc[i]);
+      const float d_o = dhv * tc;
+      const float dct = fmaf(dhv * og, 1.f - tc * tc, dc[i]);
+      dc[i] = dct * fg;
+      const float vi = dct * gg * ig * (1.f - ig);
+      const float vf = dct * ccp[i] * fg * (1.f - fg);
+      const float vg = dct * ig * (1.f - gg * gg);
+      const float vo = d_o * og * (1.f - og);
+      dgb[0][j][lane] = vi;
+      dgb[1][j][lane] = vf;
+      dgb[2][j][lane] = vg;
+      dgb[3][j][lane] = vo;
+      f0 = fmaf(aa0[i][3], vo, fmaf(aa0[i][2], vg, fmaf(aa0[i][1], vf, fmaf(aa0[i][0], vi, f0))));
+      f1 = fmaf(aa1[i][3], vo, fmaf(aa1[i][2], vg, fmaf(aa1[i][1], vf, fmaf(aa1[i][0], vi, f1))));
+    }
+    f0 += __shfl_xor(f0, 16);
+    f0 += __shfl_xor(f0, 32);
+    f1 += __shfl_xor(f1, 16);
+    f1 += __shfl_xor(f1, 32);
+    if (q == 0) fbp[g][c16] = make_float2(f0, f1);
+    lds_barrier();
+
+    // gate block g of dG_t: global store + its share of dh_{t-1}
+    float bk[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bk[ks] = dgb[g][ks][lane];
+    if (decoder && t == 0) {
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) wt[mu][ks] = wt0[mu][ks];
+    }
+    floatx4 acc[MU];
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu) acc[mu] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[mu][ks], bk[ks], acc[mu], 0, 0, 0);
+    if (valid) {
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu)
+        *reinterpret_cast<float4*>(dG + ((size_t)t * B + ped) * G4 + g * H + 16 * mu + 4 * q) =
+            make_float4(bk[4 * mu], bk[4 * mu + 1], bk[4 * mu + 2], bk[4 * mu + 3]);
+    }
+    if (g == 0 && q == 0) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
+      const float2 r0 = fbp[0][c16], r1 = fbp[1][c16], r2 = fbp[2][c16], r3 = fbp[3][c16];
+      const float sx = (r0.x + r1.x) + (r2.x + r3.x), sy = (r0.y + r1.y) + (r2.y + r3.y);
+      if (valid) {
+        *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(sx, sy);
+        if (decoder) *reinterpret_cast<float2*>(drel_tot + ((size_t)t * B + ped) * 2) = make_float2(d0 + din_x, d1 + din_y);
+      }
+      din_x = sx;
+      din_y = sy;
+    }
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[g][4 * mu + r][lane] = acc[mu][r];
+    lds_barrier();
+  }
+  if (dh0 && valid) {   // dh0 = W_hh^T dG_0
+#pragma unroll
+    for (int i = 0; i < MU; ++i) {
+      const int j = g * MU + i;
+      dh0[(size_t)ped * H + slot_unit(j, q)] = (part[0][j][lane] + part[1][j][lane]) + (part[2][j][lane] + part[3][j][lane]);
+    }
+  }
+}
+
+template <int H>
+int launch_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0, const float* c0,
+               const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
+               float* rel_out, hipStream_t st) {
+  const int grid = (B + kMwPeds - 1) / kMwPeds;
+  hipLaunchKernelGGL(lstm_mw_fwd_kernel<H>, dim3(grid), dim3(kMwThreads), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp,
+                     T, B, decoder, h_all, c_all, act_all, rel_out);
+  SGG_RETURN_LAUNCH("sgg_lstm_fwd");
+}
+
+template <int H>
+int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all, const float* act_all,
+               const float* dh_last, const float* dout, int T, int B, int decoder, float* dG, float* dh0, float* drel_in,
+               float* drel_tot, hipStream_t st) {
+  const int grid = (B + kMwPeds - 1) / kMwPeds;
+  hipLaunchKernelGGL(lstm_mw_bwd_kernel<H>, dim3(grid), dim3(kMwThreads), 0, st, A, Whh, Wp, c_all, act_all, dh_last,
+                     dout, T, B, decoder, dG, dh0, drel_in, drel_tot);
+  SGG_RETURN_LAUNCH("sgg_lstm_bwd");
+}
+
+}  // namespace
+
+// Policy: H = 48 / 64 (the discriminator; the unit-per-thread kernels are
+// register-bound there).  SGG_LSTM_MW=all also routes H = 16 / 32 here,
+// SGG_LSTM_MW=0 disables this form (kernel comparisons, tools/).
+bool lstm_mw_ok(int H, int B) {
+  (void)B;
+  const char* e = getenv("SGG_LSTM_MW");
+  if (e && strcmp(e, "0") == 0) return false;
+  if (e && strcmp(e, "all") == 0) return H == 16 || H == 32 || H == 48 || H == 64;
+  return H == 48 || H == 64;
+}
+
+int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
+                const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
+                float* c_all, float* act_all, float* rel_out, hipStream_t st) {
+  switch (H) {
+    case 16: return launch_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    case 32: return launch_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    case 48: return launch_fwd<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    default: return launch_fwd<64>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+  }
+}
+
+int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all, const float* act_all,
+                const float* dh_last, const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,
+                float* drel_in, float* drel_tot, hipStream_t st) {
+  switch (H) {
+    case 16: return launch_bwd<16>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    case 32: return launch_bwd<32>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    case 48: return launch_bwd<48>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    default: return launch_bwd<64>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+  }
+}
+
+}  // namespace sgg

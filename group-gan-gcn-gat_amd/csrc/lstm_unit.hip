@@ -172,7 +172,7 @@ lstm_unit_fwd_kernel(
       const float r0 = ped_sum<TPP>(wp0 * h), r1 = ped_sum<TPP>(wp1 * h);
       if (q == 0 && valid) *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + ped) * 2) = make_float2(r0 + bp0, r1 + bp1);
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -257,7 +257,7 @@ lstm_unit_bwd_kernel(
       fb1 = ped_sum<TPP>(fmaf(a1[1], v[1], a1[0] * v[0]));
       if (q == 0 && valid) *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(fb0, fb1);
     }
-    __syncthreads();
+    lds_barrier();
     const float* dsrc = dgrow + 2 * half * H;
     float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

@@ -36,6 +36,14 @@ void set_error(const char* fmt, ...);
     return 0;                                                            \
   } while (0)
 
+// Workgroup barrier for kernels whose waves exchange data through LDS only:
+// waits for the wave's own LDS operations (lgkmcnt) but not for its
+// outstanding global stores, which __syncthreads()' workgroup-scope release
+// drains (vmcnt(0)) -- in a per-step recurrence that puts a store round trip
+// on every step.  Global data written by other waves of the workgroup is NOT
+// ordered by it.
+__device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -70,6 +78,19 @@ __attribute__((visibility("hidden"))) int lstm_unit_bwd(const float* A, const fl
                                                         const float* c_all, const float* act_all, const float* dh_last,
                                                         const float* dout, int T, int B, int H, int decoder, float* dG,
                                                         float* dh0, float* drel_in, float* drel_tot, hipStream_t st);
+
+// lstm_mw.hip: MFMA LSTM sequence kernels, one workgroup of four waves (one
+// per gate block) per 16 peds; dispatched first by sgg_lstm_fwd / _bwd; internal
+__attribute__((visibility("hidden"))) bool lstm_mw_ok(int H, int B);
+__attribute__((visibility("hidden"))) int lstm_mw_fwd(const float* rel, const float* A, const float* Whh,
+                                                      const float* bias, const float* h0, const float* c0,
+                                                      const float* Wp, const float* bp, int T, int B, int H,
+                                                      int decoder, float* h_all, float* c_all, float* act_all,
+                                                      float* rel_out, hipStream_t st);
+__attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp,
+                                                      const float* c_all, const float* act_all, const float* dh_last,
+                                                      const float* dout, int T, int B, int H, int decoder, float* dG,
+                                                      float* dh0, float* drel_in, float* drel_tot, hipStream_t st);
 
 // v if keep else +0.f, as a bit mask: a plain `keep ? v : 0` lets the
 // compiler sink the load of v into an exec-masked branch that waits for it

@@ -111,33 +111,48 @@ __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restric
   }
 }
 
-// slab sum: block = 64 outputs x 4 split phases; fixed order -> deterministic.
-// The split loop is unrolled 8-wide so its loads are in flight together (the
-// partial slabs were just written: L2 hits, latency- not bandwidth-bound).
-__global__ void __launch_bounds__(256) xtw_reduce_kernel(const float* __restrict__ slab, int splits, int MN,
-                                                         float* __restrict__ C, int N, int ldc, int trans_c) {
-  __shared__ float part[4][64];
+// slab sums: block = 64 outputs x 16 split phases (1024 threads), fixed
+// order -> deterministic; the blocks past the C outputs sum the column-sum
+// slab, so C and the bias gradient take ONE launch.  Each phase walks
+// <= splits / 16 partials with 4 loads in flight (the partial slabs were just
+// written: L2 hits, latency- not bandwidth-bound).
+__global__ void __launch_bounds__(1024) xtw_reduce_kernel(const float* __restrict__ slab, int splits, int MN,
+                                                          float* __restrict__ C, int N, int ldc, int trans_c,
+                                                          const float* __restrict__ colslab,
+                                                          float* __restrict__ colsum) {
+  __shared__ float part[16][64];
   const int el = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + el;
+  const int nbm = (MN + 63) / 64;
+  const bool col = (int)blockIdx.x >= nbm;
+  const float* src = col ? colslab : slab;
+  const int cnt = col ? N : MN;
+  const int e = (col ? (int)blockIdx.x - nbm : (int)blockIdx.x) * 64 + el;
   float s = 0.f;
-  if (e < MN) {
+  if (e < cnt) {
     int k = ph;
-    for (; k + 28 < splits; k += 32) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = slab[(size_t)(k + 4 * u) * MN + e];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+    for (; k + 48 < splits; k += 64) {
+      const float v0 = src[(size_t)k * cnt + e], v1 = src[(size_t)(k + 16) * cnt + e];
+      const float v2 = src[(size_t)(k + 32) * cnt + e], v3 = src[(size_t)(k + 48) * cnt + e];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
     }
-    for (; k < splits; k += 4) s += slab[(size_t)k * MN + e];
+    for (; k < splits; k += 16) s += src[(size_t)k * cnt + e];
   }
   part[ph][el] = s;
   __syncthreads();
-  if (ph == 0 && e < MN) {
-    const float v = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
-    const int mm = e / N, n = e - mm * N;
-    if (trans_c) C[(size_t)n * ldc + mm] = v;
-    else C[(size_t)mm * ldc + n] = v;
+  if (ph == 0 && e < cnt) {
+    float v = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) v += part[p][el];
+    if (col) {
+      colsum[e] = v;
+    } else {
+      const int mm = e / N, n = e - mm * N;
+      if (trans_c) C[(size_t)n * ldc + mm] = v;
+      else C[(size_t)mm * ldc + n] = v;
+    }
   }
 }
 
@@ -146,16 +161,19 @@ __global__ void __launch_bounds__(256) xtw_reduce_kernel(const float* __restrict
 using namespace sgg;
 
 extern "C" int sgg_xtw_splits(int R, int M, int N) {
-  // ~32 rows per split (two 16-row MFMA steps: the partial kernel is one or
-  // two load latencies long), capped by the grid (<= 4096 workgroups) and
-  // by the slab (<= 2^21 floats, so the reduce stays an L2-resident pass)
+  // >= ~32 rows per split (two 16-row MFMA steps), capped by the grid
+  // (<= 1024 workgroups: thousands of one-step workgroups cost more in
+  // dispatch than they compute), by the slab (<= 2^21 floats, so the reduce
+  // stays an L2-resident pass) and at 256 partials per output (the reduce's
+  // phases walk <= 16 each)
   const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
   const long long mn = (long long)M * N;
   long long splits = (R + 31) / 32;
-  const long long by_grid = 4096 / tiles > 0 ? 4096 / tiles : 1;
+  const long long by_grid = 1024 / tiles > 0 ? 1024 / tiles : 1;
   const long long by_slab = (1ll << 21) / mn > 0 ? (1ll << 21) / mn : 1;
   if (splits > by_grid) splits = by_grid;
   if (splits > by_slab) splits = by_slab;
+  if (splits > 256) splits = 256;
   return splits < 1 ? 1 : (int)splits;
 }
 
@@ -176,8 +194,8 @@ extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const f
   hipLaunchKernelGGL(xtw_partial_kernel, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws,
                      colsum ? colslab : nullptr);
   const int MN = M * N;
-  hipLaunchKernelGGL(xtw_reduce_kernel, dim3((MN + 63) / 64), dim3(256), 0, st, ws, splits, MN, C, N, ldc, trans_c);
-  if (colsum)
-    hipLaunchKernelGGL(xtw_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, st, colslab, splits, N, colsum, N, N, 0);
+  const int nb = (MN + 63) / 64 + (colsum ? (N + 63) / 64 : 0);
+  hipLaunchKernelGGL(xtw_reduce_kernel, dim3(nb), dim3(1024), 0, st, ws, splits, MN, C, N, ldc, trans_c,
+                     colsum ? colslab : nullptr, colsum);
   SGG_RETURN_LAUNCH("sgg_xtw");
 }

@@ -346,6 +346,16 @@ def test_fused_lstm_vs_oracle(H, T, decoder, B):
         close(q.grad, p.grad.numpy(), rtol=1e-4, floor=1e-6, what="lstm d" + k)
 
 
+@pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (32, 12, True, 37), (16, 5, True, 21),
+                                            (48, 12, True, 37), (64, 3, True, 37), (48, 20, False, 2085)])
+def test_fused_lstm_multiwave_all_sizes(H, T, decoder, B, monkeypatch):
+    """lstm_mw.hip (four waves per 16 peds) on every hidden size and both
+    directions, decoder included (the default policy routes only H = 48 / 64
+    encoders there)."""
+    monkeypatch.setenv("SGG_LSTM_MW", "all")
+    test_fused_lstm_vs_oracle(H, T, decoder, B)
+
+
 def test_xtw_matches_torch():
     from sgan import kernels as K
     torch.manual_seed(1)

@@ -84,6 +84,45 @@ def lstm(B, T, H, decoder, reps=10, save=False):
         B, T, H, decoder, save, us, flops / us / 1e6), flush=True)
 
 
+def lstm_ab(B, T, H, decoder, reps=20):
+    """sgg_lstm_fwd / _bwd with the four-wave MFMA form (SGG_LSTM_MW=all)
+    against the previous forms (SGG_LSTM_MW=0)."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    lib = N.load()
+    rel = torch.randn(1 if decoder else T, B, 2, device=dev).squeeze(0) * 0.3
+    A = torch.randn(4 * H, 2, device=dev) * 0.3
+    Whh = torch.randn(4 * H, H, device=dev) * 0.2
+    bias = torch.randn(4 * H, device=dev) * 0.1
+    h0 = torch.randn(B, H, device=dev) * 0.5
+    Wp = torch.randn(2, H, device=dev) * 0.2
+    bp = torch.randn(2, device=dev) * 0.1
+    h_all = torch.empty(T + 1, B, H, device=dev)
+    c_all = torch.empty(T + 1, B, H, device=dev)
+    act = torch.empty(T, B, 4 * H, device=dev)
+    rel_out = torch.empty(T, B, 2, device=dev)
+    dG = torch.empty(T, B, 4 * H, device=dev)
+    drel_in = torch.empty(T, B, 2, device=dev)
+    drel_tot = torch.empty(T, B, 2, device=dev)
+    dh0 = torch.empty(B, H, device=dev)
+    dout = torch.randn(T, B, 2, device=dev)
+    dhl = torch.randn(B, H, device=dev)
+    fwd = lambda: N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0), None, N.ptr(Wp),
+                                           N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
+                                           N.ptr(rel_out), N.stream_ptr()), "lstm_fwd")
+    bwd = lambda: N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(c_all), N.ptr(act),
+                                           None if decoder else N.ptr(dhl), N.ptr(dout) if decoder else None, T, B,
+                                           H, int(decoder), N.ptr(dG), N.ptr(dh0), N.ptr(drel_in),
+                                           N.ptr(drel_tot), N.stream_ptr()), "lstm_bwd")
+    res = []
+    for mode in ("0", "all"):
+        os.environ["SGG_LSTM_MW"] = mode
+        res.append((timeit(fwd, reps), timeit(bwd, reps)))
+    os.environ.pop("SGG_LSTM_MW")
+    print("lstm B=%5d T=%2d H=%2d dec=%d  old fwd %6.1f bwd %6.1f us | mw fwd %6.1f bwd %6.1f us" % (
+        B, T, H, decoder, res[0][0], res[0][1], res[1][0], res[1][1]), flush=True)
+
+
 def timeit(call, reps=20):
     for _ in range(3):
         call()
@@ -120,6 +159,12 @@ if __name__ == "__main__":
         run(1280, 20, 32, 8, reps=5)
         sys.exit(0)
     if what == "dense":
+        dense()
+        sys.exit(0)
+    if what == "ab":
+        for args in ((2560, 20, 48, False), (1280, 20, 48, False), (1280, 8, 32, False), (2560, 12, 32, True),
+                     (1280, 12, 32, True)):
+            lstm_ab(*args)
         dense()
         sys.exit(0)
     if what == "lstm":
