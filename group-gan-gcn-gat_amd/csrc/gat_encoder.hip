@@ -142,13 +142,17 @@ struct PLayout {
 __host__ __device__ inline PLayout make_playout(int nh) {
   PLayout P;
   int o = 0;
-  for (int h = 0; h < nh; ++h) {
+#pragma unroll
+  for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
     P.Wi[h] = o; o += FI * FH;
     P.ai[h] = o; o += 2 * FH;
   }
   P.Wio = o; o += FH * nh * FO;
   P.aio = o; o += 2 * FO;
-  for (int h = 0; h < nh; ++h) {
+#pragma unroll
+  for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
     P.Wg[h] = o; o += FO * FH;
     P.ag[h] = o; o += 2 * FH;
   }
@@ -425,13 +429,17 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
   LW lw;
   {
     float* q = sm + L.wts;
-    for (int h = 0; h < nh; ++h) {
+#pragma unroll
+    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
       lw.Wi[h] = q; q = stage_mat(q, p.w.Wi[h], FI, FH, blockDim.x);
       lw.ai[h] = q; q = stage_vec(q, p.w.ai[h], 2 * FH, blockDim.x);
     }
     lw.Wio = q; q = stage_mat(q, p.w.Wio, FH * nh, FO, blockDim.x);
     lw.aio = q; q = stage_vec(q, p.w.aio, 2 * FO, blockDim.x);
-    for (int h = 0; h < nh; ++h) {
+#pragma unroll
+    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
       lw.Wg[h] = q; q = stage_mat(q, p.w.Wg[h], FO, FH, blockDim.x);
       lw.ag[h] = q; q = stage_vec(q, p.w.ag[h], 2 * FH, blockDim.x);
     }
@@ -480,7 +488,9 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     const int M = *Mp;
 
     // ---- intra GAT: heads (40 -> 72, ELU), out (72 nh -> 16, ELU, log_softmax)
-    for (int h = 0; h < nh; ++h) {
+#pragma unroll
+    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
       lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
       __syncthreads();
       scores(Wh, P72, n, FH, lw.ai[h], s, t);
@@ -504,7 +514,9 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     }
     __syncthreads();
     // ---- inter GAT on the complete graph of the M groups ----------------
-    for (int h = 0; h < nh; ++h) {
+#pragma unroll
+    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
       lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
       __syncthreads();
       scores(Wh, P72, M, FH, lw.ag[h], s, t);
@@ -613,7 +625,9 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     __syncthreads();
     // ---- inter heads ----
     for (int e = tid; e < M * FO; e += blockDim.x) dG[(e / FO) * P16 + e % FO] = 0.f;   // becomes d gin
-    for (int h = 0; h < nh; ++h) {
+#pragma unroll
+    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
       // ELU backward from the stored output: elu'(x) = 1 (y > 0) | y + 1
       for (int e = tid; e < M * FH; e += blockDim.x) {
         const int r = e / FH, f = e - r * FH;
@@ -644,7 +658,9 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     __syncthreads();
     // ---- intra heads ----
     float* dXo = p.dX + (size_t)o * p.lddx;
-    for (int h = 0; h < nh; ++h) {
+#pragma unroll
+    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
+      if (h >= nh) break;
       for (int e = tid; e < n * FH; e += blockDim.x) {
         const int r = e / FH, f = e - r * FH;
         const float yv = H1[r * PH + h * FH + f];

@@ -18,11 +18,9 @@
 // so their bit patterns order like the floats, and ties resolve to the
 // smallest j.  The winning j is kept for the backward.
 //
-// Backward: only (i, argmax[i,c]) carries gradient.  One workgroup of 512
-// threads, thread k = hidden unit k, walks the scene's selected pairs grouped
-// by j (lists built with a wave ballot, deterministic order): U[j,k] is read
-// once per j (coalesced), dU[j,k] is produced in a register and stored once,
-// dW2[:,k] lives in LDS (thread-owned column: no atomics), dA in registers.
+// Backward: only (i, argmax[i,c]) carries gradient; selected entries indexed
+// by (j, c) bitmasks, thread = hidden unit, W2 column and dW2 partial in
+// registers (see pool_bwd_kernel).
 #include "sgg_common.h"
 
 namespace sgg {
@@ -208,92 +206,102 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
   }
 }
 
-template <int BN>
+// ---- backward ---------------------------------------------------------------
+// Only (i, argmax[i, c]) carries gradient.  Work unit = (scene, j range): the
+// scene's pooled-from peds j are cut into jq ranges so that S x jq units fill
+// the chip (sgg_pool_bwd_grid).  The selected entries of the scene are indexed
+// by (j, c) as 64-bit masks over i, built with LDS atomic OR (order-free, so
+// deterministic).  Thread k = hidden unit k walks its unit's j range and, per
+// j, the statically unrolled c loop over the set bits i of mask (j, c): W2[c][k]
+// and the dW2[c][k] partial stay in registers (no memory access on the
+// per-entry chain), U[j, k] is read once (coalesced) and dU[j, k] stored
+// once; the per-entry operands (g, p_i) are wave-uniform LDS broadcasts and
+// the bit walk is scalar.  Each workgroup writes its [dW2 | dA | db2] partial
+// to its own slab row; WGRAD = false (frozen weights) computes dU only.
+template <int BN, bool WGRAD>
 __global__ void __launch_bounds__(512) pool_bwd_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ out,
     const int32_t* __restrict__ argmax, const float* __restrict__ dout, const int32_t* __restrict__ scene_off,
-    int S, int max_n, float* __restrict__ dU, float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int k = threadIdx.x;  // hidden unit, blockDim.x == 512
-  const int lane = k & 63;
-  const int wave = k >> 6;
-  float* dW2s = reinterpret_cast<float*>(smem);                 // BN x 512
-  float* gs = dW2s + BN * kHidden;                               // max_n*BN
-  int* js = reinterpret_cast<int*>(gs + max_n * BN);             // max_n*BN (local j)
-  int* lst = js + max_n * BN;                                    // max_n*BN entries
-  int* loff = lst + max_n * BN;                                  // max_n + 1
-  float2* ps = reinterpret_cast<float2*>(loff + ((max_n + 2) & ~1));
-
+    int S, int jq, float* __restrict__ dU, float* __restrict__ part) {
+  __shared__ unsigned long long msk[SGG_POOL_MAX_PEDS * BN];   // (j, c) -> set of i
+  __shared__ float gs[SGG_POOL_MAX_PEDS * BN];                 // masked dout (i, c)
+  __shared__ float2 ps[SGG_POOL_MAX_PEDS];
+  const int k = threadIdx.x;   // hidden unit, blockDim.x == 512
+  float w2[BN], dw2[BN];
 #pragma unroll
-  for (int c = 0; c < BN; ++c) dW2s[c * kHidden + k] = 0.f;
+  for (int c = 0; c < BN; ++c) {
+    w2[c] = W2[c * kHidden + k];
+    dw2[c] = 0.f;
+  }
   const float a0 = A[2 * k], a1 = A[2 * k + 1];
-  float dA0 = 0.f, dA1 = 0.f;
-  float db2 = 0.f;   // thread c < BN: this workgroup's share of db2[c] = sum_i [out_ic > 0] dout_ic
-
-  for (int s = blockIdx.x; s < S; s += gridDim.x) {
+  float dA0 = 0.f, dA1 = 0.f, db2 = 0.f;
+  for (int un = blockIdx.x; un < S * jq; un += gridDim.x) {
+    const int s = un / jq, jp = un - s * jq;
     const int o = scene_off[s];
     const int n = scene_off[s + 1] - o;
     const int ne = n * BN;
-    for (int e = k; e < ne; e += blockDim.x) {
+    const int j0 = (n * jp) / jq, j1 = (n * (jp + 1)) / jq;
+    for (int e = k; e < ne; e += kHidden) {
       const size_t ge = (size_t)o * BN + e;
       gs[e] = out[ge] > 0.f ? dout[ge] : 0.f;
-      js[e] = argmax[ge] - o;
+      msk[e] = 0ull;
     }
-    for (int q = k; q < n; q += blockDim.x) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
+    for (int q = k; q < n; q += kHidden) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
     __syncthreads();
-    if (k < BN)
-      for (int i = 0; i < n; ++i) db2 += gs[i * BN + k];
-    if (wave == 0) {  // stable bucket of the selected (i, c) entries by j
-      int cnt = 0;
-      for (int j = 0; j < n; ++j) {
-        if (lane == 0) loff[j] = cnt;
-        for (int b = 0; b < ne; b += 64) {
-          const int e = b + lane;
-          const bool pred = e < ne && js[e] == j && gs[e] != 0.f;
-          const unsigned long long m = __ballot(pred);
-          if (pred) lst[cnt + __popcll(m & ((1ull << lane) - 1ull))] = e;
-          cnt += __popcll(m);
-        }
+    for (int e = k; e < ne; e += kHidden) {
+      if (gs[e] != 0.f) {
+        const int i = e / BN, c = e - i * BN;
+        const int j = argmax[(size_t)o * BN + e] - o;
+        atomicOr(&msk[j * BN + c], 1ull << i);
       }
-      if (lane == 0) loff[n] = cnt;
     }
+    if (WGRAD && jp == 0 && k < BN)
+      for (int i = 0; i < n; ++i) db2 += gs[i * BN + k];
     __syncthreads();
-    const float* Us = U + (size_t)o * kHidden + k;
-    float u_next = n > 0 ? Us[0] : 0.f;
-    for (int j = 0; j < n; ++j) {
+    const float* Uc = U + (size_t)o * kHidden + k;
+    float u_next = j0 < j1 ? Uc[(size_t)j0 * kHidden] : 0.f;
+    for (int j = j0; j < j1; ++j) {
       const float u = u_next;
-      if (j + 1 < n) u_next = Us[(size_t)(j + 1) * kHidden];
+      if (j + 1 < j1) u_next = Uc[(size_t)(j + 1) * kHidden];
       const float2 pj = ps[j];
       float du = 0.f;
-      const int e1 = loff[j + 1];
-      for (int q = loff[j]; q < e1; ++q) {
-        const int e = lst[q];
-        const int i = e / BN;
-        const int c = e - i * BN;
-        const float g = gs[e];
-        const float rx = pj.x - ps[i].x;
-        const float ry = pj.y - ps[i].y;
-        const float pre = fmaf(a1, ry, fmaf(a0, rx, u));
-        if (pre > 0.f) {
-          dW2s[c * kHidden + k] += g * pre;
-          const float d = g * W2[c * kHidden + k];
+#pragma unroll
+      for (int c = 0; c < BN; ++c) {
+        const unsigned long long mv = msk[j * BN + c];
+        // (readfirstlane returns int: go through unsigned, no sign extension)
+        const unsigned mhi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(mv >> 32));
+        const unsigned mlo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mv);
+        unsigned long long m = ((unsigned long long)mhi << 32) | (unsigned long long)mlo;
+        while (m) {
+          const int i = __builtin_ctzll(m);
+          m &= m - 1;
+          const float g = gs[i * BN + c];
+          const float2 pi = ps[i];
+          const float rx = pj.x - pi.x, ry = pj.y - pi.y;
+          const float pre = fmaf(a1, ry, fmaf(a0, rx, u));
+          const float gm = pre > 0.f ? g : 0.f;
+          const float d = gm * w2[c];
           du += d;
-          dA0 = fmaf(d, rx, dA0);
-          dA1 = fmaf(d, ry, dA1);
+          if (WGRAD) {
+            dw2[c] = fmaf(gm, pre, dw2[c]);
+            dA0 = fmaf(d, rx, dA0);
+            dA1 = fmaf(d, ry, dA1);
+          }
         }
       }
       dU[(size_t)(o + j) * kHidden + k] = du;
     }
-    __syncthreads();  // lists / gs reused by the next scene
+    __syncthreads();   // msk / gs / ps reused by the next unit
   }
-  // this workgroup's row of the parameter-gradient slab: [dW2 (BN x 512) | dA (512 x 2) | db2 (BN)]
-  float* row = part + (size_t)blockIdx.x * (BN * kHidden + 2 * kHidden + BN);
+  if (WGRAD) {   // this workgroup's row of the parameter-gradient slab: [dW2 (BN x 512) | dA (512 x 2) | db2 (BN)]
+    float* row = part + (size_t)blockIdx.x * (BN * kHidden + 2 * kHidden + BN);
 #pragma unroll
-  for (int c = 0; c < BN; ++c) row[c * kHidden + k] = dW2s[c * kHidden + k];
-  row[BN * kHidden + 2 * k] = dA0;
-  row[BN * kHidden + 2 * k + 1] = dA1;
-  if (k < BN) row[BN * kHidden + 2 * kHidden + k] = db2;
+    for (int c = 0; c < BN; ++c) row[c * kHidden + k] = dw2[c];
+    row[BN * kHidden + 2 * k] = dA0;
+    row[BN * kHidden + 2 * k + 1] = dA1;
+    if (k < BN) row[BN * kHidden + 2 * kHidden + k] = db2;
+  }
 }
 
 template <int BN>
@@ -311,9 +319,11 @@ static void launch_fwd_g(const float* U, const float* pos, const float* A, const
   hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW>), dim3(grid), dim3(256), pool_fwd_lds<BN>(max_rows), st, U, pos, A,
                      W2, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, out, am);
 }
-static size_t pool_bwd_lds(int bn, int max_n) {
-  return (size_t)bn * kHidden * 4 + (size_t)max_n * bn * 12 + (size_t)(((max_n + 2) & ~1) * 4) +
-         (size_t)max_n * 8 + 16;
+// j ranges per scene of the backward: S x jq units ~ one round of the chip
+static int pool_bwd_jq(int S) {
+  if (S < 1) return 1;
+  const int jq = 256 / S;
+  return jq < 1 ? 1 : (jq > 8 ? 8 : jq);
 }
 
 template <int BN>
@@ -333,9 +343,14 @@ template <int BN>
 static int launch_bwd(const float* U, const float* pos, const float* A, const float* W2, const float* out,
                       const int32_t* am, const float* dout, const int32_t* off, int S, int max_n, float* dU,
                       float* part, hipStream_t st) {
-  const size_t lds = pool_bwd_lds(BN, max_n);
-  hipLaunchKernelGGL(pool_bwd_kernel<BN>, dim3(sgg_pool_bwd_grid(S)), dim3(512), lds, st, U, pos, A, W2, out,
-                     am, dout, off, S, max_n, dU, part);
+  (void)max_n;
+  const int grid = sgg_pool_bwd_grid(S), jq = pool_bwd_jq(S);
+  if (part)
+    hipLaunchKernelGGL((pool_bwd_kernel<BN, true>), dim3(grid), dim3(512), 0, st, U, pos, A, W2, out, am, dout, off, S,
+                       jq, dU, part);
+  else
+    hipLaunchKernelGGL((pool_bwd_kernel<BN, false>), dim3(grid), dim3(512), 0, st, U, pos, A, W2, out, am, dout, off,
+                       S, jq, dU, part);
   SGG_RETURN_LAUNCH("sgg_pool_bwd");
 }
 
@@ -417,13 +432,16 @@ extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, co
   }
 }
 
-extern "C" int sgg_pool_bwd_grid(int S) { return S < 1 ? 1 : (S < 256 ? S : 256); }
+extern "C" int sgg_pool_bwd_grid(int S) {
+  if (S < 1) return 1;
+  const long long u = (long long)S * pool_bwd_jq(S);
+  return (int)(u < 256 ? u : 256);
+}
 
 extern "C" int sgg_pool_bwd(const float* U, const float* pos, const float* A, const float* W2, const float* out,
                             const int32_t* argmax, const float* dout, const int32_t* scene_off, int S, int B,
                             int bn, int max_n, float* dU, float* part, void* stream) {
-  SGG_CHECK_ARG(U && pos && A && W2 && out && argmax && dout && scene_off && dU && part,
-                "sgg_pool_bwd: null pointer");
+  SGG_CHECK_ARG(U && pos && A && W2 && out && argmax && dout && scene_off && dU, "sgg_pool_bwd: null pointer");
   SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_bwd: bottleneck %d not built", bn);
   SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "sgg_pool_bwd: max scene size %d outside [1, %d]",
                 max_n, SGG_POOL_MAX_PEDS);

@@ -235,19 +235,19 @@ class _Pool(torch.autograd.Function):
         sc, E = ctx.scenes, ctx.E
         B, bn = out.shape
         dout = dout.contiguous()
-        grid = lib.sgg_pool_bwd_grid(sc.S)
+        need = ctx.needs_input_grad
+        wgrad = any(need[2:8])       # False: weights frozen (the G-step's discriminator), input gradient only
         P = bn * 512 + 1024 + bn
         dU = torch.empty(B, 512, device=h.device, dtype=torch.float32)
-        part = torch.empty(grid, P, device=h.device, dtype=torch.float32)
+        part = torch.empty(lib.sgg_pool_bwd_grid(sc.S), P, device=h.device, dtype=torch.float32) if wgrad else None
         N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(out), N.ptr(am), N.ptr(dout),
                                  N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(part),
                                  N.stream_ptr()), "sgg_pool_bwd")
-        need = ctx.needs_input_grad
         dh = xw_raw(dU, W1[:, E:], None, trans_w=False) if need[0] else None
-        if not any(need[2:8]):       # weights frozen (the G-step's discriminator): input gradient only
+        if not wgrad:
             return dh, None, None, None, None, None, None, None, None
         flat = torch.empty(P, device=h.device, dtype=torch.float32)     # [dW2 | dA | db2]
-        N.check(lib.sgg_slab_reduce(N.ptr(part), grid, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+        N.check(lib.sgg_slab_reduce(N.ptr(part), part.shape[0], P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
         dW1 = torch.empty_like(W1)
         _, dc = xtw(h, dU, colsum=True, trans_c=True, out=dW1[:, E:])   # dW1h = dU^T h, dc = sum_j dU_j
         _, dWe, dbe = fold_bwd(W1[:, :E], We, be, flat[bn * 512:bn * 512 + 1024].view(512, 2), dc, dW=dW1[:, :E])

@@ -90,7 +90,8 @@ int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* 
  * and one row per workgroup of the parameter-gradient slab `part`
  * (grid x (bn*512 + 1024 + bn), grid = sgg_pool_bwd_grid(S)): the
  * workgroup's partial sums of [dW2 (bn x 512) | dA (512 x 2) | db2 (bn)];
- * sgg_slab_reduce sums the rows (fixed order => deterministic).
+ * sgg_slab_reduce sums the rows (fixed order => deterministic).  part may be
+ * NULL (frozen weights, e.g. the G-step's discriminator): dU only.
  * pos gets no gradient (it is an input trajectory in every caller). */
 int sgg_pool_bwd_grid(int S);
 int sgg_pool_bwd(const float* U, const float* pos, const float* A, const float* W2,

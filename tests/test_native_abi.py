@@ -34,7 +34,9 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, n), n
     assert set(declared()) == set(_native.SIGNATURES), "ctypes table out of sync with include/sgg.h"
     assert lib.sgg_version() >= 1
-    assert lib.sgg_pool_bwd_grid(10) == 10 and lib.sgg_pool_bwd_grid(100000) == 256
+    # S x jq (scene, j-range) units, jq = clamp(256 / S, 1, 8), capped at 256 workgroups
+    assert lib.sgg_pool_bwd_grid(10) == 80 and lib.sgg_pool_bwd_grid(64) == 256
+    assert lib.sgg_pool_bwd_grid(100000) == 256 and lib.sgg_pool_bwd_grid(0) == 1
 
 
 def test_product_path_has_no_cpu_fallback():
