@@ -21,6 +21,8 @@
 // Backward: only (i, argmax[i,c]) carries gradient; selected entries indexed
 // by (j, c) bitmasks, thread = hidden unit, W2 column and dW2 partial in
 // registers (see pool_bwd_kernel).
+#include <stdlib.h>
+
 #include "sgg_common.h"
 
 namespace sgg {
@@ -206,6 +208,156 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
   }
 }
 
+// ---- forward, resident form -------------------------------------------------
+// When the whole W2^T (bn rows x 512, rows padded to 16 NT with zeros) and a
+// scene's U rows fit in LDS beside each other: the workgroup stages W2 and A
+// once for its lifetime (persistent grid over the chunk table) and the U rows
+// of a chunk's scene when the scene changes, then runs all 128 k-steps with
+// no barrier.  Same chunk table, pair set-up, MFMA step and epilogue as the
+// tiled kernel above (bitwise the same results).
+constexpr int kUP = kHidden + 2;   // resident row pitch (U rows, W2 rows): 2 mod 32 -> conflict-free b32 reads
+
+// rows x 512 row-major block -> LDS at pitch kUP (rows >= zrow read as 0,
+// zrow >= 1): float4 loads, 8 per thread in flight before the stores
+__device__ inline void stage_rows512(float* dst, const float* __restrict__ src, int rows, int zrow) {
+  const int tot = rows * (kHidden / 4);
+  for (int e0 = threadIdx.x; e0 < tot; e0 += 8 * (int)blockDim.x) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = min(e0 + u * (int)blockDim.x, tot - 1);
+      const int r = e / (kHidden / 4), c4 = e - r * (kHidden / 4);
+      const float4 x = *reinterpret_cast<const float4*>(src + (size_t)min(r, zrow - 1) * kHidden + 4 * c4);
+      const bool ok = r < zrow;
+      v[u] = make_float4(keep_if(x.x, ok), keep_if(x.y, ok), keep_if(x.z, ok), keep_if(x.w, ok));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * (int)blockDim.x;
+      if (e < tot) {
+        const int r = e / (kHidden / 4), c4 = e - r * (kHidden / 4);
+        float2* d = reinterpret_cast<float2*>(dst + r * kUP + 4 * c4);
+        d[0] = make_float2(v[u].x, v[u].y);
+        d[1] = make_float2(v[u].z, v[u].w);
+      }
+    }
+  }
+}
+
+template <int BN, int GPW>
+__global__ void __launch_bounds__(256) pool_fwd_res_kernel(
+    const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
+    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks, int max_n,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+  constexpr int NT = PoolCfg<BN>::NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* W2s = reinterpret_cast<float*>(smem);                                    // 16 NT rows x kUP
+  float* As = W2s + 16 * NT * kUP;                                                // 512 x 2
+  float* Us = As + 2 * kHidden;                                                   // max_n rows x kUP
+  float2* ps = reinterpret_cast<float2*>(Us + (size_t)max_n * kUP);               // max_n
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + max_n);   // rows x BN
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kq = lane >> 4;
+
+  stage_rows512(W2s, W2, 16 * NT, BN);
+  for (int e = threadIdx.x; e < 2 * kHidden; e += 256) As[e] = A[e];
+  int cur = -1;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int4 cd = chunks[ch];
+    const int s = cd.x, i0 = cd.y, i1 = cd.z;
+    const int o = scene_off[s];
+    const int n = scene_off[s + 1] - o;
+    const int rows = i1 - i0;
+    const int npairs = rows * n;
+    __syncthreads();   // W2s / As staged (first chunk); the previous chunk's readers of Us, ps, keys done
+    if (s != cur) {
+      stage_rows512(Us, U + (size_t)o * kHidden, n, n);
+      for (int q = threadIdx.x; q < n; q += 256) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
+      cur = s;
+    }
+    for (int q = threadIdx.x; q < rows * BN; q += 256) keys[q] = 0ull;
+    __syncthreads();
+
+    int uoff[GPW];
+    float rx[GPW], ry[GPW];
+    bool gv[GPW];
+    floatx4 acc[GPW][NT];
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int p = (wave * GPW + g) * 16 + c16;
+      gv[g] = (wave * GPW + g) * 16 < npairs;   // wave-uniform: a group with pairs
+      int il = 0, j = 0;
+      if (p < npairs) { il = p / n; j = p - il * n; }
+      uoff[g] = j * kUP + kq;
+      const float2 pj = ps[j], pi = ps[i0 + il];
+      rx[g] = p < npairs ? pj.x - pi.x : 0.f;
+      ry[g] = p < npairs ? pj.y - pi.y : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    float b[NT], u[GPW];
+    float2 a;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[t] = W2s[(16 * t + c16) * kUP + kq];
+    a = *reinterpret_cast<const float2*>(As + 2 * kq);
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) u[g] = Us[uoff[g]];
+#pragma unroll 2
+    for (int s4 = 0; s4 < kHidden / 4; ++s4) {
+      float h[GPW], bc[NT];
+#pragma unroll
+      for (int g = 0; g < GPW; ++g) h[g] = fmaxf(fmaf(a.y, ry[g], fmaf(a.x, rx[g], u[g])), 0.f);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bc[t] = b[t];
+      if (s4 + 1 < kHidden / 4) {  // prefetch the next k-step's operands
+        const int kn = 4 * (s4 + 1);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) b[t] = W2s[(16 * t + c16) * kUP + kn + kq];
+        a = *reinterpret_cast<const float2*>(As + 2 * (kn + kq));
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) u[g] = Us[uoff[g] + kn];
+      }
+#pragma unroll
+      for (int g = 0; g < GPW; ++g)
+        if (gv[g])
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(h[g], bc[t], acc[g][t], 0, 0, 0);
+    }
+
+    // epilogue: bias, ReLU, max over j (LDS atomic max on (bits << 32 | ~j))
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int grp = wave * GPW + g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = grp * 16 + kq * 4 + r;
+        if (p < npairs) {
+          const int il = p / n, j = p - il * n;
+          const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int cc = 16 * t + c16;
+            if (cc < BN) {
+              float v = acc[g][t][r] + b2[cc];
+              v = v > 0.f ? v : 0.f;
+              atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < rows * BN; q += 256) {
+      const unsigned long long key = keys[q];
+      const size_t oi = (size_t)(o + i0) * BN + q;
+      out[oi] = __uint_as_float((unsigned)(key >> 32));
+      argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+    }
+  }
+}
+
 // ---- backward ---------------------------------------------------------------
 // Only (i, argmax[i, c]) carries gradient.  Work unit = (scene, j range): the
 // scene's pooled-from peds j are cut into jq ranges so that S x jq units fill
@@ -327,9 +479,53 @@ static int pool_bwd_jq(int S) {
 }
 
 template <int BN>
+static size_t pool_res_lds(int max_n, int max_rows) {
+  return sizeof(float) * ((size_t)16 * PoolCfg<BN>::NT * kUP + 2 * kHidden + (size_t)max_n * kUP) +
+         sizeof(float2) * (size_t)max_n + sizeof(unsigned long long) * (size_t)max_rows * BN;
+}
+
+static int device_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int d = 0, v = 0;
+    if (hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess)
+      ncu = v > 0 ? v : 256;
+    else
+      ncu = 256;
+  }
+  return ncu;
+}
+
+template <int BN, int GPW>
+static void launch_fwd_res(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
+                           const int32_t* off, const int32_t* chunks, int nchunks, int max_n, size_t lds, float* out,
+                           int32_t* am, hipStream_t st) {
+  const int per_cu = (int)((160u * 1024u) / lds);
+  long long grid = (long long)device_cus() * (per_cu < 1 ? 1 : per_cu);
+  if (grid > nchunks) grid = nchunks;
+  hipLaunchKernelGGL((pool_fwd_res_kernel<BN, GPW>), dim3((unsigned)grid), dim3(256), lds, st, U, pos, A, W2, b2, off,
+                     reinterpret_cast<const int4*>(chunks), nchunks, max_n, out, am);
+}
+
+template <int BN>
 static int launch_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                      const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, int gpw, float* out,
-                      int32_t* am, hipStream_t st) {
+                      const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, int max_n, int gpw,
+                      float* out, int32_t* am, hipStream_t st) {
+  const size_t res = pool_res_lds<BN>(max_n, max_rows);
+  // measured (tools/bench_kernels.py, round 1): the resident form is slower
+  // than the tiled one at the training shapes (one workgroup of four waves
+  // per CU cannot hide its LDS latency; the tiled form runs two per CU), so
+  // it is opt-in (SGG_POOL_RESIDENT=1)
+  const char* rs = getenv("SGG_POOL_RESIDENT");
+  if (res <= 160u * 1024u && rs && rs[0] == '1') {
+    switch (gpw) {
+      case 1: launch_fwd_res<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
+      case 2: launch_fwd_res<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
+      case 4: launch_fwd_res<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
+      default: launch_fwd_res<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
+    }
+    SGG_RETURN_LAUNCH("sgg_pool_fwd");
+  }
   switch (gpw) {
     case 1: launch_fwd_g<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
     case 2: launch_fwd_g<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
@@ -391,7 +587,8 @@ extern "C" int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int t
   for (int s = 0; s < S; ++s) {
     const int n = host_scene_off[s + 1] - host_scene_off[s];
     if (n <= 0) continue;
-    const int rows = plan_rows(n, gpw);
+    // the fewest chunks of <= plan_rows rows each, rows spread evenly over them
+    const int rmax = plan_rows(n, gpw), nck = (n + rmax - 1) / rmax, rows = (n + nck - 1) / nck;
     for (int i0 = 0; i0 < n; i0 += rows) {
       const int i1 = i0 + rows < n ? i0 + rows : n;
       if (nc >= cap) {
@@ -424,11 +621,11 @@ extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, co
   if (nchunks == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (bn) {
-    case 8: return launch_fwd<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    case 16: return launch_fwd<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    case 32: return launch_fwd<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    case 48: return launch_fwd<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
-    default: return launch_fwd<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, out, argmax, st);
+    case 8: return launch_fwd<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
+    case 16: return launch_fwd<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
+    case 32: return launch_fwd<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
+    case 48: return launch_fwd<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
+    default: return launch_fwd<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
   }
 }
 

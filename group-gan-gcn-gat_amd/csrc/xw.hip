@@ -5,85 +5,149 @@
 //   B lane map: B[l >> 4][l & 15]    (4 k x 16 cols)
 //   C/D map   : row = (l >> 4) * 4 + r, col = l & 15   (r = 0..3)
 // Workgroup = 4 waves = 64 rows x 64 cols of Y; each wave owns 16 rows x 64
-// cols (4 accumulator tiles).  K is small on this path (2..144, 512 for the
-// pooling backward), so operands are read straight from L1/L2: the X row
-// fragment is reused across the 4 column tiles in registers, the W fragment
-// is shared by the 4 waves through L1.  These launches are latency-bound
-// (a few dozen workgroups), hence the deep register prefetch below.
+// cols (4 accumulator tiles).  K is small on most of this path (2..144), so
+// the X fragments are read straight from L1/L2 with a deep register prefetch
+// (these launches are latency-bound: a few dozen workgroups).  A weight in the
+// nn.Linear layout (N x K, TRANS_W) with K <= 256 is staged once per
+// workgroup in LDS -- its 64 rows read along k, coalesced -- instead of a
+// lane-per-column fragment read that touches one cache line per lane.
+// Large K (>= 256: the pooling backward dh = dU W1h, K = 512) takes the
+// split-K form: a workgroup = 16 rows x 64 cols whose 4 waves each walk a
+// quarter of K, the partial tiles summed through LDS in wave order.
 #include "sgg_common.h"
 
 namespace sgg {
 
-template <bool TRANS_W>
+constexpr int kXwKC = 32;            // K chunk: 8 MFMA k-steps, double-buffered in registers
+constexpr int kXwS4 = kXwKC / 4;
+constexpr int kXwStageMaxK = 256;    // TRANS_W weights staged in LDS up to this K
+
+// Operand fetch of one 16-row x 64-col wave tile over k in [kb, kend):
+// X rows from global, W from global (row-major K x N, or N x K if TRANS_W)
+// or from the LDS image `ws` (64 rows x K at pitch K + 1, TRANS_W staged).
+// Loads use clamped (in-bounds) addresses; only k >= kend must contribute
+// zero, which concerns the last chunk alone -- a wave-uniform branch (a
+// per-load `cond ? v : 0` makes the compiler sink each load into an
+// exec-masked branch that waits for it).
+template <bool TRANS_W, bool STAGED>
+struct XwFrag {
+  const float* xrow;
+  const float* mrow;
+  const float* W;
+  const float* ws;
+  int ldw, kp, kend;
+  int ncl[4];   // clamped global output columns (unstaged) / local rows of ws (staged)
+  int kq;
+
+  __device__ __forceinline__ float wval(int t, int k) const {
+    if (STAGED) return ws[ncl[t] * kp + k];
+    return TRANS_W ? W[(size_t)ncl[t] * ldw + k] : W[(size_t)k * ldw + ncl[t]];
+  }
+  __device__ __forceinline__ void load(int kb, float (&aa)[kXwS4], float (&bb)[kXwS4][4]) const {
+    if (kb + kXwKC <= kend) {
+#pragma unroll
+      for (int s = 0; s < kXwS4; ++s) {
+        const int k = kb + 4 * s + kq;
+        aa[s] = mrow ? keep_if(xrow[k], mrow[k] > 0.f) : xrow[k];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bb[s][t] = wval(t, k);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < kXwS4; ++s) {
+        const int k = kb + 4 * s + kq;
+        const int kc = min(k, kend - 1);
+        aa[s] = keep_if(xrow[kc], k < kend && (!mrow || mrow[kc] > 0.f));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bb[s][t] = wval(t, kc);
+      }
+    }
+  }
+};
+
+// acc[t] += X[rows, kb0..kend) W[kb0..kend), cols]: the next chunk's loads are
+// in flight while the current chunk runs through the MFMAs
+template <bool TRANS_W, bool STAGED>
+__device__ __forceinline__ void xw_walk(const XwFrag<TRANS_W, STAGED>& f, int kb0, floatx4 (&acc)[4]) {
+  if (kb0 >= f.kend) return;
+  float a0[kXwS4], b0[kXwS4][4], a1[kXwS4], b1[kXwS4][4];
+  f.load(kb0, a0, b0);
+  for (int k0 = kb0; k0 < f.kend; k0 += 2 * kXwKC) {
+    if (k0 + kXwKC < f.kend) f.load(k0 + kXwKC, a1, b1);
+#pragma unroll
+    for (int s = 0; s < kXwS4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b0[s][t], acc[t], 0, 0, 0);
+    if (k0 + kXwKC >= f.kend) break;
+    if (k0 + 2 * kXwKC < f.kend) f.load(k0 + 2 * kXwKC, a0, b0);
+#pragma unroll
+    for (int s = 0; s < kXwS4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], b1[s][t], acc[t], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ float xw_epi(float v, const float* bias, int n, int act) {
+  if (bias) v += bias[n];
+  if (act == 1) v = v > 0.f ? v : 0.f;
+  return v;
+}
+
+template <bool TRANS_W, bool STAGED>
 __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, int ldx,
                                                  const float* __restrict__ Xmask, int ldm,
                                                  const float* __restrict__ W, int ldw,
                                                  const float* __restrict__ bias, float* __restrict__ Y,
                                                  int ldy, int M, int K, int N, int act) {
+  extern __shared__ float wsm[];   // STAGED: this workgroup's 64 W rows x K at pitch K + 1
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int row0 = blockIdx.x * 64 + wave * 16;
   const int col0 = blockIdx.y * 64;
   const int ar = lane & 15;   // A row / B col within the 16x16 tile
   const int kq = lane >> 4;   // k within the 4-deep step
+  if (STAGED) {
+    // the 64 rows of the N x K weight this workgroup needs, read along k
+    // (4 loads per thread in flight before the LDS stores)
+    const int tot = 64 * K, kp = K + 1;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += 4 * 256) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = min(e0 + u * 256, tot - 1);
+        const int nl = e / K, k = e - nl * K;
+        v[u] = W[(size_t)min(col0 + nl, N - 1) * ldw + k];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * 256;
+        if (e < tot) {
+          const int nl = e / K, k = e - nl * K;
+          wsm[nl * kp + k] = v[u];
+        }
+      }
+    }
+    __syncthreads();
+  }
   const int arow = row0 + ar;
   const bool arow_ok = arow < M;
-  const float* xrow = X + (size_t)(arow_ok ? arow : 0) * ldx;
+  XwFrag<TRANS_W, STAGED> f;
+  f.xrow = X + (size_t)(arow_ok ? arow : 0) * ldx;
   // ReLU backward fused into the operand: X[m, k] counts where Xmask[m, k] > 0
-  const float* mrow = Xmask ? Xmask + (size_t)(arow_ok ? arow : 0) * ldm : nullptr;
+  f.mrow = Xmask ? Xmask + (size_t)(arow_ok ? arow : 0) * ldm : nullptr;
+  f.W = W;
+  f.ws = wsm;
+  f.ldw = ldw;
+  f.kp = K + 1;
+  f.kend = K;
+  f.kq = kq;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) f.ncl[t] = STAGED ? min(16 * t + ar, N - 1 - col0) : min(col0 + 16 * t + ar, N - 1);
 
   floatx4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // K is walked in 32-deep chunks (8 MFMA k-steps), double-buffered in
-  // registers: the next chunk's loads are all in flight while the current
-  // chunk computes, so a K <= 144 transform costs ~K/32 load latencies
-  // instead of one per 4-deep step.  Out-of-range k / n read as 0 (adds 0).
-  constexpr int KC = 32, S4 = KC / 4;
-  // Loads come from clamped (in-bounds) addresses: rows >= M and columns
-  // >= N compute values that the epilogue never stores, so they need no
-  // mask; only k >= K must contribute zero, which concerns the last chunk
-  // alone -- a wave-uniform branch.  (A per-load `cond ? v : 0` makes the
-  // compiler sink each load into an exec-masked branch that waits for it.)
-  int ncl[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) ncl[t] = min(col0 + 16 * t + ar, N - 1);
-  auto load_chunk = [&](int kb, float (&aa)[S4], float (&bb)[S4][4]) {
-    if (kb + KC <= K) {
-#pragma unroll
-      for (int s = 0; s < S4; ++s) {
-        const int k = kb + 4 * s + kq;
-        aa[s] = mrow ? keep_if(xrow[k], mrow[k] > 0.f) : xrow[k];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bb[s][t] = TRANS_W ? W[ncl[t] * ldw + k] : W[k * ldw + ncl[t]];
-      }
-    } else {
-#pragma unroll
-      for (int s = 0; s < S4; ++s) {
-        const int k = kb + 4 * s + kq;
-        const int kc = min(k, K - 1);
-        aa[s] = keep_if(xrow[kc], k < K && (!mrow || mrow[kc] > 0.f));
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bb[s][t] = TRANS_W ? W[ncl[t] * ldw + kc] : W[kc * ldw + ncl[t]];
-      }
-    }
-  };
-  float a0[S4], b0[S4][4], a1[S4], b1[S4][4];
-  load_chunk(0, a0, b0);
-  for (int k0 = 0; k0 < K; k0 += 2 * KC) {
-    if (k0 + KC < K) load_chunk(k0 + KC, a1, b1);
-#pragma unroll
-    for (int s = 0; s < S4; ++s)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b0[s][t], acc[t], 0, 0, 0);
-    if (k0 + KC >= K) break;
-    if (k0 + 2 * KC < K) load_chunk(k0 + 2 * KC, a0, b0);
-#pragma unroll
-    for (int s = 0; s < S4; ++s)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], b1[s][t], acc[t], 0, 0, 0);
-  }
+  xw_walk(f, 0, acc);
 
   // epilogue (direct stores: an LDS-staged full-row variant measured slower,
   // 67 vs 42 us on the 25600 x 512 pooling U -- L2 merges the 64-B pieces)
@@ -91,16 +155,55 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   for (int t = 0; t < 4; ++t) {
     const int n = col0 + 16 * t + ar;
     if (n >= N) continue;
-    const float bv = bias ? bias[n] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = row0 + kq * 4 + r;
-      if (m < M) {
-        float v = acc[t][r] + bv;
-        if (act == 1) v = v > 0.f ? v : 0.f;
-        Y[(size_t)m * ldy + n] = v;
-      }
+      if (m < M) Y[(size_t)m * ldy + n] = xw_epi(acc[t][r], bias, n, act);
     }
+  }
+}
+
+template <bool TRANS_W>
+__global__ void __launch_bounds__(256) xw_splitk_kernel(const float* __restrict__ X, int ldx,
+                                                        const float* __restrict__ Xmask, int ldm,
+                                                        const float* __restrict__ W, int ldw,
+                                                        const float* __restrict__ bias, float* __restrict__ Y,
+                                                        int ldy, int M, int K, int N, int act) {
+  __shared__ float part[4][16][65];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * 16;
+  const int col0 = blockIdx.y * 64;
+  const int ar = lane & 15, kq = lane >> 4;
+  const int arow = row0 + ar;
+  const bool arow_ok = arow < M;
+  const int span = (((K + 3) / 4) + kXwKC - 1) / kXwKC * kXwKC;   // this wave's K range
+  XwFrag<TRANS_W, false> f;
+  f.xrow = X + (size_t)(arow_ok ? arow : 0) * ldx;
+  f.mrow = Xmask ? Xmask + (size_t)(arow_ok ? arow : 0) * ldm : nullptr;
+  f.W = W;
+  f.ws = nullptr;
+  f.ldw = ldw;
+  f.kp = 0;
+  f.kend = min(K, (wave + 1) * span);
+  f.kq = kq;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) f.ncl[t] = min(col0 + 16 * t + ar, N - 1);
+  floatx4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  xw_walk(f, wave * span, acc);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[wave][kq * 4 + r][16 * t + ar] = acc[t][r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 16 * 64; e += 256) {
+    const int rr = e >> 6, cc = e & 63;
+    const int m = row0 + rr, n = col0 + cc;
+    if (m < M && n < N)
+      Y[(size_t)m * ldy + n] =
+          xw_epi(((part[0][rr][cc] + part[1][rr][cc]) + part[2][rr][cc]) + part[3][rr][cc], bias, n, act);
   }
 }
 
@@ -115,11 +218,26 @@ extern "C" int sgg_xw(const float* X, int ldx, const float* Xmask, int ldm, cons
   SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw: act must be 0 or 1");
   SGG_CHECK_ARG(!Xmask || ldm >= K, "sgg_xw: mask leading dim %d < K", ldm);
   if (M == 0) return 0;
-  dim3 grid((M + 63) / 64, (N + 63) / 64);
   hipStream_t s = (hipStream_t)stream;
-  if (trans_w)
-    hipLaunchKernelGGL(sgg::xw_kernel<true>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy, M, K, N, act);
+  if (K >= 256) {
+    dim3 grid((M + 15) / 16, (N + 63) / 64);
+    if (trans_w)
+      hipLaunchKernelGGL(sgg::xw_splitk_kernel<true>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy,
+                         M, K, N, act);
+    else
+      hipLaunchKernelGGL(sgg::xw_splitk_kernel<false>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy,
+                         M, K, N, act);
+    SGG_RETURN_LAUNCH("sgg_xw");
+  }
+  dim3 grid((M + 63) / 64, (N + 63) / 64);
+  if (trans_w && K <= sgg::kXwStageMaxK)
+    hipLaunchKernelGGL((sgg::xw_kernel<true, true>), grid, dim3(256), sizeof(float) * 64 * (K + 1), s, X, ldx, Xmask,
+                       ldm, W, ldw, bias, Y, ldy, M, K, N, act);
+  else if (trans_w)
+    hipLaunchKernelGGL((sgg::xw_kernel<true, false>), grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy,
+                       M, K, N, act);
   else
-    hipLaunchKernelGGL(sgg::xw_kernel<false>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy, M, K, N, act);
+    hipLaunchKernelGGL((sgg::xw_kernel<false, false>), grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y,
+                       ldy, M, K, N, act);
   SGG_RETURN_LAUNCH("sgg_xw");
 }

@@ -356,6 +356,48 @@ def test_fused_lstm_multiwave_all_sizes(H, T, decoder, B, monkeypatch):
     test_fused_lstm_vs_oracle(H, T, decoder, B)
 
 
+@pytest.mark.parametrize("bn", [8, 48])
+def test_pool_resident_equals_tiled(bn, monkeypatch):
+    """sgg_pool_fwd's resident form (W2^T and the scene's U rows in LDS, used
+    when they fit) against the k-tiled form on the same chunk table: the
+    same MFMA sequence, so outputs and argmax are bitwise equal."""
+    from sgan import _native as N
+    from sgan import kernels as K
+    from sgan.scene import SceneIndex
+    torch.manual_seed(bn)
+    sizes = [20, 1, 7, 13, 20, 2, 17] * 3
+    B = sum(sizes)
+    sc = SceneIndex(np.concatenate([[0], np.cumsum(sizes)]), DEV)
+    U = torch.randn(B, 512, device=DEV) * 0.3
+    pos = torch.rand(B, 2, device=DEV) * 15
+    A = torch.randn(512, 2, device=DEV) * 0.3
+    W2 = torch.randn(bn, 512, device=DEV) * 0.05
+    b2 = torch.randn(bn, device=DEV) * 0.1
+    lib = N.load()
+    chunks, nchunks, max_rows, gpw = sc.pool_plan(bn)
+    res = []
+    for tiled in (False, True):
+        if tiled:
+            monkeypatch.delenv("SGG_POOL_RESIDENT")
+        else:
+            monkeypatch.setenv("SGG_POOL_RESIDENT", "1")
+        out = torch.empty(B, bn, device=DEV)
+        am = torch.empty(B, bn, device=DEV, dtype=torch.int32)
+        N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(sc.scene_off),
+                                 N.ptr(chunks), nchunks, max_rows, gpw, B, bn, sc.max_n, N.ptr(out), N.ptr(am),
+                                 N.stream_ptr()), "pool")
+        res.append((out.cpu(), am.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    # and against a torch restatement of the pair MLP
+    ref = torch.empty(B, bn)
+    Uc, pc, Ac, Wc, bc = U.cpu(), pos.cpu(), A.cpu(), W2.cpu(), b2.cpu()
+    for s0, s1 in zip(sc.host_off[:-1], sc.host_off[1:]):
+        r = pc[s0:s1].unsqueeze(0) - pc[s0:s1].unsqueeze(1)          # [i, j] = p_j - p_i
+        hid = torch.relu(Uc[s0:s1].unsqueeze(0) + r @ Ac.t())          # (i, j, 512)
+        ref[s0:s1] = torch.relu(hid @ Wc.t() + bc).max(1)[0]
+    close(res[0][0], ref.numpy(), rtol=1e-5, what="pool resident")
+
+
 def test_xtw_matches_torch():
     from sgan import kernels as K
     torch.manual_seed(1)
