@@ -78,6 +78,21 @@ def pool_flops(sc, bn):
     return float((sizes.astype(np.float64) ** 2).sum()) * 512.0 * (4 + 2 * bn)
 
 
+def pmc_traffic(kname, key):
+    """HBM bytes per launch of the roofline kernel from the committed PMC
+    passes (profiles/r01_pool_traffic.json, written by tools/pmc_traffic.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench, with the
+    gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or None when that
+    file holds no entry for this exact launch shape."""
+    path = os.path.join(ROOT, "profiles", "r01_pool_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        tab = json.load(f)
+    ent = tab.get("%s|%s" % (kname, list(key)))
+    return None if ent is None else ent["hbm_bytes"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,32 +161,33 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
-    # roofline of the pooling kernel: HIP events around every sgg_pool_fwd
-    # launch of instrumented iterations on the same inputs (the graph replays
-    # carry no events); rocprofv3's kernel trace of the same command is the
-    # cross-check (profiles/)
+    # roofline of the pooling kernel: every sgg_pool_fwd launch of a few
+    # instrumented iterations on the same inputs is recorded (graph replays
+    # carry no events), then each distinct launch is re-issued back to back
+    # between HIP events on its launch stream (device-busy average duration);
+    # rocprofv3's kernel trace of the same command is the cross-check (profiles/)
+    n_it = max(1, min(args.steps, 3))
     K.pool_timer.start()
-    for _ in range(max(1, min(args.steps, 3))):
+    for _ in range(n_it):
         trainer.step(batch, sc, batch_g, sc_g, **kw)
-    launches = K.pool_timer.stop()
+    timed = K.pool_timer.replay(K.pool_timer.stop())
 
     if rank == 0:
-        # dominant kernel: the pooling forward variant with the most device time
-        by_bn = {}
-        for bn, flops, ms in launches:
-            a = by_bn.setdefault(bn, [0, 0.0, 0.0])
-            a[0] += 1
-            a[1] += flops
-            a[2] += ms
-        bn_dom = max(by_bn, key=lambda b: by_bn[b][2])
-        n, fl, ms = by_bn[bn_dom]
-        achieved = (fl / n) / (ms / n * 1e-3) / 1e12
+        # dominant kernel: the pool forward launch with the most device time per iteration
+        key = max(timed, key=lambda k: timed[k][0] * timed[k][2])
+        n, fl, ms = timed[key]
+        bn, gpw = key[0], key[1]
+        kname = "sgg::pool_fwd_kernel<%d, %d>" % (bn, gpw)
+        achieved = fl / (ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                    "kernel": "sgg::pool_fwd_kernel<%d>" % bn_dom, "launches": n,
-                    "avg_launch_us": round(ms / n * 1e3, 2),
-                    "note": "fp32 (VALU FMA, same peak as f32 MFMA); all pool variants: %s" % {
-                        "bn%d" % b: {"launches": v[0], "ms": round(v[2], 3)} for b, v in by_bn.items()}}
+                    "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": pmc_traffic(kname, key),
+                    "kernel": kname, "launches_per_iteration": round(n / n_it, 2),
+                    "avg_launch_us": round(ms * 1e3, 2), "flop_per_launch": fl,
+                    "note": "fp32 (f32 MFMA, same peak as VALU FMA); all pool forward launches per iteration "
+                            "[bn, gpw, scenes, peds]: %s" % {
+                                "%s" % list(k): {"per_iter": round(v[0] / n_it, 2), "avg_us": round(v[2] * 1e3, 2),
+                                                 "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 2)}
+                                for k, v in timed.items()}}
         ms_step = elapsed / args.steps * 1e3
         value = world * args.batch / (elapsed / args.steps)
         cpu = None

@@ -67,7 +67,13 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
 
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  // XCD-aware chunk order: the grid is a multiple of 8 and blocks b, b + 8,
+  // b + 16, ... share an XCD (round-robin dispatch; speed only, never
+  // correctness), so they take CONSECUTIVE chunks -- the chunks of one scene,
+  // which all stage the same U rows, then hit one XCD's L2 instead of
+  // fetching those rows once per XCD.
+  const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  for (int ch = xb; ch < nchunks; ch += gridDim.x) {
     const int4 cd = chunks[ch];
     const int s = cd.x, i0 = cd.y, i1 = cd.z;
     const int o = scene_off[s];
@@ -467,7 +473,7 @@ template <int BN, int GPW>
 static void launch_fwd_g(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
                          const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, float* out,
                          int32_t* am, hipStream_t st) {
-  const int grid = nchunks < 65536 ? nchunks : 65536;
+  const int grid = nchunks < 65536 ? (nchunks + 7) & ~7 : 65536;   // multiple of 8 (XCD-aware order)
   hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW>), dim3(grid), dim3(256), pool_fwd_lds<BN>(max_rows), st, U, pos, A,
                      W2, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, out, am);
 }
