@@ -14,44 +14,50 @@
 
 namespace sgg {
 
+// One workgroup = one 64 x 64 output tile of one split.  The four waves split
+// the ROWS (wave w takes rows r0 + 16 w + 64 i), each wave accumulating the
+// whole tile: per 4-row step a lane loads MT A values (one per 16-wide m-tile)
+// and 4 B values and issues MT x 4 MFMAs, so every loaded Y element feeds MT
+// MFMAs (the column tiles of M no longer each re-load the Y rows).  MT =
+// ceil(min(M, 64) / 16): a narrow X (M = 16 / 32 / 48) skips the m-tiles it
+// does not have instead of running idle waves.  The four partial tiles are
+// summed in LDS in wave order (deterministic) and stored coalesced.
+template <int MT>
 __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restrict__ X, int ldx,
                                                           const float* __restrict__ Y, int ldy,
                                                           const float* __restrict__ Ym, int ldm, int R, int M,
                                                           int N, int rows_per_split, float* __restrict__ slab,
                                                           float* __restrict__ colslab) {
+  __shared__ float red[64 * 65 + 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c16 = lane & 15, kq = lane >> 4;
-  const int m0 = blockIdx.x * 64 + wave * 16;
+  const int m0 = blockIdx.x * 64;
   const int n0 = blockIdx.y * 64;
   const int split = blockIdx.z;
   const int r0 = split * rows_per_split;
   const int r1 = min(R, r0 + rows_per_split);
-  const int m = m0 + c16;
-  const bool mok = m < M;
-  bool nok[4];
+  const bool do_col = colslab && blockIdx.x == 0;
+  // clamped columns: values of columns >= M / >= N are never stored; only rows
+  // >= r1 must contribute zero (the last 16-row step of a wave alone)
+  int mcl[MT], ncl[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) nok[t] = n0 + 16 * t + c16 < N;
-  const bool do_col = colslab && blockIdx.x == 0 && wave == 0;
-  floatx4 acc[4];
+  for (int u = 0; u < MT; ++u) mcl[u] = min(m0 + 16 * u + c16, M - 1);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ncl[t] = min(n0 + 16 * t + c16, N - 1);
+  floatx4 acc[MT][4];
   float col[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // software pipeline: the next 16 rows' loads are in flight while the current
-  // 16 rows run through the MFMAs
-  float a[4], b[4][4], an[4], bnx[4][4];
-  // Loads come from clamped addresses: columns >= M / >= N produce values
-  // that are never stored; only rows >= r1 must contribute zero, which
-  // concerns the last 16-row step alone -- a wave-uniform branch.
-  const int mcl = mok ? m : M - 1;
-  int ncl[4];
+  for (int u = 0; u < MT; ++u)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) ncl[t] = nok[t] ? n0 + 16 * t + c16 : N - 1;
-  auto load16 = [&](int r, float (&aa)[4], float (&bb)[4][4]) {
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float a[4][MT], b[4][4], an[4][MT], bnx[4][4];
+  auto load16 = [&](int r, float (&aa)[4][MT], float (&bb)[4][4]) {
     if (r + 16 <= r1) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const size_t row = (size_t)(r + 4 * s + kq);
-        aa[s] = X[row * ldx + mcl];
+#pragma unroll
+        for (int u = 0; u < MT; ++u) aa[s][u] = X[row * ldx + mcl[u]];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           bb[s][t] = Ym ? keep_if(Y[row * ldy + ncl[t]], Ym[row * ldm + ncl[t]] > 0.f) : Y[row * ldy + ncl[t]];
@@ -61,54 +67,70 @@ __global__ void __launch_bounds__(256) xtw_partial_kernel(const float* __restric
       for (int s = 0; s < 4; ++s) {
         const int row = r + 4 * s + kq;
         const size_t rc = (size_t)min(row, r1 - 1);
-        aa[s] = keep_if(X[rc * ldx + mcl], row < r1);
+#pragma unroll
+        for (int u = 0; u < MT; ++u) aa[s][u] = keep_if(X[rc * ldx + mcl[u]], row < r1);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           bb[s][t] = keep_if(Y[rc * ldy + ncl[t]], row < r1 && (!Ym || Ym[rc * ldm + ncl[t]] > 0.f));
       }
     }
   };
-  if (r0 < r1) load16(r0, a, b);
-  for (int r = r0; r < r1; r += 16) {
-    const bool more = r + 16 < r1;
-    if (more) load16(r + 16, an, bnx);
+  const int rw = r0 + 16 * wave;
+  if (rw < r1) load16(rw, a, b);
+  for (int r = rw; r < r1; r += 64) {
+    const bool more = r + 64 < r1;
+    if (more) load16(r + 64, an, bnx);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < MT; ++u) acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][u], b[s][t], acc[u][t], 0, 0, 0);
         if (do_col) col[t] += b[s][t];
       }
     if (more) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        a[s] = an[s];
+#pragma unroll
+        for (int u = 0; u < MT; ++u) a[s][u] = an[s][u];
 #pragma unroll
         for (int t = 0; t < 4; ++t) b[s][t] = bnx[s][t];
       }
     }
   }
-  float* out = slab + (size_t)split * M * N;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int n = n0 + 16 * t + c16;
-    if (n >= N) continue;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int mm = m0 + kq * 4 + rr;
-      if (mm < M) out[(size_t)mm * N + n] = acc[t][rr];
-    }
-  }
   if (do_col) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {  // sum the 4 row phases (lanes c16, c16+16, +32, +48)
-      float v = col[t];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      const int n = n0 + 16 * t + c16;
-      if (kq == 0 && n < N) colslab[(size_t)split * N + n] = v;
+      col[t] += __shfl_xor(col[t], 16);
+      col[t] += __shfl_xor(col[t], 32);
     }
   }
+  // wave-ordered sum of the four partial tiles in LDS (row stride 65)
+  float* cred = red + 64 * 65;
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int u = 0; u < MT; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            float* d = red + (16 * u + 4 * kq + rr) * 65 + 16 * t + c16;
+            *d = w == 0 ? acc[u][t][rr] : *d + acc[u][t][rr];
+          }
+      if (do_col && kq == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cred[16 * t + c16] = w == 0 ? col[t] : cred[16 * t + c16] + col[t];
+      }
+    }
+    __syncthreads();
+  }
+  float* out = slab + (size_t)split * M * N;
+  for (int e = threadIdx.x; e < 16 * MT * 64; e += 256) {
+    const int mm = e >> 6, nn = e & 63;
+    if (m0 + mm < M && n0 + nn < N) out[(size_t)(m0 + mm) * N + n0 + nn] = red[mm * 65 + nn];
+  }
+  if (do_col && threadIdx.x < 64 && n0 + (int)threadIdx.x < N) colslab[(size_t)split * N + n0 + threadIdx.x] = cred[threadIdx.x];
 }
 
 // slab sums: block = 64 outputs x 16 split phases (1024 threads), fixed
@@ -161,14 +183,14 @@ __global__ void __launch_bounds__(1024) xtw_reduce_kernel(const float* __restric
 using namespace sgg;
 
 extern "C" int sgg_xtw_splits(int R, int M, int N) {
-  // >= ~32 rows per split (two 16-row MFMA steps), capped by the grid
+  // >= 64 rows per split (one 16-row MFMA step per wave), capped by the grid
   // (<= 1024 workgroups: thousands of one-step workgroups cost more in
   // dispatch than they compute), by the slab (<= 2^21 floats, so the reduce
   // stays an L2-resident pass) and at 256 partials per output (the reduce's
   // phases walk <= 16 each)
   const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
   const long long mn = (long long)M * N;
-  long long splits = (R + 31) / 32;
+  long long splits = (R + 63) / 64;
   const long long by_grid = 1024 / tiles > 0 ? 1024 / tiles : 1;
   const long long by_slab = (1ll << 21) / mn > 0 ? (1ll << 21) / mn : 1;
   if (splits > by_grid) splits = by_grid;
@@ -188,11 +210,16 @@ extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const f
   SGG_CHECK_ARG(ws_bytes >= need, "sgg_xtw: workspace %zu < %zu bytes", ws_bytes, need);
   SGG_CHECK_ARG(!Ymask || ldm >= N, "sgg_xtw: mask leading dim %d < N", ldm);
   hipStream_t st = (hipStream_t)stream;
-  const int rps = ((R + splits - 1) / splits + 15) & ~15;
+  const int rps = ((R + splits - 1) / splits + 63) & ~63;   // whole 64-row steps (16 rows per wave)
   float* colslab = ws + (size_t)splits * M * N;
   dim3 grid((M + 63) / 64, (N + 63) / 64, splits);
-  hipLaunchKernelGGL(xtw_partial_kernel, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws,
-                     colsum ? colslab : nullptr);
+  float* cs = colsum ? colslab : nullptr;
+  switch (M >= 64 ? 4 : (M + 15) / 16) {   // 16-wide m-tiles of a 64-row output block
+    case 1: hipLaunchKernelGGL(xtw_partial_kernel<1>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+    case 2: hipLaunchKernelGGL(xtw_partial_kernel<2>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+    case 3: hipLaunchKernelGGL(xtw_partial_kernel<3>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+    default: hipLaunchKernelGGL(xtw_partial_kernel<4>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+  }
   const int MN = M * N;
   const int nb = (MN + 63) / 64 + (colsum ? (N + 63) / 64 : 0);
   hipLaunchKernelGGL(xtw_reduce_kernel, dim3(nb), dim3(1024), 0, st, ws, splits, MN, C, N, ldc, trans_c,

@@ -401,7 +401,8 @@ def test_pool_resident_equals_tiled(bn, monkeypatch):
 def test_xtw_matches_torch():
     from sgan import kernels as K
     torch.manual_seed(1)
-    for (R, M, Nn) in [(0, 3, 4), (5, 3, 7), (1000, 32, 128), (51200, 48, 192), (25600, 32, 512), (300, 144, 2)]:
+    for (R, M, Nn) in [(0, 3, 4), (5, 3, 7), (1000, 32, 128), (51200, 48, 192), (25600, 32, 512), (300, 144, 2),
+                       (777, 16, 128), (4099, 72, 40), (63, 64, 65)]:
         X = torch.randn(R, M, device=DEV)
         Y = torch.randn(R, Nn, device=DEV)
         C, cs = K.xtw(X, Y, colsum=True)
@@ -414,6 +415,11 @@ def test_xtw_matches_torch():
         K.xtw(X, Y, trans_c=True, out=big[:, 3:3 + M])
         close(big[:, 3:3 + M], ref.t().cpu(), rtol=5e-6, floor=1.0, what="xtw^T in place")
         assert float(big[:, :3].sub(7).abs().max()) == 0 and float(big[:, 3 + M:].sub(7).abs().max()) == 0
+        if R:                                                        # fused ReLU-backward mask on Y
+            Ym = torch.randn(R, Nn, device=DEV)
+            Cm = K.xtw(X, Y, mask=Ym)
+            refm = (X.double().t() @ (Y * (Ym > 0)).double()).float()
+            close(Cm, refm.cpu(), rtol=5e-6, floor=1.0, what="masked xtw %s" % ((R, M, Nn),))
 
 
 def test_xw_strided_weight_block():

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v -k "${1:-.}" -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/i_tests.log 2>&1 || { echo TESTS_FAIL; tail -40 gpurun_out/i_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v ${1:+-k "$1"} -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/i_tests.log 2>&1 || { echo TESTS_FAIL; tail -40 gpurun_out/i_tests.log; exit 1; }
 tail -2 gpurun_out/i_tests.log
 timeout -k 10 400 python bench.py --steps 100 --warmup 10 --no-cpu-baseline > gpurun_out/i_bench.json 2> gpurun_out/i_bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/i_bench.err; exit 1; }
 cat gpurun_out/i_bench.json
