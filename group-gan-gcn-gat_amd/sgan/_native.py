@@ -54,6 +54,9 @@ SIGNATURES = {
     "sgg_seg_reduce": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i, _p]),
     "sgg_seg_gather": (_i, [_p, _i, _i, _p, _p, _p, _i, _p, _i, _p]),
     "sgg_xtw_splits": (_i, [_i, _i, _i]),
+    "sgg_adam_parts": (_i, [ctypes.c_longlong]),
+    "sgg_adam_step": (_i, [_p, _p, _p, _p, _p, _i, ctypes.c_double, ctypes.c_double, ctypes.c_double, _f, _f, _p, _p,
+                          _sz, _p]),
     "sgg_xtw": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _sz, _p]),
     "sgg_fold_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "sgg_fold_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),

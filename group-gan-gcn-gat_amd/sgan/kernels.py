@@ -155,6 +155,78 @@ def linear(x, lin, act=0):
 
 
 # ---------------------------------------------------------------------------
+# optimizer step
+# ---------------------------------------------------------------------------
+class ClipAdam:
+    """[nn.utils.clip_grad_norm_(params, max_norm)] + optim.Adam.step() in two
+    launches (sgg_adam_step; scripts/train.py:418-427, :472-482).
+
+    The state lives in a torch.optim.Adam (capturable layout: per-parameter
+    float32 device 'step', 'exp_avg', 'exp_avg_sq'), created eagerly, so
+    `state_dict()` / `load_state_dict()` are torch's.  Parameters whose grad
+    is None are skipped, exactly as torch's Adam skips them (their step does
+    not advance).  Graph-capturable: the tensor list is passed by value."""
+
+    MAX_TENSORS = 48
+
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.params = [p for p in params]
+        self.opt = torch.optim.Adam(self.params, lr=lr, betas=betas, eps=eps, capturable=True)
+        for p in self.params:
+            st = self.opt.state[p]
+            st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        self._ws = None
+
+    @property
+    def param_groups(self):
+        return self.opt.param_groups
+
+    def state_dict(self):
+        return self.opt.state_dict()
+
+    def load_state_dict(self, sd):
+        self.opt.load_state_dict(sd)
+
+    def zero_grad(self, set_to_none=True):
+        self.opt.zero_grad(set_to_none=set_to_none)
+
+    def step(self, max_norm=0.0):
+        lib = _lib()
+        grp = self.opt.param_groups[0]
+        act = [p for p in self.params if p.grad is not None]
+        if max_norm > 0:            # the norm spans every tensor: one call
+            self._launch(lib, act, grp, max_norm)
+            return
+        for i in range(0, len(act), self.MAX_TENSORS):
+            self._launch(lib, act[i:i + self.MAX_TENSORS], grp, 0.0)
+
+    def _launch(self, lib, act, grp, max_norm):
+        import ctypes
+        if len(act) > self.MAX_TENSORS:
+            raise N.NativeError("ClipAdam: %d tensors with gradients, the fused step takes <= %d (clipping needs "
+                              "them in one call)" % (len(act), self.MAX_TENSORS))
+        for p in act:
+            for t in (p, p.grad):
+                if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+                    raise N.NativeError("ClipAdam: parameters and grads must be contiguous fp32 device tensors")
+        n = len(act)
+        st = [self.opt.state[p] for p in act]
+        arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])
+        numel = (ctypes.c_longlong * n)(*[p.numel() for p in act])
+        total = sum(p.numel() for p in act)
+        parts = lib.sgg_adam_parts(total)
+        if self._ws is None or self._ws.numel() < parts:
+            self._ws = torch.empty(parts, device=act[0].device, dtype=torch.float32)
+        b1, b2 = grp["betas"]
+        N.check(lib.sgg_adam_step(arr(act), arr([p.grad for p in act]), arr([s["exp_avg"] for s in st]),
+                                  arr([s["exp_avg_sq"] for s in st]), numel, n, float(grp["lr"]), float(b1),
+                                  float(b2), float(grp["eps"]), float(max_norm), arr([s["step"] for s in st]),
+                                  N.ptr(self._ws), self._ws.numel() * 4, N.stream_ptr()), "sgg_adam_step")
+
+
+# ---------------------------------------------------------------------------
 # social pooling
 # ---------------------------------------------------------------------------
 class _PoolTimer:

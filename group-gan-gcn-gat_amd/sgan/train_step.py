@@ -115,26 +115,30 @@ class KernelOps:
     bce_pair = staticmethod(K.bce_pair)
     split2 = staticmethod(K.split2)
     one = staticmethod(lambda device: K.const(1.0, device))
+    # clip_grad_norm_ + Adam in two launches (sgg_adam_step; torch's state
+    # layout, capturable): optimizer(params, lr).step(max_norm)
+    optimizer = staticmethod(lambda params, lr: K.ClipAdam(params, lr=lr))
 
 
 class GanTrainer:
     def __init__(self, G, D, args=None, dp=None, selective_backward=True, capturable=False, bce_pair=None, ops=None):
-        """ops: KernelOps-like (traj_cat, l2_select, l2_loss, bce_pair);
-        bce_pair(scores, split, y_a, y_b, w) overrides ops.bce_pair."""
+        """ops: KernelOps-like (traj_cat, l2_select, l2_loss, bce_pair,
+        optimizer); bce_pair(scores, split, y_a, y_b, w) overrides
+        ops.bce_pair.  `capturable` is kept for API compatibility: the
+        optimizer step is always graph-capturable."""
         self.G, self.D = G, D
         self.ops = ops or KernelOps()
         self.bce_pair = bce_pair or self.ops.bce_pair
         self.args = args or TrainArgs()
         self.dp = dp or DataParallel()
         self.selective_backward = selective_backward
-        # fused multi-tensor Adam: 2 launches per step instead of ~10 per tensor
-        self.opt_g = torch.optim.Adam(G.parameters(), lr=self.args.g_learning_rate, capturable=capturable,
-                                      fused=True)
-        self.opt_d = torch.optim.Adam(D.parameters(), lr=self.args.d_learning_rate, capturable=capturable,
-                                      fused=True)
         skip = "gcn_module." if getattr(G, "graph", "gat") == "gat" else "gatencoder."
         self.g_params = [p for n, p in G.named_parameters() if not n.startswith(skip)]
         self.d_params = list(D.parameters())
+        # the unused graph module gets no gradient, so Adam would skip it anyway
+        # (train.py builds Adam over G.parameters())
+        self.opt_g = self.ops.optimizer(self.g_params, self.args.g_learning_rate)
+        self.opt_d = self.ops.optimizer(self.d_params, self.args.d_learning_rate)
 
     # -- helpers -----------------------------------------------------------
     def _noise(self, S_global, s0, s1):
@@ -151,9 +155,7 @@ class GanTrainer:
         grads = [p.grad for p in params if p.grad is not None]
         vals = torch.stack([t.detach().reshape(()) for t in loss_terms])
         self.dp.allreduce_(grads + [vals])
-        if clip > 0:
-            torch.nn.utils.clip_grad_norm_(params, clip)
-        opt.step()
+        opt.step(max_norm=clip)    # clip_grad_norm_(params, clip) when clip > 0, then Adam
         return vals
 
     # -- steps ---------------------------------------------------------------

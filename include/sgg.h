@@ -266,6 +266,21 @@ int sgg_bce_bwd(const float* x, int n, int split, const float* ya, const float* 
                 const float* gout, float* dx, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Optimizer step of the training loop (scripts/train.py:418-427 and :472-482:
+ * optional nn.utils.clip_grad_norm_(params, max_norm), then optim.Adam.step()
+ * without weight decay / amsgrad).  params[i], grads[i], exp_avg[i],
+ * exp_avg_sq[i] are device fp32 buffers of numel[i] elements and step[i] the
+ * tensor's device fp32 step counter (torch's capturable Adam state['step']),
+ * incremented first (host arrays of n <= 48 pointers).  max_norm <= 0: no clipping; otherwise the
+ * clipped gradient is written back, as clip_grad_norm_ does.  ws holds
+ * sgg_adam_parts(sum numel) floats (partial norms + per-tensor step scalars).
+ * Two launches, graph-capturable. */
+int sgg_adam_parts(long long total);
+int sgg_adam_step(float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                  const long long* numel, int n, double lr, double beta1, double beta2, float eps, float max_norm,
+                  float* const* step, float* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * The group GAT encoder of every scene in ONE launch (GATEncoder.forward,
  * models.py:254-294, with GAT.forward :231-237 and GraphAttentionLayer
  * :198-220): per scene (workgroup) the group mask of the last-observed labels

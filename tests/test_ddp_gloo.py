@@ -80,8 +80,25 @@ def _bce_pair(scores, split, y_a, y_b, w=1.0):
     return w * sum(terms)
 
 
+class _TorchClipAdam:
+    """Torch restatement of kernels.ClipAdam (adam.hip)."""
+
+    def __init__(self, params, lr):
+        self.params = list(params)
+        self.opt = torch.optim.Adam(self.params, lr=lr)
+
+    def zero_grad(self, set_to_none=True):
+        self.opt.zero_grad(set_to_none=set_to_none)
+
+    def step(self, max_norm=0.0):
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(self.params, max_norm)
+        self.opt.step()
+
+
 class _TorchOps:
-    """Torch restatement of train_step.KernelOps (glue.hip / loss.hip)."""
+    """Torch restatement of train_step.KernelOps (glue.hip / loss.hip / adam.hip)."""
+    optimizer = staticmethod(_TorchClipAdam)
 
     @staticmethod
     def traj_cat(head, a, b=None):

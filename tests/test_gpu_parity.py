@@ -575,3 +575,35 @@ def test_step_glue_kernels_match_torch():
     pk = p[:, :B].clone().requires_grad_(True)
     K.l2_loss(pk, gt, mask, sc, 1.0).backward()
     close(pk.grad, pv.grad.cpu().numpy(), rtol=1e-5, what="l2 loss grad")
+
+
+@pytest.mark.parametrize("max_norm", [0.0, 2.0, 1e6])
+def test_clip_adam_matches_torch(max_norm):
+    """sgg_adam_step (ClipAdam) against nn.utils.clip_grad_norm_ + optim.Adam
+    (scripts/train.py:418-427, :472-482) over 3 steps, one parameter without a
+    gradient in the second step (skipped by both, its step does not advance)."""
+    from sgan.kernels import ClipAdam
+    torch.manual_seed(7)
+    shapes = [(512, 48), (512,), (48, 512), (48,), (7,), (192, 48), (3, 5, 2)]
+    ref = [torch.randn(s, device=DEV) for s in shapes]
+    ours = [r.clone() for r in ref]
+    o_ref = torch.optim.Adam(ref, lr=1e-3)
+    o_our = ClipAdam(ours, lr=1e-3)
+    for it in range(3):
+        for i, (a, b) in enumerate(zip(ref, ours)):
+            if it == 1 and i == 4:
+                a.grad = b.grad = None
+                continue
+            g = torch.randn_like(a) * (0.5 + i)
+            a.grad, b.grad = g.clone(), g.clone()
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(ref, max_norm)
+        o_ref.step()
+        o_our.step(max_norm=max_norm)
+        for i, (a, b) in enumerate(zip(ref, ours)):
+            close(b.detach(), a.detach().cpu(), rtol=2e-6, floor=1e-6, what="param %d it %d" % (i, it))
+            if a.grad is not None:
+                close(b.grad, a.grad.cpu(), rtol=2e-6, floor=1e-6, what="clipped grad %d it %d" % (i, it))
+            sa, sb = o_ref.state[a], o_our.opt.state[b]
+            assert float(sa["step"]) == float(sb["step"]), (i, it)
+            close(sb["exp_avg_sq"], sa["exp_avg_sq"].cpu(), rtol=2e-6, floor=1e-9, what="v %d it %d" % (i, it))
