@@ -310,15 +310,20 @@ class GraphedTrainer:
         G = trainer.G
         nd = tuple(G.noise_dim) if G.noise_dim else None
         k = trainer.args.best_k
-        # two pinned staging sets, alternated, each guarded by an event so the
-        # host never overwrites a buffer whose H2D copy is still pending
-        mk = lambda shape: torch.empty(shape, dtype=torch.float32).pin_memory() if nd else None
-        self.stage = [(mk((sc.S,) + (nd or ())), mk((k, sc.S) + (nd or ())), torch.empty(3).pin_memory())
-                      for _ in range(2)]
+        # the step's host RNG numbers [z_d | z_g | y] in ONE flat buffer (one
+        # H2D copy per replay); two pinned staging copies, alternated, each
+        # guarded by an event so the host never overwrites a buffer whose
+        # copy is still pending
+        shp = [(sc.S,) + (nd or ()), (k, sc.S) + (nd or ()), (3,)] if nd else [(3,)]
+        sizes = [int(np.prod(x)) for x in shp]
+        views = lambda flat: [flat[o:o + n].view(x) for o, n, x in zip(np.cumsum([0] + sizes[:-1]), sizes, shp)]
+        self.stage_flat = [torch.empty(sum(sizes)).pin_memory() for _ in range(2)]
+        self.stage = [tuple(views(f)) if nd else (None, None, views(f)[0]) for f in self.stage_flat]
         self.stage_ev = [None, None]
         self.cur = 0
-        dv = lambda shape: torch.zeros(shape, device=dev) if nd else None
-        self.inp = StepInputs(dv((sc.S,) + (nd or ())), dv((k, sc.S) + (nd or ())), torch.zeros(3, device=dev))
+        self.inp_flat = torch.zeros(sum(sizes), device=dev)
+        dv = views(self.inp_flat)
+        self.inp = StepInputs(dv[0], dv[1], dv[2]) if nd else StepInputs(None, None, dv[0])
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -341,12 +346,10 @@ class GraphedTrainer:
         h_zd, h_zg, h_y = self.stage[i]
         if z_d is not None:
             h_zd.copy_(z_d)
-            self.inp.z_d.copy_(h_zd, non_blocking=True)
         if z_g is not None:
             h_zg.copy_(z_g)
-            self.inp.z_g.copy_(h_zg, non_blocking=True)
         h_y.copy_(y)
-        self.inp.y.copy_(h_y, non_blocking=True)
+        self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.stage_ev[i] = ev
