@@ -176,15 +176,14 @@ def main():
         # dominant kernel: the pool forward launch with the most device time per iteration
         key = max(timed, key=lambda k: timed[k][0] * timed[k][2])
         n, fl, ms = timed[key]
-        bn, gpw = key[0], key[1]
-        kname = "sgg::pool_fwd_kernel<%d, %d>" % (bn, gpw)
+        kname = "sgg::pool_fwd_kernel<%d, %d, %d>" % key[:3]
         achieved = fl / (ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": pmc_traffic(kname, key),
                     "kernel": kname, "launches_per_iteration": round(n / n_it, 2),
                     "avg_launch_us": round(ms * 1e3, 2), "flop_per_launch": fl,
                     "note": "fp32 (f32 MFMA, same peak as VALU FMA); all pool forward launches per iteration "
-                            "[bn, gpw, scenes, peds]: %s" % {
+                            "[bn, gpw, unroll, scenes, peds]: %s" % {
                                 "%s" % list(k): {"per_iter": round(v[0] / n_it, 2), "avg_us": round(v[2] * 1e3, 2),
                                                  "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 2)}
                                 for k, v in timed.items()}}

@@ -314,7 +314,9 @@ class _Pool(torch.autograd.Function):
                                      N.ptr(am), N.stream_ptr()), "sgg_pool_fwd")
         launch()
         if pool_timer.active:
-            pool_timer.rec.append(((bn, gpw, scenes.S, B), _pool_flops(scenes, bn), launch))
+            # the k-step unroll the library picks (pool.hip launch_fwd_g)
+            unr = 16 if nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count else 2
+            pool_timer.rec.append(((bn, gpw, unr, scenes.S, B), _pool_flops(scenes, bn), launch))
         ctx.scenes = scenes
         ctx.E = E
         ctx.save_for_backward(h, pos, W1, We, be, A, W2, U, out, am)

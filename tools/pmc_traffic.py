@@ -5,7 +5,7 @@ usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR BENCH_JSON OUT_JSON
 FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports half the
 bytes of wide (16 B/lane) coalesced reads (MI355X_MICROARCH.md, HBM section),
 so reads are doubled; WRITE_SIZE is exact for the kernels' 4-16 B/lane stores.
-Output keys are "<kernel>|[bn, gpw, scenes, peds]" for the pool forward
+Output keys are "<kernel>|[bn, gpw, unroll, scenes, peds]" for the pool forward
 launches that bench.py reports (matched by kernel name, only where one launch
 shape has that name), plus a per-kernel-name table of every kernel.
 """
@@ -47,7 +47,7 @@ def main():
            "kernels": kernels}
     by_name = collections.defaultdict(list)
     for key in keys:
-        by_name["sgg::pool_fwd_kernel<%d, %d>" % (key[0], key[1])].append(key)
+        by_name["sgg::pool_fwd_kernel<%d, %d, %d>" % tuple(key[:3])].append(key)
     for name, ks in by_name.items():
         if len(ks) == 1 and name in kernels:
             res["%s|%s" % (name, ks[0])] = kernels[name]
