@@ -109,10 +109,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; SGG_BENCH_BACKEND=gloo (and more ranks than GPUs,
+    # ranks sharing a device) is only for rehearsing the multi-rank path on a
+    # one-GPU box -- the driver's runs use nccl (RCCL over xGMI)
+    backend = os.environ.get("SGG_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from sgan import kernels as K
     from sgan.data.synthetic import synthetic_batch

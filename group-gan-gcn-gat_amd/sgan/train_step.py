@@ -76,6 +76,7 @@ class DataParallel:
         self.group = group
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
+        self.cut = None   # set by GraphedTrainer while capturing: graph segment boundary
 
     def shard(self, S_global):
         """Contiguous scene range [s0, s1) of this rank."""
@@ -87,13 +88,15 @@ class DataParallel:
         """SUM-all-reduce a list of tensors through one flat bucket."""
         if not self.on or self.world == 1 or not tensors:
             return
+        if self.cut is not None:       # capturing: end the graph segment here
+            self.cut(tensors)
+            return
         flat = torch.cat([t.reshape(-1) for t in tensors])
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-        o = 0
-        for t in tensors:
-            n = t.numel()
-            t.copy_(flat[o:o + n].view_as(t))
-            o += n
+        # unpack with one multi-tensor copy (a copy per tensor would add ~45
+        # launches per optimizer step)
+        views = flat.split([t.numel() for t in tensors])
+        torch._foreach_copy_(tensors, [v.view_as(t) for v, t in zip(views, tensors)])
 
 
 class StepInputs:
@@ -286,8 +289,9 @@ class GanTrainer:
 
 
 class GraphedTrainer:
-    """One full iteration (D-step + G-step, both Adam updates and the DP
-    all-reduces) captured once into a HIP graph and replayed.
+    """One full iteration (D-step + G-step, both Adam updates) captured once
+    into a HIP graph and replayed; with several ranks, three graph segments
+    with the two gradient all-reduces run eagerly between them.
 
     The batch lives in static device tensors (copy new data into
     `self.batch` between replays for real training); each replay first draws
@@ -332,11 +336,37 @@ class GraphedTrainer:
                 trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
         trainer.opt_g.zero_grad(set_to_none=True)
         trainer.opt_d.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph):
-            self.losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
+        # One graph at world size 1.  With several ranks the capture is cut at
+        # each gradient all-reduce (DataParallel.cut): the collectives run
+        # eagerly between graph segments on the segments' static buffers, so
+        # the replay never depends on capturing a collective (gloo cannot be
+        # captured; a failed capture would poison the stream).
+        self.segments = []
+        pool = torch.cuda.graph_pool_handle()
+        dp = trainer.dp
+        cap = torch.cuda.Stream()
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=pool)
+
+            def cut(tensors):
+                nonlocal g
+                g.capture_end()
+                self.segments.append((g, list(tensors)))
+                g = torch.cuda.CUDAGraph()
+                g.capture_begin(pool=pool)
+            dp.cut = cut if (dp.on and dp.world > 1) else None
+            try:
+                self.losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
+            finally:
+                dp.cut = None
+            g.capture_end()
+            self.segments.append((g, None))
+        torch.cuda.current_stream().wait_stream(cap)
+        torch.cuda.synchronize()
 
     def _load(self, z_d, z_g, y):
         i = self.cur
@@ -358,7 +388,10 @@ class GraphedTrainer:
         """Draw this iteration's host RNG numbers, replay the graph; returns the
         (device) loss dicts of the captured step."""
         self._load(*self.t.draw_inputs(*self.span))
-        self.graph.replay()
+        for g, tensors in self.segments:
+            g.replay()
+            if tensors is not None:
+                self.t.dp.allreduce_(tensors)
         return self.losses
 
 
