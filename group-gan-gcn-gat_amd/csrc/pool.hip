@@ -483,9 +483,10 @@ static void launch_fwd_g(const float* U, const float* pos, const float* A, const
   const int grid = nchunks < 65536 ? (nchunks + 7) & ~7 : 65536;   // multiple of 8 (XCD-aware order)
   const size_t lds = pool_fwd_lds<BN>(max_rows);
   const int4* ck = reinterpret_cast<const int4*>(chunks);
-  // <= 4 chunks per CU: full unroll (measured 5-8 % faster at 64-128 scenes,
-  // 10-20 % slower at >= 1024 scenes where occupancy hides the LDS latency)
-  if (nchunks <= 4 * device_cus())
+  // <= 4 chunks per CU and <= 2 pair groups per wave: full unroll (measured
+  // 5-8 % faster at 64-128 scenes; 10-20 % slower at >= 1024 scenes where
+  // occupancy hides the LDS latency, and at gpw 4 the wave needs ~350 VGPRs)
+  if (GPW <= 2 && nchunks <= 4 * device_cus())
     hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW, kKT / 4>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off,
                        ck, nchunks, out, am);
   else

@@ -315,7 +315,8 @@ class _Pool(torch.autograd.Function):
         launch()
         if pool_timer.active:
             # the k-step unroll the library picks (pool.hip launch_fwd_g)
-            unr = 16 if nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count else 2
+            unr = 16 if gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count \
+                else 2
             pool_timer.rec.append(((bn, gpw, unr, scenes.S, B), _pool_flops(scenes, bn), launch))
         ctx.scenes = scenes
         ctx.E = E
