@@ -1,9 +1,9 @@
 """Autograd wrappers around the libsgg.so C ABI (include/sgg.h).
 
 Every op launches on torch's current stream through ctypes; forward and
-backward are hand-written HIP kernels, except the parameter-gradient
-reductions over all nodes (X^T dY, column sums), which are plain GEMMs /
-reductions left to rocBLAS via torch.  No op has a CPU path.
+backward are hand-written HIP kernels, the parameter-gradient reductions over
+all nodes (X^T dY, column sums) included (sgg_xtw, xtw.hip).  No op has a CPU
+path.
 """
 import os
 
@@ -162,22 +162,30 @@ class ClipAdam:
     launches (sgg_adam_step; scripts/train.py:418-427, :472-482).
 
     The state lives in a torch.optim.Adam (capturable layout: per-parameter
-    float32 device 'step', 'exp_avg', 'exp_avg_sq'), created eagerly, so
-    `state_dict()` / `load_state_dict()` are torch's.  Parameters whose grad
-    is None are skipped, exactly as torch's Adam skips them (their step does
-    not advance).  Graph-capturable: the tensor list is passed by value."""
+    float32 device 'step', 'exp_avg', 'exp_avg_sq'), so `state_dict()` /
+    `load_state_dict()` are torch's: a parameter gets its state the first
+    time it has a gradient, exactly as torch's Adam (parameters whose grad is
+    None are skipped and keep no state), so a state dict round-trips with a
+    reference checkpoint's optimizer state (train.py:238, :363).  Graph-
+    capturable: the tensor list is passed by value (the trainers warm up
+    eagerly before capturing, which creates the state)."""
 
     MAX_TENSORS = 48
 
     def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8):
         self.params = [p for p in params]
         self.opt = torch.optim.Adam(self.params, lr=lr, betas=betas, eps=eps, capturable=True)
-        for p in self.params:
-            st = self.opt.state[p]
+        self._ws = None
+
+    def _state(self, p):
+        st = self.opt.state[p]
+        if "exp_avg" not in st:
             st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-        self._ws = None
+        elif not torch.is_tensor(st["step"]) or st["step"].device != p.device or st["step"].dtype != torch.float32:
+            st["step"] = torch.as_tensor(float(st["step"]), dtype=torch.float32).to(p.device)
+        return st
 
     @property
     def param_groups(self):
@@ -187,7 +195,13 @@ class ClipAdam:
         return self.opt.state_dict()
 
     def load_state_dict(self, sd):
+        """torch's Adam state dict, e.g. a reference checkpoint's
+        g_optim_state / d_optim_state (host 'step' counters are moved to the
+        device, the capturable layout the fused step reads)."""
         self.opt.load_state_dict(sd)
+        for p in self.params:
+            if self.opt.state.get(p):
+                self._state(p)
 
     def zero_grad(self, set_to_none=True):
         self.opt.zero_grad(set_to_none=set_to_none)
@@ -212,7 +226,7 @@ class ClipAdam:
                 if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
                     raise N.NativeError("ClipAdam: parameters and grads must be contiguous fp32 device tensors")
         n = len(act)
-        st = [self.opt.state[p] for p in act]
+        st = [self._state(p) for p in act]
         arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])
         numel = (ctypes.c_longlong * n)(*[p.numel() for p in act])
         total = sum(p.numel() for p in act)
@@ -743,15 +757,21 @@ class _Bce(torch.autograd.Function):
 
 
 _CONST = {}
+_CONST_VALUES = (0.0, 1.0)
 
 
 def const(v, device):
-    """A cached device scalar (no fill launch per use; created on first use,
-    outside graph capture: the trainers warm up before capturing)."""
-    key = (str(device), float(v))
+    """A cached device scalar for the FIXED constants 0 and 1 (no fill launch
+    per use; created on first use, outside graph capture: the trainers warm up
+    before capturing).  Any other value gets a fresh tensor: caching per value
+    would keep one device scalar per random label-smoothing draw forever."""
+    v = float(v)
+    if v not in _CONST_VALUES:
+        return torch.full((), v, device=device, dtype=torch.float32)
+    key = (str(device), v)
     t = _CONST.get(key)
     if t is None:
-        t = _CONST[key] = torch.full((), float(v), device=device, dtype=torch.float32)
+        t = _CONST[key] = torch.full((), v, device=device, dtype=torch.float32)
     return t
 
 

@@ -16,12 +16,14 @@ decoder rollout are single fused launches (sgg_lstm_fwd / sgg_lstm_bwd).
 
 Extra keyword-only arguments beyond the reference's are optional and default
 to the reference behaviour:
-  TrajectoryGenerator(..., graph='gat'|'gcn'|'sgangat')  selects the
-      message-passing module the forward calls ('gat' = the committed forward,
-      models.py:903-905; 'gcn' = the sgan-g(-p) checkpoint families, :902;
-      'sgangat' = the sgangat-g-p family: the batched multi-head GAT of the
-      commented sgan/GAT.py:6-106 text, then gcn_module; n_heads is then the
-      per-layer head list, e.g. [4, 1]).
+  TrajectoryGenerator(..., graph='gat'|'gcn'|'sgangat'|'vanilla')  selects
+      the message-passing module the forward calls ('gat' = the committed
+      forward, models.py:903-905; 'gcn' = the sgan-g(-p) checkpoint families,
+      :902; 'sgangat' = the sgangat-g-p family: the batched multi-head GAT of
+      the commented sgan/GAT.py:6-106 text, then gcn_module; n_heads is then
+      the per-layer head list, e.g. [4, 1]; 'vanilla' = upstream Social-GAN,
+      the sgan-models / sgan-p-models families: mlp_decoder_context, the
+      commented models.py:796-804 / :898, and no group module).
   forward(..., scenes=SceneIndex)  reuses a precomputed scene index.
 """
 import torch
@@ -425,8 +427,8 @@ class TrajectoryGenerator(nn.Module):
         super().__init__()
         if pooling_type and pooling_type.lower() == "none":
             pooling_type = None
-        if graph not in ("gat", "gcn", "sgangat"):
-            raise ValueError("graph must be 'gat', 'gcn' or 'sgangat'")
+        if graph not in ("gat", "gcn", "sgangat", "vanilla"):
+            raise ValueError("graph must be 'gat', 'gcn', 'sgangat' or 'vanilla'")
         self.obs_len = obs_len
         self.pred_len = pred_len
         self.mlp_dim = mlp_dim
@@ -466,17 +468,20 @@ class TrajectoryGenerator(nn.Module):
         #   gat     : committed models.py:800-812 -> gatencoder, gcn_module
         #   gcn     : sgan-g(-p)-models            -> mlp_decoder_context, gcn_module
         #   sgangat : sgangat-g-p-models           -> gatencoder.gat_net, mlp_decoder_context, gcn_module
-        # (mlp_decoder_context is carried by those checkpoints but not called)
+        #   vanilla : sgan-models / sgan-p-models  -> mlp_decoder_context only (upstream Social-GAN,
+        #             the commented models.py:796-804 / :898; no group module at all)
+        # (mlp_decoder_context is carried by the gcn / sgangat checkpoints but not called)
         if graph == "gat":
             self.gatencoder = GATEncoder(n_units=n_units, n_heads=n_heads, dropout=dropout1, alpha=alpha)
         elif graph == "sgangat":
             heads = list(n_heads) if isinstance(n_heads, (list, tuple)) else [n_heads] * (len(n_units) - 2) + [1]
             self.gatencoder = BatchGATEncoder(n_units=list(n_units), n_heads=heads, dropout=dropout1, alpha=alpha)
-        if graph != "gat":
+        if graph in ("gcn", "sgangat") or (graph == "vanilla" and self.mlp_decoder_needed()):
             self.mlp_decoder_context = make_mlp([input_dim, mlp_dim, decoder_h_dim - self.noise_first_dim],
                                                 activation=activation, batch_norm=batch_norm, dropout=dropout)
-        self.gcn_module = GCNModule(input_dim=input_dim, hidden_dim=72, out_dim=16, gcn_layers=2,
-                                    final_dim=decoder_h_dim - self.noise_first_dim)
+        if graph != "vanilla":
+            self.gcn_module = GCNModule(input_dim=input_dim, hidden_dim=72, out_dim=16, gcn_layers=2,
+                                        final_dim=decoder_h_dim - self.noise_first_dim)
 
     def add_noise(self, _input, seq_start_end, user_noise=None, scenes=None):
         """models.py:814-850 (noise drawn on the host, one draw per call)."""
@@ -518,6 +523,10 @@ class TrajectoryGenerator(nn.Module):
         if self.mlp_decoder_needed():
             if self.graph == "gat":
                 noise_input = self.gatencoder(ctx, seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
+            elif self.graph == "vanilla":
+                # upstream Social-GAN: noise_input = mlp_decoder_context(ctx) (models.py:898, dims
+                # :796-804); both Linear layers on the MFMA node transform, ReLU fused
+                noise_input = run_mlp(self.mlp_decoder_context, ctx)
             else:
                 if self.graph == "sgangat":
                     ctx = self.gatencoder(ctx, seq_start_end, scenes=sc)

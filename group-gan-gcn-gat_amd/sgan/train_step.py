@@ -79,10 +79,18 @@ class DataParallel:
         self.cut = None   # set by GraphedTrainer while capturing: graph segment boundary
 
     def shard(self, S_global):
-        """Contiguous scene range [s0, s1) of this rank."""
-        per = (S_global + self.world - 1) // self.world
-        s0 = min(self.rank * per, S_global)
-        return s0, min(s0 + per, S_global)
+        """Contiguous scene range [s0, s1) of this rank: a balanced split
+        (floor + remainder: shard sizes differ by at most one scene).  Every
+        rank must hold >= 1 scene (the kernels take no empty batch); the check
+        depends only on (S_global, world), so every rank raises together,
+        before any collective is entered."""
+        if S_global < self.world:
+            raise ValueError("scene-sharded DP needs >= %d scenes (one per rank), got %d: the reference loader "
+                             "keeps a short last batch (loader.py:22-27); drop it or run it on fewer ranks"
+                             % (self.world, S_global))
+        per, rem = divmod(S_global, self.world)
+        s0 = self.rank * per + min(self.rank, rem)
+        return s0, s0 + per + (1 if self.rank < rem else 0)
 
     def allreduce_(self, tensors):
         """SUM-all-reduce a list of tensors through one flat bucket."""
@@ -135,11 +143,17 @@ class GanTrainer:
         self.args = args or TrainArgs()
         self.dp = dp or DataParallel()
         self.selective_backward = selective_backward
-        skip = "gcn_module." if getattr(G, "graph", "gat") == "gat" else "gatencoder."
-        self.g_params = [p for n, p in G.named_parameters() if not n.startswith(skip)]
+        bn = [n for n, m in list(G.named_modules()) + list(D.named_modules()) if isinstance(m, torch.nn.BatchNorm1d)]
+        if bn:
+            # the execution plan (one stacked [fake | real] D call, the shared G
+            # context, scene sharding) changes the batch a BatchNorm averages over
+            raise NotImplementedError("GanTrainer: BatchNorm layers (%s) are not supported (train.py's batch_norm=0 "
+                                      "default); drive the modules with the reference's own step functions" % bn[:3])
+        # Adam over ALL of G's parameters, as train.py:238 builds it, so the
+        # optimizer state (and its index order) matches reference checkpoints;
+        # the unused graph module gets no gradient and Adam skips it
+        self.g_params = list(G.parameters())
         self.d_params = list(D.parameters())
-        # the unused graph module gets no gradient, so Adam would skip it anyway
-        # (train.py builds Adam over G.parameters())
         self.opt_g = self.ops.optimizer(self.g_params, self.args.g_learning_rate)
         self.opt_d = self.ops.optimizer(self.d_params, self.args.d_learning_rate)
 
@@ -258,13 +272,24 @@ class GanTrainer:
         adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global)    # gan_g_loss
         loss = adv + (terms[0] if terms else 0.0)
         self.opt_g.zero_grad(set_to_none=True)
-        torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self.g_params)
+        torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self._g_inputs())
         vals = self._finish(self.g_params, self.opt_g, [terms[0] if terms else adv * 0, adv, loss],
                             a.clipping_threshold_g)
         out = {"G_discriminator_loss": vals[1], "G_total_loss": vals[2]}
         if use_l2:
             out["G_l2_loss_rel"] = vals[0]
         return out
+
+    def _g_inputs(self):
+        """G parameters on the forward's path (the family's unused graph
+        module -- gcn_module under 'gat', mlp_decoder_context under 'gcn' /
+        'sgangat' -- has no gradient and is left out of backward's inputs)."""
+        if not hasattr(self, "_g_in"):
+            graph = getattr(self.G, "graph", "gat")
+            skip = {"gat": ("gcn_module.",), "gcn": ("gatencoder.", "mlp_decoder_context."),
+                    "sgangat": ("mlp_decoder_context.",), "vanilla": ()}.get(graph, ())
+            self._g_in = [p for n, p in self.G.named_parameters() if not n.startswith(skip)]
+        return self._g_in
 
     def step(self, batch, sc, batch_g=None, sc_g=None, **kw):
         """One reference iteration (d_steps = g_steps = 1): the D-step on

@@ -1,7 +1,14 @@
-"""Worker of test_gpu_parity.test_graphed_trainer_two_ranks (launched by
+"""Worker of test_gpu_parity.test_graphed_trainer_two_ranks and
+test_gpu_configs.test_two_rank_512_scene_shard_equals_single (launched by
 torch.distributed.run, 2 ranks sharing one GPU over gloo): the segmented
 HIP-graph replay (GraphedTrainer, all-reduces between graph segments) must
-match the eager scene-sharded GanTrainer step for step."""
+match the eager scene-sharded GanTrainer step for step.
+
+SGG_DP_SCENES=N: N synthetic 20-ped scenes as the global batch (default: a
+6-scene ragged batch).  SGG_DP_VS_SINGLE=1: also run the whole global batch
+on ONE rank (no data parallelism) and require the 2-rank result to equal it
+(losses 1e-4 rel; weights within Adam's sign-flip bound on noise-level
+gradients, 2 lr per step)."""
 import os
 import random
 import sys
@@ -25,14 +32,23 @@ def models():
     return g.cuda(), d.cuda()
 
 
+def weights(g, d):
+    """G and D state under distinct prefixes (both have an `encoder.`)."""
+    out = {"g." + k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
+    out.update({"d." + k: v.detach().cpu().clone() for k, v in d.state_dict().items()})
+    return out
+
+
 def main():
     from sgan.data.synthetic import synthetic_batch
     from sgan.scene import SceneIndex
     from sgan.train_step import DataParallel, GanTrainer, GraphedTrainer, shard_batch
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
-    sizes = [20, 7, 13, 20, 2, 9]
+    n_sc = int(os.environ.get("SGG_DP_SCENES", "0"))
+    sizes = [20] * n_sc if n_sc else [20, 7, 13, 20, 2, 9]
     res = []
+    hist = []
     for graphed in (False, True):
         g, d = models()
         tr = GanTrainer(g, d, dp=DataParallel())
@@ -51,15 +67,36 @@ def main():
         else:
             for _ in range(4):
                 ld, lg = tr.step(local, lsc, **kw)
+                hist.append([float(v) for v in list(ld.values()) + list(lg.values())])
         torch.cuda.synchronize()
-        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())},
-                    {k: v.detach().cpu().clone() for k, v in list(g.state_dict().items()) + list(d.state_dict().items())}))
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, weights(g, d)))
     (la, wa), (lb, wb) = res
     for k in la:
         assert abs(la[k] - lb[k]) <= 1e-5 * max(1.0, abs(la[k])), (k, la[k], lb[k])
     for k in wa:
         err = (wa[k] - wb[k]).abs().max().item()
         assert err <= 1e-5 + 1e-5 * wa[k].abs().max().item(), (k, err)
+    if os.environ.get("SGG_DP_VS_SINGLE") == "1":
+        # the same 4 iterations on the WHOLE global batch, one rank, no DP
+        g, d = models()
+        dp1 = DataParallel()
+        dp1.on, dp1.world, dp1.rank = False, 1, 0
+        tr = GanTrainer(g, d, dp=dp1)
+        batch = synthetic_batch(sizes, seed=3, device="cuda")
+        sc = SceneIndex(np.concatenate([[0], np.cumsum(sizes)]), "cuda")
+        torch.manual_seed(9)
+        random.seed(9)
+        for it in range(4):
+            ld, lg = tr.step(batch, sc)
+            one = [float(v) for v in list(ld.values()) + list(lg.values())]
+            for a, b in zip(hist[it], one):
+                assert abs(a - b) <= 1e-4 * max(1.0, abs(b)), ("loss vs single rank", it, a, b)
+        torch.cuda.synchronize()
+        ws = weights(g, d)
+        for k in ws:
+            lr = 1e-3 if k.startswith("d.") else 1e-4
+            err = (wa[k] - ws[k]).abs().max().item()
+            assert err <= 2 * lr * 4 + 1e-5 * ws[k].abs().max().item(), ("weights vs single rank", k, err)
     dist.barrier()
     dist.destroy_process_group()
     print("rank %d OK" % int(os.environ["RANK"]), flush=True)

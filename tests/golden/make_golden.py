@@ -412,6 +412,89 @@ def fx_sgangat():
     save("gen_fwd_sgangat.npz", out)
 
 
+# ----------------------------------------------------------------------------
+# vanilla family (upstream Social-GAN: sgan-models / sgan-p-models)
+# ----------------------------------------------------------------------------
+def build_vanilla(pooling, seed=0):
+    """Generator of the sgan-models (pooling None, BASELINE configs[0]) /
+    sgan-p-models (pool_net) families: the reference's own TrajectoryGenerator
+    built with those checkpoints' args (read as text from
+    models/sgan-models/eth_12_model.pt: embedding 16, encoder/decoder h 32,
+    mlp 64, noise (8,) gaussian 'global', pooling 'none', bottleneck 8,
+    batch_norm 0) plus the mlp_decoder_context the committed file comments
+    out (models.py:796-804), built by the reference's make_mlp.  Its
+    gatencoder / gcn_module are constructed by the reference but not part of
+    the family (dropped from the saved state)."""
+    torch.manual_seed(seed)
+    g = M.TrajectoryGenerator(
+        obs_len=8, pred_len=12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32, mlp_dim=64,
+        num_layers=1, noise_dim=(8,), noise_type="gaussian", noise_mix_type="global",
+        pooling_type=pooling or "none", pool_every_timestep=False, dropout=0.0, bottleneck_dim=8,
+        batch_norm=False, n_units=[40, 16, 40], n_heads=1, dropout1=0, alpha=0.2)
+    in_dim = 32 + 8 if pooling else 32
+    g.mlp_decoder_context = M.make_mlp([in_dim, 64, 32 - 8], activation="relu", batch_norm=False, dropout=0.0)
+    g.apply(TR.init_weights)
+    g.train()
+    return g
+
+
+def _vanilla_forward(g, batch, noise):
+    """TrajectoryGenerator.forward (models.py:862-927) with the upstream
+    context line models.py:898 (noise_input = mlp_decoder_context(ctx)) in
+    place of the GAT call :903-905."""
+    obs_traj, obs_rel, sse = batch["obs_traj"], batch["obs_traj_rel"], batch["seq_start_end"]
+    Bn = obs_rel.size(1)
+    h = g.encoder(obs_rel)
+    ctx = h.view(-1, g.encoder_h_dim)
+    if g.pooling_type:                                                      # :878-886
+        ctx = torch.cat([ctx, g.pool_net(h, sse, obs_traj[-1])], dim=1)
+    ni = g.mlp_decoder_context(ctx)                                         # :898
+    dh = g.add_noise(ni, sse, user_noise=noise).unsqueeze(0)                # :909-910
+    dc = torch.zeros(g.num_layers, Bn, g.decoder_h_dim)
+    out, _ = g.decoder(obs_traj[-1], obs_rel[-1], (dh, dc), sse)
+    return out
+
+
+def _vanilla_state(g, grads=False):
+    out = {}
+    for k, p in g.named_parameters():
+        if k.startswith("gatencoder.") or k.startswith("gcn_module."):
+            continue
+        if grads:
+            if p.grad is not None:
+                out[k] = p.grad.detach().numpy().copy()
+        else:
+            out[k] = p.detach().numpy().copy()
+    return out
+
+
+def fx_vanilla():
+    out = {}
+    batches = {"synth": synth_batch([20] * 6 + [2, 5, 33], seed=5), "zara1": real_batch("zara1", "test", 16),
+               "eth": real_batch("eth", "test", 16)}
+    for tag, pooling in (("none", None), ("pool", "pool_net")):
+        g = build_vanilla(pooling, 0)
+        for k, v in _vanilla_state(g).items():
+            out[tag + "/w/" + k] = v
+        for bname, b in batches.items():
+            S = b["seq_start_end"].size(0)
+            torch.manual_seed(77)
+            noise = torch.randn(S, 8)
+            g.zero_grad()
+            y = _vanilla_forward(g, b, noise)
+            dy = torch.randn_like(y)
+            (y * dy).sum().backward()
+            pre = "%s/%s/" % (tag, bname)
+            for k in ("obs_traj", "obs_traj_rel", "obs_traj_g", "seq_start_end", "pred_traj", "pred_traj_rel"):
+                out[pre + k] = b[k].numpy()
+            out[pre + "noise"] = noise.numpy()
+            out[pre + "out"] = y.detach().numpy()
+            out[pre + "dout"] = dy.numpy()
+            for k, v in _vanilla_state(g, grads=True).items():
+                out[pre + "dw/" + k] = v
+    save("gen_fwd_vanilla.npz", out)
+
+
 def fx_disc():
     g, d = build_models(0)
     b = synth_batch([20] * 4 + [2, 9], seed=6)
@@ -430,12 +513,30 @@ def fx_disc():
     save("disc_fwd.npz", out)
 
 
+class _RecordingAdam(torch.optim.Adam):
+    """torch.optim.Adam that records every parameter's .grad when step() is
+    called, i.e. after loss.backward() and after the reference's
+    clip_grad_norm_ (train.py:423-427, 478-482), before the update."""
+
+    def __init__(self, named, rec, **kw):
+        named = list(named)
+        super().__init__([p for _, p in named], **kw)
+        self._named, self._rec = named, rec
+
+    def step(self, closure=None):
+        self._rec.append({k: p.grad.detach().numpy().copy() for k, p in self._named if p.grad is not None})
+        return super().step(closure)
+
+
 def fx_train_step():
     """discriminator_step + generator_step (scripts/train.py:395-484), 2 iterations,
-    fresh Adam, seeded host RNGs (noise: torch CPU RNG, label smoothing: random)."""
+    fresh Adam, seeded host RNGs (noise: torch CPU RNG, label smoothing: random).
+    Also records the gradients each optimizer step consumes (D: raw; G: after
+    clip_grad_norm_ 2.0) as it%d/gradD/<param>, it%d/gradG/<param>."""
     g, d = build_models(0)
-    opt_g = torch.optim.Adam(g.parameters(), lr=ARGS.g_learning_rate)
-    opt_d = torch.optim.Adam(d.parameters(), lr=ARGS.d_learning_rate)
+    rec_g, rec_d = [], []
+    opt_g = _RecordingAdam(g.named_parameters(), rec_g, lr=ARGS.g_learning_rate)
+    opt_d = _RecordingAdam(d.named_parameters(), rec_d, lr=ARGS.d_learning_rate)
     out = {}
     batches = [synth_batch([20] * 5 + [7], seed=41), synth_batch([20] * 4 + [3, 12], seed=42)]
     torch.manual_seed(1234)
@@ -457,37 +558,55 @@ def fx_train_step():
             out["it%d/G/%s" % (it, k)] = np.float64(v)
         out.update(sd_arrays(g, "it%d/g/" % it))
         out.update(sd_arrays(d, "it%d/d/" % it))
+        for k, v in rec_d[-1].items():
+            out["it%d/gradD/%s" % (it, k)] = v
+        for k, v in rec_g[-1].items():
+            out["it%d/gradG/%s" % (it, k)] = v
     save("train_step.npz", out)
 
 
-def fx_eval(splits):
+EVAL_MODES = ("gat", "gcn", "sgangat", "vanilla", "vanilla_p")
+
+
+def fx_eval(splits, modes=EVAL_MODES):
     """scripts/evaluate_model.py:72-99 on the test split, 20 samples, seeded host RNG,
     seeded random-init weights (trained checkpoints are not loadable with the
-    safe loader: they hold collections.defaultdict)."""
-    res = {}
-    for mode in ("gat", "gcn", "sgangat"):
-        for split in splits:
-            g, _ = build_models(0)
-            if mode == "sgangat":
-                g, sg, _ = build_sgangat(0)
-                g.forward = types.MethodType(
-                    lambda self, ot, orl, sse, og, user_noise=None, sg=sg: _sgangat_forward(
-                        self, sg, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse, obs_traj_g=og), user_noise),
-                    g)
-            if mode == "gcn":
-                g.forward = types.MethodType(
-                    lambda self, ot, orl, sse, og, user_noise=None: _gen_forward(
-                        self, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse, obs_traj_g=og), user_noise, "gcn"), g)
-            path = os.path.join(REF, "datasets_group", split, "test")
-            a = EV.AttrDict(dict(vars(ARGS)))
-            _, loader = DL.data_loader(a, path)
-            torch.manual_seed(0)
-            t0 = time.time()
-            ade, fde = EV.evaluate(a, loader, g, 20)
-            res["%s/%s" % (mode, split)] = dict(ade=float(ade), fde=float(fde), seconds=time.time() - t0,
-                                                 num_seq=len(loader.dataset))
-            print(mode, split, res["%s/%s" % (mode, split)], flush=True)
-    with open(os.path.join(HERE, "evaluate.json"), "w") as f:
+    safe loader: they hold collections.defaultdict).  Also the vanilla family
+    on ETH with batch_size 1 (BASELINE configs[0]) as 'vanilla_b1/eth'.
+    Entries are merged into the existing evaluate.json."""
+    path_json = os.path.join(HERE, "evaluate.json")
+    res = json.load(open(path_json)) if os.path.exists(path_json) else {}
+    runs = [(m, sp, 64) for m in modes for sp in splits]
+    if "vanilla" in modes and "eth" in splits:
+        runs.append(("vanilla_b1", "eth", 1))
+    for mode, split, bs in runs:
+        g, _ = build_models(0)
+        if mode.startswith("vanilla"):
+            g = build_vanilla("pool_net" if mode == "vanilla_p" else None, 0)
+            g.forward = types.MethodType(
+                lambda self, ot, orl, sse, og, user_noise=None: _vanilla_forward(
+                    self, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse), user_noise), g)
+        if mode == "sgangat":
+            g, sg, _ = build_sgangat(0)
+            g.forward = types.MethodType(
+                lambda self, ot, orl, sse, og, user_noise=None, sg=sg: _sgangat_forward(
+                    self, sg, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse, obs_traj_g=og), user_noise),
+                g)
+        if mode == "gcn":
+            g.forward = types.MethodType(
+                lambda self, ot, orl, sse, og, user_noise=None: _gen_forward(
+                    self, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse, obs_traj_g=og), user_noise, "gcn"), g)
+        path = os.path.join(REF, "datasets_group", split, "test")
+        a = EV.AttrDict(dict(vars(ARGS)))
+        a["batch_size"] = bs
+        _, loader = DL.data_loader(a, path)
+        torch.manual_seed(0)
+        t0 = time.time()
+        ade, fde = EV.evaluate(a, loader, g, 20)
+        res["%s/%s" % (mode, split)] = dict(ade=float(ade), fde=float(fde), seconds=time.time() - t0,
+                                             num_seq=len(loader.dataset))
+        print(mode, split, res["%s/%s" % (mode, split)], flush=True)
+    with open(path_json, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
 
 
@@ -500,33 +619,64 @@ def copy_test_data():
             shutil.copyfile(os.path.join(src, f), os.path.join(dst, f))
 
 
-def fx_cpu_timing():
-    """Reference CPU train-iteration timing on this host, used to
-    validate the oracle's reference-formulation timing (ratio check)."""
-    g, d = build_models(0)
-    opt_g = torch.optim.Adam(g.parameters(), lr=ARGS.g_learning_rate)
-    opt_d = torch.optim.Adam(d.parameters(), lr=ARGS.d_learning_rate)
+def _time_iters(disc_step, gen_step, b, n):
+    disc_step(b)                                        # warm-up (not timed)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        disc_step(b)
+        gen_step(b)
+    return (time.perf_counter() - t0) / n
+
+
+def fx_cpu_timing(batch=64, threads=8, iters=2):
+    """CPU train-iteration timing on this host of the REAL
+    reference (scripts/train.py discriminator_step + generator_step) and of
+    the oracle's reference formulation (oracle/sgan_oracle.py, what bench.py's
+    cpu_baseline leg times on the GPU box) on the same synthetic batch, same
+    thread count; the two must agree within +-20 % for the oracle to stand in
+    for the reference (SURVEY.md:450-453)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import sgan_oracle as O
+    torch.set_num_threads(threads)
     keys = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel",
             "obs_traj_g", "pred_traj_g", "non_linear_ped", "loss_mask", "seq_start_end"]
-    b = synth_batch([20] * 16, seed=0)
+    b = synth_batch([20] * batch, seed=0)
     b["obs_vel"] = b["obs_traj_rel"] * 2.5
     b["pred_vel"] = b["pred_traj_rel"] * 2.5
     tup = [b[k] for k in keys]
-    TR.discriminator_step(ARGS, tup, g, d, TR.gan_d_loss, opt_d)
-    t0 = time.time()
-    n = 2
-    for _ in range(n):
-        TR.discriminator_step(ARGS, tup, g, d, TR.gan_d_loss, opt_d)
-        TR.generator_step(ARGS, tup, g, d, TR.gan_g_loss, opt_g)
-    dt = (time.time() - t0) / n
-    res = dict(scenes_per_s=16 / dt, threads=torch.get_num_threads(), batch=16, n_peds=20)
-    print("reference cpu timing", res)
+    g, d = build_models(0)
+    opt_g = torch.optim.Adam(g.parameters(), lr=ARGS.g_learning_rate)
+    opt_d = torch.optim.Adam(d.parameters(), lr=ARGS.d_learning_rate)
+    dt_ref = _time_iters(lambda x: TR.discriminator_step(ARGS, x, g, d, TR.gan_d_loss, opt_d),
+                         lambda x: TR.generator_step(ARGS, x, g, d, TR.gan_g_loss, opt_g), tup, iters)
+    torch.manual_seed(0)
+    og, od = O.build_default("gat")
+    oopt_g = torch.optim.Adam(og.parameters(), lr=1e-4)
+    oopt_d = torch.optim.Adam(od.parameters(), lr=1e-3)
+    dt_orc = _time_iters(lambda x: O.discriminator_step(O.Args, x, og, od, oopt_d),
+                         lambda x: O.generator_step(O.Args, x, og, od, oopt_g), tup, iters)
+    ratio = dt_ref / dt_orc
+    res = dict(reference_scenes_per_s=batch / dt_ref, oracle_scenes_per_s=batch / dt_orc,
+               oracle_over_reference=ratio, threads=threads, batch=batch, n_peds=20, iters=iters,
+               cpu=_cpu_model(), note="D-step + G-step (best_k=20) per iteration, 1 warm-up D-step")
+    print("cpu timing", res)
     with open(os.path.join(HERE, "ref_cpu_timing.json"), "w") as f:
         json.dump(res, f, indent=1)
+    assert 0.8 <= ratio <= 1.2, "oracle reference formulation is not within 20%% of the reference: %.3f" % ratio
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 ALL = dict(weights=fx_weights, pool=fx_pool, gat=fx_gat, gcn=fx_gcn, gen=fx_gen, sgangat=fx_sgangat,
-           disc=fx_disc,
+           vanilla=fx_vanilla, disc=fx_disc,
            train=fx_train_step, data=copy_test_data, timing=fx_cpu_timing)
 
 if __name__ == "__main__":
@@ -534,6 +684,7 @@ if __name__ == "__main__":
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--skip-eval", action="store_true")
     ap.add_argument("--splits", nargs="*", default=SPLITS)
+    ap.add_argument("--modes", nargs="*", default=list(EVAL_MODES))
     a = ap.parse_args()
     names = a.only if a.only else list(ALL)
     for n in names:
@@ -543,4 +694,4 @@ if __name__ == "__main__":
         ALL[n]()
         print("[%s] %.1fs" % (n, time.time() - t0), flush=True)
     if (a.only is None and not a.skip_eval) or (a.only and "eval" in a.only):
-        fx_eval(a.splits)
+        fx_eval(a.splits, tuple(a.modes))

@@ -1,0 +1,328 @@
+"""GPU coverage of every BASELINE.json config and of the drop-in call
+pattern (the HIP path through the C ABI against the reference's fixtures and
+the CPU oracle):
+
+  configs[0]  vanilla Social-GAN (sgan-models, mlp_decoder_context), ETH --
+              generator fwd/bwd fixtures, ADE/FDE on all five splits and the
+              batch=1 ETH evaluation;
+  configs[1]  covered by test_gpu_parity (zara1 GAT, batch 64);
+  configs[3]  512 x 20-ped scenes (config 4's per-GPU shard): graph replay
+              == eager == selective_backward=False, and a 2-rank shard of the
+              512-scene global batch == one rank;
+  configs[4]  sgangat-g-p on 64-ped scenes: generator fwd/bwd and a whole
+              training iteration against the oracle;
+  drop-in     the product modules driven exactly as scripts/train.py:395-484
+              and scripts/evaluate_model.py:72-99 drive them (20 generator
+              calls with host noise, two D calls, torch.optim.Adam,
+              clip_grad_norm_), against the reference's own run.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, RecordingAdam, check_step_grads
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+SPLITS = ("eth", "hotel", "univ", "zara1", "zara2")
+KEYS = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel", "obs_traj_g",
+        "pred_traj_g", "non_linear_ped", "loss_mask", "seq_start_end"]
+
+
+def npz(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def T(a, dev=DEV):
+    return torch.from_numpy(np.asarray(a)).clone().to(dev)
+
+
+def close(a, b, rtol=1e-4, floor=1e-6, what=""):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, np.float64)
+    scale = max(np.abs(b).max(), floor)
+    err = np.abs(a - b).max() / scale
+    assert err <= rtol, "%s max rel err %.3e (scale %.3e)" % (what, err, scale)
+
+
+def generator(graph="gat", pooling="pool_net", dev=DEV):
+    from sgan.models import TrajectoryGenerator
+    return TrajectoryGenerator(8, 12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32, mlp_dim=64,
+                               num_layers=1, noise_dim=(8,), noise_type="gaussian", noise_mix_type="global",
+                               pooling_type=pooling, pool_every_timestep=False, dropout=0.0, bottleneck_dim=8,
+                               batch_norm=False, n_units=[40, 16, 40], n_heads=[4, 1] if graph == "sgangat" else 1,
+                               dropout1=0.0, alpha=0.2, graph=graph).to(dev)
+
+
+def discriminator(dev=DEV):
+    from sgan.models import TrajectoryDiscriminator
+    return TrajectoryDiscriminator(8, 12, embedding_dim=16, h_dim=48, mlp_dim=64, num_layers=1, batch_norm=False,
+                                   dropout=0.0, d_type="global").to(dev)
+
+
+def load(mod, f, prefix, strict=True):
+    mod.load_state_dict({k[len(prefix):]: torch.from_numpy(f[k]) for k in f.files if k.startswith(prefix)},
+                        strict=strict)
+    return mod
+
+
+def reference_gd(graph="gat"):
+    """Product G / D with the weights the reference fixtures were made from."""
+    w = npz("weights.npz")
+    g = generator(graph)
+    if graph == "sgangat":
+        load(g, npz("gen_fwd_sgangat.npz"), "w/")
+    else:
+        own = g.state_dict()
+        g.load_state_dict({k[2:]: torch.from_numpy(w[k]) for k in w.files if k.startswith("g/") and k[2:] in own},
+                          strict=False)
+    return g, load(discriminator(), w, "d/")
+
+
+# ---------------------------------------------------------------------------
+# configs[0]: vanilla Social-GAN (sgan-models / sgan-p-models)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("tag,pooling", [("none", None), ("pool", "pool_net")])
+def test_vanilla_generator_vs_reference_fixture(tag, pooling):
+    f = npz("gen_fwd_vanilla.npz")
+    g = load(generator("vanilla", pooling), f, tag + "/w/")          # strict: the upstream key set
+    for b in ("synth", "zara1", "eth"):
+        p = "%s/%s/" % (tag, b)
+        g.zero_grad()
+        y = g(T(f[p + "obs_traj"]), T(f[p + "obs_traj_rel"]), T(f[p + "seq_start_end"]), T(f[p + "obs_traj_g"]),
+              user_noise=T(f[p + "noise"]))
+        close(y, f[p + "out"], rtol=1e-4, what="vanilla %s %s out" % (tag, b))
+        (y * T(f[p + "dout"])).sum().backward()
+        fl = 1e-2 * max(np.abs(f[k]).max() for k in f.files if k.startswith(p + "dw/"))
+        for k, q in g.named_parameters():
+            close(q.grad, f[p + "dw/" + k], rtol=1e-3, floor=fl, what="vanilla %s %s d%s" % (tag, b, k))
+
+
+def _vanilla_weights(mode):
+    f = npz("gen_fwd_vanilla.npz")
+    tag, pooling = ("pool", "pool_net") if mode == "vanilla_p" else ("none", None)
+    return load(generator("vanilla", pooling), f, tag + "/w/")
+
+
+def test_evaluate_vanilla_all_splits():
+    """configs[0] family: ADE/FDE (20 samples, seeded host RNG) on the five
+    test splits, and ETH at batch_size 1, within 1e-3 of the reference run."""
+    from sgan.evaluate import evaluate_split
+    ev = json.load(open(os.path.join(GOLDEN, "evaluate.json")))
+    runs = [(m, s, 64) for m in ("vanilla", "vanilla_p") for s in SPLITS] + [("vanilla_b1", "eth", 1)]
+    for mode, split, bs in runs:
+        g = _vanilla_weights("vanilla" if mode == "vanilla_b1" else mode)
+        torch.manual_seed(0)
+        ade, fde = evaluate_split(g, os.path.join(GOLDEN, "datasets_group", split, "test"), num_samples=20,
+                                  batch_size=bs)
+        ref = ev["%s/%s" % (mode, split)]
+        assert abs(ade - ref["ade"]) <= 1e-3 * ref["ade"], (mode, split, ade, ref)
+        assert abs(fde - ref["fde"]) <= 1e-3 * ref["fde"], (mode, split, fde, ref)
+
+
+# ---------------------------------------------------------------------------
+# drop-in: the reference's own call pattern driving the product modules
+# ---------------------------------------------------------------------------
+def test_dropin_train_call_pattern_vs_reference():
+    """scripts/train.py:395-484 verbatim in structure (oracle.discriminator_step
+    / generator_step restate it line by line): 1 + 20 generator calls with
+    host noise per iteration, D(fake) and D(real) as two calls,
+    torch.optim.Adam, clip_grad_norm_(G, 2.0) -- on the product
+    TrajectoryGenerator / TrajectoryDiscriminator (HIP kernels), two
+    iterations against the reference's run (train_step.npz)."""
+    from oracle import sgan_oracle as O
+    g, d = reference_gd("gat")
+    og = RecordingAdam.make(g.named_parameters(), lr=O.Args.g_learning_rate)
+    od = RecordingAdam.make(d.named_parameters(), lr=O.Args.d_learning_rate)
+    f = npz("train_step.npz")
+    torch.manual_seed(1234)
+    random.seed(1234)
+    for it in range(2):
+        b = [T(f["b%d/%s" % (it, k)]) for k in KEYS]
+        ld = O.discriminator_step(O.Args, b, g, d, od)
+        lg = O.generator_step(O.Args, b, g, d, og)
+        for tag, lv in (("D", ld), ("G", lg)):
+            for k, v in lv.items():
+                ref = float(f["it%d/%s/%s" % (it, tag, k)])
+                assert abs(v - ref) <= 1e-4 * max(1.0, abs(ref)), (it, k, v, ref)
+        check_step_grads(od.rec[-1], f, it, "D")
+        check_step_grads(og.rec[-1], f, it, "G")
+        for mod, tag, lr in ((g, "g", 1e-4), (d, "d", 1e-3)):
+            for k, v in mod.state_dict().items():
+                ref = f["it%d/%s/%s" % (it, tag, k)]
+                err = np.abs(v.detach().cpu().numpy().astype(np.float64) - ref).max()
+                assert err <= 2 * lr * (it + 1) + 1e-5 * np.abs(ref).max(), (it, tag, k, err)
+
+
+@pytest.mark.parametrize("mode,split,bs", [("gat", "eth", 64), ("vanilla_b1", "eth", 1)])
+def test_dropin_evaluate_loop_vs_reference(mode, split, bs):
+    """scripts/evaluate_model.py:72-99 as written: per batch, num_samples=20
+    separate generator calls (each drawing its host noise), relative_to_abs,
+    displacement errors, per-scene min -- on the product generator."""
+    from oracle import sgan_oracle as O
+    from sgan.data.loader import data_loader
+    from sgan.evaluate import _Args
+    g = reference_gd("gat")[0] if mode == "gat" else _vanilla_weights("vanilla")
+    a = _Args(obs_len=8, pred_len=12, skip=1, delim="tab", batch_size=bs, loader_num_workers=0)
+    _, loader = data_loader(a, os.path.join(GOLDEN, "datasets_group", split, "test"))
+    torch.manual_seed(0)
+    ade, fde = O.evaluate(loader, g, num_samples=20, device=DEV)
+    ref = json.load(open(os.path.join(GOLDEN, "evaluate.json")))["%s/%s" % (mode, split)]
+    assert abs(ade - ref["ade"]) <= 1e-3 * ref["ade"], (mode, ade, ref)
+    assert abs(fde - ref["fde"]) <= 1e-3 * ref["fde"], (mode, fde, ref)
+
+
+# ---------------------------------------------------------------------------
+# configs[4]: sgangat-g-p, 64 peds per scene
+# ---------------------------------------------------------------------------
+SIZES64 = [64, 64, 64, 33, 64, 2]
+
+
+def _oracle_pair(g, d):
+    from oracle import sgan_oracle as O
+    og, od = O.build_default("sgangat")
+    og.load_state_dict({k: v.detach().cpu() for k, v in g.state_dict().items()})
+    od.load_state_dict({k: v.detach().cpu() for k, v in d.state_dict().items()})
+    return og, od
+
+
+def test_sgangat_64ped_generator_vs_oracle():
+    from sgan.data.synthetic import synthetic_batch
+    g, d = reference_gd("sgangat")
+    og, _ = _oracle_pair(g, d)
+    b = synthetic_batch(SIZES64, seed=64)
+    obs, _, obs_rel, _, _, _, obs_g, _, _, _, sse = b
+    z = torch.randn(len(SIZES64), 8)
+    y_ref = og(obs, obs_rel, sse, obs_g, user_noise=z)
+    dy = torch.randn_like(y_ref)
+    (y_ref * dy).sum().backward()
+    y = g(obs.to(DEV), obs_rel.to(DEV), sse.to(DEV), obs_g.to(DEV), user_noise=z.to(DEV))
+    (y * dy.to(DEV)).sum().backward()
+    close(y, y_ref, rtol=1e-4, what="sgangat-64 out")
+    ref_g = {k: p.grad for k, p in og.named_parameters() if p.grad is not None}
+    fl = 1e-2 * max(float(v.abs().max()) for v in ref_g.values())
+    for k, p in g.named_parameters():
+        if k in ref_g:
+            close(p.grad, ref_g[k], rtol=1e-3 if k.endswith("stack.0.bias") else 2e-4, floor=fl,
+                  what="sgangat-64 d" + k)
+
+
+def test_sgangat_64ped_train_step_vs_oracle():
+    """configs[4]: two GanTrainer iterations (D-step + G-step, best_k 20) on
+    64-ped scenes (SGG_POOL_MAX_PEDS, the fused GAT limit) against the
+    oracle's reference-formulation steps from the same seeds: losses, the
+    gradients each optimizer step consumed, weights."""
+    from oracle import sgan_oracle as O
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer
+    g, d = reference_gd("sgangat")
+    og, od = _oracle_pair(g, d)
+    oog = RecordingAdam.make(og.named_parameters(), lr=1e-4)
+    ood = RecordingAdam.make(od.named_parameters(), lr=1e-3)
+    tr = GanTrainer(g, d)
+    batches = [synthetic_batch(SIZES64, seed=640 + i) for i in range(2)]
+    torch.manual_seed(21)
+    random.seed(21)
+    ref = []
+    for b in batches:
+        ld = O.discriminator_step(O.Args, b, og, od, ood)
+        lg = O.generator_step(O.Args, b, og, od, oog)
+        ref.append((ld, lg, dict(ood.rec[-1]), dict(oog.rec[-1]),
+                    {k: v.clone() for k, v in og.state_dict().items()}, {k: v.clone() for k, v in od.state_dict().items()}))
+    torch.manual_seed(21)
+    random.seed(21)
+    for it, b in enumerate(batches):
+        bd = [t.to(DEV) for t in b]
+        sc = SceneIndex.from_seq_start_end(b[-1], DEV)
+        ld, lg = tr.step(bd, sc)
+        rld, rlg, rgd, rgg, rwg, rwd = ref[it]
+        for k, v in list(ld.items()) + list(lg.items()):
+            r = (rld if k.startswith("D") else rlg)[k]
+            assert abs(float(v) - r) <= 1e-4 * max(1.0, abs(r)), (it, k, float(v), r)
+        for mod, rg in ((d, rgd), (g, rgg)):
+            mine = {k: p.grad for k, p in mod.named_parameters() if p.grad is not None}
+            assert sorted(mine) == sorted(k for k in rg), (sorted(set(mine) ^ set(rg)))
+            fl = 1e-2 * max(float(v.abs().max()) for v in rg.values())
+            for k in rg:
+                close(mine[k], rg[k], rtol=1e-3 if k.endswith("stack.0.bias") else 2e-4, floor=fl,
+                      what="it%d grad %s" % (it, k))
+        for mod, rw, lr in ((g, rwg, 1e-4), (d, rwd, 1e-3)):
+            for k, v in mod.state_dict().items():
+                err = (v.detach().cpu().double() - rw[k].double()).abs().max().item()
+                assert err <= 2 * lr * (it + 1) + 1e-5 * rw[k].abs().max().item(), (it, k, err)
+
+
+# ---------------------------------------------------------------------------
+# configs[3]: 512 x 20-ped scenes (config 4's per-GPU shard)
+# ---------------------------------------------------------------------------
+def _grads(g, d):
+    out = {"g." + k: p.grad.detach().cpu().clone() for k, p in g.named_parameters() if p.grad is not None}
+    out.update({"d." + k: p.grad.detach().cpu().clone() for k, p in d.named_parameters() if p.grad is not None})
+    return out
+
+
+def test_512_scenes_graph_eager_selective_agree():
+    """At config 4's per-GPU shard (512 scenes x 20 peds = 10,240 peds; the
+    G-step decodes 204,800 ped rollouts) the captured HIP-graph replay, the
+    eager step and the step that keeps all best_k rollouts in the autograd
+    graph (selective_backward=False) consume the same host RNG stream and
+    produce the same losses and gradients."""
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, GraphedTrainer
+    sizes = [20] * 512
+    batch = synthetic_batch(sizes, seed=512, device=DEV)
+    batch_g = synthetic_batch(sizes, seed=513, device=DEV)
+    res = {}
+    for mode in ("eager", "graphed", "full"):
+        g, d = reference_gd("gat")
+        tr = GanTrainer(g, d, capturable=True, selective_backward=(mode != "full"))
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
+        torch.manual_seed(3)
+        random.seed(3)
+        if mode == "graphed":
+            gt = GraphedTrainer(tr, batch, sc, warmup=1, batch_g=batch_g, sc_g=scg)
+            ld, lg = gt.step()
+        else:
+            for _ in range(2):
+                ld, lg = tr.step(batch, sc, batch_g, scg)
+        torch.cuda.synchronize()
+        res[mode] = ({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, _grads(g, d))
+        del tr, g, d
+    la, ga = res["eager"]
+    for mode in ("graphed", "full"):
+        lb, gb = res[mode]
+        for k in la:
+            assert abs(la[k] - lb[k]) <= 1e-5 * max(1.0, abs(la[k])), (mode, k, la[k], lb[k])
+        assert sorted(ga) == sorted(gb), mode
+        fl = 1e-2 * max(float(v.abs().max()) for v in ga.values())
+        for k in ga:
+            close(gb[k], ga[k], rtol=1e-5 if mode == "graphed" else 2e-4, floor=fl, what="%s grad %s" % (mode, k))
+
+
+def test_two_rank_512_scene_shard_equals_single():
+    """config 4's data parallelism: 2 ranks (gloo, sharing this GPU) on a
+    512-scene global batch, segmented graph replay, == eager per rank, == the
+    whole batch on one rank (tests/_dp_graph_worker.py, SGG_DP_VS_SINGLE)."""
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, OMP_NUM_THREADS="1", SGG_DP_SCENES="512", SGG_DP_VS_SINGLE="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(here, "_dp_graph_worker.py")],
+                       capture_output=True, text=True, timeout=110, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and out.count(" OK") == 2, out[-3000:]

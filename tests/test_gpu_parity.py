@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, load_family
+from conftest import GOLDEN, check_step_grads, load_family
 
 pytestmark = pytest.mark.gpu
 
@@ -281,6 +281,8 @@ KEYS = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pr
 def test_train_step_vs_reference_fixture(selective):
     """Two reference iterations (discriminator_step + generator_step, fresh
     Adam, seeded host RNGs) reproduced by GanTrainer: losses within 1e-4 rel,
+    the gradients each optimizer step consumed (D raw, G after the 2.0 clip)
+    within 1e-3 of the tensor max (floor 1 % of the step's largest gradient),
     weights within Adam's sign-flip bound on noise-level gradients."""
     from sgan.scene import SceneIndex
     from sgan.train_step import GanTrainer
@@ -297,6 +299,10 @@ def test_train_step_vs_reference_fixture(selective):
             tag = "D" if k.startswith("D") else "G"
             ref = float(f["it%d/%s/%s" % (it, tag, k)])
             assert abs(float(v) - ref) <= 1e-4 * max(1.0, abs(ref)), (it, k, float(v), ref)
+        # after step(): D holds its D-step gradient (clip 0: raw), G its
+        # G-step gradient as clipped in place by the fused clip + Adam
+        check_step_grads({k: p.grad for k, p in d.named_parameters() if p.grad is not None}, f, it, "D")
+        check_step_grads({k: p.grad for k, p in g.named_parameters() if p.grad is not None}, f, it, "G")
         for mod, tag, lr in ((g, "g", 1e-4), (d, "d", 1e-3)):
             for k, v in mod.state_dict().items():
                 ref = f["it%d/%s/%s" % (it, tag, k)]
@@ -476,8 +482,9 @@ def test_graphed_trainer_equals_eager():
             for _ in range(4):
                 ld, lg = tr.step(batch, sc)
         torch.cuda.synchronize()
-        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())},
-                    {k: v.detach().cpu().clone() for k, v in list(g.state_dict().items()) + list(d.state_dict().items())}))
+        ws = {"g." + k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
+        ws.update({"d." + k: v.detach().cpu().clone() for k, v in d.state_dict().items()})
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws))
     (la, wa), (lb, wb) = res
     for k in la:
         assert abs(la[k] - lb[k]) <= 1e-5 * max(1.0, abs(la[k])), (k, la[k], lb[k])

@@ -1,0 +1,84 @@
+"""Host-side logic of the product that needs no GPU: optimizer-state format,
+scene sharding, trainer guards, device-scalar cache, the vanilla family's
+module set.  (No kernel is launched here.)"""
+import pytest
+import torch
+
+from conftest import GOLDEN  # noqa: F401  (sys.path setup)
+
+
+def _gen(graph="gat", pooling="pool_net"):
+    from sgan.models import TrajectoryGenerator
+    return TrajectoryGenerator(8, 12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32, mlp_dim=64,
+                               noise_dim=(8,), noise_mix_type="global", pooling_type=pooling,
+                               pool_every_timestep=False, bottleneck_dim=8, batch_norm=False, n_units=[40, 16, 40],
+                               n_heads=[4, 1] if graph == "sgangat" else 1, dropout1=0.0, alpha=0.2, graph=graph)
+
+
+def test_clip_adam_state_dict_roundtrips_reference_format():
+    """A reference checkpoint's g_optim_state is torch.optim.Adam over ALL of
+    G.parameters() (train.py:238, :363) with state only for the parameters
+    that had gradients: ClipAdam loads it, and torch's Adam loads ClipAdam's."""
+    from sgan.kernels import ClipAdam
+    torch.manual_seed(0)
+    g = _gen()
+    ref = torch.optim.Adam(g.parameters(), lr=1e-4)
+    for n, p in g.named_parameters():
+        p.grad = None if n.startswith("gcn_module.") else torch.randn_like(p)
+    ref.step()
+    sd = ref.state_dict()
+    ours = ClipAdam(g.parameters(), lr=1e-4)
+    ours.load_state_dict(sd)
+    out = ours.state_dict()
+    assert len(out["param_groups"][0]["params"]) == len(list(g.parameters()))
+    assert sorted(out["state"]) == sorted(sd["state"])
+    for k, st in sd["state"].items():
+        assert float(out["state"][k]["step"]) == float(st["step"]) == 1.0
+        assert torch.equal(out["state"][k]["exp_avg"].cpu(), st["exp_avg"])
+    back = torch.optim.Adam(g.parameters(), lr=1e-4)
+    back.load_state_dict(out)
+    # a fresh ClipAdam keeps no state for a parameter that never had a gradient
+    assert not ClipAdam(g.parameters(), lr=1e-4).state_dict()["state"]
+
+
+def test_shard_balanced_and_guarded():
+    from sgan.train_step import DataParallel
+    dp = DataParallel()
+    dp.world = 8
+    spans = []
+    for r in range(8):
+        dp.rank = r
+        spans.append(dp.shard(9))
+    assert spans[0] == (0, 2) and all(b - a == 1 for a, b in spans[1:])
+    assert spans[-1][1] == 9 and all(spans[i][1] == spans[i + 1][0] for i in range(7))
+    with pytest.raises(ValueError):
+        dp.shard(7)
+
+
+def test_trainer_rejects_batchnorm():
+    from sgan.models import TrajectoryDiscriminator
+    from sgan.train_step import GanTrainer
+    d = TrajectoryDiscriminator(8, 12, embedding_dim=16, h_dim=48, mlp_dim=64, batch_norm=True, d_type="global")
+    with pytest.raises(NotImplementedError):
+        GanTrainer(_gen(), d)
+
+
+def test_const_caches_only_fixed_values():
+    from sgan import kernels as K
+    n0 = len(K._CONST)
+    for _ in range(5):
+        K.const(0.913, "cpu")
+    assert len(K._CONST) == n0
+    assert K.const(1.0, "cpu") is K.const(1.0, "cpu")
+
+
+@pytest.mark.parametrize("pooling,n", [(None, 18), ("pool_net", 24)])
+def test_vanilla_family_state_dict_keys(pooling, n):
+    """The vanilla family carries exactly the upstream Social-GAN module set
+    (sgan-models checkpoints: encoder, decoder, [pool_net], mlp_decoder_context)."""
+    g = _gen("vanilla", pooling)
+    keys = [k for k, _ in g.named_parameters()]
+    assert len(keys) == n
+    assert not any(k.startswith(("gatencoder.", "gcn_module.")) for k in keys)
+    assert "mlp_decoder_context.0.weight" in keys and "mlp_decoder_context.2.bias" in keys
+    assert ("pool_net.mlp_pre_pool.0.weight" in keys) == bool(pooling)

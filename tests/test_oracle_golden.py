@@ -10,7 +10,7 @@ import torch
 
 from oracle import sgan_oracle as O
 
-from conftest import GOLDEN, load_family
+from conftest import GOLDEN, RecordingAdam, check_step_grads, load_family
 
 RTOL = 2e-5
 
@@ -157,8 +157,8 @@ def test_train_step_fixture():
         pytest.skip("train_step fixture not generated")
     f = np.load(path)
     g, d = load_models()
-    og = torch.optim.Adam(g.parameters(), lr=O.Args.g_learning_rate)
-    od = torch.optim.Adam(d.parameters(), lr=O.Args.d_learning_rate)
+    og = RecordingAdam.make(g.named_parameters(), lr=O.Args.g_learning_rate)
+    od = RecordingAdam.make(d.named_parameters(), lr=O.Args.d_learning_rate)
     torch.manual_seed(1234)
     random.seed(1234)
     keys = ["obs_traj", "pred_traj", "obs_traj_rel", "pred_traj_rel", "obs_vel", "pred_vel",
@@ -171,6 +171,9 @@ def test_train_step_fixture():
             assert abs(v - float(f["it%d/D/%s" % (it, k)])) <= 1e-4 * max(1.0, abs(v))
         for k, v in lg.items():
             assert abs(v - float(f["it%d/G/%s" % (it, k)])) <= 1e-4 * max(1.0, abs(v))
+        # the gradients each Adam step consumed (D raw, G after clip 2.0)
+        check_step_grads(od.rec[-1], f, it, "D", rtol=1e-4)
+        check_step_grads(og.rec[-1], f, it, "G", rtol=1e-4)
         # Adam's first steps move each weight by ~lr * sign(grad); weights whose
         # gradient is rounding noise (the attention vectors `a`, whose source
         # half cancels in the row softmax) may flip sign: allow 2*lr per step.
@@ -179,3 +182,27 @@ def test_train_step_fixture():
                 ref = f["it%d/%s/%s" % (it, tag, k)]
                 err = np.abs(v.numpy().astype(np.float64) - ref).max()
                 assert err <= 2 * lr * (it + 1) + 1e-5 * np.abs(ref).max(), (tag, k, err)
+
+
+@pytest.mark.parametrize("tag,pooling", [("none", None), ("pool", "pool_net")])
+def test_vanilla_generator_fixture(tag, pooling):
+    """Upstream Social-GAN generator (sgan-models / sgan-p-models families,
+    mlp_decoder_context of models.py:796-804 / :898) vs the reference run."""
+    f = npz("gen_fwd_vanilla.npz")
+    g = O.TrajectoryGenerator(8, 12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32, mlp_dim=64,
+                              noise_dim=(8,), noise_mix_type="global", pooling_type=pooling,
+                              pool_every_timestep=False, bottleneck_dim=8, batch_norm=False, graph="vanilla")
+    pre = tag + "/w/"
+    g.load_state_dict({k[len(pre):]: T(f[k]) for k in f.files if k.startswith(pre)})
+    for b in ("synth", "zara1", "eth"):
+        p = "%s/%s/" % (tag, b)
+        g.zero_grad()
+        y = g(T(f[p + "obs_traj"]), T(f[p + "obs_traj_rel"]), T(f[p + "seq_start_end"]), T(f[p + "obs_traj_g"]),
+              user_noise=T(f[p + "noise"]))
+        close(y.detach(), f[p + "out"])
+        (y * T(f[p + "dout"])).sum().backward()
+        n = 0
+        for k, q in g.named_parameters():
+            close(q.grad, f[p + "dw/" + k], rtol=1e-4, floor=grad_floor(f, p + "dw/"))
+            n += 1
+        assert n == (24 if pooling else 18)
