@@ -257,6 +257,17 @@ static int launch_lstm_bwd(const float* A, const float* Whh, const float* Wp, co
 
 using namespace sgg;
 
+extern "C" long long sgg_lstm_state_floats(int T, int B, int H, int which) {
+  if (T < 1 || B < 0 || (which != 0 && which != 1)) return -1;
+  if (lstm_mw_ok(H, B)) return lstm_mw_state_floats(T, B, H, which);
+  return which == 0 ? (long long)T * B * 4 * H : (long long)(T + 1) * B * H;
+}
+
+extern "C" int sgg_lstm_wpart_rows(int H, int B) {
+  if (B < 0) return -1;
+  return lstm_mw_ok(H, B) ? lstm_mw_wpart_rows(H, B) : 0;
+}
+
 extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
                             const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
                             float* c_all, float* act_all, float* rel_out, void* stream) {
@@ -265,9 +276,15 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_fwd: bad sizes T=%d B=%d", T, B);
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  // saved states are read back by the backward of the same family
+  // (sgg_lstm_state_floats): the four-wave family whenever lstm_mw_ok; the
+  // MFMA rollout only without saved states (inference / no-grad samples)
+  const bool mw = lstm_mw_ok(H, B);
+  if (act_all && mw)
+    return lstm_mw_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
   if (lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
     return lstm_fwd_mfma(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
-  if (lstm_mw_ok(H, B))
+  if (mw)
     return lstm_mw_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
   if (lstm_unit_ok(H, decoder) && !getenv("SGG_LSTM_ROWS"))
     return lstm_unit_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
@@ -280,16 +297,23 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   }
 }
 
-extern "C" int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all,
-                            const float* act_all, const float* dh_last, const float* dout, int T, int B, int H,
-                            int decoder, float* dG, float* dh0, float* drel_in, float* drel_tot, void* stream) {
-  SGG_CHECK_ARG(A && Whh && c_all && act_all && dG && drel_in, "sgg_lstm_bwd: null pointer");
+extern "C" int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
+                            const float* act_all, const float* rel, const float* rel_out, const float* dh_last,
+                            const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,
+                            float* drel_in, float* drel_tot, float* wpart, void* stream) {
+  SGG_CHECK_ARG(A && Whh && c_all && act_all && drel_in, "sgg_lstm_bwd: null pointer");
   SGG_CHECK_ARG(!decoder || (Wp && dout && drel_tot), "sgg_lstm_bwd: decoder needs Wp, dout, drel_tot");
   SGG_CHECK_ARG(T >= 1 && B >= 0, "sgg_lstm_bwd: bad sizes");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (lstm_mw_ok(H, B))
-    return lstm_mw_bwd(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, H, decoder, dG, dh0, drel_in, drel_tot, st);
+  if (lstm_mw_ok(H, B)) {
+    SGG_CHECK_ARG(!wpart || (h_all && rel && (!decoder || rel_out)),
+                  "sgg_lstm_bwd: weight gradients need h_all, rel (and rel_out for the decoder)");
+    return lstm_mw_bwd(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, H, decoder, dh0, drel_in,
+                       drel_tot, wpart, st);
+  }
+  SGG_CHECK_ARG(!wpart, "sgg_lstm_bwd: this (H=%d, B=%d) has no in-kernel weight gradient (sgg_lstm_wpart_rows = 0)", H, B);
+  SGG_CHECK_ARG(dG, "sgg_lstm_bwd: dG is required unless the in-kernel form is used");
   if (lstm_unit_ok(H, decoder) && !getenv("SGG_LSTM_ROWS"))
     return lstm_unit_bwd(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, H, decoder, dG, dh0, drel_in, drel_tot, st);
   switch (H) {

@@ -1,10 +1,10 @@
 // Fused LSTM sequences on v_mfma_f32_16x16x4_f32, one workgroup of four
 // waves per 16 peds (Encoder, reference sgan/models.py:62-92; Decoder
 // rollout :142-178).  Same contract as sgg_lstm_fwd / sgg_lstm_bwd
-// (include/sgg.h), dispatched by lstm.hip for batches of a few thousand peds
-// (the discriminator's real+fake sequences): one workgroup per CU, where
-// every step of the recurrence is latency-bound and the per-ped gate GEMM
-// (4H x H) has to be spread over all four SIMDs of the CU.
+// (include/sgg.h), dispatched by lstm.hip for the discriminator's H = 48
+// sequences (and every H with SGG_LSTM_MW=all): each step of the recurrence
+// is latency-bound and the per-ped gate GEMM (4H x H) is spread over all four
+// SIMDs of a CU.
 //
 // Forward step, wave g = gate block g (i | f | g | o):
 //   G_g^T (H x 16 peds) = [W_hh,g | A_g b_g] . [h_{t-1} | r_x r_y 1 0]^T
@@ -22,16 +22,35 @@
 // r_t is off the critical path: wave partials in LDS, summed by wave 0 after
 // the step's second barrier.
 //
+// Saved states for the backward are TILE-NATIVE (this family's private
+// layout, sized by sgg_lstm_state_floats): the gate activations of block b,
+// step t, gate g, slot j are the 64 floats act[((b T + t) 4 + g) KS + j][lane]
+// and the cells c[(b (T+1) + t) KS + j][lane] -- each a 256-byte line written
+// and read by one lane-linear instruction, i.e. exactly the LDS images of
+// the recurrence.  h_all stays in the public (T+1) x B x H layout (it is the
+// encoder's output).
+//
 // Backward step t (reverse): the slot owners turn dh_t (four gate-block
 // partials of W^T dG_{t+1} from LDS, + Wp^T dout_t for the decoder) into dG_t
 // with the saved activations (loaded a step ahead), writing dG_t to LDS
-// dgb[g][j][lane]; after a barrier wave g stores its gate block of dG_t
-// (float4 per lane) and computes that block's share of dh_{t-1}:
+// dgb[t & 1][g][j][lane]; after a barrier wave g computes its gate block's
+// share of dh_{t-1}:
 //   P_g (H x 16) = W_hh,g^T (H x H) . dG_g^T       (MU tiles x H / 4 k-steps)
 // written to LDS for the next step's owners; second barrier.  The decoder
 // uses the folded W' for t >= 1 (its input r_{t-1} depends on h_{t-1}) and
 // plain W_hh at t = 0 (dh0).  drel_in = A^T dG_t is a slot partial reduced
 // over the q lanes and the waves off the critical path.
+//
+// Weight gradients in the kernel (wpart != NULL): wave g accumulates, on the
+// MFMA, its gate block's
+//   [dW_hh,g | db_g | dA_g] += dG_g^T (H x 16 peds) . [h_{t-1} | 1 | r_x r_y]
+// (MU x (MU + 1) tiles, K = the block's 16 peds = 4 k-steps), the A operand
+// read straight from the double-buffered dG image in LDS, h_{t-1} staged
+// from h_all one step ahead.  The MFMAs of step t + 1 are issued at the top
+// of step t, ahead of that step's VALU work, so the matrix core runs them in
+// the shadow of the cell-gradient arithmetic.  dG never reaches HBM: the
+// workgroup writes one slab row [dW_hh (4H x H) | db (4H) | dA (4H x 2)]
+// that sgg_slab_reduce sums (fixed order).
 #include <stdlib.h>
 #include <string.h>
 
@@ -44,6 +63,7 @@ namespace {
 constexpr int kMwThreads = 256;   // four waves: one per gate block, one per SIMD
 constexpr int kMwPeds = 16;       // MFMA columns
 constexpr int kMwMaxT = 32;       // encoder inputs of up to this many steps are staged in LDS
+constexpr int kDgPitch = 68;      // dG image row pitch: conflict-free for the transposed A-operand read
 
 // v_exp_f32 / v_rcp_f32 forms (~2 ulp), as the other LSTM kernels.
 // s = 1: sigmoid(x); s = 2: tanh(x) = 2 sigmoid(2x) - 1 (the same
@@ -58,13 +78,23 @@ __device__ __forceinline__ float tanh_m(float x) {
 // unit held by slot j of lane quarter q
 __device__ __forceinline__ int slot_unit(int j, int q) { return 16 * (j >> 2) + 4 * q + (j & 3); }
 
+// h staging pitch: q * pitch mod 64 in {0, 16, 32, 48} keeps the B-operand
+// read (4 peds x 16 consecutive units) on distinct banks
+template <int H>
+struct MwCfg {
+  static constexpr int MU = H / 16, KS = H / 4, G4 = 4 * H;
+  static constexpr int HP = H <= 16 ? 16 : 80;
+  static constexpr int NHS = (kMwPeds * H + kMwThreads - 1) / kMwThreads;   // staged h floats per thread
+  static constexpr int P = G4 * H + G4 + 2 * G4;                           // slab row floats
+};
+
 template <int H>
 __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
     const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
-    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out) {
-  constexpr int MU = H / 16, KS = H / 4, G4 = 4 * H;
+    float* __restrict__ h_all, float* __restrict__ c_tile, float* __restrict__ act_tile, float* __restrict__ rel_out) {
+  constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS;
   __shared__ float gate[4][KS][64];
   __shared__ float hb[KS][64];
   __shared__ float2 rpart[4][kMwPeds];
@@ -72,10 +102,11 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, c16 = lane & 15;
-  const int ped = blockIdx.x * kMwPeds + c16;
+  const int blk = blockIdx.x;
+  const int ped = blk * kMwPeds + c16;
   const bool valid = ped < B;
   const int pc = valid ? ped : B - 1;   // clamped: every load unconditional and in bounds
-  const bool save = act_all != nullptr;
+  const bool save = act_tile != nullptr;
 
   // [W_hh,g | A_g b_g] in registers, W_hh's columns in the permuted k order
   float w[MU][KS + 1], ak0[MU], ak1[MU];
@@ -95,9 +126,9 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     const float hv = h0 ? h0[(size_t)pc * H + u] : 0.f;
     c[i] = c0 ? c0[(size_t)pc * H + u] : 0.f;
     hb[j][lane] = hv;
-    if (valid && save) {
-      h_all[(size_t)ped * H + u] = hv;
-      c_all[(size_t)ped * H + u] = c[i];
+    if (save) {
+      if (valid) h_all[(size_t)ped * H + u] = hv;
+      c_tile[((size_t)blk * (T + 1) * KS + j) * 64 + lane] = c[i];
     }
     wp0[i] = decoder ? Wp[u] : 0.f;
     wp1[i] = decoder ? Wp[H + u] : 0.f;
@@ -107,7 +138,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
   if (staged)
     for (int e = threadIdx.x; e < 2 * kMwPeds * T; e += kMwThreads) {
       const int t = e / (2 * kMwPeds), p = (e >> 1) & (kMwPeds - 1), k = e & 1;
-      const int pp = blockIdx.x * kMwPeds + p;
+      const int pp = blk * kMwPeds + p;
       relseq[t][p][k] = pp < B ? rel[((size_t)t * B + pp) * 2 + k] : 0.f;
     }
   __syncthreads();
@@ -149,17 +180,15 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
 #pragma unroll
       for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][ks], hk[ks], acc[mu], 0, 0, 0);
 
+    float* at = save ? act_tile + (((size_t)blk * T + t) * 4 + g) * KS * 64 + lane : nullptr;
 #pragma unroll
     for (int mu = 0; mu < MU; ++mu) {
-      float a[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        a[r] = gate_act(acc[mu][r], s);
-        gate[g][4 * mu + r][lane] = a[r];
+        const float a = gate_act(acc[mu][r], s);
+        gate[g][4 * mu + r][lane] = a;
+        if (save) at[(4 * mu + r) * 64] = a;   // lane-linear 256-byte line per slot
       }
-      if (valid && save)
-        *reinterpret_cast<float4*>(act_all + ((size_t)t * B + ped) * G4 + g * H + 16 * mu + 4 * q) =
-            make_float4(a[0], a[1], a[2], a[3]);
     }
     lds_barrier();
 
@@ -172,11 +201,8 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
       c[i] = fmaf(fg, c[i], ig * gg);
       const float h = og * tanh_m(c[i]);
       hb[j][lane] = h;
-      if (valid && (save || t == T - 1)) {
-        const size_t o = ((size_t)(save ? t + 1 : T) * B + ped) * H + slot_unit(j, q);
-        h_all[o] = h;
-        c_all[o] = c[i];
-      }
+      if (valid && (save || t == T - 1)) h_all[((size_t)(save ? t + 1 : T) * B + ped) * H + slot_unit(j, q)] = h;
+      if (save) c_tile[(((size_t)blk * (T + 1) + t + 1) * KS + j) * 64 + lane] = c[i];
       px = fmaf(wp0[i], h, px);
       py = fmaf(wp1[i], h, py);
     }
@@ -199,19 +225,25 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
 template <int H>
 __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Whh, const float* __restrict__ Wp,
-    const float* __restrict__ c_all, const float* __restrict__ act_all, const float* __restrict__ dh_last,
-    const float* __restrict__ dout, int T, int B, int decoder, float* __restrict__ dG, float* __restrict__ dh0,
-    float* __restrict__ drel_in, float* __restrict__ drel_tot) {
-  constexpr int MU = H / 16, KS = H / 4, G4 = 4 * H;
-  __shared__ float dgb[4][KS][64];
+    const float* __restrict__ h_all, const float* __restrict__ c_tile, const float* __restrict__ act_tile,
+    const float* __restrict__ rel, const float* __restrict__ rel_out, const float* __restrict__ dh_last,
+    const float* __restrict__ dout, int T, int B, int decoder, float* __restrict__ dh0, float* __restrict__ drel_in,
+    float* __restrict__ drel_tot, float* __restrict__ wpart) {
+  constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
+  constexpr int NHS = MwCfg<H>::NHS, P = MwCfg<H>::P;
+  __shared__ float dgb[2][4][KS][kDgPitch];
   __shared__ float part[4][KS][64];
   __shared__ float2 fbp[4][kMwPeds];
+  __shared__ float hs[2][kMwPeds][HP];
+  __shared__ float rs[2][kMwPeds][2];
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, c16 = lane & 15;
-  const int ped = blockIdx.x * kMwPeds + c16;
+  const int blk = blockIdx.x;
+  const int ped = blk * kMwPeds + c16;
   const bool valid = ped < B;
   const int pc = valid ? ped : B - 1;
+  const bool wgrad = wpart != nullptr;
 
   // W_hh,g^T in registers: wt[mu][ks] = W_hh[g H + slot_unit(ks, q)][16 mu + c16]
   // (decoder: the folded W' = W_hh + A Wp for t >= 1, plain W_hh kept for t = 0)
@@ -245,19 +277,20 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
   }
 
   // saved activations and cells of the owned slots (and the decoder's output
-  // gradient), one step ahead
+  // gradient), one step ahead; tile-native, lane-linear
   float ni[MU], nf[MU], ng[MU], no[MU], nc[MU], ncp[MU], nd0 = 0.f, nd1 = 0.f;
   auto load_step = [&](int t) {
+    const float* ab = act_tile + ((size_t)blk * T + t) * 4 * KS * 64 + lane;
+    const float* cb = c_tile + ((size_t)blk * (T + 1) + t) * KS * 64 + lane;
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
-      const int u = slot_unit(g * MU + i, q);
-      const float* ab = act_all + ((size_t)t * B + pc) * G4 + u;
-      ni[i] = ab[0];
-      nf[i] = ab[H];
-      ng[i] = ab[2 * H];
-      no[i] = ab[3 * H];
-      nc[i] = c_all[((size_t)(t + 1) * B + pc) * H + u];
-      ncp[i] = c_all[((size_t)t * B + pc) * H + u];
+      const int j = g * MU + i;
+      ni[i] = ab[(0 * KS + j) * 64];
+      nf[i] = ab[(1 * KS + j) * 64];
+      ng[i] = ab[(2 * KS + j) * 64];
+      no[i] = ab[(3 * KS + j) * 64];
+      nc[i] = cb[(KS + j) * 64];
+      ncp[i] = cb[j * 64];
     }
     if (decoder) {
       const float2 dv = *reinterpret_cast<const float2*>(dout + ((size_t)t * B + pc) * 2);
@@ -265,10 +298,67 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
       nd1 = dv.y;
     }
   };
+
+  // weight-gradient operands of step t: h_{t-1} = h_all[t] and the step input
+  // r_in(t) of the block's 16 peds, fetched one step ahead, staged in LDS
+  float hv[NHS];
+  float rv = 0.f;
+  auto stage_load = [&](int t) {
+#pragma unroll
+    for (int m = 0; m < NHS; ++m) {
+      const int e = threadIdx.x + m * kMwThreads;
+      const int p = min(e / H, kMwPeds - 1), u = e % H;
+      hv[m] = h_all[((size_t)t * B + min(blk * kMwPeds + p, B - 1)) * H + u];
+    }
+    if (threadIdx.x < 2 * kMwPeds) {
+      const int p = threadIdx.x >> 1, k = threadIdx.x & 1;
+      const int pp = min(blk * kMwPeds + p, B - 1);
+      rv = !decoder ? rel[((size_t)t * B + pp) * 2 + k]
+                    : (t == 0 ? rel[(size_t)pp * 2 + k] : rel_out[((size_t)(t - 1) * B + pp) * 2 + k]);
+    }
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int m = 0; m < NHS; ++m) {
+      const int e = threadIdx.x + m * kMwThreads;
+      if (e < kMwPeds * H) hs[buf][e / H][e % H] = hv[m];
+    }
+    if (threadIdx.x < 2 * kMwPeds) rs[buf][threadIdx.x >> 1][threadIdx.x & 1] = rv;
+  };
+  floatx4 dw[MU][MU + 1];
+#pragma unroll
+  for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+    for (int nu = 0; nu <= MU; ++nu) dw[mu][nu] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // dw[mu][nu] += dG_g^T (units 16 mu..) x [h | 1 r_x r_y] (cols 16 nu..) over the 16 peds
+  auto dw_accum = [&](int buf) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int p = 4 * kk + q;
+      float bh[MU + 1];
+#pragma unroll
+      for (int nu = 0; nu < MU; ++nu) bh[nu] = hs[buf][p][16 * nu + c16];
+      bh[MU] = c16 == 0 ? 1.f : c16 == 1 ? rs[buf][p][0] : c16 == 2 ? rs[buf][p][1] : 0.f;
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu) {
+        const float a = dgb[buf][g][4 * mu + (c16 & 3)][((c16 >> 2) << 4) + p];
+#pragma unroll
+        for (int nu = 0; nu <= MU; ++nu) dw[mu][nu] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bh[nu], dw[mu][nu], 0, 0, 0);
+      }
+    }
+  };
+
   load_step(T - 1);
+  if (wgrad) stage_load(T - 1);
   float din_x = 0.f, din_y = 0.f;   // drel_in[t + 1] (wave 0, q = 0 lanes)
 
   for (int t = T - 1; t >= 0; --t) {
+    const int cur = t & 1;
+    if (wgrad) {
+      if (t < T - 1) dw_accum(cur ^ 1);   // step t + 1: its dG image and h_t, in the VALU shadow below
+      stage_store(cur);                  // h_{t-1}, r_in(t) for step t (read after this step's barriers)
+      if (t > 0) stage_load(t - 1);
+    }
     const float d0 = nd0, d1 = nd1;
     float ci[MU], cf[MU], cg[MU], co[MU], cc[MU], ccp[MU];
 #pragma unroll
@@ -294,14 +384,16 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
       const float d_o = dhv * tc;
       const float dct = fmaf(dhv * og, 1.f - tc * tc, dc[i]);
       dc[i] = dct * fg;
-      const float vi = dct * gg * ig * (1.f - ig);
-      const float vf = dct * ccp[i] * fg * (1.f - fg);
-      const float vg = dct * ig * (1.f - gg * gg);
-      const float vo = d_o * og * (1.f - og);
-      dgb[0][j][lane] = vi;
-      dgb[1][j][lane] = vf;
-      dgb[2][j][lane] = vg;
-      dgb[3][j][lane] = vo;
+      // a padded ped (last block) carries no gradient: its dG is zero, so it
+      // adds nothing to the weight gradients
+      const float vi = keep_if(dct * gg * ig * (1.f - ig), valid);
+      const float vf = keep_if(dct * ccp[i] * fg * (1.f - fg), valid);
+      const float vg = keep_if(dct * ig * (1.f - gg * gg), valid);
+      const float vo = keep_if(d_o * og * (1.f - og), valid);
+      dgb[cur][0][j][lane] = vi;
+      dgb[cur][1][j][lane] = vf;
+      dgb[cur][2][j][lane] = vg;
+      dgb[cur][3][j][lane] = vo;
       f0 = fmaf(aa0[i][3], vo, fmaf(aa0[i][2], vg, fmaf(aa0[i][1], vf, fmaf(aa0[i][0], vi, f0))));
       f1 = fmaf(aa1[i][3], vo, fmaf(aa1[i][2], vg, fmaf(aa1[i][1], vf, fmaf(aa1[i][0], vi, f1))));
     }
@@ -312,10 +404,10 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     if (q == 0) fbp[g][c16] = make_float2(f0, f1);
     lds_barrier();
 
-    // gate block g of dG_t: global store + its share of dh_{t-1}
+    // gate block g of dG_t: its share of dh_{t-1}
     float bk[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) bk[ks] = dgb[g][ks][lane];
+    for (int ks = 0; ks < KS; ++ks) bk[ks] = dgb[cur][g][ks][lane];
     if (decoder && t == 0) {
 #pragma unroll
       for (int mu = 0; mu < MU; ++mu)
@@ -329,12 +421,6 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[mu][ks], bk[ks], acc[mu], 0, 0, 0);
-    if (valid) {
-#pragma unroll
-      for (int mu = 0; mu < MU; ++mu)
-        *reinterpret_cast<float4*>(dG + ((size_t)t * B + ped) * G4 + g * H + 16 * mu + 4 * q) =
-            make_float4(bk[4 * mu], bk[4 * mu + 1], bk[4 * mu + 2], bk[4 * mu + 3]);
-    }
     if (g == 0 && q == 0) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
       const float2 r0 = fbp[0][c16], r1 = fbp[1][c16], r2 = fbp[2][c16], r3 = fbp[3][c16];
       const float sx = (r0.x + r1.x) + (r2.x + r3.x), sy = (r0.y + r1.y) + (r2.y + r3.y);
@@ -358,6 +444,22 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
       dh0[(size_t)ped * H + slot_unit(j, q)] = (part[0][j][lane] + part[1][j][lane]) + (part[2][j][lane] + part[3][j][lane]);
     }
   }
+  if (wgrad) {
+    dw_accum(0);   // step 0 (its dG image and h_{-1} = h0 are visible since the loop's last barriers)
+    // slab row of this workgroup: D tile (mu, nu) holds rows g H + 16 mu + 4 q + r, cols 16 nu + c16
+    float* row = wpart + (size_t)blk * P;
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = g * H + 16 * mu + 4 * q + r;
+#pragma unroll
+        for (int nu = 0; nu < MU; ++nu) row[(size_t)gr * H + 16 * nu + c16] = dw[mu][nu][r];
+        if (c16 == 0) row[G4 * H + gr] = dw[mu][MU][r];                        // db
+        else if (c16 <= 2) row[G4 * H + G4 + 2 * gr + (c16 - 1)] = dw[mu][MU][r];   // dA (x, y)
+      }
+    }
+  }
 }
 
 template <int H>
@@ -371,12 +473,12 @@ int launch_fwd(const float* rel, const float* A, const float* Whh, const float* 
 }
 
 template <int H>
-int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all, const float* act_all,
-               const float* dh_last, const float* dout, int T, int B, int decoder, float* dG, float* dh0, float* drel_in,
-               float* drel_tot, hipStream_t st) {
+int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
+               const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
+               int T, int B, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart, hipStream_t st) {
   const int grid = (B + kMwPeds - 1) / kMwPeds;
-  hipLaunchKernelGGL(lstm_mw_bwd_kernel<H>, dim3(grid), dim3(kMwThreads), 0, st, A, Whh, Wp, c_all, act_all, dh_last,
-                     dout, T, B, decoder, dG, dh0, drel_in, drel_tot);
+  hipLaunchKernelGGL(lstm_mw_bwd_kernel<H>, dim3(grid), dim3(kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all,
+                     rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart);
   SGG_RETURN_LAUNCH("sgg_lstm_bwd");
 }
 
@@ -384,13 +486,25 @@ int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* c
 
 // Policy: H = 48 / 64 (the discriminator; the unit-per-thread kernels are
 // register-bound there).  SGG_LSTM_MW=all also routes H = 16 / 32 here,
-// SGG_LSTM_MW=0 disables this form (kernel comparisons, tools/).
+// SGG_LSTM_MW=0 disables this form (kernel comparisons, tools/).  The same
+// predicate picks the forward (when it saves states) and the backward, so
+// the tile-native saved layout is always read by the kernel that wrote it.
 bool lstm_mw_ok(int H, int B) {
   (void)B;
   const char* e = getenv("SGG_LSTM_MW");
   if (e && strcmp(e, "0") == 0) return false;
   if (e && strcmp(e, "all") == 0) return H == 16 || H == 32 || H == 48 || H == 64;
   return H == 48 || H == 64;
+}
+
+long long lstm_mw_state_floats(int T, int B, int H, int which) {
+  const long long padded = (long long)(B + kMwPeds - 1) / kMwPeds * kMwPeds;
+  return which == 0 ? (long long)T * padded * 4 * H : (long long)(T + 1) * padded * H;
+}
+
+int lstm_mw_wpart_rows(int H, int B) {
+  (void)H;
+  return (B + kMwPeds - 1) / kMwPeds;
 }
 
 int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
@@ -404,14 +518,15 @@ int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float*
   }
 }
 
-int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all, const float* act_all,
-                const float* dh_last, const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,
-                float* drel_in, float* drel_tot, hipStream_t st) {
+int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
+                const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
+                int T, int B, int H, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart,
+                hipStream_t st) {
   switch (H) {
-    case 16: return launch_bwd<16>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
-    case 32: return launch_bwd<32>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
-    case 48: return launch_bwd<48>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
-    default: return launch_bwd<64>(A, Whh, Wp, c_all, act_all, dh_last, dout, T, B, decoder, dG, dh0, drel_in, drel_tot, st);
+    case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
+    case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
+    case 48: return launch_bwd<48>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
+    default: return launch_bwd<64>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
   }
 }
 

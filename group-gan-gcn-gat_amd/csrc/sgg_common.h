@@ -80,17 +80,23 @@ __attribute__((visibility("hidden"))) int lstm_unit_bwd(const float* A, const fl
                                                         float* dh0, float* drel_in, float* drel_tot, hipStream_t st);
 
 // lstm_mw.hip: MFMA LSTM sequence kernels, one workgroup of four waves (one
-// per gate block) per 16 peds; dispatched first by sgg_lstm_fwd / _bwd; internal
+// per gate block) per 16 peds, tile-native saved states, weight gradients
+// accumulated in the backward kernel; dispatched first by sgg_lstm_fwd /
+// _bwd; internal
 __attribute__((visibility("hidden"))) bool lstm_mw_ok(int H, int B);
+__attribute__((visibility("hidden"))) long long lstm_mw_state_floats(int T, int B, int H, int which);
+__attribute__((visibility("hidden"))) int lstm_mw_wpart_rows(int H, int B);
 __attribute__((visibility("hidden"))) int lstm_mw_fwd(const float* rel, const float* A, const float* Whh,
                                                       const float* bias, const float* h0, const float* c0,
                                                       const float* Wp, const float* bp, int T, int B, int H,
                                                       int decoder, float* h_all, float* c_all, float* act_all,
                                                       float* rel_out, hipStream_t st);
 __attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp,
-                                                      const float* c_all, const float* act_all, const float* dh_last,
-                                                      const float* dout, int T, int B, int H, int decoder, float* dG,
-                                                      float* dh0, float* drel_in, float* drel_tot, hipStream_t st);
+                                                      const float* h_all, const float* c_all, const float* act_all,
+                                                      const float* rel, const float* rel_out, const float* dh_last,
+                                                      const float* dout, int T, int B, int H, int decoder,
+                                                      float* dh0, float* drel_in, float* drel_tot, float* wpart,
+                                                      hipStream_t st);
 
 // v if keep else +0.f, as a bit mask: a plain `keep ? v : 0` lets the
 // compiler sink the load of v into an exec-masked branch that waits for it

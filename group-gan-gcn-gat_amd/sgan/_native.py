@@ -61,7 +61,9 @@ SIGNATURES = {
     "sgg_fold_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "sgg_fold_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "sgg_lstm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
-    "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "sgg_lstm_state_floats": (ctypes.c_longlong, [_i, _i, _i, _i]),
+    "sgg_lstm_wpart_rows": (_i, [_i, _i]),
+    "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
     "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p]),
     "sgg_bce_bwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p]),
     "sgg_gatenc_param_size": (_i, [_i]),

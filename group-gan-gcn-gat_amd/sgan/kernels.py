@@ -643,7 +643,11 @@ class _LSTMSeq(torch.autograd.Function):
     """Fused LSTM sequence on the raw parameters of Linear(2, E) + LSTM(E, H)
     (+ hidden2pos for the decoder): the embedding fold is one launch
     (sgg_fold_fwd), the T-step recurrence another; the backward returns
-    the raw parameters' gradients (sgg_fold_bwd maps dA, dbias back)."""
+    the raw parameters' gradients (sgg_fold_bwd maps dA, dbias back).  Where
+    the library accumulates the weight gradients inside the backward kernel
+    (sgg_lstm_wpart_rows > 0) the gate gradients never reach HBM: one slab
+    row per workgroup, summed by sgg_slab_reduce; otherwise dG is written
+    and reduced by sgg_xtw."""
 
     @staticmethod
     def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save):
@@ -654,8 +658,10 @@ class _LSTMSeq(torch.autograd.Function):
         dev = rel.device
         A, bias = fold_fwd(W_ih, We, be, b_ih, b_hh)
         h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
-        c_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
-        act = torch.empty(T, B, 4 * H, device=dev, dtype=torch.float32) if save else None
+        # saved states in the layout of the kernel family (H, B) picks
+        c_all = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 1)), device=dev, dtype=torch.float32)
+        act = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 0)), device=dev, dtype=torch.float32) \
+            if save else None
         rel_out = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
         Whh = W_hh.contiguous()
         h0c = h0.contiguous() if h0 is not None else None
@@ -679,9 +685,15 @@ class _LSTMSeq(torch.autograd.Function):
         decoder, T, B, H, has_h0 = ctx.meta
         rel, W_ih, We, be, A, Whh, Wp, h_all, c_all, act, rel_out = ctx.saved_tensors
         dev = rel.device
-        dG = torch.empty(T, B, 4 * H, device=dev, dtype=torch.float32)
+        need = ctx.needs_input_grad
+        wgrad = any(need[1:7])
+        rows = int(lib.sgg_lstm_wpart_rows(H, B))
+        G4 = 4 * H
+        P = G4 * H + G4 + 2 * G4
+        wpart = torch.empty(rows, P, device=dev, dtype=torch.float32) if (wgrad and rows > 0) else None
+        dG = torch.empty(T, B, G4, device=dev, dtype=torch.float32) if rows == 0 else None
         drel_in = torch.empty(T, B, 2, device=dev, dtype=torch.float32)
-        dh0 = torch.empty(B, H, device=dev, dtype=torch.float32)
+        dh0 = torch.empty(B, H, device=dev, dtype=torch.float32) if has_h0 else None
         drel_tot = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
         if decoder:
             dout = drel_out.contiguous() if drel_out is not None else torch.zeros(T, B, 2, device=dev)
@@ -689,17 +701,23 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             dout = None
             dhl = dh_last.contiguous() if dh_last is not None else None
-        N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(c_all), N.ptr(act), N.ptr(dhl), N.ptr(dout),
-                                 T, B, H, int(decoder), N.ptr(dG), N.ptr(dh0), N.ptr(drel_in), N.ptr(drel_tot),
-                                 N.stream_ptr()), "sgg_lstm_bwd")
-        dGf = dG.view(T * B, 4 * H)
-        need = ctx.needs_input_grad
+        N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel),
+                                 N.ptr(rel_out), N.ptr(dhl), N.ptr(dout), T, B, H, int(decoder), N.ptr(dG), N.ptr(dh0),
+                                 N.ptr(drel_in), N.ptr(drel_tot), N.ptr(wpart), N.stream_ptr()), "sgg_lstm_bwd")
         dW_ih = dW_hh = db_ih = db_hh = dWe = dbe = dWp = dbp = None
-        if any(need[1:7]):
-            # dW_hh = dG^T h_{t-1} (4H x H, transposed reduction), dbias = sum dG
-            dW_hh, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True, trans_c=True)
-            rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0) if decoder else rel
-            dA = xtw(rel_in.reshape(T * B, 2), dGf, trans_c=True)                   # 4H x 2
+        if wgrad:
+            if wpart is not None:
+                flat = torch.empty(P, device=dev, dtype=torch.float32)     # [dW_hh | dbias | dA]
+                N.check(lib.sgg_slab_reduce(N.ptr(wpart), rows, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+                dW_hh = flat[:G4 * H].view(G4, H)
+                dbias = flat[G4 * H:G4 * H + G4]
+                dA = flat[G4 * H + G4:].view(G4, 2)
+            else:
+                dGf = dG.view(T * B, G4)
+                # dW_hh = dG^T h_{t-1} (4H x H, transposed reduction), dbias = sum dG
+                dW_hh, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True, trans_c=True)
+                rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0) if decoder else rel
+                dA = xtw(rel_in.reshape(T * B, 2), dGf, trans_c=True)                   # 4H x 2
             db_hh = torch.empty_like(dbias)          # two leaves: no shared gradient storage
             dW_ih, dWe, dbe = fold_bwd(W_ih, We, be, dA, dbias, dbias_copy=db_hh)
             db_ih = dbias

@@ -229,10 +229,14 @@ int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const f
  * encoder (decoder = 0): r_t = rel[t] (T x B x 2); h_{-1} = h0, c_{-1} = c0 (NULL = 0).
  * decoder (decoder = 1): r_0 = rel (B x 2), r_t = Wp h_{t-1} + bp (hidden2pos) for
  *   t >= 1; rel_out[t] = Wp h_t + bp (T x B x 2) is the predicted displacement.
- * H in {16, 32, 48, 64}.  Outputs h_all, c_all: (T+1) x B x H with index 0 the
- * initial state; act_all (T x B x 4H, gate activations i|f|g|o) may be NULL
- * (inference: then only h_all[T], c_all[T] are written) and is required by the
- * backward. */
+ * H in {16, 32, 48, 64}.  h_all: (T+1) x B x H with index 0 the initial state.
+ * act_all (gate activations) and c_all (cells) are the saved states the
+ * backward reads, in a layout private to the kernel family the dispatcher
+ * picks for (H, B): allocate sgg_lstm_state_floats(T, B, H, 0) floats for
+ * act_all and (.., 1) for c_all.  act_all may be NULL (inference: then only
+ * h_all[T] is written) and is required by the backward.
+ */
+long long sgg_lstm_state_floats(int T, int B, int H, int which);
 int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float* bias,
                  const float* h0, const float* c0, const float* Wp, const float* bp, int T, int B, int H,
                  int decoder, float* h_all, float* c_all, float* act_all, float* rel_out,
@@ -240,15 +244,27 @@ int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float
 
 /* Backward of sgg_lstm_fwd (BPTT).  encoder: dh_last = dL/dh_{T-1} (B x H, may
  * be NULL); decoder: dout = dL/drel_out (T x B x 2) (the decoder feedback
- * r_t -> step t+1 is included).  Writes dG (T x B x 4H, gradient of the gate
- * pre-activations), drel_in (T x B x 2, dL/dr_t of the step inputs), dh0
- * (B x H, may be NULL; no gradient is produced for c0) and, for the decoder, drel_tot (T x B x 2, total
- * dL/d rel_out[t]).  Parameter gradients are outer-product sums over (t, ped)
- * of these and the saved states -- plain GEMMs left to the caller. */
-int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* c_all,
-                 const float* act_all, const float* dh_last, const float* dout, int T, int B,
-                 int H, int decoder, float* dG, float* dh0, float* drel_in, float* drel_tot,
-                 void* stream);
+ * r_t -> step t+1 is included).  Writes drel_in (T x B x 2, dL/dr_t of the
+ * step inputs), dh0 (B x H, may be NULL; no gradient is produced for c0)
+ * and, for the decoder, drel_tot (T x B x 2, total dL/d rel_out[t]).
+ * Weight gradients, two forms:
+ *  - sgg_lstm_wpart_rows(H, B) > 0 (the four-wave MFMA family): pass wpart
+ *    (rows x (4H*H + 4H + 8H) floats) and the kernel accumulates, per
+ *    workgroup, one slab row [dW_hh (4H x H) | dbias (4H) | dA (4H x 2)] =
+ *    sum over its peds and all steps of dG_t^T [h_{t-1} | 1 | r_in(t)]
+ *    (h_all and rel -- and rel_out for the decoder, r_in(t) = rel_out[t-1] --
+ *    are read for that); sgg_slab_reduce sums the rows.  wpart = NULL: input
+ *    gradients only (frozen weights).  dG is not used (may be NULL).
+ *  - otherwise dG (T x B x 4H, gradient of the gate pre-activations) is
+ *    written and the caller forms the outer-product sums (sgg_xtw); wpart
+ *    must be NULL.
+ * dWp / dbp of the decoder are X^T sums of drel_tot and h_all, left to the
+ * caller in both forms. */
+int sgg_lstm_wpart_rows(int H, int B);
+int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
+                 const float* act_all, const float* rel, const float* rel_out, const float* dh_last,
+                 const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,
+                 float* drel_in, float* drel_tot, float* wpart, void* stream);
 
 /* ------------------------------------------------------------------------
  * Adversarial loss (losses.py:5-21 bce_loss; gan_d_loss :36-49 sums two of
