@@ -1,23 +1,37 @@
 """Benchmark: train-scenes/s of the group-aware Social-GAN hot path on MI355X.
 
 One step = one reference training iteration (scripts/train.py defaults, GAT
-generator): D-step + G-step (best_k = 20) with Adam updates, on a batch of
-`--batch` synthetic 20-ped scenes per GPU (obs 8 / pred 12), inputs resident
-in HBM before the timed region.  Multi-GPU: one process per GPU launched by
-torch.distributed.run, scenes sharded (weak scaling), RCCL all-reduce of the
-G/D gradients once per optimizer step.
+generator): D-step + G-step (best_k = 20) with Adam updates, on synthetic
+20-ped scenes (obs 8 / pred 12), inputs resident in HBM before the timed
+region.
+
+  N = 1 (default): BASELINE configs[1]'s shape, 64 scenes on one GPU.
+  N > 1: BASELINE configs[3], the 4096-scene global batch split over the N
+         GPUs (4096 / N scenes per GPU, strong scaling): one process per GPU
+         (`--gpus N` spawns them through torch.distributed.run when it is
+         not already running under it), scenes sharded, RCCL all-reduce of the
+         G / D gradients once per optimizer step.  The N = 1 line carries the
+         same 4096-scene workload on one GPU as `scaling_reference`, the
+         denominator of that strong-scaling curve.
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline     the dominant kernel (by summed device time over the timed
-               steps, measured with HIP events on its launch stream) against
-               the fp32 peak; `achieved` = algorithmic FLOP per launch / avg
-               launch time (FLOP model in DESIGN.md);
-  cpu_baseline the CPU oracle (reference formulation, per-scene loops) timed
-               on this host for a bounded sample of the same workload.
+  kernels      every instrumented kernel's device time per iteration
+               (HIP events on its launch stream, LaunchTimer in sgan/kernels.py);
+  roofline     the dominant one (most device time per iteration) against its
+               bound: the fp32 MFMA peak when its arithmetic intensity is
+               above the ridge, HBM otherwise; `achieved` = algorithmic FLOP
+               (or bytes) per launch / average launch time (work models in
+               DESIGN.md section 4); `traffic` = PMC-measured HBM bytes per
+               launch of that kernel (profiles/, tools/pmc_traffic.py);
+  cpu_baseline the CPU oracle (reference formulation) timed on this host for a
+               bounded sample of the same workload, validated against the
+               real reference in the build container (ref_cpu_timing.json).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,6 +45,10 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "scenes/sec (obs8/pred12, 20 peds) at 1/2/4/8 GPUs; ADE/FDE vs ref"
 FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 dense (vector == f32 MFMA), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md
+RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)   # FLOP / byte
+CONFIG4_GLOBAL = 4096      # BASELINE configs[3]: synthetic 20-ped, batch 4096, 8 x MI355X
+TRAFFIC_TABLE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
 def build_models(seed, graph="gat"):
@@ -65,32 +83,137 @@ def cpu_baseline(batch_scenes, n_peds, iters=2, threads=None):
         O.discriminator_step(O.Args, b, g, d, od)
         O.generator_step(O.Args, b, g, d, og)
     dt = time.perf_counter() - t0
+    val = ""
+    vpath = os.path.join(ROOT, "tests", "golden", "ref_cpu_timing.json")
+    if os.path.exists(vpath):
+        v = json.load(open(vpath))
+        val = ("; validated in the build container (%s, %d threads, batch %d): reference %.2f vs oracle %.2f "
+               "scenes/s, ratio %.2f (tests/golden/ref_cpu_timing.json)"
+               % (v.get("cpu", "?"), v["threads"], v["batch"], v["reference_scenes_per_s"],
+                  v["oracle_scenes_per_s"], v["oracle_over_reference"]))
     return {"value": round(batch_scenes * iters / dt, 3), "unit": "scenes/s", "cores": threads, "kind": "port",
             "sample": "%d train iterations (D-step + G-step, best_k=20) on %d x %d-ped synthetic scenes, oracle/"
-                      "sgan_oracle.py reference formulation, torch CPU fp32, %d threads (%.1f s)"
-                      % (iters, batch_scenes, n_peds, threads, dt)}
+                      "sgan_oracle.py reference formulation, torch CPU fp32, %d threads (%.1f s)%s"
+                      % (iters, batch_scenes, n_peds, threads, dt, val)}
 
 
-def pool_flops(sc, bn):
-    """Algorithmic FLOP of one sgg_pool_fwd launch: per (i, j) pair 512 hidden
-    units x (2 FMA for A.r + bn FMA for layer 2) = 512 * (4 + 2 bn)."""
-    sizes = np.diff(sc.host_off)
-    return float((sizes.astype(np.float64) ** 2).sum()) * 512.0 * (4 + 2 * bn)
-
-
-def pmc_traffic(kname, key):
-    """HBM bytes per launch of the roofline kernel from the committed PMC
-    passes (profiles/r01_pool_traffic.json, written by tools/pmc_traffic.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench, with the
-    gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or None when that
-    file holds no entry for this exact launch shape."""
-    path = os.path.join(ROOT, "profiles", "r01_pool_traffic.json")
-    if not os.path.exists(path):
+def traffic_lookup(name, key):
+    """HBM bytes per launch of (kernel, launch shape) from the committed PMC
+    table (tools/pmc_traffic.py: separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench with the gfx950 corrections of
+    MI355X_MICROARCH.md), or None when the table has no such launch."""
+    if not os.path.exists(TRAFFIC_TABLE):
         return None
-    with open(path) as f:
-        tab = json.load(f)
-    ent = tab.get("%s|%s" % (kname, list(key)))
+    tab = json.load(open(TRAFFIC_TABLE))
+    ent = tab.get("%s|%s" % (name, list(key[1:])))
     return None if ent is None else ent["hbm_bytes"]
+
+
+def kernel_table(timed, n_it):
+    """{name: per-iteration stats} from LaunchTimer.replay records."""
+    agg = {}
+    for key, r in timed.items():
+        a = agg.setdefault(r["name"], dict(us_per_iter=0.0, launches_per_iter=0.0, flop=0.0, bytes=0.0, shapes=[]))
+        per_it = r["launches"] / n_it
+        a["us_per_iter"] += per_it * r["ms"] * 1e3
+        a["launches_per_iter"] += per_it
+        a["flop"] += per_it * r["flop"]
+        a["bytes"] += per_it * r["bytes"]
+        a["shapes"].append((key, r, per_it))
+    return agg
+
+
+def roofline_of(name, a):
+    us = a["us_per_iter"]
+    ai = a["flop"] / max(a["bytes"], 1.0)
+    if ai >= RIDGE:
+        achieved, peak, unit, bound = a["flop"] / (us * 1e-6) / 1e12, FP32_PEAK_TFLOPS, "TFLOP/s", "mfma"
+    else:
+        achieved, peak, unit, bound = a["bytes"] / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
+    # the launch shape carrying most of the kernel's time: its PMC traffic
+    key, r, per_it = max(a["shapes"], key=lambda s: s[2] * s[1]["ms"])
+    return {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": traffic_lookup(name, key),
+            "kernel": name, "launches_per_iteration": round(a["launches_per_iter"], 2),
+            "avg_launch_us": round(us / a["launches_per_iter"], 2), "us_per_iteration": round(us, 1),
+            "flop_per_launch": a["flop"] / a["launches_per_iter"],
+            "algorithmic_bytes_per_launch": a["bytes"] / a["launches_per_iter"],
+            "arithmetic_intensity": round(ai, 2), "ridge": round(RIDGE, 2),
+            "traffic_launch": "%s %s (avg %.2f us, %.3g algorithmic B)" % (name, list(key[1:]), r["ms"] * 1e3,
+                                                                          r["bytes"]),
+            "note": "fp32 (f32 MFMA, same peak as VALU FMA); achieved = algorithmic work of the kernel's launches "
+                    "in one iteration / their summed device time (HIP events around back-to-back re-issues of each "
+                    "launch on its stream); traffic = PMC HBM bytes of the named launch (null if not profiled)"}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(n):
+    """Run this script under torch.distributed.run with one process per GPU.
+    The parent never initialises HIP (no torch.cuda call before this), and
+    starts the launcher as a child process (no exec from a GPU process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph):
+    from sgan.train_step import GraphedTrainer
+    if graph:
+        try:
+            gt = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, **kw)
+            return gt.step, True
+        except Exception as e:  # capture unsupported (e.g. a collective): eager
+            print("bench: graph capture failed (%s: %s); running eager" % (type(e).__name__, e), file=sys.stderr)
+            torch.cuda.synchronize()
+    return (lambda: trainer.step(batch, sc, batch_g, sc_g, **kw)), False
+
+
+def timed_run(step, steps, warmup, world, dev):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    return elapsed
+
+
+def setup(per_gpu, peds, rank, world, dev, graph_kind):
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import DataParallel, GanTrainer
+    g, d = build_models(0, graph_kind)
+    g, d = g.to(dev), d.to(dev)
+    trainer = GanTrainer(g, d, dp=DataParallel(), capturable=True)
+    # the reference feeds consecutive loader batches to the D-step and the
+    # G-step (scripts/train.py:279-297): two distinct synthetic batches
+    batch = synthetic_batch([peds] * per_gpu, seed=1000 + rank, device=dev)
+    batch_g = synthetic_batch([peds] * per_gpu, seed=5000 + rank, device=dev)
+    sc = SceneIndex.from_seq_start_end(batch[-1], dev)
+    sc_g = SceneIndex.from_seq_start_end(batch_g[-1], dev)
+    kw = dict(S_global=sc.S * world, B_global=sc.B * world, shard=(rank * sc.S, (rank + 1) * sc.S))
+    return trainer, batch, sc, batch_g, sc_g, kw
 
 
 def main():
@@ -98,17 +221,27 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="scenes per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="scenes per GPU (default: 64 at N = 1, BASELINE configs[1]; 4096 / N at N > 1, configs[3])")
     ap.add_argument("--peds", type=int, default=20)
     ap.add_argument("--graph-kind", dest="graph_kind", default="gat", choices=["gat", "gcn"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-scaling-reference", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="capture the iteration in a HIP graph (1) or run eager (0)")
     ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--pmc-target", type=int, default=0,
+                    help="after timing, re-issue the dominant kernel's main launch this many times (the LAST "
+                         "dispatches of that kernel in a rocprofv3 --pmc run; tools/pmc_traffic.py)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     # one process per GPU; SGG_BENCH_BACKEND=gloo (and more ranks than GPUs,
     # ranks sharing a device) is only for rehearsing the multi-rank path on a
     # one-GPU box -- the driver's runs use nccl (RCCL over xGMI)
@@ -121,95 +254,83 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus
 
     from sgan import kernels as K
-    from sgan.data.synthetic import synthetic_batch
-    from sgan.scene import SceneIndex
-    from sgan.train_step import DataParallel, GanTrainer, GraphedTrainer
 
-    g, d = build_models(0, args.graph_kind)
-    g, d = g.to(dev), d.to(dev)
-    trainer = GanTrainer(g, d, dp=DataParallel(), capturable=bool(args.graph))
-    # the reference feeds consecutive loader batches to the D-step and the
-    # G-step (scripts/train.py:279-297): two distinct synthetic batches
-    batch = synthetic_batch([args.peds] * args.batch, seed=1000 + rank, device=dev)
-    batch_g = synthetic_batch([args.peds] * args.batch, seed=5000 + rank, device=dev)
-    sc = SceneIndex.from_seq_start_end(batch[-1], dev)
-    sc_g = SceneIndex.from_seq_start_end(batch_g[-1], dev)
-    S_glob, B_glob = sc.S * world, sc.B * world
-    kw = dict(S_global=S_glob, B_global=B_glob, shard=(rank * sc.S, (rank + 1) * sc.S))
+    per_gpu = args.batch or (64 if world == 1 else CONFIG4_GLOBAL // world)
+    trainer, batch, sc, batch_g, sc_g, kw = setup(per_gpu, args.peds, rank, world, dev, args.graph_kind)
+    step, graphed = make_step(trainer, batch, sc, batch_g, sc_g, kw, args.graph)
+    elapsed = timed_run(step, args.steps, args.warmup, world, dev)
 
-    graphed = False
-    if args.graph:
-        try:
-            gt = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, **kw)
-            step = gt.step
-            graphed = True
-        except Exception as e:  # capture unsupported (e.g. a collective): eager
-            print("bench: graph capture failed (%s: %s); running eager" % (type(e).__name__, e), file=sys.stderr)
-            torch.cuda.synchronize()
-    if not graphed:
-        step = lambda: trainer.step(batch, sc, batch_g, sc_g, **kw)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-    # roofline of the pooling kernel: every sgg_pool_fwd launch of a few
-    # instrumented iterations on the same inputs is recorded (graph replays
-    # carry no events), then each distinct launch is re-issued back to back
-    # between HIP events on its launch stream (device-busy average duration);
-    # rocprofv3's kernel trace of the same command is the cross-check (profiles/)
+    # per-kernel device time: every instrumented launch of a few eager
+    # iterations on the same inputs is recorded (graph replays carry no
+    # events), then each distinct launch is re-issued back to back between
+    # HIP events on its launch stream; rocprofv3's kernel trace of the same
+    # command is the cross-check (profiles/)
     n_it = max(1, min(args.steps, 3))
-    K.pool_timer.start()
+    K.timer.start()
     for _ in range(n_it):
         trainer.step(batch, sc, batch_g, sc_g, **kw)
-    timed = K.pool_timer.replay(K.pool_timer.stop())
+    recs = K.timer.stop()
+    timed = K.timer.replay(recs)
+    agg = kernel_table(timed, n_it)
+    pmc_target = None
+    if args.pmc_target > 0 and rank == 0:
+        name, a = max(agg.items(), key=lambda kv: kv[1]["us_per_iter"])
+        key = max(a["shapes"], key=lambda s: s[2] * s[1]["ms"])[0]
+        fn = next(r[4] for r in recs if r[1] == key)
+        for _ in range(args.pmc_target):
+            fn()
+        torch.cuda.synchronize()
+        pmc_target = {"kernel": name, "shape": list(key[1:]), "reps": args.pmc_target}
+    del timed, recs
+
+    scaling_ref = None
+    if world == 1 and not args.no_scaling_reference and per_gpu != CONFIG4_GLOBAL:
+        # configs[3]'s 4096-scene global batch on this one GPU: the N = 1 point
+        # of the strong-scaling curve the N > 1 runs measure
+        tr4, b4, sc4, bg4, scg4, kw4 = setup(CONFIG4_GLOBAL, args.peds, 0, 1, dev, args.graph_kind)
+        st4, gr4 = make_step(tr4, b4, sc4, bg4, scg4, kw4, args.graph)
+        k4 = max(3, args.steps // 4)
+        e4 = timed_run(st4, k4, 2, 1, dev)
+        scaling_ref = {"global_batch": CONFIG4_GLOBAL, "n_gpus": 1, "steps": k4, "ms_per_step": round(e4 / k4 * 1e3, 3),
+                       "value": round(CONFIG4_GLOBAL / (e4 / k4), 2), "unit": "scenes/s", "hip_graph": gr4,
+                       "note": "BASELINE configs[3] workload on one GPU: strong-scaling efficiency at N GPUs = "
+                               "value(N) / (N * this value)"}
+        del tr4, b4, bg4, st4
 
     if rank == 0:
-        # dominant kernel: the pool forward launch with the most device time per iteration
-        key = max(timed, key=lambda k: timed[k][0] * timed[k][2])
-        n, fl, ms = timed[key]
-        kname = "sgg::pool_fwd_kernel<%d, %d, %d>" % key[:3]
-        achieved = fl / (ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": pmc_traffic(kname, key),
-                    "kernel": kname, "launches_per_iteration": round(n / n_it, 2),
-                    "avg_launch_us": round(ms * 1e3, 2), "flop_per_launch": fl,
-                    "note": "fp32 (f32 MFMA, same peak as VALU FMA); all pool forward launches per iteration "
-                            "[bn, gpw, unroll, scenes, peds]: %s" % {
-                                "%s" % list(k): {"per_iter": round(v[0] / n_it, 2), "avg_us": round(v[2] * 1e3, 2),
-                                                 "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 2)}
-                                for k, v in timed.items()}}
+        top = sorted(agg.items(), key=lambda kv: -kv[1]["us_per_iter"])
+        dom_name, dom = top[0]
+        roofline = roofline_of(dom_name, dom)
+        kernels = {n: {"us_per_iter": round(a["us_per_iter"], 1), "launches_per_iter": round(a["launches_per_iter"], 2),
+                       "GB/s": round(a["bytes"] / (a["us_per_iter"] * 1e-6) / 1e9, 1),
+                       "TFLOP/s": round(a["flop"] / (a["us_per_iter"] * 1e-6) / 1e12, 2)} for n, a in top[:10]}
         ms_step = elapsed / args.steps * 1e3
-        value = world * args.batch / (elapsed / args.steps)
+        value = world * per_gpu / (elapsed / args.steps)
         cpu = None
-        if not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.batch, args.peds, iters=args.cpu_iters)
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(per_gpu, args.peds, iters=args.cpu_iters)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "scenes/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights, SURVEY.md 8d recipe)",
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak" if world == 1 else "strong", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (random-init weights, SURVEY.md 8d recipe)",
             "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam) of the GAT generator "
-                                   "(scripts/train.py defaults)", "scenes_per_gpu": args.batch,
-                       "global_batch": args.batch * world, "peds_per_scene": args.peds, "obs_len": 8, "pred_len": 12,
-                       "generator": args.graph_kind, "hip_graph": graphed, "parallelism": "dp%d" % world},
-            "roofline": roofline, "cpu_baseline": cpu,
+                                   "(scripts/train.py defaults)%s" % (
+                                       "; BASELINE configs[1] shape (batch 64)" if world == 1 and per_gpu == 64 else
+                                       "; BASELINE configs[3] (4096-scene global batch)"
+                                       if world * per_gpu == CONFIG4_GLOBAL else ""),
+                       "scenes_per_gpu": per_gpu, "global_batch": per_gpu * world, "peds_per_scene": args.peds,
+                       "obs_len": 8, "pred_len": 12, "generator": args.graph_kind, "hip_graph": graphed,
+                       "parallelism": "dp%d" % world},
+            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
         }
+        if scaling_ref is not None:
+            line["scaling_reference"] = scaling_ref
+        if pmc_target is not None:
+            line["pmc_target"] = pmc_target
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

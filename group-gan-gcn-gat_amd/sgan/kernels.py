@@ -54,9 +54,18 @@ def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None, mask=None):
         bias = _req(bias, "bias").contiguous()
         assert bias.numel() == Nn
     y = out if out is not None else torch.empty(M, Nn, device=x.device, dtype=torch.float32)
-    N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(mask), mask.stride(0) if mask is not None else 0, N.ptr(w),
-                          w.stride(0), int(bool(trans_w)), N.ptr(bias), N.ptr(y),
-                          y.stride(0), M, K, Nn, int(act), N.stream_ptr()), "sgg_xw")
+
+    def launch():
+        N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(mask), mask.stride(0) if mask is not None else 0,
+                              N.ptr(w), w.stride(0), int(bool(trans_w)), N.ptr(bias), N.ptr(y), y.stride(0), M, K, Nn,
+                              int(act), N.stream_ptr()), "sgg_xw")
+    launch()
+    if timer.active and M > 0:
+        name = ("sgg::xw_splitk_kernel<%s>" % ("true" if trans_w else "false") if K >= 256 else
+                "sgg::xw_kernel<true, true>" if trans_w and K <= 256 else
+                "sgg::xw_kernel<%s, false>" % ("true" if trans_w else "false"))
+        timer.add(name, (M, K, Nn, mask is not None), 2.0 * M * K * Nn,
+                  4.0 * (M * K * (2 if mask is not None else 1) + K * Nn + M * Nn), launch)
     return y
 
 
@@ -86,9 +95,14 @@ def xtw(X, Y, colsum=False, trans_c=False, out=None, mask=None):
     splits = lib.sgg_xtw_splits(R, M, Nn)
     ws = torch.empty(splits * (M * Nn + Nn), device=X.device, dtype=torch.float32)
     cs = torch.empty(Nn, device=X.device, dtype=torch.float32) if colsum else None
-    N.check(lib.sgg_xtw(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), N.ptr(mask),
-                        mask.stride(0) if mask is not None else 0, R, M, Nn, N.ptr(C), C.stride(0), int(trans_c),
-                        N.ptr(cs), N.ptr(ws), ws.numel() * 4, N.stream_ptr()), "sgg_xtw")
+    def launch():
+        N.check(lib.sgg_xtw(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), N.ptr(mask),
+                            mask.stride(0) if mask is not None else 0, R, M, Nn, N.ptr(C), C.stride(0), int(trans_c),
+                            N.ptr(cs), N.ptr(ws), ws.numel() * 4, N.stream_ptr()), "sgg_xtw")
+    launch()
+    if timer.active:
+        timer.add("sgg::xtw_partial_kernel+xtw_reduce_kernel", (R, M, Nn, mask is not None), 2.0 * R * M * Nn,
+                  4.0 * (R * M + R * Nn * (2 if mask is not None else 1) + M * Nn) + 8.0 * ws.numel(), launch)
     return (C, cs) if colsum else C
 
 
@@ -243,15 +257,20 @@ class ClipAdam:
 # ---------------------------------------------------------------------------
 # social pooling
 # ---------------------------------------------------------------------------
-class _PoolTimer:
-    """Optional timing of sgg_pool_fwd launches (bench.py's roofline).
+class LaunchTimer:
+    """Per-kernel device timing of the hot ops (bench.py's roofline).
 
-    While active, every launch is recorded with a closure that re-issues the
-    identical launch (same buffers; the kernel is idempotent).  `replay()`
-    then runs each distinct launch `reps` times back to back between two HIP
-    events on the launch stream, so the device never waits on the host and
-    elapsed / reps is the kernel's average device duration (an event pair
-    around a single eager launch also counts host launch latency)."""
+    While active, every instrumented launch (pooling, LSTM sequences, GAT
+    encoder, node transforms, weight-gradient reductions) is recorded with
+    its kernel name (as rocprofv3 lists it), its algorithmic FLOP and HBM
+    bytes (work models in DESIGN.md section 4) and a closure that re-issues
+    the identical launch on the same buffers (every instrumented op is
+    idempotent: it rewrites its outputs from its inputs; the closure keeps the
+    tensors alive).  `replay()` runs each distinct launch `reps` times back to
+    back between two HIP events on the current stream, so the device never
+    waits for the host and elapsed / reps is the kernel's average device
+    duration (an event pair around one eager launch would also count host
+    launch latency)."""
 
     def __init__(self):
         self.active = False
@@ -266,14 +285,18 @@ class _PoolTimer:
         out, self.rec = self.rec, []
         return out
 
+    def add(self, name, key, flop, nbytes, relaunch):
+        if self.active:
+            self.rec.append((name, (name,) + tuple(key), float(flop), float(nbytes), relaunch))
+
     @staticmethod
-    def replay(records, reps=50):
-        """records: [(key, flops, relaunch)] -> {key: (launches, flops per
-        launch, average device ms per launch)}"""
+    def replay(records, reps=20):
+        """records -> {key: dict(name, launches, flop, bytes, ms)} with ms the
+        average device time of one launch."""
         res = {}
-        for key, fl, fn in records:
+        for name, key, fl, nb, fn in records:
             if key in res:
-                res[key][0] += 1
+                res[key]["launches"] += 1
                 continue
             fn()                                  # warm (instruction cache, L2)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -282,11 +305,11 @@ class _PoolTimer:
                 fn()
             e1.record()
             e1.synchronize()
-            res[key] = [1, fl, e0.elapsed_time(e1) / reps]
-        return {k: tuple(v) for k, v in res.items()}
+            res[key] = dict(name=name, launches=1, flop=fl, bytes=nb, ms=e0.elapsed_time(e1) / reps)
+        return res
 
 
-pool_timer = _PoolTimer()
+timer = LaunchTimer()
 
 
 def _pool_flops(scenes, bn):
@@ -327,11 +350,13 @@ class _Pool(torch.autograd.Function):
                                      N.ptr(chunks), nchunks, max_rows, gpw, B, bn, scenes.max_n, N.ptr(out),
                                      N.ptr(am), N.stream_ptr()), "sgg_pool_fwd")
         launch()
-        if pool_timer.active:
+        if timer.active:
             # the k-step unroll the library picks (pool.hip launch_fwd_g)
             unr = 16 if gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count \
                 else 2
-            pool_timer.rec.append(((bn, gpw, unr, scenes.S, B), _pool_flops(scenes, bn), launch))
+            nb = 4.0 * (B * 512 + 2 * B + 1024 + bn * 512 + bn) + 8.0 * B * bn
+            timer.add("sgg::pool_fwd_kernel<%d, %d, %d>" % (bn, gpw, unr), (scenes.S, B), _pool_flops(scenes, bn), nb,
+                      launch)
         ctx.scenes = scenes
         ctx.E = E
         ctx.save_for_backward(h, pos, W1, We, be, A, W2, U, out, am)
@@ -351,9 +376,15 @@ class _Pool(torch.autograd.Function):
         P = bn * 512 + 1024 + bn
         dU = torch.empty(B, 512, device=h.device, dtype=torch.float32)
         part = torch.empty(lib.sgg_pool_bwd_grid(sc.S), P, device=h.device, dtype=torch.float32) if wgrad else None
-        N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(out), N.ptr(am), N.ptr(dout),
-                                 N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(part),
-                                 N.stream_ptr()), "sgg_pool_bwd")
+        def launch():
+            N.check(lib.sgg_pool_bwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(out), N.ptr(am), N.ptr(dout),
+                                     N.ptr(sc.scene_off), sc.S, B, bn, sc.max_n, N.ptr(dU), N.ptr(part),
+                                     N.stream_ptr()), "sgg_pool_bwd")
+        launch()
+        if timer.active:
+            nb = 8.0 * B * 512 + 12.0 * B * bn + 4.0 * 512 * (2 + bn) + (4.0 * part.numel() if wgrad else 0.0)
+            timer.add("sgg::pool_bwd_kernel<%d, %s>" % (bn, "true" if wgrad else "false"), (sc.S, B),
+                      8.0 * B * bn * 512, nb, launch)
         dh = xw_raw(dU, W1[:, E:], None, trans_w=False) if need[0] else None
         if not wgrad:
             return dh, None, None, None, None, None, None, None, None
@@ -454,6 +485,11 @@ class _GatEnc(torch.autograd.Function):
         a = _gatenc_args(x, labels, scenes, nh, alpha, ps)
         a.y, a.ldy = N.ptr(y), 24
         N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_fwd")
+        if timer.active:
+            keep = (x, y, labels, scenes, ps)   # the replay closure holds every buffer `a` points to
+            timer.add("sgg::gatenc_kernel<false>", (scenes.S, B, nh), _gatenc_flops(scenes, nh), 4.0 * B * (40 + 1 + 24),
+                      lambda a=a, keep=keep: N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                     "sgg_gatenc_fwd"))
         ctx.meta = (labels, scenes, nh, alpha)
         ctx.save_for_backward(x, *ps)
         return y
@@ -473,6 +509,12 @@ class _GatEnc(torch.autograd.Function):
         a.dX, a.lddx = N.ptr(dx), 40
         a.slab = N.ptr(slab)
         N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_bwd")
+        if timer.active:
+            keep = (x, dy, dx, slab, labels, scenes, ps)
+            timer.add("sgg::gatenc_kernel<true>", (scenes.S, B, nh), 3.0 * _gatenc_flops(scenes, nh),
+                      4.0 * (B * (40 + 1 + 24 + 40) + scenes.S * P),
+                      lambda a=a, keep=keep: N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                     "sgg_gatenc_bwd"))
         flat = torch.empty(P, device=x.device, dtype=torch.float32)
         N.check(lib.sgg_slab_reduce(N.ptr(slab), scenes.S, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
         grads, o = [], 0
@@ -480,6 +522,18 @@ class _GatEnc(torch.autograd.Function):
             grads.append(flat[o:o + q.numel()].view_as(q))
             o += q.numel()
         return (dx, None, None, None, None) + tuple(grads)
+
+
+def _gatenc_flops(scenes, nh):
+    """GATEncoder forward FLOP (models.py:254-294) per scene of N peds, G
+    groups: node transforms 2 N (40*72 nh + 72 nh*16) + 2 G (16*72 nh + 72 nh*16)
+    + 2 N 32*24; attention (score + softmax + aggregate) ~ 3 F per edge over
+    the N^2 intra pairs (F = 72 nh and 16) and G^2 inter pairs (upper bound N^2)."""
+    import numpy as np
+    n = np.diff(scenes.host_off).astype(np.float64)
+    node = 2 * n * (40 * 72 * nh + 72 * nh * 16) + 2 * n * (16 * 72 * nh + 72 * nh * 16) + 2 * n * 32 * 24
+    edge = 2 * n * n * 3 * (72 * nh + 16)
+    return float((node + edge).sum())
 
 
 def _gatenc_args(x, labels, scenes, nh, alpha, ps):
@@ -667,9 +721,18 @@ class _LSTMSeq(torch.autograd.Function):
         h0c = h0.contiguous() if h0 is not None else None
         c0c = c0.contiguous() if c0 is not None else None
         Wpc = Wp.contiguous() if Wp is not None else None
-        N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), N.ptr(Wpc),
-                                 N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
-                                 N.ptr(rel_out), N.stream_ptr()), "sgg_lstm_fwd")
+        def launch():
+            N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c),
+                                     N.ptr(Wpc), N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all),
+                                     N.ptr(act), N.ptr(rel_out), N.stream_ptr()), "sgg_lstm_fwd")
+        launch()
+        if timer.active:
+            # per ped-step: gates 2 4H (H + 3) FLOP + ~12 H cell / activation; bytes: inputs, saved states
+            fl = T * B * (8.0 * H * (H + 3) + 12.0 * H)
+            nb = 4.0 * (T * B * 2 + (act.numel() + c_all.numel() + (T + 1) * B * H if save else B * H)
+                        + 4 * H * (H + 3) + (T * B * 2 if decoder else 0))
+            timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), int(save), 0).decode(),
+                      (T, B, int(decoder), int(save)), fl, nb, launch)
         ctx.meta = (decoder, T, B, H, h0 is not None)
         ctx.set_materialize_grads(False)   # unused outputs (the decoder's h_last) get None, not a zero fill
         if save:
@@ -701,9 +764,22 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             dout = None
             dhl = dh_last.contiguous() if dh_last is not None else None
-        N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel),
-                                 N.ptr(rel_out), N.ptr(dhl), N.ptr(dout), T, B, H, int(decoder), N.ptr(dG), N.ptr(dh0),
-                                 N.ptr(drel_in), N.ptr(drel_tot), N.ptr(wpart), N.stream_ptr()), "sgg_lstm_bwd")
+        def launch():
+            N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
+                                     N.ptr(rel), N.ptr(rel_out), N.ptr(dhl), N.ptr(dout), T, B, H, int(decoder),
+                                     N.ptr(dG), N.ptr(dh0), N.ptr(drel_in), N.ptr(drel_tot), N.ptr(wpart),
+                                     N.stream_ptr()), "sgg_lstm_bwd")
+        launch()
+        if timer.active:
+            # per ped-step: dh = W^T dG 2 4H H, cell gradient ~30 H, in-kernel
+            # weight gradient 2 4H (H + 3); bytes: saved states read, input
+            # gradients written, dG or the slab written
+            fl = T * B * (8.0 * H * H + 30.0 * H + (8.0 * H * (H + 3) if wpart is not None else 0.0))
+            nb = 4.0 * (act.numel() + c_all.numel() + T * B * 2 + (B * H if has_h0 else 0)
+                        + ((T * B * (H + 2) + wpart.numel()) if wpart is not None else 0)
+                        + (dG.numel() if dG is not None else 0) + (T * B * 4 if decoder else 0))
+            timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), 1, 1).decode(),
+                      (T, B, int(decoder), int(wpart is not None)), fl, nb, launch)
         dW_ih = dW_hh = db_ih = db_hh = dWe = dbe = dWp = dbp = None
         if wgrad:
             if wpart is not None:

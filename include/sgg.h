@@ -261,6 +261,10 @@ int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float
  * dWp / dbp of the decoder are X^T sums of drel_tot and h_all, left to the
  * caller in both forms. */
 int sgg_lstm_wpart_rows(int H, int B);
+/* Name of the kernel sgg_lstm_fwd (bwd = 0; save = act_all != NULL) or
+ * sgg_lstm_bwd (bwd = 1) launches for these sizes, as rocprofv3 lists it
+ * (bench.py's per-kernel timing). */
+const char* sgg_lstm_kernel_name(int H, int B, int decoder, int save, int bwd);
 int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                  const float* act_all, const float* rel, const float* rel_out, const float* dh_last,
                  const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,

@@ -326,3 +326,20 @@ def test_two_rank_512_scene_shard_equals_single():
                        capture_output=True, text=True, timeout=110, env=env)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and out.count(" OK") == 2, out[-3000:]
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """`bench.py --gpus 2` (not under torch.distributed.run) spawns one
+    process per rank itself and reports the 2-rank job (gloo rehearsal on this
+    one GPU: both ranks share it)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SGG_BENCH_BACKEND="gloo", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--batch", "16", "--no-cpu-baseline"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 32 and line["config"]["parallelism"] == "dp2"
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0

@@ -2,26 +2,31 @@
 
 usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR BENCH_JSON OUT_JSON
 
+Both passes run `bench.py ... --pmc-target R`: after its timing, bench
+re-issues the dominant kernel's main launch R times, so the LAST R
+dispatches of that kernel name in each counter CSV are exactly that launch
+shape; their mean FETCH_SIZE / WRITE_SIZE is its HBM traffic per launch.
 FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports half the
 bytes of wide (16 B/lane) coalesced reads (MI355X_MICROARCH.md, HBM section),
 so reads are doubled; WRITE_SIZE is exact for the kernels' 4-16 B/lane stores.
-Output keys are "<kernel>|[bn, gpw, unroll, scenes, peds]" for the pool forward
-launches that bench.py reports (matched by kernel name, only where one launch
-shape has that name), plus a per-kernel-name table of every kernel.
+The table is merged into OUT_JSON under "<kernel>|<shape>" (bench.py's
+traffic_lookup key), plus a per-kernel-name mean over every dispatch.
 """
 import collections
 import csv
 import json
+import os
 import re
 import sys
 
 
-def per_kernel(path, counter):
-    vals = collections.defaultdict(list)
-    for r in csv.DictReader(open(path + "/run_counter_collection.csv")):
+def rows(path, counter):
+    out = []
+    for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
         if r["Counter_Name"] == counter:
-            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+            out.append((int(r.get("Dispatch_Id", 0) or 0), short(r["Kernel_Name"]), float(r["Counter_Value"])))
+    out.sort()
+    return out
 
 
 def short(name):
@@ -32,27 +37,32 @@ def short(name):
 
 def main():
     fdir, wdir, bench, out = sys.argv[1:5]
-    fetch, nf = per_kernel(fdir, "FETCH_SIZE")
-    write, _ = per_kernel(wdir, "WRITE_SIZE")
-    kernels = {}
-    for k in fetch:
-        rd = 2.0 * fetch[k] * 1024.0
-        wr = write.get(k, 0.0) * 1024.0
-        kernels[short(k)] = {"read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr, "dispatches": nf[k]}
+    fr, wr = rows(fdir, "FETCH_SIZE"), rows(wdir, "WRITE_SIZE")
     line = json.loads(open(bench).read().strip().splitlines()[-1])
-    note = line["roofline"]["note"]
-    keys = [json.loads(s) for s in re.findall(r"'(\[[0-9, ]+\])'", note)]
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
-                     "`bench.py --steps 2 --warmup 1 --graph 0 --no-cpu-baseline`; FETCH_SIZE x2 (gfx950)",
-           "kernels": kernels}
-    by_name = collections.defaultdict(list)
-    for key in keys:
-        by_name["sgg::pool_fwd_kernel<%d, %d, %d>" % tuple(key[:3])].append(key)
-    for name, ks in by_name.items():
-        if len(ks) == 1 and name in kernels:
-            res["%s|%s" % (name, ks[0])] = kernels[name]
+    tgt = line["pmc_target"]
+    name, reps = tgt["kernel"], tgt["reps"]
+    res = json.load(open(out)) if os.path.exists(out) else {}
+    res["source"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of `bench.py --pmc-target R`; "
+                     "the last R dispatches of the target kernel; FETCH_SIZE x2 (gfx950)")
+    f_t = [v for _, k, v in fr if k == name.split("+")[0]][-reps:]
+    w_t = [v for _, k, v in wr if k == name.split("+")[0]][-reps:]
+    rd = 2.0 * 1024.0 * sum(f_t) / max(len(f_t), 1)
+    wb = 1024.0 * sum(w_t) / max(len(w_t), 1)
+    res["%s|%s" % (name, tgt["shape"])] = {"read_bytes": rd, "write_bytes": wb, "hbm_bytes": rd + wb,
+                                           "dispatches": len(f_t)}
+    per = collections.defaultdict(list)
+    for _, k, v in fr:
+        per[k].append(v)
+    perw = collections.defaultdict(list)
+    for _, k, v in wr:
+        perw[k].append(v)
+    res["kernels"] = {k: {"read_bytes": 2048.0 * sum(v) / len(v),
+                          "write_bytes": 1024.0 * sum(perw.get(k, [0.0])) / max(len(perw.get(k, [])), 1),
+                          "dispatches": len(v)} for k, v in per.items()}
+    for k in res["kernels"]:
+        res["kernels"][k]["hbm_bytes"] = res["kernels"][k]["read_bytes"] + res["kernels"][k]["write_bytes"]
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
-    print(json.dumps({k: v for k, v in res.items() if "|" in k}, indent=1))
+    print(json.dumps(res["%s|%s" % (name, tgt["shape"])], indent=1))
 
 
 if __name__ == "__main__":
