@@ -37,6 +37,29 @@ __global__ void __launch_bounds__(512) fold_fwd_kernel(const float* __restrict__
   }
 }
 
+// every fold of a module set in one launch: workgroup k computes fold k
+struct FoldList {
+  SggFold f[SGG_FOLD_MAX];
+};
+
+__global__ void __launch_bounds__(512) fold_fwd_multi_kernel(FoldList L) {
+  const SggFold& d = L.f[blockIdx.x];
+  for (int r = threadIdx.x; r < d.R; r += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f, bb = 0.f;
+    const float* w = d.W + (size_t)r * d.ldw;
+#pragma unroll 8
+    for (int e = 0; e < d.E; ++e) {
+      const float we = w[e];
+      a0 = fmaf(we, d.We[2 * e], a0);
+      a1 = fmaf(we, d.We[2 * e + 1], a1);
+      bb = fmaf(we, d.be[e], bb);
+    }
+    d.A[2 * r] = a0;
+    d.A[2 * r + 1] = a1;
+    d.bias[r] = bb + d.b1[r] + (d.b2 ? d.b2[r] : 0.f);
+  }
+}
+
 __global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__ W, int ldw, int R, int E,
                                                        const float* __restrict__ We, const float* __restrict__ be,
                                                        const float* __restrict__ dA, const float* __restrict__ dbias,
@@ -89,6 +112,19 @@ extern "C" int sgg_fold_fwd(const float* W, int ldw, int R, int E, const float* 
   hipLaunchKernelGGL(fold_fwd_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, W, ldw, R, E, We, be, b1, b2, A,
                      bias);
   SGG_RETURN_LAUNCH("sgg_fold_fwd");
+}
+
+extern "C" int sgg_fold_fwd_multi(const SggFold* folds, int n, void* stream) {
+  SGG_CHECK_ARG(folds && n >= 1 && n <= SGG_FOLD_MAX, "sgg_fold_fwd_multi: 1 <= n <= %d folds (got %d)", SGG_FOLD_MAX, n);
+  FoldList L;
+  for (int k = 0; k < n; ++k) {
+    const SggFold& d = folds[k];
+    SGG_CHECK_ARG(d.W && d.We && d.be && d.b1 && d.A && d.bias, "sgg_fold_fwd_multi: null pointer in fold %d", k);
+    SGG_CHECK_ARG(d.R >= 1 && d.E >= 1 && d.ldw >= d.E, "sgg_fold_fwd_multi: bad sizes in fold %d", k);
+    L.f[k] = d;
+  }
+  hipLaunchKernelGGL(fold_fwd_multi_kernel, dim3(n), dim3(512), 0, (hipStream_t)stream, L);
+  SGG_RETURN_LAUNCH("sgg_fold_fwd_multi");
 }
 
 extern "C" int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be, const float* dA,

@@ -264,22 +264,25 @@ extern "C" long long sgg_lstm_state_floats(int T, int B, int H, int which) {
 }
 
 extern "C" const char* sgg_lstm_kernel_name(int H, int B, int decoder, int save, int bwd) {
-  // mirrors the dispatch of sgg_lstm_fwd / sgg_lstm_bwd below
-  (void)decoder;
-  static const char* names[][4] = {
-      {"sgg::lstm_mw_fwd_kernel<16>", "sgg::lstm_mw_fwd_kernel<32>", "sgg::lstm_mw_fwd_kernel<48>", "sgg::lstm_mw_fwd_kernel<64>"},
-      {"sgg::lstm_mw_bwd_kernel<16>", "sgg::lstm_mw_bwd_kernel<32>", "sgg::lstm_mw_bwd_kernel<48>", "sgg::lstm_mw_bwd_kernel<64>"},
-      {"sgg::lstm_fwd_mfma_kernel<32>", "sgg::lstm_fwd_mfma_kernel<32>", "sgg::lstm_fwd_mfma_kernel<48>", "sgg::lstm_fwd_mfma_kernel<48>"},
-      {"sgg::lstm_unit_fwd_kernel<16>", "sgg::lstm_unit_fwd_kernel<32>", "sgg::lstm_fwd_kernel<48>", "sgg::lstm_fwd_kernel<64>"},
-      {"sgg::lstm_unit_bwd_kernel<16>", "sgg::lstm_unit_bwd_kernel<32>", "sgg::lstm_bwd_kernel<48>", "sgg::lstm_bwd_kernel<64>"}};
+  // mirrors the dispatch of sgg_lstm_fwd / sgg_lstm_bwd below (save = act_all
+  // != NULL for the forward, = weight gradients in the kernel for the backward)
+  static char buf[96];
   const int h = H == 16 ? 0 : H == 32 ? 1 : H == 48 ? 2 : H == 64 ? 3 : -1;
   if (h < 0 || B <= 0) return "";
   const bool mw = lstm_mw_ok(H, B);
-  if (bwd) return mw ? names[1][h] : names[4][h];
-  if (save && mw) return names[0][h];
-  if (lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) return names[2][h];
-  if (mw) return names[0][h];
-  return names[3][h];
+  const char* tf[2] = {"false", "true"};
+  if (bwd) {
+    if (mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_bwd_kernel<%d, %s, %s>", H, tf[decoder != 0], tf[save != 0]);
+    else if (H <= 32) snprintf(buf, sizeof buf, "sgg::lstm_unit_bwd_kernel<%d>", H);
+    else snprintf(buf, sizeof buf, "sgg::lstm_bwd_kernel<%d>", H);
+    return buf;
+  }
+  if (save && mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_fwd_kernel<%d, %s, true>", H, tf[decoder != 0]);
+  else if (lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) snprintf(buf, sizeof buf, "sgg::lstm_fwd_mfma_kernel<%d>", H);
+  else if (mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_fwd_kernel<%d, %s, %s>", H, tf[decoder != 0], tf[save != 0]);
+  else if (H <= 32) snprintf(buf, sizeof buf, "sgg::lstm_unit_fwd_kernel<%d>", H);
+  else snprintf(buf, sizeof buf, "sgg::lstm_fwd_kernel<%d>", H);
+  return buf;
 }
 
 extern "C" int sgg_lstm_wpart_rows(int H, int B) {

@@ -43,14 +43,16 @@
 //
 // Weight gradients in the kernel (wpart != NULL): wave g accumulates, on the
 // MFMA, its gate block's
-//   [dW_hh,g | db_g | dA_g] += dG_g^T (H x 16 peds) . [h_{t-1} | 1 | r_x r_y]
-// (MU x (MU + 1) tiles, K = the block's 16 peds = 4 k-steps), the A operand
-// read straight from the double-buffered dG image in LDS, h_{t-1} staged
-// from h_all one step ahead.  The MFMAs of step t + 1 are issued at the top
-// of step t, ahead of that step's VALU work, so the matrix core runs them in
-// the shadow of the cell-gradient arithmetic.  dG never reaches HBM: the
-// workgroup writes one slab row [dW_hh (4H x H) | db (4H) | dA (4H x 2)]
-// that sgg_slab_reduce sums (fixed order).
+//   dW_hh,g += dG_g^T (H x 16 peds) . h_{t-1}
+// (MU x MU tiles, K = the block's 16 peds = 4 k-steps), the A operand read
+// straight from the double-buffered dG image in LDS, h_{t-1} staged from
+// h_all one step ahead.  The MFMAs of step t + 1 are issued at the top of
+// step t, ahead of that step's VALU work, so the matrix core runs them in the
+// shadow of the cell-gradient arithmetic.  The slot owners sum db += dG and
+// dA += dG r_in^T on the VALU (3 FMA per gate value; reduced over the 16 peds
+// by lane shuffles at the end).  dG never reaches HBM: the workgroup writes
+// one slab row [dW_hh (4H x H) | db (4H) | dA (4H x 2)] that sgg_slab_reduce
+// sums (fixed order).
 #include <stdlib.h>
 #include <string.h>
 
@@ -62,7 +64,7 @@ namespace {
 
 constexpr int kMwThreads = 256;   // four waves: one per gate block, one per SIMD
 constexpr int kMwPeds = 16;       // MFMA columns
-constexpr int kMwMaxT = 32;       // encoder inputs of up to this many steps are staged in LDS
+constexpr int kMwMaxT = 64;       // encoder inputs (all T steps) are staged in LDS: T <= this
 constexpr int kDgPitch = 68;      // dG image row pitch: conflict-free for the transposed A-operand read
 
 // v_exp_f32 / v_rcp_f32 forms (~2 ulp), as the other LSTM kernels.
@@ -88,13 +90,18 @@ struct MwCfg {
   static constexpr int P = G4 * H + G4 + 2 * G4;                           // slab row floats
 };
 
-template <int H>
+// DEC / SAVE are compile-time, so the step loop carries no per-store
+// branches.  A padded lane (ped >= B, last block) runs on the clamped ped's
+// inputs, so it computes bit-identical values and its stores to that ped's
+// rows (h_all, rel_out) are benign duplicates: no store needs a guard.
+template <int H, bool DEC, bool SAVE>
 __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
-    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
+    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B,
     float* __restrict__ h_all, float* __restrict__ c_tile, float* __restrict__ act_tile, float* __restrict__ rel_out) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS;
+  constexpr bool decoder = DEC, save = SAVE;
   __shared__ float gate[4][KS][64];
   __shared__ float hb[KS][64];
   __shared__ float2 rpart[4][kMwPeds];
@@ -104,9 +111,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
   const int q = lane >> 4, c16 = lane & 15;
   const int blk = blockIdx.x;
   const int ped = blk * kMwPeds + c16;
-  const bool valid = ped < B;
-  const int pc = valid ? ped : B - 1;   // clamped: every load unconditional and in bounds
-  const bool save = act_tile != nullptr;
+  const int pc = ped < B ? ped : B - 1;   // clamped: every load and store unconditional and in bounds
 
   // [W_hh,g | A_g b_g] in registers, W_hh's columns in the permuted k order
   float w[MU][KS + 1], ak0[MU], ak1[MU];
@@ -127,27 +132,26 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     c[i] = c0 ? c0[(size_t)pc * H + u] : 0.f;
     hb[j][lane] = hv;
     if (save) {
-      if (valid) h_all[(size_t)ped * H + u] = hv;
+      h_all[(size_t)pc * H + u] = hv;
       c_tile[((size_t)blk * (T + 1) * KS + j) * 64 + lane] = c[i];
     }
     wp0[i] = decoder ? Wp[u] : 0.f;
     wp1[i] = decoder ? Wp[H + u] : 0.f;
   }
   const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
-  const bool staged = !decoder && T <= kMwMaxT;
-  if (staged)
+  if (!decoder)
     for (int e = threadIdx.x; e < 2 * kMwPeds * T; e += kMwThreads) {
       const int t = e / (2 * kMwPeds), p = (e >> 1) & (kMwPeds - 1), k = e & 1;
-      const int pp = blk * kMwPeds + p;
-      relseq[t][p][k] = pp < B ? rel[((size_t)t * B + pp) * 2 + k] : 0.f;
+      const int pp = min(blk * kMwPeds + p, B - 1);   // padded lanes see the clamped ped's inputs
+      relseq[t][p][k] = rel[((size_t)t * B + pp) * 2 + k];
     }
   __syncthreads();
 
   // input k-step operand: r_x (q = 0), r_y (q = 1), 1 (q = 2), 0 (q = 3)
+  // (loads unconditional, the constant lanes selected after)
   auto input = [&](int t) -> float {
-    if (q >= 2) return q == 2 ? 1.f : 0.f;
-    if (decoder) return rel[(size_t)pc * 2 + q];
-    return staged ? relseq[t][c16][q] : rel[((size_t)t * B + pc) * 2 + q];
+    const float v = decoder ? rel[(size_t)pc * 2 + (q & 1)] : relseq[t][c16][q & 1];
+    return q < 2 ? v : (q == 2 ? 1.f : 0.f);
   };
   float xin = input(0);
   const float s = g == 2 ? 2.f : 1.f;   // g: tanh, i f o: sigmoid
@@ -201,7 +205,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
       c[i] = fmaf(fg, c[i], ig * gg);
       const float h = og * tanh_m(c[i]);
       hb[j][lane] = h;
-      if (valid && (save || t == T - 1)) h_all[((size_t)(save ? t + 1 : T) * B + ped) * H + slot_unit(j, q)] = h;
+      if (save || t == T - 1) h_all[((size_t)(save ? t + 1 : T) * B + pc) * H + slot_unit(j, q)] = h;
       if (save) c_tile[(((size_t)blk * (T + 1) + t + 1) * KS + j) * 64 + lane] = c[i];
       px = fmaf(wp0[i], h, px);
       py = fmaf(wp1[i], h, py);
@@ -214,28 +218,28 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
       if (q == 0) rpart[g][c16] = make_float2(px, py);
     }
     lds_barrier();
-    if (decoder && g == 0 && q == 0 && valid) {   // r_t = Wp h_t + bp
+    if (decoder && g == 0 && q == 0) {   // r_t = Wp h_t + bp
       const float2 r0 = rpart[0][c16], r1 = rpart[1][c16], r2 = rpart[2][c16], r3 = rpart[3][c16];
-      *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + ped) * 2) =
+      *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + pc) * 2) =
           make_float2(((r0.x + r1.x) + (r2.x + r3.x)) + bp0, ((r0.y + r1.y) + (r2.y + r3.y)) + bp1);
     }
   }
 }
 
-template <int H>
+template <int H, bool DEC, bool WGRAD>
 __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Whh, const float* __restrict__ Wp,
     const float* __restrict__ h_all, const float* __restrict__ c_tile, const float* __restrict__ act_tile,
     const float* __restrict__ rel, const float* __restrict__ rel_out, const float* __restrict__ dh_last,
-    const float* __restrict__ dout, int T, int B, int decoder, float* __restrict__ dh0, float* __restrict__ drel_in,
+    const float* __restrict__ dout, int T, int B, float* __restrict__ dh0, float* __restrict__ drel_in,
     float* __restrict__ drel_tot, float* __restrict__ wpart) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
+  constexpr bool decoder = DEC, wgrad = WGRAD;
   constexpr int NHS = MwCfg<H>::NHS, P = MwCfg<H>::P;
   __shared__ float dgb[2][4][KS][kDgPitch];
   __shared__ float part[4][KS][64];
   __shared__ float2 fbp[4][kMwPeds];
   __shared__ float hs[2][kMwPeds][HP];
-  __shared__ float rs[2][kMwPeds][2];
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, c16 = lane & 15;
@@ -243,7 +247,6 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
   const int ped = blk * kMwPeds + c16;
   const bool valid = ped < B;
   const int pc = valid ? ped : B - 1;
-  const bool wgrad = wpart != nullptr;
 
   // W_hh,g^T in registers: wt[mu][ks] = W_hh[g H + slot_unit(ks, q)][16 mu + c16]
   // (decoder: the folded W' = W_hh + A Wp for t >= 1, plain W_hh kept for t = 0)
@@ -277,9 +280,17 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
   }
 
   // saved activations and cells of the owned slots (and the decoder's output
-  // gradient), one step ahead; tile-native, lane-linear
-  float ni[MU], nf[MU], ng[MU], no[MU], nc[MU], ncp[MU], nd0 = 0.f, nd1 = 0.f;
+  // gradient, the step input of the weight gradient), one step ahead;
+  // tile-native, lane-linear
+  float ni[MU], nf[MU], ng[MU], no[MU], nc[MU], ncp[MU], nd0 = 0.f, nd1 = 0.f, nr0 = 0.f, nr1 = 0.f;
   auto load_step = [&](int t) {
+    if (wgrad) {   // r_in(t): rel[t] (encoder); rel0, then rel_out[t - 1] (decoder)
+      const float* rp = !decoder ? rel + ((size_t)t * B + pc) * 2
+                                 : (t == 0 ? rel + (size_t)pc * 2 : rel_out + ((size_t)(t - 1) * B + pc) * 2);
+      const float2 rv = *reinterpret_cast<const float2*>(rp);
+      nr0 = rv.x;
+      nr1 = rv.y;
+    }
     const float* ab = act_tile + ((size_t)blk * T + t) * 4 * KS * 64 + lane;
     const float* cb = c_tile + ((size_t)blk * (T + 1) + t) * KS * 64 + lane;
 #pragma unroll
@@ -299,51 +310,46 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     }
   };
 
-  // weight-gradient operands of step t: h_{t-1} = h_all[t] and the step input
-  // r_in(t) of the block's 16 peds, fetched one step ahead, staged in LDS
+  // weight-gradient operand of step t: h_{t-1} = h_all[t] of the block's 16
+  // peds, fetched one step ahead, staged in LDS
   float hv[NHS];
-  float rv = 0.f;
   auto stage_load = [&](int t) {
 #pragma unroll
     for (int m = 0; m < NHS; ++m) {
-      const int e = threadIdx.x + m * kMwThreads;
-      const int p = min(e / H, kMwPeds - 1), u = e % H;
-      hv[m] = h_all[((size_t)t * B + min(blk * kMwPeds + p, B - 1)) * H + u];
-    }
-    if (threadIdx.x < 2 * kMwPeds) {
-      const int p = threadIdx.x >> 1, k = threadIdx.x & 1;
-      const int pp = min(blk * kMwPeds + p, B - 1);
-      rv = !decoder ? rel[((size_t)t * B + pp) * 2 + k]
-                    : (t == 0 ? rel[(size_t)pp * 2 + k] : rel_out[((size_t)(t - 1) * B + pp) * 2 + k]);
+      const int e = threadIdx.x + m * kMwThreads;   // < 16 H exactly (NHS = 16 H / 256)
+      hv[m] = h_all[((size_t)t * B + min(blk * kMwPeds + e / H, B - 1)) * H + e % H];
     }
   };
   auto stage_store = [&](int buf) {
 #pragma unroll
     for (int m = 0; m < NHS; ++m) {
       const int e = threadIdx.x + m * kMwThreads;
-      if (e < kMwPeds * H) hs[buf][e / H][e % H] = hv[m];
+      hs[buf][e / H][e % H] = hv[m];
     }
-    if (threadIdx.x < 2 * kMwPeds) rs[buf][threadIdx.x >> 1][threadIdx.x & 1] = rv;
   };
-  floatx4 dw[MU][MU + 1];
+  floatx4 dw[MU][MU];
 #pragma unroll
   for (int mu = 0; mu < MU; ++mu)
 #pragma unroll
-    for (int nu = 0; nu <= MU; ++nu) dw[mu][nu] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // dw[mu][nu] += dG_g^T (units 16 mu..) x [h | 1 r_x r_y] (cols 16 nu..) over the 16 peds
+    for (int nu = 0; nu < MU; ++nu) dw[mu][nu] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float db[MU][4], dax[MU][4], day[MU][4];
+#pragma unroll
+  for (int i = 0; i < MU; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) db[i][k] = dax[i][k] = day[i][k] = 0.f;
+  // dw[mu][nu] += dG_g^T (units 16 mu..) x h (units 16 nu..) over the 16 peds
   auto dw_accum = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int p = 4 * kk + q;
-      float bh[MU + 1];
+      float bh[MU];
 #pragma unroll
       for (int nu = 0; nu < MU; ++nu) bh[nu] = hs[buf][p][16 * nu + c16];
-      bh[MU] = c16 == 0 ? 1.f : c16 == 1 ? rs[buf][p][0] : c16 == 2 ? rs[buf][p][1] : 0.f;
 #pragma unroll
       for (int mu = 0; mu < MU; ++mu) {
         const float a = dgb[buf][g][4 * mu + (c16 & 3)][((c16 >> 2) << 4) + p];
 #pragma unroll
-        for (int nu = 0; nu <= MU; ++nu) dw[mu][nu] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bh[nu], dw[mu][nu], 0, 0, 0);
+        for (int nu = 0; nu < MU; ++nu) dw[mu][nu] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bh[nu], dw[mu][nu], 0, 0, 0);
       }
     }
   };
@@ -356,10 +362,10 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     const int cur = t & 1;
     if (wgrad) {
       if (t < T - 1) dw_accum(cur ^ 1);   // step t + 1: its dG image and h_t, in the VALU shadow below
-      stage_store(cur);                  // h_{t-1}, r_in(t) for step t (read after this step's barriers)
+      stage_store(cur);                  // h_{t-1} of step t (read after this step's barriers)
       if (t > 0) stage_load(t - 1);
     }
-    const float d0 = nd0, d1 = nd1;
+    const float d0 = nd0, d1 = nd1, r0 = nr0, r1 = nr1;
     float ci[MU], cf[MU], cg[MU], co[MU], cc[MU], ccp[MU];
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
@@ -394,6 +400,15 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
       dgb[cur][1][j][lane] = vf;
       dgb[cur][2][j][lane] = vg;
       dgb[cur][3][j][lane] = vo;
+      if (wgrad) {
+        const float vv[4] = {vi, vf, vg, vo};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          db[i][k] += vv[k];
+          dax[i][k] = fmaf(vv[k], r0, dax[i][k]);
+          day[i][k] = fmaf(vv[k], r1, day[i][k]);
+        }
+      }
       f0 = fmaf(aa0[i][3], vo, fmaf(aa0[i][2], vg, fmaf(aa0[i][1], vf, fmaf(aa0[i][0], vi, f0))));
       f1 = fmaf(aa1[i][3], vo, fmaf(aa1[i][2], vg, fmaf(aa1[i][1], vf, fmaf(aa1[i][0], vi, f1))));
     }
@@ -449,14 +464,31 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     // slab row of this workgroup: D tile (mu, nu) holds rows g H + 16 mu + 4 q + r, cols 16 nu + c16
     float* row = wpart + (size_t)blk * P;
 #pragma unroll
-    for (int mu = 0; mu < MU; ++mu) {
+    for (int mu = 0; mu < MU; ++mu)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gr = g * H + 16 * mu + 4 * q + r;
 #pragma unroll
         for (int nu = 0; nu < MU; ++nu) row[(size_t)gr * H + 16 * nu + c16] = dw[mu][nu][r];
-        if (c16 == 0) row[G4 * H + gr] = dw[mu][MU][r];                        // db
-        else if (c16 <= 2) row[G4 * H + G4 + 2 * gr + (c16 - 1)] = dw[mu][MU][r];   // dA (x, y)
+      }
+    // db / dA of the owned slots: sum over the 16 peds (lanes c16 of each q)
+#pragma unroll
+    for (int i = 0; i < MU; ++i) {
+      const int u = slot_unit(g * MU + i, q);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = db[i][k], x = dax[i][k], y = day[i][k];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o);
+          x += __shfl_xor(x, o);
+          y += __shfl_xor(y, o);
+        }
+        if (c16 == 0) {
+          row[G4 * H + k * H + u] = a;
+          row[G4 * H + G4 + 2 * (k * H + u)] = x;
+          row[G4 * H + G4 + 2 * (k * H + u) + 1] = y;
+        }
       }
     }
   }
@@ -467,8 +499,10 @@ int launch_fwd(const float* rel, const float* A, const float* Whh, const float* 
                const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
                float* rel_out, hipStream_t st) {
   const int grid = (B + kMwPeds - 1) / kMwPeds;
-  hipLaunchKernelGGL(lstm_mw_fwd_kernel<H>, dim3(grid), dim3(kMwThreads), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp,
-                     T, B, decoder, h_all, c_all, act_all, rel_out);
+  auto k = decoder ? (act_all ? lstm_mw_fwd_kernel<H, true, true> : lstm_mw_fwd_kernel<H, true, false>)
+                   : (act_all ? lstm_mw_fwd_kernel<H, false, true> : lstm_mw_fwd_kernel<H, false, false>);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kMwThreads), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B, h_all, c_all,
+                     act_all, rel_out);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
 }
 
@@ -477,24 +511,30 @@ int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* h
                const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
                int T, int B, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart, hipStream_t st) {
   const int grid = (B + kMwPeds - 1) / kMwPeds;
-  hipLaunchKernelGGL(lstm_mw_bwd_kernel<H>, dim3(grid), dim3(kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all,
-                     rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart);
+  auto k = decoder ? (wpart ? lstm_mw_bwd_kernel<H, true, true> : lstm_mw_bwd_kernel<H, true, false>)
+                   : (wpart ? lstm_mw_bwd_kernel<H, false, true> : lstm_mw_bwd_kernel<H, false, false>);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all, rel, rel_out,
+                     dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart);
   SGG_RETURN_LAUNCH("sgg_lstm_bwd");
 }
 
 }  // namespace
 
-// Policy: H = 48 / 64 (the discriminator; the unit-per-thread kernels are
-// register-bound there).  SGG_LSTM_MW=all also routes H = 16 / 32 here,
-// SGG_LSTM_MW=0 disables this form (kernel comparisons, tools/).  The same
-// predicate picks the forward (when it saves states) and the backward, so
-// the tile-native saved layout is always read by the kernel that wrote it.
+// Policy: every H (16 / 32 / 48 / 64).  Measured at the training shapes
+// (tools/lstm_probe.py, profiles/r02_lstm_*): the generator's H = 32 encoder
+// (T 8, B 1280) fwd 10.7 / bwd 18.2 us here vs 11.2 / 18.9 us + two weight-
+// gradient reductions in the unit-per-thread family, its decoder (T 12,
+// B 2560) 17.6 / 25.8 vs 23.1 / 35.6 us + three reductions.  SGG_LSTM_MW=0
+// disables this form, SGG_LSTM_MW=big keeps it to H >= 48 (kernel
+// comparisons, tools/).  The same predicate picks the forward (when it
+// saves states) and the backward, so the tile-native saved layout is always
+// read by the kernel that wrote it.
 bool lstm_mw_ok(int H, int B) {
   (void)B;
   const char* e = getenv("SGG_LSTM_MW");
   if (e && strcmp(e, "0") == 0) return false;
-  if (e && strcmp(e, "all") == 0) return H == 16 || H == 32 || H == 48 || H == 64;
-  return H == 48 || H == 64;
+  if (e && strcmp(e, "big") == 0) return H == 48 || H == 64;
+  return H == 16 || H == 32 || H == 48 || H == 64;
 }
 
 long long lstm_mw_state_floats(int T, int B, int H, int which) {
@@ -510,6 +550,8 @@ int lstm_mw_wpart_rows(int H, int B) {
 int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
                 const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
                 float* c_all, float* act_all, float* rel_out, hipStream_t st) {
+  SGG_CHECK_ARG(decoder || T <= kMwMaxT, "sgg_lstm_fwd: encoder sequences of the H=%d kernels hold <= %d steps (T=%d)",
+                H, kMwMaxT, T);
   switch (H) {
     case 16: return launch_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
     case 32: return launch_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);

@@ -36,6 +36,14 @@ class GatEncArgs(ctypes.Structure):
 
 _pargs = ctypes.POINTER(GatEncArgs)
 
+FOLD_MAX = 8   # SGG_FOLD_MAX
+
+
+class Fold(ctypes.Structure):
+    """SggFold (include/sgg.h)."""
+    _fields_ = [("W", _p), ("ldw", _i), ("R", _i), ("E", _i), ("We", _p), ("be", _p), ("b1", _p), ("b2", _p),
+                ("A", _p), ("bias", _p)]
+
 # name -> (restype, argtypes); must mirror include/sgg.h exactly
 SIGNATURES = {
     "sgg_version": (_i, []),
@@ -59,6 +67,7 @@ SIGNATURES = {
                           _sz, _p]),
     "sgg_xtw": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _sz, _p]),
     "sgg_fold_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
+    "sgg_fold_fwd_multi": (_i, [ctypes.POINTER(Fold), _i, _p]),
     "sgg_fold_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "sgg_lstm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_lstm_state_floats": (ctypes.c_longlong, [_i, _i, _i, _i]),

@@ -110,15 +110,80 @@ def xtw(X, Y, colsum=False, trans_c=False, out=None, mask=None):
 # input-embedding fold (sgg_fold_fwd / sgg_fold_bwd)
 # ---------------------------------------------------------------------------
 def fold_fwd(W, We, be, b1, b2=None):
-    """A = W We (R x 2), bias = W be + b1 (+ b2); W may be a column block."""
-    W = _rows(W, "W")
-    R, E = W.shape
-    A = torch.empty(R, 2, device=W.device, dtype=torch.float32)
-    bias = torch.empty(R, device=W.device, dtype=torch.float32)
-    N.check(_lib().sgg_fold_fwd(N.ptr(W), W.stride(0), R, E, N.ptr(We.contiguous()), N.ptr(be.contiguous()),
-                                N.ptr(b1.contiguous()), N.ptr(b2.contiguous() if b2 is not None else None), N.ptr(A),
-                                N.ptr(bias), N.stream_ptr()), "sgg_fold_fwd")
-    return A, bias
+    """A = W We (R x 2), bias = W be + b1 (+ b2); W may be a column block.
+    Cached: the fold depends on weights only, so it is recomputed only after
+    they change (torch's version counter, or an epoch ClipAdam bumps when it
+    updates parameters through raw pointers) -- see prefold()."""
+    key, ver = _fold_key(W, We, be, b1, b2)
+    ent = _FOLD_CACHE.get(key)
+    if ent is not None and ent[0] == ver:
+        return ent[1], ent[2]
+    prefold([(W, We, be, b1, b2)])
+    ent = _FOLD_CACHE[key]
+    return ent[1], ent[2]
+
+
+# parameter data_ptr -> epoch, bumped by ClipAdam for every tensor it updates
+# in place (its raw-pointer update does not move torch's version counter)
+_EPOCH = {}
+_FOLD_CACHE = {}
+
+
+def _fold_key(W, We, be, b1, b2):
+    ts = (W, We, be, b1, b2)
+    key = tuple((t.data_ptr(), tuple(t.shape), t.stride(0)) if t is not None else None for t in ts)
+    ver = tuple((t._version, _EPOCH.get(t.data_ptr(), 0)) if t is not None else None for t in ts)
+    return key, ver
+
+
+def clear_fold_cache():
+    """Drop every cached fold (a HIP-graph capture must start from an empty
+    cache, so every fold its replays need is a node of the graph)."""
+    _FOLD_CACHE.clear()
+
+
+def prefold(specs):
+    """Make sure the folds of `specs` [(W, We, be, b1, b2), ...] are cached and
+    current, computing all missing / stale ones in ONE launch
+    (sgg_fold_fwd_multi).  Called once per module set per forward (the
+    generator's encoder + pooling + decoder, the discriminator's encoder +
+    pooling), so a training iteration runs three fold launches instead of one
+    per layer call."""
+    todo = []
+    for W, We, be, b1, b2 in specs:
+        key, ver = _fold_key(W, We, be, b1, b2)
+        ent = _FOLD_CACHE.get(key)
+        if ent is None or ent[0] != ver:
+            todo.append((key, ver, (W, We, be, b1, b2)))
+    if not todo:
+        return
+    arr = (N.Fold * len(todo))()
+    outs = []
+    for k, (key, ver, (W, We, be, b1, b2)) in enumerate(todo):
+        W = _rows(W, "W")
+        R, E = W.shape
+        A = torch.empty(R, 2, device=W.device, dtype=torch.float32)
+        bias = torch.empty(R, device=W.device, dtype=torch.float32)
+        parts = (W, We.contiguous(), be.contiguous(), b1.contiguous(), b2.contiguous() if b2 is not None else None)
+        arr[k] = N.Fold(N.ptr(parts[0]), W.stride(0), R, E, N.ptr(parts[1]), N.ptr(parts[2]), N.ptr(parts[3]),
+                        N.ptr(parts[4]), N.ptr(A), N.ptr(bias))
+        outs.append((key, ver, A, bias, parts))
+    for i in range(0, len(todo), N.FOLD_MAX):
+        chunk = (N.Fold * min(N.FOLD_MAX, len(todo) - i))(*arr[i:i + N.FOLD_MAX])
+        N.check(_lib().sgg_fold_fwd_multi(chunk, len(chunk), N.stream_ptr()), "sgg_fold_fwd_multi")
+    for key, ver, A, bias, parts in outs:
+        # the entry keeps the weights alive: their addresses cannot be reused
+        # by other tensors while the entry exists
+        _FOLD_CACHE[key] = (ver, A, bias, parts)
+
+
+def lstm_fold_spec(lstm, emb):
+    return (lstm.weight_ih_l0, emb.weight, emb.bias, lstm.bias_ih_l0, lstm.bias_hh_l0)
+
+
+def pool_fold_spec(pool):
+    l1, E = pool.mlp_pre_pool[0], pool.embedding_dim
+    return (l1.weight[:, :E], pool.spatial_embedding.weight, pool.spatial_embedding.bias, l1.bias, None)
 
 
 def fold_bwd(W, We, be, dA, dbias, dW=None, dbias_copy=None):
@@ -241,6 +306,8 @@ class ClipAdam:
                     raise N.NativeError("ClipAdam: parameters and grads must be contiguous fp32 device tensors")
         n = len(act)
         st = [self._state(p) for p in act]
+        for p in act:    # in-place update through raw pointers: invalidate cached folds of these weights
+            _EPOCH[p.data_ptr()] = _EPOCH.get(p.data_ptr(), 0) + 1
         arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])
         numel = (ctypes.c_longlong * n)(*[p.numel() for p in act])
         total = sum(p.numel() for p in act)
@@ -778,7 +845,7 @@ class _LSTMSeq(torch.autograd.Function):
             nb = 4.0 * (act.numel() + c_all.numel() + T * B * 2 + (B * H if has_h0 else 0)
                         + ((T * B * (H + 2) + wpart.numel()) if wpart is not None else 0)
                         + (dG.numel() if dG is not None else 0) + (T * B * 4 if decoder else 0))
-            timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), 1, 1).decode(),
+            timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), int(wpart is not None), 1).decode(),
                       (T, B, int(decoder), int(wpart is not None)), fl, nb, launch)
         dW_ih = dW_hh = db_ih = db_hh = dWe = dbe = dWp = dbp = None
         if wgrad:

@@ -506,6 +506,16 @@ class TrajectoryGenerator(nn.Module):
         noise_input = self.context(obs_traj, obs_traj_rel, seq_start_end, obs_traj_g, scenes=sc)
         return self.decode(noise_input, obs_traj, obs_traj_rel, seq_start_end, user_noise=user_noise, scenes=sc)
 
+    def fold_specs(self):
+        """The generator's input-embedding folds (encoder, pooling, decoder),
+        computed together in one launch (kernels.prefold)."""
+        specs = [K.lstm_fold_spec(self.encoder.encoder, self.encoder.spatial_embedding)]
+        if self.pooling_type:
+            specs.append(K.pool_fold_spec(self.pool_net))
+        if not self.pool_every_timestep and self.num_layers == 1:
+            specs.append(K.lstm_fold_spec(self.decoder.decoder, self.decoder.spatial_embedding))
+        return specs
+
     def context(self, obs_traj, obs_traj_rel, seq_start_end, obs_traj_g, *, scenes=None):
         """The noise-independent part of forward() (models.py:877-906):
         encoder -> pooling -> GAT / GCN -> the decoder context (B, dec_h - noise).
@@ -514,6 +524,8 @@ class TrajectoryGenerator(nn.Module):
         point, so it runs once per batch and `decode(copies=k)` rolls the k
         samples out (the reference recomputes it k times, bit-identically)."""
         sc = _scenes(seq_start_end, obs_traj.device, scenes)
+        if self.num_layers == 1:
+            K.prefold(self.fold_specs())
         final_encoder_h = self.encoder(obs_traj_rel)
         ctx = final_encoder_h.view(-1, self.encoder_h_dim)
         end_pos = obs_traj[-1]
@@ -601,6 +613,11 @@ class TrajectoryDiscriminator(nn.Module):
                                         dropout=dropout)
 
     def forward(self, traj, traj_rel, seq_start_end=None, *, scenes=None):
+        if self.encoder.num_layers == 1:   # encoder + pooling folds in one launch (kernels.prefold)
+            specs = [K.lstm_fold_spec(self.encoder.encoder, self.encoder.spatial_embedding)]
+            if self.d_type != "local":
+                specs.append(K.pool_fold_spec(self.pool_net))
+            K.prefold(specs)
         final_h = self.encoder(traj_rel)
         if self.d_type == "local":
             x = final_h.squeeze()

@@ -369,6 +369,7 @@ class GraphedTrainer:
         # the replay never depends on capturing a collective (gloo cannot be
         # captured; a failed capture would poison the stream).
         self.segments = []
+        K.clear_fold_cache()   # every fold the replays need must be a node of the graph
         pool = torch.cuda.graph_pool_handle()
         dp = trainer.dp
         cap = torch.cuda.Stream()

@@ -215,6 +215,22 @@ int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const float* Ymask
  * dWe = W^T dA (E x 2), dbe = W^T dbias (E); db1 = db2 = dbias. */
 int sgg_fold_fwd(const float* W, int ldw, int R, int E, const float* We, const float* be,
                  const float* b1, const float* b2, float* A, float* bias, void* stream);
+/* Several folds (a module set's: encoder, pooling, decoder) in ONE launch,
+ * one workgroup each; the descriptors are copied into the kernel arguments. */
+#define SGG_FOLD_MAX 8
+typedef struct {
+  const float* W;
+  int ldw;
+  int R;
+  int E;
+  const float* We;
+  const float* be;
+  const float* b1;
+  const float* b2;
+  float* A;
+  float* bias;
+} SggFold;
+int sgg_fold_fwd_multi(const SggFold* folds, int n, void* stream);
 /* dbias_copy (may be NULL) receives a copy of dbias: the LSTM's second bias
  * leaf b_hh gets its own gradient tensor without an extra launch. */
 int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be, const float* dA,

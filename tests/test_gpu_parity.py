@@ -354,11 +354,11 @@ def test_fused_lstm_vs_oracle(H, T, decoder, B):
 
 @pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (32, 12, True, 37), (16, 5, True, 21),
                                             (48, 12, True, 37), (64, 3, True, 37), (48, 20, False, 2085)])
-def test_fused_lstm_multiwave_all_sizes(H, T, decoder, B, monkeypatch):
-    """lstm_mw.hip (four waves per 16 peds) on every hidden size and both
-    directions, decoder included (the default policy routes only H = 48 / 64
-    encoders there)."""
-    monkeypatch.setenv("SGG_LSTM_MW", "all")
+def test_fused_lstm_other_families(H, T, decoder, B, monkeypatch):
+    """With the four-wave MFMA family disabled (SGG_LSTM_MW=0) the
+    unit-per-thread (H 16 / 32) and row kernels (H 48 / 64) take over:
+    every family stays checked against the oracle, both directions."""
+    monkeypatch.setenv("SGG_LSTM_MW", "0")
     test_fused_lstm_vs_oracle(H, T, decoder, B)
 
 

@@ -44,8 +44,10 @@ def main():
     res = json.load(open(out)) if os.path.exists(out) else {}
     res["source"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of `bench.py --pmc-target R`; "
                      "the last R dispatches of the target kernel; FETCH_SIZE x2 (gfx950)")
-    f_t = [v for _, k, v in fr if k == name.split("+")[0]][-reps:]
-    w_t = [v for _, k, v in wr if k == name.split("+")[0]][-reps:]
+    base = name.split("+")[0]
+    match = (lambda k: k == base) if "<" in base else (lambda k: k.split("<")[0] == base)
+    f_t = [v for _, k, v in fr if match(k)][-reps:]
+    w_t = [v for _, k, v in wr if match(k)][-reps:]
     rd = 2.0 * 1024.0 * sum(f_t) / max(len(f_t), 1)
     wb = 1024.0 * sum(w_t) / max(len(w_t), 1)
     res["%s|%s" % (name, tgt["shape"])] = {"read_bytes": rd, "write_bytes": wb, "hbm_bytes": rd + wb,
