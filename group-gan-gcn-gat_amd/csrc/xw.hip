@@ -207,14 +207,97 @@ __global__ void __launch_bounds__(256) xw_splitk_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 variant (opt-in, BASELINE configs 3 and 5: "bf16 + MFMA XW"): X and W
+// rounded to bf16 (round-to-nearest-even), v_mfma_f32_16x16x32_bf16, fp32
+// accumulate, fp32 epilogue / output.  Same tiling as xw_kernel (4 waves x
+// 16 rows x 64 cols); lane l holds A[row l & 15][k = 8 (l >> 4) + j] and
+// B[k = 8 (l >> 4) + j][col l & 15], j = 0..7, so one k-step covers 32 k.
+// Operands are read straight from global (L2-resident: K <= 512 here).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <bool TRANS_W>
+__global__ void __launch_bounds__(256) xw_bf16_kernel(const float* __restrict__ X, int ldx,
+                                                      const float* __restrict__ Xmask, int ldm,
+                                                      const float* __restrict__ W, int ldw,
+                                                      const float* __restrict__ bias, float* __restrict__ Y,
+                                                      int ldy, int M, int K, int N, int act) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * 64 + wave * 16;
+  const int col0 = blockIdx.y * 64;
+  const int ar = lane & 15, kg = lane >> 4;
+  const int arow = min(row0 + ar, M - 1);
+  const float* xrow = X + (size_t)arow * ldx;
+  const float* mrow = Xmask ? Xmask + (size_t)arow * ldm : nullptr;
+  int ncl[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ncl[t] = min(col0 + 16 * t + ar, N - 1);
+  floatx4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    const int kb = k0 + 8 * kg;
+    bf16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kb + j, kc = min(k, K - 1);
+      const bool keep = k < K && (!mrow || mrow[kc] > 0.f);
+      a[j] = (__bf16)keep_if(xrow[kc], keep);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bf16x8 b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kc = min(kb + j, K - 1);   // k >= K meets a zero A element
+        b[j] = (__bf16)(TRANS_W ? W[(size_t)ncl[t] * ldw + kc] : W[(size_t)kc * ldw + ncl[t]]);
+      }
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n = col0 + 16 * t + ar;
+    if (n >= N) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = row0 + kg * 4 + r;
+      if (m < M) Y[(size_t)m * ldy + n] = xw_epi(acc[t][r], bias, n, act);
+    }
+  }
+}
+
 }  // namespace sgg
+
+extern "C" int sgg_xw_bf16(const float* X, int ldx, const float* Xmask, int ldm, const float* W, int ldw, int trans_w,
+                           const float* bias, float* Y, int ldy, int M, int K, int N, int act, void* stream) {
+  SGG_CHECK_ARG(X && W && Y, "sgg_xw_bf16: null pointer");
+  SGG_CHECK_ARG(M >= 0 && K > 0 && N > 0, "sgg_xw_bf16: bad sizes M=%d K=%d N=%d", M, K, N);
+  // (the row stride of a one-row weight is never used: torch reports any value for it)
+  SGG_CHECK_ARG(ldx >= K && ldy >= N && (trans_w ? (N == 1 || ldw >= K) : (K == 1 || ldw >= N)),
+                "sgg_xw_bf16: bad leading dims ldx=%d ldw=%d ldy=%d (M=%d K=%d N=%d trans=%d)", ldx, ldw, ldy, M, K, N,
+                trans_w);
+  SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw_bf16: act must be 0 or 1");
+  SGG_CHECK_ARG(!Xmask || ldm >= K, "sgg_xw_bf16: mask leading dim %d < K", ldm);
+  if (M == 0) return 0;
+  dim3 grid((M + 63) / 64, (N + 63) / 64);
+  hipStream_t s = (hipStream_t)stream;
+  if (trans_w)
+    hipLaunchKernelGGL(sgg::xw_bf16_kernel<true>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy, M, K,
+                       N, act);
+  else
+    hipLaunchKernelGGL(sgg::xw_bf16_kernel<false>, grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy, M,
+                       K, N, act);
+  SGG_RETURN_LAUNCH("sgg_xw_bf16");
+}
 
 extern "C" int sgg_xw(const float* X, int ldx, const float* Xmask, int ldm, const float* W, int ldw, int trans_w,
                       const float* bias, float* Y, int ldy, int M, int K, int N, int act, void* stream) {
   SGG_CHECK_ARG(X && W && Y, "sgg_xw: null pointer");
   SGG_CHECK_ARG(M >= 0 && K > 0 && N > 0, "sgg_xw: bad sizes M=%d K=%d N=%d", M, K, N);
-  SGG_CHECK_ARG(ldx >= K && ldy >= N && ldw >= (trans_w ? K : N), "sgg_xw: bad leading dims ldx=%d ldw=%d ldy=%d",
-                ldx, ldw, ldy);
+  SGG_CHECK_ARG(ldx >= K && ldy >= N && (trans_w ? (N == 1 || ldw >= K) : (K == 1 || ldw >= N)),
+                "sgg_xw: bad leading dims ldx=%d ldw=%d ldy=%d", ldx, ldw, ldy);
   SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw: act must be 0 or 1");
   SGG_CHECK_ARG(!Xmask || ldm >= K, "sgg_xw: mask leading dim %d < K", ldm);
   if (M == 0) return 0;

@@ -49,6 +49,7 @@ SIGNATURES = {
     "sgg_version": (_i, []),
     "sgg_last_error": (ctypes.c_char_p, []),
     "sgg_xw": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "sgg_xw_bf16": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
     "sgg_pool_plan": (_i, [_p, _i, _i, _i, _i, _p, _i, _p, _p]),
     "sgg_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_pool_bwd_grid": (_i, [_i]),

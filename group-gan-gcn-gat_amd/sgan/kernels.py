@@ -36,12 +36,38 @@ def _rows(t, name):
 
 
 # ---------------------------------------------------------------------------
+# precision of the node transforms
+# ---------------------------------------------------------------------------
+_PRECISION = os.environ.get("SGG_PRECISION", "fp32")
+
+
+def set_precision(p):
+    """'fp32' (default; exact f32 MFMA, the parity path) or 'bf16': every
+    forward dense node transform X W (sgg_xw: the GAT / GCN XW, Linear
+    layers, the pooling's h W1h) runs on bf16 MFMA with fp32 accumulation
+    (BASELINE configs 3 and 5: "bf16 + MFMA XW"); the backward's input
+    gradients, LSTMs, attention, pooling pairs and weight-gradient
+    reductions stay fp32 (bf16 input gradients through the sgangat instance
+    norms lose the encoder's gradient: tests/test_gpu_configs.py)."""
+    global _PRECISION
+    if p not in ("fp32", "bf16"):
+        raise ValueError("precision must be 'fp32' or 'bf16'")
+    _PRECISION = p
+
+
+def precision():
+    return _PRECISION
+
+
+# ---------------------------------------------------------------------------
 # dense node transform
 # ---------------------------------------------------------------------------
-def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None, mask=None):
+def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None, mask=None, prec=None):
     """act(x @ W + bias); W = w (K x N) or w^T (w stored N x K, trans_w).  w
     may be a row-strided column block (e.g. W1[:, E:]), passed in place.
-    mask (same shape as x): x counts only where mask > 0 (fused ReLU backward)."""
+    mask (same shape as x): x counts only where mask > 0 (fused ReLU backward).
+    prec: None = the global precision (set_precision) -- the forward
+    transforms; 'fp32' forces exact f32 (the backward's input gradients)."""
     x = _rows(x, "x")
     if mask is not None:
         mask = _rows(mask, "mask")
@@ -55,15 +81,20 @@ def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None, mask=None):
         assert bias.numel() == Nn
     y = out if out is not None else torch.empty(M, Nn, device=x.device, dtype=torch.float32)
 
+    bf16 = (prec or _PRECISION) == "bf16"
+    fn = _lib().sgg_xw_bf16 if bf16 else _lib().sgg_xw
+
     def launch():
-        N.check(_lib().sgg_xw(N.ptr(x), x.stride(0), N.ptr(mask), mask.stride(0) if mask is not None else 0,
-                              N.ptr(w), w.stride(0), int(bool(trans_w)), N.ptr(bias), N.ptr(y), y.stride(0), M, K, Nn,
-                              int(act), N.stream_ptr()), "sgg_xw")
+        N.check(fn(N.ptr(x), x.stride(0), N.ptr(mask), mask.stride(0) if mask is not None else 0,
+                   N.ptr(w), w.stride(0), int(bool(trans_w)), N.ptr(bias), N.ptr(y), y.stride(0), M, K, Nn,
+                   int(act), N.stream_ptr()), "sgg_xw")
     launch()
     if timer.active and M > 0:
-        name = ("sgg::xw_splitk_kernel<%s>" % ("true" if trans_w else "false") if K >= 256 else
+        tw = "true" if trans_w else "false"
+        name = ("sgg::xw_bf16_kernel<%s>" % tw if bf16 else
+                "sgg::xw_splitk_kernel<%s>" % tw if K >= 256 else
                 "sgg::xw_kernel<true, true>" if trans_w and K <= 256 else
-                "sgg::xw_kernel<%s, false>" % ("true" if trans_w else "false"))
+                "sgg::xw_kernel<%s, false>" % tw)
         timer.add(name, (M, K, Nn, mask is not None), 2.0 * M * K * Nn,
                   4.0 * (M * K * (2 if mask is not None else 1) + K * Nn + M * Nn), launch)
     return y
@@ -215,7 +246,7 @@ class _XW(torch.autograd.Function):
         m = y if ctx.act else None    # ReLU backward dy * (y > 0), fused into the operands
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = xw_raw(dy, w, None, not ctx.trans_w, 0, mask=m)
+            dx = xw_raw(dy, w, None, not ctx.trans_w, 0, mask=m, prec="fp32")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             # X^T dY (K x N); nn.Linear-layout weights take it transposed (N x K)
             dw, cs = xtw(x, dy, colsum=True, trans_c=ctx.trans_w, mask=m)
@@ -452,7 +483,7 @@ class _Pool(torch.autograd.Function):
             nb = 8.0 * B * 512 + 12.0 * B * bn + 4.0 * 512 * (2 + bn) + (4.0 * part.numel() if wgrad else 0.0)
             timer.add("sgg::pool_bwd_kernel<%d, %s>" % (bn, "true" if wgrad else "false"), (sc.S, B),
                       8.0 * B * bn * 512, nb, launch)
-        dh = xw_raw(dU, W1[:, E:], None, trans_w=False) if need[0] else None
+        dh = xw_raw(dU, W1[:, E:], None, trans_w=False, prec="fp32") if need[0] else None
         if not wgrad:
             return dh, None, None, None, None, None, None, None, None
         flat = torch.empty(P, device=h.device, dtype=torch.float32)     # [dW2 | dA | db2]

@@ -55,6 +55,12 @@ const char* sgg_last_error(void);
 int sgg_xw(const float* X, int ldx, const float* Xmask, int ldm, const float* W, int ldw, int trans_w,
            const float* bias, float* Y, int ldy, int M, int K, int N, int act, void* stream);
 
+/* The same transform with X and W rounded to bf16 (round-to-nearest-even) on
+ * v_mfma_f32_16x16x32_bf16, fp32 accumulation and output: the opt-in "bf16 +
+ * MFMA XW" precision of BASELINE configs 3 and 5 (sgan.kernels.set_precision). */
+int sgg_xw_bf16(const float* X, int ldx, const float* Xmask, int ldm, const float* W, int ldw, int trans_w,
+                const float* bias, float* Y, int ldy, int M, int K, int N, int act, void* stream);
+
 /* ------------------------------------------------------------------------
  * Social pooling (PoolHiddenNet.forward, models.py:497-549), factored:
  *   hidden(i,j,k) = ReLU( U[j,k] + A[k,0]*(p_j - p_i)_x + A[k,1]*(p_j - p_i)_y )

@@ -343,3 +343,119 @@ def test_bench_gpus2_spawns_two_ranks():
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 32 and line["config"]["parallelism"] == "dp2"
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+
+
+# ---------------------------------------------------------------------------
+# configs[2] / configs[4]: the opt-in bf16 "MFMA XW" precision
+# ---------------------------------------------------------------------------
+@pytest.fixture
+def bf16():
+    from sgan import kernels as K
+    K.set_precision("bf16")
+    try:
+        yield
+    finally:
+        K.set_precision("fp32")
+
+
+def test_xw_bf16_kernel_is_exact_on_rounded_operands():
+    """sgg_xw_bf16 = fp32 accumulation of the bf16-rounded operands: checked
+    against an fp64 product of the same rounded values (tight), plain and
+    nn.Linear weight layouts, fused ReLU, the ReLU-backward mask, ragged K."""
+    from sgan import _native as N
+    lib = N.load()
+    torch.manual_seed(0)
+    for (M, Kd, Nn) in [(1, 3, 5), (37, 40, 72), (1000, 32, 512), (257, 48, 48), (64, 16, 24), (130, 144, 16),
+                        (515, 72, 1)]:
+        x = torch.randn(M, Kd, device=DEV)
+        w = torch.randn(Kd, Nn, device=DEV)
+        b = torch.randn(Nn, device=DEV)
+        m = torch.randn(M, Kd, device=DEV)
+        r = lambda t: t.to(torch.bfloat16).double()
+        for trans in (False, True):
+            wt = w.t().contiguous() if trans else w
+            for act, mask in ((0, None), (1, None), (0, m)):
+                y = torch.empty(M, Nn, device=DEV)
+                N.check(lib.sgg_xw_bf16(N.ptr(x), Kd, N.ptr(mask), Kd if mask is not None else 0, N.ptr(wt),
+                                        wt.stride(0), int(trans), N.ptr(b), N.ptr(y), Nn, M, Kd, Nn, act,
+                                        N.stream_ptr()), "xw_bf16")
+                xr = r(x) * (m > 0).double() if mask is not None else r(x)
+                ref = xr @ r(w) + b.double()
+                if act:
+                    ref = ref.clamp(min=0)
+                close(y, ref.float(), rtol=2e-6, floor=1.0, what="xw_bf16 %s trans=%d act=%d mask=%d"
+                      % ((M, Kd, Nn), trans, act, mask is not None))
+
+
+def nrms(a, b):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(((a - b) ** 2).mean()) / max(np.sqrt((b ** 2).mean()), 1e-12))
+
+
+@pytest.mark.parametrize("graph", ["gcn", "sgangat"])
+def test_bf16_generator_within_tolerance_of_fp32_reference(graph, bf16):
+    """configs[2] (GCN) / configs[4] (sgangat) generator forward in bf16
+    against the fp32 reference fixtures: normalised RMS error
+    ||y - y_ref|| / ||y_ref|| <= 5e-2 (measured 1.5-3.1e-2).  (Measured, not gated: per-tensor
+    parameter gradients of these random-init weights differ from fp32 by
+    20-180 % of their scale -- the GCN's unscaled randn weights,
+    models.py:567-571, grow activations ~50x per layer into saturated LSTM
+    gates, where the bf16-perturbed forward lands on different slopes; the
+    quantities training and evaluation consume hold: losses of whole
+    iterations within 2e-2, ADE / FDE within 1e-2, tests below.  bf16 is
+    opt-in; fp32 is the parity path.)"""
+    g, _ = reference_gd(graph)
+    f = npz("gen_fwd_%s.npz" % graph)
+    for b in ("synth", "zara1"):
+        with torch.no_grad():
+            y = g(T(f[b + "/obs_traj"]), T(f[b + "/obs_traj_rel"]), T(f[b + "/seq_start_end"]),
+                  T(f[b + "/obs_traj_g"]), user_noise=T(f[b + "/noise"]))
+        e = nrms(y, f[b + "/out"])
+        assert e <= 5e-2, ("bf16 G %s %s out nrms" % (graph, b), e)
+
+
+@pytest.mark.parametrize("graph", ["gcn", "sgangat"])
+def test_bf16_evaluate_all_splits(graph, bf16):
+    """configs[2] / configs[4] families: best-of-20 ADE / FDE on all five
+    test splits in bf16, within 1e-2 relative of the fp32 reference run (the
+    fp32 path holds 1e-3: test_evaluate_ade_fde_all_splits)."""
+    from sgan.evaluate import evaluate_split
+    ev = json.load(open(os.path.join(GOLDEN, "evaluate.json")))
+    g, _ = reference_gd(graph)
+    for split in SPLITS:
+        torch.manual_seed(0)
+        ade, fde = evaluate_split(g, os.path.join(GOLDEN, "datasets_group", split, "test"), num_samples=20)
+        ref = ev["%s/%s" % (graph, split)]
+        assert abs(ade - ref["ade"]) <= 1e-2 * ref["ade"], (split, ade, ref)
+        assert abs(fde - ref["fde"]) <= 1e-2 * ref["fde"], (split, fde, ref)
+
+
+@pytest.mark.parametrize("graph,sizes", [("sgangat", SIZES64), ("gcn", [20] * 12 + [7, 33])])
+def test_bf16_train_step_close_to_fp32(graph, sizes):
+    """configs[4] (sgangat, 64-ped scenes) / configs[2] (GCN) training in
+    bf16: two GanTrainer iterations; losses within 2e-2 of the same
+    iterations in fp32 (which the fixture / oracle tests pin)."""
+    from sgan import kernels as K
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer
+    batches = [synthetic_batch(sizes, seed=640 + i, device=DEV) for i in range(2)]
+    res = {}
+    for prec in ("fp32", "bf16"):
+        K.set_precision(prec)
+        try:
+            g, d = reference_gd(graph)
+            tr = GanTrainer(g, d)
+            torch.manual_seed(21)
+            random.seed(21)
+            out = []
+            for b in batches:
+                ld, lg = tr.step(b, SceneIndex.from_seq_start_end(b[-1], DEV))
+                out.append({k: float(v) for k, v in list(ld.items()) + list(lg.items())})
+            res[prec] = out
+        finally:
+            K.set_precision("fp32")
+    for a, b in zip(res["fp32"], res["bf16"]):
+        for k in a:
+            assert abs(a[k] - b[k]) <= 2e-2 * max(1.0, abs(a[k])), (k, a[k], b[k])
