@@ -146,6 +146,59 @@ def roofline_of(name, a):
                     "launch on its stream); traffic = PMC HBM bytes of the named launch (null if not profiled)"}
 
 
+def real_data_leg(dev, iters=20, warmup=3, batch=64):
+    """configs[1] on REAL data: eager training iterations over the zara1
+    train split (tests/golden/datasets_group/zara1/train, the reference's
+    datasets_group files), batch 64, consecutive loader batches to the D-step
+    and the G-step (scripts/train.py:279-297) -- the variable scene / ped
+    counts of real batches rule out one captured graph.  Batches come from
+    the device-resident data path (sgan/data/device.py: the split in HBM, one
+    gather launch per batch); the host DataLoader + .cuda() path is timed
+    beside it."""
+    from sgan.data.device import DeviceLoader, DeviceTrajectoryDataset
+    from sgan.data.trajectories_GCN import TrajectoryDataset, seq_collate
+    from sgan.scene import SceneIndex
+    from sgan.train_step import DataParallel, GanTrainer
+    from torch.utils.data import DataLoader
+    path = os.path.join(ROOT, "tests", "golden", "datasets_group", "zara1", "train")
+    if not os.path.isdir(path):
+        return None
+    dset = TrajectoryDataset(path)
+    dd = DeviceTrajectoryDataset(dset, dev)
+    out = {}
+    for mode in ("device", "host"):
+        g, d = build_models(0)
+        tr = GanTrainer(g.to(dev), d.to(dev), dp=DataParallel(), capturable=True)
+
+        def batches():
+            while True:
+                if mode == "device":
+                    yield from DeviceLoader(dd, batch_size=batch, shuffle=True)
+                else:
+                    for b in DataLoader(dset, batch_size=batch, shuffle=True, collate_fn=seq_collate):
+                        yield ([t.to(dev, non_blocking=True) for t in b[:-1]] + [b[-1]],
+                               SceneIndex.from_seq_start_end(b[-1], dev))
+        it = batches()
+        for _ in range(warmup):
+            (bd, scd), (bg, scg) = next(it), next(it)
+            tr.d_step(bd, scd)
+            tr.g_step(bg, scg)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        scenes = 0
+        for _ in range(iters):
+            (bd, scd), (bg, scg) = next(it), next(it)
+            tr.d_step(bd, scd)
+            tr.g_step(bg, scg)
+            scenes += scd.S
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out[mode] = {"value": round(scenes / dt, 2), "ms_per_iteration": round(dt / iters * 1e3, 3)}
+    return {"metric": "train-scenes/s on real data (D-step scenes per second, eager)", "split": "zara1 train",
+            "batch": batch, "iterations": iters, "num_seq": len(dset), "device_data_path": out["device"],
+            "host_data_path": out["host"], "unit": "scenes/s", "hip_graph": False}
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -227,6 +280,7 @@ def main():
     ap.add_argument("--graph-kind", dest="graph_kind", default="gat", choices=["gat", "gcn"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scaling-reference", action="store_true")
+    ap.add_argument("--no-real-data", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="capture the iteration in a HIP graph (1) or run eager (0)")
     ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--pmc-target", type=int, default=0,
@@ -300,6 +354,10 @@ def main():
                                "value(N) / (N * this value)"}
         del tr4, b4, bg4, st4
 
+    real = None
+    if world == 1 and not args.no_real_data:
+        real = real_data_leg(dev)
+
     if rank == 0:
         top = sorted(agg.items(), key=lambda kv: -kv[1]["us_per_iter"])
         dom_name, dom = top[0]
@@ -329,6 +387,8 @@ def main():
         }
         if scaling_ref is not None:
             line["scaling_reference"] = scaling_ref
+        if real is not None:
+            line["real_data"] = real
         if pmc_target is not None:
             line["pmc_target"] = pmc_target
         print(json.dumps(line), flush=True)

@@ -82,6 +82,8 @@ SIGNATURES = {
     "sgg_gatenc_fwd": (_i, [_pargs, _p]),
     "sgg_gatenc_bwd": (_i, [_pargs, _p]),
     "sgg_slab_reduce": (_i, [_p, _i, _i, _p, _p]),
+    "sgg_gather_batch_floats": (ctypes.c_longlong, [_i, _i, _i]),
+    "sgg_gather_batch": (_i, [_p, _i, _p, _i, _i, _i, _p, _p]),
     "sgg_traj_cat": (_i, [_p, _i, _i, _p, _i, _p, _i, _i, _i, _p, _p]),
     "sgg_decoder_init": (_i, [_p, _i, _i, _p, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p]),
     "sgg_l2_select": (_i, [_p, _p, _p, _i, _p, _i, _i, _i, _i, _p, _p]),

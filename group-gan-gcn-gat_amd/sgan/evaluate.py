@@ -51,7 +51,10 @@ def evaluate(args, loader, generator, num_samples, device="cuda"):
     fde_tot = torch.zeros((), dtype=torch.float64, device=device)
     total_traj = 0
     for batch in loader:
-        sc = SceneIndex.from_seq_start_end(batch[-1], device)   # host seq_start_end: no sync
+        if len(batch) == 2:          # sgan.data.device.DeviceLoader: (11-tuple on the device, SceneIndex)
+            batch, sc = batch
+        else:
+            sc = SceneIndex.from_seq_start_end(batch[-1], device)   # host seq_start_end: no sync
         batch = [t.to(device, non_blocking=True) for t in batch]
         obs_traj, pred_gt = batch[0], batch[1]
         B = pred_gt.size(1)
@@ -77,10 +80,16 @@ class _Args:
         self.__dict__.update(kw)
 
 
-def evaluate_split(generator, path, num_samples=20, batch_size=64, obs_len=8, pred_len=12, device="cuda"):
+def evaluate_split(generator, path, num_samples=20, batch_size=64, obs_len=8, pred_len=12, device="cuda",
+                   device_data=False):
     """Evaluate on one split directory with the reference's loader settings
-    (shuffle=True, host RNG)."""
-    from .data.loader import data_loader
+    (shuffle=True, host RNG); device_data=True assembles the batches in HBM
+    (sgan.data.device) in the same order."""
     a = _Args(obs_len=obs_len, pred_len=pred_len, skip=1, delim="tab", batch_size=batch_size, loader_num_workers=0)
-    _, loader = data_loader(a, path)
+    if device_data:
+        from .data.device import device_data_loader
+        _, loader = device_data_loader(a, path, device)
+    else:
+        from .data.loader import data_loader
+        _, loader = data_loader(a, path)
     return evaluate(a, loader, generator, num_samples, device)

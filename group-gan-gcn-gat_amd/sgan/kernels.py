@@ -992,6 +992,10 @@ class _TrajCat(torch.autograd.Function):
     def forward(ctx, head, a, b):
         T0, B = head.shape[0], head.shape[1]
         T1 = a.shape[0]
+        # rows of (x, y) pairs with a free step stride; anything else (e.g. the
+        # permuted views seq_collate yields, trajectories_GCN.py:33) is copied
+        fix = lambda t: t if t is None or (t.stride(1) == 2 and t.stride(2) == 1) else t.contiguous()
+        head, a, b = fix(head), fix(a), fix(b)
         for t, nm in ((head, "head"), (a, "a")) + (((b, "b"),) if b is not None else ()):
             _req(t, nm)
             assert t.shape[1:] == (B, 2) and t.stride(1) == 2 and t.stride(2) == 1, (nm, t.shape, t.stride())

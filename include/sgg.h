@@ -423,6 +423,21 @@ int sgg_l2_loss_fwd(const float* pred, int ldp, const float* gt, const float* ma
 int sgg_l2_loss_bwd(const float* pred, int ldp, const float* gt, const float* mask, int ldm, const int32_t* ped_scene,
                     const float* msum, int T, int B, float w, const float* gout, float* dpred, int ldd, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Device-resident data path (sgan/data/device.py): a split's peds live in
+ * HBM as one table of `rec` floats per ped
+ *   [abs x, y (T x 2) | rel x, y (T x 2) | group label (T) | loss mask (T) | non_linear]
+ * (T = obs_len + pred_len); one launch gathers the B ped rows of a batch
+ * (`rows`, int32, the scenes' peds in batch order) into the time-major
+ * 11-tuple of seq_collate (trajectories_GCN.py:15-42) packed in `out`
+ * (sgg_gather_batch_floats(B, ..) floats): obs_traj, pred_traj,
+ * obs_traj_rel, pred_traj_rel, obs_vel, pred_vel ((T_part x B x 2) each;
+ * velocity = 2.5 x displacement), obs_traj_g, pred_traj_g (T_part x B),
+ * non_linear_ped (B), loss_mask (B x T).  seq_start_end stays on the host. */
+long long sgg_gather_batch_floats(int B, int obs_len, int pred_len);
+int sgg_gather_batch(const float* table, int rec, const int32_t* rows, int B, int obs_len, int pred_len, float* out,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

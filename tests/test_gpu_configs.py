@@ -459,3 +459,81 @@ def test_bf16_train_step_close_to_fp32(graph, sizes):
     for a, b in zip(res["fp32"], res["bf16"]):
         for k in a:
             assert abs(a[k] - b[k]) <= 2e-2 * max(1.0, abs(a[k])), (k, a[k], b[k])
+
+
+# ---------------------------------------------------------------------------
+# device-resident data path and real-data training
+# ---------------------------------------------------------------------------
+def test_device_batches_equal_host_collate():
+    """sgg_gather_batch assembles exactly seq_collate's 11-tuple
+    (trajectories_GCN.py:15-42) for the same scenes, bitwise, and the
+    DeviceLoader yields the reference DataLoader's batch order (same host RNG
+    draws) -- zara1 train split, batch 64."""
+    from sgan.data.device import DeviceLoader, DeviceTrajectoryDataset
+    from sgan.data.trajectories_GCN import TrajectoryDataset, seq_collate
+    from torch.utils.data import DataLoader
+    dset = TrajectoryDataset(os.path.join(GOLDEN, "datasets_group", "zara1", "train"))
+    dd = DeviceTrajectoryDataset(dset, DEV)
+    torch.manual_seed(5)
+    host = [b for _, b in zip(range(4), DataLoader(dset, batch_size=64, shuffle=True, collate_fn=seq_collate))]
+    torch.manual_seed(5)
+    dev = [b for _, b in zip(range(4), DeviceLoader(dd, batch_size=64, shuffle=True))]
+    for hb, (db, sc) in zip(host, dev):
+        assert len(hb) == len(db) == 11
+        for k, (h, d) in enumerate(zip(hb, db)):
+            assert tuple(h.shape) == tuple(d.shape), (k, h.shape, d.shape)
+            assert torch.equal(h, d.cpu()), k
+        assert sc.S == hb[-1].shape[0] and sc.B == hb[0].shape[1]
+
+
+@pytest.mark.parametrize("graph,split", [("gat", "zara1"), ("vanilla", "eth")])
+def test_evaluate_with_device_data_path(graph, split):
+    """evaluate_model semantics over the device-resident batches: ADE / FDE
+    within 1e-3 of the reference run (the batch order and noise stream are
+    the reference loader's)."""
+    from sgan.evaluate import evaluate_split
+    ev = json.load(open(os.path.join(GOLDEN, "evaluate.json")))
+    g = reference_gd("gat")[0] if graph == "gat" else _vanilla_weights("vanilla")
+    torch.manual_seed(0)
+    ade, fde = evaluate_split(g, os.path.join(GOLDEN, "datasets_group", split, "test"), num_samples=20,
+                              device_data=True)
+    ref = ev["%s/%s" % (graph, split)]
+    assert abs(ade - ref["ade"]) <= 1e-3 * ref["ade"], (ade, ref)
+    assert abs(fde - ref["fde"]) <= 1e-3 * ref["fde"], (fde, ref)
+
+
+def test_real_data_training_device_path_equals_host_path():
+    """configs[1] on real data: GanTrainer iterations over zara1-train
+    batches (variable scene / ped counts, consecutive batches to the D- and
+    G-step as scripts/train.py:279-297 feeds them) from the device loader ==
+    the same iterations from the host DataLoader + .cuda() copies."""
+    from sgan.data.device import DeviceLoader, DeviceTrajectoryDataset
+    from sgan.data.trajectories_GCN import TrajectoryDataset, seq_collate
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer
+    from torch.utils.data import DataLoader
+    dset = TrajectoryDataset(os.path.join(GOLDEN, "datasets_group", "zara1", "train"))
+    res = []
+    for mode in ("host", "device"):
+        g, d = reference_gd("gat")
+        tr = GanTrainer(g, d)
+        torch.manual_seed(8)
+        random.seed(8)
+        if mode == "host":
+            it = iter(DataLoader(dset, batch_size=64, shuffle=True, collate_fn=seq_collate))
+            nxt = lambda: (lambda b: ([t.to(DEV) for t in b[:-1]] + [b[-1]],
+                                      SceneIndex.from_seq_start_end(b[-1], DEV)))(next(it))
+        else:
+            it = iter(DeviceLoader(DeviceTrajectoryDataset(dset, DEV), batch_size=64, shuffle=True))
+            nxt = lambda: next(it)
+        losses = []
+        for _ in range(2):
+            (bd, scd), (bg, scg) = nxt(), nxt()
+            ld, lg = tr.d_step(bd, scd), tr.g_step(bg, scg)
+            losses.append([float(v) for v in list(ld.values()) + list(lg.values())])
+        torch.cuda.synchronize()
+        res.append((losses, {k: v.detach().cpu().clone() for k, v in g.state_dict().items()}))
+    (la, wa), (lb, wb) = res
+    assert la == lb, (la, lb)
+    for k in wa:
+        assert torch.equal(wa[k], wb[k]), k
