@@ -164,6 +164,53 @@ __host__ __device__ inline PLayout make_playout(int nh) {
   return P;
 }
 
+// forward state of one scene kept for the backward (floats; written by the
+// forward when args.saved != NULL, read back by the backward instead of
+// recomputing the four attention layers): every layer's Wh, the head / out
+// activations, the group structure
+struct SLayout {
+  int Whi[kGatEncMaxHeads], Whio, Whg[kGatEncMaxHeads], Whgo, H1, yI, preI, gin, G1, preG, gout, ints, total;
+};
+
+__host__ __device__ inline SLayout make_slayout(int np, int nh) {
+  SLayout S;
+  int o = 0;
+  for (int h = 0; h < kGatEncMaxHeads; ++h) {
+    S.Whi[h] = o;
+    if (h < nh) o += np * FH;
+  }
+  S.Whio = o; o += np * FO;
+  for (int h = 0; h < kGatEncMaxHeads; ++h) {
+    S.Whg[h] = o;
+    if (h < nh) o += np * FH;
+  }
+  S.Whgo = o; o += np * FO;
+  S.H1 = o; o += np * FH * nh;
+  S.yI = o; o += np * FO;
+  S.preI = o; o += np * FO;
+  S.gin = o; o += np * FO;
+  S.G1 = o; o += np * FH * nh;
+  S.preG = o; o += np * FO;
+  S.gout = o; o += np * FO;
+  S.ints = o; o += 5 * np + 4;
+  S.total = (o + 3) & ~3;
+  return S;
+}
+
+// rows x cols between an LDS image at pitch ld and a dense global block
+__device__ inline void rows_to_global(float* __restrict__ dst, const float* src, int ld, int rows, int cols) {
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+    const int r = e / cols, c = e - r * cols;
+    dst[e] = src[r * ld + c];
+  }
+}
+__device__ inline void rows_from_global(float* dst, int ld, const float* __restrict__ src, int rows, int cols) {
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+    const int r = e / cols, c = e - r * cols;
+    dst[r * ld + c] = src[e];
+  }
+}
+
 __device__ __forceinline__ float lrelu(float x, float a) { return x > 0.f ? x : a * x; }
 
 // out[r][c] = sum_k in[r][k] W[k][c]   (W: K x N in LDS at pitch ldw, K % 4 == 0)
@@ -404,6 +451,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const Layout L = make_layout(p.np, p.nh, BWD);
   const PLayout PL = make_playout(p.nh);
+  const SLayout SL = make_slayout(p.np, p.nh);
   const int nh = p.nh, PH = L.PH;
   float* X = sm + L.X;
   float* H1 = sm + L.H1;
@@ -454,6 +502,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     const int o = p.scene_off[sc];
     const int n = p.scene_off[sc + 1] - o;
     if (n <= 0) continue;   // uniform over the workgroup
+    float* saved = p.saved ? p.saved + (size_t)sc * SL.total : nullptr;
     // ---- inputs and group structure ------------------------------------
     for (int e = tid; e < n * FI; e += blockDim.x) {
       const int r = e / FI, k = e - r * FI;
@@ -461,38 +510,46 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     }
     for (int i = tid; i < n; i += blockDim.x) lab[i] = p.labels[o + i];
     __syncthreads();
-    for (int i = tid; i < n; i += blockDim.x) {
-      int g = i;
-      const float li = lab[i];
-      if (li != 0.f)
-        for (int j = 0; j < i; ++j)
-          if (lab[j] == li) { g = j; break; }
-      gidl[i] = g;
-    }
-    __syncthreads();
-    for (int i = tid; i < n; i += blockDim.x) {
-      int r = 0;
-      for (int j = 0; j < gidl[i]; ++j) r += gidl[j] == j;
-      grank[i] = r;
-      int c = 0;
-      for (int j = 0; j < n; ++j) c += gidl[j] == gidl[i];
-      ginv[i] = 1.f / (float)c;
-      if (gidl[i] == i) cnt[r] = c;
-      if (i == n - 1) {
-        int m = 0;
-        for (int j = 0; j < n; ++j) m += gidl[j] == j;
-        *Mp = m;
+    if (!BWD || !p.saved) {
+      // group structure (models.py:263-278) in ONE wave, lane = ped (n <= 64):
+      // g(i) = first ped with i's non-zero label (or i), groups ranked by
+      // their first member, sizes by a lane sweep -- no workgroup barrier
+      if (tid < 64) {
+        const int i = tid;
+        const float li = i < n ? lab[i] : 0.f;
+        int g = i;
+        for (int j = 0; j < n; ++j) {
+          const float lj = __shfl(li, j);
+          if (li != 0.f && lj == li && j < g) g = j;
+        }
+        const bool lead = i < n && g == i;
+        const unsigned long long leaders = __ballot(lead);
+        int c = 0;
+        for (int j = 0; j < n; ++j) c += __shfl(g, j) == g;
+        const int r = __popcll(leaders & ((1ull << g) - 1ull));
+        if (i < n) {
+          gidl[i] = g;
+          grank[i] = r;
+          ginv[i] = 1.f / (float)c;
+          if (lead) cnt[r] = c;
+        }
+        if (i == 0) *Mp = __popcll(leaders);
       }
+      __syncthreads();
+    } else {
+      rows_from_global(lab, 5 * L.NP + 4, saved + SL.ints, 1, 5 * L.NP + 4);
+      __syncthreads();
     }
-    __syncthreads();
     const int M = *Mp;
 
+    if (!BWD || !saved) {
     // ---- intra GAT: heads (40 -> 72, ELU), out (72 nh -> 16, ELU, log_softmax)
 #pragma unroll
     for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
       if (h >= nh) break;
       lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
       __syncthreads();
+      if (saved) rows_to_global(saved + SL.Whi[h], Wh, P72, n, FH);
       scores(Wh, P72, n, FH, lw.ai[h], s, t);
       __syncthreads();
       att_fwd(Wh, P72, n, FH, gidl, s, t, p.alpha, 1, H1 + h * FH, PH, nullptr, 0, attw);
@@ -500,6 +557,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     }
     lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72);
     __syncthreads();
+    if (saved) rows_to_global(saved + SL.Whio, Wh, P72, n, FO);
     scores(Wh, P72, n, FO, lw.aio, s, t);
     __syncthreads();
     att_fwd(Wh, P72, n, FO, gidl, s, t, p.alpha, 2, yI, P16, preI, P16, attw);
@@ -519,6 +577,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       if (h >= nh) break;
       lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
       __syncthreads();
+      if (saved) rows_to_global(saved + SL.Whg[h], Wh, P72, M, FH);
       scores(Wh, P72, M, FH, lw.ag[h], s, t);
       __syncthreads();
       att_fwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, 1, G1 + h * FH, PH, nullptr, 0, attw);
@@ -526,10 +585,32 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     }
     lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72);
     __syncthreads();
+    if (saved) rows_to_global(saved + SL.Whgo, Wh, P72, M, FO);
     scores(Wh, P72, M, FO, lw.ago, s, t);
     __syncthreads();
     att_fwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, 2, gout, P16, preG, P16, attw);
     __syncthreads();
+    if (saved) {   // the activations and the group structure for the backward
+      rows_to_global(saved + SL.H1, H1, PH, n, FH * nh);
+      rows_to_global(saved + SL.yI, yI, P16, n, FO);
+      rows_to_global(saved + SL.preI, preI, P16, n, FO);
+      rows_to_global(saved + SL.gin, gin, P16, M, FO);
+      rows_to_global(saved + SL.G1, G1, PH, M, FH * nh);
+      rows_to_global(saved + SL.preG, preG, P16, M, FO);
+      rows_to_global(saved + SL.gout, gout, P16, M, FO);
+      rows_to_global(saved + SL.ints, lab, 5 * L.NP + 4, 1, 5 * L.NP + 4);
+    }
+    } else {
+      // backward with the forward's saved state: no recompute
+      rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
+      rows_from_global(yI, P16, saved + SL.yI, n, FO);
+      rows_from_global(preI, P16, saved + SL.preI, n, FO);
+      rows_from_global(gin, P16, saved + SL.gin, M, FO);
+      rows_from_global(G1, PH, saved + SL.G1, M, FH * nh);
+      rows_from_global(preG, P16, saved + SL.preG, M, FO);
+      rows_from_global(gout, P16, saved + SL.gout, M, FO);
+      __syncthreads();
+    }
 
     if (!BWD) {
       // ---- out = Woe [intra, gout[g(i)] / |g(i)|] + boe ------------------
@@ -617,7 +698,8 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     __syncthreads();
     // ---- inter out layer ----
     epi_bwd(dG, P16, preG, P16, M, FO, 2);
-    lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72);
+    if (saved) rows_from_global(Wh, P72, saved + SL.Whgo, M, FO);
+    else lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72);
     __syncthreads();
     att_bwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, lw.ago, dG, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.ago);
     wgrad(G1, PH, M, FH * nh, dWh, P72, FO, slab + PL.Wgo);
@@ -634,7 +716,8 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         const float yv = G1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
+      if (saved) rows_from_global(Wh, P72, saved + SL.Whg[h], M, FH);
+      else lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
       __syncthreads();
       att_bwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, lw.ag[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
               slab + PL.ag[h]);
@@ -650,7 +733,8 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     __syncthreads();
     // ---- intra out layer ----
     epi_bwd(dI, P16, preI, P16, n, FO, 2);
-    lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72);
+    if (saved) rows_from_global(Wh, P72, saved + SL.Whio, n, FO);
+    else lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72);
     __syncthreads();
     att_bwd(Wh, P72, n, FO, gidl, s, t, p.alpha, lw.aio, dI, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.aio);
     wgrad(H1, PH, n, FH * nh, dWh, P72, FO, slab + PL.Wio);
@@ -666,7 +750,8 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         const float yv = H1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
+      if (saved) rows_from_global(Wh, P72, saved + SL.Whi[h], n, FH);
+      else lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
       __syncthreads();
       att_bwd(Wh, P72, n, FH, gidl, s, t, p.alpha, lw.ai[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
               slab + PL.ai[h]);
@@ -729,6 +814,11 @@ using namespace sgg;
 extern "C" int sgg_gatenc_param_size(int nh) {
   if (nh < 1 || nh > kGatEncMaxHeads) return -1;
   return make_playout(nh).total;
+}
+
+extern "C" long long sgg_gatenc_saved_floats(int S, int max_n, int nh) {
+  if (S < 0 || max_n < 1 || nh < 1 || nh > kGatEncMaxHeads) return -1;
+  return (long long)S * make_slayout(max_n, nh).total;
 }
 
 extern "C" long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd) {

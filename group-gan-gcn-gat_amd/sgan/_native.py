@@ -31,7 +31,7 @@ class GatEncArgs(ctypes.Structure):
     """SggGatEncArgs (include/sgg.h)."""
     _fields_ = [("X", _p), ("ldx", _i), ("labels", _p), ("scene_off", _p), ("S", _i), ("np", _i), ("nh", _i),
                 ("alpha", _f), ("w", GatEncWeights), ("y", _p), ("ldy", _i), ("dy", _p), ("lddy", _i), ("dX", _p),
-                ("lddx", _i), ("slab", _p)]
+                ("lddx", _i), ("slab", _p), ("saved", _p)]
 
 
 _pargs = ctypes.POINTER(GatEncArgs)
@@ -79,6 +79,7 @@ SIGNATURES = {
     "sgg_bce_bwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p]),
     "sgg_gatenc_param_size": (_i, [_i]),
     "sgg_gatenc_lds_bytes": (ctypes.c_longlong, [_i, _i, _i]),
+    "sgg_gatenc_saved_floats": (ctypes.c_longlong, [_i, _i, _i]),
     "sgg_gatenc_fwd": (_i, [_pargs, _p]),
     "sgg_gatenc_bwd": (_i, [_pargs, _p]),
     "sgg_slab_reduce": (_i, [_p, _i, _i, _p, _p]),

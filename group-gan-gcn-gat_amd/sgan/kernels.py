@@ -13,6 +13,8 @@ from . import _native as N
 
 # the one-launch GATEncoder (sgg_gatenc_*); "0" forces the per-layer kernels
 GATENC_FUSED = os.environ.get("SGG_GATENC_FUSED", "1") != "0"
+# the fused GATEncoder forward keeps its layer state for the backward (0: the backward recomputes it)
+GATENC_SAVE = os.environ.get("SGG_GATENC_SAVE", "1") != "0"
 
 
 def _lib():
@@ -568,8 +570,11 @@ def gat_attention(wh, a, alpha, graph, epilogue, heads=1, bias=None):
 
 class _GatEnc(torch.autograd.Function):
     """The whole GATEncoder of every scene in one launch (sgg_gatenc_fwd);
-    backward = one recompute + back-propagation launch (sgg_gatenc_bwd) + the
-    scene-ordered slab sum of the parameter gradients (sgg_slab_reduce).
+    when a gradient is needed the forward also writes each scene's layer
+    state (Wh of every layer, activations, group structure) to a saved buffer
+    (sgg_gatenc_saved_floats) and the backward is one back-propagation launch
+    over it (sgg_gatenc_bwd, no forward recompute) + the scene-ordered slab
+    sum of the parameter gradients (sgg_slab_reduce).
     params: [W_h, a_h for each intra head], W_out, a_out (intra), the same for
     the inter GAT, out_embedding weight, bias -- the slab order of sgg.h."""
 
@@ -582,20 +587,26 @@ class _GatEnc(torch.autograd.Function):
         ps = [_req(q, "gat weight").contiguous() for q in params]
         a = _gatenc_args(x, labels, scenes, nh, alpha, ps)
         a.y, a.ldy = N.ptr(y), 24
+        saved = None
+        if any(ctx.needs_input_grad) and GATENC_SAVE:
+            nf = int(lib.sgg_gatenc_saved_floats(max(scenes.S, 1), a.np, nh))
+            saved = torch.empty(max(nf, 1), device=x.device, dtype=torch.float32)
+            a.saved = N.ptr(saved)
         N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_fwd")
         if timer.active:
-            keep = (x, y, labels, scenes, ps)   # the replay closure holds every buffer `a` points to
-            timer.add("sgg::gatenc_kernel<false>", (scenes.S, B, nh), _gatenc_flops(scenes, nh), 4.0 * B * (40 + 1 + 24),
+            keep = (x, y, labels, scenes, ps, saved)   # the replay closure holds every buffer `a` points to
+            timer.add("sgg::gatenc_kernel<false>", (scenes.S, B, nh), _gatenc_flops(scenes, nh),
+                      4.0 * B * (40 + 1 + 24) + (_gatenc_saved_bytes(B, nh) if saved is not None else 0.0),
                       lambda a=a, keep=keep: N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()),
                                                      "sgg_gatenc_fwd"))
         ctx.meta = (labels, scenes, nh, alpha)
-        ctx.save_for_backward(x, *ps)
+        ctx.save_for_backward(x, saved, *ps)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = _lib()
-        x, *ps = ctx.saved_tensors
+        x, saved, *ps = ctx.saved_tensors
         labels, scenes, nh, alpha = ctx.meta
         dy = _rows(dy, "dy")
         B = x.shape[0]
@@ -606,11 +617,12 @@ class _GatEnc(torch.autograd.Function):
         a.dy, a.lddy = N.ptr(dy), dy.stride(0)
         a.dX, a.lddx = N.ptr(dx), 40
         a.slab = N.ptr(slab)
+        a.saved = N.ptr(saved)
         N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_bwd")
         if timer.active:
-            keep = (x, dy, dx, slab, labels, scenes, ps)
+            keep = (x, dy, dx, slab, labels, scenes, ps, saved)
             timer.add("sgg::gatenc_kernel<true>", (scenes.S, B, nh), 3.0 * _gatenc_flops(scenes, nh),
-                      4.0 * (B * (40 + 1 + 24 + 40) + scenes.S * P),
+                      4.0 * (B * (40 + 1 + 24 + 40) + scenes.S * P) + _gatenc_saved_bytes(B, nh),
                       lambda a=a, keep=keep: N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()),
                                                      "sgg_gatenc_bwd"))
         flat = torch.empty(P, device=x.device, dtype=torch.float32)
@@ -632,6 +644,13 @@ def _gatenc_flops(scenes, nh):
     node = 2 * n * (40 * 72 * nh + 72 * nh * 16) + 2 * n * (16 * 72 * nh + 72 * nh * 16) + 2 * n * 32 * 24
     edge = 2 * n * n * 3 * (72 * nh + 16)
     return float((node + edge).sum())
+
+
+def _gatenc_saved_bytes(B, nh):
+    """Saved forward state per launch (upper bound: as many groups as peds):
+    every layer's Wh (72 nh + 16, twice), H1 / G1 (72 nh each), the 16-wide
+    activations (yI, preI, gin, preG, gout) and 5 words of group structure."""
+    return 4.0 * B * (4 * 72 * nh + 2 * 16 + 5 * 16 + 5)
 
 
 def _gatenc_args(x, labels, scenes, nh, alpha, ps):

@@ -375,9 +375,15 @@ typedef struct {
   float* dX;
   int lddx;
   float* slab;
+  float* saved;   /* may be NULL: S x sgg_gatenc_saved_floats(1, np, nh) floats of forward state */
 } SggGatEncArgs;
 
 int sgg_gatenc_param_size(int nh);
+/* Forward state kept for the backward: when args->saved != NULL the forward
+ * writes every scene's layer inputs / activations and group structure there
+ * and the backward reads them instead of recomputing the forward (it must
+ * then be called with the same saved buffer, np and nh). */
+long long sgg_gatenc_saved_floats(int S, int max_n, int nh);
 long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd);
 int sgg_gatenc_fwd(const SggGatEncArgs* args, void* stream);
 int sgg_gatenc_bwd(const SggGatEncArgs* args, void* stream);
