@@ -28,6 +28,8 @@
 // with lane j (n <= 64), row max / sum by wave shuffles.
 #include "sgg_common.h"
 
+
+
 namespace sgg {
 
 namespace {
@@ -36,7 +38,10 @@ namespace {
 // 20-ped scene are ~1 per wave / thread, so the dependent chains overlap);
 // the same for the backward
 constexpr int kFwdThreads = 1024, kBwdThreads = 1024;
-constexpr int kMaxWaves = kFwdThreads / 64;
+#ifndef SGG_GATENC_GRID_CAP
+#define SGG_GATENC_GRID_CAP 65536
+#endif
+constexpr int kGridCap = SGG_GATENC_GRID_CAP;   // workgroups (scenes loop over them); a probe build lowers it
 constexpr int FI = 40, FH = 72, FO = 16, FE = 24;   // GATEncoder dims (models.py:242-244)
 constexpr int P40 = FI + 1, P72 = FH + 1, P16 = FO + 1;
 
@@ -61,36 +66,115 @@ struct LW {
   const float* boe;
 };
 
-// copy a K x N row-major global matrix to LDS at pitch N + 1; each thread
-// issues its (up to 4 per round) loads before any store, so a matrix costs
-// one memory latency per 4 trips instead of one per trip
-__device__ inline float* stage_mat(float* dst, const float* __restrict__ src, int K, int N, int nthreads) {
-  const int tot = K * N;
-  for (int e0 = threadIdx.x; e0 < tot; e0 += 4 * nthreads) {
-    float v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = src[min(e0 + u * nthreads, tot - 1)];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * nthreads;
-      if (e < tot) {
-        const int k = e / N, c = e - k * N;
-        dst[k * (N + 1) + c] = v[u];
-      }
+// The module's weights to LDS in ONE memory round trip.  The host lays the
+// 22 segments (per head Wi, ai; Wio, aio; per head Wg, ag; Wgo, ago; Woe,
+// boe -- unused heads have length 0) out as 8-float chunks (a segment starts
+// on a chunk); thread c copies chunk c: 8 loads in flight, then the stores
+// into the LDS image (matrices at pitch N + 1, vectors packed).
+constexpr int kSegs = 4 * kGatEncMaxHeads + 6;
+constexpr int kChunk = 8;
+struct StageTab {
+  const float* src[kSegs];
+  int coff[kSegs];   // first chunk (non-decreasing)
+  int len[kSegs];    // floats
+  int dst[kSegs];    // LDS image offset
+  int rowN[kSegs];   // matrix row length (pitch rowN + 1); 0: vector
+  int nchunks;
+  int floats;        // LDS image size
+};
+
+inline StageTab make_stage_tab(const SggGatEncWeights& w, int nh) {
+  StageTab T = {};
+  int q = 0, ch = 0;
+  auto put = [&](int sl, const float* sp, int K, int N, bool mat, bool live) {
+    T.src[sl] = sp;
+    T.coff[sl] = ch;
+    T.len[sl] = live ? K * N : 0;
+    T.dst[sl] = q;
+    T.rowN[sl] = mat ? N : 0;
+    if (live) {
+      ch += (K * N + kChunk - 1) / kChunk;
+      q += mat ? K * (N + 1) : K * N;
     }
+  };
+  for (int h = 0; h < kGatEncMaxHeads; ++h) {
+    put(2 * h, w.Wi[h], FI, FH, true, h < nh);
+    put(2 * h + 1, w.ai[h], 2 * FH, 1, false, h < nh);
   }
-  return dst + K * (N + 1);
+  put(2 * kGatEncMaxHeads, w.Wio, FH * nh, FO, true, true);
+  put(2 * kGatEncMaxHeads + 1, w.aio, 2 * FO, 1, false, true);
+  for (int h = 0; h < kGatEncMaxHeads; ++h) {
+    put(2 * kGatEncMaxHeads + 2 + 2 * h, w.Wg[h], FO, FH, true, h < nh);
+    put(2 * kGatEncMaxHeads + 3 + 2 * h, w.ag[h], 2 * FH, 1, false, h < nh);
+  }
+  put(4 * kGatEncMaxHeads + 2, w.Wgo, FH * nh, FO, true, true);
+  put(4 * kGatEncMaxHeads + 3, w.ago, 2 * FO, 1, false, true);
+  put(4 * kGatEncMaxHeads + 4, w.Woe, FE, 2 * FO, true, true);
+  put(4 * kGatEncMaxHeads + 5, w.boe, FE, 1, false, true);
+  T.nchunks = ch;
+  T.floats = q;
+  return T;
 }
-__device__ inline float* stage_vec(float* dst, const float* __restrict__ src, int n, int nthreads) {
-  for (int e = threadIdx.x; e < n; e += nthreads) dst[e] = src[e];
-  return dst + n;
+
+__device__ inline void stage_weights(float* base, const StageTab& T, LW& lw) {
+  lw.Wi[0] = base + T.dst[0];
+  lw.ai[0] = base + T.dst[1];
+  lw.Wio = base + T.dst[2 * kGatEncMaxHeads];
+  lw.aio = base + T.dst[2 * kGatEncMaxHeads + 1];
+  lw.Wg[0] = base + T.dst[2 * kGatEncMaxHeads + 2];
+  lw.ag[0] = base + T.dst[2 * kGatEncMaxHeads + 3];
+  lw.Wgo = base + T.dst[4 * kGatEncMaxHeads + 2];
+  lw.ago = base + T.dst[4 * kGatEncMaxHeads + 3];
+  lw.Woe = base + T.dst[4 * kGatEncMaxHeads + 4];
+  lw.boe = base + T.dst[4 * kGatEncMaxHeads + 5];
+  for (int c = threadIdx.x; c < T.nchunks; c += blockDim.x) {
+    int seg = 0;
+#pragma unroll
+    for (int k = 1; k < kSegs; ++k)
+      if (c >= T.coff[k]) seg = k;
+    const float* sp = T.src[0];
+    int len = 0, dst = 0, N = 0, c0 = 0;
+#pragma unroll
+    for (int k = 0; k < kSegs; ++k)
+      if (seg == k) {
+        sp = T.src[k];
+        len = T.len[k];
+        dst = T.dst[k];
+        N = T.rowN[k];
+        c0 = T.coff[k];
+      }
+    const int r0 = (c - c0) * kChunk;
+    float v[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u) v[u] = r0 + u < len ? sp[r0 + u] : 0.f;
+    int row = N ? r0 / N : 0, col = N ? r0 - row * N : r0;
+    int d = dst + (N ? row * (N + 1) + col : r0);
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u)
+      if (r0 + u < len) {
+        base[d++] = v[u];
+        if (N && ++col == N) {   // next row (chunks are shorter than a row)
+          col = 0;
+          ++d;
+        }
+      }
+  }
 }
+
+// int region of a scene: lab (float), gidl, grank, cnt, ginv (float), M, then
+// the groups' member masks (64-bit, 8-byte aligned)
+__host__ __device__ inline int gm_offset(int np) { return (5 * np + 4 + 1) & ~1; }
+__host__ __device__ inline int ints_floats(int np) { return gm_offset(np) + 2 * np; }
+// attention matrix pitch: >= the 4-padded row count (the aggregation's
+// reduction reads columns up to it), odd
+__host__ __device__ inline int att_pitch(int np) { return (((np + 3) & ~3)) | 1; }
+constexpr int kScoreTiles = (FH + 15) / 16;   // score partial sums: one per 16-column tile
 
 struct Layout {
   // float offsets into the workgroup's LDS
-  int X, H1, yI, preI, gin, G1, preG, gout, Wh, s, t, ds, dt, att;   // forward
-  int dWh, dH, dI, dG, dpre, attm;                                    // backward
-  int ints;       // int region: lab (float), gidl, grank, cnt, M
+  int X, H1, yI, preI, gin, G1, preG, gout, Wh, s, t, sp, tp, attm;   // forward
+  int dWh, dH, dI, dG, dpre, dz, ds, dt;                             // backward
+  int ints;       // see ints_floats
   int wts;        // the module's weights, staged once per workgroup (odd row pitches)
   int total;      // floats
   int PH, NP, NPP;
@@ -100,7 +184,7 @@ __host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
   Layout L;
   L.NP = np;
   L.PH = FH * nh + 1;
-  L.NPP = np | 1;
+  L.NPP = att_pitch(np);
   int o = 0;
   auto take = [&](int n) { const int r = o; o += (n + 3) & ~3; return r; };
   L.X = take(np * P40);
@@ -114,20 +198,22 @@ __host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
   L.Wh = take(np * P72);
   L.s = take(np);
   L.t = take(np);
-  L.ds = take(np);
-  L.dt = take(np);
-  L.att = take(kMaxWaves * 64);
+  L.sp = take(kScoreTiles * np);
+  L.tp = take(kScoreTiles * np);
+  L.attm = take(np * L.NPP);
   if (bwd) {
     L.dWh = take(np * P72);
     L.dH = take(np * L.PH);
     L.dI = take(np * P16);
     L.dG = take(np * P16);
     L.dpre = take(np * P16);
-    L.attm = take(np * L.NPP);
+    L.dz = take(np * L.NPP);
+    L.ds = take(np);
+    L.dt = take(np);
   } else {
-    L.dWh = L.dH = L.dI = L.dG = L.dpre = L.attm = 0;
+    L.dWh = L.dH = L.dI = L.dG = L.dpre = L.dz = L.ds = L.dt = 0;
   }
-  L.ints = take(5 * np + 4);
+  L.ints = take(ints_floats(np));
   L.wts = take(weights_floats(nh));
   L.total = o;
   return L;
@@ -144,7 +230,7 @@ __host__ __device__ inline PLayout make_playout(int nh) {
   int o = 0;
 #pragma unroll
   for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
+    if (h >= nh) break;
     P.Wi[h] = o; o += FI * FH;
     P.ai[h] = o; o += 2 * FH;
   }
@@ -152,7 +238,7 @@ __host__ __device__ inline PLayout make_playout(int nh) {
   P.aio = o; o += 2 * FO;
 #pragma unroll
   for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
+    if (h >= nh) break;
     P.Wg[h] = o; o += FO * FH;
     P.ag[h] = o; o += 2 * FH;
   }
@@ -166,10 +252,12 @@ __host__ __device__ inline PLayout make_playout(int nh) {
 
 // forward state of one scene kept for the backward (floats; written by the
 // forward when args.saved != NULL, read back by the backward instead of
-// recomputing the four attention layers): every layer's Wh, the head / out
-// activations, the group structure
+// recomputing the four attention layers): every layer's Wh and attention
+// scores s | t, the head / out activations, the group structure
 struct SLayout {
-  int Whi[kGatEncMaxHeads], Whio, Whg[kGatEncMaxHeads], Whgo, H1, yI, preI, gin, G1, preG, gout, ints, total;
+  int Whi[kGatEncMaxHeads], Whio, Whg[kGatEncMaxHeads], Whgo;
+  int sti[kGatEncMaxHeads], stio, stg[kGatEncMaxHeads], stgo;
+  int H1, yI, preI, gin, G1, preG, gout, ints, total;
 };
 
 __host__ __device__ inline SLayout make_slayout(int np, int nh) {
@@ -177,14 +265,18 @@ __host__ __device__ inline SLayout make_slayout(int np, int nh) {
   int o = 0;
   for (int h = 0; h < kGatEncMaxHeads; ++h) {
     S.Whi[h] = o;
-    if (h < nh) o += np * FH;
+    S.sti[h] = o + np * FH;
+    if (h < nh) o += np * FH + 2 * np;
   }
   S.Whio = o; o += np * FO;
+  S.stio = o; o += 2 * np;
   for (int h = 0; h < kGatEncMaxHeads; ++h) {
     S.Whg[h] = o;
-    if (h < nh) o += np * FH;
+    S.stg[h] = o + np * FH;
+    if (h < nh) o += np * FH + 2 * np;
   }
   S.Whgo = o; o += np * FO;
+  S.stgo = o; o += 2 * np;
   S.H1 = o; o += np * FH * nh;
   S.yI = o; o += np * FO;
   S.preI = o; o += np * FO;
@@ -192,7 +284,7 @@ __host__ __device__ inline SLayout make_slayout(int np, int nh) {
   S.G1 = o; o += np * FH * nh;
   S.preG = o; o += np * FO;
   S.gout = o; o += np * FO;
-  S.ints = o; o += 5 * np + 4;
+  S.ints = (o + 1) & ~1; o = S.ints + ints_floats(np);
   S.total = (o + 3) & ~3;
   return S;
 }
@@ -213,137 +305,216 @@ __device__ inline void rows_from_global(float* dst, int ld, const float* __restr
 
 __device__ __forceinline__ float lrelu(float x, float a) { return x > 0.f ? x : a * x; }
 
-// out[r][c] = sum_k in[r][k] W[k][c]   (W: K x N in LDS at pitch ldw, K % 4 == 0)
-__device__ void lin(const float* in, int ldi, int rows, int K, const float* W, int ldw, int N, float* out, int ldo) {
-  for (int e = threadIdx.x; e < rows * N; e += blockDim.x) {
-    const int r = e / N, c = e - r * N;
-    const float* x = in + r * ldi;
-    const float* w = W + c;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = 0; k < K; k += 4) {
-      a0 = fmaf(x[k], w[k * ldw], a0);
-      a1 = fmaf(x[k + 1], w[(k + 1) * ldw], a1);
-      a2 = fmaf(x[k + 2], w[(k + 2) * ldw], a2);
-      a3 = fmaf(x[k + 3], w[(k + 3) * ldw], a3);
+// ---------------------------------------------------------------------------
+// cross-lane reductions on DPP lane moves (VALU; the shuffle forms cost an LDS
+// round trip per step).  Every lane ends with the bitwise-same value (each
+// step adds a lane pair in both orders, and + / max commute exactly).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ float dpp(float v, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+// over each row of 16 lanes
+__device__ __forceinline__ float row_sum(float v) {
+  v += dpp<0xB1>(v, 0.f);    // quad_perm [1, 0, 3, 2]
+  v += dpp<0x4E>(v, 0.f);    // quad_perm [2, 3, 0, 1]
+  v += dpp<0x141>(v, 0.f);   // row_half_mirror
+  v += dpp<0x140>(v, 0.f);   // row_mirror
+  return v;
+}
+__device__ __forceinline__ float row_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v, -INFINITY));
+  v = fmaxf(v, dpp<0x4E>(v, -INFINITY));
+  v = fmaxf(v, dpp<0x141>(v, -INFINITY));
+  v = fmaxf(v, dpp<0x140>(v, -INFINITY));
+  return v;
+}
+__device__ __forceinline__ float lane63(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// over the wave: rows, then row_bcast:15 into rows 1 / 3 and row_bcast:31
+// into rows 2 / 3; lane 63 holds the total, broadcast by readlane
+__device__ __forceinline__ float wsum(float v) {
+  v = row_sum(v);
+  v += dpp<0x142, 0xA>(v, 0.f);
+  v += dpp<0x143, 0xC>(v, 0.f);
+  return lane63(v);
+}
+__device__ __forceinline__ float wmax(float v) {
+  v = row_max(v);
+  v = fmaxf(v, dpp<0x142, 0xA>(v, -INFINITY));
+  v = fmaxf(v, dpp<0x143, 0xC>(v, -INFINITY));
+  return lane63(v);
+}
+
+// ---------------------------------------------------------------------------
+// Matrix products on the f32 MFMA (v_mfma_f32_16x16x4_f32): 16 x 16 output
+// tiles, one wavefront per tile (tiles dealt round-robin over the
+// workgroup's waves, starting at wave `first` so that two products issued in
+// one phase share the waves out).  Operand lanes: A[i = lane & 15][k = lane >>
+// 4], B[k = lane >> 4][j = lane & 15]; the D lane holds rows 4 (lane >> 4) + r,
+// column lane & 15.  Rows / columns past the edge read a clamped (valid)
+// element and are not stored; a reduction over rows masks them to zero.
+__device__ __forceinline__ int mm_wave(int first) {
+  const int nw = blockDim.x >> 6;
+  return ((int)(threadIdx.x >> 6) + nw - first % nw) % nw;
+}
+
+// out[r][c] = sum_k in[r][k] W[k][c]   (W: K x N in LDS at pitch ldw, K % 4 == 0).
+// With a (2N: a_src | a_dst), also the attention score partials of the tile:
+// sp[tile column][r] = sum over its 16 columns of out[r][c] a[c], tp the same
+// with a[N + c] (att_rows sums the column tiles).
+__device__ void lin(const float* in, int ldi, int rows, int K, const float* W, int ldw, int N, float* out, int ldo,
+                    int first = 0, const float* a = nullptr, float* sp = nullptr, float* tp = nullptr, int np = 0) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
+  const int ct = (N + 15) >> 4, nt = ((rows + 15) >> 4) * ct;
+  for (int tile = mm_wave(first); tile < nt; tile += nw) {
+    const int r0 = (tile / ct) << 4, c0 = (tile % ct) << 4;
+    const float* pa = in + min(r0 + i, rows - 1) * ldi + kq;
+    const float* pb = W + kq * ldw + min(c0 + i, N - 1);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int k = 0; k < K; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k], pb[k * ldw], acc, 0, 0, 0);
+    const int col = c0 + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + 4 * kq + r;
+      if (row < rows && col < N) out[row * ldo + col] = acc[r];
     }
-    out[r * ldo + c] = (a0 + a1) + (a2 + a3);
+    if (a) {
+      const float as = col < N ? a[col] : 0.f, at = col < N ? a[N + col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ps = row_sum(acc[r] * as), pt = row_sum(acc[r] * at);
+        const int row = r0 + 4 * kq + r;
+        if (i == 0 && row < rows) {
+          sp[(c0 >> 4) * np + row] = ps;
+          tp[(c0 >> 4) * np + row] = pt;
+        }
+      }
+    }
   }
 }
 
-// out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin; N % 4 == 0)
+// out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin; N % 4 == 0;
+// out may be global memory)
 __device__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, int ldw, int K, float* out, int ldo,
-                      bool acc) {
-  for (int e = threadIdx.x; e < rows * K; e += blockDim.x) {
-    const int r = e / K, k = e - r * K;
-    const float* dr = d + r * ldd;
-    const float* wr = W + k * ldw;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int c = 0; c < N; c += 4) {
-      a0 = fmaf(dr[c], wr[c], a0);
-      a1 = fmaf(dr[c + 1], wr[c + 1], a1);
-      a2 = fmaf(dr[c + 2], wr[c + 2], a2);
-      a3 = fmaf(dr[c + 3], wr[c + 3], a3);
+                      bool accum, int first = 0) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
+  const int ct = (K + 15) >> 4, nt = ((rows + 15) >> 4) * ct;
+  for (int tile = mm_wave(first); tile < nt; tile += nw) {
+    const int r0 = (tile / ct) << 4, k0 = (tile % ct) << 4;
+    const float* pa = d + min(r0 + i, rows - 1) * ldd + kq;
+    const float* pb = W + min(k0 + i, K - 1) * ldw + kq;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int c = 0; c < N; c += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[c], pb[c], acc, 0, 0, 0);
+    const int col = k0 + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + 4 * kq + r;
+      if (row < rows && col < K) {
+        float* po = out + row * ldo + col;
+        *po = accum ? *po + acc[r] : acc[r];
+      }
     }
-    const float v = (a0 + a1) + (a2 + a3);
-    out[r * ldo + k] = acc ? out[r * ldo + k] + v : v;
   }
 }
 
-// dst[k][c] = sum_r x[r][k] d[r][c]   (weight gradient of lin, to the slab)
-__device__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, int ldd, int N, float* dst) {
-  for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
-    const int k = e / N, c = e - k * N;
-    float a0 = 0.f, a1 = 0.f;
-    int r = 0;
-    for (; r + 1 < rows; r += 2) {
-      a0 = fmaf(x[r * ldx + k], d[r * ldd + c], a0);
-      a1 = fmaf(x[(r + 1) * ldx + k], d[(r + 1) * ldd + c], a1);
+// dst[k][c] = sum_r x[r][k] d[r][c]  (weight gradient of lin: to the slab,
+// ldo = N; or an LDS image)
+__device__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, int ldd, int N, float* dst, int ldo,
+                      int first = 0) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
+  const int ct = (N + 15) >> 4, nt = ((K + 15) >> 4) * ct;
+  for (int tile = mm_wave(first); tile < nt; tile += nw) {
+    const int k0 = (tile / ct) << 4, c0 = (tile % ct) << 4;
+    const float* pa = x + min(k0 + i, K - 1);
+    const float* pb = d + min(c0 + i, N - 1);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int r = kq; r < rows + kq; r += 4) {   // the lane's row r; the step covers rows r - kq .. r - kq + 3
+      const bool ok = r < rows;
+      const float av = ok ? pa[r * ldx] : 0.f, bv = ok ? pb[r * ldd] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
     }
-    if (r < rows) a0 = fmaf(x[r * ldx + k], d[r * ldd + c], a0);
-    dst[e] = a0 + a1;
-  }
-}
-
-// s_i = a[:F].Wh_i, t_i = a[F:].Wh_i: one wavefront per dot product (lanes
-// over the F <= 128 features, a wave-shuffle sum) instead of an F-long
-// serial chain of LDS reads per thread
-__device__ void scores(const float* Wh, int ldw, int rows, int F, const float* a, float* s, float* t) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int e = wave; e < 2 * rows; e += nw) {
-    const int r = e >> 1, w = e & 1;
-    const float* av = a + w * F;
-    const float* x = Wh + r * ldw;
-    float v = lane < F ? x[lane] * av[lane] : 0.f;
-    if (lane + 64 < F) v = fmaf(x[lane + 64], av[lane + 64], v);
-    v = wave_sum(v);
-    if (lane == 0) (w ? t : s)[r] = v;
+    const int col = c0 + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = k0 + 4 * kq + r;
+      if (row < K && col < N) dst[row * ldo + col] = acc[r];
+    }
   }
 }
 
 __device__ __forceinline__ bool edge(const int* gidl, int i, int j) { return gidl == nullptr || gidl[i] == gidl[j]; }
 
-// softmax row i of the attention, lane j (n <= 64)
-__device__ __forceinline__ float att_row(int i, int rows, const int* gidl, const float* s, const float* t, float alpha,
-                                         int lane) {
-  const bool ok = lane < rows && edge(gidl, i, lane);
-  const float e = ok ? lrelu(s[i] + t[lane], alpha) : -INFINITY;
-  const float m = wave_max(e);
-  const float p = ok ? __expf(e - m) : 0.f;
-  const float sum = wave_sum(p);
-  return p / sum;
+// s_i / t_i from lin's score partials (ct column tiles)
+__device__ __forceinline__ float score_of(const float* part, int ct, int np, int i) {
+  float v = part[i];
+  for (int c = 1; c < ct; ++c) v += part[c * np + i];
+  return v;
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// attention rows (one wavefront per row i, lane j; rows <= 64): att_ij =
+// softmax_j(LeakyReLU(s_i + t_j)) over the graph's edges, to attm (columns
+// up to the 4-padded row count, zero past the rows).  s / t from lin's
+// partials (ct >= 1) or, ct == 0, already in s / t.  Writes s / t (and the
+// saved copy sv: s | t, when given).
+__device__ void att_rows(int rows, int ct, const float* sp, const float* tp, int np, const int* gidl, float alpha,
+                         float* s, float* t, float* attm, int npp, float* sv) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int cols = (rows + 3) & ~3;
+  for (int i = threadIdx.x >> 6; i < rows; i += nw) {
+    const int j = min(lane, rows - 1);
+    const float si = ct ? score_of(sp, ct, np, i) : s[i];
+    const float tj = ct ? score_of(tp, ct, np, j) : t[j];
+    const bool ok = lane < rows && edge(gidl, i, lane);
+    const float e = ok ? lrelu(si + tj, alpha) : -INFINITY;
+    const float m = wmax(e);
+    const float pe = ok ? __expf(e - m) : 0.f;
+    const float sum = wsum(pe);
+    if (lane < cols) attm[i * npp + lane] = pe / sum;
+    if (ct) {
+      if (lane == 0) s[i] = si;
+      if (lane == i) t[i] = tj;
+      if (sv) {
+        if (lane == 0) sv[i] = si;
+        if (lane == i) sv[np + i] = tj;
+      }
+    }
+  }
 }
 
-// attention layer forward: out = epi(att . Wh); pre (optional) = att . Wh
-// epi: 1 ELU, 2 ELU + log_softmax over the F features
-__device__ void att_fwd(const float* Wh, int ldw, int rows, int F, const int* gidl, const float* s, const float* t,
-                        float alpha, int epi, float* out, int ldo, float* pre, int ldp, float* attw) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* aw = attw + wave * 64;
-  for (int i = wave; i < rows; i += (int)(blockDim.x >> 6)) {
-    aw[lane] = att_row(i, rows, gidl, s, t, alpha, lane);
-    wave_lds_sync();
-    float hv[2], zv[2], zmax = -INFINITY;
+// out = epi(att Wh) on the MFMA (reduction over the rows' 4-padded columns
+// of attm; B rows past the edge clamp, their A columns are zero).  epi 1:
+// ELU; epi 2 (F == 16: a row is one lane row): pre = att Wh, out =
+// log_softmax(ELU(pre)) over the 16 features
+__device__ void att_agg(const float* attm, int npp, int rows, const float* Wh, int ldw, int F, int epi, float* out,
+                        int ldo, float* pre, int ldp) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
+  const int ct = (F + 15) >> 4, nt = ((rows + 15) >> 4) * ct;
+  const int K = (rows + 3) & ~3;
+  for (int tile = threadIdx.x >> 6; tile < nt; tile += nw) {
+    const int r0 = (tile / ct) << 4, c0 = (tile % ct) << 4;
+    const float* pa = attm + min(r0 + i, rows - 1) * npp + kq;
+    const float* pb = Wh + min(c0 + i, F - 1);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k], pb[min(k + kq, rows - 1) * ldw], acc, 0, 0, 0);
+    const int col = c0 + i;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int f = lane + 64 * c;
-      float acc = 0.f, acc2 = 0.f;
-      if (f < F) {
-        int j = 0;
-        for (; j + 1 < rows; j += 2) {
-          acc = fmaf(aw[j], Wh[j * ldw + f], acc);
-          acc2 = fmaf(aw[j + 1], Wh[(j + 1) * ldw + f], acc2);
-        }
-        if (j < rows) acc = fmaf(aw[j], Wh[j * ldw + f], acc);
-        acc += acc2;
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + 4 * kq + r;
+      const float z = elu(acc[r]);
+      float v = z;
+      if (epi == 2) {
+        const float zm = row_max(z);
+        const float lse = zm + __logf(row_sum(__expf(z - zm)));
+        v = z - lse;
       }
-      hv[c] = acc;
-      zv[c] = elu(acc);
-      if (f < F) zmax = fmaxf(zmax, zv[c]);
-    }
-    float lse = 0.f;
-    if (epi == 2) {
-      zmax = wave_max(zmax);
-      float se = 0.f;
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        if (lane + 64 * c < F) se += __expf(zv[c] - zmax);
-      lse = zmax + __logf(wave_sum(se));
-    }
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int f = lane + 64 * c;
-      if (f < F) {
-        if (pre) pre[i * ldp + f] = hv[c];
-        out[i * ldo + f] = epi == 2 ? zv[c] - lse : zv[c];
+      if (row < rows && col < F) {
+        out[row * ldo + col] = v;
+        if (pre) pre[row * ldp + col] = acc[r];
       }
     }
-    wave_lds_sync();   // aw is rewritten by the wave's next row
   }
 }
 
@@ -366,13 +537,13 @@ __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, 
     }
     float lse = 0.f;
     if (epi == 2) {
-      zmax = wave_max(zmax);
-      sdy = wave_sum(sdy);
+      zmax = wmax(zmax);
+      sdy = wsum(sdy);
       float se = 0.f;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         if (lane + 64 * c < F) se += __expf(zv[c] - zmax);
-      lse = zmax + __logf(wave_sum(se));
+      lse = zmax + __logf(wsum(se));
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -386,55 +557,42 @@ __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, 
   }
 }
 
-// attention layer backward.  dpre: gradient of the aggregate (rows x F);
-// writes dWh (rows x F) and the a-gradient (2F) to da; attm scratch rows x npp
-__device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gidl, float* s, float* t, float alpha,
-                        const float* a, const float* dpre, int ldd, float* dWh, int lddw, float* ds,
-                        float* dt, float* attm, int npp, float* da) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  scores(Wh, ldw, rows, F, a, s, t);
-  __syncthreads();
-  for (int i = wave; i < rows; i += (int)(blockDim.x >> 6)) {
-    const float v = att_row(i, rows, gidl, s, t, alpha, lane);
-    if (lane < rows) attm[i * npp + lane] = v;
-  }
-  __syncthreads();
-  // attention-weighted part: dWh_j = sum_i att_ij dpre_i
-  for (int e = threadIdx.x; e < rows * F; e += blockDim.x) {
-    const int j = e / F, f = e - j * F;
-    float acc = 0.f;
-    for (int i = 0; i < rows; ++i) acc = fmaf(attm[i * npp + j], dpre[i * ldd + f], acc);
-    dWh[j * lddw + f] = acc;
-  }
-  __syncthreads();   // attm is overwritten with dz below
-  for (int i = wave; i < rows; i += (int)(blockDim.x >> 6)) {
-    const int j = lane;
-    float datt = 0.f, at = 0.f;
-    if (j < rows) {
-      at = attm[i * npp + j];
-      for (int f = 0; f < F; ++f) datt = fmaf(dpre[i * ldd + f], Wh[j * ldw + f], datt);
-    }
-    const float dot = wave_sum(at * datt);
-    float dz = 0.f;
-    if (j < rows) {
-      const float de = at * (datt - dot);
-      dz = (s[i] + t[j]) > 0.f ? de : alpha * de;
-      attm[i * npp + j] = dz;
-    }
-    const float dsum = wave_sum(dz);
+// attention layer backward, s / t / Wh in LDS.  dpre: gradient of the
+// aggregate (rows x F).  Writes dWh (rows x F) and starts the a-gradient
+// (2F, to da) in the last phase WITHOUT a closing barrier: the caller adds
+// its weight / input gradient products to that phase.  attm, dz: scratch
+// rows x npp.
+__device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gidl, const float* s, const float* t,
+                        float alpha, const float* a, const float* dpre, int ldd, float* dWh, int lddw, float* ds,
+                        float* dt, float* attm, float* dz, int npp, float* da) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  att_rows(rows, 0, nullptr, nullptr, 0, gidl, alpha, const_cast<float*>(s), const_cast<float*>(t), attm, npp,
+           nullptr);
+  lds_barrier();
+  // dWh = att^T dpre; datt = dpre Wh^T (to dz)
+  wgrad(attm, npp, rows, rows, dpre, ldd, F, dWh, lddw, 0);
+  lin_t(dpre, ldd, rows, F, Wh, ldw, rows, dz, npp, false, 8);
+  lds_barrier();
+  // softmax + LeakyReLU backward, row i: dz_ij = lrelu'(.) att_ij (datt_ij - sum_k att_ik datt_ik)
+  for (int i = threadIdx.x >> 6; i < rows; i += nw) {
+    const bool ok = lane < rows;
+    const float at = ok ? attm[i * npp + lane] : 0.f, dv = ok ? dz[i * npp + lane] : 0.f;
+    const float dot = wsum(at * dv);
+    const float de = at * (dv - dot);
+    const float z = ok ? ((s[i] + t[lane]) > 0.f ? de : alpha * de) : 0.f;
+    if (ok) dz[i * npp + lane] = z;
+    const float dsum = wsum(z);
     if (lane == 0) ds[i] = dsum;
   }
-  __syncthreads();
-  for (int j = threadIdx.x; j < rows; j += blockDim.x) {
-    float acc = 0.f;
-    for (int i = 0; i < rows; ++i) acc += attm[i * npp + j];
-    dt[j] = acc;
+  lds_barrier();
+  // column j: dt_j = sum_i dz_ij; dWh_j += ds_j a[:F] + dt_j a[F:]
+  for (int j = threadIdx.x >> 6; j < rows; j += nw) {
+    const float dtj = wsum(lane < rows ? dz[lane * npp + j] : 0.f);
+    if (lane == 0) dt[j] = dtj;
+    const float dsj = ds[j];
+    for (int f = lane; f < F; f += 64) dWh[j * lddw + f] += dsj * a[f] + dtj * a[F + f];
   }
-  __syncthreads();
-  for (int e = threadIdx.x; e < rows * F; e += blockDim.x) {
-    const int j = e / F, f = e - j * F;
-    dWh[j * lddw + f] += ds[j] * a[f] + dt[j] * a[F + f];
-  }
+  lds_barrier();
   // da[f] = sum_i ds_i Wh_i[f], da[F + f] = sum_j dt_j Wh_j[f]
   for (int e = threadIdx.x; e < 2 * F; e += blockDim.x) {
     const int w = e / F, f = e - w * F;
@@ -443,16 +601,27 @@ __device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gi
     for (int r = 0; r < rows; ++r) acc = fmaf(g[r], Wh[r * ldw + f], acc);
     da[e] = acc;
   }
-  __syncthreads();
 }
 
+// phase timestamps of workgroup 0's first scene (tools/gatenc_probe.hip)
+#ifdef SGG_GATENC_PROF
+__device__ long long g_gatenc_prof[2][64];
+#define PMARK(i) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_gatenc_prof[BWD][i] = wall_clock64();
+#else
+#define PMARK(i)
+#endif
+
 template <bool BWD>
-__global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel(GatEncArgs p) {
+__global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel(GatEncArgs p, StageTab tab) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const Layout L = make_layout(p.np, p.nh, BWD);
   const PLayout PL = make_playout(p.nh);
   const SLayout SL = make_slayout(p.np, p.nh);
-  const int nh = p.nh, PH = L.PH;
+  const int nh = p.nh, PH = L.PH, NP = L.NP, NPP = L.NPP;
+  // per-head strides of the weight image, the slab row and the saved state
+  constexpr int SEGI = FI * PW72 + 2 * FH, SEGG = FO * PW72 + 2 * FH, PLI = FI * FH + 2 * FH, PLG = FO * FH + 2 * FH;
+  const int SLH = NP * FH + 2 * NP;
   float* X = sm + L.X;
   float* H1 = sm + L.H1;
   float* yI = sm + L.yI;
@@ -464,142 +633,134 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
   float* Wh = sm + L.Wh;
   float* s = sm + L.s;
   float* t = sm + L.t;
-  float* ds = sm + L.ds;
-  float* dt = sm + L.dt;
-  float* attw = sm + L.att;
+  float* sp = sm + L.sp;
+  float* tp = sm + L.tp;
+  float* attm = sm + L.attm;
   float* lab = sm + L.ints;
-  int* gidl = reinterpret_cast<int*>(lab + L.NP);
-  int* grank = gidl + L.NP;
-  int* cnt = grank + L.NP;
-  float* ginv = reinterpret_cast<float*>(cnt + L.NP);
-  int* Mp = reinterpret_cast<int*>(ginv + L.NP);
+  int* gidl = reinterpret_cast<int*>(lab + NP);
+  int* grank = gidl + NP;
+  int* cnt = grank + NP;
+  float* ginv = reinterpret_cast<float*>(cnt + NP);
+  int* Mp = reinterpret_cast<int*>(ginv + NP);
+  unsigned long long* gm = reinterpret_cast<unsigned long long*>(lab + gm_offset(NP));
   const int tid = threadIdx.x;
+  PMARK(40);
   LW lw;
-  {
-    float* q = sm + L.wts;
-#pragma unroll
-    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
-      lw.Wi[h] = q; q = stage_mat(q, p.w.Wi[h], FI, FH, blockDim.x);
-      lw.ai[h] = q; q = stage_vec(q, p.w.ai[h], 2 * FH, blockDim.x);
-    }
-    lw.Wio = q; q = stage_mat(q, p.w.Wio, FH * nh, FO, blockDim.x);
-    lw.aio = q; q = stage_vec(q, p.w.aio, 2 * FO, blockDim.x);
-#pragma unroll
-    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
-      lw.Wg[h] = q; q = stage_mat(q, p.w.Wg[h], FO, FH, blockDim.x);
-      lw.ag[h] = q; q = stage_vec(q, p.w.ag[h], 2 * FH, blockDim.x);
-    }
-    lw.Wgo = q; q = stage_mat(q, p.w.Wgo, FH * nh, FO, blockDim.x);
-    lw.ago = q; q = stage_vec(q, p.w.ago, 2 * FO, blockDim.x);
-    lw.Woe = q; q = stage_mat(q, p.w.Woe, FE, 2 * FO, blockDim.x);
-    lw.boe = q; q = stage_vec(q, p.w.boe, FE, blockDim.x);
-  }
+  stage_weights(sm + L.wts, tab, lw);
   // (the first scene's input loads are followed by a barrier before any use)
+  PMARK(41);
 
   for (int sc = blockIdx.x; sc < p.S; sc += gridDim.x) {
     const int o = p.scene_off[sc];
     const int n = p.scene_off[sc + 1] - o;
     if (n <= 0) continue;   // uniform over the workgroup
+    PMARK(0);
     float* saved = p.saved ? p.saved + (size_t)sc * SL.total : nullptr;
     // ---- inputs and group structure ------------------------------------
     for (int e = tid; e < n * FI; e += blockDim.x) {
       const int r = e / FI, k = e - r * FI;
       X[r * P40 + k] = p.X[(size_t)(o + r) * p.ldx + k];
     }
-    for (int i = tid; i < n; i += blockDim.x) lab[i] = p.labels[o + i];
-    __syncthreads();
-    if (!BWD || !p.saved) {
+    if (!BWD || !saved) {
+      for (int i = tid; i < n; i += blockDim.x) lab[i] = p.labels[o + i];
+    } else {
+      rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
+    }
+    lds_barrier(); PMARK(1);
+    if (!BWD || !saved) {
       // group structure (models.py:263-278) in ONE wave, lane = ped (n <= 64):
-      // g(i) = first ped with i's non-zero label (or i), groups ranked by
-      // their first member, sizes by a lane sweep -- no workgroup barrier
+      // the lowest ungrouped ped leads the next group, its members are the
+      // peds with its non-zero label (a zero label: itself alone); groups are
+      // ranked by their first member, as the reference's unique rows
       if (tid < 64) {
         const int i = tid;
-        const float li = i < n ? lab[i] : 0.f;
-        int g = i;
-        for (int j = 0; j < n; ++j) {
-          const float lj = __shfl(li, j);
-          if (li != 0.f && lj == li && j < g) g = j;
+        const bool in = i < n;
+        const float li = in ? lab[i] : 0.f;
+        unsigned long long rem = __ballot(in);
+        int g = i, r = 0, c = 1, m = 0;
+        while (rem) {   // wave-uniform
+          const int lead = __ffsll((long long)rem) - 1;
+          const float ll = __shfl(li, lead);
+          const unsigned long long same = ll != 0.f ? __ballot(in && li == ll) : (1ull << lead);
+          if ((same >> i) & 1ull) {
+            g = lead;
+            r = m;
+            c = __popcll(same);
+          }
+          if (i == 0) gm[m] = same;
+          ++m;
+          rem &= ~same;
         }
-        const bool lead = i < n && g == i;
-        const unsigned long long leaders = __ballot(lead);
-        int c = 0;
-        for (int j = 0; j < n; ++j) c += __shfl(g, j) == g;
-        const int r = __popcll(leaders & ((1ull << g) - 1ull));
-        if (i < n) {
+        if (in) {
           gidl[i] = g;
           grank[i] = r;
           ginv[i] = 1.f / (float)c;
-          if (lead) cnt[r] = c;
+          if (g == i) cnt[r] = c;
         }
-        if (i == 0) *Mp = __popcll(leaders);
+        if (i == 0) *Mp = m;
       }
-      __syncthreads();
-    } else {
-      rows_from_global(lab, 5 * L.NP + 4, saved + SL.ints, 1, 5 * L.NP + 4);
-      __syncthreads();
+      lds_barrier(); PMARK(2);
     }
     const int M = *Mp;
 
     if (!BWD || !saved) {
-    // ---- intra GAT: heads (40 -> 72, ELU), out (72 nh -> 16, ELU, log_softmax)
-#pragma unroll
-    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
-      lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
-      __syncthreads();
-      if (saved) rows_to_global(saved + SL.Whi[h], Wh, P72, n, FH);
-      scores(Wh, P72, n, FH, lw.ai[h], s, t);
-      __syncthreads();
-      att_fwd(Wh, P72, n, FH, gidl, s, t, p.alpha, 1, H1 + h * FH, PH, nullptr, 0, attw);
-      __syncthreads();
-    }
-    lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72);
-    __syncthreads();
-    if (saved) rows_to_global(saved + SL.Whio, Wh, P72, n, FO);
-    scores(Wh, P72, n, FO, lw.aio, s, t);
-    __syncthreads();
-    att_fwd(Wh, P72, n, FO, gidl, s, t, p.alpha, 2, yI, P16, preI, P16, attw);
-    __syncthreads();
-    // ---- group mean (R intra) ------------------------------------------
-    for (int e = tid; e < M * FO; e += blockDim.x) {
-      const int g = e / FO, f = e - g * FO;
-      float acc = 0.f;
-      for (int i = 0; i < n; ++i)
-        if (grank[i] == g) acc = fmaf(ginv[i], yI[i * P16 + f], acc);
-      gin[g * P16 + f] = acc;
-    }
-    __syncthreads();
-    // ---- inter GAT on the complete graph of the M groups ----------------
-#pragma unroll
-    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
-      lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
-      __syncthreads();
-      if (saved) rows_to_global(saved + SL.Whg[h], Wh, P72, M, FH);
-      scores(Wh, P72, M, FH, lw.ag[h], s, t);
-      __syncthreads();
-      att_fwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, 1, G1 + h * FH, PH, nullptr, 0, attw);
-      __syncthreads();
-    }
-    lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72);
-    __syncthreads();
-    if (saved) rows_to_global(saved + SL.Whgo, Wh, P72, M, FO);
-    scores(Wh, P72, M, FO, lw.ago, s, t);
-    __syncthreads();
-    att_fwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, 2, gout, P16, preG, P16, attw);
-    __syncthreads();
-    if (saved) {   // the activations and the group structure for the backward
-      rows_to_global(saved + SL.H1, H1, PH, n, FH * nh);
-      rows_to_global(saved + SL.yI, yI, P16, n, FO);
-      rows_to_global(saved + SL.preI, preI, P16, n, FO);
-      rows_to_global(saved + SL.gin, gin, P16, M, FO);
-      rows_to_global(saved + SL.G1, G1, PH, M, FH * nh);
-      rows_to_global(saved + SL.preG, preG, P16, M, FO);
-      rows_to_global(saved + SL.gout, gout, P16, M, FO);
-      rows_to_global(saved + SL.ints, lab, 5 * L.NP + 4, 1, 5 * L.NP + 4);
-    }
+      // ---- intra GAT: heads (40 -> 72, ELU), out (72 nh -> 16, ELU, log_softmax)
+      for (int h = 0; h < nh; ++h) {   // per-head offsets are strides (no indexed arrays)
+        lin(X, P40, n, FI, (lw.Wi[0] + h * SEGI), PW72, FH, Wh, P72, 0, (lw.ai[0] + h * SEGI), sp, tp, NP);
+        lds_barrier(); PMARK(3);
+        att_rows(n, kScoreTiles, sp, tp, NP, gidl, p.alpha, s, t, attm, NPP, saved ? saved + (SL.sti[0] + h * SLH) : nullptr);
+        if (saved) rows_to_global(saved + (SL.Whi[0] + h * SLH), Wh, P72, n, FH);
+        lds_barrier(); PMARK(4);
+        att_agg(attm, NPP, n, Wh, P72, FH, 1, H1 + h * FH, PH, nullptr, 0);
+        lds_barrier(); PMARK(5);
+      }
+      lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72, 0, lw.aio, sp, tp, NP);
+      lds_barrier(); PMARK(6);
+      att_rows(n, 1, sp, tp, NP, gidl, p.alpha, s, t, attm, NPP, saved ? saved + SL.stio : nullptr);
+      if (saved) rows_to_global(saved + SL.Whio, Wh, P72, n, FO);
+      lds_barrier(); PMARK(7);
+      att_agg(attm, NPP, n, Wh, P72, FO, 2, yI, P16, preI, P16);
+      lds_barrier(); PMARK(8);
+      // ---- group mean (R intra): members in ascending ped order ---------
+      for (int e = tid; e < M * FO; e += blockDim.x) {
+        const int g = e / FO, f = e - g * FO;
+        unsigned long long mk = gm[g];
+        float acc = 0.f;
+        while (mk) {
+          const int i = __ffsll((long long)mk) - 1;
+          mk &= mk - 1;
+          acc = fmaf(ginv[i], yI[i * P16 + f], acc);
+        }
+        gin[g * P16 + f] = acc;
+      }
+      lds_barrier(); PMARK(9);
+      // ---- inter GAT on the complete graph of the M groups ----------------
+      for (int h = 0; h < nh; ++h) {   // per-head offsets are strides (no indexed arrays)
+        lin(gin, P16, M, FO, (lw.Wg[0] + h * SEGG), PW72, FH, Wh, P72, 0, (lw.ag[0] + h * SEGG), sp, tp, NP);
+        lds_barrier(); PMARK(10);
+        att_rows(M, kScoreTiles, sp, tp, NP, nullptr, p.alpha, s, t, attm, NPP, saved ? saved + (SL.stg[0] + h * SLH) : nullptr);
+        if (saved) rows_to_global(saved + (SL.Whg[0] + h * SLH), Wh, P72, M, FH);
+        lds_barrier(); PMARK(11);
+        att_agg(attm, NPP, M, Wh, P72, FH, 1, G1 + h * FH, PH, nullptr, 0);
+        lds_barrier(); PMARK(12);
+      }
+      lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72, 0, lw.ago, sp, tp, NP);
+      lds_barrier(); PMARK(13);
+      att_rows(M, 1, sp, tp, NP, nullptr, p.alpha, s, t, attm, NPP, saved ? saved + SL.stgo : nullptr);
+      if (saved) rows_to_global(saved + SL.Whgo, Wh, P72, M, FO);
+      lds_barrier(); PMARK(14);
+      att_agg(attm, NPP, M, Wh, P72, FO, 2, gout, P16, preG, P16);
+      lds_barrier(); PMARK(15);
+      if (saved) {   // the activations and the group structure for the backward
+        rows_to_global(saved + SL.H1, H1, PH, n, FH * nh);
+        rows_to_global(saved + SL.yI, yI, P16, n, FO);
+        rows_to_global(saved + SL.preI, preI, P16, n, FO);
+        rows_to_global(saved + SL.gin, gin, P16, M, FO);
+        rows_to_global(saved + SL.G1, G1, PH, M, FH * nh);
+        rows_to_global(saved + SL.preG, preG, P16, M, FO);
+        rows_to_global(saved + SL.gout, gout, P16, M, FO);
+        rows_to_global(saved + SL.ints, lab, 0, 1, ints_floats(NP));
+      }
     } else {
       // backward with the forward's saved state: no recompute
       rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
@@ -609,24 +770,38 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       rows_from_global(G1, PH, saved + SL.G1, M, FH * nh);
       rows_from_global(preG, P16, saved + SL.preG, M, FO);
       rows_from_global(gout, P16, saved + SL.gout, M, FO);
-      __syncthreads();
+      lds_barrier();
     }
 
     if (!BWD) {
-      // ---- out = Woe [intra, gout[g(i)] / |g(i)|] + boe ------------------
-      for (int e = tid; e < n * FE; e += blockDim.x) {
-        const int i = e / FE, c = e - i * FE;
-        const float* wr = lw.Woe + c * PWE;
-        const float* gi = gout + grank[i] * P16;
-        const float sc_i = ginv[i];
-        float a0 = lw.boe[c], a1 = 0.f;
-        for (int f = 0; f < FO; ++f) {
-          a0 = fmaf(wr[f], yI[i * P16 + f], a0);
-          a1 = fmaf(wr[FO + f], gi[f] * sc_i, a1);
+      // ---- out = Woe [intra, gout[g(i)] / |g(i)|] + boe on the MFMA ------
+      // (n x 32) x (32 x 24): A row i = [yI_i | gout_g(i) / |g(i)|]
+      const int lane = tid & 63, nw = blockDim.x >> 6, i16 = lane & 15, kq = lane >> 4;
+      const int nt = ((n + 15) >> 4) * 2;
+      for (int tile = tid >> 6; tile < nt; tile += nw) {
+        const int r0 = (tile >> 1) << 4, c0 = (tile & 1) << 4;
+        const int ar = min(r0 + i16, n - 1);
+        const float* gi = gout + grank[ar] * P16;
+        const float sci = ginv[ar];
+        const int col = c0 + i16;
+        const float* wr = lw.Woe + min(col, FE - 1) * PWE;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 2 * FO; k += 4) {
+          const int kk = k + kq;
+          const float av = kk < FO ? yI[ar * P16 + kk] : gi[kk - FO] * sci;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wr[kk], acc, 0, 0, 0);
         }
-        p.y[(size_t)(o + i) * p.ldy + c] = a0 + a1;
+        if (col < FE) {
+          const float bc = lw.boe[col];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = r0 + 4 * kq + r;
+            if (row < n) p.y[(size_t)(o + row) * p.ldy + col] = acc[r] + bc;
+          }
+        }
       }
-      __syncthreads();
+      lds_barrier(); PMARK(16);
       continue;
     }
 
@@ -636,140 +811,149 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     float* dI = sm + L.dI;
     float* dG = sm + L.dG;
     float* dpre = sm + L.dpre;
-    float* attm = sm + L.attm;
+    float* dz = sm + L.dz;
+    float* ds = sm + L.ds;
+    float* dt = sm + L.dt;
     float* slab = p.slab + (size_t)sc * PL.total;
-    // the scene's dy rows to LDS first (the Wh scratch, pitch FE + 1): the
-    // loops below walk them n-deep, one memory latency per step from global
-    constexpr int PDY = FE + 1;
+    // dy rows and the out embedding's input v = [yI | gout_g(i) / |g(i)|] to
+    // LDS (the Wh scratch: dy at pitch FE + 1, v after it at pitch 2 FO + 1)
+    constexpr int PDY = FE + 1, PV = 2 * FO + 1;
     float* dy = Wh;
+    float* v = Wh + NP * PDY;
     {
       const float* dyg = p.dy + (size_t)o * p.lddy;
-      const int tot = n * FE;
-      for (int e0 = tid; e0 < tot; e0 += 4 * blockDim.x) {
-        float v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = min(e0 + u * (int)blockDim.x, tot - 1);
-          const int i = e / FE, k = e - i * FE;
-          v[u] = dyg[(size_t)i * p.lddy + k];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = e0 + u * (int)blockDim.x;
-          if (e < tot) {
-            const int i = e / FE, k = e - i * FE;
-            dy[i * PDY + k] = v[u];
-          }
-        }
+      for (int e = tid; e < n * FE; e += blockDim.x) {
+        const int i = e / FE, k = e - i * FE;
+        dy[i * PDY + k] = dyg[(size_t)i * p.lddy + k];
+      }
+      for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
+        const int i = e / (2 * FO), c = e - i * 2 * FO;
+        v[i * PV + c] = c < FO ? yI[i * P16 + c] : gout[grank[i] * P16 + c - FO] * ginv[i];
       }
     }
-    __syncthreads();
-    // out embedding: d[intra | inter] = dy Woe; dWoe = dy^T [intra | inter]; dboe = sum dy
-    for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
-      const int i = e / (2 * FO), c = e - i * 2 * FO;
-      float acc = 0.f;
-      for (int k = 0; k < FE; ++k) acc = fmaf(dy[i * PDY + k], lw.Woe[k * PWE + c], acc);
-      if (c < FO) dI[i * P16 + c] = acc;
-      else dpre[i * P16 + c - FO] = acc;   // d inter (scratch)
-    }
-    for (int e = tid; e < FE * 2 * FO; e += blockDim.x) {
-      const int k = e / (2 * FO), c = e - k * 2 * FO;
-      float acc = 0.f;
-      for (int i = 0; i < n; ++i) {
-        const float v = c < FO ? yI[i * P16 + c] : gout[grank[i] * P16 + c - FO] * ginv[i];
-        acc = fmaf(dy[i * PDY + k], v, acc);
-      }
-      slab[PL.Woe + e] = acc;
-    }
+    lds_barrier(); PMARK(17);
+    // out embedding: [d intra | d inter] = dy Woe; dWoe = dy^T v; dboe = sum dy
+    lin(dy, PDY, n, FE, lw.Woe, PWE, FO, dI, P16, 0);
+    lin(dy, PDY, n, FE, lw.Woe + FO, PWE, FO, dpre, P16, 4);   // d inter (scratch)
+    wgrad(dy, PDY, n, FE, v, PV, 2 * FO, slab + PL.Woe, 2 * FO, 8);
     for (int k = tid; k < FE; k += blockDim.x) {
       float acc = 0.f;
       for (int i = 0; i < n; ++i) acc += dy[i * PDY + k];
       slab[PL.boe + k] = acc;
     }
-    __syncthreads();
+    lds_barrier(); PMARK(18);
     // un-pool backward: d gout[g] = sum_{i in g} d inter_i / |g|
     for (int e = tid; e < M * FO; e += blockDim.x) {
       const int g = e / FO, f = e - g * FO;
+      unsigned long long mk = gm[g];
       float acc = 0.f;
-      for (int i = 0; i < n; ++i)
-        if (grank[i] == g) acc = fmaf(ginv[i], dpre[i * P16 + f], acc);
+      while (mk) {
+        const int i = __ffsll((long long)mk) - 1;
+        mk &= mk - 1;
+        acc = fmaf(ginv[i], dpre[i * P16 + f], acc);
+      }
       dG[g * P16 + f] = acc;
     }
-    __syncthreads();
+    lds_barrier(); PMARK(19);
     // ---- inter out layer ----
     epi_bwd(dG, P16, preG, P16, M, FO, 2);
-    if (saved) rows_from_global(Wh, P72, saved + SL.Whgo, M, FO);
-    else lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72);
-    __syncthreads();
-    att_bwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, lw.ago, dG, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.ago);
-    wgrad(G1, PH, M, FH * nh, dWh, P72, FO, slab + PL.Wgo);
-    lin_t(dWh, P72, M, FO, lw.Wgo, PW16, FH * nh, dH, PH, false);
-    __syncthreads();
+    if (saved) {
+      rows_from_global(Wh, P72, saved + SL.Whgo, M, FO);
+      rows_from_global(s, 0, saved + SL.stgo, 1, M);
+      rows_from_global(t, 0, saved + SL.stgo + NP, 1, M);
+    } else {
+      lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72, 0, lw.ago, sp, tp, NP);
+      lds_barrier();
+      for (int i = tid; i < M; i += blockDim.x) {
+        s[i] = score_of(sp, 1, NP, i);
+        t[i] = score_of(tp, 1, NP, i);
+      }
+    }
+    lds_barrier(); PMARK(20);
+    att_bwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, lw.ago, dG, P16, dWh, P72, ds, dt, attm, dz, NPP, slab + PL.ago);
+    wgrad(G1, PH, M, FH * nh, dWh, P72, FO, slab + PL.Wgo, FO, 0);
+    lin_t(dWh, P72, M, FO, lw.Wgo, PW16, FH * nh, dH, PH, false, 8);
+    lds_barrier(); PMARK(21);
     // ---- inter heads ----
     for (int e = tid; e < M * FO; e += blockDim.x) dG[(e / FO) * P16 + e % FO] = 0.f;   // becomes d gin
-#pragma unroll
-    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
+    for (int h = 0; h < nh; ++h) {   // per-head offsets are strides (no indexed arrays)
       // ELU backward from the stored output: elu'(x) = 1 (y > 0) | y + 1
       for (int e = tid; e < M * FH; e += blockDim.x) {
         const int r = e / FH, f = e - r * FH;
         const float yv = G1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      if (saved) rows_from_global(Wh, P72, saved + SL.Whg[h], M, FH);
-      else lin(gin, P16, M, FO, lw.Wg[h], PW72, FH, Wh, P72);
-      __syncthreads();
-      att_bwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, lw.ag[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
-              slab + PL.ag[h]);
-      wgrad(gin, P16, M, FO, dWh, P72, FH, slab + PL.Wg[h]);
-      lin_t(dWh, P72, M, FH, lw.Wg[h], PW72, FO, dG, P16, true);
-      __syncthreads();
+      if (saved) {
+        rows_from_global(Wh, P72, saved + (SL.Whg[0] + h * SLH), M, FH);
+        rows_from_global(s, 0, saved + (SL.stg[0] + h * SLH), 1, M);
+        rows_from_global(t, 0, saved + (SL.stg[0] + h * SLH) + NP, 1, M);
+      } else {
+        lin(gin, P16, M, FO, (lw.Wg[0] + h * SEGG), PW72, FH, Wh, P72, 0, (lw.ag[0] + h * SEGG), sp, tp, NP);
+        lds_barrier();
+        for (int i = tid; i < M; i += blockDim.x) {
+          s[i] = score_of(sp, kScoreTiles, NP, i);
+          t[i] = score_of(tp, kScoreTiles, NP, i);
+        }
+      }
+      lds_barrier(); PMARK(22);
+      att_bwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, (lw.ag[0] + h * SEGG), dH + h * FH, PH, dWh, P72, ds, dt, attm, dz, NPP,
+              slab + (PL.ag[0] + h * PLG));
+      wgrad(gin, P16, M, FO, dWh, P72, FH, slab + (PL.Wg[0] + h * PLG), FH, 0);
+      lin_t(dWh, P72, M, FH, (lw.Wg[0] + h * SEGG), PW72, FO, dG, P16, true, 8);
+      lds_barrier(); PMARK(23);
     }
     // group-mean backward: d intra_i += d gin[g(i)] / |g(i)|
     for (int e = tid; e < n * FO; e += blockDim.x) {
       const int i = e / FO, f = e - i * FO;
       dI[i * P16 + f] = fmaf(ginv[i], dG[grank[i] * P16 + f], dI[i * P16 + f]);
     }
-    __syncthreads();
+    lds_barrier(); PMARK(24);
     // ---- intra out layer ----
     epi_bwd(dI, P16, preI, P16, n, FO, 2);
-    if (saved) rows_from_global(Wh, P72, saved + SL.Whio, n, FO);
-    else lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72);
-    __syncthreads();
-    att_bwd(Wh, P72, n, FO, gidl, s, t, p.alpha, lw.aio, dI, P16, dWh, P72, ds, dt, attm, L.NPP, slab + PL.aio);
-    wgrad(H1, PH, n, FH * nh, dWh, P72, FO, slab + PL.Wio);
-    lin_t(dWh, P72, n, FO, lw.Wio, PW16, FH * nh, dH, PH, false);
-    __syncthreads();
+    if (saved) {
+      rows_from_global(Wh, P72, saved + SL.Whio, n, FO);
+      rows_from_global(s, 0, saved + SL.stio, 1, n);
+      rows_from_global(t, 0, saved + SL.stio + NP, 1, n);
+    } else {
+      lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72, 0, lw.aio, sp, tp, NP);
+      lds_barrier();
+      for (int i = tid; i < n; i += blockDim.x) {
+        s[i] = score_of(sp, 1, NP, i);
+        t[i] = score_of(tp, 1, NP, i);
+      }
+    }
+    lds_barrier(); PMARK(25);
+    att_bwd(Wh, P72, n, FO, gidl, s, t, p.alpha, lw.aio, dI, P16, dWh, P72, ds, dt, attm, dz, NPP, slab + PL.aio);
+    wgrad(H1, PH, n, FH * nh, dWh, P72, FO, slab + PL.Wio, FO, 0);
+    lin_t(dWh, P72, n, FO, lw.Wio, PW16, FH * nh, dH, PH, false, 8);
+    lds_barrier(); PMARK(26);
     // ---- intra heads ----
     float* dXo = p.dX + (size_t)o * p.lddx;
-#pragma unroll
-    for (int h = 0; h < kGatEncMaxHeads; ++h) {  // static head index: the LW / PLayout arrays stay in registers
-      if (h >= nh) break;
+    for (int h = 0; h < nh; ++h) {   // per-head offsets are strides (no indexed arrays)
       for (int e = tid; e < n * FH; e += blockDim.x) {
         const int r = e / FH, f = e - r * FH;
         const float yv = H1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      if (saved) rows_from_global(Wh, P72, saved + SL.Whi[h], n, FH);
-      else lin(X, P40, n, FI, lw.Wi[h], PW72, FH, Wh, P72);
-      __syncthreads();
-      att_bwd(Wh, P72, n, FH, gidl, s, t, p.alpha, lw.ai[h], dH + h * FH, PH, dWh, P72, ds, dt, attm, L.NPP,
-              slab + PL.ai[h]);
-      wgrad(X, P40, n, FI, dWh, P72, FH, slab + PL.Wi[h]);
-      // dX (global) accumulates over heads in a fixed order
-      for (int e = tid; e < n * FI; e += blockDim.x) {
-        const int r = e / FI, k = e - r * FI;
-        const float* dr = dWh + r * P72;
-        const float* wr = lw.Wi[h] + k * PW72;
-        float a0 = 0.f, a1 = 0.f;
-        for (int c = 0; c < FH; c += 2) {
-          a0 = fmaf(dr[c], wr[c], a0);
-          a1 = fmaf(dr[c + 1], wr[c + 1], a1);
+      if (saved) {
+        rows_from_global(Wh, P72, saved + (SL.Whi[0] + h * SLH), n, FH);
+        rows_from_global(s, 0, saved + (SL.sti[0] + h * SLH), 1, n);
+        rows_from_global(t, 0, saved + (SL.sti[0] + h * SLH) + NP, 1, n);
+      } else {
+        lin(X, P40, n, FI, (lw.Wi[0] + h * SEGI), PW72, FH, Wh, P72, 0, (lw.ai[0] + h * SEGI), sp, tp, NP);
+        lds_barrier();
+        for (int i = tid; i < n; i += blockDim.x) {
+          s[i] = score_of(sp, kScoreTiles, NP, i);
+          t[i] = score_of(tp, kScoreTiles, NP, i);
         }
-        float* dst = dXo + (size_t)r * p.lddx + k;
-        *dst = h ? *dst + (a0 + a1) : a0 + a1;
       }
-      __syncthreads();
+      lds_barrier(); PMARK(27);
+      att_bwd(Wh, P72, n, FH, gidl, s, t, p.alpha, (lw.ai[0] + h * SEGI), dH + h * FH, PH, dWh, P72, ds, dt, attm, dz, NPP,
+              slab + (PL.ai[0] + h * PLI));
+      wgrad(X, P40, n, FI, dWh, P72, FH, slab + (PL.Wi[0] + h * PLI), FH, 0);
+      // dX (global) accumulates over heads in a fixed order
+      lin_t(dWh, P72, n, FH, (lw.Wi[0] + h * SEGI), PW72, FI, dXo, p.lddx, h > 0, 8);
+      __syncthreads();   // dX read-modify-write by the next head: global ordering PMARK(28);
     }
   }
 }
@@ -850,8 +1034,8 @@ extern "C" int sgg_gatenc_fwd(const GatEncArgs* args, void* stream) {
   if (rc) return rc;
   if (args->S == 0) return 0;
   const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 0);
-  hipLaunchKernelGGL(gatenc_kernel<false>, dim3(args->S < 65536 ? args->S : 65536), dim3(kFwdThreads), lds,
-                     (hipStream_t)stream, *args);
+  hipLaunchKernelGGL(gatenc_kernel<false>, dim3(args->S < kGridCap ? args->S : kGridCap), dim3(kFwdThreads), lds,
+                     (hipStream_t)stream, *args, make_stage_tab(args->w, args->nh));
   SGG_RETURN_LAUNCH("sgg_gatenc_fwd");
 }
 
@@ -860,8 +1044,8 @@ extern "C" int sgg_gatenc_bwd(const GatEncArgs* args, void* stream) {
   if (rc) return rc;
   if (args->S == 0) return 0;
   const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 1);
-  hipLaunchKernelGGL(gatenc_kernel<true>, dim3(args->S < 65536 ? args->S : 65536), dim3(kBwdThreads), lds,
-                     (hipStream_t)stream, *args);
+  hipLaunchKernelGGL(gatenc_kernel<true>, dim3(args->S < kGridCap ? args->S : kGridCap), dim3(kBwdThreads), lds,
+                     (hipStream_t)stream, *args, make_stage_tab(args->w, args->nh));
   SGG_RETURN_LAUNCH("sgg_gatenc_bwd");
 }
 

@@ -338,8 +338,8 @@ int sgg_adam_step(float* const* params, float* const* grads, float* const* exp_a
  * gat_inter; Woe (24 x 32, nn.Linear layout), boe (24).  X: B x 40 rows
  * (stride ldx), labels: B floats, scene_off: S + 1, np = the largest scene
  * (<= 64; the LDS plan is sized by it, sgg_gatenc_lds_bytes <= 160 KiB).
- * Forward writes y (B x 24, stride ldy).  Backward (recomputes the forward)
- * reads dy and writes dX (B x 40, stride lddx) and, per scene s, the
+ * Forward writes y (B x 24, stride ldy).  Backward (reads the forward's
+ * saved state, or recomputes it when saved == NULL) reads dy and writes dX (B x 40, stride lddx) and, per scene s, the
  * parameter gradients into slab row s (sgg_gatenc_param_size(nh) floats, in
  * the order Wi[0], ai[0], .., Wio, aio, Wg[0], ag[0], .., Wgo, ago, Woe, boe);
  * sgg_slab_reduce sums the rows in scene order.
