@@ -365,6 +365,12 @@ def main():
         kernels = {n: {"us_per_iter": round(a["us_per_iter"], 1), "launches_per_iter": round(a["launches_per_iter"], 2),
                        "GB/s": round(a["bytes"] / (a["us_per_iter"] * 1e-6) / 1e9, 1),
                        "TFLOP/s": round(a["flop"] / (a["us_per_iter"] * 1e-6) / 1e12, 2)} for n, a in top[:10]}
+        launches = sorted(((r["launches"] / n_it * r["ms"] * 1e3, n, r, k) for n, a in agg.items()
+                           for k, r, _ in a["shapes"]), key=lambda x: -x[0])
+        launch_table = [{"kernel": n, "shape": list(k[1:]), "per_iter": round(r["launches"] / n_it, 2),
+                         "avg_us": round(r["ms"] * 1e3, 2), "us_per_iter": round(us, 1)}
+                        for us, n, r, k in launches[:30]]
+        total_launch_us = sum(x[0] for x in launches)
         ms_step = elapsed / args.steps * 1e3
         value = world * per_gpu / (elapsed / args.steps)
         cpu = None
@@ -384,6 +390,7 @@ def main():
                        "obs_len": 8, "pred_len": 12, "generator": args.graph_kind, "hip_graph": graphed,
                        "parallelism": "dp%d" % world},
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
+            "instrumented_us_per_iter": round(total_launch_us, 1), "launch_table": launch_table,
         }
         if scaling_ref is not None:
             line["scaling_reference"] = scaling_ref

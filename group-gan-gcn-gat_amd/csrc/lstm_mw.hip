@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
 }
 
 template <int H, bool DEC, bool WGRAD>
-__global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
+__global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_bwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Whh, const float* __restrict__ Wp,
     const float* __restrict__ h_all, const float* __restrict__ c_tile, const float* __restrict__ act_tile,
     const float* __restrict__ rel, const float* __restrict__ rel_out, const float* __restrict__ dh_last,
@@ -247,6 +247,79 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
   const int ped = blk * kMwPeds + c16;
   const bool valid = ped < B;
   const int pc = valid ? ped : B - 1;
+
+  // weight-gradient operand of step t: h_{t-1} = h_all[t] of the block's 16
+  // peds, fetched one step ahead, staged in LDS
+  float hv[NHS];
+  const int ht = threadIdx.x & (kMwThreads - 1);   // thread index among the four (helper) waves
+  auto stage_load = [&](int t) {
+#pragma unroll
+    for (int m = 0; m < NHS; ++m) {
+      const int e = ht + m * kMwThreads;   // < 16 H exactly (NHS = 16 H / 256)
+      hv[m] = h_all[((size_t)t * B + min(blk * kMwPeds + e / H, B - 1)) * H + e % H];
+    }
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int m = 0; m < NHS; ++m) {
+      const int e = ht + m * kMwThreads;
+      hs[buf][e / H][e % H] = hv[m];
+    }
+  };
+  if (wgrad && g >= 4) {
+    // helper waves 4..7: the weight gradient of gate block hg, off the
+    // recurrence's critical path.  They pass the same two barriers per step:
+    // after barrier A(t) dG_t is in dgb[t & 1] and h_{t-1} in hs[t & 1]; the
+    // MFMAs run while the owners compute dh_{t-1}, then h_{t-2} is staged into
+    // the other buffer (its last reader, step t + 1, finished before B(t + 1)).
+    const int hg = g - 4;
+    floatx4 dw[MU][MU];
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+      for (int nu = 0; nu < MU; ++nu) dw[mu][nu] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // dw[mu][nu] += dG_g^T (units 16 mu..) x h (units 16 nu..) over the 16 peds
+    auto dw_accum = [&](int buf) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int p = 4 * kk + q;
+        float bh[MU];
+#pragma unroll
+        for (int nu = 0; nu < MU; ++nu) bh[nu] = hs[buf][p][16 * nu + c16];
+#pragma unroll
+        for (int mu = 0; mu < MU; ++mu) {
+          const float a = dgb[buf][hg][4 * mu + (c16 & 3)][((c16 >> 2) << 4) + p];
+#pragma unroll
+          for (int nu = 0; nu < MU; ++nu) dw[mu][nu] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bh[nu], dw[mu][nu], 0, 0, 0);
+        }
+      }
+    };
+
+    stage_load(T - 1);
+    stage_store((T - 1) & 1);
+    if (T >= 2) stage_load(T - 2);
+    for (int t = T - 1; t >= 0; --t) {
+      const int cur = t & 1;
+      lds_barrier();   // A(t)
+      dw_accum(cur);
+      if (t > 0) {
+        stage_store(cur ^ 1);
+        if (t > 1) stage_load(t - 2);
+      }
+      lds_barrier();   // B(t)
+    }
+    // slab row of this workgroup: D tile (mu, nu) holds rows hg H + 16 mu + 4 q + r, cols 16 nu + c16
+    float* row = wpart + (size_t)blk * P;
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = hg * H + 16 * mu + 4 * q + r;
+#pragma unroll
+        for (int nu = 0; nu < MU; ++nu) row[(size_t)gr * H + 16 * nu + c16] = dw[mu][nu][r];
+      }
+    return;
+  }
 
   // W_hh,g^T in registers: wt[mu][ks] = W_hh[g H + slot_unit(ks, q)][16 mu + c16]
   // (decoder: the folded W' = W_hh + A Wp for t >= 1, plain W_hh kept for t = 0)
@@ -310,61 +383,17 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     }
   };
 
-  // weight-gradient operand of step t: h_{t-1} = h_all[t] of the block's 16
-  // peds, fetched one step ahead, staged in LDS
-  float hv[NHS];
-  auto stage_load = [&](int t) {
-#pragma unroll
-    for (int m = 0; m < NHS; ++m) {
-      const int e = threadIdx.x + m * kMwThreads;   // < 16 H exactly (NHS = 16 H / 256)
-      hv[m] = h_all[((size_t)t * B + min(blk * kMwPeds + e / H, B - 1)) * H + e % H];
-    }
-  };
-  auto stage_store = [&](int buf) {
-#pragma unroll
-    for (int m = 0; m < NHS; ++m) {
-      const int e = threadIdx.x + m * kMwThreads;
-      hs[buf][e / H][e % H] = hv[m];
-    }
-  };
-  floatx4 dw[MU][MU];
-#pragma unroll
-  for (int mu = 0; mu < MU; ++mu)
-#pragma unroll
-    for (int nu = 0; nu < MU; ++nu) dw[mu][nu] = floatx4{0.f, 0.f, 0.f, 0.f};
   float db[MU][4], dax[MU][4], day[MU][4];
 #pragma unroll
   for (int i = 0; i < MU; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) db[i][k] = dax[i][k] = day[i][k] = 0.f;
-  // dw[mu][nu] += dG_g^T (units 16 mu..) x h (units 16 nu..) over the 16 peds
-  auto dw_accum = [&](int buf) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int p = 4 * kk + q;
-      float bh[MU];
-#pragma unroll
-      for (int nu = 0; nu < MU; ++nu) bh[nu] = hs[buf][p][16 * nu + c16];
-#pragma unroll
-      for (int mu = 0; mu < MU; ++mu) {
-        const float a = dgb[buf][g][4 * mu + (c16 & 3)][((c16 >> 2) << 4) + p];
-#pragma unroll
-        for (int nu = 0; nu < MU; ++nu) dw[mu][nu] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bh[nu], dw[mu][nu], 0, 0, 0);
-      }
-    }
-  };
 
   load_step(T - 1);
-  if (wgrad) stage_load(T - 1);
   float din_x = 0.f, din_y = 0.f;   // drel_in[t + 1] (wave 0, q = 0 lanes)
 
   for (int t = T - 1; t >= 0; --t) {
     const int cur = t & 1;
-    if (wgrad) {
-      if (t < T - 1) dw_accum(cur ^ 1);   // step t + 1: its dG image and h_t, in the VALU shadow below
-      stage_store(cur);                  // h_{t-1} of step t (read after this step's barriers)
-      if (t > 0) stage_load(t - 1);
-    }
     const float d0 = nd0, d1 = nd1, r0 = nr0, r1 = nr1;
     float ci[MU], cf[MU], cg[MU], co[MU], cc[MU], ccp[MU];
 #pragma unroll
@@ -460,17 +489,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_bwd_kernel(
     }
   }
   if (wgrad) {
-    dw_accum(0);   // step 0 (its dG image and h_{-1} = h0 are visible since the loop's last barriers)
-    // slab row of this workgroup: D tile (mu, nu) holds rows g H + 16 mu + 4 q + r, cols 16 nu + c16
     float* row = wpart + (size_t)blk * P;
-#pragma unroll
-    for (int mu = 0; mu < MU; ++mu)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = g * H + 16 * mu + 4 * q + r;
-#pragma unroll
-        for (int nu = 0; nu < MU; ++nu) row[(size_t)gr * H + 16 * nu + c16] = dw[mu][nu][r];
-      }
     // db / dA of the owned slots: sum over the 16 peds (lanes c16 of each q)
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
@@ -513,7 +532,7 @@ int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* h
   const int grid = (B + kMwPeds - 1) / kMwPeds;
   auto k = decoder ? (wpart ? lstm_mw_bwd_kernel<H, true, true> : lstm_mw_bwd_kernel<H, true, false>)
                    : (wpart ? lstm_mw_bwd_kernel<H, false, true> : lstm_mw_bwd_kernel<H, false, false>);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all, rel, rel_out,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(wpart ? 2 * kMwThreads : kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all, rel, rel_out,
                      dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart);
   SGG_RETURN_LAUNCH("sgg_lstm_bwd");
 }
