@@ -397,8 +397,9 @@ __device__ void lin(const float* in, int ldi, int rows, int K, const float* W, i
 
 // out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin; N % 4 == 0;
 // out may be global memory)
+// (out2: columns >= ksplit go to out2 at pitch ldo2 instead)
 __device__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, int ldw, int K, float* out, int ldo,
-                      bool accum, int first = 0) {
+                      bool accum, int first = 0, float* out2 = nullptr, int ldo2 = 0, int ksplit = 0) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
   const int ct = (K + 15) >> 4, nt = ((rows + 15) >> 4) * ct;
   for (int tile = mm_wave(first); tile < nt; tile += nw) {
@@ -413,7 +414,7 @@ __device__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, 
     for (int r = 0; r < 4; ++r) {
       const int row = r0 + 4 * kq + r;
       if (row < rows && col < K) {
-        float* po = out + row * ldo + col;
+        float* po = out2 && col >= ksplit ? out2 + row * ldo2 + (col - ksplit) : out + row * ldo + col;
         *po = accum ? *po + acc[r] : acc[r];
       }
     }
@@ -659,7 +660,8 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     // ---- inputs and group structure ------------------------------------
     for (int e = tid; e < n * FI; e += blockDim.x) {
       const int r = e / FI, k = e - r * FI;
-      X[r * P40 + k] = p.X[(size_t)(o + r) * p.ldx + k];
+      X[r * P40 + k] = p.X2 && k >= p.kx1 ? p.X2[(size_t)(o + r) * p.ldx2 + (k - p.kx1)]
+                                          : p.X[(size_t)(o + r) * p.ldx + k];
     }
     if (!BWD || !saved) {
       for (int i = tid; i < n; i += blockDim.x) lab[i] = p.labels[o + i];
@@ -929,6 +931,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     lds_barrier(); PMARK(26);
     // ---- intra heads ----
     float* dXo = p.dX + (size_t)o * p.lddx;
+    float* dX2o = p.X2 ? p.dX2 + (size_t)o * p.lddx2 : nullptr;
     for (int h = 0; h < nh; ++h) {   // per-head offsets are strides (no indexed arrays)
       for (int e = tid; e < n * FH; e += blockDim.x) {
         const int r = e / FH, f = e - r * FH;
@@ -952,7 +955,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
               slab + (PL.ai[0] + h * PLI));
       wgrad(X, P40, n, FI, dWh, P72, FH, slab + (PL.Wi[0] + h * PLI), FH, 0);
       // dX (global) accumulates over heads in a fixed order
-      lin_t(dWh, P72, n, FH, (lw.Wi[0] + h * SEGI), PW72, FI, dXo, p.lddx, h > 0, 8);
+      lin_t(dWh, P72, n, FH, (lw.Wi[0] + h * SEGI), PW72, FI, dXo, p.lddx, h > 0, 8, dX2o, p.lddx2, p.kx1);
       __syncthreads();   // dX read-modify-write by the next head: global ordering PMARK(28);
     }
   }
@@ -1015,12 +1018,18 @@ static int gatenc_check(const char* who, const GatEncArgs* a, int bwd) {
   SGG_CHECK_ARG(a->X && a->labels && a->scene_off, "%s: null input", who);
   SGG_CHECK_ARG(a->nh >= 1 && a->nh <= kGatEncMaxHeads, "%s: heads %d outside [1, %d]", who, a->nh, kGatEncMaxHeads);
   SGG_CHECK_ARG(a->np >= 1 && a->np <= 64, "%s: max scene size %d outside [1, 64]", who, a->np);
-  SGG_CHECK_ARG(a->S >= 0 && a->ldx >= FI, "%s: bad sizes", who);
+  SGG_CHECK_ARG(a->S >= 0 && a->ldx >= (a->X2 ? a->kx1 : FI), "%s: bad sizes", who);
+  if (a->X2) {
+    SGG_CHECK_ARG(a->kx1 > 0 && a->kx1 < FI && a->ldx2 >= FI - a->kx1, "%s: bad split input (kx1 %d)", who, a->kx1);
+    if (bwd)
+      SGG_CHECK_ARG(a->dX2 && a->lddx2 >= FI - a->kx1 && a->lddx >= a->kx1, "%s: null / bad split gradient", who);
+  }
   for (int h = 0; h < a->nh; ++h)
     SGG_CHECK_ARG(a->w.Wi[h] && a->w.ai[h] && a->w.Wg[h] && a->w.ag[h], "%s: null head weight %d", who, h);
   SGG_CHECK_ARG(a->w.Wio && a->w.aio && a->w.Wgo && a->w.ago && a->w.Woe && a->w.boe, "%s: null weight", who);
   if (bwd) {
-    SGG_CHECK_ARG(a->dy && a->dX && a->slab && a->lddy >= FE && a->lddx >= FI, "%s: null / bad gradient buffer", who);
+    SGG_CHECK_ARG(a->dy && a->dX && a->slab && a->lddy >= FE && a->lddx >= (a->X2 ? a->kx1 : FI),
+                  "%s: null / bad gradient buffer", who);
   } else {
     SGG_CHECK_ARG(a->y && a->ldy >= FE, "%s: null / bad output", who);
   }

@@ -25,10 +25,16 @@ namespace {
 __global__ void __launch_bounds__(256) traj_cat_kernel(const float* __restrict__ head, int ldh, int T0,
                                                        const float* __restrict__ a, int lda,
                                                        const float* __restrict__ b, int ldb, int T1, int B,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out, const float* __restrict__ pos0,
+                                                       float* __restrict__ start) {
   const int NB = b ? 2 * B : B;
   const int total = (T0 + T1) * NB;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total + (start ? NB : 0); e += gridDim.x * blockDim.x) {
+    if (e >= total) {   // the start positions of every column: pos0 of its ped
+      const int p = e - total;
+      reinterpret_cast<float2*>(start)[p] = reinterpret_cast<const float2*>(pos0)[p < B ? p : p - B];
+      continue;
+    }
     const int t = e / NB, p = e - t * NB;
     const float* src;
     if (t < T0) {
@@ -191,14 +197,15 @@ int grid_for(long long n, int per) {
 using namespace sgg;
 
 extern "C" int sgg_traj_cat(const float* head, int ldh, int T0, const float* a, int lda, const float* b, int ldb,
-                            int T1, int B, float* out, void* stream) {
+                            int T1, int B, float* out, const float* pos0, float* start, void* stream) {
   SGG_CHECK_ARG(head && a && out, "sgg_traj_cat: null pointer");
+  SGG_CHECK_ARG(!start || pos0, "sgg_traj_cat: start positions need pos0");
   SGG_CHECK_ARG(T0 >= 0 && T1 >= 0 && B >= 0 && ldh >= 2 * B && lda >= 2 * B && (!b || ldb >= 2 * B),
                 "sgg_traj_cat: bad sizes");
-  const long long total = (long long)(T0 + T1) * (b ? 2 * B : B);
+  const long long total = (long long)(T0 + T1 + (start ? 1 : 0)) * (b ? 2 * B : B);
   if (total == 0) return 0;
   hipLaunchKernelGGL(traj_cat_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, head, ldh, T0, a,
-                     lda, b, ldb, T1, B, out);
+                     lda, b, ldb, T1, B, out, pos0, start);
   SGG_RETURN_LAUNCH("sgg_traj_cat");
 }
 

@@ -31,7 +31,8 @@ class GatEncArgs(ctypes.Structure):
     """SggGatEncArgs (include/sgg.h)."""
     _fields_ = [("X", _p), ("ldx", _i), ("labels", _p), ("scene_off", _p), ("S", _i), ("np", _i), ("nh", _i),
                 ("alpha", _f), ("w", GatEncWeights), ("y", _p), ("ldy", _i), ("dy", _p), ("lddy", _i), ("dX", _p),
-                ("lddx", _i), ("slab", _p), ("saved", _p)]
+                ("lddx", _i), ("slab", _p), ("saved", _p), ("X2", _p), ("ldx2", _i), ("kx1", _i),
+                ("dX2", _p), ("lddx2", _i)]
 
 
 _pargs = ctypes.POINTER(GatEncArgs)
@@ -85,7 +86,7 @@ SIGNATURES = {
     "sgg_slab_reduce": (_i, [_p, _i, _i, _p, _p]),
     "sgg_gather_batch_floats": (ctypes.c_longlong, [_i, _i, _i]),
     "sgg_gather_batch": (_i, [_p, _i, _p, _i, _i, _i, _p, _p]),
-    "sgg_traj_cat": (_i, [_p, _i, _i, _p, _i, _p, _i, _i, _i, _p, _p]),
+    "sgg_traj_cat": (_i, [_p, _i, _i, _p, _i, _p, _i, _i, _i, _p, _p, _p, _p]),
     "sgg_decoder_init": (_i, [_p, _i, _i, _p, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p]),
     "sgg_l2_select": (_i, [_p, _p, _p, _i, _p, _i, _i, _i, _i, _p, _p]),
     "sgg_l2_loss_fwd": (_i, [_p, _i, _p, _p, _i, _p, _i, _i, _i, _f, _p, _p, _p, _p]),

@@ -579,13 +579,16 @@ class _GatEnc(torch.autograd.Function):
     the inter GAT, out_embedding weight, bias -- the slab order of sgg.h."""
 
     @staticmethod
-    def forward(ctx, x, labels, scenes, nh, alpha, *params):
+    def forward(ctx, x, labels, scenes, nh, alpha, x2, *params):
         lib = _lib()
         x = _rows(x, "x")
         B = x.shape[0]
+        if x2 is not None:
+            x2 = _rows(x2, "x2")
+            assert x2.shape[0] == B and x.shape[1] + x2.shape[1] == 40, (x.shape, x2.shape)
         y = torch.empty(B, 24, device=x.device, dtype=torch.float32)
         ps = [_req(q, "gat weight").contiguous() for q in params]
-        a = _gatenc_args(x, labels, scenes, nh, alpha, ps)
+        a = _gatenc_args(x, labels, scenes, nh, alpha, ps, x2)
         a.y, a.ldy = N.ptr(y), 24
         saved = None
         if any(ctx.needs_input_grad) and GATENC_SAVE:
@@ -594,33 +597,36 @@ class _GatEnc(torch.autograd.Function):
             a.saved = N.ptr(saved)
         N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_fwd")
         if timer.active:
-            keep = (x, y, labels, scenes, ps, saved)   # the replay closure holds every buffer `a` points to
+            keep = (x, x2, y, labels, scenes, ps, saved)   # the replay closure holds every buffer `a` points to
             timer.add("sgg::gatenc_kernel<false>", (scenes.S, B, nh), _gatenc_flops(scenes, nh),
                       4.0 * B * (40 + 1 + 24) + (_gatenc_saved_bytes(B, nh) if saved is not None else 0.0),
                       lambda a=a, keep=keep: N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()),
                                                      "sgg_gatenc_fwd"))
         ctx.meta = (labels, scenes, nh, alpha)
-        ctx.save_for_backward(x, saved, *ps)
+        ctx.save_for_backward(x, x2, saved, *ps)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = _lib()
-        x, saved, *ps = ctx.saved_tensors
+        x, x2, saved, *ps = ctx.saved_tensors
         labels, scenes, nh, alpha = ctx.meta
         dy = _rows(dy, "dy")
         B = x.shape[0]
         P = lib.sgg_gatenc_param_size(nh)
-        dx = torch.empty(B, 40, device=x.device, dtype=torch.float32)
+        dx = torch.empty(B, x.shape[1], device=x.device, dtype=torch.float32)
+        dx2 = torch.empty(B, x2.shape[1], device=x.device, dtype=torch.float32) if x2 is not None else None
         slab = torch.empty(max(scenes.S, 1), P, device=x.device, dtype=torch.float32)
-        a = _gatenc_args(x, labels, scenes, nh, alpha, ps)
+        a = _gatenc_args(x, labels, scenes, nh, alpha, ps, x2)
         a.dy, a.lddy = N.ptr(dy), dy.stride(0)
-        a.dX, a.lddx = N.ptr(dx), 40
+        a.dX, a.lddx = N.ptr(dx), dx.shape[1]
+        if dx2 is not None:
+            a.dX2, a.lddx2 = N.ptr(dx2), dx2.shape[1]
         a.slab = N.ptr(slab)
         a.saved = N.ptr(saved)
         N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_bwd")
         if timer.active:
-            keep = (x, dy, dx, slab, labels, scenes, ps, saved)
+            keep = (x, x2, dy, dx, dx2, slab, labels, scenes, ps, saved)
             timer.add("sgg::gatenc_kernel<true>", (scenes.S, B, nh), 3.0 * _gatenc_flops(scenes, nh),
                       4.0 * (B * (40 + 1 + 24 + 40) + scenes.S * P) + _gatenc_saved_bytes(B, nh),
                       lambda a=a, keep=keep: N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()),
@@ -631,7 +637,7 @@ class _GatEnc(torch.autograd.Function):
         for q in ps:
             grads.append(flat[o:o + q.numel()].view_as(q))
             o += q.numel()
-        return (dx, None, None, None, None) + tuple(grads)
+        return (dx, None, None, None, None, dx2) + tuple(grads)
 
 
 def _gatenc_flops(scenes, nh):
@@ -653,9 +659,11 @@ def _gatenc_saved_bytes(B, nh):
     return 4.0 * B * (4 * 72 * nh + 2 * 16 + 5 * 16 + 5)
 
 
-def _gatenc_args(x, labels, scenes, nh, alpha, ps):
+def _gatenc_args(x, labels, scenes, nh, alpha, ps, x2=None):
     a = N.GatEncArgs()
     a.X, a.ldx = N.ptr(x), x.stride(0)
+    if x2 is not None:
+        a.X2, a.ldx2, a.kx1 = N.ptr(x2), x2.stride(0), x.shape[1]
     a.labels, a.scene_off = N.ptr(labels), N.ptr(scenes.scene_off)
     a.S, a.np, a.nh, a.alpha = scenes.S, max(scenes.max_n, 1), nh, float(alpha)
     it = iter(ps)
@@ -676,10 +684,11 @@ def gat_encoder_fused_ok(scenes, nh, need_grad):
     return _lib().sgg_gatenc_lds_bytes(max(scenes.max_n, 1), nh, int(bool(need_grad))) <= 160 * 1024
 
 
-def gat_encoder(x, labels, scenes, nh, alpha, params):
-    """GATEncoder.forward (models.py:254-294) for all scenes: (B, 40) -> (B, 24)."""
+def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None):
+    """GATEncoder.forward (models.py:254-294) for all scenes: (B, 40) -> (B, 24).
+    x2: the input as two column blocks [x | x2] (no concatenation copy)."""
     lab = _req(labels, "labels").contiguous().view(-1)
-    return _GatEnc.apply(x, lab, scenes, nh, alpha, *params)
+    return _GatEnc.apply(x, lab, scenes, nh, alpha, x2, *params)
 
 
 class _SegNorm(torch.autograd.Function):
@@ -1005,10 +1014,12 @@ def bce_pair(scores, split, y_a, y_b, w=1.0):
 class _TrajCat(torch.autograd.Function):
     """cat over time of head (T0 x B x 2, repeated for both halves when b is
     given) and a | b (T1 x B x 2 each, side by side); a may be a batch slice
-    of a wider tensor.  Gradient flows to `a` only (the generator output)."""
+    of a wider tensor.  Gradient flows to `a` only (the generator output).
+    With pos0 (B x 2) the same launch also returns the start positions of
+    every column (pos0 repeated for both halves: the discriminator's traj[0])."""
 
     @staticmethod
-    def forward(ctx, head, a, b):
+    def forward(ctx, head, a, b, pos0):
         T0, B = head.shape[0], head.shape[1]
         T1 = a.shape[0]
         # rows of (x, y) pairs with a free step stride; anything else (e.g. the
@@ -1020,20 +1031,28 @@ class _TrajCat(torch.autograd.Function):
             assert t.shape[1:] == (B, 2) and t.stride(1) == 2 and t.stride(2) == 1, (nm, t.shape, t.stride())
         NB = 2 * B if b is not None else B
         out = torch.empty(T0 + T1, NB, 2, device=a.device, dtype=torch.float32)
+        start = None
+        if pos0 is not None:
+            pos0 = _req(pos0, "pos0").reshape(B, 2).contiguous()
+            start = torch.empty(1, NB, 2, device=a.device, dtype=torch.float32)
         N.check(_lib().sgg_traj_cat(N.ptr(head), head.stride(0), T0, N.ptr(a), a.stride(0), N.ptr(b),
-                                    b.stride(0) if b is not None else 0, T1, B, N.ptr(out), N.stream_ptr()),
-                "sgg_traj_cat")
+                                    b.stride(0) if b is not None else 0, T1, B, N.ptr(out), N.ptr(pos0),
+                                    N.ptr(start), N.stream_ptr()), "sgg_traj_cat")
         ctx.dims = (T0, B)
-        return out
+        if start is None:
+            return out
+        ctx.mark_non_differentiable(start)
+        return out, start
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, dout, *_):
         T0, B = ctx.dims
-        return None, dout[T0:, :B], None
+        return None, dout[T0:, :B], None, None
 
 
-def traj_cat(head, a, b=None):
-    return _TrajCat.apply(head, a, b)
+def traj_cat(head, a, b=None, pos0=None):
+    """-> traj_rel, or (traj_rel, start) when pos0 is given."""
+    return _TrajCat.apply(head, a, b, pos0)
 
 
 class _DecoderInit(torch.autograd.Function):

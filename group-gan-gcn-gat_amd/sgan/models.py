@@ -268,15 +268,23 @@ class GATEncoder(nn.Module):
         return ps + [self.out_embedding.weight, self.out_embedding.bias]
 
     def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None):
+        """h_states: (B, 40), or the pair (encoder state, pooled vector) whose
+        concatenation it is (the fused kernel reads both blocks in place)."""
+        x2 = None
+        if isinstance(h_states, (tuple, list)):
+            h_states, x2 = h_states
         sc = _scenes(seq_start_end, h_states.device, scenes)
         if sc.max_n > 128:
             raise ValueError("GAT kernels hold <= 128 peds per scene (got %d)" % sc.max_n)
         nh = len(self.gat_intra.attentions)
         params = self.fused_params()
-        need_grad = torch.is_grad_enabled() and (h_states.requires_grad or any(p.requires_grad for p in params))
+        need_grad = torch.is_grad_enabled() and (h_states.requires_grad or (x2 is not None and x2.requires_grad)
+                                                 or any(p.requires_grad for p in params))
         if (self.gat_intra.dropout == 0 or not self.training) and K.gat_encoder_fused_ok(sc, nh, need_grad):
             # one launch per direction for the whole module (sgg_gatenc_fwd / _bwd)
-            return K.gat_encoder(h_states, end_group, sc, nh, self.gat_intra.attentions[0].alpha, params)
+            return K.gat_encoder(h_states, end_group, sc, nh, self.gat_intra.attentions[0].alpha, params, x2=x2)
+        if x2 is not None:
+            h_states = torch.cat([h_states, x2], dim=1)
         g = sc.groups(end_group.reshape(-1))
         intra_graph = K.SegmentGraph(sc.scene_off, sc.S, sc.max_n, 0, g.labels)
         inter_graph = K.SegmentGraph(g.group_off, sc.S, sc.max_n, 1, None)
@@ -405,6 +413,11 @@ class GCNModule(nn.Module):
         self.out_embedding = nn.Linear(out_dim * 2, final_dim)
 
     def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None):
+        """h_states: (B, 40), or the pair (encoder state, pooled vector) whose
+        concatenation it is (the fused kernel reads both blocks in place)."""
+        x2 = None
+        if isinstance(h_states, (tuple, list)):
+            h_states, x2 = h_states
         sc = _scenes(seq_start_end, h_states.device, scenes)
         g = sc.groups(end_group.reshape(-1))
         # A_intra = D^-1 M: row i averages its group (models.py:658-665)
@@ -531,6 +544,10 @@ class TrajectoryGenerator(nn.Module):
         end_pos = obs_traj[-1]
         if self.pooling_type:
             pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc)
+            if self.graph == "gat" and self.mlp_decoder_needed():
+                # the GAT encoder reads [h | pool_h] as two blocks (no cat)
+                noise_input = self.gatencoder((ctx, pool_h), seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
+                return noise_input
             ctx = torch.cat([ctx, pool_h], dim=1)
         if self.mlp_decoder_needed():
             if self.graph == "gat":

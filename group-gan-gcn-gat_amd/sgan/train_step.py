@@ -170,8 +170,11 @@ class GanTrainer:
     def _finish(self, params, opt, loss_terms, clip):
         """all-reduce grads (+ loss values), clip, step."""
         grads = [p.grad for p in params if p.grad is not None]
-        vals = torch.stack([t.detach().reshape(()) for t in loss_terms])
-        self.dp.allreduce_(grads + [vals])
+        if self.dp.on and self.dp.world > 1:   # the loss values ride along with the gradients
+            vals = torch.stack([t.detach().reshape(()) for t in loss_terms])
+            self.dp.allreduce_(grads + [vals])
+        else:                                  # one rank: no copy (callers index the values)
+            vals = [t.detach().reshape(()) for t in loss_terms]
         opt.step(max_norm=clip)    # clip_grad_norm_(params, clip) when clip > 0, then Adam
         return vals
 
@@ -190,8 +193,7 @@ class GanTrainer:
             fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
         # D reads traj[0] (the start positions, models.py:989) and traj_rel
         # only: [fake | real] side by side, no relative_to_abs needed
-        traj_rel = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel)
-        start = obs[:1].repeat(1, 2, 1)
+        traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
         sc2 = sc.repeat(2)
         scores = self.D(start, traj_rel, _sse_of(sc2), scenes=sc2)
         if inputs is not None:

@@ -376,6 +376,15 @@ typedef struct {
   int lddx;
   float* slab;
   float* saved;   /* may be NULL: S x sgg_gatenc_saved_floats(1, np, nh) floats of forward state */
+  /* optional second input block: when X2 != NULL a row of the 40-wide input
+   * is [X[r][0 .. kx1) | X2[r][0 .. 40 - kx1)] (the encoder state and the
+   * pooled vector without a concatenation copy), and the backward writes the
+   * input gradient split the same way into dX (kx1 columns) and dX2 */
+  const float* X2;
+  int ldx2;
+  int kx1;
+  float* dX2;
+  int lddx2;
 } SggGatEncArgs;
 
 int sgg_gatenc_param_size(int nh);
@@ -400,10 +409,12 @@ int sgg_slab_reduce(const float* slab, int rows, int cols, float* out, void* str
  *   cat over time of head (T0 steps, B peds; repeated for both halves) and
  *   a (T1 steps, B peds) | b (T1 steps, B peds) side by side -- the
  *   discriminator input traj_rel of the fake and real trajectories
- *   (train.py:409-415, 468-470).
+ *   (train.py:409-415, 468-470).  start (optional, NB x 2): the same launch
+ *   writes pos0 (B x 2) for every column (traj[0] of the D input, both halves
+ *   start where the observation starts).
  */
 int sgg_traj_cat(const float* head, int ldh, int T0, const float* a, int lda, const float* b, int ldb, int T1, int B,
-                 float* out, void* stream);
+                 float* out, const float* pos0, float* start, void* stream);
 
 /* sgg_decoder_init: add_noise ('global' mix, models.py:827-850) for `copies`
  * sample-major copies of the batch: h0[r*B + p] = [ctx[p] (Dc) | z[k, s(p)] (nz)]

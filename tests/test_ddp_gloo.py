@@ -101,10 +101,14 @@ class _TorchOps:
     optimizer = staticmethod(_TorchClipAdam)
 
     @staticmethod
-    def traj_cat(head, a, b=None):
+    def traj_cat(head, a, b=None, pos0=None):
         if b is None:
-            return torch.cat([head, a], 0)
-        return torch.cat([torch.cat([head, a], 0), torch.cat([head, b], 0)], 1)
+            out = torch.cat([head, a], 0)
+        else:
+            out = torch.cat([torch.cat([head, a], 0), torch.cat([head, b], 0)], 1)
+        if pos0 is None:
+            return out
+        return out, pos0.reshape(1, -1, 2).repeat(1, out.shape[1] // pos0.reshape(-1, 2).shape[0], 1)
 
     @staticmethod
     def l2_select(pred, gt, mask, scenes, k):

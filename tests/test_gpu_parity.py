@@ -525,6 +525,15 @@ def test_gat_encoder_fused_equals_per_layer(nh, sizes):
             res.append((y.detach(), xi.grad, {k: p.grad.clone() for k, p in mod.named_parameters()}))
         finally:
             K.GATENC_FUSED = True
+    # the two-block input ([encoder state | pooled vector], no cat): bitwise the one-block result
+    mod.zero_grad(set_to_none=True)
+    x1, x2 = x[:, :32].clone().requires_grad_(True), x[:, 32:].clone().requires_grad_(True)
+    y2 = mod((x1, x2), None, None, lab, scenes=sc)
+    (y2 * dy).sum().backward()
+    assert torch.equal(y2, res[0][0]), "split-input output"
+    assert torch.equal(torch.cat([x1.grad, x2.grad], 1), res[0][1]), "split-input dx"
+    for k, q in mod.named_parameters():
+        assert torch.equal(q.grad, res[0][2][k]), "split-input d" + k
     (yf, dxf, gf), (yr, dxr, gr) = res
     close(yf, yr.cpu().numpy(), rtol=2e-5, what="fused out")
     close(dxf, dxr.cpu().numpy(), rtol=1e-4, what="fused dx")
@@ -550,6 +559,11 @@ def test_step_glue_kernels_match_torch():
           rtol=0, what="traj_cat")
     ar = wide[:, B:].requires_grad_(False)
     close(K.traj_cat(obs_rel, ar), torch.cat([obs_rel, ar]).cpu().numpy(), rtol=0, what="traj_cat slice")
+    pos0 = torch.randn(B, 2, device=DEV)
+    tr, st = K.traj_cat(obs_rel, a, b, pos0)
+    close(tr, torch.cat([torch.cat([obs_rel, a]), torch.cat([obs_rel, b])], 1).cpu().numpy(), rtol=0,
+          what="traj_cat + start")
+    close(st, pos0.unsqueeze(0).repeat(1, 2, 1).cpu().numpy(), rtol=0, what="traj_cat start positions")
     # decoder init: copies with a best index
     ctx = torch.randn(B, 24, device=DEV, requires_grad=True)
     z = torch.randn(k, S, 8, device=DEV)
