@@ -25,7 +25,8 @@ __device__ __forceinline__ float bce_grad(float x, float y) {
 
 __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ x, int n, int split,
                                                       const float* __restrict__ ya, const float* __restrict__ yb,
-                                                      float w, float* __restrict__ loss) {
+                                                      float w, float* __restrict__ loss,
+                                                      const float* __restrict__ addend, float* __restrict__ total) {
   __shared__ float red[2][4];
   const float a = *ya, b = *yb;
   float s0 = 0.f, s1 = 0.f;
@@ -47,7 +48,9 @@ __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ 
     const float t1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
     const float m0 = split > 0 ? t0 / (float)split : 0.f;
     const float m1 = n - split > 0 ? t1 / (float)(n - split) : 0.f;
-    *loss = w * (m0 + m1);
+    const float l = w * (m0 + m1);
+    *loss = l;
+    if (total) *total = l + *addend;
   }
 }
 
@@ -66,10 +69,12 @@ __global__ void bce_bwd_kernel(const float* __restrict__ x, int n, int split, co
 using namespace sgg;
 
 extern "C" int sgg_bce_fwd(const float* x, int n, int split, const float* ya, const float* yb, float w, float* loss,
-                           void* stream) {
+                           const float* addend, float* total, void* stream) {
   SGG_CHECK_ARG(loss && ya && yb && (n == 0 || x), "sgg_bce_fwd: null pointer");
+  SGG_CHECK_ARG(!total || addend, "sgg_bce_fwd: total needs the addend");
   SGG_CHECK_ARG(n >= 0 && split >= 0 && split <= n, "sgg_bce_fwd: bad sizes n=%d split=%d", n, split);
-  hipLaunchKernelGGL(bce_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, split, ya, yb, w, loss);
+  hipLaunchKernelGGL(bce_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, split, ya, yb, w, loss,
+                     addend, total);
   SGG_RETURN_LAUNCH("sgg_bce_fwd");
 }
 

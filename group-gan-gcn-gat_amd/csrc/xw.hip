@@ -89,7 +89,7 @@ __device__ __forceinline__ void xw_walk(const XwFrag<TRANS_W, STAGED>& f, int kb
 
 __device__ __forceinline__ float xw_epi(float v, const float* bias, int n, int act) {
   if (bias) v += bias[n];
-  if (act == 1) v = v > 0.f ? v : 0.f;
+  if (act & 1) v = v > 0.f ? v : 0.f;
   return v;
 }
 
@@ -158,7 +158,10 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = row0 + kq * 4 + r;
-      if (m < M) Y[(size_t)m * ldy + n] = xw_epi(acc[t][r], bias, n, act);
+      if (m < M) {
+        float* py = Y + (size_t)m * ldy + n;
+        *py = xw_epi(acc[t][r], bias, n, act) + ((act & 2) ? *py : 0.f);
+      }
     }
   }
 }
@@ -201,9 +204,11 @@ __global__ void __launch_bounds__(256) xw_splitk_kernel(const float* __restrict_
   for (int e = threadIdx.x; e < 16 * 64; e += 256) {
     const int rr = e >> 6, cc = e & 63;
     const int m = row0 + rr, n = col0 + cc;
-    if (m < M && n < N)
-      Y[(size_t)m * ldy + n] =
-          xw_epi(((part[0][rr][cc] + part[1][rr][cc]) + part[2][rr][cc]) + part[3][rr][cc], bias, n, act);
+    if (m < M && n < N) {
+      float* py = Y + (size_t)m * ldy + n;
+      *py = xw_epi(((part[0][rr][cc] + part[1][rr][cc]) + part[2][rr][cc]) + part[3][rr][cc], bias, n, act) +
+            ((act & 2) ? *py : 0.f);
+    }
   }
 }
 
@@ -263,7 +268,10 @@ __global__ void __launch_bounds__(256) xw_bf16_kernel(const float* __restrict__ 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = row0 + kg * 4 + r;
-      if (m < M) Y[(size_t)m * ldy + n] = xw_epi(acc[t][r], bias, n, act);
+      if (m < M) {
+        float* py = Y + (size_t)m * ldy + n;
+        *py = xw_epi(acc[t][r], bias, n, act) + ((act & 2) ? *py : 0.f);
+      }
     }
   }
 }
@@ -278,7 +286,7 @@ extern "C" int sgg_xw_bf16(const float* X, int ldx, const float* Xmask, int ldm,
   SGG_CHECK_ARG(ldx >= K && ldy >= N && (trans_w ? (N == 1 || ldw >= K) : (K == 1 || ldw >= N)),
                 "sgg_xw_bf16: bad leading dims ldx=%d ldw=%d ldy=%d (M=%d K=%d N=%d trans=%d)", ldx, ldw, ldy, M, K, N,
                 trans_w);
-  SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw_bf16: act must be 0 or 1");
+  SGG_CHECK_ARG(act >= 0 && act <= 3, "sgg_xw_bf16: act must be 0..3 (bit 0 ReLU, bit 1 accumulate)");
   SGG_CHECK_ARG(!Xmask || ldm >= K, "sgg_xw_bf16: mask leading dim %d < K", ldm);
   if (M == 0) return 0;
   dim3 grid((M + 63) / 64, (N + 63) / 64);
@@ -298,7 +306,7 @@ extern "C" int sgg_xw(const float* X, int ldx, const float* Xmask, int ldm, cons
   SGG_CHECK_ARG(M >= 0 && K > 0 && N > 0, "sgg_xw: bad sizes M=%d K=%d N=%d", M, K, N);
   SGG_CHECK_ARG(ldx >= K && ldy >= N && (trans_w ? (N == 1 || ldw >= K) : (K == 1 || ldw >= N)),
                 "sgg_xw: bad leading dims ldx=%d ldw=%d ldy=%d", ldx, ldw, ldy);
-  SGG_CHECK_ARG(act == 0 || act == 1, "sgg_xw: act must be 0 or 1");
+  SGG_CHECK_ARG(act >= 0 && act <= 3, "sgg_xw: act must be 0..3 (bit 0 ReLU, bit 1 accumulate)");
   SGG_CHECK_ARG(!Xmask || ldm >= K, "sgg_xw: mask leading dim %d < K", ldm);
   if (M == 0) return 0;
   hipStream_t s = (hipStream_t)stream;

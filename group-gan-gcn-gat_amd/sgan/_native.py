@@ -76,7 +76,7 @@ SIGNATURES = {
     "sgg_lstm_wpart_rows": (_i, [_i, _i]),
     "sgg_lstm_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
     "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
-    "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p]),
+    "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p, _p]),
     "sgg_bce_bwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p]),
     "sgg_gatenc_param_size": (_i, [_i]),
     "sgg_gatenc_lds_bytes": (ctypes.c_longlong, [_i, _i, _i]),

@@ -427,8 +427,9 @@ class _Pool(torch.autograd.Function):
     transposed -> right block)."""
 
     @staticmethod
-    def forward(ctx, h, pos, W1, We, be, b1, W2, b2, scenes):
+    def forward(ctx, h, pos, W1, We, be, b1, W2, b2, scenes, link=None):
         lib = _lib()
+        ctx.link = link
         h = _rows(h, "h")
         pos = _req(pos, "pos").contiguous()
         B, Hd = h.shape
@@ -485,20 +486,45 @@ class _Pool(torch.autograd.Function):
             nb = 8.0 * B * 512 + 12.0 * B * bn + 4.0 * 512 * (2 + bn) + (4.0 * part.numel() if wgrad else 0.0)
             timer.add("sgg::pool_bwd_kernel<%d, %s>" % (bn, "true" if wgrad else "false"), (sc.S, B),
                       8.0 * B * bn * 512, nb, launch)
-        dh = xw_raw(dU, W1[:, E:], None, trans_w=False, prec="fp32") if need[0] else None
+        dh = None
+        if need[0]:
+            base = ctx.link.take() if ctx.link is not None else None
+            # dh = dU W1h (+ the other consumer's gradient of h, accumulated in the same launch)
+            dh = xw_raw(dU, W1[:, E:], None, trans_w=False, prec="fp32", out=base, act=0 if base is None else 2)
         if not wgrad:
-            return dh, None, None, None, None, None, None, None, None
+            return dh, None, None, None, None, None, None, None, None, None
         flat = torch.empty(P, device=h.device, dtype=torch.float32)     # [dW2 | dA | db2]
         N.check(lib.sgg_slab_reduce(N.ptr(part), part.shape[0], P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
         dW1 = torch.empty_like(W1)
         _, dc = xtw(h, dU, colsum=True, trans_c=True, out=dW1[:, E:])   # dW1h = dU^T h, dc = sum_j dU_j
         _, dWe, dbe = fold_bwd(W1[:, :E], We, be, flat[bn * 512:bn * 512 + 1024].view(512, 2), dc, dW=dW1[:, :E])
-        return dh, None, dW1, dWe, dbe, dc, flat[:bn * 512].view(bn, 512), flat[bn * 512 + 1024:], None
+        return dh, None, dW1, dWe, dbe, dc, flat[:bn * 512].view(bn, 512), flat[bn * 512 + 1024:], None, None
 
 
-def social_pool(h, pos, W1, We, be, b1, W2, b2, scenes):
-    """PoolHiddenNet core (models.py:497-549) -> (B, bn); see sgg_pool_fwd."""
-    out, _ = _Pool.apply(h, pos, W1, We, be, b1, W2, b2, scenes)
+class GradLink:
+    """Carries one input gradient from a backward to a LATER backward of the
+    same tensor's other consumer, which adds it inside its own launch: the
+    generator's encoder state feeds the pooling net and (as the first input
+    block) the GAT encoder, whose backward runs first; the pooling backward's
+    dh = dU W1h then accumulates it (sgg_xw act bit 1) instead of autograd
+    summing the two gradients in an extra launch."""
+
+    def __init__(self):
+        self.grad = None
+
+    def put(self, g):
+        assert self.grad is None, "GradLink: gradient already pending"
+        self.grad = g.contiguous()
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
+def social_pool(h, pos, W1, We, be, b1, W2, b2, scenes, link=None):
+    """PoolHiddenNet core (models.py:497-549) -> (B, bn); see sgg_pool_fwd.
+    link: a GradLink whose pending gradient of h the backward adds to dh."""
+    out, _ = _Pool.apply(h, pos, W1, We, be, b1, W2, b2, scenes, link)
     return out
 
 
@@ -579,8 +605,9 @@ class _GatEnc(torch.autograd.Function):
     the inter GAT, out_embedding weight, bias -- the slab order of sgg.h."""
 
     @staticmethod
-    def forward(ctx, x, labels, scenes, nh, alpha, x2, *params):
+    def forward(ctx, x, labels, scenes, nh, alpha, x2, link, *params):
         lib = _lib()
+        ctx.link = link
         x = _rows(x, "x")
         B = x.shape[0]
         if x2 is not None:
@@ -637,7 +664,10 @@ class _GatEnc(torch.autograd.Function):
         for q in ps:
             grads.append(flat[o:o + q.numel()].view_as(q))
             o += q.numel()
-        return (dx, None, None, None, None, dx2) + tuple(grads)
+        if ctx.link is not None and ctx.needs_input_grad[0]:
+            ctx.link.put(dx)   # added by the pooling backward (the other consumer of x), which runs next
+            dx = None
+        return (dx, None, None, None, None, dx2, None) + tuple(grads)
 
 
 def _gatenc_flops(scenes, nh):
@@ -684,11 +714,13 @@ def gat_encoder_fused_ok(scenes, nh, need_grad):
     return _lib().sgg_gatenc_lds_bytes(max(scenes.max_n, 1), nh, int(bool(need_grad))) <= 160 * 1024
 
 
-def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None):
+def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None, link=None):
     """GATEncoder.forward (models.py:254-294) for all scenes: (B, 40) -> (B, 24).
-    x2: the input as two column blocks [x | x2] (no concatenation copy)."""
+    x2: the input as two column blocks [x | x2] (no concatenation copy).
+    link: a GradLink that takes the gradient of x instead of returning it
+    (x's other consumer, the pooling net, adds it in its own backward)."""
     lab = _req(labels, "labels").contiguous().view(-1)
-    return _GatEnc.apply(x, lab, scenes, nh, alpha, x2, *params)
+    return _GatEnc.apply(x, lab, scenes, nh, alpha, x2, link, *params)
 
 
 class _SegNorm(torch.autograd.Function):
@@ -959,8 +991,8 @@ class _Bce(torch.autograd.Function):
         ctx.shape = x.shape
         x = _req(x, "scores").contiguous().view(-1)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
-        N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
-                                   N.stream_ptr()), "sgg_bce_fwd")
+        N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss), None,
+                                   None, N.stream_ptr()), "sgg_bce_fwd")
         ctx.meta = (split, float(w))
         ctx.save_for_backward(x, ya, yb)
         return loss
@@ -999,6 +1031,46 @@ def _scalar_dev(y, device):
     if torch.is_tensor(y):
         return y.to(device=device, dtype=torch.float32).reshape(())
     return const(y, device)
+
+
+class _BceTotal(torch.autograd.Function):
+    """(bce, bce + addend) in one launch: the generator's adversarial term
+    and its total loss with the L2 term (no separate add launch)."""
+
+    @staticmethod
+    def forward(ctx, x, ya, yb, split, w, addend):
+        ctx.shape = x.shape
+        x = _req(x, "scores").contiguous().view(-1)
+        addend = _req(addend, "addend").reshape(())
+        loss = torch.empty((), device=x.device, dtype=torch.float32)
+        total = torch.empty((), device=x.device, dtype=torch.float32)
+        N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
+                                   N.ptr(addend), N.ptr(total), N.stream_ptr()), "sgg_bce_fwd")
+        ctx.meta = (split, float(w))
+        ctx.save_for_backward(x, ya, yb)
+        ctx.set_materialize_grads(False)
+        return loss, total
+
+    @staticmethod
+    def backward(ctx, g_loss, g_total):
+        x, ya, yb = ctx.saved_tensors
+        split, w = ctx.meta
+        g = g_total if g_loss is None else (g_loss if g_total is None else g_loss + g_total)
+        dx = None
+        if g is not None and ctx.needs_input_grad[0]:
+            g = g.contiguous()
+            dx = torch.empty_like(x)
+            N.check(_lib().sgg_bce_bwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), w, N.ptr(g), N.ptr(dx),
+                                       N.stream_ptr()), "sgg_bce_bwd")
+            dx = dx.view(ctx.shape)
+        return dx, None, None, None, None, g_total
+
+
+def bce_pair_total(scores, split, y_a, y_b, w, addend):
+    """(bce_pair(...), bce_pair(...) + addend) from one launch; the backward of
+    the total passes its gradient to the addend unchanged."""
+    dev = scores.device
+    return _BceTotal.apply(scores, _scalar_dev(y_a, dev), _scalar_dev(y_b, dev), int(split), w, addend)
 
 
 def bce_pair(scores, split, y_a, y_b, w=1.0):
@@ -1070,6 +1142,7 @@ class _DecoderInit(torch.autograd.Function):
                                         N.stream_ptr()), "sgg_decoder_init")
         ctx.dims = (copies, B, Dc)
         ctx.mark_non_differentiable(rel0)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for rel0
         return h0, rel0
 
     @staticmethod

@@ -196,7 +196,7 @@ class PoolHiddenNet(nn.Module):
         self.mlp_pre_pool = make_mlp([embedding_dim + h_dim, 512, bottleneck_dim], activation=activation,
                                      batch_norm=batch_norm, dropout=dropout)
 
-    def forward(self, h_states, seq_start_end, end_pos, scenes=None):
+    def forward(self, h_states, seq_start_end, end_pos, scenes=None, link=None):
         if self.batch_norm or self.activation != "relu" or self.dropout > 0:
             raise NotImplementedError("the fused pooling kernel implements the reference configs "
                                       "(batch_norm=0, relu, dropout=0)")
@@ -204,7 +204,7 @@ class PoolHiddenNet(nn.Module):
         l1, l2 = self.mlp_pre_pool[0], self.mlp_pre_pool[2]
         emb = self.spatial_embedding
         return K.social_pool(h_states.reshape(-1, self.h_dim), end_pos, l1.weight, emb.weight, emb.bias, l1.bias,
-                             l2.weight, l2.bias, sc)
+                             l2.weight, l2.bias, sc, link=link)
 
 
 # ---------------------------------------------------------------------------
@@ -267,9 +267,10 @@ class GATEncoder(nn.Module):
             ps += [gat.out_att.W, gat.out_att.a]
         return ps + [self.out_embedding.weight, self.out_embedding.bias]
 
-    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None):
+    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None, link=None):
         """h_states: (B, 40), or the pair (encoder state, pooled vector) whose
-        concatenation it is (the fused kernel reads both blocks in place)."""
+        concatenation it is (the fused kernel reads both blocks in place).
+        link: GradLink shared with the pooling net (see kernels.GradLink)."""
         x2 = None
         if isinstance(h_states, (tuple, list)):
             h_states, x2 = h_states
@@ -282,7 +283,8 @@ class GATEncoder(nn.Module):
                                                  or any(p.requires_grad for p in params))
         if (self.gat_intra.dropout == 0 or not self.training) and K.gat_encoder_fused_ok(sc, nh, need_grad):
             # one launch per direction for the whole module (sgg_gatenc_fwd / _bwd)
-            return K.gat_encoder(h_states, end_group, sc, nh, self.gat_intra.attentions[0].alpha, params, x2=x2)
+            return K.gat_encoder(h_states, end_group, sc, nh, self.gat_intra.attentions[0].alpha, params, x2=x2,
+                                 link=link)
         if x2 is not None:
             h_states = torch.cat([h_states, x2], dim=1)
         g = sc.groups(end_group.reshape(-1))
@@ -412,9 +414,10 @@ class GCNModule(nn.Module):
         self.gcn_inter = GCN(input_dim=16, hidden_dim=hidden_dim, out_dim=out_dim, gcn_layers=gcn_layers)
         self.out_embedding = nn.Linear(out_dim * 2, final_dim)
 
-    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None):
+    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None, link=None):
         """h_states: (B, 40), or the pair (encoder state, pooled vector) whose
-        concatenation it is (the fused kernel reads both blocks in place)."""
+        concatenation it is (the fused kernel reads both blocks in place).
+        link: GradLink shared with the pooling net (see kernels.GradLink)."""
         x2 = None
         if isinstance(h_states, (tuple, list)):
             h_states, x2 = h_states
@@ -543,10 +546,14 @@ class TrajectoryGenerator(nn.Module):
         ctx = final_encoder_h.view(-1, self.encoder_h_dim)
         end_pos = obs_traj[-1]
         if self.pooling_type:
-            pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc)
-            if self.graph == "gat" and self.mlp_decoder_needed():
+            fused_gat = self.graph == "gat" and self.mlp_decoder_needed()
+            # the GAT encoder's gradient of h reaches the pooling backward, which adds it in its own launch
+            link = K.GradLink() if fused_gat and torch.is_grad_enabled() else None
+            pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc, link=link)
+            if fused_gat:
                 # the GAT encoder reads [h | pool_h] as two blocks (no cat)
-                noise_input = self.gatencoder((ctx, pool_h), seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)
+                noise_input = self.gatencoder((ctx, pool_h), seq_start_end, end_pos, obs_traj_g[-1], scenes=sc,
+                                              link=link)
                 return noise_input
             ctx = torch.cat([ctx, pool_h], dim=1)
         if self.mlp_decoder_needed():

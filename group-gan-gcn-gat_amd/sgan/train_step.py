@@ -124,6 +124,7 @@ class KernelOps:
     l2_select = staticmethod(K.l2_select)
     l2_loss = staticmethod(K.l2_loss)
     bce_pair = staticmethod(K.bce_pair)
+    bce_pair_total = staticmethod(K.bce_pair_total)
     split2 = staticmethod(K.split2)
     one = staticmethod(lambda device: K.const(1.0, device))
     # clip_grad_norm_ + Adam in two launches (sgg_adam_step; torch's state
@@ -139,6 +140,7 @@ class GanTrainer:
         optimizer step is always graph-capturable."""
         self.G, self.D = G, D
         self.ops = ops or KernelOps()
+        self._bce_override = bce_pair
         self.bce_pair = bce_pair or self.ops.bce_pair
         self.args = args or TrainArgs()
         self.dp = dp or DataParallel()
@@ -271,8 +273,13 @@ class GanTrainer:
             for p in self.d_params:
                 p.requires_grad_(True)
         y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)
-        adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global)    # gan_g_loss
-        loss = adv + (terms[0] if terms else 0.0)
+        total = getattr(self.ops, "bce_pair_total", None)
+        if terms and total is not None and self._bce_override is None:
+            # gan_g_loss and the total loss with the L2 term from one launch
+            adv, loss = total(scores, scores.shape[0], y, y, sc.B / B_global, terms[0])
+        else:
+            adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global)    # gan_g_loss
+            loss = adv + (terms[0] if terms else 0.0)
         self.opt_g.zero_grad(set_to_none=True)
         torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self._g_inputs())
         vals = self._finish(self.g_params, self.opt_g, [terms[0] if terms else adv * 0, adv, loss],

@@ -42,7 +42,9 @@ const char* sgg_last_error(void);
  * Dense node-feature transform on MFMA (v_mfma_f32_16x16x4_f32, exact fp32):
  *   Y[m, n] = act( sum_k X[m, k] * Wop[k, n] + bias[n] )
  * Wop = W (K x N row-major) when trans_w = 0, or W^T for a W stored N x K when
- * trans_w = 1.  act: 0 none, 1 ReLU.  bias may be NULL.  ldx / ldw / ldy are
+ * trans_w = 1.  act: bit 0 ReLU; bit 1 accumulate, Y = act(..) + Y (the
+ * pooling backward adds its dh into the GAT encoder's input gradient in
+ * place of an autograd sum).  bias may be NULL.  ldx / ldw / ldy are
  * the row strides of X, W (as stored) and Y (elements); a column block of a
  * wider weight (the h-half W1[:, E:] of the pooling layer) is passed in place.
  * Replaces the per-node `torch.mm(h, W)` / nn.Linear calls of
@@ -298,9 +300,11 @@ int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float*
  *   loss = w * (mean_{i < split} f(x_i, *ya) + mean_{i >= split} f(x_i, *yb))
  *   f(x, y) = max(x, 0) - x y + log(1 + exp(-|x|))
  * An empty range contributes 0.  ya, yb are device scalars (graph-capturable
- * label smoothing); loss is one device float. */
+ * label smoothing); loss is one device float.  total (optional, with the
+ * device scalar addend): *total = *loss + *addend -- the generator's total
+ * loss (gan_g_loss + the L2 term, train.py:471-474) in the same launch. */
 int sgg_bce_fwd(const float* x, int n, int split, const float* ya, const float* yb, float w, float* loss,
-                void* stream);
+                const float* addend, float* total, void* stream);
 
 /* dx_i = *gout * w / |range(i)| * df/dx(x_i, y_range(i)) with torch's
  * subgradients at 0 (clamp passes x >= 0, d|x| = sign(x) = 0 at 0). */

@@ -159,6 +159,15 @@ def test_bce_pair_matches_reference_formula():
             (ref * 1.7).backward()
             close(loss, np.array(float(ref)), rtol=2e-6, what="bce loss n=%d" % n)
             close(xa.grad, xr.grad.cpu().numpy(), rtol=2e-6, what="bce grad n=%d" % n)
+            # (bce, bce + addend) from one launch: the total's gradient reaches the addend
+            xb = x.clone().requires_grad_(True)
+            l2 = torch.tensor(0.37, device=DEV, requires_grad=True)
+            adv, tot = K.bce_pair_total(xb, split, ya, torch.tensor(yb, device=DEV), w, l2 * 1.0)
+            tot.backward(torch.tensor(1.7, device=DEV))
+            assert torch.equal(adv, loss.detach()), "bce_pair_total loss"
+            close(tot, np.array(float(ref) + 0.37), rtol=2e-6, what="bce total n=%d" % n)
+            assert torch.equal(xb.grad, xa.grad), "bce_pair_total grad"
+            close(l2.grad, np.array(1.7, np.float32), rtol=0, what="bce total d addend")
 
 
 def test_sgangat_module_vs_reference_fixture():
