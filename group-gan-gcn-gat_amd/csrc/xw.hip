@@ -43,14 +43,12 @@ struct XwFrag {
     if (STAGED) return ws[ncl[t] * kp + k];
     return TRANS_W ? W[(size_t)ncl[t] * ldw + k] : W[(size_t)k * ldw + ncl[t]];
   }
-  __device__ __forceinline__ void load(int kb, float (&aa)[kXwS4], float (&bb)[kXwS4][4]) const {
+  __device__ __forceinline__ void load_a(int kb, float (&aa)[kXwS4]) const {
     if (kb + kXwKC <= kend) {
 #pragma unroll
       for (int s = 0; s < kXwS4; ++s) {
         const int k = kb + 4 * s + kq;
         aa[s] = mrow ? keep_if(xrow[k], mrow[k] > 0.f) : xrow[k];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bb[s][t] = wval(t, k);
       }
     } else {
 #pragma unroll
@@ -58,20 +56,39 @@ struct XwFrag {
         const int k = kb + 4 * s + kq;
         const int kc = min(k, kend - 1);
         aa[s] = keep_if(xrow[kc], k < kend && (!mrow || mrow[kc] > 0.f));
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bb[s][t] = wval(t, kc);
       }
     }
+  }
+  __device__ __forceinline__ void load_b(int kb, float (&bb)[kXwS4][4]) const {
+#pragma unroll
+    for (int s = 0; s < kXwS4; ++s) {
+      const int kc = min(kb + 4 * s + kq, kend - 1);   // past kend the A operand is zero
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bb[s][t] = wval(t, kc);
+    }
+  }
+  __device__ __forceinline__ void load(int kb, float (&aa)[kXwS4], float (&bb)[kXwS4][4]) const {
+    load_a(kb, aa);
+    load_b(kb, bb);
   }
 };
 
 // acc[t] += X[rows, kb0..kend) W[kb0..kend), cols]: the next chunk's loads are
 // in flight while the current chunk runs through the MFMAs
+// apre: the first chunk's A fragments, already loaded by the caller (issued
+// before the weight staging, so the two memory latencies overlap)
 template <bool TRANS_W, bool STAGED>
-__device__ __forceinline__ void xw_walk(const XwFrag<TRANS_W, STAGED>& f, int kb0, floatx4 (&acc)[4]) {
+__device__ __forceinline__ void xw_walk(const XwFrag<TRANS_W, STAGED>& f, int kb0, floatx4 (&acc)[4],
+                                        const float (*apre)[kXwS4] = nullptr) {
   if (kb0 >= f.kend) return;
   float a0[kXwS4], b0[kXwS4][4], a1[kXwS4], b1[kXwS4][4];
-  f.load(kb0, a0, b0);
+  if (apre) {
+#pragma unroll
+    for (int s = 0; s < kXwS4; ++s) a0[s] = (*apre)[s];
+    f.load_b(kb0, b0);
+  } else {
+    f.load(kb0, a0, b0);
+  }
   for (int k0 = kb0; k0 < f.kend; k0 += 2 * kXwKC) {
     if (k0 + kXwKC < f.kend) f.load(k0 + kXwKC, a1, b1);
 #pragma unroll
@@ -106,29 +123,6 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   const int col0 = blockIdx.y * 64;
   const int ar = lane & 15;   // A row / B col within the 16x16 tile
   const int kq = lane >> 4;   // k within the 4-deep step
-  if (STAGED) {
-    // the 64 rows of the N x K weight this workgroup needs, read along k
-    // (4 loads per thread in flight before the LDS stores)
-    const int tot = 64 * K, kp = K + 1;
-    for (int e0 = threadIdx.x; e0 < tot; e0 += 4 * 256) {
-      float v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = min(e0 + u * 256, tot - 1);
-        const int nl = e / K, k = e - nl * K;
-        v[u] = W[(size_t)min(col0 + nl, N - 1) * ldw + k];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = e0 + u * 256;
-        if (e < tot) {
-          const int nl = e / K, k = e - nl * K;
-          wsm[nl * kp + k] = v[u];
-        }
-      }
-    }
-    __syncthreads();
-  }
   const int arow = row0 + ar;
   const bool arow_ok = arow < M;
   XwFrag<TRANS_W, STAGED> f;
@@ -143,11 +137,35 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   f.kq = kq;
 #pragma unroll
   for (int t = 0; t < 4; ++t) f.ncl[t] = STAGED ? min(16 * t + ar, N - 1 - col0) : min(col0 + 16 * t + ar, N - 1);
-
+  float apre[kXwS4];
+  if (STAGED) {
+    f.load_a(0, apre);   // the first X chunk in flight across the weight staging
+    // the 64 rows of the N x K weight this workgroup needs, read along k
+    // (16 loads per thread in flight before the LDS stores: one round trip for K <= 64)
+    const int tot = 64 * K, kp = K + 1;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += 16 * 256) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = min(e0 + u * 256, tot - 1);
+        const int nl = e / K, k = e - nl * K;
+        v[u] = W[(size_t)min(col0 + nl, N - 1) * ldw + k];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = e0 + u * 256;
+        if (e < tot) {
+          const int nl = e / K, k = e - nl * K;
+          wsm[nl * kp + k] = v[u];
+        }
+      }
+    }
+    __syncthreads();
+  }
   floatx4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  xw_walk(f, 0, acc);
+  xw_walk(f, 0, acc, STAGED ? &apre : nullptr);
 
   // epilogue (direct stores: an LDS-staged full-row variant measured slower,
   // 67 vs 42 us on the 25600 x 512 pooling U -- L2 merges the 64-B pieces)
