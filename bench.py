@@ -101,12 +101,19 @@ def traffic_lookup(name, key):
     """HBM bytes per launch of (kernel, launch shape) from the committed PMC
     table (tools/pmc_traffic.py: separate rocprofv3 --pmc FETCH_SIZE /
     WRITE_SIZE passes of this bench with the gfx950 corrections of
-    MI355X_MICROARCH.md), or None when the table has no such launch."""
+    MI355X_MICROARCH.md) -> (bytes, source): the exact launch shape when the
+    PMC run re-issued it (--pmc-target), else the kernel's mean over all its
+    launches in that run, else (None, None)."""
     if not os.path.exists(TRAFFIC_TABLE):
-        return None
+        return None, None
     tab = json.load(open(TRAFFIC_TABLE))
     ent = tab.get("%s|%s" % (name, list(key[1:])))
-    return None if ent is None else ent["hbm_bytes"]
+    if ent is not None:
+        return ent["hbm_bytes"], "PMC bytes of this launch shape (re-issued %d x)" % ent.get("dispatches", 0)
+    ent = tab.get("kernels", {}).get(name)
+    if ent is not None:   # the kernel's mean over every launch of the PMC run (all its launch shapes)
+        return ent["hbm_bytes"], "PMC bytes per launch, mean over the %d launches of the PMC run" % ent["dispatches"]
+    return None, None
 
 
 def kernel_table(timed, n_it):
@@ -132,8 +139,9 @@ def roofline_of(name, a):
         achieved, peak, unit, bound = a["bytes"] / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
     # the launch shape carrying most of the kernel's time: its PMC traffic
     key, r, per_it = max(a["shapes"], key=lambda s: s[2] * s[1]["ms"])
+    traffic = traffic_lookup(name, key)
     return {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": traffic_lookup(name, key),
+            "frac": round(achieved / peak, 4), "traffic": traffic[0], "traffic_source": traffic[1],
             "kernel": name, "launches_per_iteration": round(a["launches_per_iter"], 2),
             "avg_launch_us": round(us / a["launches_per_iter"], 2), "us_per_iteration": round(us, 1),
             "flop_per_launch": a["flop"] / a["launches_per_iter"],

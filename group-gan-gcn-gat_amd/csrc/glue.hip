@@ -86,19 +86,27 @@ __global__ void __launch_bounds__(512) l2_select_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float2* g2 = reinterpret_cast<const float2*>(gt);
   const float2* p2 = reinterpret_cast<const float2*>(pred);
+  const int tot = n * T;
   for (int r = wave; r < k; r += 8) {
+    // lane over the scene's (ped, step) elements, four load sets in flight per trip
     float acc = 0.f;
-    for (int i = lane; i < n; i += 64) {
-      const int p = o + i;
-      float a = 0.f;
-#pragma unroll 4
-      for (int t = 0; t < T; ++t) {
-        const float2 g = g2[(size_t)t * B + p];
-        const float2 q = p2[((size_t)t * k + r) * B + p];
-        const float dx = g.x - q.x, dy = g.y - q.y;
-        a = fmaf(mask[(size_t)p * ldm + t], fmaf(dx, dx, dy * dy), a);
+    for (int e0 = lane; e0 < tot; e0 += 256) {
+      float mk[4];
+      float2 g[4], q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = min(e0 + 64 * u, tot - 1);
+        const int i = e / T, t = e - i * T, p = o + i;
+        mk[u] = mask[(size_t)p * ldm + t];
+        g[u] = g2[(size_t)t * B + p];
+        q[u] = p2[((size_t)t * k + r) * B + p];
       }
-      acc += a;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (e0 + 64 * u < tot) {
+          const float dx = g[u].x - q[u].x, dy = g[u].y - q[u].y;
+          acc = fmaf(mk[u], fmaf(dx, dx, dy * dy), acc);
+        }
     }
     acc = wave_sum(acc);
     if (lane == 0) part[r] = acc;
@@ -133,21 +141,28 @@ __global__ void __launch_bounds__(1024) l2_loss_fwd_kernel(const float* __restri
   float run = 0.f;
   for (int s = wave; s < S; s += nw) {
     const int o = scene_off[s], n = scene_off[s + 1] - o;
+    // lane over the scene's (ped, step) elements, four independent load sets
+    // in flight per trip: one memory latency per 256 elements
     float acc = 0.f, ms = 0.f;
-    for (int i = lane; i < n; i += 64) {
-      const int p = o + i;
-      float a = 0.f, m = 0.f;
-#pragma unroll 4
-      for (int t = 0; t < T; ++t) {
-        const float mk = mask[(size_t)p * ldm + t];
-        const float2 g = g2[(size_t)t * B + p];
-        const float2 q = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
-        const float dx = g.x - q.x, dy = g.y - q.y;
-        a = fmaf(mk, fmaf(dx, dx, dy * dy), a);
-        m += mk;
+    const int tot = n * T;
+    for (int e0 = lane; e0 < tot; e0 += 256) {
+      float mk[4];
+      float2 g[4], q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = min(e0 + 64 * u, tot - 1);
+        const int i = e / T, t = e - i * T, p = o + i;
+        mk[u] = mask[(size_t)p * ldm + t];
+        g[u] = g2[(size_t)t * B + p];
+        q[u] = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
       }
-      acc += a;
-      ms += m;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (e0 + 64 * u < tot) {
+          const float dx = g[u].x - q[u].x, dy = g[u].y - q[u].y;
+          acc = fmaf(mk[u], fmaf(dx, dx, dy * dy), acc);
+          ms += mk[u];
+        }
     }
     acc = wave_sum(acc);
     ms = wave_sum(ms);
