@@ -14,11 +14,13 @@
 // Large K (>= 256: the pooling backward dh = dU W1h, K = 512) takes the
 // split-K form: a workgroup = 16 rows x 64 cols whose 4 waves each walk a
 // quarter of K, the partial tiles summed through LDS in wave order.
+#include <stdlib.h>
+
 #include "sgg_common.h"
 
 namespace sgg {
 
-constexpr int kXwKC = 32;            // K chunk: 8 MFMA k-steps, double-buffered in registers
+constexpr int kXwKC = 16;            // K chunk: 4 MFMA k-steps, double-buffered in registers
 constexpr int kXwS4 = kXwKC / 4;
 constexpr int kXwStageMaxK = 256;    // TRANS_W weights staged in LDS up to this K
 
@@ -137,27 +139,28 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   f.kq = kq;
 #pragma unroll
   for (int t = 0; t < 4; ++t) f.ncl[t] = STAGED ? min(16 * t + ar, N - 1 - col0) : min(col0 + 16 * t + ar, N - 1);
+  // the lane's four bias values, fetched up front (not a memory round trip in the epilogue)
+  float bcol[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) bcol[t] = bias ? bias[min(col0 + 16 * t + ar, N - 1)] : 0.f;
   float apre[kXwS4];
   if (STAGED) {
     f.load_a(0, apre);   // the first X chunk in flight across the weight staging
-    // the 64 rows of the N x K weight this workgroup needs, read along k
-    // (16 loads per thread in flight before the LDS stores: one round trip for K <= 64)
-    const int tot = 64 * K, kp = K + 1;
-    for (int e0 = threadIdx.x; e0 < tot; e0 += 16 * 256) {
+    // the 64 rows of the N x K weight this workgroup needs: four threads per
+    // row, thread k0 takes k = k0, k0 + 4, ... (no index division), 16 loads
+    // in flight before the LDS stores (one round trip for K <= 64)
+    const int kp = K + 1;
+    const int nl = threadIdx.x >> 2, k0 = threadIdx.x & 3;
+    const float* wrow = W + (size_t)min(col0 + nl, N - 1) * ldw;
+    float* srow = wsm + nl * kp;
+    for (int j0 = 0; j0 < K; j0 += 64) {
       float v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int e = min(e0 + u * 256, tot - 1);
-        const int nl = e / K, k = e - nl * K;
-        v[u] = W[(size_t)min(col0 + nl, N - 1) * ldw + k];
-      }
+      for (int u = 0; u < 16; ++u) v[u] = wrow[min(j0 + k0 + 4 * u, K - 1)];
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
-        const int e = e0 + u * 256;
-        if (e < tot) {
-          const int nl = e / K, k = e - nl * K;
-          wsm[nl * kp + k] = v[u];
-        }
+        const int k = j0 + k0 + 4 * u;
+        if (k < K) srow[k] = v[u];
       }
     }
     __syncthreads();
@@ -178,7 +181,9 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
       const int m = row0 + kq * 4 + r;
       if (m < M) {
         float* py = Y + (size_t)m * ldy + n;
-        *py = xw_epi(acc[t][r], bias, n, act) + ((act & 2) ? *py : 0.f);
+        float v = acc[t][r] + bcol[t];
+        if (act & 1) v = v > 0.f ? v : 0.f;
+        *py = v + ((act & 2) ? *py : 0.f);
       }
     }
   }
