@@ -150,8 +150,8 @@ def roofline_of(name, a):
             "traffic_launch": "%s %s (avg %.2f us, %.3g algorithmic B)" % (name, list(key[1:]), r["ms"] * 1e3,
                                                                           r["bytes"]),
             "note": "fp32 (f32 MFMA, same peak as VALU FMA); achieved = algorithmic work of the kernel's launches "
-                    "in one iteration / their summed device time (HIP events around back-to-back re-issues of each "
-                    "launch on its stream); traffic = PMC HBM bytes of the named launch (null if not profiled)"}
+                    "in one iteration / their summed device time (HIP events around a HIP-graph replay of back-to-back "
+                    "re-issues of each launch on its stream); traffic = PMC HBM bytes of the named launch (null if not profiled)"}
 
 
 def real_data_leg(dev, iters=20, warmup=3, batch=64):

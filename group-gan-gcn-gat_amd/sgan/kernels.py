@@ -366,8 +366,9 @@ class LaunchTimer:
     bytes (work models in DESIGN.md section 4) and a closure that re-issues
     the identical launch on the same buffers (every instrumented op is
     idempotent: it rewrites its outputs from its inputs; the closure keeps the
-    tensors alive).  `replay()` runs each distinct launch `reps` times back to
-    back between two HIP events on the current stream, so the device never
+    tensors alive).  `replay()` captures `reps` back-to-back re-issues of each
+    distinct launch into a HIP graph and replays it between two HIP events on
+    the current stream, so the device never
     waits for the host and elapsed / reps is the kernel's average device
     duration (an event pair around one eager launch would also count host
     launch latency)."""
@@ -394,18 +395,38 @@ class LaunchTimer:
         """records -> {key: dict(name, launches, flop, bytes, ms)} with ms the
         average device time of one launch."""
         res = {}
+        cur = torch.cuda.current_stream()
         for name, key, fl, nb, fn in records:
             if key in res:
                 res[key]["launches"] += 1
                 continue
-            fn()                                  # warm (instruction cache, L2)
+            # the re-issues are captured into a HIP graph and replayed, so the
+            # events bracket device work only (an eager loop of ctypes launches
+            # is host-bound for the few-us kernels)
+            side = torch.cuda.Stream()
+            side.wait_stream(cur)
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.stream(side):
+                    fn()                          # warm (instruction cache, L2)
+                    graph.capture_begin()
+                    for _ in range(reps):
+                        fn()
+                    graph.capture_end()
+            except RuntimeError:
+                graph = None
+            cur.wait_stream(side)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(reps):
-                fn()
+            if graph is not None:
+                graph.replay()
+            else:
+                for _ in range(reps):
+                    fn()
             e1.record()
             e1.synchronize()
             res[key] = dict(name=name, launches=1, flop=fl, bytes=nb, ms=e0.elapsed_time(e1) / reps)
+            del graph
         return res
 
 
