@@ -5,6 +5,7 @@ backward are hand-written HIP kernels, the parameter-gradient reductions over
 all nodes (X^T dY, column sums) included (sgg_xtw, xtw.hip).  No op has a CPU
 path.
 """
+import contextlib
 import os
 
 import torch
@@ -15,6 +16,11 @@ from . import _native as N
 GATENC_FUSED = os.environ.get("SGG_GATENC_FUSED", "1") != "0"
 # the fused GATEncoder forward keeps its layer state for the backward (0: the backward recomputes it)
 GATENC_SAVE = os.environ.get("SGG_GATENC_SAVE", "1") != "0"
+# weight-gradient reductions of the backward on a side stream (needed only by
+# the optimizer step, which joins it).  Off by default: measured slower at
+# configs[1] (61.1k vs 68.9k scenes/s graph-replayed, 12.4k vs 14.8k eager
+# real data) -- the cross-stream edges cost more than the overlap wins
+SIDE_STREAM = os.environ.get("SGG_SIDE_STREAM", "0") == "1"
 
 
 def _lib():
@@ -64,6 +70,49 @@ def precision():
 # ---------------------------------------------------------------------------
 # dense node transform
 # ---------------------------------------------------------------------------
+class _Side:
+    stream = None
+    origin = None   # the stream that must wait for the side work
+    keep = []
+    active = False
+
+
+@contextlib.contextmanager
+def side(*keep):
+    """Run the block's launches on the weight-gradient side stream: it first
+    waits for everything issued so far on the current stream; the tensors in
+    `keep` (read by the block, allocated on the current stream) stay alive
+    until side_join().  Off (SGG_SIDE_STREAM=0): the block runs in line."""
+    if not SIDE_STREAM:
+        yield
+        return
+    cur = torch.cuda.current_stream()
+    if _Side.stream is None or _Side.stream.device != cur.device:
+        _Side.stream = torch.cuda.Stream(device=cur.device)
+    st = _Side.stream
+    st.wait_stream(cur)
+    _Side.keep.extend(t for t in keep if t is not None)
+    if not _Side.active:
+        _Side.active = True
+        _Side.origin = cur
+        try:   # inside a backward pass: join when it ends (any optimizer, e.g. torch.optim.Adam, then sees .grad)
+            torch.autograd.Variable._execution_engine.queue_callback(side_join)
+        except RuntimeError:
+            pass    # outside backward: the caller joins
+    with torch.cuda.stream(st):
+        yield
+
+
+def side_join():
+    """The stream the side work was forked from waits for it (end of the
+    backward pass, or explicitly before reading .grad); no-op when idle."""
+    if _Side.active:
+        _Side.origin.wait_stream(_Side.stream)
+        _Side.keep.clear()
+        _Side.active = False
+        _Side.origin = None
+
+
 def xw_raw(x, w, bias=None, trans_w=False, act=0, out=None, mask=None, prec=None):
     """act(x @ W + bias); W = w (K x N) or w^T (w stored N x K, trans_w).  w
     may be a row-strided column block (e.g. W1[:, E:]), passed in place.
@@ -251,7 +300,8 @@ class _XW(torch.autograd.Function):
             dx = xw_raw(dy, w, None, not ctx.trans_w, 0, mask=m, prec="fp32")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             # X^T dY (K x N); nn.Linear-layout weights take it transposed (N x K)
-            dw, cs = xtw(x, dy, colsum=True, trans_c=ctx.trans_w, mask=m)
+            with side(x, dy, m):
+                dw, cs = xtw(x, dy, colsum=True, trans_c=ctx.trans_w, mask=m)
             db = cs if ctx.has_bias else None
         return dx, dw, db, None, None
 
@@ -514,11 +564,14 @@ class _Pool(torch.autograd.Function):
             dh = xw_raw(dU, W1[:, E:], None, trans_w=False, prec="fp32", out=base, act=0 if base is None else 2)
         if not wgrad:
             return dh, None, None, None, None, None, None, None, None, None
-        flat = torch.empty(P, device=h.device, dtype=torch.float32)     # [dW2 | dA | db2]
-        N.check(lib.sgg_slab_reduce(N.ptr(part), part.shape[0], P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
-        dW1 = torch.empty_like(W1)
-        _, dc = xtw(h, dU, colsum=True, trans_c=True, out=dW1[:, E:])   # dW1h = dU^T h, dc = sum_j dU_j
-        _, dWe, dbe = fold_bwd(W1[:, :E], We, be, flat[bn * 512:bn * 512 + 1024].view(512, 2), dc, dW=dW1[:, :E])
+        with side(part, h, dU, W1, We, be):
+            flat = torch.empty(P, device=h.device, dtype=torch.float32)     # [dW2 | dA | db2]
+            N.check(lib.sgg_slab_reduce(N.ptr(part), part.shape[0], P, N.ptr(flat), N.stream_ptr()),
+                    "sgg_slab_reduce")
+            dW1 = torch.empty_like(W1)
+            _, dc = xtw(h, dU, colsum=True, trans_c=True, out=dW1[:, E:])   # dW1h = dU^T h, dc = sum_j dU_j
+            _, dWe, dbe = fold_bwd(W1[:, :E], We, be, flat[bn * 512:bn * 512 + 1024].view(512, 2), dc,
+                                   dW=dW1[:, :E])
         return dh, None, dW1, dWe, dbe, dc, flat[:bn * 512].view(bn, 512), flat[bn * 512 + 1024:], None, None
 
 
@@ -679,8 +732,9 @@ class _GatEnc(torch.autograd.Function):
                       4.0 * (B * (40 + 1 + 24 + 40) + scenes.S * P) + _gatenc_saved_bytes(B, nh),
                       lambda a=a, keep=keep: N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()),
                                                      "sgg_gatenc_bwd"))
-        flat = torch.empty(P, device=x.device, dtype=torch.float32)
-        N.check(lib.sgg_slab_reduce(N.ptr(slab), scenes.S, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+        with side(slab):
+            flat = torch.empty(P, device=x.device, dtype=torch.float32)
+            N.check(lib.sgg_slab_reduce(N.ptr(slab), scenes.S, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
         grads, o = [], 0
         for q in ps:
             grads.append(flat[o:o + q.numel()].view_as(q))
@@ -960,31 +1014,41 @@ class _LSTMSeq(torch.autograd.Function):
             timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), int(wpart is not None), 1).decode(),
                       (T, B, int(decoder), int(wpart is not None)), fl, nb, launch)
         dW_ih = dW_hh = db_ih = db_hh = dWe = dbe = dWp = dbp = None
-        if wgrad:
-            if wpart is not None:
-                flat = torch.empty(P, device=dev, dtype=torch.float32)     # [dW_hh | dbias | dA]
-                N.check(lib.sgg_slab_reduce(N.ptr(wpart), rows, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
-                dW_hh = flat[:G4 * H].view(G4, H)
-                dbias = flat[G4 * H:G4 * H + G4]
-                dA = flat[G4 * H + G4:].view(G4, 2)
-            else:
-                dGf = dG.view(T * B, G4)
-                # dW_hh = dG^T h_{t-1} (4H x H, transposed reduction), dbias = sum dG
-                dW_hh, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True, trans_c=True)
-                rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0) if decoder else rel
-                dA = xtw(rel_in.reshape(T * B, 2), dGf, trans_c=True)                   # 4H x 2
-            db_hh = torch.empty_like(dbias)          # two leaves: no shared gradient storage
-            dW_ih, dWe, dbe = fold_bwd(W_ih, We, be, dA, dbias, dbias_copy=db_hh)
-            db_ih = dbias
-        if decoder:
-            if need[9] or need[10]:
+        side_ctx = side(wpart, dG, h_all, rel, rel_out, drel_tot, W_ih, We, be) if wgrad or decoder \
+            else contextlib.nullcontext()
+        with side_ctx:
+            if wgrad:
+                dW_ih, dW_hh, db_ih, db_hh, dWe, dbe = _lstm_wgrads(lib, wpart, rows, P, G4, H, T, B, dG, h_all,
+                                                                    rel, rel_out, decoder, W_ih, We, be, dev)
+            if decoder and (need[9] or need[10]):
                 dr = drel_tot.view(T * B, 2)
                 dWp, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True, trans_c=True)
+        if decoder:
             drel = drel_in[0]
         else:
             drel = drel_in
         return (drel, dW_ih, dW_hh, db_ih, db_hh, dWe, dbe, (dh0 if has_h0 else None), None, dWp, dbp,
                 None, None, None)
+
+
+def _lstm_wgrads(lib, wpart, rows, P, G4, H, T, B, dG, h_all, rel, rel_out, decoder, W_ih, We, be, dev):
+    """dW_ih, dW_hh, db_ih, db_hh, dWe, dbe of an LSTM sequence from the
+    kernel's slab (or from dG for the families that write it)."""
+    if wpart is not None:
+        flat = torch.empty(P, device=dev, dtype=torch.float32)     # [dW_hh | dbias | dA]
+        N.check(lib.sgg_slab_reduce(N.ptr(wpart), rows, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+        dW_hh = flat[:G4 * H].view(G4, H)
+        dbias = flat[G4 * H:G4 * H + G4]
+        dA = flat[G4 * H + G4:].view(G4, 2)
+    else:
+        dGf = dG.view(T * B, G4)
+        # dW_hh = dG^T h_{t-1} (4H x H, transposed reduction), dbias = sum dG
+        dW_hh, dbias = xtw(h_all[:T].reshape(T * B, H), dGf, colsum=True, trans_c=True)
+        rel_in = torch.cat([rel.unsqueeze(0), rel_out[:-1]], 0) if decoder else rel
+        dA = xtw(rel_in.reshape(T * B, 2), dGf, trans_c=True)                   # 4H x 2
+    db_hh = torch.empty_like(dbias)          # two leaves: no shared gradient storage
+    dW_ih, dWe, dbe = fold_bwd(W_ih, We, be, dA, dbias, dbias_copy=db_hh)
+    return dW_ih, dW_hh, dbias, db_hh, dWe, dbe
 
 
 def lstm_sequence(rel, lstm, emb, h0=None, c0=None, proj=None, decoder=False, T=None):

@@ -171,6 +171,7 @@ class GanTrainer:
 
     def _finish(self, params, opt, loss_terms, clip):
         """all-reduce grads (+ loss values), clip, step."""
+        K.side_join()   # the weight gradients of the side stream (normally joined at the end of backward)
         grads = [p.grad for p in params if p.grad is not None]
         if self.dp.on and self.dp.world > 1:   # the loss values ride along with the gradients
             vals = torch.stack([t.detach().reshape(()) for t in loss_terms])

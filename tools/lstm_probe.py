@@ -21,6 +21,8 @@ def main():
     dev = "cuda"
     cases = [("D enc wgrad", 48, 20, 2560, False, True), ("D enc frozen", 48, 20, 1280, False, False),
              ("G enc", 32, 8, 1280, False, True), ("G dec", 32, 12, 2560, True, True)]
+    if os.environ.get("LSTM_PROBE_MORE"):   # batch-size vs weight-gradient effects of the D encoder
+        cases += [("D wgrad 1280", 48, 20, 1280, False, True), ("D frozen 2560", 48, 20, 2560, False, False)]
     for name, H, T, B, dec, wgrad in cases:
         if dec:
             mod = M.Decoder(T, 16, H, 64, 1, False).to(dev)
