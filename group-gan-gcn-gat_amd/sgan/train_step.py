@@ -379,11 +379,32 @@ class GraphedTrainer:
         # the replay never depends on capturing a collective (gloo cannot be
         # captured; a failed capture would poison the stream).
         self.segments = []
-        K.clear_fold_cache()   # every fold the replays need must be a node of the graph
+        self.pair = []
         pool = torch.cuda.graph_pool_handle()
         dp = trainer.dp
         cap = torch.cuda.Stream()
         cap.wait_stream(torch.cuda.current_stream())
+        if not (dp.on and dp.world > 1):
+            # one rank: TWO graphs, each starting with the H2D copy of its own
+            # pinned staging buffer, replayed alternately -- the next replay is
+            # queued behind the running one with no host copy between them,
+            # and the host fills buffer i while graph i's previous replay
+            # (two steps back) is known to be done
+            for i in range(2):
+                K.clear_fold_cache()   # every fold the replays need must be a node of this graph
+                with torch.cuda.stream(cap):
+                    g = torch.cuda.CUDAGraph()
+                    g.capture_begin(pool=pool)
+                    self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
+                    losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
+                    g.capture_end()
+                self.pair.append((g, losses))
+            torch.cuda.current_stream().wait_stream(cap)
+            torch.cuda.synchronize()
+            self.done_ev = [None, None]
+            self.losses = self.pair[0][1]
+            return
+        K.clear_fold_cache()   # every fold the replays need must be a node of the graph
         with torch.cuda.stream(cap):
             g = torch.cuda.CUDAGraph()
             g.capture_begin(pool=pool)
@@ -423,6 +444,24 @@ class GraphedTrainer:
     def step(self):
         """Draw this iteration's host RNG numbers, replay the graph; returns the
         (device) loss dicts of the captured step."""
+        if self.pair:
+            i = self.cur
+            self.cur ^= 1
+            if self.done_ev[i] is not None:
+                self.done_ev[i].synchronize()     # graph i's previous replay has read buffer i
+            z_d, z_g, y = self.t.draw_inputs(*self.span)
+            h_zd, h_zg, h_y = self.stage[i]
+            if z_d is not None:
+                h_zd.copy_(z_d)
+            if z_g is not None:
+                h_zg.copy_(z_g)
+            h_y.copy_(y)
+            g, self.losses = self.pair[i]
+            g.replay()
+            ev = torch.cuda.Event()
+            ev.record()
+            self.done_ev[i] = ev
+            return self.losses
         self._load(*self.t.draw_inputs(*self.span))
         for g, tensors in self.segments:
             g.replay()
