@@ -645,10 +645,30 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
   int* Mp = reinterpret_cast<int*>(ginv + NP);
   unsigned long long* gm = reinterpret_cast<unsigned long long*>(lab + gm_offset(NP));
   const int tid = threadIdx.x;
+  // element e = r * FI + k of a scene's input rows (the split input: X2)
+  auto xval = [&](int o, int e) -> float {
+    const int r = e / FI, k = e - r * FI;
+    return p.X2 && k >= p.kx1 ? p.X2[(size_t)(o + r) * p.ldx2 + (k - p.kx1)] : p.X[(size_t)(o + r) * p.ldx + k];
+  };
+  // the first scene's inputs are loaded before the weight staging so their
+  // latency hides under it (registers; stored after the staging)
+  constexpr int kXPre = 3;
+  const int o0 = p.scene_off[blockIdx.x], n0 = p.scene_off[blockIdx.x + 1] - o0;
+  const bool pre = n0 > 0 && n0 * FI <= kXPre * (int)blockDim.x;   // uniform
+  float xp[kXPre];
+  float lp = 0.f;
+  if (pre) {
+#pragma unroll
+    for (int m = 0; m < kXPre; ++m) {
+      const int e = tid + m * (int)blockDim.x;
+      xp[m] = e < n0 * FI ? xval(o0, e) : 0.f;
+    }
+    if (tid < n0) lp = p.labels[o0 + tid];
+  }
   PMARK(40);
   LW lw;
   stage_weights(sm + L.wts, tab, lw);
-  // (the first scene's input loads are followed by a barrier before any use)
+  // (the first scene's input stores are followed by a barrier before any use)
   PMARK(41);
 
   for (int sc = blockIdx.x; sc < p.S; sc += gridDim.x) {
@@ -656,28 +676,37 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     const int n = p.scene_off[sc + 1] - o;
     if (n <= 0) continue;   // uniform over the workgroup
     PMARK(0);
+    const bool first = pre && sc == (int)blockIdx.x;   // uniform
     float* saved = p.saved ? p.saved + (size_t)sc * SL.total : nullptr;
-    // ---- inputs and group structure ------------------------------------
-    for (int e = tid; e < n * FI; e += blockDim.x) {
-      const int r = e / FI, k = e - r * FI;
-      X[r * P40 + k] = p.X2 && k >= p.kx1 ? p.X2[(size_t)(o + r) * p.ldx2 + (k - p.kx1)]
-                                          : p.X[(size_t)(o + r) * p.ldx + k];
-    }
-    if (!BWD || !saved) {
-      for (int i = tid; i < n; i += blockDim.x) lab[i] = p.labels[o + i];
+    // ---- inputs and group structure (one phase) ------------------------
+    if (first) {
+#pragma unroll
+      for (int m = 0; m < kXPre; ++m) {
+        const int e = tid + m * (int)blockDim.x;
+        if (e < n * FI) {
+          const int r = e / FI;
+          X[r * P40 + (e - r * FI)] = xp[m];
+        }
+      }
     } else {
-      rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
+      for (int e = tid; e < n * FI; e += blockDim.x) {
+        const int r = e / FI;
+        X[r * P40 + (e - r * FI)] = xval(o, e);
+      }
     }
-    lds_barrier(); PMARK(1);
-    if (!BWD || !saved) {
-      // group structure (models.py:263-278) in ONE wave, lane = ped (n <= 64):
+    if (BWD && saved) {
+      rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
+    } else {
+      // group structure (models.py:263-278) in ONE wave, lane = ped (n <= 64),
+      // from the labels in global memory (no barrier after the X stores):
       // the lowest ungrouped ped leads the next group, its members are the
       // peds with its non-zero label (a zero label: itself alone); groups are
       // ranked by their first member, as the reference's unique rows
       if (tid < 64) {
         const int i = tid;
         const bool in = i < n;
-        const float li = in ? lab[i] : 0.f;
+        const float li = !in ? 0.f : first ? lp : p.labels[o + i];
+        if (in) lab[i] = li;
         unsigned long long rem = __ballot(in);
         int g = i, r = 0, c = 1, m = 0;
         while (rem) {   // wave-uniform
@@ -701,8 +730,8 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         }
         if (i == 0) *Mp = m;
       }
-      lds_barrier(); PMARK(2);
     }
+    lds_barrier(); PMARK(1); PMARK(2);
     const int M = *Mp;
 
     if (!BWD || !saved) {
