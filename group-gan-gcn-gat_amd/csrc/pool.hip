@@ -219,6 +219,178 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
   }
 }
 
+// ---- forward, fragment-native tiles ------------------------------------------
+// Same work units, chunk order, arithmetic and epilogue as pool_fwd_kernel, but
+// each 64-unit k-tile is stored in LDS in the order the MFMA lanes consume it:
+// unit k = 4 s + kq of the tile (k-step s, lane quarter kq) sits at column
+// 16 kq + s, so a lane's 16 k-steps of U[j, .], W2[c, .] and (A_x, A_y) are
+// contiguous and come in with a few ds_read_b128 issued together at the top of
+// the tile -- one LDS latency per 16 k-steps instead of one per k-step -- and
+// the next tile's global loads are in flight meanwhile (register-staged).
+constexpr int kVP = kKT + 4;     // row pitch (16-B aligned rows; 4 j mod 64 -> b128 reads spread over the banks)
+
+__device__ __forceinline__ int perm16(int k) { return (k & 3) * 16 + (k >> 2); }
+
+template <int BN, int GPW>
+__global__ void __launch_bounds__(256) pool_fwd_v_kernel(
+    const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
+    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+  constexpr int NT = PoolCfg<BN>::NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Us = reinterpret_cast<float*>(smem);                              // 64 x kVP
+  float* W2s = Us + SGG_POOL_MAX_PEDS * kVP;                               // 16 NT x kVP
+  float* As = W2s + 16 * NT * kVP;                                         // 4 kq x 16 s x 2
+  float2* ps = reinterpret_cast<float2*>(As + 2 * kKT);                    // scene positions (<= 64)
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // 64 x BN
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kq = lane >> 4;
+
+  const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);   // XCD-aware (pool_fwd_kernel)
+  for (int ch = xb; ch < nchunks; ch += gridDim.x) {
+    const int4 cd = chunks[ch];
+    const int s = cd.x, i0 = cd.y, i1 = cd.z;
+    const int o = scene_off[s];
+    const int n = scene_off[s + 1] - o;
+    const int rows = i1 - i0;
+    const int npairs = rows * n;
+
+    for (int q = threadIdx.x; q < n; q += blockDim.x) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) keys[q] = 0ull;
+    __syncthreads();
+
+    int uoff[GPW];
+    float rx[GPW], ry[GPW];
+    floatx4 acc[GPW][NT];
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int p = (wave * GPW + g) * 16 + c16;
+      int il = 0, j = 0;
+      if (p < npairs) { il = p / n; j = p - il * n; }
+      uoff[g] = j * kVP + 16 * kq;
+      const float2 pj = ps[j], pi = ps[i0 + il];
+      rx[g] = p < npairs ? pj.x - pi.x : 0.f;
+      ry[g] = p < npairs ? pj.y - pi.y : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + 255) / 256;   // float4 of U per thread
+    constexpr int kWQ = (16 * NT * (kKT / 4) + 255) / 256;            // float4 of W2 per thread
+    float4 ureg[kUQ], wreg[kWQ];
+    float areg = 0.f;
+    auto load_tile = [&](int k0) {
+#pragma unroll
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n) ureg[e] = *reinterpret_cast<const float4*>(U + (size_t)(o + r) * kHidden + k0 + 4 * c4);
+      }
+#pragma unroll
+      for (int e = 0; e < kWQ; ++e) {   // W2 rows (nn.Linear layout), rows >= BN are zero
+        const int q = threadIdx.x + 256 * e;
+        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
+        wreg[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c < BN) wreg[e] = *reinterpret_cast<const float4*>(W2 + (size_t)c * kHidden + k0 + 4 * c4);
+      }
+      if (threadIdx.x < 2 * kKT) areg = A[2 * k0 + threadIdx.x];
+    };
+    // float4 c4 of a row holds units 4 c4 .. 4 c4 + 3 = k-step c4 of lane quarters 0..3
+    auto store_tile = [&]() {
+#pragma unroll
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n) {
+          float* d = Us + r * kVP + c4;
+          d[0] = ureg[e].x; d[16] = ureg[e].y; d[32] = ureg[e].z; d[48] = ureg[e].w;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < kWQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
+        if (c < 16 * NT) {
+          float* d = W2s + c * kVP + c4;
+          d[0] = wreg[e].x; d[16] = wreg[e].y; d[32] = wreg[e].z; d[48] = wreg[e].w;
+        }
+      }
+      if (threadIdx.x < 2 * kKT) {   // (A_x, A_y) of unit k at [kq][s]
+        const int k = threadIdx.x >> 1;
+        As[2 * perm16(k) + (threadIdx.x & 1)] = areg;
+      }
+    };
+    load_tile(0);
+    __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
+    store_tile();
+    __syncthreads();
+    for (int k0 = 0; k0 < kHidden; k0 += kKT) {
+      if (k0 + kKT < kHidden) load_tile(k0 + kKT);
+      // the lane's 16 k-steps of operands, in the order they are consumed
+      float uu[GPW][16], aa[32], bb[NT][16];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+#pragma unroll
+        for (int g = 0; g < GPW; ++g)
+          *reinterpret_cast<float4*>(&uu[g][4 * v]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 4 * v);
+        *reinterpret_cast<float4*>(&aa[8 * v]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v);
+        *reinterpret_cast<float4*>(&aa[8 * v + 4]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v + 4);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          *reinterpret_cast<float4*>(&bb[t][4 * v]) =
+              *reinterpret_cast<const float4*>(W2s + (16 * t + c16) * kVP + 16 * kq + 4 * v);
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < kKT / 4; ++s4) {
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) {
+          const float h = fmaxf(fmaf(aa[2 * s4 + 1], ry[g], fmaf(aa[2 * s4], rx[g], uu[g][s4])), 0.f);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(h, bb[t][s4], acc[g][t], 0, 0, 0);
+        }
+      }
+      __syncthreads();  // tile consumed
+      if (k0 + kKT < kHidden) {
+        store_tile();
+        __syncthreads();
+      }
+    }
+
+    // epilogue: bias, ReLU, max over j (as pool_fwd_kernel)
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int grp = wave * GPW + g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = grp * 16 + kq * 4 + r;
+        if (p < npairs) {
+          const int il = p / n, j = p - il * n;
+          const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int cc = 16 * t + c16;
+            if (cc < BN) {
+              float v = acc[g][t][r] + b2[cc];
+              v = v > 0.f ? v : 0.f;
+              atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) {
+      const unsigned long long key = keys[q];
+      const size_t oi = (size_t)(o + i0) * BN + q;
+      out[oi] = __uint_as_float((unsigned)(key >> 32));
+      argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+    }
+    __syncthreads();
+  }
+}
+
 // ---- forward, resident form -------------------------------------------------
 // When the whole W2^T (bn rows x 512, rows padded to 16 NT with zeros) and a
 // scene's U rows fit in LDS beside each other: the workgroup stages W2 and A
@@ -483,15 +655,22 @@ static void launch_fwd_g(const float* U, const float* pos, const float* A, const
   const int grid = nchunks < 65536 ? (nchunks + 7) & ~7 : 65536;   // multiple of 8 (XCD-aware order)
   const size_t lds = pool_fwd_lds<BN>(max_rows);
   const int4* ck = reinterpret_cast<const int4*>(chunks);
-  // <= 4 chunks per CU and <= 2 pair groups per wave: full unroll (measured
-  // 5-8 % faster at 64-128 scenes; 10-20 % slower at >= 1024 scenes where
-  // occupancy hides the LDS latency, and at gpw 4 the wave needs ~350 VGPRs)
-  if (GPW <= 2 && nchunks <= 4 * device_cus())
-    hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW, kKT / 4>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off,
-                       ck, nchunks, out, am);
-  else
-    hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW, 2>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off, ck,
-                       nchunks, out, am);
+  // small grids (<= 4 chunks per CU, <= 2 pair groups per wave): the
+  // fragment-native tiles (measured 1.25-1.45x faster at 64-128 scenes;
+  // slower at gpw 4 / >= 1024 scenes, where occupancy hides the LDS latency)
+  if constexpr (GPW <= 2) {
+    const char* vv = getenv("SGG_POOL_V");
+    if (nchunks <= 4 * device_cus() && !(vv && vv[0] == '0')) {
+      const size_t lv = sizeof(float) * ((size_t)SGG_POOL_MAX_PEDS * kVP + (size_t)16 * PoolCfg<BN>::NT * kVP +
+                                         2 * kKT) +
+                        sizeof(float2) * SGG_POOL_MAX_PEDS + sizeof(unsigned long long) * (size_t)max_rows * BN;
+      hipLaunchKernelGGL((pool_fwd_v_kernel<BN, GPW>), dim3(grid), dim3(256), lv, st, U, pos, A, W2, b2, off, ck,
+                         nchunks, out, am);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW, 2>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off, ck,
+                     nchunks, out, am);
 }
 // j ranges per scene of the backward: S x jq units ~ one round of the chip
 static int pool_bwd_jq(int S) {
@@ -525,8 +704,8 @@ static void launch_fwd_res(const float* U, const float* pos, const float* A, con
   const int per_cu = (int)((160u * 1024u) / lds);
   long long grid = (long long)device_cus() * (per_cu < 1 ? 1 : per_cu);
   if (grid > nchunks) grid = nchunks;
-  hipLaunchKernelGGL((pool_fwd_res_kernel<BN, GPW>), dim3((unsigned)grid), dim3(256), lds, st, U, pos, A, W2, b2, off,
-                     reinterpret_cast<const int4*>(chunks), nchunks, max_n, out, am);
+  hipLaunchKernelGGL((pool_fwd_res_kernel<BN, GPW>), dim3((unsigned)grid), dim3(256), lds, st, U, pos, A,
+                     W2, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, max_n, out, am);
 }
 
 template <int BN>

@@ -523,12 +523,11 @@ class _Pool(torch.autograd.Function):
                                      N.ptr(am), N.stream_ptr()), "sgg_pool_fwd")
         launch()
         if timer.active:
-            # the k-step unroll the library picks (pool.hip launch_fwd_g)
-            unr = 16 if gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count \
-                else 2
+            # the form the library picks (pool.hip launch_fwd_g)
+            small = gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count
+            name = "pool_fwd_v_kernel<%d, %d>" % (bn, gpw) if small else "pool_fwd_kernel<%d, %d, 2>" % (bn, gpw)
             nb = 4.0 * (B * 512 + 2 * B + 1024 + bn * 512 + bn) + 8.0 * B * bn
-            timer.add("sgg::pool_fwd_kernel<%d, %d, %d>" % (bn, gpw, unr), (scenes.S, B), _pool_flops(scenes, bn), nb,
-                      launch)
+            timer.add("sgg::" + name, (scenes.S, B), _pool_flops(scenes, bn), nb, launch)
         ctx.scenes = scenes
         ctx.E = E
         ctx.save_for_backward(h, pos, W1, We, be, A, W2, U, out, am)

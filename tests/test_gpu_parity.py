@@ -371,11 +371,13 @@ def test_fused_lstm_other_families(H, T, decoder, B, monkeypatch):
     test_fused_lstm_vs_oracle(H, T, decoder, B)
 
 
+@pytest.mark.parametrize("form", ["SGG_POOL_RESIDENT", "SGG_POOL_V"])
 @pytest.mark.parametrize("bn", [8, 48])
-def test_pool_resident_equals_tiled(bn, monkeypatch):
-    """sgg_pool_fwd's resident form (W2^T and the scene's U rows in LDS, used
-    when they fit) against the k-tiled form on the same chunk table: the
-    same MFMA sequence, so outputs and argmax are bitwise equal."""
+def test_pool_resident_equals_tiled(bn, form, monkeypatch):
+    """sgg_pool_fwd's alternative forms -- resident (W2^T and the scene's U
+    rows in LDS, used when they fit) and fragment-native k-tiles -- against the
+    k-tiled form on the same chunk table: the same MFMA sequence, so outputs
+    and argmax are bitwise equal."""
     from sgan import _native as N
     from sgan import kernels as K
     from sgan.scene import SceneIndex
@@ -393,9 +395,9 @@ def test_pool_resident_equals_tiled(bn, monkeypatch):
     res = []
     for tiled in (False, True):
         if tiled:
-            monkeypatch.delenv("SGG_POOL_RESIDENT")
+            monkeypatch.delenv(form)
         else:
-            monkeypatch.setenv("SGG_POOL_RESIDENT", "1")
+            monkeypatch.setenv(form, "1")
         out = torch.empty(B, bn, device=DEV)
         am = torch.empty(B, bn, device=DEV, dtype=torch.int32)
         N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(sc.scene_off),

@@ -1,12 +1,16 @@
-"""Pool forward: tiled vs resident form (SGG_POOL_RESIDENT) on the training shapes."""
+"""Pool forward A/B on the training shapes: tiled (default), fragment-native
+tiles (SGG_POOL_V=1), resident (SGG_POOL_RESIDENT=1)."""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from bench_kernels import run  # noqa: E402
 
-for res in ("0", "1"):
-    os.environ["SGG_POOL_RESIDENT"] = res
-    print("SGG_POOL_RESIDENT=" + res, flush=True)
-    run(64, 20, 32, 8, gpws=(1, 2))
-    run(64, 20, 48, 48, gpws=(1, 2))
-    run(128, 20, 48, 48, gpws=(1, 2, 4))
+for name, env in (("tiled", {}), ("v", {"SGG_POOL_V": "1"}), ("resident", {"SGG_POOL_RESIDENT": "1"})):
+    for k in ("SGG_POOL_V", "SGG_POOL_RESIDENT"):
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    print(name, flush=True)
+    run(64, 20, 32, 8, gpws=(0,))
+    run(64, 20, 48, 48, gpws=(0,))
+    run(128, 20, 48, 48, gpws=(0,))
+    run(4096, 20, 48, 48, gpws=(0,))
