@@ -238,11 +238,11 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
     const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
     float* __restrict__ out, int32_t* __restrict__ argmax) {
   constexpr int NT = PoolCfg<BN>::NT;
+  constexpr int TB = (SGG_POOL_MAX_PEDS + 16 * NT) * kVP + 2 * kKT;   // one tile buffer: U | W2 | A
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* Us = reinterpret_cast<float*>(smem);                              // 64 x kVP
-  float* W2s = Us + SGG_POOL_MAX_PEDS * kVP;                               // 16 NT x kVP
-  float* As = W2s + 16 * NT * kVP;                                         // 4 kq x 16 s x 2
-  float2* ps = reinterpret_cast<float2*>(As + 2 * kKT);                    // scene positions (<= 64)
+  float* const tb0 = reinterpret_cast<float*>(smem);
+  float* const tb1 = tb0 + TB;
+  float2* ps = reinterpret_cast<float2*>(tb0 + 2 * TB);                                      // scene positions
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // 64 x BN
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -298,7 +298,10 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
       if (threadIdx.x < 2 * kKT) areg = A[2 * k0 + threadIdx.x];
     };
     // float4 c4 of a row holds units 4 c4 .. 4 c4 + 3 = k-step c4 of lane quarters 0..3
-    auto store_tile = [&]() {
+    auto store_tile = [&](float* tb) {
+      float* Us = tb;
+      float* W2s = tb + SGG_POOL_MAX_PEDS * kVP;
+      float* As = W2s + 16 * NT * kVP;
 #pragma unroll
       for (int e = 0; e < kUQ; ++e) {
         const int q = threadIdx.x + 256 * e;
@@ -322,40 +325,65 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
         As[2 * perm16(k) + (threadIdx.x & 1)] = areg;
       }
     };
-    load_tile(0);
-    __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
-    store_tile();
-    __syncthreads();
-    for (int k0 = 0; k0 < kHidden; k0 += kKT) {
-      if (k0 + kKT < kHidden) load_tile(k0 + kKT);
-      // the lane's 16 k-steps of operands, in the order they are consumed
+    // the lane's 16 k-steps of operands of one tile, in the order they are consumed
+    struct Frag {
       float uu[GPW][16], aa[32], bb[NT][16];
+    };
+    auto read_frag = [&](const float* tb, Frag& F) {
+      const float* Us = tb;
+      const float* W2s = tb + SGG_POOL_MAX_PEDS * kVP;
+      const float* As = W2s + 16 * NT * kVP;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
 #pragma unroll
         for (int g = 0; g < GPW; ++g)
-          *reinterpret_cast<float4*>(&uu[g][4 * v]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 4 * v);
-        *reinterpret_cast<float4*>(&aa[8 * v]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v);
-        *reinterpret_cast<float4*>(&aa[8 * v + 4]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v + 4);
+          *reinterpret_cast<float4*>(&F.uu[g][4 * v]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 4 * v);
+        *reinterpret_cast<float4*>(&F.aa[8 * v]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v);
+        *reinterpret_cast<float4*>(&F.aa[8 * v + 4]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v + 4);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          *reinterpret_cast<float4*>(&bb[t][4 * v]) =
+          *reinterpret_cast<float4*>(&F.bb[t][4 * v]) =
               *reinterpret_cast<const float4*>(W2s + (16 * t + c16) * kVP + 16 * kq + 4 * v);
       }
+    };
+    auto compute = [&](const Frag& F) {
 #pragma unroll
       for (int s4 = 0; s4 < kKT / 4; ++s4) {
 #pragma unroll
         for (int g = 0; g < GPW; ++g) {
-          const float h = fmaxf(fmaf(aa[2 * s4 + 1], ry[g], fmaf(aa[2 * s4], rx[g], uu[g][s4])), 0.f);
+          const float h = fmaxf(fmaf(F.aa[2 * s4 + 1], ry[g], fmaf(F.aa[2 * s4], rx[g], F.uu[g][s4])), 0.f);
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(h, bb[t][s4], acc[g][t], 0, 0, 0);
+          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(h, F.bb[t][s4], acc[g][t], 0, 0, 0);
         }
       }
-      __syncthreads();  // tile consumed
-      if (k0 + kKT < kHidden) {
-        store_tile();
-        __syncthreads();
-      }
+    };
+    // two LDS tile buffers, one barrier per tile: while tile k computes (its
+    // fragments in registers), tile k + 1's fragments come in from the other
+    // buffer and tile k + 2's global loads are in flight; tile k + 2 is then
+    // stored over tile k (whose fragments every wave read before the last
+    // barrier)
+    constexpr int NKT = kHidden / kKT;   // 8 (even)
+    Frag F0, F1;
+    load_tile(0);
+    __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
+    store_tile(tb0);
+    load_tile(kKT);
+    __syncthreads();
+    read_frag(tb0, F0);
+    store_tile(tb1);
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < NKT; kt += 2) {
+      if (kt + 2 < NKT) load_tile((kt + 2) * kKT);
+      read_frag(tb1, F1);
+      compute(F0);
+      if (kt + 2 < NKT) store_tile(tb0);
+      __syncthreads();
+      if (kt + 3 < NKT) load_tile((kt + 3) * kKT);
+      if (kt + 2 < NKT) read_frag(tb0, F0);
+      compute(F1);
+      if (kt + 3 < NKT) store_tile(tb1);
+      __syncthreads();
     }
 
     // epilogue: bias, ReLU, max over j (as pool_fwd_kernel)
@@ -661,8 +689,7 @@ static void launch_fwd_g(const float* U, const float* pos, const float* A, const
   if constexpr (GPW <= 2) {
     const char* vv = getenv("SGG_POOL_V");
     if (nchunks <= 4 * device_cus() && !(vv && vv[0] == '0')) {
-      const size_t lv = sizeof(float) * ((size_t)SGG_POOL_MAX_PEDS * kVP + (size_t)16 * PoolCfg<BN>::NT * kVP +
-                                         2 * kKT) +
+      const size_t lv = sizeof(float) * 2 * ((size_t)(SGG_POOL_MAX_PEDS + 16 * PoolCfg<BN>::NT) * kVP + 2 * kKT) +
                         sizeof(float2) * SGG_POOL_MAX_PEDS + sizeof(unsigned long long) * (size_t)max_rows * BN;
       hipLaunchKernelGGL((pool_fwd_v_kernel<BN, GPW>), dim3(grid), dim3(256), lv, st, U, pos, A, W2, b2, off, ck,
                          nchunks, out, am);
