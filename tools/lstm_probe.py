@@ -21,6 +21,8 @@ def main():
     dev = "cuda"
     cases = [("D enc wgrad", 48, 20, 2560, False, True), ("D enc frozen", 48, 20, 1280, False, False),
              ("G enc", 32, 8, 1280, False, True), ("G dec", 32, 12, 2560, True, True)]
+    if os.environ.get("LSTM_PROBE_BOK"):   # the best-of-k rollout alone (20 samples x 1280 peds, no grad)
+        cases = [("G dec bok", 32, 12, 25600, True, False)]
     if os.environ.get("LSTM_PROBE_MORE"):   # batch-size vs weight-gradient effects of the D encoder
         cases += [("D wgrad 1280", 48, 20, 1280, False, True), ("D frozen 2560", 48, 20, 2560, False, False)]
     for name, H, T, B, dec, wgrad in cases:
@@ -31,7 +33,7 @@ def main():
         for p in mod.parameters():
             p.requires_grad_(wgrad)
         if dec:
-            h0 = (torch.randn(1, B, H, device=dev) * 0.5).requires_grad_(True)
+            h0 = (torch.randn(1, B, H, device=dev) * 0.5).requires_grad_(wgrad)
             lp, lr = torch.randn(B, 2, device=dev), torch.randn(B, 2, device=dev) * 0.3
             fwd = lambda: mod(lp, lr, (h0, None), None)[0]
         else:
@@ -42,14 +44,16 @@ def main():
         for _ in range(3):
             y = fwd()
             dy = torch.randn_like(y)
-            y.backward(dy)
+            if y.requires_grad:
+                y.backward(dy)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         tf = tb = 0.0
         for _ in range(reps):
             e[0].record()
             y = fwd()
             e[1].record()
-            y.backward(dy)
+            if y.requires_grad:
+                y.backward(dy)
             e[2].record()
             e[2].synchronize()
             tf += e[0].elapsed_time(e[1])
