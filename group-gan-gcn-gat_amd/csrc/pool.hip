@@ -629,18 +629,26 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
       if (j + 1 < j1) u_next = Uc[(size_t)(j + 1) * kHidden];
       const float2 pj = ps[j];
       float du = 0.f;
+      // the row's masks in blocks of 16 up front: one LDS latency per block,
+      // not per (j, c) (blocks bound the registers at bn 64)
+      constexpr int CB = BN < 16 ? BN : 16;
+      unsigned long long mrow[CB];
 #pragma unroll
       for (int c = 0; c < BN; ++c) {
-        const unsigned long long mv = msk[j * BN + c];
+        if (c % CB == 0) {
+#pragma unroll
+          for (int cc = 0; cc < CB; ++cc) mrow[cc] = msk[j * BN + c + cc];
+        }
+        const unsigned long long mv = mrow[c % CB];
         // (readfirstlane returns int: go through unsigned, no sign extension)
         const unsigned mhi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(mv >> 32));
         const unsigned mlo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mv);
         unsigned long long m = ((unsigned long long)mhi << 32) | (unsigned long long)mlo;
-        while (m) {
-          const int i = __builtin_ctzll(m);
-          m &= m - 1;
-          const float g = gs[i * BN + c];
-          const float2 pi = ps[i];
+        // two set bits per trip: both entries' LDS operands are in flight
+        // together (the walk is scalar and the reads are broadcasts, so the
+        // per-entry cost is their latency); entries are still taken in
+        // ascending i, one at a time, so every sum keeps its order
+        auto entry = [&](float g, float2 pi) {
           const float rx = pj.x - pi.x, ry = pj.y - pi.y;
           const float pre = fmaf(a1, ry, fmaf(a0, rx, u));
           const float gm = pre > 0.f ? g : 0.f;
@@ -651,6 +659,17 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
             dA0 = fmaf(d, rx, dA0);
             dA1 = fmaf(d, ry, dA1);
           }
+        };
+        while (m) {
+          const int i = __builtin_ctzll(m);
+          m &= m - 1;
+          const bool two = m != 0;   // uniform
+          const int i2 = two ? __builtin_ctzll(m) : i;
+          if (two) m &= m - 1;
+          const float g = gs[i * BN + c], g2 = gs[i2 * BN + c];
+          const float2 pi = ps[i], pi2 = ps[i2];
+          entry(g, pi);
+          if (two) entry(g2, pi2);
         }
       }
       dU[(size_t)(o + j) * kHidden + k] = du;
