@@ -72,44 +72,73 @@ __global__ void __launch_bounds__(256) decoder_init_kernel(const float* __restri
   }
 }
 
-// one workgroup (8 waves) per scene: wave w takes samples w, w + 8, ...;
-// lane = ped (its sum over the T steps of mask (gt - pred)^2: independent
-// loads), the scene sum by a wave shuffle; argmin over the k samples (first
-// minimum, as torch.argmin)
+// Both L2 kernels walk a scene's (step, ped) elements PED-FASTEST, so the gt
+// and pred reads of a wave are contiguous runs (gt / pred are step-major:
+// [T][B][2]); the scene's loss-mask block (ped-major, [B][ldm]) is first
+// staged in LDS with coalesced reads and then read at (ped, step).
+constexpr int kL2MaxElems = SGG_POOL_MAX_PEDS * 32;   // n * T staged per scene (larger: read in place)
+
+// the scene's mask block -> msk[i * T + t] (coalesced: t fastest)
+__device__ __forceinline__ void stage_mask(float* msk, const float* __restrict__ mask, int ldm, int o, int n, int T,
+                                           int t0, int nt) {
+  for (int e = t0; e < n * T; e += nt) {
+    const int i = e / T, t = e - i * T;
+    msk[e] = mask[(size_t)(o + i) * ldm + t];
+  }
+}
+
+// one workgroup (8 waves) per scene: wave w takes samples w, w + 8, ...
+// (their loads together); lane = element, the scene sum by a wave shuffle;
+// argmin over the k samples (first minimum, as torch.argmin)
 __global__ void __launch_bounds__(512) l2_select_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
                                                         const float* __restrict__ mask, int ldm,
                                                         const int32_t* __restrict__ scene_off, int T, int B, int k,
                                                         int64_t* __restrict__ best) {
   __shared__ float part[256];   // k <= 256
+  __shared__ float msk[kL2MaxElems];
   const int s = blockIdx.x;
   const int o = scene_off[s], n = scene_off[s + 1] - o;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float2* g2 = reinterpret_cast<const float2*>(gt);
   const float2* p2 = reinterpret_cast<const float2*>(pred);
   const int tot = n * T;
-  for (int r = wave; r < k; r += 8) {
-    // lane over the scene's (ped, step) elements, four load sets in flight per trip
-    float acc = 0.f;
-    for (int e0 = lane; e0 < tot; e0 += 256) {
-      float mk[4];
-      float2 g[4], q[4];
+  const bool staged = tot <= kL2MaxElems;   // uniform
+  if (staged) stage_mask(msk, mask, ldm, o, n, T, threadIdx.x, blockDim.x);
+  __syncthreads();
+  constexpr int kRS = 4;
+  for (int r0 = wave; r0 < k; r0 += 8 * kRS) {
+    float acc[kRS];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+    for (int j = 0; j < kRS; ++j) acc[j] = 0.f;
+    for (int e0 = lane; e0 < tot; e0 += 128) {
+      float mk[2];
+      float2 g[2], q[kRS][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
         const int e = min(e0 + 64 * u, tot - 1);
-        const int i = e / T, t = e - i * T, p = o + i;
-        mk[u] = mask[(size_t)p * ldm + t];
+        const int t = e / n, i = e - t * n, p = o + i;
+        mk[u] = staged ? msk[i * T + t] : mask[(size_t)p * ldm + t];
         g[u] = g2[(size_t)t * B + p];
-        q[u] = p2[((size_t)t * k + r) * B + p];
+#pragma unroll
+        for (int j = 0; j < kRS; ++j) {
+          const int r = min(r0 + 8 * j, k - 1);
+          q[j][u] = p2[((size_t)t * k + r) * B + p];
+        }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (e0 + 64 * u < tot) {
-          const float dx = g[u].x - q[u].x, dy = g[u].y - q[u].y;
-          acc = fmaf(mk[u], fmaf(dx, dx, dy * dy), acc);
-        }
+      for (int j = 0; j < kRS; ++j)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (e0 + 64 * u < tot) {
+            const float dx = g[u].x - q[j][u].x, dy = g[u].y - q[j][u].y;
+            acc[j] = fmaf(mk[u], fmaf(dx, dx, dy * dy), acc[j]);
+          }
     }
-    acc = wave_sum(acc);
-    if (lane == 0) part[r] = acc;
+#pragma unroll
+    for (int j = 0; j < kRS; ++j) {
+      const float a = wave_sum(acc[j]);
+      if (lane == 0 && r0 + 8 * j < k) part[r0 + 8 * j] = a;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -124,62 +153,55 @@ __global__ void __launch_bounds__(512) l2_select_kernel(const float* __restrict_
   }
 }
 
-// single workgroup: wave w takes scenes w, w + 16, ... (lane = ped: its sums
-// over the T steps of mask (gt - pred)^2 and of the mask, independent loads),
-// term_s = w * l2_s / msum_s; loss = the terms summed in a fixed order (per
-// wave in scene order, then the waves in order)
-__global__ void __launch_bounds__(1024) l2_loss_fwd_kernel(const float* __restrict__ pred, int ldp,
-                                                           const float* __restrict__ gt,
-                                                           const float* __restrict__ mask, int ldm,
-                                                           const int32_t* __restrict__ scene_off, int S, int T,
-                                                           int B, float w, float* __restrict__ loss,
-                                                           float* __restrict__ msum_out,
-                                                           float* __restrict__ term) {
-  __shared__ float wsum[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+// loss = sum_s w * (sum_{i in s, t} m (gt - pred)^2) / (sum_{i in s, t} m)
+// (losses.py:52-71, mode 'raw' summed per scene): one wave per scene writes
+// its term and mask sum (kept for the backward), then l2_sum_kernel adds the
+// terms in scene order (lane-strided partials, a fixed shuffle tree)
+__global__ void __launch_bounds__(64) l2_terms_kernel(const float* __restrict__ pred, int ldp,
+                                                      const float* __restrict__ gt, const float* __restrict__ mask,
+                                                      int ldm, const int32_t* __restrict__ scene_off, int T, int B,
+                                                      float w, float* __restrict__ msum_out,
+                                                      float* __restrict__ term) {
+  __shared__ float msk[kL2MaxElems];
+  const int lane = threadIdx.x, s = blockIdx.x;
   const float2* g2 = reinterpret_cast<const float2*>(gt);
-  float run = 0.f;
-  for (int s = wave; s < S; s += nw) {
-    const int o = scene_off[s], n = scene_off[s + 1] - o;
-    // lane over the scene's (ped, step) elements, four independent load sets
-    // in flight per trip: one memory latency per 256 elements
-    float acc = 0.f, ms = 0.f;
-    const int tot = n * T;
-    for (int e0 = lane; e0 < tot; e0 += 256) {
-      float mk[4];
-      float2 g[4], q[4];
+  const int o = scene_off[s], n = scene_off[s + 1] - o;
+  const int tot = n * T;
+  const bool staged = tot <= kL2MaxElems;   // uniform
+  if (staged) stage_mask(msk, mask, ldm, o, n, T, lane, 64);   // (one wave: no barrier)
+  float acc = 0.f, ms = 0.f;
+  for (int e0 = lane; e0 < tot; e0 += 256) {
+    float mk[4];
+    float2 g[4], q[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = min(e0 + 64 * u, tot - 1);
-        const int i = e / T, t = e - i * T, p = o + i;
-        mk[u] = mask[(size_t)p * ldm + t];
-        g[u] = g2[(size_t)t * B + p];
-        q[u] = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + 64 * u, tot - 1);
+      const int t = e / n, i = e - t * n, p = o + i;
+      mk[u] = staged ? msk[i * T + t] : mask[(size_t)p * ldm + t];
+      g[u] = g2[(size_t)t * B + p];
+      q[u] = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e0 + 64 * u < tot) {
+        const float dx = g[u].x - q[u].x, dy = g[u].y - q[u].y;
+        acc = fmaf(mk[u], fmaf(dx, dx, dy * dy), acc);
+        ms += mk[u];
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (e0 + 64 * u < tot) {
-          const float dx = g[u].x - q[u].x, dy = g[u].y - q[u].y;
-          acc = fmaf(mk[u], fmaf(dx, dx, dy * dy), acc);
-          ms += mk[u];
-        }
-    }
-    acc = wave_sum(acc);
-    ms = wave_sum(ms);
-    if (lane == 0) {
-      msum_out[s] = ms;
-      const float tv = (w * acc) / ms;
-      term[s] = tv;
-      run += tv;
-    }
   }
-  if (lane == 0) wsum[wave] = run;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float tot = 0.f;
-    for (int i = 0; i < nw; ++i) tot += wsum[i];
-    *loss = tot;
+  acc = wave_sum(acc);
+  ms = wave_sum(ms);
+  if (lane == 0) {
+    msum_out[s] = ms;
+    term[s] = (w * acc) / ms;
   }
+}
+
+__global__ void __launch_bounds__(64) l2_sum_kernel(const float* __restrict__ term, int S, float* __restrict__ loss) {
+  float a = 0.f;
+  for (int s = threadIdx.x; s < S; s += 64) a += term[s];
+  a = wave_sum(a);
+  if (threadIdx.x == 0) *loss = a;
 }
 
 __global__ void __launch_bounds__(256) l2_loss_bwd_kernel(const float* __restrict__ pred, int ldp,
@@ -252,8 +274,10 @@ extern "C" int sgg_l2_loss_fwd(const float* pred, int ldp, const float* gt, cons
                                float* term_ws, void* stream) {
   SGG_CHECK_ARG(pred && gt && mask && scene_off && loss && msum && term_ws, "sgg_l2_loss_fwd: null pointer");
   SGG_CHECK_ARG(S >= 0 && T >= 1 && B >= 0 && ldm >= T && ldp >= 2 * B, "sgg_l2_loss_fwd: bad sizes");
-  hipLaunchKernelGGL(l2_loss_fwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, pred, ldp, gt, mask, ldm,
-                     scene_off, S, T, B, w, loss, msum, term_ws);
+  if (S > 0)
+    hipLaunchKernelGGL(l2_terms_kernel, dim3(S), dim3(64), 0, (hipStream_t)stream, pred, ldp, gt, mask, ldm, scene_off,
+                       T, B, w, msum, term_ws);
+  hipLaunchKernelGGL(l2_sum_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, term_ws, S, loss);
   SGG_RETURN_LAUNCH("sgg_l2_loss_fwd");
 }
 
