@@ -50,6 +50,73 @@ __device__ __forceinline__ float block_sum(float x, float* red) {
   return s;
 }
 
+// A workgroup's chunk [e0, e0 + kAdamChunk) of the concatenation spans a few
+// tensors; each thread takes kAdamPer elements (stride kAdamThreads).  The
+// tensor table is read ONCE per wave, lane t holding tensor t's offsets and
+// pointers (vector loads of the kernel arguments, all in flight together --
+// a walk of scalar loads, one dependent load per tensor, was the cost of the
+// previous form); an element finds its tensor among the chunk's few with
+// s_readlane'd bounds and takes its pointers by a lane shuffle.  All loads of
+// a thread's elements are then issued together: one memory latency per chunk.
+constexpr int kAdamPer = kAdamChunk / kAdamThreads;
+
+struct Tab {   // lane t: tensor t (t < n)
+  long long lo, hi;
+  unsigned long long p, g, m, v;
+};
+
+__device__ __forceinline__ Tab lane_tab(const AdamList& L) {
+  const int t = threadIdx.x & 63;
+  Tab r = {0, 0, 0, 0, 0, 0};
+  if (t < L.n) {
+    r.lo = L.off[t];
+    r.hi = L.off[t + 1];
+    r.p = reinterpret_cast<unsigned long long>(L.p[t]);
+    r.g = reinterpret_cast<unsigned long long>(L.g[t]);
+    r.m = reinterpret_cast<unsigned long long>(L.m[t]);
+    r.v = reinterpret_cast<unsigned long long>(L.v[t]);
+  }
+  return r;
+}
+
+__device__ __forceinline__ long long rl64(long long x, int k) {
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned)(unsigned long long)x, k);
+  const int hi = __builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)x >> 32), k);
+  return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ unsigned long long shfl64(unsigned long long x, int k) {
+  const unsigned lo = (unsigned)__shfl((int)(unsigned)x, k), hi = (unsigned)__shfl((int)(unsigned)(x >> 32), k);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// tensor (-1 past the end) and in-tensor index of the thread's elements
+__device__ __forceinline__ void chunk_elems(const AdamList& L, const Tab& T, long long e0, int (&ek)[kAdamPer],
+                                            long long (&ei)[kAdamPer]) {
+  const long long total = L.off[L.n];
+  const long long e1 = (e0 + kAdamChunk < total ? e0 + kAdamChunk : total) - 1;   // last element
+  const int t = threadIdx.x & 63;
+  // the chunk's tensors k0 .. k1: the lanes holding e0 / e1
+  const unsigned long long b0 = __ballot(t < L.n && T.lo <= e0 && e0 < T.hi);
+  const unsigned long long b1 = __ballot(t < L.n && T.lo <= e1 && e1 < T.hi);
+  const int k0 = b0 ? __ffsll((long long)b0) - 1 : 0, k1 = b1 ? __ffsll((long long)b1) - 1 : k0;
+#pragma unroll
+  for (int u = 0; u < kAdamPer; ++u) {
+    ek[u] = -1;
+    ei[u] = 0;
+  }
+  for (int k = k0; k <= k1; ++k) {   // (uniform; empty tensors have lo == hi)
+    const long long lo = rl64(T.lo, k), hi = rl64(T.hi, k);
+#pragma unroll
+    for (int u = 0; u < kAdamPer; ++u) {
+      const long long e = e0 + threadIdx.x + (long long)u * kAdamThreads;
+      if (e >= lo && e < hi) {
+        ek[u] = k;
+        ei[u] = e - lo;
+      }
+    }
+  }
+}
+
 // step scalars per tensor, as torch's Adam forms them (Python doubles, cast
 // once to fp32): scal[2k] = lr / (1 - b1^t), scal[2k + 1] = sqrt(1 - b2^t)
 __global__ void __launch_bounds__(kAdamThreads) adam_prep_kernel(AdamList L, int clip, float* __restrict__ partial,
@@ -63,17 +130,20 @@ __global__ void __launch_bounds__(kAdamThreads) adam_prep_kernel(AdamList L, int
     scal[2 * threadIdx.x + 1] = (float)sqrt(1.0 - pow(beta2, (double)t));
   }
   if (!clip) return;
-  const long long e0 = (long long)blockIdx.x * kAdamChunk, e1 = e0 + kAdamChunk;
-  float acc = 0.f;
-  for (int t = 0; t < L.n; ++t) {
-    const long long lo = e0 > L.off[t] ? e0 : L.off[t];
-    const long long hi = e1 < L.off[t + 1] ? e1 : L.off[t + 1];
-    const float* g = L.g[t];
-    for (long long e = lo + threadIdx.x; e < hi; e += kAdamThreads) {
-      const float x = g[e - L.off[t]];
-      acc = fmaf(x, x, acc);
-    }
+  const long long e0 = (long long)blockIdx.x * kAdamChunk;
+  const Tab T = lane_tab(L);
+  int ek[kAdamPer];
+  long long ei[kAdamPer];
+  chunk_elems(L, T, e0, ek, ei);
+  float x[kAdamPer];
+#pragma unroll
+  for (int u = 0; u < kAdamPer; ++u) {
+    const float* g = reinterpret_cast<const float*>(shfl64(T.g, ek[u] < 0 ? 0 : ek[u]));
+    x[u] = ek[u] >= 0 ? g[ei[u]] : 0.f;
   }
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < kAdamPer; ++u) acc = fmaf(x[u], x[u], acc);
   const float s = block_sum(acc, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = s;
 }
@@ -83,6 +153,11 @@ __global__ void __launch_bounds__(kAdamThreads) adam_update_kernel(AdamList L, i
                                                                    const float* __restrict__ scal, float beta2,
                                                                    float w1, float w2, float eps) {
   __shared__ float red[kAdamThreads / 64];
+  const long long e0 = (long long)blockIdx.x * kAdamChunk;
+  const Tab T = lane_tab(L);
+  int ek[kAdamPer];
+  long long ei[kAdamPer];
+  chunk_elems(L, T, e0, ek, ei);
   float coef = 1.f;
   if (max_norm > 0.f) {
     float acc = 0.f;
@@ -90,26 +165,43 @@ __global__ void __launch_bounds__(kAdamThreads) adam_update_kernel(AdamList L, i
     const float norm = sqrtf(block_sum(acc, red));
     coef = fminf(max_norm / (norm + 1e-6f), 1.f);
   }
-  const long long e0 = (long long)blockIdx.x * kAdamChunk, e1 = e0 + kAdamChunk;
-  for (int k = 0; k < L.n; ++k) {
-    const long long lo = e0 > L.off[k] ? e0 : L.off[k];
-    const long long hi = e1 < L.off[k + 1] ? e1 : L.off[k + 1];
-    if (lo >= hi) continue;
-    float *p = L.p[k], *g = L.g[k], *m = L.m[k], *v = L.v[k];
-    const float step_size = scal[2 * k], bc2s = scal[2 * k + 1];
-    for (long long e = lo + threadIdx.x; e < hi; e += kAdamThreads) {
-      const long long i = e - L.off[k];
-      float gr = g[i];
-      if (max_norm > 0.f) {
-        gr *= coef;
-        g[i] = gr;
-      }
-      const float mi = m[i] + w1 * (gr - m[i]);                 // exp_avg.lerp_(g, 1 - b1)
-      const float vi = v[i] * beta2 + w2 * gr * gr;     // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
-      m[i] = mi;
-      v[i] = vi;
-      p[i] += -step_size * (mi / (sqrtf(vi) / bc2s + eps));   // addcdiv_(m, denom, -step_size)
+  float* pp[kAdamPer];
+  float* gp[kAdamPer];
+  float* mp[kAdamPer];
+  float* vp[kAdamPer];
+  float gr[kAdamPer], m0[kAdamPer], v0[kAdamPer], p0[kAdamPer], ss[kAdamPer], bc[kAdamPer];
+#pragma unroll
+  for (int u = 0; u < kAdamPer; ++u) {
+    const int k = ek[u] >= 0 ? ek[u] : 0;
+    const long long i = ek[u] >= 0 ? ei[u] : 0;
+    pp[u] = reinterpret_cast<float*>(shfl64(T.p, k)) + i;
+    gp[u] = reinterpret_cast<float*>(shfl64(T.g, k)) + i;
+    mp[u] = reinterpret_cast<float*>(shfl64(T.m, k)) + i;
+    vp[u] = reinterpret_cast<float*>(shfl64(T.v, k)) + i;
+    ss[u] = scal[2 * k];
+    bc[u] = scal[2 * k + 1];
+  }
+  // every load of the thread's elements first, then the updates
+#pragma unroll
+  for (int u = 0; u < kAdamPer; ++u) {
+    gr[u] = *gp[u];
+    m0[u] = *mp[u];
+    v0[u] = *vp[u];
+    p0[u] = *pp[u];
+  }
+#pragma unroll
+  for (int u = 0; u < kAdamPer; ++u) {
+    if (ek[u] < 0) continue;
+    float g = gr[u];
+    if (max_norm > 0.f) {
+      g *= coef;
+      *gp[u] = g;
     }
+    const float mi = m0[u] + w1 * (g - m0[u]);        // exp_avg.lerp_(g, 1 - b1)
+    const float vi = v0[u] * beta2 + w2 * g * g;      // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    *mp[u] = mi;
+    *vp[u] = vi;
+    *pp[u] = p0[u] + -ss[u] * (mi / (sqrtf(vi) / bc[u] + eps));   // addcdiv_(m, denom, -step_size)
   }
 }
 

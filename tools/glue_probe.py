@@ -47,6 +47,18 @@ def main():
     with torch.no_grad():
         print("l2_select   %6.2f us" % graph_time(lambda: K.l2_select(pred, gt, mask, sc, k)))
         print("l2_loss fwd %6.2f us" % graph_time(lambda: K.l2_loss(p, gt, mask, sc, 1.0)))
+    sys.path.insert(0, ROOT)
+    import bench
+    g, d = bench.build_models(0)
+    for name, mod, clip in (("G", g, 2.0), ("D", d, 0.0)):
+        mod = mod.to(dev)
+        ps = [q for q in mod.parameters() if q.requires_grad]
+        for q in ps:
+            q.grad = torch.randn_like(q) * 1e-2
+        opt = K.ClipAdam(ps, lr=1e-4)
+        opt.step(clip)   # state
+        print("adam %s (%d tensors, %d floats, clip %.1f) %6.2f us" % (
+            name, len(ps), sum(q.numel() for q in ps), clip, graph_time(lambda: opt.step(clip), reps=20)))
     x = torch.empty(1, device=dev)
     print("empty fill  %6.2f us" % graph_time(lambda: x.fill_(1.0)))
 
