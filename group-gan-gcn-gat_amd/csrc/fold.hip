@@ -60,42 +60,52 @@ __global__ void __launch_bounds__(512) fold_fwd_multi_kernel(FoldList L) {
   }
 }
 
+// (dA, dbias) staged in LDS once; thread t owns column e = t % E of row group
+// g = t / E (ng = 512 / E groups): its dW entries need no global load (We, be
+// of its column in registers), and its three column sums walk the group's
+// rows with the W loads all independent (many in flight); the groups are
+// summed in LDS in a fixed order.
 __global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__ W, int ldw, int R, int E,
                                                        const float* __restrict__ We, const float* __restrict__ be,
                                                        const float* __restrict__ dA, const float* __restrict__ dbias,
                                                        float* __restrict__ dW, int lddw, float* __restrict__ dWe,
                                                        float* __restrict__ dbe, float* __restrict__ dbias_copy) {
-  // the second bias leaf (b_hh next to b_ih) gets its own copy of dbias
-  if (dbias_copy)
-    for (int r = threadIdx.x; r < R; r += blockDim.x) dbias_copy[r] = dbias[r];
-  // dW: one (r, e) element per thread-iteration
-#pragma unroll 4
-  for (int q = threadIdx.x; q < R * E; q += blockDim.x) {
-    const int r = q / E, e = q - r * E;
-    dW[(size_t)r * lddw + e] = fmaf(dA[2 * r], We[2 * e], fmaf(dA[2 * r + 1], We[2 * e + 1], dbias[r] * be[e]));
-  }
-  // dWe, dbe: 3E column sums over R rows.  Thread t takes output o = t % 3E
-  // and every rg-th row from t / 3E (rg = blockDim / 3E row groups), then
-  // the row groups are summed in LDS in a fixed order.
-  __shared__ float part[512];
-  const int no = 3 * E;
-  const int rg = blockDim.x / no;
-  if (threadIdx.x < no * rg) {
-    const int o = threadIdx.x % no, g = threadIdx.x / no;
-    const int e = o / 3, j = o - 3 * e;
-    float s = 0.f;
-#pragma unroll 8
-    for (int r = g; r < R; r += rg) {
-      const float gv = j < 2 ? dA[2 * r + j] : dbias[r];
-      s = fmaf(W[(size_t)r * ldw + e], gv, s);
-    }
-    part[threadIdx.x] = s;
+  __shared__ float g3[3 * 512];        // (dA_x, dA_y, dbias) per row, R <= 512
+  __shared__ float part[3 * 512];      // per (group, column) sums
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    const float2 a = reinterpret_cast<const float2*>(dA)[r];
+    const float b = dbias[r];
+    g3[3 * r] = a.x;
+    g3[3 * r + 1] = a.y;
+    g3[3 * r + 2] = b;
+    // the second bias leaf (b_hh next to b_ih) gets its own copy of dbias
+    if (dbias_copy) dbias_copy[r] = b;
   }
   __syncthreads();
-  if (threadIdx.x < no) {
-    const int e = threadIdx.x / 3, j = threadIdx.x - 3 * e;
+  const int ng = blockDim.x / E;
+  const int t = threadIdx.x;
+  if (t < ng * E) {
+    const int e = t % E, g = t / E;
+    const float we0 = We[2 * e], we1 = We[2 * e + 1], bee = be[e];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+    for (int r = g; r < R; r += ng) {
+      const float a0 = g3[3 * r], a1 = g3[3 * r + 1], b = g3[3 * r + 2];
+      dW[(size_t)r * lddw + e] = fmaf(a0, we0, fmaf(a1, we1, b * bee));
+      const float w = W[(size_t)r * ldw + e];
+      s0 = fmaf(w, a0, s0);
+      s1 = fmaf(w, a1, s1);
+      s2 = fmaf(w, b, s2);
+    }
+    part[3 * t] = s0;
+    part[3 * t + 1] = s1;
+    part[3 * t + 2] = s2;
+  }
+  __syncthreads();
+  if (t < 3 * E) {   // output (e, j): dWe[e][j] (j < 2) or dbe[e] (j = 2)
+    const int e = t / 3, j = t - 3 * e;
     float s = 0.f;
-    for (int g = 0; g < rg; ++g) s += part[g * no + threadIdx.x];
+    for (int g = 0; g < ng; ++g) s += part[3 * (g * E + e) + j];
     if (j < 2) dWe[2 * e + j] = s;
     else dbe[e] = s;
   }
@@ -131,7 +141,7 @@ extern "C" int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* 
                             const float* dbias, float* dW, int lddw, float* dWe, float* dbe, float* dbias_copy,
                             void* stream) {
   SGG_CHECK_ARG(W && We && be && dA && dbias && dW && dWe && dbe, "sgg_fold_bwd: null pointer");
-  SGG_CHECK_ARG(R >= 1 && E >= 1 && E <= 128 && ldw >= E && lddw >= E, "sgg_fold_bwd: bad sizes");
+  SGG_CHECK_ARG(R >= 1 && R <= 512 && E >= 1 && E <= 128 && ldw >= E && lddw >= E, "sgg_fold_bwd: bad sizes");
   hipLaunchKernelGGL(fold_bwd_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, W, ldw, R, E, We, be, dA, dbias,
                      dW, lddw, dWe, dbe, dbias_copy);
   SGG_RETURN_LAUNCH("sgg_fold_bwd");

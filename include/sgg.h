@@ -240,7 +240,8 @@ typedef struct {
 } SggFold;
 int sgg_fold_fwd_multi(const SggFold* folds, int n, void* stream);
 /* dbias_copy (may be NULL) receives a copy of dbias: the LSTM's second bias
- * leaf b_hh gets its own gradient tensor without an extra launch. */
+ * leaf b_hh gets its own gradient tensor without an extra launch.
+ * R <= 512, E <= 128. */
 int sgg_fold_bwd(const float* W, int ldw, int R, int E, const float* We, const float* be, const float* dA,
                  const float* dbias, float* dW, int lddw, float* dWe, float* dbe, float* dbias_copy, void* stream);
 

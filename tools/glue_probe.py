@@ -47,6 +47,10 @@ def main():
     with torch.no_grad():
         print("l2_select   %6.2f us" % graph_time(lambda: K.l2_select(pred, gt, mask, sc, k)))
         print("l2_loss fwd %6.2f us" % graph_time(lambda: K.l2_loss(p, gt, mask, sc, 1.0)))
+    for R, E in ((512, 64), (192, 16)):
+        W, We, be = torch.randn(R, E, device=dev), torch.randn(E, 2, device=dev), torch.randn(E, device=dev)
+        dA, db = torch.randn(R, 2, device=dev), torch.randn(R, device=dev)
+        print("fold_bwd R=%d E=%d %6.2f us" % (R, E, graph_time(lambda: K.fold_bwd(W, We, be, dA, db))))
     sys.path.insert(0, ROOT)
     import bench
     g, d = bench.build_models(0)
