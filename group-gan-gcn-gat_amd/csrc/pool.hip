@@ -581,7 +581,12 @@ __global__ void __launch_bounds__(256) pool_fwd_res_kernel(
 // once; the per-entry operands (g, p_i) are wave-uniform LDS broadcasts and
 // the bit walk is scalar.  Each workgroup writes its [dW2 | dA | db2] partial
 // to its own slab row; WGRAD = false (frozen weights) computes dU only.
-template <int BN, bool WGRAD>
+// STAGE: the unit's U rows (<= kBwdStageRows) are copied to LDS in the
+// prologue, issued together with the out / dout / argmax / position loads (one
+// memory round trip before the walk instead of three)
+constexpr int kBwdStageRows = 16;
+
+template <int BN, bool WGRAD, bool STAGE>
 __global__ void __launch_bounds__(512) pool_bwd_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ out,
@@ -589,7 +594,9 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
     int S, int jq, float* __restrict__ dU, float* __restrict__ part) {
   __shared__ unsigned long long msk[SGG_POOL_MAX_PEDS * BN];   // (j, c) -> set of i
   __shared__ float gs[SGG_POOL_MAX_PEDS * BN];                 // masked dout (i, c)
+  __shared__ int jsel[SGG_POOL_MAX_PEDS * BN];                 // argmax j of (i, c) (scene-local)
   __shared__ float2 ps[SGG_POOL_MAX_PEDS];
+  extern __shared__ float Us[];                                // STAGE: rows j0 .. j1 of U
   const int k = threadIdx.x;   // hidden unit, blockDim.x == 512
   float w2[BN], dw2[BN];
 #pragma unroll
@@ -605,9 +612,18 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
     const int n = scene_off[s + 1] - o;
     const int ne = n * BN;
     const int j0 = (n * jp) / jq, j1 = (n * (jp + 1)) / jq;
+    if (STAGE) {   // this thread's column of the unit's U rows (coalesced rows)
+      const float* Ur = U + (size_t)(o + j0) * kHidden + k;
+#pragma unroll 4
+      for (int r = 0; r < j1 - j0; ++r) Us[r * kHidden + k] = Ur[(size_t)r * kHidden];
+    }
+#pragma unroll 2
     for (int e = k; e < ne; e += kHidden) {
       const size_t ge = (size_t)o * BN + e;
-      gs[e] = out[ge] > 0.f ? dout[ge] : 0.f;
+      const float ov = out[ge], dv = dout[ge];
+      const int av = argmax[ge];
+      gs[e] = ov > 0.f ? dv : 0.f;
+      jsel[e] = av - o;
       msk[e] = 0ull;
     }
     for (int q = k; q < n; q += kHidden) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
@@ -615,18 +631,22 @@ __global__ void __launch_bounds__(512) pool_bwd_kernel(
     for (int e = k; e < ne; e += kHidden) {
       if (gs[e] != 0.f) {
         const int i = e / BN, c = e - i * BN;
-        const int j = argmax[(size_t)o * BN + e] - o;
-        atomicOr(&msk[j * BN + c], 1ull << i);
+        atomicOr(&msk[jsel[e] * BN + c], 1ull << i);
       }
     }
     if (WGRAD && jp == 0 && k < BN)
       for (int i = 0; i < n; ++i) db2 += gs[i * BN + k];
     __syncthreads();
     const float* Uc = U + (size_t)o * kHidden + k;
-    float u_next = j0 < j1 ? Uc[(size_t)j0 * kHidden] : 0.f;
+    float u_next = STAGE ? 0.f : (j0 < j1 ? Uc[(size_t)j0 * kHidden] : 0.f);
     for (int j = j0; j < j1; ++j) {
-      const float u = u_next;
-      if (j + 1 < j1) u_next = Uc[(size_t)(j + 1) * kHidden];
+      float u;
+      if (STAGE) {
+        u = Us[(j - j0) * kHidden + k];
+      } else {
+        u = u_next;
+        if (j + 1 < j1) u_next = Uc[(size_t)(j + 1) * kHidden];
+      }
       const float2 pj = ps[j];
       float du = 0.f;
       // the row's masks in blocks of 16 up front: one LDS latency per block,
@@ -786,14 +806,19 @@ template <int BN>
 static int launch_bwd(const float* U, const float* pos, const float* A, const float* W2, const float* out,
                       const int32_t* am, const float* dout, const int32_t* off, int S, int max_n, float* dU,
                       float* part, hipStream_t st) {
-  (void)max_n;
   const int grid = sgg_pool_bwd_grid(S), jq = pool_bwd_jq(S);
-  if (part)
-    hipLaunchKernelGGL((pool_bwd_kernel<BN, true>), dim3(grid), dim3(512), 0, st, U, pos, A, W2, out, am, dout, off, S,
-                       jq, dU, part);
-  else
-    hipLaunchKernelGGL((pool_bwd_kernel<BN, false>), dim3(grid), dim3(512), 0, st, U, pos, A, W2, out, am, dout, off,
-                       S, jq, dU, part);
+  const int rows = (max_n + jq - 1) / jq + 1;   // a unit's j range (floor boundaries: <= ceil + 1)
+  const bool stage = rows <= kBwdStageRows;
+  const size_t lds = stage ? sizeof(float) * (size_t)rows * kHidden : 0;
+#define SGG_POOL_BWD(W, SG)                                                                                          \
+  hipLaunchKernelGGL((pool_bwd_kernel<BN, W, SG>), dim3(grid), dim3(512), lds, st, U, pos, A, W2, out, am, dout, off, \
+                     S, jq, dU, part)
+  if (part) {
+    if (stage) SGG_POOL_BWD(true, true); else SGG_POOL_BWD(true, false);
+  } else {
+    if (stage) SGG_POOL_BWD(false, true); else SGG_POOL_BWD(false, false);
+  }
+#undef SGG_POOL_BWD
   SGG_RETURN_LAUNCH("sgg_pool_bwd");
 }
 

@@ -554,7 +554,10 @@ class _Pool(torch.autograd.Function):
         launch()
         if timer.active:
             nb = 8.0 * B * 512 + 12.0 * B * bn + 4.0 * 512 * (2 + bn) + (4.0 * part.numel() if wgrad else 0.0)
-            timer.add("sgg::pool_bwd_kernel<%d, %s>" % (bn, "true" if wgrad else "false"), (sc.S, B),
+            jq = max(1, min(8, 256 // sc.S)) if sc.S >= 1 else 1   # pool.hip pool_bwd_jq / launch_bwd
+            stage = (sc.max_n + jq - 1) // jq + 1 <= 16
+            timer.add("sgg::pool_bwd_kernel<%d, %s, %s>" % (bn, "true" if wgrad else "false",
+                                                            "true" if stage else "false"), (sc.S, B),
                       8.0 * B * bn * 512, nb, launch)
         dh = None
         if need[0]:
