@@ -1,0 +1,145 @@
+// Weight-gradient finish of one backward op in ONE launch (sgg_grad_finish,
+// include/sgg.h): the slab row sums (SggRed) and the input-embedding fold
+// backwards (SggFoldBwd) of the pooling backward (reference sgan/models.py:
+// 497-549) and of the LSTM backward (:62-92, :142-178).
+//
+// Before, the row sums took a sgg_slab_reduce and sgg_xtw's reduce pass per
+// op, launches of a few microseconds of work each behind the fixed per-
+// dispatch cost.  A fold job needs (dA, dbias), which are row sums of the
+// same slabs: two more row-sum jobs write them to a scratch buffer and the
+// fold backward (fold.hip) follows as the op's one other launch.  (Running
+// the folds in the same launch needs a grid-wide handoff: a device-scope
+// release fence per workgroup writes back the XCD's L2 and measured 5x
+// slower than the second launch; a single workgroup re-summing the slabs
+// reads up to 1.5 MB through one CU.)  Every sum keeps the order of the
+// reductions it replaces, so the outputs are bit-identical to the separate
+// launches.
+//
+// Row-sum order (shared with slab_reduce_kernel / xtw_reduce_kernel): column
+// c's 16 phases p each add rows p, p + 16, p + 32, ... in row order starting
+// from 0, then the 16 phase sums are added in phase order.
+#include <string.h>
+
+#include "sgg_common.h"
+
+namespace sgg {
+
+namespace {
+
+constexpr int kRedJobs = SGG_RED_MAX + 2 * SGG_FOLDB_MAX;   // + each fold's (dA, dbias) row sums
+
+struct FinishArgs {
+  SggRed red[kRedJobs];
+  int nred;
+  int blk0[kRedJobs + 1];   // first workgroup of red job j; blk0[nred] = the grid
+};
+
+__device__ __forceinline__ float phase_sum(const float* __restrict__ src, int rows, int ld, int col, int ph) {
+  float s = 0.f;
+  int r = ph;
+  for (; r + 48 < rows; r += 64) {
+    const float v0 = src[(size_t)r * ld + col], v1 = src[(size_t)(r + 16) * ld + col];
+    const float v2 = src[(size_t)(r + 32) * ld + col], v3 = src[(size_t)(r + 48) * ld + col];
+    s += v0;
+    s += v1;
+    s += v2;
+    s += v3;
+  }
+  for (; r < rows; r += 16) s += src[(size_t)r * ld + col];
+  return s;
+}
+
+__device__ void red_job(const SggRed& d, int blk, float (*rpart)[64]) {
+  const int el = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blk * 64 + el;
+  const float s = c < d.cols ? phase_sum(d.src + d.col0, d.rows, d.ld, c, ph) : 0.f;
+  rpart[ph][el] = s;
+  __syncthreads();
+  if (ph == 0 && c < d.cols) {
+    float v = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) v += rpart[p][el];
+    if (d.map == 0) {
+      d.out[c] = v;
+    } else {
+      const int m = c / d.N, n = c - m * d.N;
+      d.out[d.trans ? (size_t)n * d.ldo + m : (size_t)m * d.ldo + n] = v;
+    }
+  }
+}
+
+// workgroups = the red jobs' 64-column blocks (1024 threads: 64 columns x 16
+// row phases)
+__global__ void __launch_bounds__(1024) grad_finish_kernel(FinishArgs a) {
+  __shared__ float rpart[16][64];
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < a.nred && b >= a.blk0[j + 1]) ++j;
+  red_job(a.red[j], b - a.blk0[j], rpart);
+}
+
+}  // namespace
+
+}  // namespace sgg
+
+using namespace sgg;
+
+extern "C" int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* folds, int nfold, float* scratch,
+                               size_t scratch_bytes, void* stream) {
+  SGG_CHECK_ARG(nred >= 0 && nred <= SGG_RED_MAX && nfold >= 0 && nfold <= SGG_FOLDB_MAX,
+                "sgg_grad_finish: 0 <= nred <= %d, 0 <= nfold <= %d (got %d, %d)", SGG_RED_MAX, SGG_FOLDB_MAX, nred,
+                nfold);
+  SGG_CHECK_ARG((nred == 0 || reds) && (nfold == 0 || (folds && scratch)), "sgg_grad_finish: null job list or scratch");
+  FinishArgs a;
+  memset(&a, 0, sizeof(a));
+  int nj = 0;
+  auto add_red = [&](const SggRed& d) {
+    a.red[nj] = d;
+    ++nj;
+  };
+  for (int j = 0; j < nred; ++j) {
+    const SggRed& d = reds[j];
+    SGG_CHECK_ARG(d.src && d.out && d.rows >= 0 && d.cols >= 1 && d.col0 >= 0 && d.ld >= d.col0 + d.cols,
+                  "sgg_grad_finish: bad reduction job %d (rows %d ld %d col0 %d cols %d)", j, d.rows, d.ld, d.col0,
+                  d.cols);
+    SGG_CHECK_ARG(d.map == 0 || (d.map == 1 && d.N >= 1 && d.cols % d.N == 0 &&
+                                 d.ldo >= (d.trans ? d.cols / d.N : d.N)),
+                  "sgg_grad_finish: bad output map of reduction job %d", j);
+    add_red(d);
+  }
+  size_t need = 0;
+  for (int k = 0; k < nfold; ++k) need += sizeof(float) * 3 * (size_t)folds[k].R;
+  SGG_CHECK_ARG(scratch_bytes >= need, "sgg_grad_finish: scratch %zu < %zu bytes", scratch_bytes, need);
+  float* g = scratch;
+  for (int k = 0; k < nfold; ++k) {
+    const SggFoldBwd& d = folds[k];
+    SGG_CHECK_ARG(d.W && d.We && d.be && d.dA_src && d.db_src && d.dW && d.dWe && d.dbe,
+                  "sgg_grad_finish: null pointer in fold job %d", k);
+    SGG_CHECK_ARG(d.R >= 1 && d.R <= 512 && d.E >= 1 && d.E <= 128 && d.ldw >= d.E && d.lddw >= d.E,
+                  "sgg_grad_finish: bad fold sizes in job %d (R %d E %d)", k, d.R, d.E);
+    SGG_CHECK_ARG(d.dA_rows >= 0 && d.db_rows >= 0 && d.dA_col0 >= 0 && d.db_col0 >= 0 &&
+                      d.dA_ld >= d.dA_col0 + 2 * d.R && d.db_ld >= d.db_col0 + d.R,
+                  "sgg_grad_finish: bad (dA, dbias) sources in fold job %d", k);
+    add_red(SggRed{d.dA_src, d.dA_rows, d.dA_ld, d.dA_col0, 2 * d.R, g, 0, 0, 0, 0});
+    add_red(SggRed{d.db_src, d.db_rows, d.db_ld, d.db_col0, d.R, g + 2 * d.R, 0, 0, 0, 0});
+    g += 3 * (size_t)d.R;
+  }
+  a.nred = nj;
+  int blk = 0;
+  for (int j = 0; j < nj; ++j) {
+    a.blk0[j] = blk;
+    blk += (a.red[j].cols + 63) / 64;
+  }
+  a.blk0[nj] = blk;
+  hipStream_t st = (hipStream_t)stream;
+  if (blk > 0) hipLaunchKernelGGL(grad_finish_kernel, dim3(blk), dim3(1024), 0, st, a);
+  g = scratch;
+  for (int k = 0; k < nfold; ++k) {   // the fold backwards on the summed (dA, dbias)
+    const SggFoldBwd& d = folds[k];
+    const int rc = sgg_fold_bwd(d.W, d.ldw, d.R, d.E, d.We, d.be, g, g + 2 * d.R, d.dW, d.lddw, d.dWe, d.dbe,
+                                d.dbias_copy, stream);
+    if (rc != 0) return rc;
+    g += 3 * (size_t)d.R;
+  }
+  SGG_RETURN_LAUNCH("sgg_grad_finish");
+}

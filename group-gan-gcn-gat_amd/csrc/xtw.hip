@@ -199,6 +199,31 @@ extern "C" int sgg_xtw_splits(int R, int M, int N) {
   return splits < 1 ? 1 : (int)splits;
 }
 
+static void launch_partial(const float* X, int ldx, const float* Y, int ldy, const float* Ymask, int ldm, int R,
+                           int M, int N, int splits, float* ws, float* cs, hipStream_t st) {
+  const int rps = ((R + splits - 1) / splits + 63) & ~63;   // whole 64-row steps (16 rows per wave)
+  dim3 grid((M + 63) / 64, (N + 63) / 64, splits);
+  switch (M >= 64 ? 4 : (M + 15) / 16) {   // 16-wide m-tiles of a 64-row output block
+    case 1: hipLaunchKernelGGL(xtw_partial_kernel<1>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+    case 2: hipLaunchKernelGGL(xtw_partial_kernel<2>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+    case 3: hipLaunchKernelGGL(xtw_partial_kernel<3>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+    default: hipLaunchKernelGGL(xtw_partial_kernel<4>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
+  }
+}
+
+extern "C" int sgg_xtw_partial(const float* X, int ldx, const float* Y, int ldy, const float* Ymask, int ldm, int R,
+                               int M, int N, int colsum, float* ws, size_t ws_bytes, void* stream) {
+  SGG_CHECK_ARG(X && Y && ws, "sgg_xtw_partial: null pointer");
+  SGG_CHECK_ARG(R >= 1 && M > 0 && N > 0 && ldx >= M && ldy >= N, "sgg_xtw_partial: bad sizes");
+  const int splits = sgg_xtw_splits(R, M, N);
+  const size_t need = sizeof(float) * (size_t)splits * ((size_t)M * N + (colsum ? N : 0));
+  SGG_CHECK_ARG(ws_bytes >= need, "sgg_xtw_partial: workspace %zu < %zu bytes", ws_bytes, need);
+  SGG_CHECK_ARG(!Ymask || ldm >= N, "sgg_xtw_partial: mask leading dim %d < N", ldm);
+  launch_partial(X, ldx, Y, ldy, Ymask, ldm, R, M, N, splits, ws, colsum ? ws + (size_t)splits * M * N : nullptr,
+                 (hipStream_t)stream);
+  SGG_RETURN_LAUNCH("sgg_xtw_partial");
+}
+
 extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const float* Ymask, int ldm, int R, int M,
                        int N, float* C, int ldc, int trans_c, float* colsum, float* ws, size_t ws_bytes,
                        void* stream) {
@@ -210,16 +235,8 @@ extern "C" int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const f
   SGG_CHECK_ARG(ws_bytes >= need, "sgg_xtw: workspace %zu < %zu bytes", ws_bytes, need);
   SGG_CHECK_ARG(!Ymask || ldm >= N, "sgg_xtw: mask leading dim %d < N", ldm);
   hipStream_t st = (hipStream_t)stream;
-  const int rps = ((R + splits - 1) / splits + 63) & ~63;   // whole 64-row steps (16 rows per wave)
   float* colslab = ws + (size_t)splits * M * N;
-  dim3 grid((M + 63) / 64, (N + 63) / 64, splits);
-  float* cs = colsum ? colslab : nullptr;
-  switch (M >= 64 ? 4 : (M + 15) / 16) {   // 16-wide m-tiles of a 64-row output block
-    case 1: hipLaunchKernelGGL(xtw_partial_kernel<1>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
-    case 2: hipLaunchKernelGGL(xtw_partial_kernel<2>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
-    case 3: hipLaunchKernelGGL(xtw_partial_kernel<3>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
-    default: hipLaunchKernelGGL(xtw_partial_kernel<4>, grid, dim3(256), 0, st, X, ldx, Y, ldy, Ymask, ldm, R, M, N, rps, ws, cs); break;
-  }
+  launch_partial(X, ldx, Y, ldy, Ymask, ldm, R, M, N, splits, ws, colsum ? colslab : nullptr, st);
   const int MN = M * N;
   const int nb = (MN + 63) / 64 + (colsum ? (N + 63) / 64 : 0);
   hipLaunchKernelGGL(xtw_reduce_kernel, dim3(nb), dim3(1024), 0, st, ws, splits, MN, C, N, ldc, trans_c,

@@ -45,6 +45,24 @@ class Fold(ctypes.Structure):
     _fields_ = [("W", _p), ("ldw", _i), ("R", _i), ("E", _i), ("We", _p), ("be", _p), ("b1", _p), ("b2", _p),
                 ("A", _p), ("bias", _p)]
 
+RED_MAX = 8     # SGG_RED_MAX
+FOLDB_MAX = 2   # SGG_FOLDB_MAX
+
+
+class Red(ctypes.Structure):
+    """SggRed (include/sgg.h): one slab row-sum job of sgg_grad_finish."""
+    _fields_ = [("src", _p), ("rows", _i), ("ld", _i), ("col0", _i), ("cols", _i), ("out", _p), ("map", _i),
+                ("N", _i), ("ldo", _i), ("trans", _i)]
+
+
+class FoldBwd(ctypes.Structure):
+    """SggFoldBwd (include/sgg.h): one fold backward of sgg_grad_finish."""
+    _fields_ = [("W", _p), ("ldw", _i), ("R", _i), ("E", _i), ("We", _p), ("be", _p),
+                ("dA_src", _p), ("dA_rows", _i), ("dA_ld", _i), ("dA_col0", _i),
+                ("db_src", _p), ("db_rows", _i), ("db_ld", _i), ("db_col0", _i),
+                ("dW", _p), ("lddw", _i), ("dWe", _p), ("dbe", _p), ("dbias_copy", _p)]
+
+
 # name -> (restype, argtypes); must mirror include/sgg.h exactly
 SIGNATURES = {
     "sgg_version": (_i, []),
@@ -64,6 +82,8 @@ SIGNATURES = {
     "sgg_seg_reduce": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i, _p]),
     "sgg_seg_gather": (_i, [_p, _i, _i, _p, _p, _p, _i, _p, _i, _p]),
     "sgg_xtw_splits": (_i, [_i, _i, _i]),
+    "sgg_xtw_partial": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
+    "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
     "sgg_adam_parts": (_i, [ctypes.c_longlong]),
     "sgg_adam_step": (_i, [_p, _p, _p, _p, _p, _i, ctypes.c_double, ctypes.c_double, ctypes.c_double, _f, _f, _p, _p,
                           _sz, _p]),

@@ -282,6 +282,96 @@ def fold_bwd(W, We, be, dA, dbias, dW=None, dbias_copy=None):
     return dW, dWe, dbe
 
 
+# ---------------------------------------------------------------------------
+# weight-gradient finish: a backward op's slab row sums + fold backwards in
+# ONE launch (sgg_grad_finish)
+# ---------------------------------------------------------------------------
+def xtw_partial(X, Y, colsum=False):
+    """sgg_xtw's split pass alone; returns (ws, splits): C's partials are the
+    first splits x (M N) floats of ws, the column-sum partials the next
+    splits x N.  The sums join a GradFinish."""
+    lib = _lib()
+    X = _rows(X, "X")
+    Y = _rows(Y, "Y")
+    R, M = X.shape
+    Nn = Y.shape[1]
+    assert Y.shape[0] == R and R > 0
+    splits = lib.sgg_xtw_splits(R, M, Nn)
+    ws = torch.empty(splits * (M * Nn + (Nn if colsum else 0)), device=X.device, dtype=torch.float32)
+
+    def launch():
+        N.check(lib.sgg_xtw_partial(N.ptr(X), X.stride(0), N.ptr(Y), Y.stride(0), None, 0, R, M, Nn, int(colsum),
+                                    N.ptr(ws), ws.numel() * 4, N.stream_ptr()), "sgg_xtw_partial")
+    launch()
+    if timer.active:
+        mt = 4 if M >= 64 else (M + 15) // 16
+        timer.add("sgg::xtw_partial_kernel<%d>" % mt, (R, M, Nn), 2.0 * R * M * Nn,
+                  4.0 * (R * M + R * Nn) + 4.0 * ws.numel(), launch)
+    return ws, splits
+
+
+class GradFinish:
+    """Collects the row-sum jobs (SggRed) and fold backwards (SggFoldBwd) of
+    one backward op, then runs them through sgg_grad_finish: one launch for
+    every row sum, one per fold.  Results are bit-identical to
+    sgg_slab_reduce / sgg_xtw / sgg_fold_bwd in turn."""
+
+    def __init__(self):
+        self.reds, self.folds, self.keep = [], [], []
+
+    def rowsum(self, src, rows, ld, col0, cols, out):
+        """out[c] = sum over src's rows of src[:, col0 + c] (out contiguous)."""
+        assert out.is_contiguous() and out.numel() == cols
+        self.reds.append(N.Red(N.ptr(src), rows, ld, col0, cols, N.ptr(out), 0, 0, 0, 0))
+        self.keep += [src, out]
+
+    def xtw_sums(self, ws, splits, M, Nn, C, trans_c=False, colsum=None):
+        """C (M x Nn, or its transpose; row-strided view) and optionally the
+        column sums from xtw_partial's workspace."""
+        assert C.stride(1) == 1 and tuple(C.shape) == ((Nn, M) if trans_c else (M, Nn))
+        self.reds.append(N.Red(N.ptr(ws), splits, M * Nn, 0, M * Nn, N.ptr(C), 1, Nn, C.stride(0), int(trans_c)))
+        self.keep += [ws, C]
+        if colsum is not None:
+            self.rowsum(ws[splits * M * Nn:], splits, Nn, 0, Nn, colsum)
+
+    def fold(self, W, We, be, dA_src, dA_rows, dA_ld, dA_col0, db_src, db_rows, db_ld, db_col0, dW=None,
+             dbias_copy=None):
+        """fold_bwd with (dA, dbias) given as slab column row sums; returns
+        (dW, dWe, dbe)."""
+        W = _rows(W, "W")
+        R, E = W.shape
+        dW = dW if dW is not None else torch.empty(R, E, device=W.device, dtype=torch.float32)
+        dWe = torch.empty(E, 2, device=W.device, dtype=torch.float32)
+        dbe = torch.empty(E, device=W.device, dtype=torch.float32)
+        We, be = We.contiguous(), be.contiguous()
+        self.folds.append(N.FoldBwd(N.ptr(W), W.stride(0), R, E, N.ptr(We), N.ptr(be),
+                                    N.ptr(dA_src), dA_rows, dA_ld, dA_col0, N.ptr(db_src), db_rows, db_ld, db_col0,
+                                    N.ptr(dW), dW.stride(0), N.ptr(dWe), N.ptr(dbe), N.ptr(dbias_copy)))
+        self.keep += [W, We, be, dA_src, db_src, dW, dWe, dbe, dbias_copy]
+        return dW, dWe, dbe
+
+    def run(self):
+        if not self.reds and not self.folds:
+            return
+        lib = _lib()
+        assert len(self.reds) <= N.RED_MAX and len(self.folds) <= N.FOLDB_MAX
+        reds = (N.Red * max(1, len(self.reds)))(*self.reds)
+        folds = (N.FoldBwd * max(1, len(self.folds)))(*self.folds)
+        nr, nf = len(self.reds), len(self.folds)
+        dev = self.keep[0].device
+        scratch = torch.empty(max(1, sum(3 * f.R for f in self.folds)), device=dev, dtype=torch.float32)
+
+        def launch(reds=reds, folds=folds, nr=nr, nf=nf, keep=list(self.keep)):
+            N.check(lib.sgg_grad_finish(reds, nr, folds, nf, N.ptr(scratch), scratch.numel() * 4, N.stream_ptr()),
+                    "sgg_grad_finish")
+        launch()
+        if timer.active:
+            nb = sum(4.0 * r.rows * r.cols for r in self.reds) + sum(4.0 * 3 * f.R * max(f.dA_rows, f.db_rows)
+                                                                     for f in self.folds)
+            timer.add("sgg::grad_finish_kernel", (nr, nf, tuple((r.rows, r.cols) for r in self.reds)), nb / 4.0, nb,
+                      launch)
+
+
 class _XW(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, trans_w, act):
@@ -567,14 +657,24 @@ class _Pool(torch.autograd.Function):
         if not wgrad:
             return dh, None, None, None, None, None, None, None, None, None
         with side(part, h, dU, W1, We, be):
-            flat = torch.empty(P, device=h.device, dtype=torch.float32)     # [dW2 | dA | db2]
-            N.check(lib.sgg_slab_reduce(N.ptr(part), part.shape[0], P, N.ptr(flat), N.stream_ptr()),
-                    "sgg_slab_reduce")
+            # one launch after the dW1h partials: dW2, db2 (slab [dW2 | dA | db2]
+            # row sums), dW1h = dU^T h, dc = sum_j dU_j, and the fold backward
+            # of (dA, dc) -> dW1e, dWe, dbe
+            H = h.shape[1]
+            rows = part.shape[0]
+            ws, splits = xtw_partial(h, dU, colsum=True)
             dW1 = torch.empty_like(W1)
-            _, dc = xtw(h, dU, colsum=True, trans_c=True, out=dW1[:, E:])   # dW1h = dU^T h, dc = sum_j dU_j
-            _, dWe, dbe = fold_bwd(W1[:, :E], We, be, flat[bn * 512:bn * 512 + 1024].view(512, 2), dc,
-                                   dW=dW1[:, :E])
-        return dh, None, dW1, dWe, dbe, dc, flat[:bn * 512].view(bn, 512), flat[bn * 512 + 1024:], None, None
+            dW2 = torch.empty(bn, 512, device=h.device, dtype=torch.float32)
+            db2 = torch.empty(bn, device=h.device, dtype=torch.float32)
+            dc = torch.empty(512, device=h.device, dtype=torch.float32)
+            gf = GradFinish()
+            gf.rowsum(part, rows, P, 0, bn * 512, dW2)
+            gf.rowsum(part, rows, P, bn * 512 + 1024, bn, db2)
+            gf.xtw_sums(ws, splits, H, 512, dW1[:, E:], trans_c=True, colsum=dc)
+            _, dWe, dbe = gf.fold(W1[:, :E], We, be, part, rows, P, bn * 512, ws[splits * H * 512:], splits, 512, 0,
+                                  dW=dW1[:, :E])
+            gf.run()
+        return dh, None, dW1, dWe, dbe, dc, dW2, db2, None, None
 
 
 class GradLink:
@@ -1019,12 +1119,32 @@ class _LSTMSeq(torch.autograd.Function):
         side_ctx = side(wpart, dG, h_all, rel, rel_out, drel_tot, W_ih, We, be) if wgrad or decoder \
             else contextlib.nullcontext()
         with side_ctx:
-            if wgrad:
-                dW_ih, dW_hh, db_ih, db_hh, dWe, dbe = _lstm_wgrads(lib, wpart, rows, P, G4, H, T, B, dG, h_all,
-                                                                    rel, rel_out, decoder, W_ih, We, be, dev)
-            if decoder and (need[9] or need[10]):
-                dr = drel_tot.view(T * B, 2)
-                dWp, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True, trans_c=True)
+            need_p = decoder and (need[9] or need[10])
+            if wpart is not None:
+                # one launch: dW_hh, dbias (slab [dW_hh | dbias | dA] row sums),
+                # the fold backward of (dA, dbias) -> dW_ih, dWe, dbe (+ the b_hh
+                # copy), and the decoder's dWp, dbp from their split partials
+                gf = GradFinish()
+                if need_p:
+                    ws, splits = xtw_partial(h_all[1:].reshape(T * B, H), drel_tot.view(T * B, 2), colsum=True)
+                    dWp = torch.empty(2, H, device=dev, dtype=torch.float32)
+                    dbp = torch.empty(2, device=dev, dtype=torch.float32)
+                    gf.xtw_sums(ws, splits, H, 2, dWp, trans_c=True, colsum=dbp)
+                dW_hh = torch.empty(G4, H, device=dev, dtype=torch.float32)
+                db_ih = torch.empty(G4, device=dev, dtype=torch.float32)
+                db_hh = torch.empty(G4, device=dev, dtype=torch.float32)
+                gf.rowsum(wpart, rows, P, 0, G4 * H, dW_hh)
+                gf.rowsum(wpart, rows, P, G4 * H, G4, db_ih)
+                dW_ih, dWe, dbe = gf.fold(W_ih, We, be, wpart, rows, P, G4 * H + G4, wpart, rows, P, G4 * H,
+                                          dbias_copy=db_hh)
+                gf.run()
+            else:
+                if wgrad:
+                    dW_ih, dW_hh, db_ih, db_hh, dWe, dbe = _lstm_wgrads(lib, wpart, rows, P, G4, H, T, B, dG, h_all,
+                                                                        rel, rel_out, decoder, W_ih, We, be, dev)
+                if need_p:
+                    dr = drel_tot.view(T * B, 2)
+                    dWp, dbp = xtw(h_all[1:].reshape(T * B, H), dr, colsum=True, trans_c=True)
         if decoder:
             drel = drel_in[0]
         else:

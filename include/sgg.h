@@ -212,6 +212,70 @@ int sgg_seg_gather(const float* src, int lds, int F, const int32_t* seg_of_row,
 int sgg_xtw_splits(int R, int M, int N);
 int sgg_xtw(const float* X, int ldx, const float* Y, int ldy, const float* Ymask, int ldm, int R, int M, int N,
             float* C, int ldc, int trans_c, float* colsum, float* ws, size_t ws_bytes, void* stream);
+/* sgg_xtw's first pass alone: the split partials land in ws (C partials:
+ * splits rows of M*N floats; then, when colsum != 0, the column-sum partials:
+ * splits rows of N floats at ws + splits*M*N).  The row sums join the
+ * backward's one sgg_grad_finish launch (SggRed jobs, map 1 for C). */
+int sgg_xtw_partial(const float* X, int ldx, const float* Y, int ldy, const float* Ymask, int ldm, int R, int M,
+                    int N, int colsum, float* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Weight-gradient finish of one backward op (the pooling
+ * backward of models.py:497-549, the LSTM backward of :62-92 / :142-178):
+ * every slab row sum the op needs (SggRed: the kernels' per-workgroup slab
+ * rows, sgg_xtw_partial's split partials) and the input-embedding fold
+ * backwards (SggFoldBwd, the algebra of sgg_fold_bwd) whose (dA, dbias) are
+ * themselves row sums of such slabs (summed into `scratch` by the row-sum
+ * launch).  Every sum keeps
+ * the fixed order of sgg_slab_reduce, so every output is bit-identical to
+ * sgg_slab_reduce / sgg_xtw / sgg_fold_bwd run one after the other.
+ * SggRed: out_c = sum_{s < rows} src[s * ld + col0 + c], c < cols, summed as
+ * sgg_slab_reduce does (16 row phases, then the phases in order); map 0:
+ * out[c]; map 1 (sgg_xtw's C, c = m * N + n): out[m * ldo + n], or
+ * out[n * ldo + m] when trans != 0. */
+#define SGG_RED_MAX 8
+#define SGG_FOLDB_MAX 2
+typedef struct {
+  const float* src;
+  int rows;
+  int ld;
+  int col0;
+  int cols;
+  float* out;
+  int map;
+  int N;
+  int ldo;
+  int trans;
+} SggRed;
+/* dA[r][j] = row sum of dA_src at column dA_col0 + 2 r + j, dbias[r] = row sum
+ * of db_src at column db_col0 + r; then, as sgg_fold_bwd: dW (R x E, row
+ * stride lddw), dWe (E x 2), dbe (E), dbias_copy (may be NULL).  R <= 512,
+ * E <= 128. */
+typedef struct {
+  const float* W;
+  int ldw;
+  int R;
+  int E;
+  const float* We;
+  const float* be;
+  const float* dA_src;
+  int dA_rows;
+  int dA_ld;
+  int dA_col0;
+  const float* db_src;
+  int db_rows;
+  int db_ld;
+  int db_col0;
+  float* dW;
+  int lddw;
+  float* dWe;
+  float* dbe;
+  float* dbias_copy;
+} SggFoldBwd;
+/* scratch: 3 R floats per fold job (its (dA, dbias) row sums).  Launches:
+ * one for all row sums, then one sgg_fold_bwd per fold job. */
+int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* folds, int nfold, float* scratch,
+                    size_t scratch_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Input-embedding fold (a Linear(2, E) displacement embedding feeding a

@@ -470,6 +470,58 @@ def test_fold_matches_torch():
         close(dbe, (W.t() @ db).cpu().numpy(), rtol=2e-6, what="fold dbe")
 
 
+@pytest.mark.parametrize("rows,R,E,ld,M,Nn,R_x", [(160, 192, 16, 16, 48, 2, 30720), (80, 512, 16, 64, 32, 512, 1280),
+                                                 (1, 128, 16, 16, 16, 2, 70), (257, 512, 16, 16, 64, 65, 4099)])
+def test_grad_finish_bitwise_equals_three_launches(rows, R, E, ld, M, Nn, R_x):
+    """sgg_grad_finish (one launch: slab row sums, sgg_xtw's reduce pass, fold
+    backwards whose (dA, dbias) are slab row sums) is bit-identical to
+    sgg_slab_reduce + sgg_xtw + sgg_fold_bwd run one after the other."""
+    from sgan import _native as N
+    from sgan import kernels as K
+    torch.manual_seed(rows)
+    lib = K._lib()
+    P = 7 + 3 * R + 11                               # [junk | dA (2R) | dbias (R) | junk]
+    slab = torch.randn(rows, P, device=DEV)
+    Wfull = torch.randn(R, ld, device=DEV)
+    W = Wfull[:, :E]
+    We, be = torch.randn(E, 2, device=DEV), torch.randn(E, device=DEV)
+    X, Y = torch.randn(R_x, M, device=DEV), torch.randn(R_x, Nn, device=DEV)
+    # reference: three launches
+    flat = torch.empty(P, device=DEV)
+    N.check(lib.sgg_slab_reduce(N.ptr(slab), rows, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+    C_ref, cs_ref = K.xtw(X, Y, colsum=True, trans_c=True)
+    dW_ref, dWe_ref, dbe_ref = K.fold_bwd(W, We, be, flat[7:7 + 2 * R].view(R, 2), flat[7 + 2 * R:7 + 3 * R])
+    dW2_ref, dWe2_ref, dbe2_ref = K.fold_bwd(W, We, be, flat[7:7 + 2 * R].view(R, 2), cs_ref) if Nn == R else \
+        (None, None, None)
+    # one launch
+    ws, splits = K.xtw_partial(X, Y, colsum=True)
+    gf = K.GradFinish()
+    head = torch.empty(7, device=DEV)
+    C = torch.full((Nn, M + 3), 5.0, device=DEV)
+    cs = torch.empty(Nn, device=DEV)
+    copy = torch.empty(R, device=DEV)
+    gf.rowsum(slab, rows, P, 0, 7, head)
+    gf.xtw_sums(ws, splits, M, Nn, C[:, 1:1 + M], trans_c=True, colsum=cs)
+    dW, dWe, dbe = gf.fold(W, We, be, slab, rows, P, 7, slab, rows, P, 7 + 2 * R, dbias_copy=copy)
+    if Nn == R:   # the pooling form: dbias from the xtw column-sum partials
+        dW2, dWe2, dbe2 = gf.fold(W, We, be, slab, rows, P, 7, ws[splits * M * Nn:], splits, Nn, 0)
+    gf.run()
+    torch.cuda.synchronize()
+    eq = lambda a, b, what: torch.testing.assert_close(a, b, rtol=0, atol=0, msg=what)
+    eq(head, flat[:7], "slab row sums")
+    eq(C[:, 1:1 + M], C_ref, "xtw C^T")
+    assert float(C[:, 0].sub(5).abs().max()) == 0 and float(C[:, 1 + M:].sub(5).abs().max()) == 0
+    eq(cs, cs_ref, "xtw colsum")
+    eq(copy, flat[7 + 2 * R:7 + 3 * R], "dbias copy")
+    eq(dW, dW_ref, "fold dW")
+    eq(dWe, dWe_ref, "fold dWe")
+    eq(dbe, dbe_ref, "fold dbe")
+    if Nn == R:
+        eq(dW2, dW2_ref, "fold dW (colsum dbias)")
+        eq(dWe2, dWe2_ref, "fold dWe (colsum dbias)")
+        eq(dbe2, dbe2_ref, "fold dbe (colsum dbias)")
+
+
 def test_graphed_trainer_equals_eager():
     """The HIP-graph replay of a training iteration (GraphedTrainer) consumes
     the host RNGs in the same order and produces the same updates as the eager
