@@ -1,0 +1,235 @@
+// The discriminator's scoring head in one launch per direction:
+//   real_classifier = make_mlp([h_dim, mlp_dim, 1]) (reference sgan/models.py:
+//   958-965, make_mlp :7-20, called at :991): Linear(K, N1) -> ReLU ->
+//   Linear(N1, 1) -> ReLU.
+// Forward (sgg_head_fwd): hid = act1(X W1^T + b1) on v_mfma_f32_16x16x4_f32
+// (exact fp32), then y = act2(hid . w2 + b2) from the accumulator tiles
+// (per-lane partial over the column tiles, then a 16-lane xor tree) -- the
+// hidden layer never makes a second pass through memory; hid is stored for
+// the backward's ReLU mask.
+// Backward (sgg_head_bwd): g2 = dY (Y > 0), dhid = g2 w2 (hid > 0) staged in
+// LDS, dX = dhid W1 on the MFMA, and (wslab != NULL) one slab row per
+// workgroup [dW1 (N1 x K) | db1 (N1) | dW2 (N1) | db2] over its 64 rows:
+// dW1 = dhid^T X on the MFMA (each wave a quarter of the output tiles over all
+// 64 rows: no cross-wave sum), the vector sums in row order.  sgg_grad_finish
+// sums the rows.  Replaces 2 forward and up to 6 backward launches (two node
+// transforms, two input-gradient transforms, two split-K reductions).
+#include "sgg_common.h"
+
+namespace sgg {
+
+namespace {
+
+constexpr int kHeadRows = 64;   // rows per workgroup (4 waves x 16)
+
+template <int NT>   // NT = N1 / 16 hidden column tiles
+__global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__ X, int ldx, int M, int K,
+                                                       const float* __restrict__ W1, const float* __restrict__ b1,
+                                                       const float* __restrict__ w2, const float* __restrict__ b2,
+                                                       int act, float* __restrict__ hid, float* __restrict__ Y) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, q = lane >> 4;
+  const int row0 = blockIdx.x * kHeadRows + wave * 16;
+  const float* xr = X + (size_t)min(row0 + c16, M - 1) * ldx;
+  floatx4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // the lane's bias / w2 values first (independent of the k loop)
+  float bc[NT], wc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    bc[t] = b1[16 * t + c16];
+    wc[t] = w2[16 * t + c16];
+  }
+  const float bb2 = b2[0];
+  // K in chunks of 16 (4 k-steps), all of a chunk's loads issued together
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    float a[4], b[4][NT];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = k0 + 4 * s + q;
+      a[s] = xr[k];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[s][t] = W1[(size_t)(16 * t + c16) * K + k];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
+  }
+  // epilogue: lane holds rows 4 q + r, columns 16 t + c16
+  const int N1 = 16 * NT;
+  float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float h = acc[t][r] + bc[t];
+      if (act & 1) h = h > 0.f ? h : 0.f;
+      const int m = row0 + 4 * q + r;
+      if (m < M) hid[(size_t)m * N1 + 16 * t + c16] = h;
+      p[r] = fmaf(h, wc[t], p[r]);
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) p[r] += __shfl_xor(p[r], o);
+    float y = p[r] + bb2;
+    if (act & 2) y = y > 0.f ? y : 0.f;
+    const int m = row0 + 4 * q + r;
+    if (c16 == 0 && m < M) Y[m] = y;
+  }
+}
+
+template <int NT, int KT>   // N1 = 16 NT hidden units, K = 16 KT inputs
+__global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__ X, int ldx, int M,
+                                                       const float* __restrict__ W1, const float* __restrict__ w2,
+                                                       const float* __restrict__ hid, const float* __restrict__ Y,
+                                                       const float* __restrict__ dY, int act,
+                                                       float* __restrict__ dX, int lddx, float* __restrict__ wslab) {
+  constexpr int N1 = 16 * NT, K = 16 * KT;
+  constexpr int DP = N1 + 4;   // dhid row pitch
+  __shared__ float dh[kHeadRows][DP];
+  __shared__ float hg[kHeadRows][DP];   // g2 * hid (the dW2 terms)
+  __shared__ float g2s[kHeadRows];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, q = lane >> 4;
+  const int rb = blockIdx.x * kHeadRows;
+  const bool wgrad = wslab != nullptr;
+  // stage dhid (rows past M are zero: they add nothing to the weight sums)
+  for (int e = tid; e < kHeadRows * N1; e += 256) {
+    const int r = e / N1, n = e - r * N1;
+    const int m = rb + r;
+    const int mc = min(m, M - 1);
+    const float y = Y[mc], dy = dY[mc];
+    const float g = (m < M && (!(act & 2) || y > 0.f)) ? dy : 0.f;
+    const float h = hid[(size_t)mc * N1 + n];
+    dh[r][n] = (!(act & 1) || h > 0.f) ? g * w2[n] : 0.f;
+    hg[r][n] = g * h;
+    if (n == 0) g2s[r] = g;
+  }
+  __syncthreads();
+  // dX (this wave's 16 rows) = dhid W1: A[row][k = n] from LDS, B[n][col] = W1[n][col]
+  {
+    floatx4 acc[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int s = 0; s < N1 / 4; ++s) {
+      const int n = 4 * s + q;
+      const float a = dh[16 * wave + c16][n];
+      float b[KT];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) b[t] = W1[(size_t)n * K + 16 * t + c16];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[t], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = rb + 16 * wave + 4 * q + r;
+        if (m < M) dX[(size_t)m * lddx + 16 * t + c16] = acc[t][r];
+      }
+  }
+  if (!wgrad) return;
+  float* row = wslab + (size_t)blockIdx.x * (N1 * K + 2 * N1 + 1);
+  // dW1 = dhid^T X over the 64 rows: output tiles (mt, nt) dealt to the waves
+  for (int tile = wave; tile < NT * KT; tile += 4) {
+    const int mt = tile / KT, nt = tile - mt * KT;
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int s = 0; s < kHeadRows / 4; ++s) {
+      const int r = 4 * s + q;
+      const float a = dh[r][16 * mt + c16];
+      const float b = X[(size_t)min(rb + r, M - 1) * ldx + 16 * nt + c16];   // row r >= M: dh is zero
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) row[(size_t)(16 * mt + 4 * q + r) * K + 16 * nt + c16] = acc[r];
+  }
+  // db1, dW2 (column sums in row order), db2
+  for (int n = tid; n < N1; n += 256) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = 0; r < kHeadRows; ++r) {
+      s1 += dh[r][n];
+      s2 += hg[r][n];
+    }
+    row[N1 * K + n] = s1;
+    row[N1 * K + N1 + n] = s2;
+  }
+  if (tid == 0) {
+    float s = 0.f;
+    for (int r = 0; r < kHeadRows; ++r) s += g2s[r];
+    row[N1 * K + 2 * N1] = s;
+  }
+}
+
+template <int NT>
+int launch_fwd_nt(const float* X, int ldx, int M, int K, const float* W1, const float* b1, const float* w2,
+                  const float* b2, int act, float* hid, float* Y, hipStream_t st) {
+  hipLaunchKernelGGL(head_fwd_kernel<NT>, dim3((M + kHeadRows - 1) / kHeadRows), dim3(256), 0, st, X, ldx, M, K, W1,
+                     b1, w2, b2, act, hid, Y);
+  SGG_RETURN_LAUNCH("sgg_head_fwd");
+}
+
+template <int NT, int KT>
+int launch_bwd_nt(const float* X, int ldx, int M, const float* W1, const float* w2, const float* hid, const float* Y,
+                  const float* dY, int act, float* dX, int lddx, float* wslab, hipStream_t st) {
+  hipLaunchKernelGGL((head_bwd_kernel<NT, KT>), dim3((M + kHeadRows - 1) / kHeadRows), dim3(256), 0, st, X, ldx, M,
+                     W1, w2, hid, Y, dY, act, dX, lddx, wslab);
+  SGG_RETURN_LAUNCH("sgg_head_bwd");
+}
+
+template <int NT>
+int launch_bwd_k(const float* X, int ldx, int M, int K, const float* W1, const float* w2, const float* hid,
+                 const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, hipStream_t st) {
+  switch (K) {
+    case 16: return launch_bwd_nt<NT, 1>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+    case 32: return launch_bwd_nt<NT, 2>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+    case 48: return launch_bwd_nt<NT, 3>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+    default: return launch_bwd_nt<NT, 4>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+  }
+}
+
+}  // namespace
+
+}  // namespace sgg
+
+using namespace sgg;
+
+extern "C" int sgg_head_ok(int K, int N1) {
+  return (K == 16 || K == 32 || K == 48 || K == 64) && (N1 == 16 || N1 == 32 || N1 == 64);
+}
+
+extern "C" int sgg_head_slab_cols(int K, int N1) { return N1 * K + 2 * N1 + 1; }
+
+extern "C" int sgg_head_fwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* b1,
+                            const float* w2, const float* b2, int act, float* hid, float* Y, void* stream) {
+  SGG_CHECK_ARG(X && W1 && b1 && w2 && b2 && hid && Y, "sgg_head_fwd: null pointer");
+  SGG_CHECK_ARG(M >= 0 && sgg_head_ok(K, N1) && ldx >= K && act >= 0 && act <= 3,
+                "sgg_head_fwd: unsupported shape M=%d K=%d N1=%d ldx=%d act=%d", M, K, N1, ldx, act);
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (N1) {
+    case 16: return launch_fwd_nt<1>(X, ldx, M, K, W1, b1, w2, b2, act, hid, Y, st);
+    case 32: return launch_fwd_nt<2>(X, ldx, M, K, W1, b1, w2, b2, act, hid, Y, st);
+    default: return launch_fwd_nt<4>(X, ldx, M, K, W1, b1, w2, b2, act, hid, Y, st);
+  }
+}
+
+extern "C" int sgg_head_bwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* w2,
+                            const float* hid, const float* Y, const float* dY, int act, float* dX, int lddx,
+                            float* wslab, void* stream) {
+  SGG_CHECK_ARG(X && W1 && w2 && hid && Y && dY && dX, "sgg_head_bwd: null pointer");
+  SGG_CHECK_ARG(M >= 0 && sgg_head_ok(K, N1) && ldx >= K && lddx >= K && act >= 0 && act <= 3,
+                "sgg_head_bwd: unsupported shape M=%d K=%d N1=%d", M, K, N1);
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (N1) {
+    case 16: return launch_bwd_k<1>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+    case 32: return launch_bwd_k<2>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+    default: return launch_bwd_k<4>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+  }
+}

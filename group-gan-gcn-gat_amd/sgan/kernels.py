@@ -407,6 +407,101 @@ def linear(x, lin, act=0):
 
 
 # ---------------------------------------------------------------------------
+# discriminator scoring head (sgg_head_fwd / sgg_head_bwd)
+# ---------------------------------------------------------------------------
+def head_ok(seq):
+    """real_classifier = make_mlp([K, N1, 1]) without BatchNorm / dropout, with
+    ReLU or no activation after each Linear, in the shapes the fused head
+    kernel takes: returns (lin1, lin2, act) or None."""
+    mods = list(seq)
+    lins = [m for m in mods if isinstance(m, torch.nn.Linear)]
+    if len(lins) != 2 or any(not isinstance(m, (torch.nn.Linear, torch.nn.ReLU)) for m in mods):
+        return None
+    l1, l2 = lins
+    if l2.out_features != 1 or l1.bias is None or l2.bias is None:
+        return None
+    if not _lib().sgg_head_ok(l1.in_features, l1.out_features):
+        return None
+    i1, i2 = mods.index(l1), mods.index(l2)
+    relu1 = i1 + 1 < len(mods) and isinstance(mods[i1 + 1], torch.nn.ReLU)
+    relu2 = i2 + 1 < len(mods) and isinstance(mods[i2 + 1], torch.nn.ReLU)
+    if len(mods) != 2 + int(relu1) + int(relu2):
+        return None
+    return l1, l2, int(relu1) | (2 * int(relu2))
+
+
+class _Head(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, act):
+        lib = _lib()
+        x = _rows(x, "x")
+        M, Kd = x.shape
+        N1 = W1.shape[0]
+        W1, W2 = W1.contiguous(), W2.contiguous()
+        b1, b2 = b1.contiguous(), b2.contiguous()
+        hid = torch.empty(M, N1, device=x.device, dtype=torch.float32)
+        y = torch.empty(M, 1, device=x.device, dtype=torch.float32)
+
+        def launch():
+            N.check(lib.sgg_head_fwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(b1), N.ptr(W2), N.ptr(b2),
+                                     act, N.ptr(hid), N.ptr(y), N.stream_ptr()), "sgg_head_fwd")
+        launch()
+        if timer.active and M > 0:
+            timer.add("sgg::head_fwd_kernel<%d>" % (N1 // 16), (M, Kd, N1), 2.0 * M * N1 * (Kd + 1),
+                      4.0 * (M * Kd + N1 * Kd + M * N1 + M), launch)
+        ctx.act = act
+        ctx.save_for_backward(x, W1, W2, hid, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib()
+        x, W1, W2, hid, y = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        M, Kd = x.shape
+        N1 = W1.shape[0]
+        dy = dy.contiguous()
+        dx = torch.empty(M, Kd, device=x.device, dtype=torch.float32)
+        wgrad = any(need[1:5])
+        P = lib.sgg_head_slab_cols(Kd, N1)
+        rows = (M + 63) // 64
+        slab = torch.empty(max(rows, 1), P, device=x.device, dtype=torch.float32) if wgrad else None
+
+        def launch():
+            N.check(lib.sgg_head_bwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(W2), N.ptr(hid), N.ptr(y),
+                                     N.ptr(dy), ctx.act, N.ptr(dx), dx.stride(0), N.ptr(slab), N.stream_ptr()),
+                    "sgg_head_bwd")
+        launch()
+        if timer.active and M > 0:
+            timer.add("sgg::head_bwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1, wgrad),
+                      2.0 * M * N1 * Kd * (2 if wgrad else 1),
+                      4.0 * (M * Kd * (3 if wgrad else 2) + 2 * M * N1 + (slab.numel() if wgrad else 0)), launch)
+        if not wgrad:
+            return dx, None, None, None, None, None
+        dW1 = torch.empty(N1, Kd, device=x.device, dtype=torch.float32)
+        db1 = torch.empty(N1, device=x.device, dtype=torch.float32)
+        dW2 = torch.empty(1, N1, device=x.device, dtype=torch.float32)
+        db2 = torch.empty(1, device=x.device, dtype=torch.float32)
+        if M == 0:
+            for t in (dW1, db1, dW2, db2):
+                t.zero_()
+        else:
+            gf = GradFinish()
+            gf.rowsum(slab, rows, P, 0, N1 * Kd, dW1)
+            gf.rowsum(slab, rows, P, N1 * Kd, N1, db1)
+            gf.rowsum(slab, rows, P, N1 * Kd + N1, N1, dW2)
+            gf.rowsum(slab, rows, P, N1 * Kd + 2 * N1, 1, db2)
+            gf.run()
+        return dx, dW1, db1, dW2, db2, None
+
+
+def head(x, spec):
+    """real_classifier forward through the fused head (spec = head_ok(seq))."""
+    l1, l2, act = spec
+    return _Head.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, act)
+
+
+# ---------------------------------------------------------------------------
 # optimizer step
 # ---------------------------------------------------------------------------
 class ClipAdam:

@@ -647,4 +647,8 @@ class TrajectoryDiscriminator(nn.Module):
             x = final_h.squeeze()
         else:
             x = self.pool_net(final_h.squeeze(), seq_start_end, traj[0], scenes=scenes)
+        # Linear -> ReLU -> Linear(., 1) -> ReLU in one launch each way
+        spec = K.head_ok(self.real_classifier)
+        if spec is not None and x.dim() == 2:
+            return K.head(x, spec)
         return run_mlp(self.real_classifier, x)

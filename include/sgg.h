@@ -278,6 +278,25 @@ int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* folds, int n
                     size_t scratch_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
+ * The discriminator's scoring head real_classifier = make_mlp([K, N1, 1])
+ * (models.py:958-965 with make_mlp :7-20, applied at :991):
+ *   hid = act1(X W1^T + b1)  (M x N1),   Y = act2(hid . w2 + b2)  (M)
+ * act: bit 0 act1 = ReLU, bit 1 act2 = ReLU.  W1: N1 x K contiguous (nn.Linear),
+ * w2: N1, b1: N1, b2: 1 (device).  hid is written for the backward.  One
+ * launch: the hidden layer on v_mfma_f32_16x16x4_f32, the N1 -> 1 layer from
+ * the accumulator tiles.  Shapes: sgg_head_ok(K, N1) (K in {16, 32, 48, 64},
+ * N1 in {16, 32, 64}).
+ * Backward: dX (row stride lddx) and, when wslab != NULL, one slab row per 64
+ * rows ((M + 63) / 64 rows of sgg_head_slab_cols(K, N1) floats):
+ * [dW1 (N1 x K) | db1 (N1) | dW2 (N1) | db2], summed by sgg_grad_finish. */
+int sgg_head_ok(int K, int N1);
+int sgg_head_slab_cols(int K, int N1);
+int sgg_head_fwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* b1, const float* w2,
+                 const float* b2, int act, float* hid, float* Y, void* stream);
+int sgg_head_bwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* w2, const float* hid,
+                 const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, void* stream);
+
+/* ------------------------------------------------------------------------
  * Input-embedding fold (a Linear(2, E) displacement embedding feeding a
  * linear layer: the LSTM input weights, models.py:52-59 / 121-125, and the
  * pooling MLP's first layer, :477-481 / 530-538):

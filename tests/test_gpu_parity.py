@@ -470,7 +470,40 @@ def test_fold_matches_torch():
         close(dbe, (W.t() @ db).cpu().numpy(), rtol=2e-6, what="fold dbe")
 
 
-@pytest.mark.parametrize("rows,R,E,ld,M,Nn,R_x", [(160, 192, 16, 16, 48, 2, 30720), (80, 512, 16, 64, 32, 512, 1280),
+@pytest.mark.parametrize("M,Kd,N1,relu1,relu2", [(2560, 48, 64, 1, 1), (1000, 64, 32, 1, 0), (1, 16, 16, 0, 1),
+                                                 (63, 32, 64, 1, 1), (129, 48, 16, 0, 0)])
+def test_fused_head_matches_torch(M, Kd, N1, relu1, relu2):
+    """sgg_head_fwd / sgg_head_bwd (+ sgg_grad_finish) against autograd of the
+    reference's real_classifier = make_mlp([K, N1, 1]) in float64."""
+    from sgan import kernels as K
+    from sgan.models import make_mlp
+    torch.manual_seed(M + Kd)
+    seq = make_mlp([Kd, N1, 1], batch_norm=False).to(DEV)
+    mods = [m for m in seq]
+    if not relu1:
+        mods.pop(1)
+    if not relu2:
+        mods.pop(-1)
+    seq = torch.nn.Sequential(*mods)
+    spec = K.head_ok(seq)
+    assert spec is not None and spec[2] == relu1 | (2 * relu2)
+    x = torch.randn(M, Kd, device=DEV, requires_grad=True)
+    y = K.head(x, spec)
+    dy = torch.randn(M, 1, device=DEV)
+    y.backward(dy)
+    ref = torch.nn.Sequential(*[type(m)(m.in_features, m.out_features).double() if isinstance(m, torch.nn.Linear)
+                                else m for m in mods]).to(DEV)
+    ref.load_state_dict({k: v.double() for k, v in seq.state_dict().items()})
+    xd = x.detach().double().requires_grad_(True)
+    yr = ref(xd)
+    yr.backward(dy.double())
+    close(y.detach(), yr.detach().cpu().numpy(), rtol=2e-6, what="head y")
+    close(x.grad, xd.grad.cpu().numpy(), rtol=2e-5, what="head dx")
+    for (n, p), pr in zip(seq.named_parameters(), ref.parameters()):
+        close(p.grad, pr.grad.cpu().numpy(), rtol=2e-5, what="head d%s" % n)
+
+
+@pytest.mark.parametrize("rows,R,E,ld,M,Nn,R_x",[(160, 192, 16, 16, 48, 2, 30720), (80, 512, 16, 64, 32, 512, 1280),
                                                  (1, 128, 16, 16, 16, 2, 70), (257, 512, 16, 16, 64, 65, 4099)])
 def test_grad_finish_bitwise_equals_three_launches(rows, R, E, ld, M, Nn, R_x):
     """sgg_grad_finish (one launch: slab row sums, sgg_xtw's reduce pass, fold
