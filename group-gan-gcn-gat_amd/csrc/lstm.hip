@@ -285,6 +285,28 @@ extern "C" const char* sgg_lstm_kernel_name(int H, int B, int decoder, int save,
   return buf;
 }
 
+// the family sgg_lstm_fwd picks for these sizes is the four-wave one
+static bool fwd_picks_mw(int H, int B, bool save) {
+  const bool mw = lstm_mw_ok(H, B);
+  if (save) return mw;
+  return mw && !(lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"));
+}
+
+extern "C" int sgg_lstm_u_ok(int T, int B, int H, int decoder, int save, int NU) {
+  return !decoder && B > 0 && T >= 1 && NU >= 16 && NU % 16 == 0 && fwd_picks_mw(H, B, save != 0);
+}
+
+extern "C" int sgg_lstm_fwd_u(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
+                              const float* c0, int T, int B, int H, float* h_all, float* c_all, float* act_all,
+                              const float* Wu, int ldwu, const float* cu, int NU, float* U, void* stream) {
+  SGG_CHECK_ARG(rel && A && Whh && bias && h_all && c_all && Wu && cu && U, "sgg_lstm_fwd_u: null pointer");
+  SGG_CHECK_ARG(sgg_lstm_u_ok(T, B, H, 0, act_all != nullptr, NU) && ldwu >= H,
+                "sgg_lstm_fwd_u: no projection epilogue for T=%d B=%d H=%d NU=%d ldwu=%d (sgg_lstm_u_ok)", T, B, H, NU,
+                ldwu);
+  return lstm_mw_fwd(rel, A, Whh, bias, h0, c0, nullptr, nullptr, T, B, H, 0, h_all, c_all, act_all, nullptr,
+                     (hipStream_t)stream, Wu, ldwu, cu, NU, U);
+}
+
 extern "C" int sgg_lstm_wpart_rows(int H, int B) {
   if (B < 0) return -1;
   return lstm_mw_ok(H, B) ? lstm_mw_wpart_rows(H, B) : 0;

@@ -99,7 +99,8 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
     const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B,
-    float* __restrict__ h_all, float* __restrict__ c_tile, float* __restrict__ act_tile, float* __restrict__ rel_out) {
+    float* __restrict__ h_all, float* __restrict__ c_tile, float* __restrict__ act_tile, float* __restrict__ rel_out,
+    const float* __restrict__ Wu, int ldwu, const float* __restrict__ cu, int NU, float* __restrict__ U) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS;
   constexpr bool decoder = DEC, save = SAVE;
   __shared__ float gate[4][KS][64];
@@ -222,6 +223,55 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
       const float2 r0 = rpart[0][c16], r1 = rpart[1][c16], r2 = rpart[2][c16], r3 = rpart[3][c16];
       *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + pc) * 2) =
           make_float2(((r0.x + r1.x) + (r2.x + r3.x)) + bp0, ((r0.y + r1.y) + (r2.y + r3.y)) + bp1);
+    }
+  }
+  if (!decoder && U) {
+    // projection epilogue: U = h_T Wu^T + cu (B x NU; the pooling MLP's h-half
+    // of its first layer, models.py:538) while h_T is still in LDS, in the
+    // recurrence's own operand layout: U^T tile (16 units x 16 peds) =
+    // Wu[tile rows][k] . h[k][peds] over the permuted k order of hb.  Wave g
+    // takes tiles g, g + 4, ...
+    float hk[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[ks][lane];
+    const int ntile = NU >> 4;
+    // tiles in pairs (two independent accumulation chains); the next pair's
+    // Wu fragments are in flight during the current pair's MFMAs
+    float wa[2][KS], wn[2][KS];
+    auto load_w = [&](int nt, float (&w)[KS]) {
+      const float* wr = Wu + (size_t)(min(nt, ntile - 1) * 16 + c16) * ldwu;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) w[ks] = wr[slot_unit(ks, q)];
+    };
+    load_w(g, wa[0]);
+    load_w(g + 4, wa[1]);
+    for (int nt = g; nt < ntile; nt += 8) {
+      const bool more = nt + 8 < ntile;
+      if (more) {
+        load_w(nt + 8, wn[0]);
+        load_w(nt + 12, wn[1]);
+      }
+      floatx4 acc0 = floatx4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[0][ks], hk[ks], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[1][ks], hk[ks], acc1, 0, 0, 0);
+      }
+      const float4 cb0 = *reinterpret_cast<const float4*>(cu + 16 * nt + 4 * q);
+      *reinterpret_cast<float4*>(U + (size_t)pc * NU + 16 * nt + 4 * q) =
+          make_float4(acc0[0] + cb0.x, acc0[1] + cb0.y, acc0[2] + cb0.z, acc0[3] + cb0.w);
+      if (nt + 4 < ntile) {
+        const float4 cb1 = *reinterpret_cast<const float4*>(cu + 16 * (nt + 4) + 4 * q);
+        *reinterpret_cast<float4*>(U + (size_t)pc * NU + 16 * (nt + 4) + 4 * q) =
+            make_float4(acc1[0] + cb1.x, acc1[1] + cb1.y, acc1[2] + cb1.z, acc1[3] + cb1.w);
+      }
+      if (more) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          wa[0][ks] = wn[0][ks];
+          wa[1][ks] = wn[1][ks];
+        }
+      }
     }
   }
 }
@@ -516,12 +566,12 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 template <int H>
 int launch_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0, const float* c0,
                const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
-               float* rel_out, hipStream_t st) {
+               float* rel_out, const float* Wu, int ldwu, const float* cu, int NU, float* U, hipStream_t st) {
   const int grid = (B + kMwPeds - 1) / kMwPeds;
   auto k = decoder ? (act_all ? lstm_mw_fwd_kernel<H, true, true> : lstm_mw_fwd_kernel<H, true, false>)
                    : (act_all ? lstm_mw_fwd_kernel<H, false, true> : lstm_mw_fwd_kernel<H, false, false>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kMwThreads), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B, h_all, c_all,
-                     act_all, rel_out);
+                     act_all, rel_out, Wu, ldwu, cu, NU, U);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
 }
 
@@ -568,14 +618,15 @@ int lstm_mw_wpart_rows(int H, int B) {
 
 int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
                 const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
-                float* c_all, float* act_all, float* rel_out, hipStream_t st) {
+                float* c_all, float* act_all, float* rel_out, hipStream_t st, const float* Wu, int ldwu,
+                const float* cu, int NU, float* U) {
   SGG_CHECK_ARG(decoder || T <= kMwMaxT, "sgg_lstm_fwd: encoder sequences of the H=%d kernels hold <= %d steps (T=%d)",
                 H, kMwMaxT, T);
   switch (H) {
-    case 16: return launch_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
-    case 32: return launch_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
-    case 48: return launch_fwd<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
-    default: return launch_fwd<64>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+    case 16: return launch_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
+    case 32: return launch_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
+    case 48: return launch_fwd<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
+    default: return launch_fwd<64>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
   }
 }
 

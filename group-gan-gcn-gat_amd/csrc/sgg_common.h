@@ -90,7 +90,9 @@ __attribute__((visibility("hidden"))) int lstm_mw_fwd(const float* rel, const fl
                                                       const float* bias, const float* h0, const float* c0,
                                                       const float* Wp, const float* bp, int T, int B, int H,
                                                       int decoder, float* h_all, float* c_all, float* act_all,
-                                                      float* rel_out, hipStream_t st);
+                                                      float* rel_out, hipStream_t st, const float* Wu = nullptr,
+                                                      int ldwu = 0, const float* cu = nullptr, int NU = 0,
+                                                      float* U = nullptr);
 __attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp,
                                                       const float* h_all, const float* c_all, const float* act_all,
                                                       const float* rel, const float* rel_out, const float* dh_last,

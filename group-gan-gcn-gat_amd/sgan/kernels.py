@@ -683,7 +683,7 @@ class _Pool(torch.autograd.Function):
     transposed -> right block)."""
 
     @staticmethod
-    def forward(ctx, h, pos, W1, We, be, b1, W2, b2, scenes, link=None):
+    def forward(ctx, h, pos, W1, We, be, b1, W2, b2, scenes, link=None, U=None):
         lib = _lib()
         ctx.link = link
         h = _rows(h, "h")
@@ -697,7 +697,10 @@ class _Pool(torch.autograd.Function):
         W2 = W2.contiguous()
         b2 = b2.contiguous()
         A, c = fold_fwd(W1[:, :E], We, be, b1)
-        U = xw_raw(h, W1[:, E:], c, trans_w=True)                 # B x 512
+        if U is None:
+            U = xw_raw(h, W1[:, E:], c, trans_w=True)             # B x 512
+        else:                                                     # from the encoder kernel's epilogue
+            assert U.shape == (B, 512) and U.is_contiguous()
         out = torch.empty(B, bn, device=h.device, dtype=torch.float32)
         am = torch.empty(B, bn, device=h.device, dtype=torch.int32)
         chunks, nchunks, max_rows, gpw = scenes.pool_plan(bn)
@@ -750,7 +753,7 @@ class _Pool(torch.autograd.Function):
             # dh = dU W1h (+ the other consumer's gradient of h, accumulated in the same launch)
             dh = xw_raw(dU, W1[:, E:], None, trans_w=False, prec="fp32", out=base, act=0 if base is None else 2)
         if not wgrad:
-            return dh, None, None, None, None, None, None, None, None, None
+            return dh, None, None, None, None, None, None, None, None, None, None
         with side(part, h, dU, W1, We, be):
             # one launch after the dW1h partials: dW2, db2 (slab [dW2 | dA | db2]
             # row sums), dW1h = dU^T h, dc = sum_j dU_j, and the fold backward
@@ -769,7 +772,7 @@ class _Pool(torch.autograd.Function):
             _, dWe, dbe = gf.fold(W1[:, :E], We, be, part, rows, P, bn * 512, ws[splits * H * 512:], splits, 512, 0,
                                   dW=dW1[:, :E])
             gf.run()
-        return dh, None, dW1, dWe, dbe, dc, dW2, db2, None, None
+        return dh, None, dW1, dWe, dbe, dc, dW2, db2, None, None, None
 
 
 class GradLink:
@@ -792,11 +795,21 @@ class GradLink:
         return g
 
 
-def social_pool(h, pos, W1, We, be, b1, W2, b2, scenes, link=None):
+def social_pool(h, pos, W1, We, be, b1, W2, b2, scenes, link=None, U=None):
     """PoolHiddenNet core (models.py:497-549) -> (B, bn); see sgg_pool_fwd.
-    link: a GradLink whose pending gradient of h the backward adds to dh."""
-    out, _ = _Pool.apply(h, pos, W1, We, be, b1, W2, b2, scenes, link)
+    link: a GradLink whose pending gradient of h the backward adds to dh.
+    U: h W1[:, E:]^T + c when the encoder kernel already produced it
+    (pool_u_spec / lstm_sequence(proj_u=...))."""
+    out, _ = _Pool.apply(h, pos, W1, We, be, b1, W2, b2, scenes, link, U)
     return out
+
+
+def pool_u_spec(pool):
+    """(Wu, cu) of a PoolHiddenNet for the encoder's projection epilogue:
+    Wu = W1[:, E:] (in place), cu = W1[:, :E] be + b1 (the cached fold)."""
+    l1, E = pool.mlp_pre_pool[0], pool.embedding_dim
+    _, c = fold_fwd(l1.weight[:, :E], pool.spatial_embedding.weight, pool.spatial_embedding.bias, l1.bias)
+    return l1.weight[:, E:], c
 
 
 # ---------------------------------------------------------------------------
@@ -1134,7 +1147,7 @@ class _LSTMSeq(torch.autograd.Function):
     and reduced by sgg_xtw."""
 
     @staticmethod
-    def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save):
+    def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save, u=None):
         lib = _lib()
         rel = _req(rel, "rel").contiguous()
         H = W_hh.shape[1]
@@ -1151,16 +1164,29 @@ class _LSTMSeq(torch.autograd.Function):
         h0c = h0.contiguous() if h0 is not None else None
         c0c = c0.contiguous() if c0 is not None else None
         Wpc = Wp.contiguous() if Wp is not None else None
-        def launch():
-            N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c),
-                                     N.ptr(Wpc), N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all),
-                                     N.ptr(act), N.ptr(rel_out), N.stream_ptr()), "sgg_lstm_fwd")
+        U = None
+        if u is not None:
+            # the pooling MLP's U = h_T Wu^T + cu from the kernel's epilogue
+            Wu, cu = u
+            Wu = _rows(Wu, "Wu")
+            cu = cu.contiguous()
+            U = torch.empty(B, Wu.shape[0], device=dev, dtype=torch.float32)
+
+            def launch():
+                N.check(lib.sgg_lstm_fwd_u(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), T,
+                                           B, H, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu), Wu.stride(0),
+                                           N.ptr(cu), Wu.shape[0], N.ptr(U), N.stream_ptr()), "sgg_lstm_fwd_u")
+        else:
+            def launch():
+                N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c),
+                                         N.ptr(Wpc), N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all),
+                                         N.ptr(act), N.ptr(rel_out), N.stream_ptr()), "sgg_lstm_fwd")
         launch()
         if timer.active:
             # per ped-step: gates 2 4H (H + 3) FLOP + ~12 H cell / activation; bytes: inputs, saved states
-            fl = T * B * (8.0 * H * (H + 3) + 12.0 * H)
+            fl = T * B * (8.0 * H * (H + 3) + 12.0 * H) + (2.0 * B * H * U.shape[1] if U is not None else 0.0)
             nb = 4.0 * (T * B * 2 + (act.numel() + c_all.numel() + (T + 1) * B * H if save else B * H)
-                        + 4 * H * (H + 3) + (T * B * 2 if decoder else 0))
+                        + 4 * H * (H + 3) + (T * B * 2 if decoder else 0) + (U.numel() if U is not None else 0))
             timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), int(save), 0).decode(),
                       (T, B, int(decoder), int(save)), fl, nb, launch)
         ctx.meta = (decoder, T, B, H, h0 is not None)
@@ -1168,6 +1194,9 @@ class _LSTMSeq(torch.autograd.Function):
         if save:
             ctx.save_for_backward(rel, W_ih, We, be, A, Whh, Wpc, h_all, c_all, act, rel_out)
         h_last = h_all[T]
+        if U is not None:
+            ctx.mark_non_differentiable(U)   # its gradient is the pooling backward's business (dh = dU Wu)
+            return h_last, U
         if decoder:
             return h_last, rel_out
         return h_last, h_last.new_empty(0)
@@ -1245,7 +1274,7 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             drel = drel_in
         return (drel, dW_ih, dW_hh, db_ih, db_hh, dWe, dbe, (dh0 if has_h0 else None), None, dWp, dbp,
-                None, None, None)
+                None, None, None, None)
 
 
 def _lstm_wgrads(lib, wpart, rows, P, G4, H, T, B, dG, h_all, rel, rel_out, decoder, W_ih, We, be, dev):
@@ -1268,9 +1297,16 @@ def _lstm_wgrads(lib, wpart, rows, P, G4, H, T, B, dG, h_all, rel, rel_out, deco
     return dW_ih, dW_hh, dbias, db_hh, dWe, dbe
 
 
-def lstm_sequence(rel, lstm, emb, h0=None, c0=None, proj=None, decoder=False, T=None):
+def lstm_u_ok(T, B, H, save, NU):
+    return bool(_lib().sgg_lstm_u_ok(T, B, H, 0, int(save), NU))
+
+
+def lstm_sequence(rel, lstm, emb, h0=None, c0=None, proj=None, decoder=False, T=None, proj_u=None):
     """Fused Linear(2, E) + 1-layer LSTM over T steps (see sgg_lstm_fwd);
-    `proj` is the decoder's hidden2pos.  Returns (h_last, rel_out)."""
+    `proj` is the decoder's hidden2pos.  Returns (h_last, rel_out).
+    proj_u = (Wu, cu) (encoder): returns (h_last, U) with U = h_last Wu^T + cu
+    from the kernel's epilogue, or (h_last, None) where the kernel family
+    the sizes select has no such epilogue."""
     T = T if T is not None else rel.shape[0]
     W_ih, W_hh, b_ih, b_hh = lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0
     Wp = proj.weight if proj is not None else None
@@ -1279,6 +1315,13 @@ def lstm_sequence(rel, lstm, emb, h0=None, c0=None, proj=None, decoder=False, T=
     save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ins)
     if c0 is not None and c0.requires_grad and torch.is_grad_enabled():
         raise NotImplementedError("gradient w.r.t. the initial cell state")
+    if proj_u is not None:
+        if decoder or not lstm_u_ok(T, rel.shape[-2], W_hh.shape[1], save, proj_u[0].shape[0]):
+            h_last, _ = _LSTMSeq.apply(rel, W_ih, W_hh, b_ih, b_hh, emb.weight, emb.bias, h0, c0, Wp, bp,
+                                       bool(decoder), T, save)
+            return h_last, None
+        return _LSTMSeq.apply(rel, W_ih, W_hh, b_ih, b_hh, emb.weight, emb.bias, h0, c0, Wp, bp, bool(decoder), T,
+                              save, proj_u)
     h_last, rel_out = _LSTMSeq.apply(rel, W_ih, W_hh, b_ih, b_hh, emb.weight, emb.bias, h0, c0, Wp, bp,
                                      bool(decoder), T, save)
     return h_last, (rel_out if decoder else None)

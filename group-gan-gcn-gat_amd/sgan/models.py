@@ -118,11 +118,16 @@ class Encoder(nn.Module):
         self.spatial_embedding = nn.Linear(2, embedding_dim)
         self.encoder = nn.LSTM(embedding_dim, h_dim, num_layers, dropout=dropout)
 
-    def forward(self, obs_traj):
+    def forward(self, obs_traj, proj_u=None):
         """Fused sgg_lstm_fwd over all T steps; the Linear(2, E) embedding is
-        folded into the input weights (A = W_ih We, b = W_ih be + b_ih + b_hh)."""
+        folded into the input weights (A = W_ih We, b = W_ih be + b_ih + b_hh).
+        proj_u = (Wu, cu): also return U = h Wu^T + cu (None where the kernel
+        has no epilogue for these sizes) -- the pooling net's first layer."""
         if self.num_layers != 1:
             raise NotImplementedError("fused LSTM kernel: num_layers must be 1 (all reference configs)")
+        if proj_u is not None:
+            h, U = K.lstm_sequence(obs_traj, self.encoder, self.spatial_embedding, proj_u=proj_u)
+            return h.unsqueeze(0), U
         h, _ = K.lstm_sequence(obs_traj, self.encoder, self.spatial_embedding)
         return h.unsqueeze(0)
 
@@ -196,15 +201,20 @@ class PoolHiddenNet(nn.Module):
         self.mlp_pre_pool = make_mlp([embedding_dim + h_dim, 512, bottleneck_dim], activation=activation,
                                      batch_norm=batch_norm, dropout=dropout)
 
-    def forward(self, h_states, seq_start_end, end_pos, scenes=None, link=None):
-        if self.batch_norm or self.activation != "relu" or self.dropout > 0:
+    def fused_ok(self):
+        return not (self.batch_norm or self.activation != "relu" or self.dropout > 0)
+
+    def forward(self, h_states, seq_start_end, end_pos, scenes=None, link=None, U=None):
+        """U (optional): h W1[:, E:]^T + c already computed by the encoder
+        kernel's epilogue (K.pool_u_spec)."""
+        if not self.fused_ok():
             raise NotImplementedError("the fused pooling kernel implements the reference configs "
                                       "(batch_norm=0, relu, dropout=0)")
         sc = _scenes(seq_start_end, end_pos.device, scenes)
         l1, l2 = self.mlp_pre_pool[0], self.mlp_pre_pool[2]
         emb = self.spatial_embedding
         return K.social_pool(h_states.reshape(-1, self.h_dim), end_pos, l1.weight, emb.weight, emb.bias, l1.bias,
-                             l2.weight, l2.bias, sc, link=link)
+                             l2.weight, l2.bias, sc, link=link, U=U)
 
 
 # ---------------------------------------------------------------------------
@@ -542,14 +552,19 @@ class TrajectoryGenerator(nn.Module):
         sc = _scenes(seq_start_end, obs_traj.device, scenes)
         if self.num_layers == 1:
             K.prefold(self.fold_specs())
-        final_encoder_h = self.encoder(obs_traj_rel)
+        U = None
+        if self.pooling_type == "pool_net" and self.num_layers == 1 and self.pool_net.fused_ok():
+            # the pooling net's first layer (h half) in the encoder kernel's epilogue
+            final_encoder_h, U = self.encoder(obs_traj_rel, proj_u=K.pool_u_spec(self.pool_net))
+        else:
+            final_encoder_h = self.encoder(obs_traj_rel)
         ctx = final_encoder_h.view(-1, self.encoder_h_dim)
         end_pos = obs_traj[-1]
         if self.pooling_type:
             fused_gat = self.graph == "gat" and self.mlp_decoder_needed()
             # the GAT encoder's gradient of h reaches the pooling backward, which adds it in its own launch
             link = K.GradLink() if fused_gat and torch.is_grad_enabled() else None
-            pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc, link=link)
+            pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc, link=link, U=U)
             if fused_gat:
                 # the GAT encoder reads [h | pool_h] as two blocks (no cat)
                 noise_input = self.gatencoder((ctx, pool_h), seq_start_end, end_pos, obs_traj_g[-1], scenes=sc,
@@ -642,11 +657,15 @@ class TrajectoryDiscriminator(nn.Module):
             if self.d_type != "local":
                 specs.append(K.pool_fold_spec(self.pool_net))
             K.prefold(specs)
-        final_h = self.encoder(traj_rel)
+        if self.d_type != "local" and self.encoder.num_layers == 1 and self.pool_net.fused_ok():
+            # the pooling net's first layer (h half) in the encoder kernel's epilogue
+            final_h, U = self.encoder(traj_rel, proj_u=K.pool_u_spec(self.pool_net))
+        else:
+            final_h, U = self.encoder(traj_rel), None
         if self.d_type == "local":
             x = final_h.squeeze()
         else:
-            x = self.pool_net(final_h.squeeze(), seq_start_end, traj[0], scenes=scenes)
+            x = self.pool_net(final_h.squeeze(), seq_start_end, traj[0], scenes=scenes, U=U)
         # Linear -> ReLU -> Linear(., 1) -> ReLU in one launch each way
         spec = K.head_ok(self.real_classifier)
         if spec is not None and x.dim() == 2:

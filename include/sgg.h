@@ -350,6 +350,17 @@ int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float
                  int decoder, float* h_all, float* c_all, float* act_all, float* rel_out,
                  void* stream);
 
+/* Encoder sequence (decoder = 0) with the pooling MLP's h-half fused into the
+ * kernel's epilogue (models.py:538): also writes U = h_T Wu^T + cu (B x NU,
+ * Wu: NU x H with row stride ldwu -- W1[:, E:] in place; cu: NU), computed
+ * while h_T is still in LDS.  Available where sgg_lstm_u_ok says so (the
+ * four-wave family; NU a multiple of 16); the other arguments and outputs are
+ * those of sgg_lstm_fwd (act_all = NULL: no saved states). */
+int sgg_lstm_u_ok(int T, int B, int H, int decoder, int save, int NU);
+int sgg_lstm_fwd_u(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
+                   const float* c0, int T, int B, int H, float* h_all, float* c_all, float* act_all,
+                   const float* Wu, int ldwu, const float* cu, int NU, float* U, void* stream);
+
 /* Backward of sgg_lstm_fwd (BPTT).  encoder: dh_last = dL/dh_{T-1} (B x H, may
  * be NULL); decoder: dout = dL/drel_out (T x B x 2) (the decoder feedback
  * r_t -> step t+1 is included).  Writes drel_in (T x B x 2, dL/dr_t of the

@@ -470,7 +470,33 @@ def test_fold_matches_torch():
         close(dbe, (W.t() @ db).cpu().numpy(), rtol=2e-6, what="fold dbe")
 
 
-@pytest.mark.parametrize("M,Kd,N1,relu1,relu2", [(2560, 48, 64, 1, 1), (1000, 64, 32, 1, 0), (1, 16, 16, 0, 1),
+@pytest.mark.parametrize("H,T,B,save", [(48, 20, 2560, True), (32, 8, 1280, False), (48, 20, 37, True),
+                                        (32, 8, 5, True), (16, 8, 17, False)])
+def test_encoder_projection_epilogue(H, T, B, save):
+    """sgg_lstm_fwd_u: the encoder kernel's U = h_T Wu^T + cu (the pooling
+    net's first layer, Wu = W1[:, E:] in place) equals the sgg_xw form, and
+    h_T is unchanged by the epilogue."""
+    from sgan import kernels as K
+    torch.manual_seed(H + B)
+    lstm = torch.nn.LSTM(16, H).to(DEV)
+    emb = torch.nn.Linear(2, 16).to(DEV)
+    rel = torch.randn(T, B, 2, device=DEV)
+    W1 = torch.randn(512, 16 + H, device=DEV) * 0.2
+    cu = torch.randn(512, device=DEV)
+    with torch.set_grad_enabled(save):
+        if save:
+            rel.requires_grad_(True)
+        h_ref, _ = K.lstm_sequence(rel, lstm, emb)
+        h, U = K.lstm_sequence(rel, lstm, emb, proj_u=(W1[:, 16:], cu))
+    assert U is not None, "the four-wave family should take the projection at these sizes"
+    torch.testing.assert_close(h, h_ref, rtol=0, atol=0)
+    U_ref = K.xw_raw(h_ref.detach(), W1[:, 16:], cu, trans_w=True)
+    ref64 = (h_ref.detach().double() @ W1[:, 16:].double().t() + cu.double()).float()
+    close(U, ref64.cpu(), rtol=2e-6, what="U vs float64")
+    close(U, U_ref.cpu(), rtol=2e-6, what="U vs sgg_xw")
+
+
+@pytest.mark.parametrize("M,Kd,N1,relu1,relu2",[(2560, 48, 64, 1, 1), (1000, 64, 32, 1, 0), (1, 16, 16, 0, 1),
                                                  (63, 32, 64, 1, 1), (129, 48, 16, 0, 0)])
 def test_fused_head_matches_torch(M, Kd, N1, relu1, relu2):
     """sgg_head_fwd / sgg_head_bwd (+ sgg_grad_finish) against autograd of the
