@@ -393,6 +393,11 @@ def main():
                          "avg_us": round(r["ms"] * 1e3, 2), "us_per_iter": round(us, 1)}
                         for us, n, r, k in launches[:30]]
         total_launch_us = sum(x[0] for x in launches)
+        if os.environ.get("SGG_BENCH_TABLE"):   # every instrumented launch (the JSON line keeps the top 30)
+            with open(os.environ["SGG_BENCH_TABLE"], "w") as f:
+                for us, n, r, k in launches:
+                    f.write("%-50s %-36s %5.2f %8.2f %8.1f\n" % (n[:50], str(list(k[1:]))[:36], r["launches"] / n_it,
+                                                              r["ms"] * 1e3, us))
         ms_step = elapsed / args.steps * 1e3
         value = world * per_gpu / (elapsed / args.steps)
         cpu = None

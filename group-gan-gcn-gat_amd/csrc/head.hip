@@ -22,41 +22,38 @@ namespace {
 
 constexpr int kHeadRows = 64;   // rows per workgroup (4 waves x 16)
 
-template <int NT>   // NT = N1 / 16 hidden column tiles
-__global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__ X, int ldx, int M, int K,
+template <int NT, int KT>   // NT = N1 / 16 hidden column tiles, K = 16 KT inputs
+__global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__ X, int ldx, int M,
                                                        const float* __restrict__ W1, const float* __restrict__ b1,
                                                        const float* __restrict__ w2, const float* __restrict__ b2,
                                                        int act, float* __restrict__ hid, float* __restrict__ Y) {
+  constexpr int K = 16 * KT, KS = 4 * KT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q = lane >> 4;
   const int row0 = blockIdx.x * kHeadRows + wave * 16;
   const float* xr = X + (size_t)min(row0 + c16, M - 1) * ldx;
-  floatx4 acc[NT];
+  // every operand of the lane issued up front: one memory round trip
+  float a[KS], b[KS][NT], bc[NT], wc[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // the lane's bias / w2 values first (independent of the k loop)
-  float bc[NT], wc[NT];
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + q;
+    a[s] = xr[k];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[s][t] = W1[(size_t)(16 * t + c16) * K + k];
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     bc[t] = b1[16 * t + c16];
     wc[t] = w2[16 * t + c16];
   }
   const float bb2 = b2[0];
-  // K in chunks of 16 (4 k-steps), all of a chunk's loads issued together
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    float a[4], b[4][NT];
+  floatx4 acc[NT];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int k = k0 + 4 * s + q;
-      a[s] = xr[k];
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < NT; ++t) b[s][t] = W1[(size_t)(16 * t + c16) * K + k];
-    }
+  for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
-  }
+    for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
   // epilogue: lane holds rows 4 q + r, columns 16 t + c16
   const int N1 = 16 * NT;
   float p[4] = {0.f, 0.f, 0.f, 0.f};
@@ -97,6 +94,12 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
   const int c16 = lane & 15, q = lane >> 4;
   const int rb = blockIdx.x * kHeadRows;
   const bool wgrad = wslab != nullptr;
+  // the dX product's W1 fragments, in flight across the staging
+  float wb[N1 / 4][KT];
+#pragma unroll
+  for (int s = 0; s < N1 / 4; ++s)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) wb[s][t] = W1[(size_t)(4 * s + q) * K + 16 * t + c16];
   // stage dhid (rows past M are zero: they add nothing to the weight sums)
   for (int e = tid; e < kHeadRows * N1; e += 256) {
     const int r = e / N1, n = e - r * N1;
@@ -111,19 +114,16 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
   }
   __syncthreads();
   // dX (this wave's 16 rows) = dhid W1: A[row][k = n] from LDS, B[n][col] = W1[n][col]
+  // (the W1 fragments were loaded before the staging barrier)
   {
     floatx4 acc[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+#pragma unroll
     for (int s = 0; s < N1 / 4; ++s) {
-      const int n = 4 * s + q;
-      const float a = dh[16 * wave + c16][n];
-      float b[KT];
+      const float a = dh[16 * wave + c16][4 * s + q];
 #pragma unroll
-      for (int t = 0; t < KT; ++t) b[t] = W1[(size_t)n * K + 16 * t + c16];
-#pragma unroll
-      for (int t = 0; t < KT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < KT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[s][t], acc[t], 0, 0, 0);
     }
 #pragma unroll
     for (int t = 0; t < KT; ++t)
@@ -139,12 +139,14 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
   for (int tile = wave; tile < NT * KT; tile += 4) {
     const int mt = tile / KT, nt = tile - mt * KT;
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+    float xb[kHeadRows / 4];
+#pragma unroll
+    for (int s = 0; s < kHeadRows / 4; ++s)   // row r >= M: dh is zero
+      xb[s] = X[(size_t)min(rb + 4 * s + q, M - 1) * ldx + 16 * nt + c16];
+#pragma unroll
     for (int s = 0; s < kHeadRows / 4; ++s) {
-      const int r = 4 * s + q;
-      const float a = dh[r][16 * mt + c16];
-      const float b = X[(size_t)min(rb + r, M - 1) * ldx + 16 * nt + c16];   // row r >= M: dh is zero
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      const float a = dh[4 * s + q][16 * mt + c16];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xb[s], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) row[(size_t)(16 * mt + 4 * q + r) * K + 16 * nt + c16] = acc[r];
@@ -169,8 +171,13 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
 template <int NT>
 int launch_fwd_nt(const float* X, int ldx, int M, int K, const float* W1, const float* b1, const float* w2,
                   const float* b2, int act, float* hid, float* Y, hipStream_t st) {
-  hipLaunchKernelGGL(head_fwd_kernel<NT>, dim3((M + kHeadRows - 1) / kHeadRows), dim3(256), 0, st, X, ldx, M, K, W1,
-                     b1, w2, b2, act, hid, Y);
+  const dim3 grid((M + kHeadRows - 1) / kHeadRows);
+  switch (K) {
+    case 16: hipLaunchKernelGGL((head_fwd_kernel<NT, 1>), grid, dim3(256), 0, st, X, ldx, M, W1, b1, w2, b2, act, hid, Y); break;
+    case 32: hipLaunchKernelGGL((head_fwd_kernel<NT, 2>), grid, dim3(256), 0, st, X, ldx, M, W1, b1, w2, b2, act, hid, Y); break;
+    case 48: hipLaunchKernelGGL((head_fwd_kernel<NT, 3>), grid, dim3(256), 0, st, X, ldx, M, W1, b1, w2, b2, act, hid, Y); break;
+    default: hipLaunchKernelGGL((head_fwd_kernel<NT, 4>), grid, dim3(256), 0, st, X, ldx, M, W1, b1, w2, b2, act, hid, Y); break;
+  }
   SGG_RETURN_LAUNCH("sgg_head_fwd");
 }
 

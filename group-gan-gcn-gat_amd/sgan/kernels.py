@@ -447,7 +447,7 @@ class _Head(torch.autograd.Function):
                                      act, N.ptr(hid), N.ptr(y), N.stream_ptr()), "sgg_head_fwd")
         launch()
         if timer.active and M > 0:
-            timer.add("sgg::head_fwd_kernel<%d>" % (N1 // 16), (M, Kd, N1), 2.0 * M * N1 * (Kd + 1),
+            timer.add("sgg::head_fwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1), 2.0 * M * N1 * (Kd + 1),
                       4.0 * (M * Kd + N1 * Kd + M * N1 + M), launch)
         ctx.act = act
         ctx.save_for_backward(x, W1, W2, hid, y)

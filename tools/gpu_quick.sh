@@ -7,7 +7,7 @@ tag=$1
 if [ -n "$2" ]; then K=(-k "$2"); else K=(); fi
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread "${K[@]}" > gpurun_out/q_${tag}_tests.log 2>&1 || { echo TESTS_FAIL; tail -40 gpurun_out/q_${tag}_tests.log; exit 1; }
 tail -2 gpurun_out/q_${tag}_tests.log
-timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-scaling-reference --no-real-data > gpurun_out/q_${tag}_bench.json 2> gpurun_out/q_${tag}_bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/q_${tag}_bench.err; exit 1; }
+SGG_BENCH_TABLE=gpurun_out/q_${tag}_table.txt timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-scaling-reference --no-real-data > gpurun_out/q_${tag}_bench.json 2> gpurun_out/q_${tag}_bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/q_${tag}_bench.err; exit 1; }
 python - gpurun_out/q_${tag}_bench.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
