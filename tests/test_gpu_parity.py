@@ -361,6 +361,34 @@ def test_fused_lstm_vs_oracle(H, T, decoder, B):
         close(q.grad, p.grad.numpy(), rtol=1e-4, floor=1e-6, what="lstm d" + k)
 
 
+@pytest.mark.parametrize("T,decoder,B", [(12, True, 25600), (8, False, 4133), (12, True, 4099)])
+def test_no_grad_rollout_mfma_vs_oracle(T, decoder, B):
+    """The no-grad batch-MFMA forward (lstm_fwd_mfma_kernel: the best-of-20
+    decoder rollout of the training step, 25,600 sequences) against the
+    oracle's modules."""
+    from oracle import sgan_oracle as O
+    from sgan import models as M
+    H = 32
+    torch.manual_seed(T + B)
+    if decoder:
+        ref, mod = O.Decoder(T, 16, H, 64, 1, False), M.Decoder(T, 16, H, 64, 1, False)
+    else:
+        ref, mod = O.Encoder(16, H), M.Encoder(16, H)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(DEV)
+    with torch.no_grad():
+        if decoder:
+            last_pos, last_rel = torch.randn(B, 2), torch.randn(B, 2) * 0.3
+            h0, c0 = torch.randn(1, B, H) * 0.5, torch.zeros(1, B, H)
+            y_ref, h_ref = ref(last_pos, last_rel, (h0, c0), None)
+            y, h = mod(last_pos.to(DEV), last_rel.to(DEV), (h0.to(DEV), c0.to(DEV)), None)
+            close(y, y_ref.numpy(), rtol=1e-5, what="rollout rel")
+            close(h, h_ref.numpy(), rtol=1e-5, what="rollout h_T")
+        else:
+            rel = torch.randn(T, B, 2) * 0.3
+            close(mod(rel.to(DEV)), ref(rel).numpy(), rtol=1e-5, what="encoder h")
+
+
 @pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (32, 12, True, 37), (16, 5, True, 21),
                                             (48, 12, True, 37), (64, 3, True, 37), (48, 20, False, 2085)])
 def test_fused_lstm_other_families(H, T, decoder, B, monkeypatch):
