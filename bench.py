@@ -308,6 +308,8 @@ def main():
     ap.add_argument("--pmc-target", type=int, default=0,
                     help="after timing, re-issue the dominant kernel's main launch this many times (the LAST "
                          "dispatches of that kernel in a rocprofv3 --pmc run; tools/pmc_traffic.py)")
+    ap.add_argument("--pmc-kernel", default="",
+                    help="with --pmc-target: re-issue this kernel's main launch (default: the dominant one here)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -353,7 +355,10 @@ def main():
     agg = kernel_table(timed, n_it)
     pmc_target = None
     if args.pmc_target > 0 and rank == 0:
-        name, a = max(agg.items(), key=lambda kv: kv[1]["us_per_iter"])
+        if args.pmc_kernel and args.pmc_kernel in agg:   # the roofline kernel of the graphed run
+            name, a = args.pmc_kernel, agg[args.pmc_kernel]
+        else:
+            name, a = max(agg.items(), key=lambda kv: kv[1]["us_per_iter"])
         key = max(a["shapes"], key=lambda s: s[2] * s[1]["ms"])[0]
         fn = next(r[4] for r in recs if r[1] == key)
         for _ in range(args.pmc_target):

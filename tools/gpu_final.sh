@@ -16,6 +16,7 @@ timeout -k 10 400 python bench.py --steps 100 --warmup 10 > gpurun_out/f_bench.j
 cat gpurun_out/f_bench.json
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/f_prof -o run -- python $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-scaling-reference --no-real-data > $R/gpurun_out/f_prof_bench.json 2> $R/gpurun_out/f_prof.err || { echo PROF_FAIL; tail -20 $R/gpurun_out/f_prof.err; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/f_pmc_fetch -o run -- python $R/bench.py --steps 2 --warmup 1 --graph 0 --no-cpu-baseline --no-scaling-reference --no-real-data --pmc-target 20 > $R/gpurun_out/f_pmc_fetch.json 2> $R/gpurun_out/f_pmc_fetch.log || { echo PMC_FETCH_FAIL; tail -20 $R/gpurun_out/f_pmc_fetch.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/f_pmc_write -o run -- python $R/bench.py --steps 2 --warmup 1 --graph 0 --no-cpu-baseline --no-scaling-reference --no-real-data --pmc-target 20 > $R/gpurun_out/f_pmc_write.json 2> $R/gpurun_out/f_pmc_write.log || { echo PMC_WRITE_FAIL; tail -20 $R/gpurun_out/f_pmc_write.log; exit 1; }
+RK=$(python -c "import json; print(json.loads(open('$R/gpurun_out/f_bench.json').read().strip().splitlines()[-1])['roofline']['kernel'])")
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/f_pmc_fetch -o run -- python $R/bench.py --steps 2 --warmup 1 --graph 0 --no-cpu-baseline --no-scaling-reference --no-real-data --pmc-target 20 --pmc-kernel "$RK" > $R/gpurun_out/f_pmc_fetch.json 2> $R/gpurun_out/f_pmc_fetch.log || { echo PMC_FETCH_FAIL; tail -20 $R/gpurun_out/f_pmc_fetch.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/f_pmc_write -o run -- python $R/bench.py --steps 2 --warmup 1 --graph 0 --no-cpu-baseline --no-scaling-reference --no-real-data --pmc-target 20 --pmc-kernel "$RK" > $R/gpurun_out/f_pmc_write.json 2> $R/gpurun_out/f_pmc_write.log || { echo PMC_WRITE_FAIL; tail -20 $R/gpurun_out/f_pmc_write.log; exit 1; }
 echo done
