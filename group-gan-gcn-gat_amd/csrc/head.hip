@@ -32,14 +32,26 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__
   const int c16 = lane & 15, q = lane >> 4;
   const int row0 = blockIdx.x * kHeadRows + wave * 16;
   const float* xr = X + (size_t)min(row0 + c16, M - 1) * ldx;
-  // every operand of the lane issued up front: one memory round trip
+  // every operand of the lane issued up front: one memory round trip.  The k
+  // order is permuted (k-step 4 m + i, lane quarter q <-> k = 16 m + 4 q + i),
+  // the same for both operands, so a lane's four k values of block m are one
+  // 16-byte load of X and of each W1 row (full 64-byte lines per instruction)
   float a[KS], b[KS][NT], bc[NT], wc[NT];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = 4 * s + q;
-    a[s] = xr[k];
+  for (int m = 0; m < KT; ++m) {
+    const float4 xv = *reinterpret_cast<const float4*>(xr + 16 * m + 4 * q);
+    a[4 * m] = xv.x;
+    a[4 * m + 1] = xv.y;
+    a[4 * m + 2] = xv.z;
+    a[4 * m + 3] = xv.w;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) b[s][t] = W1[(size_t)(16 * t + c16) * K + k];
+    for (int t = 0; t < NT; ++t) {
+      const float4 wv = *reinterpret_cast<const float4*>(W1 + (size_t)(16 * t + c16) * K + 16 * m + 4 * q);
+      b[4 * m][t] = wv.x;
+      b[4 * m + 1][t] = wv.y;
+      b[4 * m + 2][t] = wv.z;
+      b[4 * m + 3][t] = wv.w;
+    }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -217,6 +229,8 @@ extern "C" int sgg_head_fwd(const float* X, int ldx, int M, int K, int N1, const
   SGG_CHECK_ARG(X && W1 && b1 && w2 && b2 && hid && Y, "sgg_head_fwd: null pointer");
   SGG_CHECK_ARG(M >= 0 && sgg_head_ok(K, N1) && ldx >= K && act >= 0 && act <= 3,
                 "sgg_head_fwd: unsupported shape M=%d K=%d N1=%d ldx=%d act=%d", M, K, N1, ldx, act);
+  SGG_CHECK_ARG(((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W1)) & 15) == 0 && ldx % 4 == 0,
+                "sgg_head_fwd: X and W1 must be 16-byte aligned with ldx %% 4 == 0 (ldx=%d)", ldx);
   if (M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (N1) {

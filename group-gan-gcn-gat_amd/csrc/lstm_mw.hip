@@ -238,10 +238,25 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     // tiles in pairs (two independent accumulation chains); the next pair's
     // Wu fragments are in flight during the current pair's MFMAs
     float wa[2][KS], wn[2][KS];
+    // lane q's k values of unit block m, slot_unit(4 m + i, q) = 16 m + 4 q + i,
+    // are 4 consecutive floats: one 16-byte load per block (a full 64-byte line
+    // per row and wave instruction) when Wu's rows are 16-byte aligned
+    const bool vec = ((reinterpret_cast<uintptr_t>(Wu) | ((uintptr_t)ldwu * 4)) & 15) == 0;
     auto load_w = [&](int nt, float (&w)[KS]) {
       const float* wr = Wu + (size_t)(min(nt, ntile - 1) * 16 + c16) * ldwu;
+      if (vec) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) w[ks] = wr[slot_unit(ks, q)];
+        for (int m = 0; m < KS / 4; ++m) {
+          const float4 v = *reinterpret_cast<const float4*>(wr + 16 * m + 4 * q);
+          w[4 * m] = v.x;
+          w[4 * m + 1] = v.y;
+          w[4 * m + 2] = v.z;
+          w[4 * m + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) w[ks] = wr[slot_unit(ks, q)];
+      }
     };
     load_w(g, wa[0]);
     load_w(g + 4, wa[1]);

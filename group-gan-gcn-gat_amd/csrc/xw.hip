@@ -45,17 +45,37 @@ struct XwFrag {
     if (STAGED) return ws[ncl[t] * kp + k];
     return TRANS_W ? W[(size_t)ncl[t] * ldw + k] : W[(size_t)k * ldw + ncl[t]];
   }
+  // k order within a 16-deep chunk is permuted: k-step s of lane quarter kq
+  // takes k = kb + 4 kq + s (the same for both operands), so a lane's four
+  // A values of a chunk are one 16-byte load (full 64-byte lines per wave
+  // instruction instead of 16-byte pieces of 16 lines)
+  bool vec;   // X (and the mask) rows 16-byte aligned
   __device__ __forceinline__ void load_a(int kb, float (&aa)[kXwS4]) const {
     if (kb + kXwKC <= kend) {
+      if (vec) {
+        const float4 v = *reinterpret_cast<const float4*>(xrow + kb + 4 * kq);
+        aa[0] = v.x;
+        aa[1] = v.y;
+        aa[2] = v.z;
+        aa[3] = v.w;
+        if (mrow) {
+          const float4 mv = *reinterpret_cast<const float4*>(mrow + kb + 4 * kq);
+          aa[0] = keep_if(aa[0], mv.x > 0.f);
+          aa[1] = keep_if(aa[1], mv.y > 0.f);
+          aa[2] = keep_if(aa[2], mv.z > 0.f);
+          aa[3] = keep_if(aa[3], mv.w > 0.f);
+        }
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < kXwS4; ++s) {
-        const int k = kb + 4 * s + kq;
+        const int k = kb + 4 * kq + s;
         aa[s] = mrow ? keep_if(xrow[k], mrow[k] > 0.f) : xrow[k];
       }
     } else {
 #pragma unroll
       for (int s = 0; s < kXwS4; ++s) {
-        const int k = kb + 4 * s + kq;
+        const int k = kb + 4 * kq + s;
         const int kc = min(k, kend - 1);
         aa[s] = keep_if(xrow[kc], k < kend && (!mrow || mrow[kc] > 0.f));
       }
@@ -64,7 +84,7 @@ struct XwFrag {
   __device__ __forceinline__ void load_b(int kb, float (&bb)[kXwS4][4]) const {
 #pragma unroll
     for (int s = 0; s < kXwS4; ++s) {
-      const int kc = min(kb + 4 * s + kq, kend - 1);   // past kend the A operand is zero
+      const int kc = min(kb + 4 * kq + s, kend - 1);   // past kend the A operand is zero
 #pragma unroll
       for (int t = 0; t < 4; ++t) bb[s][t] = wval(t, kc);
     }
@@ -137,6 +157,8 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   f.kp = K + 1;
   f.kend = K;
   f.kq = kq;
+  f.vec = ((reinterpret_cast<uintptr_t>(X) | (uintptr_t)ldx * 4 |
+            (Xmask ? (reinterpret_cast<uintptr_t>(Xmask) | (uintptr_t)ldm * 4) : 0)) & 15) == 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) f.ncl[t] = STAGED ? min(16 * t + ar, N - 1 - col0) : min(col0 + 16 * t + ar, N - 1);
   // the lane's four bias values, fetched up front (not a memory round trip in the epilogue)
@@ -213,6 +235,8 @@ __global__ void __launch_bounds__(256) xw_splitk_kernel(const float* __restrict_
   f.kp = 0;
   f.kend = min(K, (wave + 1) * span);
   f.kq = kq;
+  f.vec = ((reinterpret_cast<uintptr_t>(X) | (uintptr_t)ldx * 4 |
+            (Xmask ? (reinterpret_cast<uintptr_t>(Xmask) | (uintptr_t)ldm * 4) : 0)) & 15) == 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) f.ncl[t] = min(col0 + 16 * t + ar, N - 1);
   floatx4 acc[4];

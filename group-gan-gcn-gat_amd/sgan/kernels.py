@@ -435,6 +435,8 @@ class _Head(torch.autograd.Function):
     def forward(ctx, x, W1, b1, W2, b2, act):
         lib = _lib()
         x = _rows(x, "x")
+        if x.data_ptr() % 16 or x.stride(0) % 4:   # the kernel reads 16-byte blocks of a row
+            x = x.contiguous()
         M, Kd = x.shape
         N1 = W1.shape[0]
         W1, W2 = W1.contiguous(), W2.contiguous()

@@ -284,7 +284,7 @@ int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* folds, int n
  * act: bit 0 act1 = ReLU, bit 1 act2 = ReLU.  W1: N1 x K contiguous (nn.Linear),
  * w2: N1, b1: N1, b2: 1 (device).  hid is written for the backward.  One
  * launch: the hidden layer on v_mfma_f32_16x16x4_f32, the N1 -> 1 layer from
- * the accumulator tiles.  Shapes: sgg_head_ok(K, N1) (K in {16, 32, 48, 64},
+ * the accumulator tiles.  X and W1 16-byte aligned, ldx % 4 == 0.  Shapes: sgg_head_ok(K, N1) (K in {16, 32, 48, 64},
  * N1 in {16, 32, 64}).
  * Backward: dX (row stride lddx) and, when wslab != NULL, one slab row per 64
  * rows ((M + 63) / 64 rows of sgg_head_slab_cols(K, N1) floats):
