@@ -112,17 +112,30 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
   for (int s = 0; s < N1 / 4; ++s)
 #pragma unroll
     for (int t = 0; t < KT; ++t) wb[s][t] = W1[(size_t)(4 * s + q) * K + 16 * t + c16];
-  // stage dhid (rows past M are zero: they add nothing to the weight sums)
-  for (int e = tid; e < kHeadRows * N1; e += 256) {
-    const int r = e / N1, n = e - r * N1;
-    const int m = rb + r;
-    const int mc = min(m, M - 1);
-    const float y = Y[mc], dy = dY[mc];
-    const float g = (m < M && (!(act & 2) || y > 0.f)) ? dy : 0.f;
-    const float h = hid[(size_t)mc * N1 + n];
-    dh[r][n] = (!(act & 1) || h > 0.f) ? g * w2[n] : 0.f;
-    hg[r][n] = g * h;
-    if (n == 0) g2s[r] = g;
+  // stage dhid (rows past M are zero: they add nothing to the weight sums):
+  // thread = (column n, row phase), every global load of the thread issued
+  // before any is used (one memory round trip)
+  {
+    constexpr int RPT = kHeadRows * N1 / 256;   // rows per thread
+    constexpr int RS = 256 / N1;                // row stride
+    const int n = tid % N1, r0 = tid / N1;
+    const float wn = w2[n];
+    float hv[RPT], yv[RPT], dyv[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int mc = min(rb + r0 + RS * i, M - 1);
+      hv[i] = hid[(size_t)mc * N1 + n];
+      yv[i] = Y[mc];
+      dyv[i] = dY[mc];
+    }
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = r0 + RS * i, m = rb + r;
+      const float g = (m < M && (!(act & 2) || yv[i] > 0.f)) ? dyv[i] : 0.f;
+      dh[r][n] = (!(act & 1) || hv[i] > 0.f) ? g * wn : 0.f;
+      hg[r][n] = g * hv[i];
+      if (n == 0) g2s[r] = g;
+    }
   }
   __syncthreads();
   // dX (this wave's 16 rows) = dhid W1: A[row][k = n] from LDS, B[n][col] = W1[n][col]

@@ -115,12 +115,19 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
   const int pc = ped < B ? ped : B - 1;   // clamped: every load and store unconditional and in bounds
 
   // [W_hh,g | A_g b_g] in registers, W_hh's columns in the permuted k order
+  // (slot_unit(4 m + i, q) = 16 m + 4 q + i: one 16-byte load per block m)
   float w[MU][KS + 1], ak0[MU], ak1[MU];
 #pragma unroll
   for (int mu = 0; mu < MU; ++mu) {
     const int row = g * H + 16 * mu + c16;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) w[mu][ks] = Whh[row * H + slot_unit(ks, q)];
+    for (int m = 0; m < KS / 4; ++m) {
+      const float4 v = *reinterpret_cast<const float4*>(Whh + row * H + 16 * m + 4 * q);
+      w[mu][4 * m] = v.x;
+      w[mu][4 * m + 1] = v.y;
+      w[mu][4 * m + 2] = v.z;
+      w[mu][4 * m + 3] = v.w;
+    }
     ak0[mu] = A[2 * row];
     ak1[mu] = A[2 * row + 1];
     w[mu][KS] = q == 0 ? ak0[mu] : q == 1 ? ak1[mu] : q == 2 ? bias[row] : 0.f;
