@@ -853,9 +853,12 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     float* v = Wh + NP * PDY;
     {
       const float* dyg = p.dy + (size_t)o * p.lddy;
+      const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
       for (int e = tid; e < n * FE; e += blockDim.x) {
         const int i = e / FE, k = e - i * FE;
-        dy[i * PDY + k] = dyg[(size_t)i * p.lddy + k];
+        float v = dyg[(size_t)i * p.lddy + k];
+        for (int c = 1; c < ncp; ++c) v += dyg[(size_t)c * p.dy_cstride + (size_t)i * p.lddy + k];
+        dy[i * PDY + k] = v;
       }
       for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
         const int i = e / (2 * FO), c = e - i * 2 * FO;

@@ -32,7 +32,7 @@ class GatEncArgs(ctypes.Structure):
     _fields_ = [("X", _p), ("ldx", _i), ("labels", _p), ("scene_off", _p), ("S", _i), ("np", _i), ("nh", _i),
                 ("alpha", _f), ("w", GatEncWeights), ("y", _p), ("ldy", _i), ("dy", _p), ("lddy", _i), ("dX", _p),
                 ("lddx", _i), ("slab", _p), ("saved", _p), ("X2", _p), ("ldx2", _i), ("kx1", _i),
-                ("dX2", _p), ("lddx2", _i)]
+                ("dX2", _p), ("lddx2", _i), ("dy_copies", _i), ("dy_cstride", _i)]
 
 
 _pargs = ctypes.POINTER(GatEncArgs)

@@ -777,6 +777,24 @@ class _Pool(torch.autograd.Function):
         return dh, None, dW1, dWe, dbe, dc, dW2, db2, None, None, None
 
 
+class CopiesLink:
+    """Carries the decoder-initial-state gradient of the best-of-k copies
+    (decoder_init's backward) to the GAT encoder's backward, which sums the
+    copies while loading dy (SggGatEncArgs.dy_copies) -- no separate sum
+    launch.  decoder_init returns copy 0's rows (a view into the same
+    buffer) as the autograd gradient."""
+
+    def __init__(self):
+        self.pending = None
+
+    def put(self, base, copies, cstride, ld):
+        self.pending = (base, copies, cstride, ld)
+
+    def take(self):
+        p, self.pending = self.pending, None
+        return p
+
+
 class GradLink:
     """Carries one input gradient from a backward to a LATER backward of the
     same tensor's other consumer, which adds it inside its own launch: the
@@ -891,9 +909,10 @@ class _GatEnc(torch.autograd.Function):
     the inter GAT, out_embedding weight, bias -- the slab order of sgg.h."""
 
     @staticmethod
-    def forward(ctx, x, labels, scenes, nh, alpha, x2, link, *params):
+    def forward(ctx, x, labels, scenes, nh, alpha, x2, link, dy_link, *params):
         lib = _lib()
         ctx.link = link
+        ctx.dy_link = dy_link
         x = _rows(x, "x")
         B = x.shape[0]
         if x2 is not None:
@@ -924,14 +943,25 @@ class _GatEnc(torch.autograd.Function):
         lib = _lib()
         x, x2, saved, *ps = ctx.saved_tensors
         labels, scenes, nh, alpha = ctx.meta
-        dy = _rows(dy, "dy")
         B = x.shape[0]
+        pend = ctx.dy_link.take() if ctx.dy_link is not None else None
+        copies = 1
+        if pend is not None:
+            base, copies, cstride, ld = pend
+            if dy.data_ptr() == base.data_ptr() and dy.stride(0) == ld:
+                dy = base   # rows 0 .. B of copy 0; the kernel adds the other copies
+            else:           # autograd summed in another consumer's gradient: add the copies here
+                dy = dy + sum(base.view(copies, B, ld)[c, :, :dy.shape[1]] for c in range(1, copies))
+                copies = 1
+        dy = _rows(dy, "dy")
         P = lib.sgg_gatenc_param_size(nh)
         dx = torch.empty(B, x.shape[1], device=x.device, dtype=torch.float32)
         dx2 = torch.empty(B, x2.shape[1], device=x.device, dtype=torch.float32) if x2 is not None else None
         slab = torch.empty(max(scenes.S, 1), P, device=x.device, dtype=torch.float32)
         a = _gatenc_args(x, labels, scenes, nh, alpha, ps, x2)
         a.dy, a.lddy = N.ptr(dy), dy.stride(0)
+        if copies > 1:
+            a.dy_copies, a.dy_cstride = copies, cstride
         a.dX, a.lddx = N.ptr(dx), dx.shape[1]
         if dx2 is not None:
             a.dX2, a.lddx2 = N.ptr(dx2), dx2.shape[1]
@@ -954,7 +984,7 @@ class _GatEnc(torch.autograd.Function):
         if ctx.link is not None and ctx.needs_input_grad[0]:
             ctx.link.put(dx)   # added by the pooling backward (the other consumer of x), which runs next
             dx = None
-        return (dx, None, None, None, None, dx2, None) + tuple(grads)
+        return (dx, None, None, None, None, dx2, None, None) + tuple(grads)
 
 
 def _gatenc_flops(scenes, nh):
@@ -1007,7 +1037,11 @@ def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None, link=None):
     link: a GradLink that takes the gradient of x instead of returning it
     (x's other consumer, the pooling net, adds it in its own backward)."""
     lab = _req(labels, "labels").contiguous().view(-1)
-    return _GatEnc.apply(x, lab, scenes, nh, alpha, x2, link, *params)
+    dl = CopiesLink() if torch.is_grad_enabled() else None
+    y = _GatEnc.apply(x, lab, scenes, nh, alpha, x2, link, dl, *params)
+    if dl is not None:
+        y._sgg_copies_link = dl   # found by decoder_init (its only consumer in the generator)
+    return y
 
 
 class _SegNorm(torch.autograd.Function):
@@ -1477,6 +1511,7 @@ def traj_cat(head, a, b=None, pos0=None):
 class _DecoderInit(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cvec, z, best, first_k, copies, scenes, last_rel):
+        ctx.dy_link = getattr(cvec, "_sgg_copies_link", None)
         cvec = _rows(cvec, "ctx")
         B, Dc = cvec.shape
         nz = z.shape[-1] if z is not None else 0
@@ -1496,6 +1531,10 @@ class _DecoderInit(torch.autograd.Function):
     def backward(ctx, dh0, _drel0):
         copies, B, Dc = ctx.dims
         d = dh0.view(copies, B, -1)[:, :, :Dc]
+        if copies > 1 and ctx.dy_link is not None and dh0.is_contiguous():
+            # the GAT encoder's backward sums the copies while loading dy
+            ctx.dy_link.put(dh0, copies, B * dh0.shape[1], dh0.shape[1])
+            return d[0], None, None, None, None, None, None
         return (d[0] if copies == 1 else d.sum(0)), None, None, None, None, None, None
 
 

@@ -651,12 +651,16 @@ class TrajectoryDiscriminator(nn.Module):
         self.real_classifier = make_mlp([h_dim, mlp_dim, 1], activation=activation, batch_norm=batch_norm,
                                         dropout=dropout)
 
+    def fold_specs(self):
+        """The discriminator's input-embedding folds (encoder, pooling)."""
+        specs = [K.lstm_fold_spec(self.encoder.encoder, self.encoder.spatial_embedding)]
+        if self.d_type != "local":
+            specs.append(K.pool_fold_spec(self.pool_net))
+        return specs
+
     def forward(self, traj, traj_rel, seq_start_end=None, *, scenes=None):
         if self.encoder.num_layers == 1:   # encoder + pooling folds in one launch (kernels.prefold)
-            specs = [K.lstm_fold_spec(self.encoder.encoder, self.encoder.spatial_embedding)]
-            if self.d_type != "local":
-                specs.append(K.pool_fold_spec(self.pool_net))
-            K.prefold(specs)
+            K.prefold(self.fold_specs())
         if self.d_type != "local" and self.encoder.num_layers == 1 and self.pool_net.fused_ok():
             # the pooling net's first layer (h half) in the encoder kernel's epilogue
             final_h, U = self.encoder(traj_rel, proj_u=K.pool_u_spec(self.pool_net))

@@ -126,6 +126,7 @@ class KernelOps:
     bce_pair = staticmethod(K.bce_pair)
     bce_pair_total = staticmethod(K.bce_pair_total)
     split2 = staticmethod(K.split2)
+    prefold = staticmethod(K.prefold)
     one = staticmethod(lambda device: K.const(1.0, device))
     # clip_grad_norm_ + Adam in two launches (sgg_adam_step; torch's state
     # layout, capturable): optimizer(params, lr).step(max_norm)
@@ -192,6 +193,12 @@ class GanTrainer:
         B_global = B_global or sc.B
         s0 = shard[0]
         z = inputs.z_d if inputs is not None else self._noise(S_global, s0, s0 + sc.S)
+        prefold = getattr(self.ops, "prefold", None)
+        if prefold is not None and hasattr(self.G, "fold_specs") and hasattr(self.D, "fold_specs") \
+                and self.G.num_layers == 1 and self.D.encoder.num_layers == 1:
+            # G's folds (stale since the last G-step) and D's (since the last
+            # D-step) in ONE launch; the forwards below find them cached
+            prefold(self.G.fold_specs() + self.D.fold_specs())
         with torch.no_grad():
             fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
         # D reads traj[0] (the start positions, models.py:989) and traj_rel

@@ -484,6 +484,11 @@ typedef struct {
   int kx1;
   float* dX2;
   int lddx2;
+  /* backward: dy of the scene rows is the sum of dy_copies blocks dy_cstride
+   * floats apart (the decoder's initial-state gradient of the best-of-k
+   * copies, summed here instead of in a separate launch); 0 or 1: one block */
+  int dy_copies;
+  int dy_cstride;
 } SggGatEncArgs;
 
 int sgg_gatenc_param_size(int nh);
