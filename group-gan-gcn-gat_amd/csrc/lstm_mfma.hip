@@ -29,6 +29,12 @@ namespace {
 // step are the VALU side of this kernel
 __device__ __forceinline__ float sigm_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_fast(float x) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f); }
+// the same activations of a pre-activation the weights already scaled by
+// -log2(e) (sigmoid) or -2 log2(e) (tanh): v_exp_f32 takes it directly (the
+// scale rides in W_ext, loaded once; one VALU multiply less per gate value)
+constexpr float kNegLog2e = -1.4426950408889634f;
+__device__ __forceinline__ float sigm_pre(float y) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y)); }
+__device__ __forceinline__ float tanh_pre(float y) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y)), -1.f); }
 
 template <int H>
 __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
@@ -55,6 +61,10 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
 #pragma unroll
     for (int ks = 0; ks < KSH; ++ks) w[mt][ks] = Whh[row * H + 16 * (ks >> 2) + 4 * q + (ks & 3)];
     w[mt][KSH] = q == 0 ? A[2 * row] : q == 1 ? A[2 * row + 1] : q == 2 ? bias[row] : 0.f;
+    // gate of tile mt: i, f, g, o blocks of MU tiles; g (tanh) takes -2 log2(e)
+    const float sc = (mt / MU == 2 ? 2.f : 1.f) * kNegLog2e;
+#pragma unroll
+    for (int ks = 0; ks <= KSH; ++ks) w[mt][ks] *= sc;
   }
   float wp0[NU], wp1[NU];
 #pragma unroll
@@ -107,10 +117,10 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
       float ai[4], af[4], ag[4], ao[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        ai[r] = sigm_fast(acc[mu][r]);
-        af[r] = sigm_fast(acc[MU + mu][r]);
-        ag[r] = tanh_fast(acc[2 * MU + mu][r]);
-        ao[r] = sigm_fast(acc[3 * MU + mu][r]);
+        ai[r] = sigm_pre(acc[mu][r]);
+        af[r] = sigm_pre(acc[MU + mu][r]);
+        ag[r] = tanh_pre(acc[2 * MU + mu][r]);
+        ao[r] = sigm_pre(acc[3 * MU + mu][r]);
         const int k = 4 * mu + r;
         c[k] = fmaf(af[r], c[k], ai[r] * ag[r]);
         h[k] = ao[r] * tanh_fast(c[k]);
