@@ -22,6 +22,13 @@ namespace {
 
 constexpr int kHeadRows = 64;   // rows per workgroup (4 waves x 16)
 
+// d bce / d x, the expression of loss.hip's bce_grad (torch autograd's form)
+__device__ __forceinline__ float bce_grad(float x, float y) {
+  const float e = expf(-fabsf(x));
+  const float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+  return (x >= 0.f ? 1.f : 0.f) - y - sg * (e / (1.f + e));
+}
+
 template <int NT, int KT>   // NT = N1 / 16 hidden column tiles, K = 16 KT inputs
 __global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__ X, int ldx, int M,
                                                        const float* __restrict__ W1, const float* __restrict__ b1,
@@ -95,7 +102,9 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
                                                        const float* __restrict__ W1, const float* __restrict__ w2,
                                                        const float* __restrict__ hid, const float* __restrict__ Y,
                                                        const float* __restrict__ dY, int act,
-                                                       float* __restrict__ dX, int lddx, float* __restrict__ wslab) {
+                                                       float* __restrict__ dX, int lddx, float* __restrict__ wslab,
+                                                       const float* __restrict__ bce_g, const float* __restrict__ bce_ya,
+                                                       const float* __restrict__ bce_yb, int bce_split, float bce_w) {
   constexpr int N1 = 16 * NT, K = 16 * KT;
   constexpr int DP = N1 + 4;   // dhid row pitch
   __shared__ float dh[kHeadRows][DP];
@@ -126,7 +135,17 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
       const int mc = min(rb + r0 + RS * i, M - 1);
       hv[i] = hid[(size_t)mc * N1 + n];
       yv[i] = Y[mc];
-      dyv[i] = dY[mc];
+      dyv[i] = bce_g ? 0.f : dY[mc];
+    }
+    if (bce_g) {   // dY of the BCE loss on Y (bce_bwd_kernel's expression, loss.hip)
+      const float gw = *bce_g * bce_w, ya = *bce_ya, yb = *bce_yb;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int mc = min(rb + r0 + RS * i, M - 1);
+        const bool first = mc < bce_split;
+        const float cnt = first ? (float)bce_split : (float)(M - bce_split);
+        dyv[i] = (gw / cnt) * bce_grad(yv[i], first ? ya : yb);
+      }
     }
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
@@ -206,22 +225,29 @@ int launch_fwd_nt(const float* X, int ldx, int M, int K, const float* W1, const 
   SGG_RETURN_LAUNCH("sgg_head_fwd");
 }
 
+struct BceArgs {
+  const float *g, *ya, *yb;
+  int split;
+  float w;
+};
+
 template <int NT, int KT>
 int launch_bwd_nt(const float* X, int ldx, int M, const float* W1, const float* w2, const float* hid, const float* Y,
-                  const float* dY, int act, float* dX, int lddx, float* wslab, hipStream_t st) {
+                  const float* dY, int act, float* dX, int lddx, float* wslab, const BceArgs& bc, hipStream_t st) {
   hipLaunchKernelGGL((head_bwd_kernel<NT, KT>), dim3((M + kHeadRows - 1) / kHeadRows), dim3(256), 0, st, X, ldx, M,
-                     W1, w2, hid, Y, dY, act, dX, lddx, wslab);
+                     W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc.g, bc.ya, bc.yb, bc.split, bc.w);
   SGG_RETURN_LAUNCH("sgg_head_bwd");
 }
 
 template <int NT>
 int launch_bwd_k(const float* X, int ldx, int M, int K, const float* W1, const float* w2, const float* hid,
-                 const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, hipStream_t st) {
+                 const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, const BceArgs& bc,
+                 hipStream_t st) {
   switch (K) {
-    case 16: return launch_bwd_nt<NT, 1>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
-    case 32: return launch_bwd_nt<NT, 2>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
-    case 48: return launch_bwd_nt<NT, 3>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
-    default: return launch_bwd_nt<NT, 4>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+    case 16: return launch_bwd_nt<NT, 1>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc, st);
+    case 32: return launch_bwd_nt<NT, 2>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc, st);
+    case 48: return launch_bwd_nt<NT, 3>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc, st);
+    default: return launch_bwd_nt<NT, 4>(X, ldx, M, W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc, st);
   }
 }
 
@@ -255,15 +281,19 @@ extern "C" int sgg_head_fwd(const float* X, int ldx, int M, int K, int N1, const
 
 extern "C" int sgg_head_bwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* w2,
                             const float* hid, const float* Y, const float* dY, int act, float* dX, int lddx,
-                            float* wslab, void* stream) {
-  SGG_CHECK_ARG(X && W1 && w2 && hid && Y && dY && dX, "sgg_head_bwd: null pointer");
+                            float* wslab, const float* bce_g, const float* bce_ya, const float* bce_yb,
+                            int bce_split, float bce_w, void* stream) {
+  SGG_CHECK_ARG(X && W1 && w2 && hid && Y && (dY || bce_g) && dX, "sgg_head_bwd: null pointer");
+  SGG_CHECK_ARG(!bce_g || (bce_ya && bce_yb && bce_split >= 0 && bce_split <= M),
+                "sgg_head_bwd: BCE targets / split (split=%d, M=%d)", bce_split, M);
+  const BceArgs bc{bce_g, bce_ya, bce_yb, bce_split, bce_w};
   SGG_CHECK_ARG(M >= 0 && sgg_head_ok(K, N1) && ldx >= K && lddx >= K && act >= 0 && act <= 3,
                 "sgg_head_bwd: unsupported shape M=%d K=%d N1=%d", M, K, N1);
   if (M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (N1) {
-    case 16: return launch_bwd_k<1>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
-    case 32: return launch_bwd_k<2>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
-    default: return launch_bwd_k<4>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, st);
+    case 16: return launch_bwd_k<1>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc, st);
+    case 32: return launch_bwd_k<2>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc, st);
+    default: return launch_bwd_k<4>(X, ldx, M, K, W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc, st);
   }
 }

@@ -87,7 +87,7 @@ SIGNATURES = {
     "sgg_head_ok": (_i, [_i, _i]),
     "sgg_head_slab_cols": (_i, [_i, _i]),
     "sgg_head_fwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p]),
-    "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p]),
+    "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _p, _i, _f, _p]),
     "sgg_xtw_partial": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
     "sgg_adam_parts": (_i, [ctypes.c_longlong]),

@@ -430,9 +430,28 @@ def head_ok(seq):
     return l1, l2, int(relu1) | (2 * int(relu2))
 
 
+class BceLink:
+    """Carries the BCE loss's backward arguments (upstream gradient, targets,
+    split, weight) from _Bce / _BceTotal to the head backward, which forms the
+    scores' gradient itself (sgg_head_bwd's bce_* arguments): one launch fewer
+    per discriminator loss.  The BCE backward returns an unwritten placeholder
+    as the scores' gradient; the head backward checks it received exactly that
+    tensor (the scores had no other consumer)."""
+
+    def __init__(self):
+        self.pending = None
+
+    def put(self, g, ya, yb, split, w, placeholder):
+        self.pending = (g, ya, yb, split, w, placeholder)
+
+    def take(self):
+        p, self.pending = self.pending, None
+        return p
+
+
 class _Head(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, act):
+    def forward(ctx, x, W1, b1, W2, b2, act, bce_link=None):
         lib = _lib()
         x = _rows(x, "x")
         if x.data_ptr() % 16 or x.stride(0) % 4:   # the kernel reads 16-byte blocks of a row
@@ -452,6 +471,7 @@ class _Head(torch.autograd.Function):
             timer.add("sgg::head_fwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1), 2.0 * M * N1 * (Kd + 1),
                       4.0 * (M * Kd + N1 * Kd + M * N1 + M), launch)
         ctx.act = act
+        ctx.bce_link = bce_link
         ctx.save_for_backward(x, W1, W2, hid, y)
         return y
 
@@ -462,24 +482,36 @@ class _Head(torch.autograd.Function):
         need = ctx.needs_input_grad
         M, Kd = x.shape
         N1 = W1.shape[0]
-        dy = dy.contiguous()
+        pend = ctx.bce_link.take() if ctx.bce_link is not None else None
+        bce = None
+        if pend is not None:
+            g, ya, yb, split, w, ph = pend
+            if dy.data_ptr() != ph.data_ptr():
+                raise N.NativeError("fused head + BCE backward: the scores have a consumer besides the BCE loss "
+                                    "(set SGG_HEAD_BCE=0)")
+            bce = (g.contiguous(), ya, yb, int(split), float(w))
+        else:
+            dy = dy.contiguous()
         dx = torch.empty(M, Kd, device=x.device, dtype=torch.float32)
         wgrad = any(need[1:5])
         P = lib.sgg_head_slab_cols(Kd, N1)
         rows = (M + 63) // 64
         slab = torch.empty(max(rows, 1), P, device=x.device, dtype=torch.float32) if wgrad else None
 
+        bg, bya, byb, bsp, bw = (N.ptr(bce[0]), N.ptr(bce[1]), N.ptr(bce[2]), bce[3], bce[4]) if bce else \
+            (None, None, None, 0, 0.0)
+
         def launch():
             N.check(lib.sgg_head_bwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(W2), N.ptr(hid), N.ptr(y),
-                                     N.ptr(dy), ctx.act, N.ptr(dx), dx.stride(0), N.ptr(slab), N.stream_ptr()),
-                    "sgg_head_bwd")
+                                     None if bce else N.ptr(dy), ctx.act, N.ptr(dx), dx.stride(0), N.ptr(slab),
+                                     bg, bya, byb, bsp, bw, N.stream_ptr()), "sgg_head_bwd")
         launch()
         if timer.active and M > 0:
             timer.add("sgg::head_bwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1, wgrad),
                       2.0 * M * N1 * Kd * (2 if wgrad else 1),
                       4.0 * (M * Kd * (3 if wgrad else 2) + 2 * M * N1 + (slab.numel() if wgrad else 0)), launch)
         if not wgrad:
-            return dx, None, None, None, None, None
+            return dx, None, None, None, None, None, None
         dW1 = torch.empty(N1, Kd, device=x.device, dtype=torch.float32)
         db1 = torch.empty(N1, device=x.device, dtype=torch.float32)
         dW2 = torch.empty(1, N1, device=x.device, dtype=torch.float32)
@@ -494,13 +526,22 @@ class _Head(torch.autograd.Function):
             gf.rowsum(slab, rows, P, N1 * Kd + N1, N1, dW2)
             gf.rowsum(slab, rows, P, N1 * Kd + 2 * N1, 1, db2)
             gf.run()
-        return dx, dW1, db1, dW2, db2, None
+        return dx, dW1, db1, dW2, db2, None, None
+
+
+HEAD_BCE = os.environ.get("SGG_HEAD_BCE", "1") != "0"
 
 
 def head(x, spec):
-    """real_classifier forward through the fused head (spec = head_ok(seq))."""
+    """real_classifier forward through the fused head (spec = head_ok(seq)).
+    With autograd on, the scores carry a BceLink: a K.bce_pair /
+    K.bce_pair_total on them hands its backward to the head's launch."""
     l1, l2, act = spec
-    return _Head.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, act)
+    link = BceLink() if (HEAD_BCE and torch.is_grad_enabled()) else None
+    y = _Head.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, act, link)
+    if link is not None:
+        y._sgg_bce_link = link
+    return y
 
 
 # ---------------------------------------------------------------------------
@@ -1370,6 +1411,7 @@ class _Bce(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, ya, yb, split, w):
         ctx.shape = x.shape
+        ctx.bce_link = getattr(x, "_sgg_bce_link", None)
         x = _req(x, "scores").contiguous().view(-1)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss), None,
@@ -1382,6 +1424,10 @@ class _Bce(torch.autograd.Function):
     def backward(ctx, g):
         x, ya, yb = ctx.saved_tensors
         split, w = ctx.meta
+        if ctx.bce_link is not None:   # the head backward forms the scores' gradient (BceLink)
+            ph = torch.empty(ctx.shape, device=x.device, dtype=torch.float32)
+            ctx.bce_link.put(g, ya, yb, split, w, ph)
+            return ph, None, None, None, None
         g = g.contiguous()
         dx = torch.empty_like(x)
         N.check(_lib().sgg_bce_bwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), w, N.ptr(g), N.ptr(dx),
@@ -1421,6 +1467,7 @@ class _BceTotal(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, ya, yb, split, w, addend):
         ctx.shape = x.shape
+        ctx.bce_link = getattr(x, "_sgg_bce_link", None)
         x = _req(x, "scores").contiguous().view(-1)
         addend = _req(addend, "addend").reshape(())
         loss = torch.empty((), device=x.device, dtype=torch.float32)
@@ -1438,7 +1485,10 @@ class _BceTotal(torch.autograd.Function):
         split, w = ctx.meta
         g = g_total if g_loss is None else (g_loss if g_total is None else g_loss + g_total)
         dx = None
-        if g is not None and ctx.needs_input_grad[0]:
+        if g is not None and ctx.needs_input_grad[0] and ctx.bce_link is not None:
+            dx = torch.empty(ctx.shape, device=x.device, dtype=torch.float32)   # the head backward forms it
+            ctx.bce_link.put(g, ya, yb, split, w, dx)
+        elif g is not None and ctx.needs_input_grad[0]:
             g = g.contiguous()
             dx = torch.empty_like(x)
             N.check(_lib().sgg_bce_bwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), w, N.ptr(g), N.ptr(dx),

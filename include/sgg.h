@@ -293,8 +293,13 @@ int sgg_head_ok(int K, int N1);
 int sgg_head_slab_cols(int K, int N1);
 int sgg_head_fwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* b1, const float* w2,
                  const float* b2, int act, float* hid, float* Y, void* stream);
+/* bce_g != NULL: dY is not read; the head's output gradient is formed in the
+ * launch from the BCE loss on Y that sgg_bce_fwd computed (losses.py:5-21):
+ * dY[m] = (bce_g * bce_w / count) * d bce(Y[m], m < bce_split ? ya : yb) / dY,
+ * count = bce_split or M - bce_split -- sgg_bce_bwd's expression. */
 int sgg_head_bwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* w2, const float* hid,
-                 const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, void* stream);
+                 const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, const float* bce_g,
+                 const float* bce_ya, const float* bce_yb, int bce_split, float bce_w, void* stream);
 
 /* ------------------------------------------------------------------------
  * Input-embedding fold (a Linear(2, E) displacement embedding feeding a

@@ -557,6 +557,35 @@ def test_fused_head_matches_torch(M, Kd, N1, relu1, relu2):
         close(p.grad, pr.grad.cpu().numpy(), rtol=2e-5, what="head d%s" % n)
 
 
+@pytest.mark.parametrize("total", [False, True])
+def test_head_bce_fused_backward_equals_separate(total, monkeypatch):
+    """The BCE loss on the fused head's scores hands its backward to the head
+    launch (BceLink): every gradient is bit-identical to sgg_bce_bwd followed
+    by sgg_head_bwd (SGG_HEAD_BCE=0)."""
+    from sgan import kernels as K
+    from sgan.models import make_mlp
+    torch.manual_seed(3)
+    seq = make_mlp([48, 64, 1], batch_norm=False).to(DEV)
+    spec = K.head_ok(seq)
+    x0 = torch.randn(2560, 48, device=DEV)
+    ya, yb = torch.tensor(0.0, device=DEV), torch.tensor(0.93, device=DEV)
+    grads = []
+    for fused in (True, False):
+        monkeypatch.setattr(K, "HEAD_BCE", fused)
+        seq.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        scores = K.head(x, spec)
+        if total:
+            addend = torch.tensor(0.4, device=DEV, requires_grad=True)
+            _, loss = K.bce_pair_total(scores, 1280, ya, yb, 0.5, addend * 1.0)
+        else:
+            loss = K.bce_pair(scores, 1280, ya, yb, 0.5)
+        loss.backward(torch.tensor(1.3, device=DEV))
+        grads.append([x.grad.clone()] + [p.grad.clone() for p in seq.parameters()])
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("rows,R,E,ld,M,Nn,R_x",[(160, 192, 16, 16, 48, 2, 30720), (80, 512, 16, 64, 32, 512, 1280),
                                                  (1, 128, 16, 16, 16, 2, 70), (257, 512, 16, 16, 64, 65, 4099)])
 def test_grad_finish_bitwise_equals_three_launches(rows, R, E, ld, M, Nn, R_x):
