@@ -307,6 +307,18 @@ extern "C" int sgg_lstm_fwd_u(const float* rel, const float* A, const float* Whh
                      (hipStream_t)stream, Wu, ldwu, cu, NU, U);
 }
 
+extern "C" int sgg_lstm_bwd_split(const float* A, const float* Whh, const float* Wp, const float* h_all,
+                                  const float* c_all, const float* act_all, const float* rel, const float* rel_out,
+                                  const float* dout, const float* dout2, int bsplit, int T, int B, int H, float* dh0,
+                                  float* drel_in, float* drel_tot, float* wpart, void* stream) {
+  SGG_CHECK_ARG(A && Whh && Wp && h_all && c_all && act_all && rel && rel_out && dout && dout2 && drel_in && drel_tot,
+                "sgg_lstm_bwd_split: null pointer");
+  SGG_CHECK_ARG(T >= 1 && B >= 1 && bsplit >= 0 && bsplit <= B && lstm_mw_ok(H, B),
+                "sgg_lstm_bwd_split: bad sizes or no four-wave kernel (T=%d B=%d H=%d bsplit=%d)", T, B, H, bsplit);
+  return lstm_mw_bwd(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, nullptr, dout, T, B, H, 1, dh0, drel_in,
+                     drel_tot, wpart, (hipStream_t)stream, dout2, bsplit);
+}
+
 extern "C" int sgg_lstm_wpart_rows(int H, int B) {
   if (B < 0) return -1;
   return lstm_mw_ok(H, B) ? lstm_mw_wpart_rows(H, B) : 0;

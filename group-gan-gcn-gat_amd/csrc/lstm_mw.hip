@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     const float* __restrict__ h_all, const float* __restrict__ c_tile, const float* __restrict__ act_tile,
     const float* __restrict__ rel, const float* __restrict__ rel_out, const float* __restrict__ dh_last,
     const float* __restrict__ dout, int T, int B, float* __restrict__ dh0, float* __restrict__ drel_in,
-    float* __restrict__ drel_tot, float* __restrict__ wpart) {
+    float* __restrict__ drel_tot, float* __restrict__ wpart, const float* __restrict__ dout2, int bsplit) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
   constexpr bool decoder = DEC, wgrad = WGRAD;
   constexpr int NHS = MwCfg<H>::NHS, P = MwCfg<H>::P;
@@ -449,7 +449,10 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       ncp[i] = cb[j * 64];
     }
     if (decoder) {
-      const float2 dv = *reinterpret_cast<const float2*>(dout + ((size_t)t * B + pc) * 2);
+      // dout2: the output gradient of peds >= bsplit is a separate (T x (B - bsplit) x 2) block
+      const float* dp = (dout2 && pc >= bsplit) ? dout2 + ((size_t)t * (B - bsplit) + (pc - bsplit)) * 2
+                                                : dout + ((size_t)t * (dout2 ? bsplit : B) + pc) * 2;
+      const float2 dv = *reinterpret_cast<const float2*>(dp);
       nd0 = dv.x;
       nd1 = dv.y;
     }
@@ -600,12 +603,13 @@ int launch_fwd(const float* rel, const float* A, const float* Whh, const float* 
 template <int H>
 int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
-               int T, int B, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart, hipStream_t st) {
+               int T, int B, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart, hipStream_t st,
+               const float* dout2, int bsplit) {
   const int grid = (B + kMwPeds - 1) / kMwPeds;
   auto k = decoder ? (wpart ? lstm_mw_bwd_kernel<H, true, true> : lstm_mw_bwd_kernel<H, true, false>)
                    : (wpart ? lstm_mw_bwd_kernel<H, false, true> : lstm_mw_bwd_kernel<H, false, false>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(wpart ? 2 * kMwThreads : kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all, rel, rel_out,
-                     dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart);
+                     dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart, dout2, bsplit);
   SGG_RETURN_LAUNCH("sgg_lstm_bwd");
 }
 
@@ -655,12 +659,12 @@ int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float*
 int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                 const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
                 int T, int B, int H, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart,
-                hipStream_t st) {
+                hipStream_t st, const float* dout2, int bsplit) {
   switch (H) {
-    case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
-    case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
-    case 48: return launch_bwd<48>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
-    default: return launch_bwd<64>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st);
+    case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
+    case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
+    case 48: return launch_bwd<48>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
+    default: return launch_bwd<64>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
   }
 }
 

@@ -818,6 +818,21 @@ class _Pool(torch.autograd.Function):
         return dh, None, dW1, dWe, dbe, dc, dW2, db2, None, None, None
 
 
+class Handoff:
+    """A one-shot slot passing a backward's arguments to the next backward
+    that consumes them (see _Split2 / _LSTMSeq)."""
+
+    def __init__(self):
+        self.pending = None
+
+    def put(self, *args):
+        self.pending = args
+
+    def take(self):
+        p, self.pending = self.pending, None
+        return p
+
+
 class CopiesLink:
     """Carries the decoder-initial-state gradient of the best-of-k copies
     (decoder_init's backward) to the GAT encoder's backward, which sums the
@@ -1224,7 +1239,7 @@ class _LSTMSeq(torch.autograd.Function):
     and reduced by sgg_xtw."""
 
     @staticmethod
-    def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save, u=None):
+    def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save, u=None, slink=None):
         lib = _lib()
         rel = _req(rel, "rel").contiguous()
         H = W_hh.shape[1]
@@ -1267,6 +1282,7 @@ class _LSTMSeq(torch.autograd.Function):
             timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), int(save), 0).decode(),
                       (T, B, int(decoder), int(save)), fl, nb, launch)
         ctx.meta = (decoder, T, B, H, h0 is not None)
+        ctx.slink = slink
         ctx.set_materialize_grads(False)   # unused outputs (the decoder's h_last) get None, not a zero fill
         if save:
             ctx.save_for_backward(rel, W_ih, We, be, A, Whh, Wpc, h_all, c_all, act, rel_out)
@@ -1294,17 +1310,38 @@ class _LSTMSeq(torch.autograd.Function):
         drel_in = torch.empty(T, B, 2, device=dev, dtype=torch.float32)
         dh0 = torch.empty(B, H, device=dev, dtype=torch.float32) if has_h0 else None
         drel_tot = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
+        split = None
+        if decoder and ctx.slink is not None:
+            pend = ctx.slink.take()
+            if pend is not None:
+                ga, gb, bsplit, ph = pend
+                if drel_out is None or drel_out.data_ptr() != ph.data_ptr():
+                    raise N.NativeError("decoder backward: the split rollout output has another consumer")
+                if rows > 0 and wgrad:   # the four-wave kernel reads the two blocks in place
+                    split = (ga, gb, bsplit)
+                else:
+                    drel_out = torch.cat([ga, gb], 1)
         if decoder:
-            dout = drel_out.contiguous() if drel_out is not None else torch.zeros(T, B, 2, device=dev)
+            if split is not None:
+                dout = split[0]
+            else:
+                dout = drel_out.contiguous() if drel_out is not None else torch.zeros(T, B, 2, device=dev)
             dhl = None  # the decoder's final state feeds nothing in the generator (models.py:925)
         else:
             dout = None
             dhl = dh_last.contiguous() if dh_last is not None else None
-        def launch():
-            N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
-                                     N.ptr(rel), N.ptr(rel_out), N.ptr(dhl), N.ptr(dout), T, B, H, int(decoder),
-                                     N.ptr(dG), N.ptr(dh0), N.ptr(drel_in), N.ptr(drel_tot), N.ptr(wpart),
-                                     N.stream_ptr()), "sgg_lstm_bwd")
+        if split is not None:
+            def launch():
+                N.check(lib.sgg_lstm_bwd_split(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(h_all), N.ptr(c_all),
+                                               N.ptr(act), N.ptr(rel), N.ptr(rel_out), N.ptr(split[0]),
+                                               N.ptr(split[1]), split[2], T, B, H, N.ptr(dh0), N.ptr(drel_in),
+                                               N.ptr(drel_tot), N.ptr(wpart), N.stream_ptr()), "sgg_lstm_bwd_split")
+        else:
+            def launch():
+                N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
+                                         N.ptr(rel), N.ptr(rel_out), N.ptr(dhl), N.ptr(dout), T, B, H, int(decoder),
+                                         N.ptr(dG), N.ptr(dh0), N.ptr(drel_in), N.ptr(drel_tot), N.ptr(wpart),
+                                         N.stream_ptr()), "sgg_lstm_bwd")
         launch()
         if timer.active:
             # per ped-step: dh = W^T dG 2 4H H, cell gradient ~30 H, in-kernel
@@ -1351,7 +1388,7 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             drel = drel_in
         return (drel, dW_ih, dW_hh, db_ih, db_hh, dWe, dbe, (dh0 if has_h0 else None), None, dWp, dbp,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def _lstm_wgrads(lib, wpart, rows, P, G4, H, T, B, dG, h_all, rel, rel_out, decoder, W_ih, We, be, dev):
@@ -1399,8 +1436,11 @@ def lstm_sequence(rel, lstm, emb, h0=None, c0=None, proj=None, decoder=False, T=
             return h_last, None
         return _LSTMSeq.apply(rel, W_ih, W_hh, b_ih, b_hh, emb.weight, emb.bias, h0, c0, Wp, bp, bool(decoder), T,
                               save, proj_u)
+    slink = Handoff() if (decoder and save) else None
     h_last, rel_out = _LSTMSeq.apply(rel, W_ih, W_hh, b_ih, b_hh, emb.weight, emb.bias, h0, c0, Wp, bp,
-                                     bool(decoder), T, save)
+                                     bool(decoder), T, save, None, slink)
+    if slink is not None:
+        rel_out._sgg_split_link = slink   # split2 of the best-of-k copies hands both gradient blocks over
     return h_last, (rel_out if decoder else None)
 
 
@@ -1647,11 +1687,18 @@ class _Split2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, B):
         ctx.meta = (x.shape, B)
+        ctx.slink = getattr(x, "_sgg_split_link", None)
         return x[:, :B], x[:, B:]
 
     @staticmethod
     def backward(ctx, ga, gb):
         shape, B = ctx.meta
+        if ctx.slink is not None and ga is not None and gb is not None:
+            # x is the decoder rollout's output: its backward reads the two
+            # blocks in place (sgg_lstm_bwd_split), no concatenation
+            ph = torch.empty(shape, device=ga.device, dtype=ga.dtype)
+            ctx.slink.put(ga.contiguous(), gb.contiguous(), B, ph)
+            return ph, None
         if ga is None:
             ga = torch.zeros(shape[0], B, *shape[2:], device=gb.device, dtype=gb.dtype)
         if gb is None:

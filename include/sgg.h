@@ -389,6 +389,15 @@ int sgg_lstm_wpart_rows(int H, int B);
  * sgg_lstm_bwd (bwd = 1) launches for these sizes, as rocprofv3 lists it
  * (bench.py's per-kernel timing). */
 const char* sgg_lstm_kernel_name(int H, int B, int decoder, int save, int bwd);
+/* The decoder backward (the four-wave family, sgg_lstm_wpart_rows > 0) with
+ * the output gradient in two blocks: peds < bsplit from dout (T x bsplit x 2),
+ * the rest from dout2 (T x (B - bsplit) x 2) -- the best-of-k step's best and
+ * last samples, whose gradients come from the L2 and the adversarial loss,
+ * without concatenating them first.  Other arguments as sgg_lstm_bwd. */
+int sgg_lstm_bwd_split(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
+                       const float* act_all, const float* rel, const float* rel_out, const float* dout,
+                       const float* dout2, int bsplit, int T, int B, int H, float* dh0, float* drel_in,
+                       float* drel_tot, float* wpart, void* stream);
 int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                  const float* act_all, const float* rel, const float* rel_out, const float* dh_last,
                  const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,
