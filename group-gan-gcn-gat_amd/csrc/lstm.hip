@@ -319,6 +319,16 @@ extern "C" int sgg_lstm_bwd_split(const float* A, const float* Whh, const float*
                      drel_tot, wpart, (hipStream_t)stream, dout2, bsplit);
 }
 
+extern "C" int sgg_lstm_bwd_tail(const float* A, const float* Whh, const float* h_all, const float* c_all,
+                                 const float* act_all, const float* rel, const float* dh_last, int T, int B, int H,
+                                 int t_stop, float* drel_in, void* stream) {
+  SGG_CHECK_ARG(A && Whh && h_all && c_all && act_all && rel && drel_in, "sgg_lstm_bwd_tail: null pointer");
+  SGG_CHECK_ARG(T >= 1 && B >= 1 && t_stop >= 0 && t_stop < T && lstm_mw_ok(H, B),
+                "sgg_lstm_bwd_tail: bad sizes or no four-wave kernel (T=%d B=%d H=%d t_stop=%d)", T, B, H, t_stop);
+  return lstm_mw_bwd(A, Whh, nullptr, h_all, c_all, act_all, rel, nullptr, dh_last, nullptr, T, B, H, 0, nullptr,
+                     drel_in, nullptr, nullptr, (hipStream_t)stream, nullptr, 0, t_stop);
+}
+
 extern "C" int sgg_lstm_wpart_rows(int H, int B) {
   if (B < 0) return -1;
   return lstm_mw_ok(H, B) ? lstm_mw_wpart_rows(H, B) : 0;

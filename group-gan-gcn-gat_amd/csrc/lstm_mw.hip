@@ -304,7 +304,8 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     const float* __restrict__ h_all, const float* __restrict__ c_tile, const float* __restrict__ act_tile,
     const float* __restrict__ rel, const float* __restrict__ rel_out, const float* __restrict__ dh_last,
     const float* __restrict__ dout, int T, int B, float* __restrict__ dh0, float* __restrict__ drel_in,
-    float* __restrict__ drel_tot, float* __restrict__ wpart, const float* __restrict__ dout2, int bsplit) {
+    float* __restrict__ drel_tot, float* __restrict__ wpart, const float* __restrict__ dout2, int bsplit,
+    int t_stop) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
   constexpr bool decoder = DEC, wgrad = WGRAD;
   constexpr int NHS = MwCfg<H>::NHS, P = MwCfg<H>::P;
@@ -467,7 +468,10 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   load_step(T - 1);
   float din_x = 0.f, din_y = 0.f;   // drel_in[t + 1] (wave 0, q = 0 lanes)
 
-  for (int t = T - 1; t >= 0; --t) {
+  // t_stop > 0 (input gradients only, no dh0): the steps below t_stop are
+  // skipped -- their input gradients are not wanted (the discriminator's
+  // observed part in the generator step)
+  for (int t = T - 1; t >= t_stop; --t) {
     const int cur = t & 1;
     const float d0 = nd0, d1 = nd1, r0 = nr0, r1 = nr1;
     float ci[MU], cf[MU], cg[MU], co[MU], cc[MU], ccp[MU];
@@ -480,7 +484,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       cc[i] = nc[i];
       ccp[i] = ncp[i];
     }
-    if (t > 0) load_step(t - 1);   // in flight while this step computes
+    if (t > t_stop) load_step(t - 1);   // in flight while this step computes
 
     float f0 = 0.f, f1 = 0.f;
 #pragma unroll
@@ -604,12 +608,12 @@ template <int H>
 int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
                int T, int B, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart, hipStream_t st,
-               const float* dout2, int bsplit) {
+               const float* dout2, int bsplit, int t_stop) {
   const int grid = (B + kMwPeds - 1) / kMwPeds;
   auto k = decoder ? (wpart ? lstm_mw_bwd_kernel<H, true, true> : lstm_mw_bwd_kernel<H, true, false>)
                    : (wpart ? lstm_mw_bwd_kernel<H, false, true> : lstm_mw_bwd_kernel<H, false, false>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(wpart ? 2 * kMwThreads : kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all, rel, rel_out,
-                     dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart, dout2, bsplit);
+                     dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart, dout2, bsplit, t_stop);
   SGG_RETURN_LAUNCH("sgg_lstm_bwd");
 }
 
@@ -659,12 +663,12 @@ int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float*
 int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                 const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
                 int T, int B, int H, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart,
-                hipStream_t st, const float* dout2, int bsplit) {
+                hipStream_t st, const float* dout2, int bsplit, int t_stop) {
   switch (H) {
-    case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
-    case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
-    case 48: return launch_bwd<48>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
-    default: return launch_bwd<64>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit);
+    case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
+    case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
+    case 48: return launch_bwd<48>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
+    default: return launch_bwd<64>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
   }
 }
 

@@ -99,7 +99,7 @@ __attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const floa
                                                       const float* dout, int T, int B, int H, int decoder,
                                                       float* dh0, float* drel_in, float* drel_tot, float* wpart,
                                                       hipStream_t st, const float* dout2 = nullptr,
-                                                      int bsplit = 0);
+                                                      int bsplit = 0, int t_stop = 0);
 
 // v if keep else +0.f, as a bit mask: a plain `keep ? v : 0` lets the
 // compiler sink the load of v into an exec-masked branch that waits for it

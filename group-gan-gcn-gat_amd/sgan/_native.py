@@ -83,6 +83,7 @@ SIGNATURES = {
     "sgg_seg_gather": (_i, [_p, _i, _i, _p, _p, _p, _i, _p, _i, _p]),
     "sgg_xtw_splits": (_i, [_i, _i, _i]),
     "sgg_lstm_bwd_split": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "sgg_lstm_bwd_tail": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p]),
     "sgg_lstm_u_ok": (_i, [_i, _i, _i, _i, _i, _i]),
     "sgg_lstm_fwd_u": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p]),
     "sgg_head_ok": (_i, [_i, _i]),

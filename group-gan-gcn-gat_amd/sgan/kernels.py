@@ -1241,6 +1241,7 @@ class _LSTMSeq(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save, u=None, slink=None):
         lib = _lib()
+        ctx.t_stop = int(getattr(rel, "_sgg_grad_from", 0))
         rel = _req(rel, "rel").contiguous()
         H = W_hh.shape[1]
         B = rel.shape[-2]
@@ -1330,7 +1331,13 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             dout = None
             dhl = dh_last.contiguous() if dh_last is not None else None
-        if split is not None:
+        tail = (not decoder and not wgrad and not has_h0 and rows > 0 and 0 < ctx.t_stop < T)
+        if tail:   # input gradients of steps t_stop .. T-1 only (the rest are not wanted)
+            def launch():
+                N.check(lib.sgg_lstm_bwd_tail(N.ptr(A), N.ptr(Whh), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
+                                              N.ptr(rel), N.ptr(dhl), T, B, H, ctx.t_stop, N.ptr(drel_in),
+                                              N.stream_ptr()), "sgg_lstm_bwd_tail")
+        elif split is not None:
             def launch():
                 N.check(lib.sgg_lstm_bwd_split(N.ptr(A), N.ptr(Whh), N.ptr(Wp), N.ptr(h_all), N.ptr(c_all),
                                                N.ptr(act), N.ptr(rel), N.ptr(rel_out), N.ptr(split[0]),
@@ -1582,6 +1589,8 @@ class _TrajCat(torch.autograd.Function):
                                     b.stride(0) if b is not None else 0, T1, B, N.ptr(out), N.ptr(pos0),
                                     N.ptr(start), N.stream_ptr()), "sgg_traj_cat")
         ctx.dims = (T0, B)
+        if not head.requires_grad:
+            out._sgg_grad_from = T0   # the consumer's backward may skip the head steps' input gradients
         if start is None:
             return out
         ctx.mark_non_differentiable(start)

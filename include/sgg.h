@@ -398,6 +398,14 @@ int sgg_lstm_bwd_split(const float* A, const float* Whh, const float* Wp, const 
                        const float* act_all, const float* rel, const float* rel_out, const float* dout,
                        const float* dout2, int bsplit, int T, int B, int H, float* dh0, float* drel_in,
                        float* drel_tot, float* wpart, void* stream);
+/* Encoder backward (the four-wave family) of steps t_stop .. T-1 only, input
+ * gradients only: drel_in rows t >= t_stop are written, rows below are left
+ * untouched, no weight gradients, no dh0 -- the generator step's pass through
+ * the frozen discriminator, whose observed-part inputs need no gradient.
+ * Other arguments as sgg_lstm_bwd (decoder = 0). */
+int sgg_lstm_bwd_tail(const float* A, const float* Whh, const float* h_all, const float* c_all,
+                      const float* act_all, const float* rel, const float* dh_last, int T, int B, int H,
+                      int t_stop, float* drel_in, void* stream);
 int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                  const float* act_all, const float* rel, const float* rel_out, const float* dh_last,
                  const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,

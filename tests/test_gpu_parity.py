@@ -557,6 +557,33 @@ def test_fused_head_matches_torch(M, Kd, N1, relu1, relu2):
         close(p.grad, pr.grad.cpu().numpy(), rtol=2e-5, what="head d%s" % n)
 
 
+@pytest.mark.parametrize("H,B", [(48, 1280), (48, 37), (32, 100)])
+def test_encoder_backward_tail_equals_full(H, B):
+    """Frozen-weight encoder backward over the steps whose input gradients are
+    wanted (sgg_lstm_bwd_tail, the generator step's pass through D: traj_cat
+    marks the observed steps as not needing a gradient) is bit-identical to
+    the full BPTT on those steps."""
+    from sgan import kernels as K
+    torch.manual_seed(H + B)
+    lstm = torch.nn.LSTM(16, H).to(DEV)
+    emb = torch.nn.Linear(2, 16).to(DEV)
+    for p in list(lstm.parameters()) + list(emb.parameters()):
+        p.requires_grad_(False)
+    obs = torch.randn(8, B, 2, device=DEV) * 0.3
+    pred0 = torch.randn(12, B, 2, device=DEV) * 0.3
+    dh = torch.randn(B, H, device=DEV)
+    grads = []
+    for tail in (True, False):
+        pred = pred0.clone().requires_grad_(True)
+        rel = K.traj_cat(obs, pred)
+        if not tail:
+            rel = rel.clone()                     # no step marker: the full backward
+        h, _ = K.lstm_sequence(rel, lstm, emb)
+        (h * dh).sum().backward()
+        grads.append(pred.grad.clone())
+    torch.testing.assert_close(grads[0], grads[1], rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("total", [False, True])
 def test_head_bce_fused_backward_equals_separate(total, monkeypatch):
     """The BCE loss on the fused head's scores hands its backward to the head
