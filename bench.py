@@ -130,6 +130,13 @@ def kernel_table(timed, n_it):
     return agg
 
 
+def main_launch(a):
+    """The kernel's main launch shape: the most algorithmic work per
+    iteration (bytes, then FLOP) -- not a timing, so that separate processes
+    (the two PMC passes, the bench) pick the same shape."""
+    return max(a["shapes"], key=lambda s: (s[2] * s[1]["bytes"], s[2] * s[1]["flop"]))
+
+
 def roofline_of(name, a):
     us = a["us_per_iter"]
     ai = a["flop"] / max(a["bytes"], 1.0)
@@ -138,7 +145,7 @@ def roofline_of(name, a):
     else:
         achieved, peak, unit, bound = a["bytes"] / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
     # the launch shape carrying most of the kernel's time: its PMC traffic
-    key, r, per_it = max(a["shapes"], key=lambda s: s[2] * s[1]["ms"])
+    key, r, per_it = main_launch(a)
     traffic = traffic_lookup(name, key)
     return {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": traffic[0], "traffic_source": traffic[1],
@@ -359,7 +366,7 @@ def main():
             name, a = args.pmc_kernel, agg[args.pmc_kernel]
         else:
             name, a = max(agg.items(), key=lambda kv: kv[1]["us_per_iter"])
-        key = max(a["shapes"], key=lambda s: s[2] * s[1]["ms"])[0]
+        key = main_launch(a)[0]
         fn = next(r[4] for r in recs if r[1] == key)
         for _ in range(args.pmc_target):
             fn()

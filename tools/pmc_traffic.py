@@ -48,6 +48,10 @@ def main():
     match = (lambda k: k == base) if "<" in base else (lambda k: k.split("<")[0] == base)
     f_t = [v for _, k, v in fr if match(k)][-reps:]
     w_t = [v for _, k, v in wr if match(k)][-reps:]
+    wt = json.loads(open(bench.replace("fetch", "write")).read().strip().splitlines()[-1]).get("pmc_target") \
+        if "fetch" in bench and os.path.exists(bench.replace("fetch", "write")) else tgt
+    if wt != tgt:
+        raise SystemExit("the FETCH and WRITE passes re-issued different launches: %s vs %s" % (tgt, wt))
     rd = 2.0 * 1024.0 * sum(f_t) / max(len(f_t), 1)
     wb = 1024.0 * sum(w_t) / max(len(w_t), 1)
     res["%s|%s" % (name, tgt["shape"])] = {"read_bytes": rd, "write_bytes": wb, "hbm_bytes": rd + wb,
