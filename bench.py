@@ -109,7 +109,8 @@ def traffic_lookup(name, key):
     tab = json.load(open(TRAFFIC_TABLE))
     ent = tab.get("%s|%s" % (name, list(key[1:])))
     if ent is not None:
-        return ent["hbm_bytes"], "PMC bytes of this launch shape (re-issued %d x)" % ent.get("dispatches", 0)
+        return ent["hbm_bytes"], "PMC bytes of this launch shape (%s)" % ent.get(
+            "note", "re-issued %s x" % ent.get("dispatches", 0))
     ent = tab.get("kernels", {}).get(name)
     if ent is not None:   # the kernel's mean over every launch of the PMC run (all its launch shapes)
         return ent["hbm_bytes"], "PMC bytes per launch, mean over the %d launches of the PMC run" % ent["dispatches"]

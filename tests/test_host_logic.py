@@ -82,3 +82,25 @@ def test_vanilla_family_state_dict_keys(pooling, n):
     assert not any(k.startswith(("gatencoder.", "gcn_module.")) for k in keys)
     assert "mlp_decoder_context.0.weight" in keys and "mlp_decoder_context.2.bias" in keys
     assert ("pool_net.mlp_pre_pool.0.weight" in keys) == bool(pooling)
+
+
+def test_bench_traffic_table_lookups():
+    """Every entry of the committed PMC traffic table is readable by bench.py's
+    roofline (the driver's bench line must not fail on it)."""
+    import importlib.util
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    tab = json.load(open(b.TRAFFIC_TABLE))
+    for k in tab:
+        if "|" in k:
+            name, shape = k.split("|")
+            shape = json.loads(shape.replace("False", "false").replace("True", "true"))
+            nb, src = b.traffic_lookup(name, (name,) + tuple(shape))
+            assert nb >= 0 and isinstance(src, str)
+    for name in tab.get("kernels", {}):
+        nb, src = b.traffic_lookup(name, (name, -1))
+        assert nb >= 0 and isinstance(src, str)
