@@ -308,7 +308,8 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     int t_stop) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
   constexpr bool decoder = DEC, wgrad = WGRAD;
-  constexpr int NHS = MwCfg<H>::NHS, P = MwCfg<H>::P;
+  // decoder slab rows carry [dWp (2 x H) | dbp (2)] after [dW_hh | db | dA]
+  constexpr int NHS = MwCfg<H>::NHS, P0 = MwCfg<H>::P, P = P0 + (DEC ? 2 * H + 2 : 0);
   __shared__ float dgb[2][4][KS][kDgPitch];
   __shared__ float part[4][KS][64];
   __shared__ float2 fbp[4][kMwPeds];
@@ -466,7 +467,13 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     for (int k = 0; k < 4; ++k) db[i][k] = dax[i][k] = day[i][k] = 0.f;
 
   load_step(T - 1);
-  float din_x = 0.f, din_y = 0.f;   // drel_in[t + 1] (wave 0, q = 0 lanes)
+  float din_x = 0.f, din_y = 0.f;   // drel_in[t + 1] (wave 0, q = 0 lanes; every lane for the decoder's dWp)
+  // decoder weight gradients of hidden2pos, lane-accumulated over the steps:
+  // dWp += drel_tot[t] h_{t+1}^T (the lane's slots), dbp += drel_tot[t]
+  constexpr bool pgrad = decoder && wgrad;
+  float dwp0[MU], dwp1[MU], dbp0 = 0.f, dbp1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < MU; ++i) dwp0[i] = dwp1[i] = 0.f;
 
   // t_stop > 0 (input gradients only, no dh0): the steps below t_stop are
   // skipped -- their input gradients are not wanted (the discriminator's
@@ -487,6 +494,12 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     if (t > t_stop) load_step(t - 1);   // in flight while this step computes
 
     float f0 = 0.f, f1 = 0.f;
+    // drel_tot[t] = dout[t] + drel_in[t + 1] of this lane's ped (zero for a padded ped)
+    const float rtx = keep_if(d0 + din_x, valid), rty = keep_if(d1 + din_y, valid);
+    if (pgrad) {
+      dbp0 += rtx;
+      dbp1 += rty;
+    }
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
       const int j = g * MU + i;
@@ -495,6 +508,11 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       if (decoder) dhv = fmaf(wp0[i], d0, fmaf(wp1[i], d1, dhv));
       const float ig = ci[i], fg = cf[i], gg = cg[i], og = co[i];
       const float tc = tanh_m(cc[i]);
+      if (pgrad) {   // h_{t+1} of the slot = o_t tanh(c_t)
+        const float hn = og * tc;
+        dwp0[i] = fmaf(rtx, hn, dwp0[i]);
+        dwp1[i] = fmaf(rty, hn, dwp1[i]);
+      }
       const float d_o = dhv * tc;
       const float dct = fmaf(dhv * og, 1.f - tc * tc, dc[i]);
       dc[i] = dct * fg;
@@ -544,10 +562,10 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[mu][ks], bk[ks], acc[mu], 0, 0, 0);
-    if (g == 0 && q == 0) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
+    if (pgrad || (g == 0 && q == 0)) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
       const float2 r0 = fbp[0][c16], r1 = fbp[1][c16], r2 = fbp[2][c16], r3 = fbp[3][c16];
       const float sx = (r0.x + r1.x) + (r2.x + r3.x), sy = (r0.y + r1.y) + (r2.y + r3.y);
-      if (valid) {
+      if (valid && g == 0 && q == 0) {
         *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(sx, sy);
         if (decoder) *reinterpret_cast<float2*>(drel_tot + ((size_t)t * B + ped) * 2) = make_float2(d0 + din_x, d1 + din_y);
       }
@@ -586,6 +604,34 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
           row[G4 * H + k * H + u] = a;
           row[G4 * H + G4 + 2 * (k * H + u)] = x;
           row[G4 * H + G4 + 2 * (k * H + u) + 1] = y;
+        }
+      }
+    }
+    if (pgrad) {   // [dWp (2 x H) | dbp (2)]: sums over the 16 peds
+#pragma unroll
+      for (int i = 0; i < MU; ++i) {
+        float x = dwp0[i], y = dwp1[i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          x += __shfl_xor(x, o);
+          y += __shfl_xor(y, o);
+        }
+        const int u = slot_unit(g * MU + i, q);
+        if (c16 == 0) {
+          row[P0 + u] = x;
+          row[P0 + H + u] = y;
+        }
+      }
+      if (g == 0 && q == 0) {
+        float x = dbp0, y = dbp1;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          x += __shfl_xor(x, o);
+          y += __shfl_xor(y, o);
+        }
+        if (c16 == 0) {
+          row[P0 + 2 * H] = x;
+          row[P0 + 2 * H + 1] = y;
         }
       }
     }

@@ -1306,7 +1306,9 @@ class _LSTMSeq(torch.autograd.Function):
         rows = int(lib.sgg_lstm_wpart_rows(H, B))
         G4 = 4 * H
         P = G4 * H + G4 + 2 * G4
-        wpart = torch.empty(rows, P, device=dev, dtype=torch.float32) if (wgrad and rows > 0) else None
+        # the decoder's rows also carry [dWp (2 x H) | dbp (2)] (lstm_mw.hip)
+        PW = P + (2 * H + 2 if decoder else 0)
+        wpart = torch.empty(rows, PW, device=dev, dtype=torch.float32) if (wgrad and rows > 0) else None
         dG = torch.empty(T, B, G4, device=dev, dtype=torch.float32) if rows == 0 else None
         drel_in = torch.empty(T, B, 2, device=dev, dtype=torch.float32)
         dh0 = torch.empty(B, H, device=dev, dtype=torch.float32) if has_h0 else None
@@ -1370,17 +1372,17 @@ class _LSTMSeq(torch.autograd.Function):
                 # the fold backward of (dA, dbias) -> dW_ih, dWe, dbe (+ the b_hh
                 # copy), and the decoder's dWp, dbp from their split partials
                 gf = GradFinish()
-                if need_p:
-                    ws, splits = xtw_partial(h_all[1:].reshape(T * B, H), drel_tot.view(T * B, 2), colsum=True)
+                if need_p:   # accumulated by the kernel into the slab rows
                     dWp = torch.empty(2, H, device=dev, dtype=torch.float32)
                     dbp = torch.empty(2, device=dev, dtype=torch.float32)
-                    gf.xtw_sums(ws, splits, H, 2, dWp, trans_c=True, colsum=dbp)
+                    gf.rowsum(wpart, rows, PW, P, 2 * H, dWp)
+                    gf.rowsum(wpart, rows, PW, P + 2 * H, 2, dbp)
                 dW_hh = torch.empty(G4, H, device=dev, dtype=torch.float32)
                 db_ih = torch.empty(G4, device=dev, dtype=torch.float32)
                 db_hh = torch.empty(G4, device=dev, dtype=torch.float32)
-                gf.rowsum(wpart, rows, P, 0, G4 * H, dW_hh)
-                gf.rowsum(wpart, rows, P, G4 * H, G4, db_ih)
-                dW_ih, dWe, dbe = gf.fold(W_ih, We, be, wpart, rows, P, G4 * H + G4, wpart, rows, P, G4 * H,
+                gf.rowsum(wpart, rows, PW, 0, G4 * H, dW_hh)
+                gf.rowsum(wpart, rows, PW, G4 * H, G4, db_ih)
+                dW_ih, dWe, dbe = gf.fold(W_ih, We, be, wpart, rows, PW, G4 * H + G4, wpart, rows, PW, G4 * H,
                                           dbias_copy=db_hh)
                 gf.run()
             else:

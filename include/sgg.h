@@ -373,17 +373,19 @@ int sgg_lstm_fwd_u(const float* rel, const float* A, const float* Whh, const flo
  * and, for the decoder, drel_tot (T x B x 2, total dL/d rel_out[t]).
  * Weight gradients, two forms:
  *  - sgg_lstm_wpart_rows(H, B) > 0 (the four-wave MFMA family): pass wpart
- *    (rows x (4H*H + 4H + 8H) floats) and the kernel accumulates, per
- *    workgroup, one slab row [dW_hh (4H x H) | dbias (4H) | dA (4H x 2)] =
- *    sum over its peds and all steps of dG_t^T [h_{t-1} | 1 | r_in(t)]
- *    (h_all and rel -- and rel_out for the decoder, r_in(t) = rel_out[t-1] --
- *    are read for that); sgg_slab_reduce sums the rows.  wpart = NULL: input
+ *    (rows x (4H*H + 4H + 8H) floats; the decoder's rows are 2H + 2 wider)
+ *    and the kernel accumulates, per workgroup, one slab row [dW_hh (4H x H)
+ *    | dbias (4H) | dA (4H x 2)] = sum over its peds and all steps of
+ *    dG_t^T [h_{t-1} | 1 | r_in(t)] (h_all and rel -- and rel_out for the
+ *    decoder, r_in(t) = rel_out[t-1] -- are read for that), followed for the
+ *    decoder by [dWp (2 x H) | dbp (2)] = sum of drel_tot[t] [h_{t+1}^T | 1];
+ *    sgg_slab_reduce / sgg_grad_finish sum the rows.  wpart = NULL: input
  *    gradients only (frozen weights).  dG is not used (may be NULL).
  *  - otherwise dG (T x B x 4H, gradient of the gate pre-activations) is
  *    written and the caller forms the outer-product sums (sgg_xtw); wpart
  *    must be NULL.
- * dWp / dbp of the decoder are X^T sums of drel_tot and h_all, left to the
- * caller in both forms. */
+ * In the dG form dWp / dbp of the decoder are X^T sums of drel_tot and h_all,
+ * left to the caller. */
 int sgg_lstm_wpart_rows(int H, int B);
 /* Name of the kernel sgg_lstm_fwd (bwd = 0; save = act_all != NULL) or
  * sgg_lstm_bwd (bwd = 1) launches for these sizes, as rocprofv3 lists it
