@@ -31,7 +31,11 @@ constexpr int kLstmMaxT = 32;   // encoder inputs of up to this many steps are s
 // v_exp_f32 / v_rcp_f32 forms (~2 ulp), as in lstm_mfma.hip: the gate
 // activations sit on the serial critical path of every step
 __device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_f(float x) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f); }
+// (exp(-2x) as v_exp_f32(x * -2 log2(e)): -2 log2(e) is exact, so the same bits as
+// __expf(-2x)'s (-2x) * log2(e) with one multiply less)
+__device__ __forceinline__ float tanh_f(float x) {
+  return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -2.8853900817779268f)), -1.f);
+}
 
 template <int H>
 __global__ void __launch_bounds__(16 * H) lstm_fwd_kernel(

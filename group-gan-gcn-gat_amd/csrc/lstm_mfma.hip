@@ -28,7 +28,11 @@ namespace {
 // v_exp_f32 / v_rcp_f32 forms (~2 ulp): the 5H transcendentals per ped and
 // step are the VALU side of this kernel
 __device__ __forceinline__ float sigm_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_fast(float x) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f); }
+// (exp(-2x) as v_exp_f32(x * -2 log2(e)): -2 log2(e) is exact, so the same bits as
+// __expf(-2x)'s (-2x) * log2(e) with one multiply less)
+__device__ __forceinline__ float tanh_fast(float x) {
+  return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -2.8853900817779268f)), -1.f);
+}
 // the same activations of a pre-activation the weights already scaled by
 // -log2(e) (sigmoid) or -2 log2(e) (tanh): v_exp_f32 takes it directly (the
 // scale rides in W_ext, loaded once; one VALU multiply less per gate value)

@@ -69,12 +69,16 @@ constexpr int kDgPitch = 68;      // dG image row pitch: conflict-free for the t
 
 // v_exp_f32 / v_rcp_f32 forms (~2 ulp), as the other LSTM kernels.
 // s = 1: sigmoid(x); s = 2: tanh(x) = 2 sigmoid(2x) - 1 (the same
-// expressions as lstm_unit.hip's sigm_u / tanh_u)
-__device__ __forceinline__ float gate_act(float x, float s) {
-  return fmaf(s, __builtin_amdgcn_rcpf(1.f + __expf(-(s * x))), 1.f - s);
+// expressions as lstm_unit.hip's sigm_u / tanh_u).  exp(-s x) is taken as
+// v_exp_f32(x * nsl), nsl = -s log2(e): s is a power of two, so nsl is exact
+// and the argument rounds exactly as __expf's (-(s x)) * log2(e) -- the same
+// bits with one multiply less per gate value
+constexpr float kNegLog2e = -1.4426950408889634f;
+__device__ __forceinline__ float gate_act(float x, float s, float nsl) {
+  return fmaf(s, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * nsl)), 1.f - s);
 }
 __device__ __forceinline__ float tanh_m(float x) {
-  return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f);
+  return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * (2.f * kNegLog2e))), -1.f);
 }
 
 // unit held by slot j of lane quarter q
@@ -163,6 +167,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
   };
   float xin = input(0);
   const float s = g == 2 ? 2.f : 1.f;   // g: tanh, i f o: sigmoid
+  const float nsl = s * kNegLog2e;
 
   for (int t = 0; t < T; ++t) {
     if (decoder && t == 1) {
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     for (int mu = 0; mu < MU; ++mu) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float a = gate_act(acc[mu][r], s);
+        const float a = gate_act(acc[mu][r], s, nsl);
         gate[g][4 * mu + r][lane] = a;
         if (save) at[(4 * mu + r) * 64] = a;   // lane-linear 256-byte line per slot
       }

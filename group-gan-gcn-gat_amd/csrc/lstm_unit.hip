@@ -26,7 +26,11 @@ namespace {
 constexpr int kUnitMaxT = 32;   // encoder inputs of up to this many steps are staged in LDS
 
 __device__ __forceinline__ float sigm_u(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_u(float x) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f); }
+// (exp(-2x) as v_exp_f32(x * -2 log2(e)): -2 log2(e) is exact, so the same bits as
+// __expf(-2x)'s (-2x) * log2(e) with one multiply less)
+__device__ __forceinline__ float tanh_u(float x) {
+  return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -2.8853900817779268f)), -1.f);
+}
 
 // sum over the H consecutive lanes of a ped (H divides 64)
 template <int H>
