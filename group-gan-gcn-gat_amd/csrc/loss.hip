@@ -30,10 +30,28 @@ __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ 
   __shared__ float red[2][4];
   const float a = *ya, b = *yb;
   float s0 = 0.f, s1 = 0.f;
+  constexpr int kPre = 16;   // up to 4,096 scores: every load in flight at once (one round trip)
+  if (n <= kPre * 256) {
+    float v[kPre];
+#pragma unroll
+    for (int m = 0; m < kPre; ++m) {
+      const int i = threadIdx.x + 256 * m;
+      v[m] = i < n ? x[i] : 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < kPre; ++m) {   // the same per-thread order as the loop below
+      const int i = threadIdx.x + 256 * m;
+      if (i < n) {
+        if (i < split) s0 += bce_term(v[m], a);
+        else s1 += bce_term(v[m], b);
+      }
+    }
+  } else {
 #pragma unroll 4
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    if (i < split) s0 += bce_term(x[i], a);
-    else s1 += bce_term(x[i], b);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (i < split) s0 += bce_term(x[i], a);
+      else s1 += bce_term(x[i], b);
+    }
   }
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
