@@ -558,11 +558,13 @@ def test_fused_head_matches_torch(M, Kd, N1, relu1, relu2):
 
 
 @pytest.mark.parametrize("H,B", [(48, 1280), (48, 37), (32, 100)])
-def test_encoder_backward_tail_equals_full(H, B):
+@pytest.mark.parametrize("proj", [False, True])
+def test_encoder_backward_tail_equals_full(H, B, proj):
     """Frozen-weight encoder backward over the steps whose input gradients are
     wanted (sgg_lstm_bwd_tail, the generator step's pass through D: traj_cat
     marks the observed steps as not needing a gradient) is bit-identical to
-    the full BPTT on those steps."""
+    the full BPTT on those steps.  proj: the discriminator's form, the encoder
+    with the pooling projection epilogue (sgg_lstm_fwd_u)."""
     from sgan import kernels as K
     torch.manual_seed(H + B)
     lstm = torch.nn.LSTM(16, H).to(DEV)
@@ -572,16 +574,25 @@ def test_encoder_backward_tail_equals_full(H, B):
     obs = torch.randn(8, B, 2, device=DEV) * 0.3
     pred0 = torch.randn(12, B, 2, device=DEV) * 0.3
     dh = torch.randn(B, H, device=DEV)
-    grads = []
+    Wu = torch.randn(512, H, device=DEV) * 0.1
+    cu = torch.randn(512, device=DEV) * 0.1
+    if proj and not K.lstm_u_ok(20, B, H, True, 512):
+        pytest.skip("no projection epilogue at this size")
+    grads, outs = [], []
     for tail in (True, False):
         pred = pred0.clone().requires_grad_(True)
         rel = K.traj_cat(obs, pred)
         if not tail:
             rel = rel.clone()                     # no step marker: the full backward
-        h, _ = K.lstm_sequence(rel, lstm, emb)
+        h, U = K.lstm_sequence(rel, lstm, emb, proj_u=(Wu, cu) if proj else None)
         (h * dh).sum().backward()
         grads.append(pred.grad.clone())
+        outs.append((h.detach().clone(), U.clone() if U is not None else None))
     torch.testing.assert_close(grads[0], grads[1], rtol=0, atol=0)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)
+    if proj:
+        assert outs[0][1] is not None
+        torch.testing.assert_close(outs[0][1], outs[1][1], rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("total", [False, True])
