@@ -370,13 +370,16 @@ class GraphedTrainer:
         self.inp_flat = torch.zeros(sum(sizes), device=dev)
         dv = views(self.inp_flat)
         self.inp = StepInputs(dv[0], dv[1], dv[2]) if nd else StepInputs(None, None, dv[0])
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
+        # warm-up and capture on the same side stream: the parameters'
+        # AccumulateGrad nodes (created by the first backward, kept alive by
+        # the captured graph) are bound to the stream that created them
+        cap = torch.cuda.Stream()
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
             for _ in range(warmup):
                 self._load(*trainer.draw_inputs(*self.span))
                 trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
-        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.current_stream().wait_stream(cap)
         torch.cuda.synchronize()
         trainer.opt_g.zero_grad(set_to_none=True)
         trainer.opt_d.zero_grad(set_to_none=True)
@@ -389,7 +392,6 @@ class GraphedTrainer:
         self.pair = []
         pool = torch.cuda.graph_pool_handle()
         dp = trainer.dp
-        cap = torch.cuda.Stream()
         cap.wait_stream(torch.cuda.current_stream())
         if not (dp.on and dp.world > 1):
             # one rank: TWO graphs, each starting with the H2D copy of its own
