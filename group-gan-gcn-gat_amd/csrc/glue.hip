@@ -170,7 +170,8 @@ __global__ void __launch_bounds__(64) l2_terms_kernel(const float* __restrict__ 
   const int o = scene_off[s], n = scene_off[s + 1] - o;
   const int tot = n * T;
   const bool staged = tot <= kL2MaxElems;   // uniform
-  if (staged) stage_mask(msk, mask, ldm, o, n, T, lane, 64);   // (one wave: no barrier)
+  if (staged) stage_mask(msk, mask, ldm, o, n, T, lane, 64);
+  __syncthreads();   // lanes read entries other lanes wrote (one wave: costs nothing)
   float acc = 0.f, ms = 0.f;
   for (int e0 = lane; e0 < tot; e0 += 256) {
     float mk[4];

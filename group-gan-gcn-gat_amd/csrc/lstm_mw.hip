@@ -583,6 +583,9 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       for (int r = 0; r < 4; ++r) part[g][4 * mu + r][lane] = acc[mu][r];
     lds_barrier();
   }
+  if (t_stop > 0 && valid && g == 0 && q == 0) {   // the skipped steps' input gradients are defined as zero
+    for (int t = 0; t < t_stop; ++t) *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(0.f, 0.f);
+  }
   if (dh0 && valid) {   // dh0 = W_hh^T dG_0
 #pragma unroll
     for (int i = 0; i < MU; ++i) {

@@ -5,17 +5,20 @@
 // run along the features, so every row read is a coalesced F-float vector:
 //   256 threads = 64 feature lanes x 4 row phases; each (phase, feature)
 //   thread accumulates its rows, the 4 phases are combined in LDS.
-// Two passes (mean, then centred sum of squares), biased variance, fp32.
+// Two passes (mean, then centred sum of squares), biased variance; the
+// per-feature sums are accumulated in fp64 (the backward's two means feed a
+// gradient whose sum over the scene's rows cancels to ~0 -- the next
+// layer's bias gradient -- so their rounding is what that sum sees).
 #include "sgg_common.h"
 
 namespace sgg {
 
 constexpr int kNormThreads = 256;
 
-__device__ __forceinline__ float phase_sum(float v, float (*red)[64], int ph, int fl) {
+__device__ __forceinline__ double phase_sum(double v, double (*red)[64], int ph, int fl) {
   red[ph][fl] = v;
   __syncthreads();
-  const float s = (red[0][fl] + red[1][fl]) + (red[2][fl] + red[3][fl]);
+  const double s = (red[0][fl] + red[1][fl]) + (red[2][fl] + red[3][fl]);
   __syncthreads();
   return s;
 }
@@ -24,25 +27,26 @@ __global__ void __launch_bounds__(kNormThreads) seg_norm_fwd_kernel(const float*
                                                                     const int32_t* __restrict__ seg_off, int nseg,
                                                                     float eps, float* __restrict__ y, int ldy,
                                                                     float* __restrict__ rstd_out) {
-  __shared__ float red[4][64];
+  __shared__ double red[4][64];
   const int fl = threadIdx.x & 63, ph = threadIdx.x >> 6;
   for (int g = blockIdx.x; g < nseg; g += gridDim.x) {
     const int o = seg_off[g], n = seg_off[g + 1] - o;
-    const float inv_n = n > 0 ? 1.f / (float)n : 0.f;
     for (int f0 = 0; f0 < F; f0 += 64) {
       const int f = f0 + fl;
       const bool fok = f < F;
-      float s = 0.f;
+      double s = 0.0;
       if (fok)
-        for (int r = ph; r < n; r += 4) s += x[(size_t)(o + r) * ldx + f];
-      const float mean = phase_sum(s, red, ph, fl) * inv_n;
-      float q = 0.f;
+        for (int r = ph; r < n; r += 4) s += (double)x[(size_t)(o + r) * ldx + f];
+      const double meand = n > 0 ? phase_sum(s, red, ph, fl) / n : phase_sum(s, red, ph, fl);
+      const float mean = (float)meand;
+      double q = 0.0;
       if (fok)
         for (int r = ph; r < n; r += 4) {
-          const float d = x[(size_t)(o + r) * ldx + f] - mean;
-          q = fmaf(d, d, q);
+          const double d = (double)x[(size_t)(o + r) * ldx + f] - meand;
+          q = fma(d, d, q);
         }
-      const float var = phase_sum(q, red, ph, fl) * inv_n;
+      const double qs = phase_sum(q, red, ph, fl);
+      const float var = n > 0 ? (float)(qs / n) : 0.f;
       const float rs = 1.f / sqrtf(var + eps);
       if (fok) {
         for (int r = ph; r < n; r += 4) y[(size_t)(o + r) * ldy + f] = (x[(size_t)(o + r) * ldx + f] - mean) * rs;
@@ -57,28 +61,27 @@ __global__ void __launch_bounds__(kNormThreads) seg_norm_bwd_kernel(const float*
                                                                     const int32_t* __restrict__ seg_off, int nseg,
                                                                     const float* __restrict__ rstd,
                                                                     float* __restrict__ dx, int lddx) {
-  __shared__ float red[4][64];
+  __shared__ double red[4][64];
   const int fl = threadIdx.x & 63, ph = threadIdx.x >> 6;
   for (int g = blockIdx.x; g < nseg; g += gridDim.x) {
     const int o = seg_off[g], n = seg_off[g + 1] - o;
-    const float inv_n = n > 0 ? 1.f / (float)n : 0.f;
     for (int f0 = 0; f0 < F; f0 += 64) {
       const int f = f0 + fl;
       const bool fok = f < F;
-      float sd = 0.f, sdy = 0.f;
+      double sd = 0.0, sdy = 0.0;
       if (fok)
         for (int r = ph; r < n; r += 4) {
-          const float d = dy[(size_t)(o + r) * lddy + f];
+          const double d = (double)dy[(size_t)(o + r) * lddy + f];
           sd += d;
-          sdy = fmaf(d, y[(size_t)(o + r) * ldy + f], sdy);
+          sdy = fma(d, (double)y[(size_t)(o + r) * ldy + f], sdy);
         }
-      const float md = phase_sum(sd, red, ph, fl) * inv_n;
-      const float mdy = phase_sum(sdy, red, ph, fl) * inv_n;
+      const double md = n > 0 ? phase_sum(sd, red, ph, fl) / n : phase_sum(sd, red, ph, fl);
+      const double mdy = n > 0 ? phase_sum(sdy, red, ph, fl) / n : phase_sum(sdy, red, ph, fl);
       if (fok) {
-        const float rs = rstd[(size_t)g * F + f];
+        const double rs = (double)rstd[(size_t)g * F + f];
         for (int r = ph; r < n; r += 4) {
-          const float d = dy[(size_t)(o + r) * lddy + f];
-          dx[(size_t)(o + r) * lddx + f] = rs * (d - md - y[(size_t)(o + r) * ldy + f] * mdy);
+          const double d = (double)dy[(size_t)(o + r) * lddy + f];
+          dx[(size_t)(o + r) * lddx + f] = (float)(rs * ((d - md) - (double)y[(size_t)(o + r) * ldy + f] * mdy));
         }
       }
     }

@@ -7,6 +7,7 @@ path.
 """
 import contextlib
 import os
+import weakref
 
 import torch
 
@@ -198,7 +199,7 @@ def fold_fwd(W, We, be, b1, b2=None):
     updates parameters through raw pointers) -- see prefold()."""
     key, ver = _fold_key(W, We, be, b1, b2)
     ent = _FOLD_CACHE.get(key)
-    if ent is not None and ent[0] == ver:
+    if _fold_hit(ent, ver, (W, We, be, b1, b2)):
         return ent[1], ent[2]
     prefold([(W, We, be, b1, b2)])
     ent = _FOLD_CACHE[key]
@@ -218,6 +219,26 @@ def _fold_key(W, We, be, b1, b2):
     return key, ver
 
 
+def _owner(t):
+    return t._base if t._base is not None else t
+
+
+def _fold_hit(ent, ver, ts):
+    """A cached fold is current iff the weights' versions match AND the
+    entry was made from these very weight tensors (weak references): a
+    tensor that reuses a freed weight's address is a different tensor."""
+    return (ent is not None and ent[0] == ver
+            and all((r is None) if t is None else (r is not None and r() is _owner(t)) for r, t in zip(ent[4], ts)))
+
+
+def _fold_purge():
+    """Drop entries whose weights are gone (models built and discarded in one
+    process: tests, sweeps, evaluating many checkpoints)."""
+    dead = [k for k, e in _FOLD_CACHE.items() if any(r is not None and r() is None for r in e[4])]
+    for k in dead:
+        del _FOLD_CACHE[k]
+
+
 def clear_fold_cache():
     """Drop every cached fold (a HIP-graph capture must start from an empty
     cache, so every fold its replays need is a node of the graph)."""
@@ -234,11 +255,11 @@ def prefold(specs):
     todo = []
     for W, We, be, b1, b2 in specs:
         key, ver = _fold_key(W, We, be, b1, b2)
-        ent = _FOLD_CACHE.get(key)
-        if ent is None or ent[0] != ver:
+        if not _fold_hit(_FOLD_CACHE.get(key), ver, (W, We, be, b1, b2)):
             todo.append((key, ver, (W, We, be, b1, b2)))
     if not todo:
         return
+    _fold_purge()
     arr = (N.Fold * len(todo))()
     outs = []
     for k, (key, ver, (W, We, be, b1, b2)) in enumerate(todo):
@@ -253,10 +274,12 @@ def prefold(specs):
     for i in range(0, len(todo), N.FOLD_MAX):
         chunk = (N.Fold * min(N.FOLD_MAX, len(todo) - i))(*arr[i:i + N.FOLD_MAX])
         N.check(_lib().sgg_fold_fwd_multi(chunk, len(chunk), N.stream_ptr()), "sgg_fold_fwd_multi")
-    for key, ver, A, bias, parts in outs:
-        # the entry keeps the weights alive: their addresses cannot be reused
-        # by other tensors while the entry exists
-        _FOLD_CACHE[key] = (ver, A, bias, parts)
+    for (key, ver, A, bias, parts), (_, _, ts) in zip(outs, todo):
+        # weak references to the caller's weights (the entry does not keep a
+        # model alive); strong ones only to the contiguous copies made here
+        refs = tuple(weakref.ref(_owner(t)) if t is not None else None for t in ts)
+        copies = tuple(p for p, t in zip(parts, ts) if p is not None and p.data_ptr() != t.data_ptr())
+        _FOLD_CACHE[key] = (ver, A, bias, copies, refs)
 
 
 def lstm_fold_spec(lstm, emb):
@@ -530,14 +553,30 @@ class _Head(torch.autograd.Function):
 
 
 HEAD_BCE = os.environ.get("SGG_HEAD_BCE", "1") != "0"
+_BCE_HANDOFF = [0]
+
+
+@contextlib.contextmanager
+def bce_handoff():
+    """Scope in which the discriminator head's scores may hand their BCE
+    backward to the head's launch (BceLink).  Only the trainer's own steps
+    open it: there the scores' gradient is never read by anyone but the head,
+    whereas outside it a direct query (autograd.grad on the scores,
+    retain_grad) must see a real gradient, not the handoff's placeholder."""
+    _BCE_HANDOFF[0] += 1
+    try:
+        yield
+    finally:
+        _BCE_HANDOFF[0] -= 1
 
 
 def head(x, spec):
     """real_classifier forward through the fused head (spec = head_ok(seq)).
-    With autograd on, the scores carry a BceLink: a K.bce_pair /
-    K.bce_pair_total on them hands its backward to the head's launch."""
+    With autograd on inside bce_handoff(), the scores carry a BceLink: a
+    K.bce_pair / K.bce_pair_total on them hands its backward to the head's
+    launch."""
     l1, l2, act = spec
-    link = BceLink() if (HEAD_BCE and torch.is_grad_enabled()) else None
+    link = BceLink() if (HEAD_BCE and _BCE_HANDOFF[0] > 0 and torch.is_grad_enabled()) else None
     y = _Head.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, act, link)
     if link is not None:
         y._sgg_bce_link = link
@@ -941,7 +980,9 @@ class _GatAttn(torch.autograd.Function):
         dbias = None
         if has_bias:
             dpre = dy if epi == 0 else dy * torch.where(hp > 0, torch.ones_like(hp), torch.exp(hp))
-            dbias = dpre.view(n, heads, F).sum((0, 1))
+            # a near-cancelling sum (the next layer's instance norm removes
+            # each feature's mean over the scene): accumulated in fp64
+            dbias = dpre.view(n, heads, F).double().sum((0, 1)).float()
         return dWh, da, dbias, None, None, None, None, None, None, None, None
 
 

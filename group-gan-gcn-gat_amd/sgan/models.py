@@ -14,10 +14,15 @@ Scene bookkeeping is an int32 CSR built once per batch (sgan/scene.py)
 instead of a `.item()` per scene per module.  The encoder LSTM and the 12-step
 decoder rollout are single fused launches (sgg_lstm_fwd / sgg_lstm_bwd).
 
+Checkpoint families: TrajectoryGenerator.load_state_dict reads the family off
+the state's key set (family_of) and rebuilds the family's modules before the
+(strict) load, so the reference's scripts/evaluate_model.py:30-52 loads every
+family's g_state unchanged.
+
 Extra keyword-only arguments beyond the reference's are optional and default
 to the reference behaviour:
   TrajectoryGenerator(..., graph='gat'|'gcn'|'sgangat'|'vanilla')  selects
-      the message-passing module the forward calls ('gat' = the committed
+      the family up front, e.g. to train one from scratch ('gat' = the committed
       forward, models.py:903-905; 'gcn' = the sgan-g(-p) checkpoint families,
       :902; 'sgangat' = the sgangat-g-p family: the batched multi-head GAT of
       the commented sgan/GAT.py:6-106 text, then gcn_module; n_heads is then
@@ -453,8 +458,6 @@ class TrajectoryGenerator(nn.Module):
         super().__init__()
         if pooling_type and pooling_type.lower() == "none":
             pooling_type = None
-        if graph not in ("gat", "gcn", "sgangat", "vanilla"):
-            raise ValueError("graph must be 'gat', 'gcn', 'sgangat' or 'vanilla'")
         self.obs_len = obs_len
         self.pred_len = pred_len
         self.mlp_dim = mlp_dim
@@ -469,7 +472,6 @@ class TrajectoryGenerator(nn.Module):
         self.noise_first_dim = 0
         self.pool_every_timestep = pool_every_timestep
         self.bottleneck_dim = 1024
-        self.graph = graph
 
         self.encoder = Encoder(embedding_dim=embedding_dim, h_dim=encoder_h_dim, mlp_dim=mlp_dim,
                                num_layers=num_layers, dropout=dropout)
@@ -488,26 +490,105 @@ class TrajectoryGenerator(nn.Module):
             self.noise_dim = None
         else:
             self.noise_first_dim = noise_dim[0]
-        input_dim = encoder_h_dim + bottleneck_dim if pooling_type else encoder_h_dim
-        # module set (and registration order, which fixes the optimizer-state
-        # order) of each checkpoint family:
-        #   gat     : committed models.py:800-812 -> gatencoder, gcn_module
-        #   gcn     : sgan-g(-p)-models            -> mlp_decoder_context, gcn_module
-        #   sgangat : sgangat-g-p-models           -> gatencoder.gat_net, mlp_decoder_context, gcn_module
-        #   vanilla : sgan-models / sgan-p-models  -> mlp_decoder_context only (upstream Social-GAN,
-        #             the commented models.py:796-804 / :898; no group module at all)
-        # (mlp_decoder_context is carried by the gcn / sgangat checkpoints but not called)
+        self._family_args = dict(n_units=list(n_units), n_heads=n_heads, dropout1=dropout1, alpha=alpha,
+                                 input_dim=encoder_h_dim + bottleneck_dim if pooling_type else encoder_h_dim,
+                                 mlp_dim=mlp_dim, decoder_h_dim=decoder_h_dim, activation=activation,
+                                 batch_norm=batch_norm, dropout=dropout)
+        self._build_family(graph)
+
+    # module set (and registration order, which fixes the optimizer-state
+    # order) of each checkpoint family:
+    #   gat     : committed models.py:800-812 -> gatencoder, gcn_module
+    #   gcn     : sgan-g(-p)-models            -> mlp_decoder_context, gcn_module
+    #   sgangat : sgangat-g-p-models           -> gatencoder.gat_net, mlp_decoder_context, gcn_module
+    #   vanilla : sgan-models / sgan-p-models  -> mlp_decoder_context only (upstream Social-GAN,
+    #             the commented models.py:796-804 / :898; no group module at all)
+    # (mlp_decoder_context is carried by the gcn / sgangat checkpoints but not called)
+    _FAMILY_MODULES = ("gatencoder", "mlp_decoder_context", "gcn_module")
+
+    @staticmethod
+    def family_of(keys):
+        """The checkpoint family a generator state dict belongs to, from its
+        key set alone (scripts/evaluate_model.py:30-52 builds the generator
+        from the checkpoint's args, which name no family, then strict-loads
+        g_state):  gatencoder.gat_net.* -> sgangat; gatencoder.gat_intra.* ->
+        gat; gcn_module.* without a gatencoder -> gcn; neither -> vanilla."""
+        keys = list(keys)
+        if any(k.startswith("gatencoder.gat_net.") for k in keys):
+            return "sgangat"
+        if any(k.startswith("gatencoder.gat_intra.") for k in keys):
+            return "gat"
+        if any(k.startswith("gcn_module.") for k in keys):
+            return "gcn"
+        return "vanilla"
+
+    def _build_family(self, graph, sgat_shapes=None):
+        """(Re)build the family's modules.  Modules the old and new family
+        share keep their objects (so e.g. gcn_module's parameters survive a
+        gat -> gcn switch); the rest are created fresh and registered in the
+        family's order.  sgat_shapes: [(heads, f_in, f_out)] per batched GAT
+        layer, read from a state dict (the checkpoint's n_units / heads)."""
+        if graph not in ("gat", "gcn", "sgangat", "vanilla"):
+            raise ValueError("graph must be 'gat', 'gcn', 'sgangat' or 'vanilla'")
+        a = self._family_args
+        old = {n: self._modules.pop(n) for n in self._FAMILY_MODULES if n in self._modules}
+        self.graph = graph
+        ctx_out = a["decoder_h_dim"] - self.noise_first_dim
         if graph == "gat":
-            self.gatencoder = GATEncoder(n_units=n_units, n_heads=n_heads, dropout=dropout1, alpha=alpha)
+            ge = old.get("gatencoder")
+            self.gatencoder = ge if isinstance(ge, GATEncoder) else GATEncoder(
+                n_units=a["n_units"], n_heads=a["n_heads"], dropout=a["dropout1"], alpha=a["alpha"])
         elif graph == "sgangat":
-            heads = list(n_heads) if isinstance(n_heads, (list, tuple)) else [n_heads] * (len(n_units) - 2) + [1]
-            self.gatencoder = BatchGATEncoder(n_units=list(n_units), n_heads=heads, dropout=dropout1, alpha=alpha)
+            if sgat_shapes is not None:
+                units = [sgat_shapes[0][1]] + [s[2] for s in sgat_shapes]
+                heads = [s[0] for s in sgat_shapes]
+            else:
+                units = list(a["n_units"])
+                nh = a["n_heads"]
+                heads = list(nh) if isinstance(nh, (list, tuple)) else [nh] * (len(units) - 2) + [1]
+            ge = old.get("gatencoder")
+            same = (isinstance(ge, BatchGATEncoder)
+                    and [(l.n_head, l.f_in, l.f_out) for l in ge.gat_net.layer_stack]
+                    == [(h, (units[i] * heads[i - 1] if i else units[i]), units[i + 1]) for i, h in enumerate(heads)])
+            self.gatencoder = ge if same else BatchGATEncoder(n_units=units, n_heads=heads, dropout=a["dropout1"],
+                                                               alpha=a["alpha"])
         if graph in ("gcn", "sgangat") or (graph == "vanilla" and self.mlp_decoder_needed()):
-            self.mlp_decoder_context = make_mlp([input_dim, mlp_dim, decoder_h_dim - self.noise_first_dim],
-                                                activation=activation, batch_norm=batch_norm, dropout=dropout)
+            m = old.get("mlp_decoder_context")
+            self.mlp_decoder_context = m if m is not None else make_mlp(
+                [a["input_dim"], a["mlp_dim"], ctx_out], activation=a["activation"], batch_norm=a["batch_norm"],
+                dropout=a["dropout"])
         if graph != "vanilla":
-            self.gcn_module = GCNModule(input_dim=input_dim, hidden_dim=72, out_dim=16, gcn_layers=2,
-                                        final_dim=decoder_h_dim - self.noise_first_dim)
+            m = old.get("gcn_module")
+            self.gcn_module = m if m is not None else GCNModule(
+                input_dim=a["input_dim"], hidden_dim=72, out_dim=16, gcn_layers=2, final_dim=ctx_out)
+        # new modules follow the rest of the generator's device / dtype
+        p0 = next(self.encoder.parameters())
+        for n in self._FAMILY_MODULES:
+            if n in self._modules and n not in old:
+                self._modules[n].to(device=p0.device, dtype=p0.dtype)
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        """nn.Module.load_state_dict after switching to the state's checkpoint
+        family (family_of), so the reference's unchanged
+        scripts/evaluate_model.py:30-52 -- TrajectoryGenerator(**checkpoint
+        args), then a strict load of g_state -- works for every family
+        (sgan-models / sgan-p-models, sgan-g(-p), sgan-gat, sgangat-g-p).  A
+        state without any family module (a partial, strict=False load) keeps
+        the current family."""
+        keys = list(state_dict.keys())
+        if strict or any(k.split(".")[0] in self._FAMILY_MODULES for k in keys):
+            fam = self.family_of(keys)
+            shapes = None
+            if fam == "sgangat":
+                ws = sorted((int(k.split(".")[3]), state_dict[k].shape) for k in keys
+                            if k.startswith("gatencoder.gat_net.layer_stack.") and k.endswith(".w"))
+                shapes = [tuple(int(d) for d in s) for _, s in ws]
+            cur = None
+            if fam == "sgangat" and isinstance(getattr(self, "gatencoder", None), BatchGATEncoder):
+                cur = [(l.n_head, l.f_in, l.f_out) for l in self.gatencoder.gat_net.layer_stack]
+            if fam != self.graph or (fam == "sgangat" and cur != shapes):
+                self._build_family(fam, sgat_shapes=shapes)
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
 
     def add_noise(self, _input, seq_start_end, user_noise=None, scenes=None):
         """models.py:814-850 (noise drawn on the host, one draw per call)."""

@@ -38,6 +38,7 @@ all-reduce per optimizer step (grads + loss values), then clip and Adam.
 The result equals single-GPU training on the global batch up to summation
 order.
 """
+import contextlib
 import random
 
 import numpy as np
@@ -131,6 +132,9 @@ class KernelOps:
     # clip_grad_norm_ + Adam in two launches (sgg_adam_step; torch's state
     # layout, capturable): optimizer(params, lr).step(max_norm)
     optimizer = staticmethod(lambda params, lr: K.ClipAdam(params, lr=lr))
+    # the discriminator head forms the BCE gradient in its own backward
+    # (kernels.BceLink) inside the steps only
+    handoff = staticmethod(K.bce_handoff)
 
 
 class GanTrainer:
@@ -183,10 +187,17 @@ class GanTrainer:
         return vals
 
     # -- steps ---------------------------------------------------------------
+    def _scope(self):
+        return getattr(self.ops, "handoff", contextlib.nullcontext)()
+
     def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """discriminator_step (train.py:395-429). `batch` holds this rank's
         scenes (device tensors), `sc` their SceneIndex.  `inputs` (StepInputs)
         replaces the host RNG draws by pre-drawn device tensors (graph mode)."""
+        with self._scope():
+            return self._d_step(batch, sc, S_global, B_global, shard, inputs)
+
+    def _d_step(self, batch, sc, S_global, B_global, shard, inputs):
         a = self.args
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, _lm, sse) = batch
         S_global = S_global or sc.S
@@ -220,6 +231,10 @@ class GanTrainer:
 
     def g_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """generator_step (train.py:432-484)."""
+        with self._scope():
+            return self._g_step(batch, sc, S_global, B_global, shard, inputs)
+
+    def _g_step(self, batch, sc, S_global, B_global, shard, inputs):
         a = self.args
         G, D, ops = self.G, self.D, self.ops
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, loss_mask, sse) = batch
@@ -390,30 +405,35 @@ class GraphedTrainer:
         # captured; a failed capture would poison the stream).
         self.segments = []
         self.pair = []
-        pool = torch.cuda.graph_pool_handle()
         dp = trainer.dp
+        params = trainer.g_params + trainer.d_params
         cap.wait_stream(torch.cuda.current_stream())
         if not (dp.on and dp.world > 1):
             # one rank: TWO graphs, each starting with the H2D copy of its own
             # pinned staging buffer, replayed alternately -- the next replay is
             # queued behind the running one with no host copy between them,
             # and the host fills buffer i while graph i's previous replay
-            # (two steps back) is known to be done
+            # (two steps back) is known to be done.  Each graph has its own
+            # memory pool: its outputs (the losses, every p.grad) can then
+            # never share memory with the other graph's temporaries, so they
+            # stay intact while the other graph replays.
             for i in range(2):
                 K.clear_fold_cache()   # every fold the replays need must be a node of this graph
                 with torch.cuda.stream(cap):
                     g = torch.cuda.CUDAGraph()
-                    g.capture_begin(pool=pool)
+                    g.capture_begin(pool=torch.cuda.graph_pool_handle())
                     self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
                     losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
                     g.capture_end()
-                self.pair.append((g, losses))
+                self.pair.append((g, losses, [(p, p.grad) for p in params]))
             torch.cuda.current_stream().wait_stream(cap)
             torch.cuda.synchronize()
+            K.clear_fold_cache()
             self.done_ev = [None, None]
-            self.losses = self.pair[0][1]
+            self.losses = self.pair[1][1]
             return
         K.clear_fold_cache()   # every fold the replays need must be a node of the graph
+        pool = torch.cuda.graph_pool_handle()   # the segments replay in capture order: one shared pool
         with torch.cuda.stream(cap):
             g = torch.cuda.CUDAGraph()
             g.capture_begin(pool=pool)
@@ -433,6 +453,7 @@ class GraphedTrainer:
             self.segments.append((g, None))
         torch.cuda.current_stream().wait_stream(cap)
         torch.cuda.synchronize()
+        K.clear_fold_cache()
 
     def _load(self, z_d, z_g, y):
         i = self.cur
@@ -465,18 +486,32 @@ class GraphedTrainer:
             if z_g is not None:
                 h_zg.copy_(z_g)
             h_y.copy_(y)
-            g, self.losses = self.pair[i]
+            g, self.losses, grads = self.pair[i]
             g.replay()
             ev = torch.cuda.Event()
             ev.record()
             self.done_ev[i] = ev
+            self._after_replay(grads)
             return self.losses
         self._load(*self.t.draw_inputs(*self.span))
         for g, tensors in self.segments:
             g.replay()
             if tensors is not None:
                 self.t.dp.allreduce_(tensors)
+        self._after_replay(None)
         return self.losses
+
+    @staticmethod
+    def _after_replay(grads):
+        """Leave eager code a consistent view: every p.grad is the gradient
+        the replayed graph consumed (with two graphs, the other graph's
+        tensors would be one step old), and the fold cache is dropped -- the
+        replay updated the weights in place without moving their version
+        counters, so a cached fold would be stale for an eager forward."""
+        if grads is not None:
+            for p, gr in grads:
+                p.grad = gr
+        K.clear_fold_cache()
 
 
 def shard_batch(batch, sc, s0, s1):

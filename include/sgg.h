@@ -401,8 +401,8 @@ int sgg_lstm_bwd_split(const float* A, const float* Whh, const float* Wp, const 
                        const float* dout2, int bsplit, int T, int B, int H, float* dh0, float* drel_in,
                        float* drel_tot, float* wpart, void* stream);
 /* Encoder backward (the four-wave family) of steps t_stop .. T-1 only, input
- * gradients only: drel_in rows t >= t_stop are written, rows below are left
- * untouched, no weight gradients, no dh0 -- the generator step's pass through
+ * gradients only: drel_in rows t >= t_stop are computed, rows below are set
+ * to zero (their gradient is not wanted), no weight gradients, no dh0 -- the generator step's pass through
  * the frozen discriminator, whose observed-part inputs need no gradient.
  * Other arguments as sgg_lstm_bwd (decoder = 0). */
 int sgg_lstm_bwd_tail(const float* A, const float* Whh, const float* h_all, const float* c_all,

@@ -610,6 +610,77 @@ def fx_eval(splits, modes=EVAL_MODES):
         json.dump(res, f, indent=1, sort_keys=True)
 
 
+# ----------------------------------------------------------------------------
+# trained checkpoints of the configs[0] families (sgan-models / sgan-p-models)
+# ----------------------------------------------------------------------------
+TRAINED = [("sgan-models", s, 12) for s in SPLITS] + [("sgan-p-models", s, 12) for s in SPLITS] + \
+          [("sgan-models", "eth", 8), ("sgan-p-models", "zara1", 8)]
+TRAINED_ARGS = ("obs_len", "pred_len", "embedding_dim", "encoder_h_dim_g", "decoder_h_dim_g", "mlp_dim", "num_layers",
+                "noise_dim", "noise_type", "noise_mix_type", "pooling_type", "pool_every_timestep", "dropout",
+                "bottleneck_dim", "neighborhood_size", "grid_size", "batch_norm", "skip", "delim", "dataset_name")
+
+
+def safe_load(path):
+    """torch.load with the weights-only unpickler (no code from the file is
+    executed); collections.defaultdict is allow-listed because the upstream
+    checkpoints store their metric histories in one.  The group-family
+    checkpoints (sgan-gat, sgan-g(-p), sgangat) are refused by this loader
+    (SETITEMS on a defaultdict) and are not used."""
+    import collections
+    with torch.serialization.safe_globals([collections.defaultdict]):
+        return torch.load(path, weights_only=True, map_location="cpu")
+
+
+def fx_trained():
+    """Trained upstream Social-GAN checkpoints (BASELINE configs[0]: the
+    sgan-models family; and sgan-p-models): their g_state and args, and the
+    reference's best-of-20 ADE / FDE on the test split (evaluate_model.py:
+    72-99 with the upstream context line models.py:898, seed 0), batch 64 on
+    every split, plus ETH at batch_size 1 for sgan-models/eth_12 (configs[0]
+    literally).  -> trained.npz, evaluate_trained.json"""
+    arrs, res = {}, {}
+    for fam, split, pl in TRAINED:
+        tag = "%s/%s_%d" % (fam, split, pl)
+        ck = safe_load(os.path.join(REF, "models", fam, "%s_%d_model.pt" % (split, pl)))
+        a = dict(ck["args"])
+        for k, v in ck["g_state"].items():
+            arrs[tag + "/g/" + k] = v.numpy().copy()
+        res.setdefault("args", {})[tag] = {k: a[k] for k in TRAINED_ARGS}
+        pooling = a["pooling_type"] if a["pooling_type"] not in (None, "none") else None
+        g = M.TrajectoryGenerator(
+            obs_len=a["obs_len"], pred_len=a["pred_len"], embedding_dim=a["embedding_dim"],
+            encoder_h_dim=a["encoder_h_dim_g"], decoder_h_dim=a["decoder_h_dim_g"], mlp_dim=a["mlp_dim"],
+            num_layers=a["num_layers"], noise_dim=a["noise_dim"], noise_type=a["noise_type"],
+            noise_mix_type=a["noise_mix_type"], pooling_type=a["pooling_type"],
+            pool_every_timestep=a["pool_every_timestep"], dropout=a["dropout"], bottleneck_dim=a["bottleneck_dim"],
+            neighborhood_size=a["neighborhood_size"], grid_size=a["grid_size"], batch_norm=a["batch_norm"],
+            n_units=[40, 16, 40], n_heads=1, dropout1=0, alpha=0.2)
+        in_dim = a["encoder_h_dim_g"] + (a["bottleneck_dim"] if pooling else 0)
+        g.mlp_decoder_context = M.make_mlp([in_dim, a["mlp_dim"], a["decoder_h_dim_g"] - a["noise_dim"][0]],
+                                           activation="relu", batch_norm=a["batch_norm"], dropout=a["dropout"])
+        r = g.load_state_dict(ck["g_state"], strict=False)
+        assert not r.unexpected_keys, r.unexpected_keys
+        assert all(k.startswith(("gatencoder.", "gcn_module.")) for k in r.missing_keys), r.missing_keys
+        g.train()
+        g.forward = types.MethodType(
+            lambda self, ot, orl, sse, og, user_noise=None: _vanilla_forward(
+                self, dict(obs_traj=ot, obs_traj_rel=orl, seq_start_end=sse), user_noise), g)
+        batches = [64] + ([1] if (fam, split, pl) == ("sgan-models", "eth", 12) else [])
+        for bs in batches:
+            ea = EV.AttrDict(dict(a))
+            ea["batch_size"], ea["loader_num_workers"] = bs, 0
+            _, loader = DL.data_loader(ea, os.path.join(REF, "datasets_group", split, "test"))
+            torch.manual_seed(0)
+            t0 = time.time()
+            ade, fde = EV.evaluate(ea, loader, g, 20)
+            res["%s/b%d" % (tag, bs)] = dict(ade=float(ade), fde=float(fde), seconds=time.time() - t0,
+                                             num_seq=len(loader.dataset))
+            print(tag, bs, res["%s/b%d" % (tag, bs)], flush=True)
+    save("trained.npz", arrs)
+    with open(os.path.join(HERE, "evaluate_trained.json"), "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+
+
 def copy_test_data():
     for split in SPLITS:
         src = os.path.join(REF, "datasets_group", split, "test")
@@ -676,7 +747,7 @@ def _cpu_model():
 
 
 ALL = dict(weights=fx_weights, pool=fx_pool, gat=fx_gat, gcn=fx_gcn, gen=fx_gen, sgangat=fx_sgangat,
-           vanilla=fx_vanilla, disc=fx_disc,
+           vanilla=fx_vanilla, disc=fx_disc, trained=fx_trained,
            train=fx_train_step, data=copy_test_data, timing=fx_cpu_timing)
 
 if __name__ == "__main__":

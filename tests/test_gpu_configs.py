@@ -191,60 +191,111 @@ def _oracle_pair(g, d):
     return og, od
 
 
-# batch seed of the 64-ped generator check: the BatchGAT scores' smallest
-# distance to the LeakyReLU kink is 1.4e-5 of their range here (float64), so
-# fp32 rounding cannot flip a branch; on a typical seed it is ~5e-7 (a few
-# ulps), where any fp32 path -- this one, or torch on the CPU -- may take the
-# other branch for one (i, j) pair and move a near-cancelling gradient sum
-# such as layer_stack.1.a_src by 1e-3 (tools/diag_gen_err.py)
-SEED64 = 73
+def _sgat_grads(og, batch, z, dy, flips=(), record=None):
+    """Oracle generator forward + backward with the BatchGAT LeakyReLU of the
+    listed (call, head, i, j) score entries on the OTHER branch (slope 1 <->
+    0.2; at |z| ~ 0 the value is the same to rounding).  record: gets every
+    call's raw scores z = src_i + dst_j.  -> (output, {param: grad})."""
+    from oracle import sgan_oracle as O
+    cls = O.BatchMultiHeadGraphAttention
+    orig = cls.forward
+    calls = [0]
 
-
-def gat_kink_margin(og, run):
-    """min |src_i + dst_j| / max over every BatchGAT layer and scene of `run`."""
-    m = []
-
-    def hook(mod, inp, out):
-        hp = torch.einsum("nf,hfo->hno", inp[0], mod.w)
-        z = ((hp @ mod.a_src) + (hp @ mod.a_dst).transpose(1, 2)).detach().abs()
-        m.append(float(z.min() / z.max()))
-    hs = [layer.register_forward_hook(hook) for layer in og.gatencoder.gat_net.layer_stack]
+    def fwd(self, x):
+        hp = torch.einsum("nf,hfo->hno", x, self.w)
+        zz = (hp @ self.a_src) + (hp @ self.a_dst).transpose(1, 2)
+        c = calls[0]
+        calls[0] += 1
+        if record is not None:
+            record.append(zz.detach().clone())
+        slope = torch.where(zz > 0, torch.ones_like(zz), torch.full_like(zz, 0.2)).detach()
+        for (cc, h, i, j) in flips:
+            if cc == c:
+                slope[h, i, j] = 1.2 - slope[h, i, j]
+        out = torch.softmax(zz * slope, dim=-1) @ hp
+        return out + self.bias if self.bias is not None else out
+    obs, obs_rel, sse, obs_g = batch
+    og.zero_grad()
+    cls.forward = fwd
     try:
-        out = run()
+        y = og(obs, obs_rel, sse, obs_g, user_noise=z)
+        (y * dy).sum().backward()
     finally:
-        for h in hs:
-            h.remove()
-    return out, min(m)
+        cls.forward = orig
+    return y.detach(), {k: p.grad.detach().clone() for k, p in og.named_parameters() if p.grad is not None}
 
 
-def test_sgangat_64ped_generator_vs_oracle():
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_sgangat_64ped_generator_error_ratio(seed):
+    """configs[4] generator (sgangat-g-p, 64-ped scenes) forward + backward on
+    unpicked seeds, judged by the error the fp32 HIP path makes against a
+    float64 oracle RELATIVE to the error equally valid fp32 evaluations make:
+    the fp32 CPU oracle on the exact inputs and on four copies whose inputs
+    and weights are moved by one ulp at random (the path is full of
+    discontinuities -- ReLU / LeakyReLU kinks, max-pool argmax near-ties --
+    which any fp32 evaluation may resolve either way, and the GCN's randn
+    weights amplify the forward's rounding).  Per parameter:
+    |HIP - f64| <= 2 max_v |CPU32_v - f64| + 1e-5 of the tensor's scale + the
+    kink allowance (a BatchGAT score within 1e-5 of its range from the
+    LeakyReLU kink: the float64 oracle re-run with each such entry on the
+    other branch, the summed |gradient change| allowed on top)."""
     from sgan.data.synthetic import synthetic_batch
     g, d = reference_gd("sgangat")
     og, _ = _oracle_pair(g, d)
-    # the oracle in float64: the check then measures the fp32 HIP path's own error
-    og = og.double()
-    b = synthetic_batch(SIZES64, seed=SEED64)
+    b = synthetic_batch(SIZES64, seed=seed)
     obs, _, obs_rel, _, _, _, obs_g, _, _, _, sse = b
-    torch.manual_seed(SEED64)
-    z = torch.randn(len(SIZES64), 8)
-    dy = torch.randn(12, sum(SIZES64), 2)
+    gen = torch.Generator().manual_seed(seed)
+    z = torch.randn(len(SIZES64), 8, generator=gen)
+    dy = torch.randn(12, sum(SIZES64), 2, generator=gen)
+    # fp32 CPU oracle: exact inputs, and four 1-ulp perturbations of inputs + weights
+    sd0 = {k: v.clone() for k, v in og.state_dict().items()}
+    v32 = []
+    for v in range(5):
+        pg = torch.Generator().manual_seed(1000 * seed + v)
+        ulp = lambda t: t if v == 0 else t * (1 + torch.randint(-1, 2, t.shape, generator=pg).float() * 2.0 ** -23)
+        og.load_state_dict({k: ulp(t) for k, t in sd0.items()})
+        v32.append(_sgat_grads(og, (ulp(obs), ulp(obs_rel), sse, obs_g), z, dy))
+    og.load_state_dict(sd0)
+    # float64 oracle, its scores, and the near-kink flips
+    og64 = og.double()
     torch.set_default_dtype(torch.float64)
     try:
-        y_ref, margin = gat_kink_margin(og, lambda: og(obs.double(), obs_rel.double(), sse, obs_g.double(),
-                                                       user_noise=z.double()))
-        (y_ref * dy.double()).sum().backward()
+        b64 = (obs.double(), obs_rel.double(), sse, obs_g.double())
+        rec = []
+        y64, g64 = _sgat_grads(og64, b64, z.double(), dy.double(), record=rec)
+        near = []
+        for c, zz in enumerate(rec):
+            rng = float(zz.abs().max())
+            for h, i, j in (zz.abs() < 1e-5 * rng).nonzero().tolist():
+                near.append((c, h, i, j))
+        assert len(near) <= 24, len(near)
+        allow = {k: torch.zeros_like(v) for k, v in g64.items()}
+        for p in near:
+            _, gp = _sgat_grads(og64, b64, z.double(), dy.double(), flips=[p])
+            for k in allow:
+                allow[k] += (gp[k] - g64[k]).abs()
     finally:
         torch.set_default_dtype(torch.float32)
-    assert margin > 1e-5, margin
     y = g(obs.to(DEV), obs_rel.to(DEV), sse.to(DEV), obs_g.to(DEV), user_noise=z.to(DEV))
     (y * dy.to(DEV)).sum().backward()
-    close(y, y_ref, rtol=1e-4, what="sgangat-64 out")
-    ref_g = {k: p.grad for k, p in og.named_parameters() if p.grad is not None}
-    fl = 1e-2 * max(float(v.abs().max()) for v in ref_g.values())
+    e_y = float((y.detach().cpu().double() - y64).abs().max())
+    e_y32 = max(float((yv.double() - y64).abs().max()) for yv, _ in v32)
+    scale_y = float(y64.abs().max())
+    assert e_y <= 2 * e_y32 + 1e-5 * scale_y, ("out", e_y, e_y32, scale_y)
+    rows = []
     for k, p in g.named_parameters():
-        if k in ref_g:
-            close(p.grad, ref_g[k], rtol=1e-3 if k.endswith("stack.0.bias") else 2e-4, floor=fl,
-                  what="sgangat-64 d" + k)
+        if k not in g64:
+            continue
+        ref = g64[k]
+        e_hip = float((p.grad.detach().cpu().double() - ref).abs().max())
+        e_cpu = max(float((gv[k].double() - ref).abs().max()) for _, gv in v32)
+        tol = 2 * e_cpu + 1e-5 * float(ref.abs().max()) + float(allow[k].max())
+        rows.append((k, e_hip, e_cpu, tol, float(ref.abs().max())))
+    print("seed %d: %d near-kink scores" % (seed, len(near)))
+    for r in rows:
+        print("  %-50s hip %.3e cpu32 %.3e tol %.3e scale %.3e" % r)
+    bad = [r for r in rows if r[1] > r[3]]
+    assert not bad, bad
 
 
 def test_sgangat_64ped_train_step_vs_oracle():
@@ -572,3 +623,107 @@ def test_real_data_training_device_path_equals_host_path():
     assert la == lb, (la, lb)
     for k in wa:
         assert torch.equal(wa[k], wb[k]), k
+
+
+# ---------------------------------------------------------------------------
+# configs[0] on TRAINED checkpoints through the reference's get_generator
+# ---------------------------------------------------------------------------
+def get_generator(checkpoint):
+    """scripts/evaluate_model.py:20-55 restated: TrajectoryGenerator(**args)
+    with NO family hint, then a strict load of g_state, .cuda(), .train().
+    (The upstream checkpoints' args lack the group-model keys hidden_units /
+    n_heads / dropout1 / alpha that the reference reads at :23-51 -- its own
+    script raises on them -- so they take train.py's defaults here.)"""
+    from sgan.models import TrajectoryGenerator
+    a = dict(dict(hidden_units="16", n_heads=1, dropout1=0, alpha=0.2), **checkpoint["args"])
+    n_units = [40] + [int(x) for x in a["hidden_units"].strip().split(",")] + [40]
+    g = TrajectoryGenerator(obs_len=a["obs_len"], pred_len=a["pred_len"], embedding_dim=a["embedding_dim"],
+                            encoder_h_dim=a["encoder_h_dim_g"], decoder_h_dim=a["decoder_h_dim_g"],
+                            mlp_dim=a["mlp_dim"], num_layers=a["num_layers"], noise_dim=tuple(a["noise_dim"]),
+                            noise_type=a["noise_type"], noise_mix_type=a["noise_mix_type"],
+                            pooling_type=a["pooling_type"], pool_every_timestep=a["pool_every_timestep"],
+                            dropout=a["dropout"], bottleneck_dim=a["bottleneck_dim"],
+                            neighborhood_size=a["neighborhood_size"], grid_size=a["grid_size"],
+                            batch_norm=a["batch_norm"], n_units=n_units, n_heads=a["n_heads"],
+                            dropout1=a["dropout1"], alpha=a["alpha"]).cuda()
+    g.load_state_dict(checkpoint["g_state"])
+    g.cuda()
+    g.train()
+    return g
+
+
+def _trained_checkpoint(tag):
+    ev = json.load(open(os.path.join(GOLDEN, "evaluate_trained.json")))
+    f = npz("trained.npz")
+    sd = {k[len(tag) + 3:]: torch.from_numpy(f[k]) for k in f.files if k.startswith(tag + "/g/")}
+    return dict(args=ev["args"][tag], g_state=sd), ev
+
+
+def test_trained_checkpoints_evaluate_through_get_generator():
+    """configs[0] (sgan-models, ETH, batch 1) and every other loadable trained
+    upstream checkpoint (sgan-models / sgan-p-models, all five splits at
+    pred_len 12, plus pred_len 8 models): the reference's get_generator
+    (no family keyword, strict load) + best-of-20 evaluation reproduces the
+    reference's ADE / FDE within 1e-3 relative (north_star)."""
+    from sgan.evaluate import evaluate_split
+    ev = json.load(open(os.path.join(GOLDEN, "evaluate_trained.json")))
+    runs = sorted(k for k in ev if k != "args")
+    assert len(runs) == 13
+    for run in runs:
+        tag, bs = run.rsplit("/b", 1)
+        ck, _ = _trained_checkpoint(tag)
+        g = get_generator(ck)
+        assert g.graph == "vanilla"
+        a = ck["args"]
+        split = a["dataset_name"]
+        torch.manual_seed(0)
+        ade, fde = evaluate_split(g, os.path.join(GOLDEN, "datasets_group", split, "test"), num_samples=20,
+                                  batch_size=int(bs), obs_len=a["obs_len"], pred_len=a["pred_len"])
+        ref = ev[run]
+        assert abs(ade - ref["ade"]) <= 1e-3 * ref["ade"], (run, ade, ref)
+        assert abs(fde - ref["fde"]) <= 1e-3 * ref["fde"], (run, fde, ref)
+
+
+def test_trained_eth_batch1_evaluate_loop_vs_reference():
+    """configs[0] literally: sgan-models/eth_12 at batch 1 through the
+    reference's own evaluate loop (scripts/evaluate_model.py:72-99, 20
+    separate generator calls per batch) on the product generator."""
+    from oracle import sgan_oracle as O
+    from sgan.data.loader import data_loader
+    from sgan.evaluate import _Args
+    ck, ev = _trained_checkpoint("sgan-models/eth_12")
+    g = get_generator(ck)
+    a = _Args(obs_len=8, pred_len=12, skip=1, delim="tab", batch_size=1, loader_num_workers=0)
+    _, loader = data_loader(a, os.path.join(GOLDEN, "datasets_group", "eth", "test"))
+    torch.manual_seed(0)
+    ade, fde = O.evaluate(loader, g, num_samples=20, device=DEV)
+    ref = ev["sgan-models/eth_12/b1"]
+    assert abs(ade - ref["ade"]) <= 1e-3 * ref["ade"], (ade, ref)
+    assert abs(fde - ref["fde"]) <= 1e-3 * ref["fde"], (fde, ref)
+
+
+@pytest.mark.parametrize("graph", ["gat", "gcn", "sgangat", "vanilla"])
+def test_every_family_strict_loads_through_get_generator(graph):
+    """A checkpoint of each family (the fixtures' reference-built weights)
+    loads strictly through get_generator without `graph=` and reproduces the
+    family's reference generator output."""
+    if graph == "vanilla":
+        f = npz("gen_fwd_vanilla.npz")
+        sd = {k[len("pool/w/"):]: torch.from_numpy(f[k]) for k in f.files if k.startswith("pool/w/")}
+        pre = "pool/synth/"
+    else:
+        g0, _ = reference_gd(graph)
+        sd = {k: v.detach().cpu() for k, v in g0.state_dict().items()}
+        f = npz("gen_fwd_%s.npz" % graph)
+        pre = "synth/"
+    args = dict(obs_len=8, pred_len=12, embedding_dim=16, encoder_h_dim_g=32, decoder_h_dim_g=32, mlp_dim=64,
+                num_layers=1, noise_dim=(8,), noise_type="gaussian", noise_mix_type="global",
+                pooling_type="pool_net", pool_every_timestep=False, dropout=0.0, bottleneck_dim=8,
+                neighborhood_size=2.0, grid_size=8, batch_norm=False, hidden_units="16", n_heads=4, dropout1=0,
+                alpha=0.2)
+    g = get_generator(dict(args=args, g_state=sd))
+    assert g.graph == graph
+    with torch.no_grad():
+        y = g(T(f[pre + "obs_traj"]), T(f[pre + "obs_traj_rel"]), T(f[pre + "seq_start_end"]),
+              T(f[pre + "obs_traj_g"]), user_noise=T(f[pre + "noise"]))
+    close(y, f[pre + "out"], rtol=1e-4, what="%s via get_generator" % graph)

@@ -612,16 +612,40 @@ def test_head_bce_fused_backward_equals_separate(total, monkeypatch):
         monkeypatch.setattr(K, "HEAD_BCE", fused)
         seq.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)
-        scores = K.head(x, spec)
-        if total:
-            addend = torch.tensor(0.4, device=DEV, requires_grad=True)
-            _, loss = K.bce_pair_total(scores, 1280, ya, yb, 0.5, addend * 1.0)
-        else:
-            loss = K.bce_pair(scores, 1280, ya, yb, 0.5)
-        loss.backward(torch.tensor(1.3, device=DEV))
+        with K.bce_handoff():
+            scores = K.head(x, spec)
+            assert (getattr(scores, "_sgg_bce_link", None) is not None) == fused
+            if total:
+                addend = torch.tensor(0.4, device=DEV, requires_grad=True)
+                _, loss = K.bce_pair_total(scores, 1280, ya, yb, 0.5, addend * 1.0)
+            else:
+                loss = K.bce_pair(scores, 1280, ya, yb, 0.5)
+            loss.backward(torch.tensor(1.3, device=DEV))
         grads.append([x.grad.clone()] + [p.grad.clone() for p in seq.parameters()])
     for a, b in zip(*grads):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_head_scores_gradient_is_real_outside_the_trainer():
+    """Outside the trainer's steps (no bce_handoff scope) the head's scores
+    carry no BceLink: autograd.grad of a BCE loss w.r.t. the scores returns
+    the BCE gradient itself (sgg_bce_bwd), equal to torch's."""
+    from sgan import kernels as K
+    from sgan.models import make_mlp
+    torch.manual_seed(4)
+    seq = make_mlp([48, 64, 1], batch_norm=False).to(DEV)
+    x = torch.randn(640, 48, device=DEV, requires_grad=True)
+    scores = K.head(x, K.head_ok(seq))
+    assert getattr(scores, "_sgg_bce_link", None) is None
+    ya, yb = torch.tensor(0.0, device=DEV), torch.tensor(0.9, device=DEV)
+    loss = K.bce_pair(scores, 320, ya, yb, 1.0)
+    (gs,) = torch.autograd.grad(loss, scores)
+    s = scores.detach().double().requires_grad_(True)
+    y = torch.cat([torch.zeros(320, 1), torch.full((320, 1), 0.9)]).double().to(DEV)
+    bce = lambda v, t: (v.clamp(min=0) - v * t + (1 + (-v.abs()).exp()).log()).mean()
+    ref = bce(s[:320], y[:320]) + bce(s[320:], y[320:])
+    (gr,) = torch.autograd.grad(ref, s)
+    torch.testing.assert_close(gs.double(), gr, rtol=1e-5, atol=1e-8)
 
 
 @pytest.mark.parametrize("rows,R,E,ld,M,Nn,R_x",[(160, 192, 16, 16, 48, 2, 30720), (80, 512, 16, 64, 32, 512, 1280),
@@ -676,13 +700,17 @@ def test_grad_finish_bitwise_equals_three_launches(rows, R, E, ld, M, Nn, R_x):
         eq(dbe2, dbe2_ref, "fold dbe (colsum dbias)")
 
 
-def test_graphed_trainer_equals_eager():
+@pytest.mark.parametrize("replays", [2, 3])
+def test_graphed_trainer_equals_eager(replays):
     """The HIP-graph replay of a training iteration (GraphedTrainer) consumes
     the host RNGs in the same order and produces the same updates as the eager
-    GanTrainer."""
+    GanTrainer -- after an even and an odd number of replays (the two
+    alternating graphs), and eager code afterwards sees the state of the LAST
+    replay: every p.grad is the gradient that replay consumed, and an eager
+    discriminator forward uses the updated weights (no stale cached fold)."""
     from sgan.data.synthetic import synthetic_batch
     from sgan.scene import SceneIndex
-    from sgan.train_step import GanTrainer, GraphedTrainer
+    from sgan.train_step import GanTrainer, GraphedTrainer, _sse_of
     batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
     res = []
     for graphed in (False, True):
@@ -693,21 +721,31 @@ def test_graphed_trainer_equals_eager():
         random.seed(9)
         if graphed:
             gt = GraphedTrainer(tr, batch, sc, warmup=2)
-            for _ in range(2):
+            for _ in range(replays):
                 ld, lg = gt.step()
         else:
-            for _ in range(4):
+            for _ in range(2 + replays):
                 ld, lg = tr.step(batch, sc)
         torch.cuda.synchronize()
         ws = {"g." + k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
         ws.update({"d." + k: v.detach().cpu().clone() for k, v in d.state_dict().items()})
-        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws))
-    (la, wa), (lb, wb) = res
+        gr = {"g." + k: p.grad.detach().cpu().clone() for k, p in g.named_parameters() if p.grad is not None}
+        gr.update({"d." + k: p.grad.detach().cpu().clone() for k, p in d.named_parameters() if p.grad is not None})
+        traj_rel = torch.cat([batch[2], batch[3]], 0)
+        with torch.no_grad():
+            scores = d(batch[0], traj_rel, _sse_of(sc), scenes=sc).cpu()
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws, gr, scores))
+    (la, wa, ga, sa), (lb, wb, gb, sb) = res
     for k in la:
         assert abs(la[k] - lb[k]) <= 1e-5 * max(1.0, abs(la[k])), (k, la[k], lb[k])
     for k in wa:
         err = (wa[k] - wb[k]).abs().max().item()
         assert err <= 1e-5 + 1e-5 * wa[k].abs().max().item(), (k, err)
+    assert sorted(ga) == sorted(gb)
+    for k in ga:
+        err = (ga[k] - gb[k]).abs().max().item()
+        assert err <= 1e-6 + 1e-5 * ga[k].abs().max().item(), ("grad", k, err)
+    assert (sa - sb).abs().max().item() <= 1e-5 + 1e-5 * sa.abs().max().item(), "eager D forward after replays"
 
 
 @pytest.mark.parametrize("nh,sizes", [(1, [1, 2, 20, 48, 13, 5]), (1, [20] * 70), (2, [20, 7, 24, 1])])

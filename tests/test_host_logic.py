@@ -104,3 +104,64 @@ def test_bench_traffic_table_lookups():
     for name in tab.get("kernels", {}):
         nb, src = b.traffic_lookup(name, (name, -1))
         assert nb >= 0 and isinstance(src, str)
+
+
+def _family_state(graph, pooling="pool_net"):
+    """A state dict of `graph`'s checkpoint family, built by an explicit-family
+    model (the layout a reference checkpoint of that family holds)."""
+    torch.manual_seed(3)
+    return {k: v.clone() for k, v in _gen(graph, pooling).state_dict().items()}
+
+
+def _reference_style_gen(pooling="pool_net", n_heads=1):
+    """TrajectoryGenerator(**checkpoint args) exactly as the reference's
+    scripts/evaluate_model.py:30-51 builds it: no family hint."""
+    from sgan.models import TrajectoryGenerator
+    return TrajectoryGenerator(obs_len=8, pred_len=12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32,
+                               mlp_dim=64, num_layers=1, noise_dim=(8,), noise_type="gaussian",
+                               noise_mix_type="global", pooling_type=pooling, pool_every_timestep=False,
+                               dropout=0.0, bottleneck_dim=8, neighborhood_size=2.0, grid_size=8, batch_norm=False,
+                               n_units=[40, 16, 40], n_heads=n_heads, dropout1=0.0, alpha=0.2)
+
+
+@pytest.mark.parametrize("graph,pooling", [("gat", "pool_net"), ("gcn", "pool_net"), ("sgangat", "pool_net"),
+                                           ("vanilla", None), ("vanilla", "pool_net")])
+def test_family_inferred_from_state_dict_on_strict_load(graph, pooling):
+    """scripts/evaluate_model.py:30-52 (construct from the checkpoint args,
+    then a strict load_state_dict of g_state) works for every checkpoint
+    family without the `graph=` keyword: the family is read off the key set,
+    the module set and its registration order are the family's (so the
+    optimizer-state order matches), and every tensor is loaded."""
+    from sgan.models import TrajectoryGenerator
+    sd = _family_state(graph, pooling)
+    assert TrajectoryGenerator.family_of(sd) == graph
+    g = _reference_style_gen(pooling)
+    g.load_state_dict(sd)                                      # strict
+    assert g.graph == graph
+    ref = _gen(graph, pooling)
+    assert [k for k, _ in g.named_parameters()] == [k for k, _ in ref.named_parameters()]
+    for k, v in g.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+
+
+def test_family_switch_keeps_shared_modules_and_sgangat_shapes():
+    """A gat -> gcn switch keeps gcn_module's parameter objects; the sgangat
+    batched-GAT head / unit lists come from the state's tensor shapes (the
+    checkpoint's `n_heads` argument is a plain int); a partial non-strict
+    load without family keys keeps the family."""
+    from sgan.models import TrajectoryGenerator
+    g = _reference_style_gen()
+    keep = g.gcn_module.gcn_intra.W[0]
+    g.load_state_dict(_family_state("gcn"))
+    assert g.graph == "gcn" and g.gcn_module.gcn_intra.W[0] is keep and hasattr(g, "mlp_decoder_context")
+    assert not hasattr(g, "gatencoder")
+    g = _reference_style_gen(n_heads=4)
+    g.load_state_dict(_family_state("sgangat"))
+    heads = [l.n_head for l in g.gatencoder.gat_net.layer_stack]
+    assert g.graph == "sgangat" and heads == [4, 1]
+    g.load_state_dict({"encoder.spatial_embedding.bias": torch.zeros(16)}, strict=False)
+    assert g.graph == "sgangat"
+    with pytest.raises(RuntimeError):                          # a genuine key mismatch still fails strictly
+        bad = _family_state("gat")
+        bad.pop("gatencoder.out_embedding.bias")
+        _reference_style_gen().load_state_dict(bad)

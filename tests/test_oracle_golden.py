@@ -206,3 +206,40 @@ def test_vanilla_generator_fixture(tag, pooling):
             close(q.grad, f[p + "dw/" + k], rtol=1e-4, floor=grad_floor(f, p + "dw/"))
             n += 1
         assert n == (24 if pooling else 18)
+
+
+def _oracle_from_trained(tag):
+    """The oracle generator built from a trained upstream checkpoint's args
+    (tests/golden/evaluate_trained.json) with its g_state (trained.npz)."""
+    ev = json.load(open(os.path.join(GOLDEN, "evaluate_trained.json")))
+    a = ev["args"][tag]
+    g = O.TrajectoryGenerator(a["obs_len"], a["pred_len"], embedding_dim=a["embedding_dim"],
+                              encoder_h_dim=a["encoder_h_dim_g"], decoder_h_dim=a["decoder_h_dim_g"],
+                              mlp_dim=a["mlp_dim"], num_layers=a["num_layers"], noise_dim=tuple(a["noise_dim"]),
+                              noise_type=a["noise_type"], noise_mix_type=a["noise_mix_type"],
+                              pooling_type=a["pooling_type"], pool_every_timestep=a["pool_every_timestep"],
+                              dropout=a["dropout"], bottleneck_dim=a["bottleneck_dim"], batch_norm=a["batch_norm"],
+                              graph="vanilla")
+    f = npz("trained.npz")
+    g.load_state_dict({k[len(tag) + 3:]: T(f[k]) for k in f.files if k.startswith(tag + "/g/")})
+    return g, a, ev
+
+
+@pytest.mark.parametrize("tag,bs", [("sgan-models/eth_12", 64), ("sgan-models/eth_12", 1),
+                                    ("sgan-p-models/hotel_12", 64), ("sgan-models/eth_8", 64)])
+def test_oracle_evaluate_trained_checkpoints(tag, bs):
+    """configs[0] on TRAINED weights: the oracle's evaluate_model restatement
+    with the upstream checkpoints' g_state (loaded by the weights-only
+    unpickler) reproduces the reference's best-of-20 ADE / FDE (seed 0)."""
+    from sgan.data.trajectories_GCN import TrajectoryDataset, seq_collate
+    from torch.utils.data import DataLoader
+    g, a, ev = _oracle_from_trained(tag)
+    split = tag.split("/")[1].split("_")[0]
+    dset = TrajectoryDataset(os.path.join(GOLDEN, "datasets_group", split, "test"), obs_len=a["obs_len"],
+                             pred_len=a["pred_len"], skip=a["skip"], delim=a["delim"])
+    torch.manual_seed(0)
+    loader = DataLoader(dset, batch_size=bs, shuffle=True, num_workers=0, collate_fn=seq_collate)
+    ade, fde = O.evaluate(loader, g, num_samples=20, pred_len=a["pred_len"])
+    ref = ev["%s/b%d" % (tag, bs)]
+    assert abs(ade - ref["ade"]) <= 1e-4 * ref["ade"], (ade, ref)
+    assert abs(fde - ref["fde"]) <= 1e-4 * ref["fde"], (fde, ref)

@@ -10,7 +10,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "group-gan-gcn-gat_amd")]
-from test_gpu_configs import SEED64, SIZES64, _oracle_pair, reference_gd  # noqa: E402
+from test_gpu_configs import SIZES64, _oracle_pair, reference_gd  # noqa: E402
+SEED64 = 73
 from sgan.data.synthetic import synthetic_batch  # noqa: E402
 
 
