@@ -719,7 +719,7 @@ def test_every_family_strict_loads_through_get_generator(graph):
     args = dict(obs_len=8, pred_len=12, embedding_dim=16, encoder_h_dim_g=32, decoder_h_dim_g=32, mlp_dim=64,
                 num_layers=1, noise_dim=(8,), noise_type="gaussian", noise_mix_type="global",
                 pooling_type="pool_net", pool_every_timestep=False, dropout=0.0, bottleneck_dim=8,
-                neighborhood_size=2.0, grid_size=8, batch_norm=False, hidden_units="16", n_heads=4, dropout1=0,
+                neighborhood_size=2.0, grid_size=8, batch_norm=False, hidden_units="16", n_heads=1, dropout1=0,
                 alpha=0.2)
     g = get_generator(dict(args=args, g_state=sd))
     assert g.graph == graph
