@@ -25,7 +25,13 @@ Prints ONE JSON line (rank 0).  Extra objects:
                launch of that kernel (profiles/, tools/pmc_traffic.py);
   cpu_baseline the CPU oracle (reference formulation) timed on this host for a
                bounded sample of the same workload, validated against the
-               real reference in the build container (ref_cpu_timing.json).
+               real reference in the build container (ref_cpu_timing.json);
+               the host's core count and CPU model beside it;
+  legs         (N = 1) the other BASELINE configurations on one GPU, each with
+               its own dominant kernel and roofline: configs[2]'s GCN
+               generator (fp32 and bf16), configs[4]'s sgangat generator on
+               64-ped scenes (bf16), and configs[3]'s per-GPU shard at N = 8
+               (512 scenes).
 """
 import argparse
 import json
@@ -48,7 +54,25 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 dense (vector == f32 MFMA), MI355X_MICR
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md
 RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)   # FLOP / byte
 CONFIG4_GLOBAL = 4096      # BASELINE configs[3]: synthetic 20-ped, batch 4096, 8 x MI355X
-TRAFFIC_TABLE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+# PMC traffic tables (tools/pmc_traffic.py), newest first
+TRAFFIC_TABLES = [os.path.join(ROOT, "profiles", f) for f in ("r03_pmc_traffic.json", "r02_pmc_traffic.json")]
+# the reference's CPU path, train iteration at batch 64, 8 threads (the survey container)
+REFERENCE_CPU_SCENES_S = 13.9
+
+# the BASELINE configurations measured beside the headline at N = 1 (one GPU each)
+LEGS = {
+    "configs1": dict(per_gpu=64, peds=20, graph="gat", prec="fp32",
+                     what="BASELINE configs[1] shape: 64 synthetic 20-ped scenes, GAT generator, fp32"),
+    "configs3_shard512": dict(per_gpu=512, peds=20, graph="gat", prec="fp32",
+                              what="configs[3]'s per-GPU shard at N = 8 (4096 / 8 = 512 scenes), GAT, fp32"),
+    "configs2_gcn_fp32": dict(per_gpu=64, peds=20, graph="gcn", prec="fp32",
+                              what="configs[2]'s GCN generator (sgan-g-p family), 64 scenes, fp32"),
+    "configs2_gcn_bf16": dict(per_gpu=64, peds=20, graph="gcn", prec="bf16",
+                              what="configs[2]'s GCN generator, 64 scenes, bf16 node transforms (fp32 accumulate)"),
+    "configs4_sgangat_bf16": dict(per_gpu=64, peds=64, graph="sgangat", prec="bf16",
+                                  what="configs[4]'s sgangat generator (sgangat-g-p family) on 64-ped scenes, "
+                                       "64 scenes, bf16 node transforms (fp32 accumulate)"),
+}
 
 
 def build_models(seed, graph="gat"):
@@ -57,7 +81,8 @@ def build_models(seed, graph="gat"):
     g = TrajectoryGenerator(8, 12, embedding_dim=16, encoder_h_dim=32, decoder_h_dim=32, mlp_dim=64, num_layers=1,
                             noise_dim=(8,), noise_type="gaussian", noise_mix_type="global", pooling_type="pool_net",
                             pool_every_timestep=False, dropout=0.0, bottleneck_dim=8, batch_norm=False,
-                            n_units=[40, 16, 40], n_heads=1, dropout1=0.0, alpha=0.2, graph=graph)
+                            n_units=[40, 16, 40], n_heads=[4, 1] if graph == "sgangat" else 1, dropout1=0.0,
+                            alpha=0.2, graph=graph)
     d = TrajectoryDiscriminator(8, 12, embedding_dim=16, h_dim=48, mlp_dim=64, num_layers=1, batch_norm=False,
                                 dropout=0.0, d_type="global")
     for m in list(g.modules()) + list(d.modules()):   # train.py:127-130 init_weights
@@ -66,11 +91,36 @@ def build_models(seed, graph="gat"):
     return g, d
 
 
+def host_cpus():
+    """(logical CPUs of the machine, CPUs this process may use, CPU model):
+    the affinity mask, further bounded by a cgroup CPU quota when one is set
+    (a GPU box's share of a large host)."""
+    total = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            usable = max(1, min(usable, int(-(-int(q) // int(per)))))
+    except (OSError, ValueError):
+        pass
+    model = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return total, usable, model
+
+
 def cpu_baseline(batch_scenes, n_peds, iters=2, threads=None):
-    """Oracle (reference formulation) D-step + G-step on the host cores."""
+    """Oracle (reference formulation) D-step + G-step on the host cores: every
+    CPU this process may use (torch.set_num_threads)."""
     from oracle import sgan_oracle as O
     from sgan.data.synthetic import synthetic_batch
-    threads = threads or min(16, os.cpu_count() or 1)
+    total, usable, model = host_cpus()
+    threads = threads or usable
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     g, d = O.build_default("gat")
@@ -92,28 +142,27 @@ def cpu_baseline(batch_scenes, n_peds, iters=2, threads=None):
                % (v.get("cpu", "?"), v["threads"], v["batch"], v["reference_scenes_per_s"],
                   v["oracle_scenes_per_s"], v["oracle_over_reference"]))
     return {"value": round(batch_scenes * iters / dt, 3), "unit": "scenes/s", "cores": threads, "kind": "port",
+            "host_cores": total, "usable_cpus": usable, "cpu_model": model,
             "sample": "%d train iterations (D-step + G-step, best_k=20) on %d x %d-ped synthetic scenes, oracle/"
-                      "sgan_oracle.py reference formulation, torch CPU fp32, %d threads (%.1f s)%s"
-                      % (iters, batch_scenes, n_peds, threads, dt, val)}
+                      "sgan_oracle.py reference formulation, torch CPU fp32, %d threads = every CPU this process may "
+                      "use (host: %d logical CPUs, %s) (%.1f s)%s"
+                      % (iters, batch_scenes, n_peds, threads, total, model, dt, val)}
 
 
 def traffic_lookup(name, key):
     """HBM bytes per launch of (kernel, launch shape) from the committed PMC
-    table (tools/pmc_traffic.py: separate rocprofv3 --pmc FETCH_SIZE /
+    tables (tools/pmc_traffic.py: separate rocprofv3 --pmc FETCH_SIZE /
     WRITE_SIZE passes of this bench with the gfx950 corrections of
-    MI355X_MICROARCH.md) -> (bytes, source): the exact launch shape when the
-    PMC run re-issued it (--pmc-target), else the kernel's mean over all its
-    launches in that run, else (None, None)."""
-    if not os.path.exists(TRAFFIC_TABLE):
-        return None, None
-    tab = json.load(open(TRAFFIC_TABLE))
-    ent = tab.get("%s|%s" % (name, list(key[1:])))
-    if ent is not None:
-        return ent["hbm_bytes"], "PMC bytes of this launch shape (%s)" % ent.get(
-            "note", "re-issued %s x" % ent.get("dispatches", 0))
-    ent = tab.get("kernels", {}).get(name)
-    if ent is not None:   # the kernel's mean over every launch of the PMC run (all its launch shapes)
-        return ent["hbm_bytes"], "PMC bytes per launch, mean over the %d launches of the PMC run" % ent["dispatches"]
+    MI355X_MICROARCH.md), newest table first -> (bytes, source): the exact
+    launch shape when a PMC run re-issued it (--pmc-target), else None."""
+    for path in TRAFFIC_TABLES:
+        if not os.path.exists(path):
+            continue
+        tab = json.load(open(path))
+        ent = tab.get("%s|%s" % (name, list(key[1:])))
+        if ent is not None:
+            return ent["hbm_bytes"], "PMC bytes of this launch shape, %s (%s)" % (
+                os.path.basename(path), ent.get("note", "re-issued %s x" % ent.get("dispatches", 0)))
     return None, None
 
 
@@ -299,6 +348,50 @@ def setup(per_gpu, peds, rank, world, dev, graph_kind):
     return trainer, batch, sc, batch_g, sc_g, kw
 
 
+def measure(spec, steps, warmup, rank, world, dev, graph_on, n_it=3):
+    """Time `steps` iterations of one configuration (HIP-graph replays), then
+    every instrumented launch of n_it eager iterations on the same inputs,
+    re-issued back to back between HIP events on its launch stream (graph
+    replays carry no events); rocprofv3's kernel trace of the same command
+    is the cross-check (profiles/)."""
+    from sgan import kernels as K
+    K.set_precision(spec["prec"])
+    try:
+        trainer, batch, sc, batch_g, sc_g, kw = setup(spec["per_gpu"], spec["peds"], rank, world, dev, spec["graph"])
+        step, graphed = make_step(trainer, batch, sc, batch_g, sc_g, kw, graph_on)
+        elapsed = timed_run(step, steps, warmup, world, dev)
+        n_it = max(1, min(steps, n_it))
+        K.timer.start()
+        for _ in range(n_it):
+            trainer.step(batch, sc, batch_g, sc_g, **kw)
+        recs = K.timer.stop()
+        timed = K.timer.replay(recs)
+    finally:
+        K.set_precision("fp32")
+    return dict(elapsed=elapsed, graphed=graphed, agg=kernel_table(timed, n_it), recs=recs, n_it=n_it)
+
+
+def top_kernels(agg, n=10):
+    top = sorted(agg.items(), key=lambda kv: -kv[1]["us_per_iter"])
+    return {k: {"us_per_iter": round(a["us_per_iter"], 1), "launches_per_iter": round(a["launches_per_iter"], 2),
+                "GB/s": round(a["bytes"] / (a["us_per_iter"] * 1e-6) / 1e9, 1),
+                "TFLOP/s": round(a["flop"] / (a["us_per_iter"] * 1e-6) / 1e12, 2)} for k, a in top[:n]}
+
+
+def leg_line(name, spec, res, steps):
+    """One extra BASELINE configuration on one GPU: its rate, its dominant
+    kernel against its roof, its top kernels."""
+    agg = res["agg"]
+    dom_name, dom = max(agg.items(), key=lambda kv: kv[1]["us_per_iter"])
+    ms = res["elapsed"] / steps * 1e3
+    return {"config": name, "workload": spec["what"], "value": round(spec["per_gpu"] / (ms * 1e-3), 2),
+            "unit": "scenes/s", "ms_per_step": round(ms, 3), "steps": steps, "scenes_per_gpu": spec["per_gpu"],
+            "peds_per_scene": spec["peds"], "generator": spec["graph"], "dtype": spec["prec"],
+            "hip_graph": res["graphed"],
+            "instrumented_launches_per_iter": round(sum(a["launches_per_iter"] for a in agg.values()), 1),
+            "roofline": roofline_of(dom_name, dom), "kernels": top_kernels(agg, 5)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,7 +400,11 @@ def main():
     ap.add_argument("--batch", type=int, default=None,
                     help="scenes per GPU (default: 64 at N = 1, BASELINE configs[1]; 4096 / N at N > 1, configs[3])")
     ap.add_argument("--peds", type=int, default=20)
-    ap.add_argument("--graph-kind", dest="graph_kind", default="gat", choices=["gat", "gcn"])
+    ap.add_argument("--graph-kind", dest="graph_kind", default="gat", choices=["gat", "gcn", "sgangat"])
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--leg", default="", choices=[""] + list(LEGS),
+                    help="measure this BASELINE configuration as the headline (e.g. for its PMC passes)")
+    ap.add_argument("--no-legs", action="store_true", help="skip the other configurations (N = 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scaling-reference", action="store_true")
     ap.add_argument("--no-real-data", action="store_true")
@@ -342,44 +439,52 @@ def main():
             dist.init_process_group(backend)
         assert dist.get_world_size() == args.gpus
 
-    from sgan import kernels as K
-
-    per_gpu = args.batch or (64 if world == 1 else CONFIG4_GLOBAL // world)
-    trainer, batch, sc, batch_g, sc_g, kw = setup(per_gpu, args.peds, rank, world, dev, args.graph_kind)
-    step, graphed = make_step(trainer, batch, sc, batch_g, sc_g, kw, args.graph)
-    elapsed = timed_run(step, args.steps, args.warmup, world, dev)
-
-    # per-kernel device time: every instrumented launch of a few eager
-    # iterations on the same inputs is recorded (graph replays carry no
-    # events), then each distinct launch is re-issued back to back between
-    # HIP events on its launch stream; rocprofv3's kernel trace of the same
-    # command is the cross-check (profiles/)
-    n_it = max(1, min(args.steps, 3))
-    K.timer.start()
-    for _ in range(n_it):
-        trainer.step(batch, sc, batch_g, sc_g, **kw)
-    recs = K.timer.stop()
-    timed = K.timer.replay(recs)
-    agg = kernel_table(timed, n_it)
+    if args.leg:
+        head = dict(LEGS[args.leg])
+    else:
+        per_gpu = args.batch or (64 if world == 1 else CONFIG4_GLOBAL // world)
+        head = dict(per_gpu=per_gpu, peds=args.peds, graph=args.graph_kind, prec=args.precision)
+    per_gpu = head["per_gpu"]
+    res = measure(head, args.steps, args.warmup, rank, world, dev, args.graph)
+    elapsed, agg, recs = res["elapsed"], res["agg"], res["recs"]
     pmc_target = None
     if args.pmc_target > 0 and rank == 0:
+        from sgan import kernels as K
         if args.pmc_kernel and args.pmc_kernel in agg:   # the roofline kernel of the graphed run
             name, a = args.pmc_kernel, agg[args.pmc_kernel]
         else:
             name, a = max(agg.items(), key=lambda kv: kv[1]["us_per_iter"])
         key = main_launch(a)[0]
         fn = next(r[4] for r in recs if r[1] == key)
-        for _ in range(args.pmc_target):
-            fn()
+        K.set_precision(head["prec"])
+        try:
+            for _ in range(args.pmc_target):
+                fn()
+        finally:
+            K.set_precision("fp32")
         torch.cuda.synchronize()
         pmc_target = {"kernel": name, "shape": list(key[1:]), "reps": args.pmc_target}
-    del timed, recs
+    del recs
+    res["recs"] = None
+
+    # the other BASELINE configurations, one GPU each (N = 1 only)
+    legs = []
+    if world == 1 and not args.no_legs and not args.leg:
+        k_leg = max(3, args.steps // 2)
+        for name, spec in LEGS.items():
+            if name == "configs1" and (head["per_gpu"], head["peds"], head["graph"], head["prec"]) == (
+                    64, 20, "gat", "fp32"):
+                continue   # the headline itself
+            r = measure(spec, k_leg, 2, 0, 1, dev, args.graph)
+            legs.append(leg_line(name, spec, r, k_leg))
+            del r
 
     scaling_ref = None
-    if world == 1 and not args.no_scaling_reference and per_gpu != CONFIG4_GLOBAL:
+    if world == 1 and not args.no_scaling_reference and per_gpu != CONFIG4_GLOBAL and not args.leg:
         # configs[3]'s 4096-scene global batch on this one GPU: the N = 1 point
         # of the strong-scaling curve the N > 1 runs measure
-        tr4, b4, sc4, bg4, scg4, kw4 = setup(CONFIG4_GLOBAL, args.peds, 0, 1, dev, args.graph_kind)
+        from sgan import kernels as K
+        tr4, b4, sc4, bg4, scg4, kw4 = setup(CONFIG4_GLOBAL, args.peds, 0, 1, dev, "gat")
         st4, gr4 = make_step(tr4, b4, sc4, bg4, scg4, kw4, args.graph)
         k4 = max(3, args.steps // 4)
         e4 = timed_run(st4, k4, 2, 1, dev)
@@ -390,16 +495,14 @@ def main():
         del tr4, b4, bg4, st4
 
     real = None
-    if world == 1 and not args.no_real_data:
+    if world == 1 and not args.no_real_data and not args.leg:
         real = real_data_leg(dev)
 
     if rank == 0:
+        n_it = res["n_it"]
         top = sorted(agg.items(), key=lambda kv: -kv[1]["us_per_iter"])
         dom_name, dom = top[0]
         roofline = roofline_of(dom_name, dom)
-        kernels = {n: {"us_per_iter": round(a["us_per_iter"], 1), "launches_per_iter": round(a["launches_per_iter"], 2),
-                       "GB/s": round(a["bytes"] / (a["us_per_iter"] * 1e-6) / 1e9, 1),
-                       "TFLOP/s": round(a["flop"] / (a["us_per_iter"] * 1e-6) / 1e12, 2)} for n, a in top[:10]}
         launches = sorted(((r["launches"] / n_it * r["ms"] * 1e3, n, r, k) for n, a in agg.items()
                            for k, r, _ in a["shapes"]), key=lambda x: -x[0])
         launch_table = [{"kernel": n, "shape": list(k[1:]), "per_iter": round(r["launches"] / n_it, 2),
@@ -415,23 +518,35 @@ def main():
         value = world * per_gpu / (elapsed / args.steps)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(per_gpu, args.peds, iters=args.cpu_iters)
+            cpu = cpu_baseline(per_gpu, head["peds"], iters=args.cpu_iters)
+        is_c1 = world == 1 and (per_gpu, head["peds"], head["graph"], head["prec"]) == (64, 20, "gat", "fp32")
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "scenes/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "weak" if world == 1 else "strong", "vs_baseline": None, "dtype": "fp32",
+            "scaling": "weak" if world == 1 else "strong",
+            "vs_baseline": round(value / REFERENCE_CPU_SCENES_S, 1) if is_c1 else None,
+            "vs_baseline_basis": "value / 13.9 scenes/s: the reference's own CPU path on this workload (train "
+                                 "iteration, batch 64, 8 threads), BASELINE.md section 2 -- the reference publishes "
+                                 "no throughput" if is_c1 else None,
+            "dtype": head["prec"],
             "data": "synthetic (random-init weights, SURVEY.md 8d recipe)",
-            "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam) of the GAT generator "
+            "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam) of the %s generator "
                                    "(scripts/train.py defaults)%s" % (
-                                       "; BASELINE configs[1] shape (batch 64)" if world == 1 and per_gpu == 64 else
+                                       head["graph"].upper(),
+                                       "; BASELINE configs[1] shape (batch 64)" if is_c1 else
                                        "; BASELINE configs[3] (4096-scene global batch)"
-                                       if world * per_gpu == CONFIG4_GLOBAL else ""),
-                       "scenes_per_gpu": per_gpu, "global_batch": per_gpu * world, "peds_per_scene": args.peds,
-                       "obs_len": 8, "pred_len": 12, "generator": args.graph_kind, "hip_graph": graphed,
+                                       if world * per_gpu == CONFIG4_GLOBAL else
+                                       "; %s" % head.get("what", "")),
+                       "scenes_per_gpu": per_gpu, "global_batch": per_gpu * world, "peds_per_scene": head["peds"],
+                       "obs_len": 8, "pred_len": 12, "generator": head["graph"], "hip_graph": res["graphed"],
                        "parallelism": "dp%d" % world},
-            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
-            "instrumented_us_per_iter": round(total_launch_us, 1), "launch_table": launch_table,
+            "roofline": roofline, "kernels": top_kernels(agg, 10), "cpu_baseline": cpu,
+            "instrumented_us_per_iter": round(total_launch_us, 1),
+            "instrumented_launches_per_iter": round(sum(a["launches_per_iter"] for a in agg.values()), 1),
+            "launch_table": launch_table,
         }
+        if legs:
+            line["legs"] = legs
         if scaling_ref is not None:
             line["scaling_reference"] = scaling_ref
         if real is not None:

@@ -37,6 +37,18 @@ class GatEncArgs(ctypes.Structure):
 
 _pargs = ctypes.POINTER(GatEncArgs)
 
+
+class GcnModArgs(ctypes.Structure):
+    """SggGcnModArgs (include/sgg.h)."""
+    _fields_ = [("X", _p), ("ldx", _i), ("X2", _p), ("ldx2", _i), ("kx1", _i), ("labels", _p), ("scene_off", _p),
+                ("S", _i), ("np", _i), ("fin", _i), ("fe", _i), ("bf16", _i), ("W0i", _p), ("W1i", _p), ("W0g", _p),
+                ("W1g", _p), ("Woe", _p), ("boe", _p), ("y", _p), ("ldy", _i), ("dy", _p), ("lddy", _i),
+                ("dy_copies", _i), ("dy_cstride", _i), ("dX", _p), ("lddx", _i), ("dX2", _p), ("lddx2", _i),
+                ("slab", _p)]
+
+
+_gargs = ctypes.POINTER(GcnModArgs)
+
 FOLD_MAX = 8   # SGG_FOLD_MAX
 
 
@@ -111,6 +123,11 @@ SIGNATURES = {
     "sgg_gatenc_saved_floats": (ctypes.c_longlong, [_i, _i, _i]),
     "sgg_gatenc_fwd": (_i, [_pargs, _p]),
     "sgg_gatenc_bwd": (_i, [_pargs, _p]),
+    "sgg_gcnmod_param_size": (_i, [_i, _i]),
+    "sgg_gcnmod_slab_rows": (_i, [_i]),
+    "sgg_gcnmod_lds_bytes": (ctypes.c_longlong, [_i, _i, _i, _i]),
+    "sgg_gcnmod_fwd": (_i, [_gargs, _p]),
+    "sgg_gcnmod_bwd": (_i, [_gargs, _p]),
     "sgg_slab_reduce": (_i, [_p, _i, _i, _p, _p]),
     "sgg_gather_batch_floats": (ctypes.c_longlong, [_i, _i, _i]),
     "sgg_gather_batch": (_i, [_p, _i, _p, _i, _i, _i, _p, _p]),

@@ -1141,6 +1141,133 @@ def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None, link=None):
     return y
 
 
+# the one-launch GCNModule (sgg_gcnmod_*); "0" forces the per-op kernels
+GCNMOD_FUSED = os.environ.get("SGG_GCNMOD_FUSED", "1") != "0"
+
+
+class _GcnMod(torch.autograd.Function):
+    """The whole GCNModule of every scene in one launch per direction
+    (sgg_gcnmod_fwd / _bwd; the backward recomputes the forward in LDS) + the
+    slab sum of the parameter gradients (sgg_slab_reduce).
+    params: gcn_intra.W.0, gcn_intra.W.1, gcn_inter.W.0, gcn_inter.W.1,
+    out_embedding weight, bias -- the slab order of sgg.h."""
+
+    @staticmethod
+    def forward(ctx, x, labels, scenes, x2, link, dy_link, bf16, *params):
+        lib = _lib()
+        ctx.link, ctx.dy_link = link, dy_link
+        x = _rows(x, "x")
+        B = x.shape[0]
+        if x2 is not None:
+            x2 = _rows(x2, "x2")
+            assert x2.shape[0] == B
+        ps = [_req(q, "gcn weight").contiguous() for q in params]
+        fe = ps[4].shape[0]
+        y = torch.empty(B, fe, device=x.device, dtype=torch.float32)
+        a = _gcnmod_args(x, x2, labels, scenes, ps, bf16)
+        a.y, a.ldy = N.ptr(y), fe
+        N.check(lib.sgg_gcnmod_fwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gcnmod_fwd")
+        if timer.active:
+            keep = (x, x2, y, labels, scenes, ps)
+            timer.add("sgg::gcnmod_fwd_kernel<%s>" % ("true" if bf16 else "false"), (scenes.S, B, a.fin),
+                      _gcnmod_flops(scenes, labels, a.fin, fe), 4.0 * B * (a.fin + 1 + fe),
+                      lambda a=a, keep=keep: N.check(lib.sgg_gcnmod_fwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                     "sgg_gcnmod_fwd"))
+        ctx.meta = (labels, scenes, bf16)
+        ctx.save_for_backward(x, x2, *ps)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib()
+        x, x2, *ps = ctx.saved_tensors
+        labels, scenes, bf16 = ctx.meta
+        B = x.shape[0]
+        pend = ctx.dy_link.take() if ctx.dy_link is not None else None
+        copies, cstride = 1, 0
+        if pend is not None:
+            base, copies, cstride, ld = pend
+            if dy.data_ptr() == base.data_ptr() and dy.stride(0) == ld:
+                dy = base   # rows 0 .. B of copy 0; the kernel adds the other copies
+            else:           # autograd summed in another consumer's gradient: add the copies here
+                dy = dy + sum(base.view(copies, B, ld)[c, :, :dy.shape[1]] for c in range(1, copies))
+                copies = 1
+        dy = _rows(dy, "dy")
+        a = _gcnmod_args(x, x2, labels, scenes, ps, bf16)
+        P = lib.sgg_gcnmod_param_size(a.fin, a.fe)
+        rows = lib.sgg_gcnmod_slab_rows(scenes.S)
+        dx = torch.empty(B, x.shape[1], device=x.device, dtype=torch.float32)
+        dx2 = torch.empty(B, x2.shape[1], device=x.device, dtype=torch.float32) if x2 is not None else None
+        slab = torch.empty(rows, P, device=x.device, dtype=torch.float32)
+        a.dy, a.lddy = N.ptr(dy), dy.stride(0)
+        a.dy_copies, a.dy_cstride = copies, cstride
+        a.dX, a.lddx = N.ptr(dx), dx.shape[1]
+        if dx2 is not None:
+            a.dX2, a.lddx2 = N.ptr(dx2), dx2.shape[1]
+        a.slab = N.ptr(slab)
+        N.check(lib.sgg_gcnmod_bwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gcnmod_bwd")
+        if timer.active:
+            keep = (x, x2, dy, dx, dx2, slab, labels, scenes, ps)
+            timer.add("sgg::gcnmod_bwd_kernel<%s>" % ("true" if bf16 else "false"), (scenes.S, B, a.fin),
+                      3.0 * _gcnmod_flops(scenes, labels, a.fin, a.fe),
+                      4.0 * (B * (a.fin + 1 + a.fe + a.fin) + rows * P),
+                      lambda a=a, keep=keep: N.check(lib.sgg_gcnmod_bwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                     "sgg_gcnmod_bwd"))
+        with side(slab):
+            flat = torch.empty(P, device=x.device, dtype=torch.float32)
+            N.check(lib.sgg_slab_reduce(N.ptr(slab), rows, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+        grads, o = [], 0
+        for q in ps:
+            grads.append(flat[o:o + q.numel()].view_as(q))
+            o += q.numel()
+        if ctx.link is not None and ctx.needs_input_grad[0]:
+            ctx.link.put(dx)   # added by the pooling backward (the other consumer of x), which runs next
+            dx = None
+        return (dx, None, None, dx2, None, None, None) + tuple(grads)
+
+
+def _gcnmod_flops(scenes, labels, fin, fe):
+    """GCNModule forward FLOP (models.py:628-712), minimal formulation: per
+    scene of N peds the two intra layers on its G group rows 2 G (fin 72 + 72
+    16), the inter layers on one row 2 (16 72 + 72 16), out_embedding 2 N 32 fe.
+    G is bounded by N (the label structure is device data; the bound keeps the
+    count host-only)."""
+    import numpy as np
+    n = np.diff(scenes.host_off).astype(np.float64)
+    return float((2 * n * (fin * 72 + 72 * 16) + 2 * (16 * 72 + 72 * 16) * (n > 0) + 2 * n * 32 * fe).sum())
+
+
+def _gcnmod_args(x, x2, labels, scenes, ps, bf16):
+    a = N.GcnModArgs()
+    a.X, a.ldx = N.ptr(x), x.stride(0)
+    fin = x.shape[1]
+    if x2 is not None:
+        a.X2, a.ldx2, a.kx1 = N.ptr(x2), x2.stride(0), x.shape[1]
+        fin += x2.shape[1]
+    a.labels, a.scene_off = N.ptr(labels), N.ptr(scenes.scene_off)
+    a.S, a.np, a.fin, a.fe, a.bf16 = scenes.S, max(scenes.max_n, 1), fin, ps[4].shape[0], int(bool(bf16))
+    a.W0i, a.W1i, a.W0g, a.W1g, a.Woe, a.boe = [N.ptr(q) for q in ps]
+    return a
+
+
+def gcn_module_fused_ok(scenes, fin, fe, params_ok=True):
+    """The fused GCNModule path holds a scene's group structure in one wavefront."""
+    if not GCNMOD_FUSED or not params_ok or scenes.max_n > 64 or scenes.max_n < 1:
+        return False
+    return 0 <= _lib().sgg_gcnmod_lds_bytes(scenes.max_n, fin, fe, 1) <= 160 * 1024
+
+
+def gcn_module(x, labels, scenes, params, x2=None, link=None):
+    """GCNModule.forward (models.py:628-712) for all scenes: (B, fin) -> (B, fe),
+    the input optionally as two column blocks [x | x2]; link as gat_encoder."""
+    lab = _req(labels, "labels").contiguous().view(-1)
+    dl = CopiesLink() if torch.is_grad_enabled() else None
+    y = _GcnMod.apply(x, lab, scenes, x2, link, dl, _PRECISION == "bf16", *params)
+    if dl is not None:
+        y._sgg_copies_link = dl   # found by decoder_init (its only consumer in the generator)
+    return y
+
+
 class _SegNorm(torch.autograd.Function):
     """Per-segment instance normalisation (sgg_seg_norm_fwd / _bwd)."""
 

@@ -429,6 +429,19 @@ class GCNModule(nn.Module):
         self.gcn_inter = GCN(input_dim=16, hidden_dim=hidden_dim, out_dim=out_dim, gcn_layers=gcn_layers)
         self.out_embedding = nn.Linear(out_dim * 2, final_dim)
 
+    def fused_params(self):
+        """[W0, W1 of gcn_intra, W0, W1 of gcn_inter, out_embedding weight,
+        bias] when the module has the shapes of the fused kernel (two layers,
+        hidden 72, out 16: GCNModule's construction in TrajectoryGenerator),
+        else None."""
+        gi, gg = self.gcn_intra.W, self.gcn_inter.W
+        if len(gi) != 2 or len(gg) != 2 or self.out_embedding.in_features != 32:
+            return None
+        if (gi[0].shape[1], tuple(gi[1].shape), tuple(gg[0].shape), tuple(gg[1].shape)) != (72, (72, 16), (16, 72),
+                                                                                          (72, 16)):
+            return None
+        return [gi[0], gi[1], gg[0], gg[1], self.out_embedding.weight, self.out_embedding.bias]
+
     def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None, link=None):
         """h_states: (B, 40), or the pair (encoder state, pooled vector) whose
         concatenation it is (the fused kernel reads both blocks in place).
@@ -437,6 +450,14 @@ class GCNModule(nn.Module):
         if isinstance(h_states, (tuple, list)):
             h_states, x2 = h_states
         sc = _scenes(seq_start_end, h_states.device, scenes)
+        params = self.fused_params()
+        fin = h_states.shape[1] + (x2.shape[1] if x2 is not None else 0)
+        if params is not None and params[0].shape[0] == fin and K.gcn_module_fused_ok(
+                sc, fin, self.out_embedding.out_features):
+            # one launch per direction for the whole module (sgg_gcnmod_fwd / _bwd)
+            return K.gcn_module(h_states, end_group, sc, params, x2=x2, link=link)
+        if x2 is not None:
+            h_states = torch.cat([h_states, x2], dim=1)
         g = sc.groups(end_group.reshape(-1))
         # A_intra = D^-1 M: row i averages its group (models.py:658-665)
         intra = self.gcn_intra(lambda H: K.group_unpool(K.group_mean(H, g), g, scale=False), h_states)
@@ -642,15 +663,15 @@ class TrajectoryGenerator(nn.Module):
         ctx = final_encoder_h.view(-1, self.encoder_h_dim)
         end_pos = obs_traj[-1]
         if self.pooling_type:
-            fused_gat = self.graph == "gat" and self.mlp_decoder_needed()
-            # the GAT encoder's gradient of h reaches the pooling backward, which adds it in its own launch
-            link = K.GradLink() if fused_gat and torch.is_grad_enabled() else None
+            two_block = self.graph in ("gat", "gcn") and self.mlp_decoder_needed()
+            # the GAT encoder's / GCN module's gradient of h reaches the pooling
+            # backward, which adds it in its own launch
+            link = K.GradLink() if two_block and torch.is_grad_enabled() else None
             pool_h = self.pool_net(final_encoder_h, seq_start_end, end_pos, scenes=sc, link=link, U=U)
-            if fused_gat:
-                # the GAT encoder reads [h | pool_h] as two blocks (no cat)
-                noise_input = self.gatencoder((ctx, pool_h), seq_start_end, end_pos, obs_traj_g[-1], scenes=sc,
-                                              link=link)
-                return noise_input
+            if two_block:
+                # the graph module reads [h | pool_h] as two blocks (no cat)
+                module = self.gatencoder if self.graph == "gat" else self.gcn_module
+                return module((ctx, pool_h), seq_start_end, end_pos, obs_traj_g[-1], scenes=sc, link=link)
             ctx = torch.cat([ctx, pool_h], dim=1)
         if self.mlp_decoder_needed():
             if self.graph == "gat":

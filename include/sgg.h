@@ -525,6 +525,68 @@ long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd);
 int sgg_gatenc_fwd(const SggGatEncArgs* args, void* stream);
 int sgg_gatenc_bwd(const SggGatEncArgs* args, void* stream);
 
+/* ------------------------------------------------------------------------
+ * The group GCN module of every scene in ONE launch per direction
+ * (GCNModule.forward, models.py:628-712, with GCN.forward :573-580 and
+ * normalize :607-613): per scene (workgroup) the group mask of the
+ * last-observed labels (:651-657), gcn_intra (fin -> 72 -> 16, A = D^-1 M,
+ * ReLU((A H) W) per layer), the group pool R.intra (:667-686), gcn_inter
+ * (16 -> 72 -> 16 on the complete group graph, A = 1/G), the un-pool R^T
+ * (:700) and out_embedding Linear(32, fe) (:703-708).  Replaces the per-op
+ * sequence sgg_group_index / sgg_seg_reduce / sgg_seg_gather / sgg_xw x 4 /
+ * concat / Linear (~14 launches forward, more backward).
+ *
+ * Weights are the module's own tensors: W0i (fin x 72), W1i (72 x 16) of
+ * gcn_intra, W0g (16 x 72), W1g (72 x 16) of gcn_inter, Woe (fe x 32, nn.Linear
+ * layout), boe (fe).  X: B rows of fin floats (stride ldx), or two column
+ * blocks [X (kx1) | X2 (fin - kx1)] as in SggGatEncArgs; labels: B floats;
+ * scene_off: S + 1; np = the largest scene (<= 64; sgg_gcnmod_lds_bytes).
+ * bf16 != 0: the forward node transforms take bf16 operands (round to nearest
+ * even) with fp32 accumulation on the bf16 MFMA (set_precision("bf16")).
+ * Forward writes y (B x fe, stride ldy).  Backward recomputes the forward,
+ * reads dy (dy_copies blocks dy_cstride floats apart, summed) and writes dX
+ * (/ dX2) and, per workgroup w < sgg_gcnmod_slab_rows(S), the parameter
+ * gradients of its scenes into slab row w (sgg_gcnmod_param_size floats in
+ * the order W0i, W1i, W0g, W1g, Woe, boe); sgg_slab_reduce sums the rows.
+ */
+typedef struct {
+  const float* X;
+  int ldx;
+  const float* X2;
+  int ldx2;
+  int kx1;
+  const float* labels;
+  const int32_t* scene_off;
+  int S;
+  int np;
+  int fin;
+  int fe;
+  int bf16;
+  const float* W0i;
+  const float* W1i;
+  const float* W0g;
+  const float* W1g;
+  const float* Woe;
+  const float* boe;
+  float* y;
+  int ldy;
+  const float* dy;
+  int lddy;
+  int dy_copies;
+  int dy_cstride;
+  float* dX;
+  int lddx;
+  float* dX2;
+  int lddx2;
+  float* slab;
+} SggGcnModArgs;
+
+int sgg_gcnmod_param_size(int fin, int fe);
+int sgg_gcnmod_slab_rows(int S);
+long long sgg_gcnmod_lds_bytes(int max_n, int fin, int fe, int bwd);
+int sgg_gcnmod_fwd(const SggGcnModArgs* args, void* stream);
+int sgg_gcnmod_bwd(const SggGcnModArgs* args, void* stream);
+
 /* out[c] = sum_r slab[r][c] (rows x cols, row-major), rows summed in order. */
 int sgg_slab_reduce(const float* slab, int rows, int cols, float* out, void* stream);
 

@@ -797,6 +797,67 @@ def test_gat_encoder_fused_equals_per_layer(nh, sizes):
         close(gf[k], gr[k].cpu().numpy(), rtol=2e-4, floor=fl, what="fused d" + k)
 
 
+@pytest.mark.parametrize("prec,sizes", [("fp32", [1, 2, 20, 48, 13, 5, 64]), ("fp32", [20] * 600),
+                                        ("fp32", [3, 0, 7, 1]), ("bf16", [20, 7, 24, 1, 64])])
+def test_gcn_module_fused_equals_per_op(prec, sizes):
+    """The one-launch GCNModule (sgg_gcnmod_fwd / _bwd + sgg_slab_reduce)
+    against the per-op kernels (group pooling + sgg_xw per layer) on the same
+    module: outputs, input and parameter gradients; singletons (label 0), one
+    big group, mixed groups, one-ped and empty scenes; 600 scenes (more than
+    the backward's 512 workgroups: a workgroup accumulates several scenes);
+    the bf16 node transforms of set_precision("bf16")."""
+    from sgan import kernels as K
+    from sgan.models import GCNModule
+    from sgan.scene import SceneIndex
+    torch.manual_seed(len(sizes))
+    mod = GCNModule(40, 72, 16, 2, 24).to(DEV)
+    with torch.no_grad():   # the reference's unscaled randn init makes ReLU-dead columns the rule; tame it
+        for p in mod.parameters():
+            if p.dim() == 2 and p.shape[1] in (72, 16):
+                p.mul_(0.2)
+    B = sum(sizes)
+    sc = SceneIndex(np.concatenate([[0], np.cumsum(sizes)]), DEV)
+    labs = []
+    for k, n in enumerate(sizes):
+        pat = k % 3
+        labs.append(np.zeros(n) if pat == 0 else np.full(n, 3.0) if pat == 1 else np.random.RandomState(k).randint(0, 4, n))
+    lab = torch.from_numpy(np.concatenate(labs).astype(np.float32)).to(DEV).view(-1, 1)
+    x = torch.randn(B, 40, device=DEV)
+    dy = torch.randn(B, 24, device=DEV)
+    res = []
+    K.set_precision(prec)
+    try:
+        for fused in (True, False):
+            K.GCNMOD_FUSED = fused
+            assert K.gcn_module_fused_ok(sc, 40, 24) == fused
+            mod.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            y = mod(xi, None, None, lab, scenes=sc)
+            (y * dy).sum().backward()
+            res.append((y.detach(), xi.grad, {k: p.grad.clone() for k, p in mod.named_parameters()}))
+        K.GCNMOD_FUSED = True
+        # the two-block input ([encoder state | pooled vector], no cat): bitwise the one-block result
+        mod.zero_grad(set_to_none=True)
+        x1, x2 = x[:, :32].clone().requires_grad_(True), x[:, 32:].clone().requires_grad_(True)
+        y2 = mod((x1, x2), None, None, lab, scenes=sc)
+        (y2 * dy).sum().backward()
+    finally:
+        K.GCNMOD_FUSED = True
+        K.set_precision("fp32")
+    assert torch.equal(y2, res[0][0]), "split-input output"
+    assert torch.equal(torch.cat([x1.grad, x2.grad], 1), res[0][1]), "split-input dx"
+    for k, q in mod.named_parameters():
+        assert torch.equal(q.grad, res[0][2][k]), "split-input d" + k
+    (yf, dxf, gf), (yr, dxr, gr) = res
+    # bf16: both paths round their own (differently summed) operands to bf16
+    t_out, t_dx, t_dw = (2e-2, 2e-2, 2e-2) if prec == "bf16" else (2e-5, 1e-4, 2e-4)
+    close(yf, yr.cpu().numpy(), rtol=t_out, what="fused out")
+    close(dxf, dxr.cpu().numpy(), rtol=t_dx, what="fused dx")
+    fl = 1e-2 * max(float(g.abs().max()) for g in gr.values())
+    for k in gr:
+        close(gf[k], gr[k].cpu().numpy(), rtol=t_dw, floor=fl, what="fused d" + k)
+
+
 def test_step_glue_kernels_match_torch():
     """glue.hip (sgg_traj_cat, sgg_decoder_init, sgg_l2_select,
     sgg_l2_loss_fwd/bwd) against the reference's torch expressions
