@@ -212,18 +212,23 @@ def roofline_of(name, a):
 
 
 def real_data_leg(dev, iters=20, warmup=3, batch=64):
-    """configs[1] on REAL data: eager training iterations over the zara1
-    train split (tests/golden/datasets_group/zara1/train, the reference's
-    datasets_group files), batch 64, consecutive loader batches to the D-step
-    and the G-step (scripts/train.py:279-297) -- the variable scene / ped
-    counts of real batches rule out one captured graph.  Batches come from
-    the device-resident data path (sgan/data/device.py: the split in HBM, one
-    gather launch per batch); the host DataLoader + .cuda() path is timed
-    beside it."""
+    """configs[1] on REAL data: training iterations over the zara1 train split
+    (tests/golden/datasets_group/zara1/train, the reference's datasets_group
+    files), batch 64, consecutive loader batches to the D-step and the G-step
+    (scripts/train.py:279-297).  Three paths:
+      graphed  HIP-graph replays through BucketedGraphTrainer: each batch
+               pair padded into a capacity bucket whose iteration was captured
+               once (the captures happen in an untimed first pass over the
+               epoch; a capture leaves the training state unchanged);
+      device   eager iterations, batches from the device-resident data path
+               (the split in HBM, one gather launch per batch);
+      host     eager iterations, the host DataLoader + .cuda() copies.
+    The rate counts the D-step's scenes; the G-step consumes the next loader
+    batch, so the loader delivers twice as many scenes per iteration."""
     from sgan.data.device import DeviceLoader, DeviceTrajectoryDataset
     from sgan.data.trajectories_GCN import TrajectoryDataset, seq_collate
     from sgan.scene import SceneIndex
-    from sgan.train_step import DataParallel, GanTrainer
+    from sgan.train_step import BucketedGraphTrainer, DataParallel, GanTrainer
     from torch.utils.data import DataLoader
     path = os.path.join(ROOT, "tests", "golden", "datasets_group", "zara1", "train")
     if not os.path.isdir(path):
@@ -231,13 +236,16 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
     dset = TrajectoryDataset(path)
     dd = DeviceTrajectoryDataset(dset, dev)
     out = {}
-    for mode in ("device", "host"):
+    for mode in ("graphed", "device", "host"):
         g, d = build_models(0)
         tr = GanTrainer(g.to(dev), d.to(dev), dp=DataParallel(), capturable=True)
+        bt = BucketedGraphTrainer(tr, dd, batch_size=batch) if mode == "graphed" else None
 
         def batches():
             while True:
-                if mode == "device":
+                if mode == "graphed":
+                    yield from DeviceLoader(dd, batch_size=batch, shuffle=True).scene_batches()
+                elif mode == "device":
                     yield from DeviceLoader(dd, batch_size=batch, shuffle=True)
                 else:
                     for b in DataLoader(dset, batch_size=batch, shuffle=True, collate_fn=seq_collate):
@@ -245,7 +253,12 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
                                SceneIndex.from_seq_start_end(b[-1], dev))
         it = batches()
         from sgan import kernels as K
-        for w in range(warmup):
+        t_cap = time.perf_counter()
+        n_warm = (len(dd) // batch + 1) if mode == "graphed" else warmup   # graphed: an epoch (every bucket)
+        for w in range(n_warm):
+            if mode == "graphed":
+                bt.step(next(it), next(it))
+                continue
             (bd, scd), (bg, scg) = next(it), next(it)
             # one warm-up iteration on the per-layer GAT path too: real batches
             # with a scene beyond the fused encoder's LDS plan take it, and the
@@ -257,14 +270,20 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
             finally:
                 K.GATENC_FUSED = True
         torch.cuda.synchronize()
+        t_cap = time.perf_counter() - t_cap
         t0 = time.perf_counter()
         scenes = 0
         marks = [t0]
         for _ in range(iters):
-            (bd, scd), (bg, scg) = next(it), next(it)
-            tr.d_step(bd, scd)
-            tr.g_step(bg, scg)
-            scenes += scd.S
+            if mode == "graphed":
+                sd, sg = next(it), next(it)
+                bt.step(sd, sg)
+                scenes += len(sd)
+            else:
+                (bd, scd), (bg, scg) = next(it), next(it)
+                tr.d_step(bd, scd)
+                tr.g_step(bg, scg)
+                scenes += scd.S
             marks.append(time.perf_counter())
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -273,9 +292,14 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
         per = sorted(b - a for a, b in zip(marks, marks[1:]))
         out[mode] = {"value": round(scenes / dt, 2), "ms_per_iteration": round(dt / iters * 1e3, 3),
                      "host_ms_median": round(per[len(per) // 2] * 1e3, 3), "host_ms_max": round(per[-1] * 1e3, 3)}
-    return {"metric": "train-scenes/s on real data (D-step scenes per second, eager)", "split": "zara1 train",
-            "batch": batch, "iterations": iters, "num_seq": len(dset), "device_data_path": out["device"],
-            "host_data_path": out["host"], "unit": "scenes/s", "hip_graph": False}
+        if bt is not None:
+            out[mode].update(buckets=sorted([list(k) for k in bt.buckets]), eager_fallback_steps=bt.eager_steps,
+                             warm_epoch_s=round(t_cap, 2), warm_iterations=n_warm)
+        del tr, g, d, bt
+    return {"metric": "train-scenes/s on real data (D-step scenes per second; the G-step takes the next loader "
+                      "batch)", "split": "zara1 train",
+            "batch": batch, "iterations": iters, "num_seq": len(dset), "graphed_device_data_path": out["graphed"],
+            "device_data_path": out["device"], "host_data_path": out["host"], "unit": "scenes/s"}
 
 
 def _free_port():

@@ -6,7 +6,9 @@
 // and uploads the list of ped rows; each thread writes one (ped, step) of
 // every time-major output: positions, displacements, velocities (2.5 x the
 // displacement: the 0.4 s frame step), group labels, the loss mask, and the
-// non-linearity flag at step 0.  Table record per ped (floats):
+// non-linearity flag at step 0.  A negative row is a padding ped (the
+// fixed-capacity batches of the graph-replayed path, PaddedScenes): zeros
+// everywhere, loss mask included.  Table record per ped (floats):
 //   [abs x, y (T x 2) | rel x, y (T x 2) | group (T) | loss mask (T) | non_linear]
 #include "sgg_common.h"
 
@@ -21,10 +23,12 @@ __global__ void __launch_bounds__(256) gather_batch_kernel(const float* __restri
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * T) return;
   const int b = e / T, t = e - b * T;
-  const float* r = table + (size_t)rows[b] * rec;
-  const float ax = r[2 * t], ay = r[2 * t + 1];
-  const float rx = r[2 * T + 2 * t], ry = r[2 * T + 2 * t + 1];
-  const float g = r[4 * T + t];
+  const int row = rows[b];
+  const bool pad = row < 0;
+  const float* r = table + (size_t)(pad ? 0 : row) * rec;
+  const float ax = keep_if(r[2 * t], !pad), ay = keep_if(r[2 * t + 1], !pad);
+  const float rx = keep_if(r[2 * T + 2 * t], !pad), ry = keep_if(r[2 * T + 2 * t + 1], !pad);
+  const float g = keep_if(r[4 * T + t], !pad);
   const size_t oB = (size_t)B;
   const size_t o_obs = 0, o_pred = o_obs + To * oB * 2, o_orel = o_pred + Tp * oB * 2, o_prel = o_orel + To * oB * 2;
   const size_t o_ovel = o_prel + Tp * oB * 2, o_pvel = o_ovel + To * oB * 2, o_og = o_pvel + Tp * oB * 2;
@@ -36,8 +40,8 @@ __global__ void __launch_bounds__(256) gather_batch_kernel(const float* __restri
   *reinterpret_cast<float2*>(out + (obs ? o_orel : o_prel) + p2) = make_float2(rx, ry);
   *reinterpret_cast<float2*>(out + (obs ? o_ovel : o_pvel) + p2) = make_float2(rx * 2.5f, ry * 2.5f);
   out[(obs ? o_og : o_pg) + p1] = g;
-  out[o_mask + (size_t)b * T + t] = r[5 * T + t];
-  if (t == 0) out[o_nl + b] = r[6 * T];
+  out[o_mask + (size_t)b * T + t] = keep_if(r[5 * T + t], !pad);
+  if (t == 0) out[o_nl + b] = keep_if(r[6 * T], !pad);
 }
 
 }  // namespace

@@ -158,7 +158,9 @@ __global__ void __launch_bounds__(512) l2_select_kernel(const float* __restrict_
 // loss = sum_s w * (sum_{i in s, t} m (gt - pred)^2) / (sum_{i in s, t} m)
 // (losses.py:52-71, mode 'raw' summed per scene): one wave per scene writes
 // its term and mask sum (kept for the backward), then l2_sum_kernel adds the
-// terms in scene order (lane-strided partials, a fixed shuffle tree)
+// terms in scene order (lane-strided partials, a fixed shuffle tree).  A
+// scene without a masked step (only the padding scenes of a fixed-capacity
+// batch, PaddedScenes: real scenes always have one) adds 0 instead of 0 / 0.
 __global__ void __launch_bounds__(64) l2_terms_kernel(const float* __restrict__ pred, int ldp,
                                                       const float* __restrict__ gt, const float* __restrict__ mask,
                                                       int ldm, const int32_t* __restrict__ scene_off, int T, int B,
@@ -196,7 +198,7 @@ __global__ void __launch_bounds__(64) l2_terms_kernel(const float* __restrict__ 
   ms = wave_sum(ms);
   if (lane == 0) {
     msum_out[s] = ms;
-    term[s] = (w * acc) / ms;
+    term[s] = ms > 0.f ? (w * acc) / ms : 0.f;
   }
 }
 
@@ -220,7 +222,8 @@ __global__ void __launch_bounds__(256) l2_loss_bwd_kernel(const float* __restric
     const float m = mask[(size_t)p * ldm + t];
     const float2 gv = reinterpret_cast<const float2*>(gt)[e];
     const float2 q = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
-    const float c = g * m / msum[ped_scene[p]];
+    const float ms = msum[ped_scene[p]];
+    const float c = ms > 0.f ? g * m / ms : 0.f;
     *reinterpret_cast<float2*>(dpred + (size_t)t * ldd + 2 * p) = make_float2(c * (gv.x - q.x), c * (gv.y - q.y));
   }
 }

@@ -104,7 +104,8 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
                                                        const float* __restrict__ dY, int act,
                                                        float* __restrict__ dX, int lddx, float* __restrict__ wslab,
                                                        const float* __restrict__ bce_g, const float* __restrict__ bce_ya,
-                                                       const float* __restrict__ bce_yb, int bce_split, float bce_w) {
+                                                       const float* __restrict__ bce_yb, int bce_split, float bce_w,
+                                                       const int32_t* __restrict__ bce_nvalid) {
   constexpr int N1 = 16 * NT, K = 16 * KT;
   constexpr int DP = N1 + 4;   // dhid row pitch
   __shared__ float dh[kHeadRows][DP];
@@ -139,12 +140,14 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
     }
     if (bce_g) {   // dY of the BCE loss on Y (bce_bwd_kernel's expression, loss.hip)
       const float gw = *bce_g * bce_w, ya = *bce_ya, yb = *bce_yb;
+      const int nv = bce_nvalid ? *bce_nvalid : M;   // a padded batch: the real rows of each range
 #pragma unroll
       for (int i = 0; i < RPT; ++i) {
         const int mc = min(rb + r0 + RS * i, M - 1);
         const bool first = mc < bce_split;
-        const float cnt = first ? (float)bce_split : (float)(M - bce_split);
-        dyv[i] = (gw / cnt) * bce_grad(yv[i], first ? ya : yb);
+        const float cnt = first ? (float)min(bce_split, nv) : (float)min(M - bce_split, nv);
+        const bool live = first ? mc < nv : mc - bce_split < nv;
+        dyv[i] = live ? (gw / cnt) * bce_grad(yv[i], first ? ya : yb) : 0.f;
       }
     }
 #pragma unroll
@@ -229,13 +232,15 @@ struct BceArgs {
   const float *g, *ya, *yb;
   int split;
   float w;
+  const int32_t* nvalid;
 };
 
 template <int NT, int KT>
 int launch_bwd_nt(const float* X, int ldx, int M, const float* W1, const float* w2, const float* hid, const float* Y,
                   const float* dY, int act, float* dX, int lddx, float* wslab, const BceArgs& bc, hipStream_t st) {
   hipLaunchKernelGGL((head_bwd_kernel<NT, KT>), dim3((M + kHeadRows - 1) / kHeadRows), dim3(256), 0, st, X, ldx, M,
-                     W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc.g, bc.ya, bc.yb, bc.split, bc.w);
+                     W1, w2, hid, Y, dY, act, dX, lddx, wslab, bc.g, bc.ya, bc.yb, bc.split, bc.w,
+                     bc.nvalid);
   SGG_RETURN_LAUNCH("sgg_head_bwd");
 }
 
@@ -282,11 +287,11 @@ extern "C" int sgg_head_fwd(const float* X, int ldx, int M, int K, int N1, const
 extern "C" int sgg_head_bwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* w2,
                             const float* hid, const float* Y, const float* dY, int act, float* dX, int lddx,
                             float* wslab, const float* bce_g, const float* bce_ya, const float* bce_yb,
-                            int bce_split, float bce_w, void* stream) {
+                            int bce_split, float bce_w, const int32_t* bce_nvalid, void* stream) {
   SGG_CHECK_ARG(X && W1 && w2 && hid && Y && (dY || bce_g) && dX, "sgg_head_bwd: null pointer");
   SGG_CHECK_ARG(!bce_g || (bce_ya && bce_yb && bce_split >= 0 && bce_split <= M),
                 "sgg_head_bwd: BCE targets / split (split=%d, M=%d)", bce_split, M);
-  const BceArgs bc{bce_g, bce_ya, bce_yb, bce_split, bce_w};
+  const BceArgs bc{bce_g, bce_ya, bce_yb, bce_split, bce_w, bce_nvalid};
   SGG_CHECK_ARG(M >= 0 && sgg_head_ok(K, N1) && ldx >= K && lddx >= K && act >= 0 && act <= 3,
                 "sgg_head_bwd: unsupported shape M=%d K=%d N1=%d", M, K, N1);
   if (M == 0) return 0;

@@ -6,7 +6,9 @@
 // The reference spends ~12 elementwise/reduction launches per bce_loss call
 // plus their backward; here it is one launch forward and one backward.  The
 // targets are device scalars so the step stays graph-capturable with fresh
-// label-smoothing draws per replay.
+// label-smoothing draws per replay.  nvalid (optional, device): only the
+// first *nvalid scores of each half are real (a padded batch, PaddedScenes);
+// the means run over those, the rest get a zero gradient.
 #include "sgg_common.h"
 
 namespace sgg {
@@ -23,12 +25,17 @@ __device__ __forceinline__ float bce_grad(float x, float y) {
   return (x >= 0.f ? 1.f : 0.f) - y - sg * (e / (1.f + e));
 }
 
+// the score i counts: inside its half's first nv scores
+__device__ __forceinline__ bool bce_live(int i, int split, int nv) { return i < split ? i < nv : i - split < nv; }
+
 __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ x, int n, int split,
                                                       const float* __restrict__ ya, const float* __restrict__ yb,
                                                       float w, float* __restrict__ loss,
-                                                      const float* __restrict__ addend, float* __restrict__ total) {
+                                                      const float* __restrict__ addend, float* __restrict__ total,
+                                                      const int32_t* __restrict__ nvalid) {
   __shared__ float red[2][4];
   const float a = *ya, b = *yb;
+  const int nv = nvalid ? *nvalid : n;
   float s0 = 0.f, s1 = 0.f;
   constexpr int kPre = 16;   // up to 4,096 scores: every load in flight at once (one round trip)
   if (n <= kPre * 256) {
@@ -41,7 +48,7 @@ __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ 
 #pragma unroll
     for (int m = 0; m < kPre; ++m) {   // the same per-thread order as the loop below
       const int i = threadIdx.x + 256 * m;
-      if (i < n) {
+      if (i < n && bce_live(i, split, nv)) {
         if (i < split) s0 += bce_term(v[m], a);
         else s1 += bce_term(v[m], b);
       }
@@ -49,6 +56,7 @@ __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ 
   } else {
 #pragma unroll 4
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (!bce_live(i, split, nv)) continue;
       if (i < split) s0 += bce_term(x[i], a);
       else s1 += bce_term(x[i], b);
     }
@@ -64,8 +72,9 @@ __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) {
     const float t0 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
     const float t1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-    const float m0 = split > 0 ? t0 / (float)split : 0.f;
-    const float m1 = n - split > 0 ? t1 / (float)(n - split) : 0.f;
+    const int c0 = min(split, nv), c1 = min(n - split, nv);
+    const float m0 = c0 > 0 ? t0 / (float)c0 : 0.f;
+    const float m1 = c1 > 0 ? t1 / (float)c1 : 0.f;
     const float l = w * (m0 + m1);
     *loss = l;
     if (total) *total = l + *addend;
@@ -74,12 +83,13 @@ __global__ void __launch_bounds__(256) bce_fwd_kernel(const float* __restrict__ 
 
 __global__ void bce_bwd_kernel(const float* __restrict__ x, int n, int split, const float* __restrict__ ya,
                                const float* __restrict__ yb, float w, const float* __restrict__ gout,
-                               float* __restrict__ dx) {
+                               float* __restrict__ dx, const int32_t* __restrict__ nvalid) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const int nv = nvalid ? *nvalid : n;
   const bool first = i < split;
-  const float cnt = first ? (float)split : (float)(n - split);
-  dx[i] = (*gout * w / cnt) * bce_grad(x[i], first ? *ya : *yb);
+  const float cnt = first ? (float)min(split, nv) : (float)min(n - split, nv);
+  dx[i] = bce_live(i, split, nv) ? (*gout * w / cnt) * bce_grad(x[i], first ? *ya : *yb) : 0.f;
 }
 
 }  // namespace sgg
@@ -87,21 +97,21 @@ __global__ void bce_bwd_kernel(const float* __restrict__ x, int n, int split, co
 using namespace sgg;
 
 extern "C" int sgg_bce_fwd(const float* x, int n, int split, const float* ya, const float* yb, float w, float* loss,
-                           const float* addend, float* total, void* stream) {
+                           const float* addend, float* total, const int32_t* nvalid, void* stream) {
   SGG_CHECK_ARG(loss && ya && yb && (n == 0 || x), "sgg_bce_fwd: null pointer");
   SGG_CHECK_ARG(!total || addend, "sgg_bce_fwd: total needs the addend");
   SGG_CHECK_ARG(n >= 0 && split >= 0 && split <= n, "sgg_bce_fwd: bad sizes n=%d split=%d", n, split);
   hipLaunchKernelGGL(bce_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, split, ya, yb, w, loss,
-                     addend, total);
+                     addend, total, nvalid);
   SGG_RETURN_LAUNCH("sgg_bce_fwd");
 }
 
 extern "C" int sgg_bce_bwd(const float* x, int n, int split, const float* ya, const float* yb, float w,
-                           const float* gout, float* dx, void* stream) {
+                           const float* gout, float* dx, const int32_t* nvalid, void* stream) {
   SGG_CHECK_ARG(ya && yb && gout && (n == 0 || (x && dx)), "sgg_bce_bwd: null pointer");
   SGG_CHECK_ARG(n >= 0 && split >= 0 && split <= n, "sgg_bce_bwd: bad sizes n=%d split=%d", n, split);
   if (n == 0) return 0;
   hipLaunchKernelGGL(bce_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, n, split, ya, yb,
-                     w, gout, dx);
+                     w, gout, dx, nvalid);
   SGG_RETURN_LAUNCH("sgg_bce_bwd");
 }

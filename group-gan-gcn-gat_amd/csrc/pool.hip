@@ -58,7 +58,7 @@ template <int BN, int GPW, int UNR>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
-    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
+    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks, const int32_t* __restrict__ nchunks_dev,
     float* __restrict__ out, int32_t* __restrict__ argmax) {
   using C = PoolCfg<BN>;
   constexpr int NT = C::NT, BNP = C::BNP;
@@ -78,9 +78,11 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
   // which all stage the same U rows, then hit one XCD's L2 instead of
   // fetching those rows once per XCD.
   const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  for (int ch = xb; ch < nchunks; ch += gridDim.x) {
+  const int nch = nchunks_dev ? *nchunks_dev : nchunks;   // a fixed-capacity plan: the count is device data
+  for (int ch = xb; ch < nch; ch += gridDim.x) {
     const int4 cd = chunks[ch];
     const int s = cd.x, i0 = cd.y, i1 = cd.z;
+    if (i1 <= i0) continue;   // an empty padding chunk (fixed-capacity plan), uniform over the workgroup
     const int o = scene_off[s];
     const int n = scene_off[s + 1] - o;
     const int rows = i1 - i0;
@@ -235,7 +237,7 @@ template <int BN, int GPW>
 __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
-    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
+    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks, const int32_t* __restrict__ nchunks_dev,
     float* __restrict__ out, int32_t* __restrict__ argmax) {
   constexpr int NT = PoolCfg<BN>::NT;
   constexpr int TB = (SGG_POOL_MAX_PEDS + 16 * NT) * kVP + 2 * kKT;   // one tile buffer: U | W2 | A
@@ -249,9 +251,11 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
   const int c16 = lane & 15, kq = lane >> 4;
 
   const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);   // XCD-aware (pool_fwd_kernel)
-  for (int ch = xb; ch < nchunks; ch += gridDim.x) {
+  const int nch = nchunks_dev ? *nchunks_dev : nchunks;   // a fixed-capacity plan: the count is device data
+  for (int ch = xb; ch < nch; ch += gridDim.x) {
     const int4 cd = chunks[ch];
     const int s = cd.x, i0 = cd.y, i1 = cd.z;
+    if (i1 <= i0) continue;   // an empty padding chunk (fixed-capacity plan), uniform over the workgroup
     const int o = scene_off[s];
     const int n = scene_off[s + 1] - o;
     const int rows = i1 - i0;
@@ -459,7 +463,7 @@ template <int BN, int GPW>
 __global__ void __launch_bounds__(256) pool_fwd_res_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
-    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks, int max_n,
+    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks, const int32_t* __restrict__ nchunks_dev, int max_n,
     float* __restrict__ out, int32_t* __restrict__ argmax) {
   constexpr int NT = PoolCfg<BN>::NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -475,9 +479,11 @@ __global__ void __launch_bounds__(256) pool_fwd_res_kernel(
   stage_rows512(W2s, W2, 16 * NT, BN);
   for (int e = threadIdx.x; e < 2 * kHidden; e += 256) As[e] = A[e];
   int cur = -1;
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  const int nch = nchunks_dev ? *nchunks_dev : nchunks;   // a fixed-capacity plan: the count is device data
+  for (int ch = blockIdx.x; ch < nch; ch += gridDim.x) {
     const int4 cd = chunks[ch];
     const int s = cd.x, i0 = cd.y, i1 = cd.z;
+    if (i1 <= i0) continue;   // an empty padding chunk (fixed-capacity plan), uniform over the workgroup
     const int o = scene_off[s];
     const int n = scene_off[s + 1] - o;
     const int rows = i1 - i0;
@@ -717,7 +723,8 @@ static int device_cus();
 
 template <int BN, int GPW>
 static void launch_fwd_g(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                         const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, float* out,
+                         const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int max_rows,
+                         float* out,
                          int32_t* am, hipStream_t st) {
   const int grid = nchunks < 65536 ? (nchunks + 7) & ~7 : 65536;   // multiple of 8 (XCD-aware order)
   const size_t lds = pool_fwd_lds<BN>(max_rows);
@@ -731,12 +738,12 @@ static void launch_fwd_g(const float* U, const float* pos, const float* A, const
       const size_t lv = sizeof(float) * 2 * ((size_t)(SGG_POOL_MAX_PEDS + 16 * PoolCfg<BN>::NT) * kVP + 2 * kKT) +
                         sizeof(float2) * SGG_POOL_MAX_PEDS + sizeof(unsigned long long) * (size_t)max_rows * BN;
       hipLaunchKernelGGL((pool_fwd_v_kernel<BN, GPW>), dim3(grid), dim3(256), lv, st, U, pos, A, W2, b2, off, ck,
-                         nchunks, out, am);
+                         nchunks, ncd, out, am);
       return;
     }
   }
   hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW, 2>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off, ck,
-                     nchunks, out, am);
+                     nchunks, ncd, out, am);
 }
 // j ranges per scene of the backward: S x jq units ~ one round of the chip
 static int pool_bwd_jq(int S) {
@@ -765,18 +772,20 @@ static int device_cus() {
 
 template <int BN, int GPW>
 static void launch_fwd_res(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                           const int32_t* off, const int32_t* chunks, int nchunks, int max_n, size_t lds, float* out,
+                           const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int max_n,
+                           size_t lds, float* out,
                            int32_t* am, hipStream_t st) {
   const int per_cu = (int)((160u * 1024u) / lds);
   long long grid = (long long)device_cus() * (per_cu < 1 ? 1 : per_cu);
   if (grid > nchunks) grid = nchunks;
   hipLaunchKernelGGL((pool_fwd_res_kernel<BN, GPW>), dim3((unsigned)grid), dim3(256), lds, st, U, pos, A,
-                     W2, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, max_n, out, am);
+                     W2, b2, off, reinterpret_cast<const int4*>(chunks), nchunks, ncd, max_n, out, am);
 }
 
 template <int BN>
 static int launch_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                      const int32_t* off, const int32_t* chunks, int nchunks, int max_rows, int max_n, int gpw,
+                      const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int max_rows,
+                      int max_n, int gpw,
                       float* out, int32_t* am, hipStream_t st) {
   const size_t res = pool_res_lds<BN>(max_n, max_rows);
   // measured (tools/bench_kernels.py, round 1): the resident form is slower
@@ -786,18 +795,18 @@ static int launch_fwd(const float* U, const float* pos, const float* A, const fl
   const char* rs = getenv("SGG_POOL_RESIDENT");
   if (res <= 160u * 1024u && rs && rs[0] == '1') {
     switch (gpw) {
-      case 1: launch_fwd_res<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
-      case 2: launch_fwd_res<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
-      case 4: launch_fwd_res<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
-      default: launch_fwd_res<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, max_n, res, out, am, st); break;
+      case 1: launch_fwd_res<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
+      case 2: launch_fwd_res<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
+      case 4: launch_fwd_res<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
+      default: launch_fwd_res<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
     }
     SGG_RETURN_LAUNCH("sgg_pool_fwd");
   }
   switch (gpw) {
-    case 1: launch_fwd_g<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
-    case 2: launch_fwd_g<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
-    case 4: launch_fwd_g<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
-    default: launch_fwd_g<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, max_rows, out, am, st); break;
+    case 1: launch_fwd_g<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
+    case 2: launch_fwd_g<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
+    case 4: launch_fwd_g<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
+    default: launch_fwd_g<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
   }
   SGG_RETURN_LAUNCH("sgg_pool_fwd");
 }
@@ -882,7 +891,8 @@ extern "C" int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int t
 
 extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
                             const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
-                            int B, int bn, int max_n, float* out, int32_t* argmax, void* stream) {
+                            int B, int bn, int max_n, float* out, int32_t* argmax, const int32_t* nchunks_dev,
+                            void* stream) {
   SGG_CHECK_ARG(U && pos && A && W2 && b2 && scene_off && chunks && out && argmax, "sgg_pool_fwd: null pointer");
   SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_fwd: bottleneck %d not built (8/16/32/48/64)", bn);
   SGG_CHECK_ARG(nchunks >= 0 && B >= 0, "sgg_pool_fwd: bad sizes");
@@ -893,11 +903,11 @@ extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, co
   if (nchunks == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (bn) {
-    case 8: return launch_fwd<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
-    case 16: return launch_fwd<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
-    case 32: return launch_fwd<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
-    case 48: return launch_fwd<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
-    default: return launch_fwd<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, max_n, gpw, out, argmax, st);
+    case 8: return launch_fwd<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
+    case 16: return launch_fwd<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
+    case 32: return launch_fwd<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
+    case 48: return launch_fwd<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
+    default: return launch_fwd<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
   }
 }
 

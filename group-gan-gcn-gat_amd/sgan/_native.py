@@ -82,7 +82,7 @@ SIGNATURES = {
     "sgg_xw": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
     "sgg_xw_bf16": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
     "sgg_pool_plan": (_i, [_p, _i, _i, _i, _i, _p, _i, _p, _p]),
-    "sgg_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    "sgg_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
     "sgg_pool_bwd_grid": (_i, [_i]),
     "sgg_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_gat_fwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _i, _p]),
@@ -101,7 +101,7 @@ SIGNATURES = {
     "sgg_head_ok": (_i, [_i, _i]),
     "sgg_head_slab_cols": (_i, [_i, _i]),
     "sgg_head_fwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p]),
-    "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _p, _i, _f, _p]),
+    "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _p, _i, _f, _p, _p]),
     "sgg_xtw_partial": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
     "sgg_adam_parts": (_i, [ctypes.c_longlong]),
@@ -116,8 +116,8 @@ SIGNATURES = {
     "sgg_lstm_wpart_rows": (_i, [_i, _i]),
     "sgg_lstm_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
     "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
-    "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p, _p]),
-    "sgg_bce_bwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p]),
+    "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p, _p, _p]),
+    "sgg_bce_bwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p, _p]),
     "sgg_gatenc_param_size": (_i, [_i]),
     "sgg_gatenc_lds_bytes": (ctypes.c_longlong, [_i, _i, _i]),
     "sgg_gatenc_saved_floats": (ctypes.c_longlong, [_i, _i, _i]),

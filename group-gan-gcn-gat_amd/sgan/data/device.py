@@ -45,20 +45,24 @@ class DeviceTrajectoryDataset:
     def __len__(self):
         return len(self.dset)
 
-    def batch(self, scenes):
-        """11-tuple (seq_collate layout; every tensor on the device except
-        seq_start_end, which stays on the host as the DataLoader yields it)
-        and the batch's SceneIndex, for the given scene indices."""
-        lib = N.load()
+    def layout(self, scenes):
+        """(scene offsets (S + 1, int64), table rows of the batch's peds (B,
+        int32)) of a batch of scene indices, on the host."""
         sizes = np.array([self.scene_off[s + 1] - self.scene_off[s] for s in scenes], dtype=np.int64)
         rows = np.concatenate([np.arange(self.scene_off[s], self.scene_off[s + 1]) for s in scenes]).astype(np.int32)
-        B = int(rows.shape[0])
+        return np.concatenate([[0], np.cumsum(sizes)]), rows
+
+    def gather_into(self, rows_d, B, out):
+        """sgg_gather_batch of B ped rows (device int32; < 0: padding) into out."""
+        lib = N.load()
+        N.check(lib.sgg_gather_batch(N.ptr(self.table), self.rec, N.ptr(rows_d), B, self.obs_len, self.pred_len,
+                                     N.ptr(out), N.stream_ptr()), "sgg_gather_batch")
+
+    def views(self, out, B, host_off):
+        """The 11-tuple (seq_collate layout) as views of a gather buffer;
+        seq_start_end on the host from host_off."""
         To, Tp = self.obs_len, self.pred_len
         T = To + Tp
-        rows_d = torch.from_numpy(rows).pin_memory().to(self.device, non_blocking=True)
-        out = torch.empty(int(lib.sgg_gather_batch_floats(B, To, Tp)), device=self.device, dtype=torch.float32)
-        N.check(lib.sgg_gather_batch(N.ptr(self.table), self.rec, N.ptr(rows_d), B, To, Tp, N.ptr(out),
-                                     N.stream_ptr()), "sgg_gather_batch")
         shapes = [(To, B, 2), (Tp, B, 2), (To, B, 2), (Tp, B, 2), (To, B, 2), (Tp, B, 2), (To, B, 1), (Tp, B, 1),
                   (B,), (B, T)]
         parts, o = [], 0
@@ -66,12 +70,24 @@ class DeviceTrajectoryDataset:
             n = int(np.prod(shp))
             parts.append(out[o:o + n].view(shp))
             o += n
-        off = np.concatenate([[0], np.cumsum(sizes)])
-        sse = torch.from_numpy(np.stack([off[:-1], off[1:]], 1).astype(np.int64))
+        sse = torch.from_numpy(np.stack([host_off[:-1], host_off[1:]], 1).astype(np.int64))
+        return tuple(parts) + (sse,)
+
+    def batch(self, scenes):
+        """11-tuple (seq_collate layout; every tensor on the device except
+        seq_start_end, which stays on the host as the DataLoader yields it)
+        and the batch's SceneIndex, for the given scene indices."""
+        lib = N.load()
+        off, rows = self.layout(scenes)
+        B = int(rows.shape[0])
+        rows_d = torch.from_numpy(rows).pin_memory().to(self.device, non_blocking=True)
+        out = torch.empty(int(lib.sgg_gather_batch_floats(B, self.obs_len, self.pred_len)), device=self.device,
+                          dtype=torch.float32)
+        self.gather_into(rows_d, B, out)
         sc = SceneIndex(off, self.device)
         # keep the row list alive until the gather has consumed it
         sc._rows = rows_d
-        return tuple(parts) + (sse,), sc
+        return self.views(out, B, off), sc
 
 
 class DeviceLoader:
@@ -87,6 +103,11 @@ class DeviceLoader:
         return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
 
     def __iter__(self):
+        return (self.ddset.batch(scenes) for scenes in self.scene_batches())
+
+    def scene_batches(self):
+        """The batches as lists of scene indices (BucketedGraphTrainer gathers
+        them itself into its fixed-capacity buffers)."""
         idx = range(len(self.ddset))
         sampler = RandomSampler(idx) if self.shuffle else SequentialSampler(idx)
         batches = iter(BatchSampler(sampler, self.batch_size, self.drop_last))
@@ -94,7 +115,7 @@ class DeviceLoader:
         # RNG when it is created (torch _BaseDataLoaderIter.__init__): so do we,
         # so the noise / shuffle stream matches the reference's loader
         torch.empty((), dtype=torch.int64).random_()
-        return (self.ddset.batch(scenes) for scenes in batches)
+        return batches
 
 
 def device_data_loader(args, path, device="cuda", shuffle=True):

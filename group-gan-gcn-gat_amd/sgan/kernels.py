@@ -464,8 +464,8 @@ class BceLink:
     def __init__(self):
         self.pending = None
 
-    def put(self, g, ya, yb, split, w, placeholder):
-        self.pending = (g, ya, yb, split, w, placeholder)
+    def put(self, g, ya, yb, split, w, placeholder, nvalid=None):
+        self.pending = (g, ya, yb, split, w, placeholder, nvalid)
 
     def take(self):
         p, self.pending = self.pending, None
@@ -508,11 +508,11 @@ class _Head(torch.autograd.Function):
         pend = ctx.bce_link.take() if ctx.bce_link is not None else None
         bce = None
         if pend is not None:
-            g, ya, yb, split, w, ph = pend
+            g, ya, yb, split, w, ph, nvalid = pend
             if dy.data_ptr() != ph.data_ptr():
                 raise N.NativeError("fused head + BCE backward: the scores have a consumer besides the BCE loss "
                                     "(set SGG_HEAD_BCE=0)")
-            bce = (g.contiguous(), ya, yb, int(split), float(w))
+            bce = (g.contiguous(), ya, yb, int(split), float(w), nvalid)
         else:
             dy = dy.contiguous()
         dx = torch.empty(M, Kd, device=x.device, dtype=torch.float32)
@@ -521,13 +521,13 @@ class _Head(torch.autograd.Function):
         rows = (M + 63) // 64
         slab = torch.empty(max(rows, 1), P, device=x.device, dtype=torch.float32) if wgrad else None
 
-        bg, bya, byb, bsp, bw = (N.ptr(bce[0]), N.ptr(bce[1]), N.ptr(bce[2]), bce[3], bce[4]) if bce else \
-            (None, None, None, 0, 0.0)
+        bg, bya, byb, bsp, bw, bnv = (N.ptr(bce[0]), N.ptr(bce[1]), N.ptr(bce[2]), bce[3], bce[4],
+                                      N.ptr(bce[5])) if bce else (None, None, None, 0, 0.0, None)
 
         def launch():
             N.check(lib.sgg_head_bwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(W2), N.ptr(hid), N.ptr(y),
                                      None if bce else N.ptr(dy), ctx.act, N.ptr(dx), dx.stride(0), N.ptr(slab),
-                                     bg, bya, byb, bsp, bw, N.stream_ptr()), "sgg_head_bwd")
+                                     bg, bya, byb, bsp, bw, bnv, N.stream_ptr()), "sgg_head_bwd")
         launch()
         if timer.active and M > 0:
             timer.add("sgg::head_bwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1, wgrad),
@@ -785,12 +785,14 @@ class _Pool(torch.autograd.Function):
             assert U.shape == (B, 512) and U.is_contiguous()
         out = torch.empty(B, bn, device=h.device, dtype=torch.float32)
         am = torch.empty(B, bn, device=h.device, dtype=torch.int32)
-        chunks, nchunks, max_rows, gpw = scenes.pool_plan(bn)
+        plan = scenes.pool_plan(bn)
+        chunks, nchunks, max_rows, gpw = plan[:4]
+        ncd = plan[4] if len(plan) > 4 else None    # a fixed-capacity plan's device chunk count
 
         def launch():
             N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(scenes.scene_off),
                                      N.ptr(chunks), nchunks, max_rows, gpw, B, bn, scenes.max_n, N.ptr(out),
-                                     N.ptr(am), N.stream_ptr()), "sgg_pool_fwd")
+                                     N.ptr(am), N.ptr(ncd), N.stream_ptr()), "sgg_pool_fwd")
         launch()
         if timer.active:
             # the form the library picks (pool.hip launch_fwd_g)
@@ -1626,30 +1628,30 @@ def lstm_sequence(rel, lstm, emb, h0=None, c0=None, proj=None, decoder=False, T=
 # ---------------------------------------------------------------------------
 class _Bce(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, ya, yb, split, w):
+    def forward(ctx, x, ya, yb, split, w, nvalid):
         ctx.shape = x.shape
         ctx.bce_link = getattr(x, "_sgg_bce_link", None)
         x = _req(x, "scores").contiguous().view(-1)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss), None,
-                                   None, N.stream_ptr()), "sgg_bce_fwd")
-        ctx.meta = (split, float(w))
+                                   None, N.ptr(nvalid), N.stream_ptr()), "sgg_bce_fwd")
+        ctx.meta = (split, float(w), nvalid)
         ctx.save_for_backward(x, ya, yb)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         x, ya, yb = ctx.saved_tensors
-        split, w = ctx.meta
+        split, w, nvalid = ctx.meta
         if ctx.bce_link is not None:   # the head backward forms the scores' gradient (BceLink)
             ph = torch.empty(ctx.shape, device=x.device, dtype=torch.float32)
-            ctx.bce_link.put(g, ya, yb, split, w, ph)
-            return ph, None, None, None, None
+            ctx.bce_link.put(g, ya, yb, split, w, ph, nvalid)
+            return ph, None, None, None, None, None
         g = g.contiguous()
         dx = torch.empty_like(x)
         N.check(_lib().sgg_bce_bwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), w, N.ptr(g), N.ptr(dx),
-                                   N.stream_ptr()), "sgg_bce_bwd")
-        return dx.view(ctx.shape), None, None, None, None
+                                   N.ptr(nvalid), N.stream_ptr()), "sgg_bce_bwd")
+        return dx.view(ctx.shape), None, None, None, None, None
 
 
 _CONST = {}
@@ -1682,7 +1684,7 @@ class _BceTotal(torch.autograd.Function):
     and its total loss with the L2 term (no separate add launch)."""
 
     @staticmethod
-    def forward(ctx, x, ya, yb, split, w, addend):
+    def forward(ctx, x, ya, yb, split, w, addend, nvalid):
         ctx.shape = x.shape
         ctx.bce_link = getattr(x, "_sgg_bce_link", None)
         x = _req(x, "scores").contiguous().view(-1)
@@ -1690,8 +1692,8 @@ class _BceTotal(torch.autograd.Function):
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         total = torch.empty((), device=x.device, dtype=torch.float32)
         N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
-                                   N.ptr(addend), N.ptr(total), N.stream_ptr()), "sgg_bce_fwd")
-        ctx.meta = (split, float(w))
+                                   N.ptr(addend), N.ptr(total), N.ptr(nvalid), N.stream_ptr()), "sgg_bce_fwd")
+        ctx.meta = (split, float(w), nvalid)
         ctx.save_for_backward(x, ya, yb)
         ctx.set_materialize_grads(False)
         return loss, total
@@ -1699,33 +1701,35 @@ class _BceTotal(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_total):
         x, ya, yb = ctx.saved_tensors
-        split, w = ctx.meta
+        split, w, nvalid = ctx.meta
         g = g_total if g_loss is None else (g_loss if g_total is None else g_loss + g_total)
         dx = None
         if g is not None and ctx.needs_input_grad[0] and ctx.bce_link is not None:
             dx = torch.empty(ctx.shape, device=x.device, dtype=torch.float32)   # the head backward forms it
-            ctx.bce_link.put(g, ya, yb, split, w, dx)
+            ctx.bce_link.put(g, ya, yb, split, w, dx, nvalid)
         elif g is not None and ctx.needs_input_grad[0]:
             g = g.contiguous()
             dx = torch.empty_like(x)
             N.check(_lib().sgg_bce_bwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), w, N.ptr(g), N.ptr(dx),
-                                       N.stream_ptr()), "sgg_bce_bwd")
+                                       N.ptr(nvalid), N.stream_ptr()), "sgg_bce_bwd")
             dx = dx.view(ctx.shape)
-        return dx, None, None, None, None, g_total
+        return dx, None, None, None, None, g_total, None
 
 
-def bce_pair_total(scores, split, y_a, y_b, w, addend):
+def bce_pair_total(scores, split, y_a, y_b, w, addend, nvalid=None):
     """(bce_pair(...), bce_pair(...) + addend) from one launch; the backward of
     the total passes its gradient to the addend unchanged."""
     dev = scores.device
-    return _BceTotal.apply(scores, _scalar_dev(y_a, dev), _scalar_dev(y_b, dev), int(split), w, addend)
+    return _BceTotal.apply(scores, _scalar_dev(y_a, dev), _scalar_dev(y_b, dev), int(split), w, addend, nvalid)
 
 
-def bce_pair(scores, split, y_a, y_b, w=1.0):
+def bce_pair(scores, split, y_a, y_b, w=1.0, nvalid=None):
     """w * (bce_loss(scores[:split], y_a) + bce_loss(scores[split:], y_b)) with
-    scalar targets (python floats or device scalars); split = len -> one term."""
+    scalar targets (python floats or device scalars); split = len -> one term.
+    nvalid (device int32 scalar, a padded batch's PaddedScenes.nvalid): only
+    the first *nvalid scores of each range are real."""
     dev = scores.device
-    return _Bce.apply(scores, _scalar_dev(y_a, dev), _scalar_dev(y_b, dev), int(split), w)
+    return _Bce.apply(scores, _scalar_dev(y_a, dev), _scalar_dev(y_b, dev), int(split), w, nvalid)
 
 
 # ---------------------------------------------------------------------------

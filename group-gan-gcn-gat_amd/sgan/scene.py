@@ -135,3 +135,242 @@ class Groups:
         self.cap = max(scenes.B, 1)                       # group rows allocated
         # 1/|g(i)| per ped (the R^T un-pool of the normalised R, models.py:286)
         self.ped_inv_size = group_count.index_select(0, ped_gid.long()).float().reciprocal()
+
+
+# ---------------------------------------------------------------------------
+# fixed-capacity scene index: HIP-graph replays over real batches
+# ---------------------------------------------------------------------------
+def padded_sizes(sizes, S_cap, B_cap, np_cap):
+    """Scene sizes of a batch padded to exactly S_cap scenes / B_cap peds: the
+    real scenes first, then S_cap - S padding scenes sharing the B_cap - B
+    padding peds evenly (>= 1 each, so no scene is empty).  None when the
+    batch does not fit (too many scenes or peds, a scene over np_cap, or too
+    few padding peds for the padding scenes)."""
+    sizes = np.asarray(sizes, dtype=np.int64)
+    S, B = len(sizes), int(sizes.sum())
+    ps, pp = S_cap - S, B_cap - B
+    if ps < 0 or pp < 0 or (S and sizes.max() > np_cap) or (ps == 0) != (pp == 0) or pp < ps \
+            or pp > ps * np_cap:
+        return None
+    pad = np.full(ps, pp // ps if ps else 0, dtype=np.int64)
+    pad[:pp - int(pad.sum())] += 1
+    return np.concatenate([sizes, pad])
+
+
+class PaddedScenes(SceneIndex):
+    """A SceneIndex of fixed capacity -- S_cap scenes, B_cap peds, scenes of
+    at most np_cap peds -- whose device arrays keep their addresses while
+    load() refreshes their contents for each batch, so a training iteration
+    captured in a HIP graph on it replays for every real batch that fits
+    (sgan.train_step.BucketedGraphTrainer; the reference's loader yields
+    batches of varying scene / ped counts, scripts/train.py:279-297).
+
+    A batch is padded with extra scenes of zero-trajectory, zero-mask peds
+    (padded_sizes; their input rows are -1 for sgg_gather_batch).  Padding
+    scenes interact with nothing (message passing never crosses a scene);
+    the losses leave them out: the L2 term of a scene without a masked step
+    is 0 (sgg_l2_loss_*), and the BCE means run over the first `nvalid`
+    scores of each range (sgg_bce_*, sgg_head_bwd) -- the real peds, which
+    come first.  Everything the kernels read per batch lives in ONE packed
+    int32 device buffer (nvalid | scene_off | ped scene | gather rows | the
+    repeats' scene_off | per pooling plan its chunk count and table; the
+    pooling kernels walk the device count, sgg_pool_fwd nchunks_dev),
+    refreshed by one host-to-device copy per batch from alternating pinned
+    staging buffers."""
+
+    MAX_PLANS = 6
+
+    def __init__(self, S_cap, B_cap, device, np_cap=64, reps=(2,), pool_cap=None):
+        self.S, self.B, self.max_n = int(S_cap), int(B_cap), int(np_cap)
+        self.device = device
+        self._labels = self._groups = None
+        self.reps = tuple(reps)
+        # every chunk holds >= 1 row: a plan over the largest repeat never needs more
+        self.pool_cap = int(pool_cap or max(self.reps + (1,)) * (self.B + self.S))
+        o = 4
+        self._lay = {"nvalid": 0, "scene_off": o}
+        o += self.S + 1
+        self._lay["ped_scene"] = o
+        o += self.B
+        self._lay["rows"] = o
+        o += self.B
+        for r in self.reps:
+            self._lay["rep%d" % r] = o
+            o += r * self.S + 1
+        self._plan_base = o = (o + 3) & ~3
+        self._plans = []                       # [(rep, bn, gpw)] registered, region k at plan_base + 4 k pool_cap
+        self._total = o + self.MAX_PLANS * (4 + 4 * self.pool_cap)
+        self._used = self._plan_base
+        self._dev = torch.zeros(self._total, dtype=torch.int32, device=device)
+        self._gpu = torch.device(device).type == "cuda"   # (a host-only index packs the same layout: tests)
+        self._stage = [torch.zeros(self._total, dtype=torch.int32) for _ in range(2)]
+        if self._gpu:
+            self._stage = [t.pin_memory() for t in self._stage]
+        self._stage_ev = [None, None]
+        self._cur = 0
+        self.nvalid = self._dev[0:1]
+        self.scene_off = self._view("scene_off", self.S + 1)
+        self._ped32 = self._view("ped_scene", self.B)
+        self.rows = self._view("rows", self.B)
+        self._children = {}
+        self.host_off = np.arange(self.S + 1, dtype=np.int64) * 0
+        self._host_rows = None
+        self._host_off_real = None
+
+    def _view(self, name, n):
+        o = self._lay[name]
+        return self._dev[o:o + n]
+
+    # -- SceneIndex API ------------------------------------------------------
+    def repeat(self, k):
+        if k == 1:
+            return self
+        if k not in self.reps:
+            raise NotImplementedError("PaddedScenes: repeat(%d) not reserved (reps=%s)" % (k, self.reps))
+        if k not in self._children:
+            self._children[k] = _PaddedRepeat(self, k)
+        return self._children[k]
+
+    def ped_scene_i32(self):
+        return self._ped32
+
+    def ped_scene_long(self):
+        raise NotImplementedError("PaddedScenes: no int64 ped-scene map (the fused decoder path does not use it)")
+
+    def _plan_region(self, k):
+        """Offset of plan k: [chunk count, 0, 0, 0 | pool_cap x (scene, i0, i1, gpw)]."""
+        return self._plan_base + (4 + 4 * self.pool_cap) * k
+
+    def pool_plan(self, bn, target_chunks=None, rep=1):
+        """(chunk table, grid basis, max rows, gpw, device chunk count): the
+        table holds up to pool_cap chunks; the kernels walk the device count,
+        the grid is sized by the chunk count of the batch that registered the
+        plan (the capture's)."""
+        for k, (r, b, gpw, grid) in enumerate(self._plans):
+            if (r, b) == (rep, bn):
+                o = self._plan_region(k)
+                tab = self._dev[o + 4:o + 4 + 4 * self.pool_cap].view(self.pool_cap, 4)
+                return tab, grid, SGG_POOL_MAX_ROWS, gpw, self._dev[o:o + 1]
+        # first use (warm-up, before capture): the chunk shape of this batch
+        # by the normal heuristic, then fixed for every later batch
+        if len(self._plans) >= self.MAX_PLANS:
+            raise RuntimeError("PaddedScenes: more than %d pooling plans" % self.MAX_PLANS)
+        off = self._rep_off(self.host_off, rep)
+        _, nc, _, gpw = _plan(off, rep * self.S, bn, target_chunks or self.POOL_TARGET_CHUNKS, self.POOL_MAX_GPW,
+                              self.pool_cap)
+        self._plans.append((rep, bn, gpw, max(nc, 1)))
+        self._used = self._plan_region(len(self._plans))
+        if self._host_off_real is not None:    # fill the new region now (synchronously: before any capture)
+            self.load(self._host_off_real, self._host_rows)
+            if self._gpu:
+                torch.cuda.current_stream(self.device).synchronize()
+        return self.pool_plan(bn, rep=rep)
+
+    def groups(self, labels):
+        """The device group index of SceneIndex.groups, rebuilt on every call:
+        the labels buffer is rewritten by each replay's batch gather behind
+        torch's back, so no cached index may outlive a step."""
+        self._groups = None
+        return SceneIndex.groups(self, labels)
+
+    # -- per batch -----------------------------------------------------------
+    def _rep_off(self, off, r):
+        return np.concatenate([[0]] + [off[1:] + k * self.B for k in range(r)]).astype(np.int64)
+
+    def fits(self, sizes):
+        return padded_sizes(sizes, self.S, self.B, self.max_n) is not None
+
+    def pack(self, host_off_real, rows_real, out):
+        """Fill `out` (int32, numpy, >= the used length) for a batch: real scene
+        offsets host_off_real (S + 1) and its peds' table rows rows_real (B)."""
+        sizes = padded_sizes(np.diff(host_off_real), self.S, self.B, self.max_n)
+        if sizes is None:
+            raise ValueError("PaddedScenes: batch (S=%d, B=%d, max n=%d) does not fit (S_cap=%d, B_cap=%d, "
+                             "np_cap=%d)" % (len(host_off_real) - 1, int(host_off_real[-1]),
+                                             int(np.diff(host_off_real).max()), self.S, self.B, self.max_n))
+        off = np.concatenate([[0], np.cumsum(sizes)])
+        B_r = int(host_off_real[-1])
+        L = self._lay
+        out[:self._used] = 0
+        out[0] = B_r
+        out[L["scene_off"]:L["scene_off"] + self.S + 1] = off
+        out[L["ped_scene"]:L["ped_scene"] + self.B] = np.repeat(np.arange(self.S), sizes)
+        r0 = L["rows"]
+        out[r0:r0 + B_r] = rows_real
+        out[r0 + B_r:r0 + self.B] = -1
+        for r in self.reps:
+            o = L["rep%d" % r]
+            out[o:o + r * self.S + 1] = self._rep_off(off, r)
+        for k, (r, bn, gpw, _) in enumerate(self._plans):
+            o = self._plan_region(k)
+            tab, nc, _, g = _plan(self._rep_off(off, r), r * self.S, bn, 0, gpw, self.pool_cap)
+            assert g == gpw, (g, gpw)
+            out[o] = nc
+            out[o + 4:o + 4 + 4 * nc] = tab[:nc].reshape(-1)
+        return off
+
+    def load(self, host_off_real, rows_real):
+        """Refresh the device arrays for a batch: one asynchronous host-to-
+        device copy on the current stream (graph replays issued after it read
+        the new contents)."""
+        i = self._cur
+        self._cur ^= 1
+        if self._stage_ev[i] is not None:
+            self._stage_ev[i].synchronize()      # that staging buffer's previous copy has been consumed
+        host_off_real = np.asarray(host_off_real, dtype=np.int64)
+        st = self._stage[i].numpy()
+        self.host_off = self.pack(host_off_real, np.asarray(rows_real, dtype=np.int32), st)
+        self._host_off_real, self._host_rows = host_off_real, np.asarray(rows_real, dtype=np.int32)
+        for ch in self._children.values():
+            ch.host_off = self._rep_off(self.host_off, ch.k)
+        self._dev[:self._used].copy_(self._stage[i][:self._used], non_blocking=self._gpu)
+        if self._gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._stage_ev[i] = ev
+
+
+class _PaddedRepeat(SceneIndex):
+    """repeat(k) of a PaddedScenes: k back-to-back copies (the D-step's
+    [fake | real] batch), views into the parent's packed buffer."""
+
+    def __init__(self, parent, k):
+        self.parent, self.k = parent, k
+        self.S, self.B, self.max_n = k * parent.S, k * parent.B, parent.max_n
+        self.device = parent.device
+        self._labels = self._groups = None
+        self.nvalid = parent.nvalid
+        self.scene_off = parent._view("rep%d" % k, self.S + 1)
+        self.host_off = parent._rep_off(parent.host_off, k)
+
+    def repeat(self, k):
+        raise NotImplementedError("repeat of a repeated PaddedScenes")
+
+    def ped_scene_i32(self):
+        raise NotImplementedError("PaddedScenes.repeat: no ped-scene map")
+
+    def ped_scene_long(self):
+        raise NotImplementedError("PaddedScenes.repeat: no ped-scene map")
+
+    def pool_plan(self, bn, target_chunks=None):
+        return self.parent.pool_plan(bn, target_chunks, rep=self.k)
+
+    def groups(self, labels):
+        raise NotImplementedError("PaddedScenes: the per-op group index is not captured")
+
+
+SGG_POOL_MAX_ROWS = 64   # chunk height bound of sgg_pool_fwd (a padded plan's LDS is sized for it)
+
+
+def _plan(off, S, bn, target, max_gpw, cap):
+    """sgg_pool_plan on a host offset array -> (table (cap x 4) int32, nchunks, max_rows, gpw)."""
+    import ctypes
+    lib = N.load(require_gpu=False)
+    off = np.ascontiguousarray(np.asarray(off).astype(np.int32))
+    tab = np.zeros((max(cap, 1), 4), dtype=np.int32)
+    mr, gpw = ctypes.c_int(0), ctypes.c_int(0)
+    nc = lib.sgg_pool_plan(off.ctypes.data_as(ctypes.c_void_p), S, bn, target, max_gpw,
+                           tab.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(mr), ctypes.byref(gpw))
+    if nc < 0:
+        N.check(nc, "sgg_pool_plan")
+    return tab, int(nc), int(mr.value), int(gpw.value)

@@ -69,6 +69,12 @@ def _sse_of(sc):
     return torch.from_numpy(np.stack([sc.host_off[:-1], sc.host_off[1:]], 1))
 
 
+def _valid(sc):
+    """The BCE's real-score count of a padded batch (PaddedScenes.nvalid)."""
+    nv = getattr(sc, "nvalid", None)
+    return {"nvalid": nv} if nv is not None else {}
+
+
 class DataParallel:
     """Scene-sharded DP context (world 1 = plain single-GPU)."""
 
@@ -223,7 +229,7 @@ class GanTrainer:
             y_real = random.uniform(0.7, 1.2)
             random.uniform(0, 0.3)   # the fake-label draw (losses.py:47): consumed, but zeros_like * y == 0
         # gan_d_loss = bce(real, y_real) + bce(fake, 0); scores = [fake | real]
-        loss = self.bce_pair(scores, sc.B, 0.0, y_real, sc.B / B_global)
+        loss = self.bce_pair(scores, sc.B, 0.0, y_real, sc.B / B_global, **_valid(sc))
         self.opt_d.zero_grad(set_to_none=True)
         torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device))
         vals = self._finish(self.d_params, self.opt_d, [loss], a.clipping_threshold_d)
@@ -299,9 +305,9 @@ class GanTrainer:
         total = getattr(self.ops, "bce_pair_total", None)
         if terms and total is not None and self._bce_override is None:
             # gan_g_loss and the total loss with the L2 term from one launch
-            adv, loss = total(scores, scores.shape[0], y, y, sc.B / B_global, terms[0])
+            adv, loss = total(scores, scores.shape[0], y, y, sc.B / B_global, terms[0], **_valid(sc))
         else:
-            adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global)    # gan_g_loss
+            adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global, **_valid(sc))    # gan_g_loss
             loss = adv + (terms[0] if terms else 0.0)
         self.opt_g.zero_grad(set_to_none=True)
         torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self._g_inputs())
@@ -358,8 +364,12 @@ class GraphedTrainer:
     device)."""
 
     def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2, batch_g=None,
-                 sc_g=None):
+                 sc_g=None, draw=None, prologue=None):
+        """draw: () -> (z_d, z_g, y) host tensors of the staging shapes (default:
+        trainer.draw_inputs over this rank's span); prologue: launches captured
+        ahead of the step (the padded real-data path's batch gathers)."""
         self.t = trainer
+        self.prologue = prologue or (lambda: None)
         self.batch, self.sc = batch, sc
         self.batch_g, self.sc_g = batch_g, sc_g
         if batch_g is not None:
@@ -368,6 +378,7 @@ class GraphedTrainer:
         dev = batch[0].device
         s0 = shard[0]
         self.span = (self.kw["S_global"], s0, s0 + sc.S)
+        self.draw = draw or (lambda: trainer.draw_inputs(*self.span))
         G = trainer.G
         nd = tuple(G.noise_dim) if G.noise_dim else None
         k = trainer.args.best_k
@@ -392,7 +403,8 @@ class GraphedTrainer:
         cap.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(cap):
             for _ in range(warmup):
-                self._load(*trainer.draw_inputs(*self.span))
+                self._load(*self.draw())
+                self.prologue()
                 trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
         torch.cuda.current_stream().wait_stream(cap)
         torch.cuda.synchronize()
@@ -423,6 +435,7 @@ class GraphedTrainer:
                     g = torch.cuda.CUDAGraph()
                     g.capture_begin(pool=torch.cuda.graph_pool_handle())
                     self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
+                    self.prologue()
                     losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
                     g.capture_end()
                 self.pair.append((g, losses, [(p, p.grad) for p in params]))
@@ -446,6 +459,7 @@ class GraphedTrainer:
                 g.capture_begin(pool=pool)
             dp.cut = cut if (dp.on and dp.world > 1) else None
             try:
+                self.prologue()
                 self.losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
             finally:
                 dp.cut = None
@@ -479,7 +493,7 @@ class GraphedTrainer:
             self.cur ^= 1
             if self.done_ev[i] is not None:
                 self.done_ev[i].synchronize()     # graph i's previous replay has read buffer i
-            z_d, z_g, y = self.t.draw_inputs(*self.span)
+            z_d, z_g, y = self.draw()
             h_zd, h_zg, h_y = self.stage[i]
             if z_d is not None:
                 h_zd.copy_(z_d)
@@ -493,7 +507,7 @@ class GraphedTrainer:
             self.done_ev[i] = ev
             self._after_replay(grads)
             return self.losses
-        self._load(*self.t.draw_inputs(*self.span))
+        self._load(*self.draw())
         for g, tensors in self.segments:
             g.replay()
             if tensors is not None:
@@ -524,3 +538,145 @@ def shard_batch(batch, sc, s0, s1):
     sse_l = _sse_of(local)
     return (t(obs), t(pred), t(obs_rel), t(pred_rel), t(ov), t(pv), t(obs_g), t(pg), nl[p0:p1], lm[p0:p1],
             sse_l), local
+
+
+class BucketedGraphTrainer:
+    """HIP-graph replayed training on REAL batches.  The reference's loader
+    yields batches of varying scene and ped counts (scripts/train.py:279-297:
+    the D-step takes one loader batch, the G-step the next), which one
+    captured graph cannot take.  Here each iteration's two batches are padded
+    into a capacity bucket -- S_cap = batch_size + pad_scenes scenes and B_cap
+    peds, a multiple of `gran` (sgan.scene.PaddedScenes: padding scenes of
+    zero-mask peds that the losses leave out) -- whose iteration was captured
+    once (GraphedTrainer over fixed-address buffers, the batch gathers from
+    the device-resident split included).  A replay then needs two packed
+    host-to-device copies (the batches' scene structure) and the host RNG
+    draws, exactly the eager step's (noise of the real scenes only).
+
+    A bucket is (B_cap, np_cap): np_cap, the largest scene it holds, is the
+    smallest of `np_caps` that fits both batches (the kernels size their LDS
+    plans by it; the one-launch GAT encoder's backward holds scenes of <= 48
+    peds, larger ones take the per-layer GAT kernels).
+
+    Capturing a new bucket runs GraphedTrainer's warm-up iterations; the
+    parameters, the optimizer state and the host RNG states are saved before
+    and restored after, so training is unchanged by a capture.  A batch that
+    fits no bucket (a scene over max(np_caps) peds) runs eagerly."""
+
+    def __init__(self, trainer, ddset, batch_size=64, pad_scenes=32, gran=256, np_caps=(48, 64), pool_cap=None):
+        if trainer.dp.on and trainer.dp.world > 1:
+            raise NotImplementedError("BucketedGraphTrainer: one rank (the padded batches are not sharded)")
+        self.t, self.dd = trainer, ddset
+        self.S_cap = batch_size + pad_scenes
+        self.gran, self.np_caps, self.pool_cap = gran, tuple(sorted(np_caps)), pool_cap
+        self.buckets = {}
+        self.eager_steps = 0
+
+    def bucket_of(self, off_d, off_g):
+        """(B_cap, np_cap) of the bucket holding both batches, or None."""
+        need, big = 0, 0
+        for off in (off_d, off_g):
+            S, B = len(off) - 1, int(off[-1])
+            if S > self.S_cap or S == 0:
+                return None
+            big = max(big, int(np.diff(off).max()))
+            need = max(need, B + max(self.S_cap - S, 1))
+        caps = [c for c in self.np_caps if c >= big]
+        if not caps:
+            return None
+        B_cap = -(-need // self.gran) * self.gran
+        from .scene import padded_sizes
+        for off in (off_d, off_g):
+            if padded_sizes(np.diff(off), self.S_cap, B_cap, caps[0]) is None:
+                return None
+        return B_cap, caps[0]
+
+    def step(self, scenes_d, scenes_g):
+        """One reference iteration: the D-step on the split's scenes scenes_d,
+        the G-step on scenes_g (the two consecutive loader batches)."""
+        off_d, rows_d = self.dd.layout(scenes_d)
+        off_g, rows_g = self.dd.layout(scenes_g)
+        key = self.bucket_of(off_d, off_g)
+        if key is None:
+            self.eager_steps += 1
+            bd, scd = self.dd.batch(scenes_d)
+            bg, scg = self.dd.batch(scenes_g)
+            return self.t.step(bd, scd, bg, scg)
+        ent = self.buckets.get(key)
+        if ent is None:
+            ent = self.buckets[key] = self._capture(key, off_d, rows_d, off_g, rows_g)
+        ent["sc_d"].load(off_d, rows_d)
+        ent["sc_g"].load(off_g, rows_g)
+        ent["S_real"] = (len(off_d) - 1, len(off_g) - 1)
+        return ent["gt"].step()
+
+    def _draw(self, ent):
+        """The host RNG draws of one iteration in the reference's order
+        (StepInputs; TrainArgs.draw_inputs with the two batches' own scene
+        counts), zero-padded to S_cap rows."""
+        t = self.t
+        S_d, S_g = ent["S_real"]
+
+        def pad(z):
+            if z is None:
+                return None
+            out = torch.zeros((self.S_cap,) + tuple(z.shape[1:]), dtype=z.dtype)
+            out[:z.shape[0]] = z
+            return out
+        z_d = pad(t._noise(S_d, 0, S_d))
+        yr, yf = random.uniform(0.7, 1.2), random.uniform(0, 0.3)
+        z_g = [pad(t._noise(S_g, 0, S_g)) for _ in range(t.args.best_k)]
+        yg = random.uniform(0.7, 1.2)
+        return z_d, (torch.stack(z_g, 0) if z_g[0] is not None else None), torch.tensor([yr, yf, yg])
+
+    def _state(self):
+        ts = [p.data for p in self.t.g_params + self.t.d_params]
+        for opt in (self.t.opt_g, self.t.opt_d):
+            for p in opt.params:
+                st = opt.opt.state.get(p)
+                if st:
+                    ts += [st["step"], st["exp_avg"], st["exp_avg_sq"]]
+        return ts
+
+    def _capture(self, key, off_d, rows_d, off_g, rows_g):
+        from .scene import PaddedScenes
+        B_cap, np_cap = key
+        lib = N_lib()
+        dev = self.dd.device
+        dd = self.dd
+        To, Tp = dd.obs_len, dd.pred_len
+        ent = {"S_real": (len(off_d) - 1, len(off_g) - 1)}
+        ent["sc_d"] = PaddedScenes(self.S_cap, B_cap, dev, np_cap, reps=(2,), pool_cap=self.pool_cap)
+        ent["sc_g"] = PaddedScenes(self.S_cap, B_cap, dev, np_cap, reps=(), pool_cap=self.pool_cap)
+        ent["sc_d"].load(off_d, rows_d)
+        ent["sc_g"].load(off_g, rows_g)
+        nf = int(lib.sgg_gather_batch_floats(B_cap, To, Tp))
+        bufs = [torch.empty(nf, device=dev, dtype=torch.float32) for _ in range(2)]
+        batches = [dd.views(b, B_cap, sc.host_off) for b, sc in zip(bufs, (ent["sc_d"], ent["sc_g"]))]
+
+        def prologue():
+            for b, sc in zip(bufs, (ent["sc_d"], ent["sc_g"])):
+                dd.gather_into(sc.rows, B_cap, b)
+        # the warm-up iterations must leave no trace: parameters, optimizer
+        # state (created here where missing: zeros == torch Adam's fresh
+        # state) and the host RNG streams are restored afterwards
+        before = {t.data_ptr(): t.clone() for t in self._state()}
+        rng = (torch.get_rng_state(), random.getstate())
+        try:
+            gt = GraphedTrainer(self.t, batches[0], ent["sc_d"], warmup=2, batch_g=batches[1], sc_g=ent["sc_g"],
+                                draw=lambda: self._draw(ent), prologue=prologue)
+        finally:
+            with torch.no_grad():
+                for t in self._state():
+                    t.copy_(before[t.data_ptr()]) if t.data_ptr() in before else t.zero_()
+            torch.set_rng_state(rng[0])
+            random.setstate(rng[1])
+            K.clear_fold_cache()
+        torch.cuda.synchronize()
+        ent.update(gt=gt, bufs=bufs, batches=batches)
+        return ent
+
+
+def N_lib():
+    from . import _native
+    return _native.load()

@@ -84,14 +84,18 @@ int sgg_xw_bf16(const float* X, int ldx, const float* Xmask, int ldm, const floa
  * 16-pair groups per wave in *gpw (1, 2, 4 or 8: the widest that still gives
  * >= target_chunks workgroups, capped by max_gpw when > 0; ~2-4x the CU
  * count keeps small batches busy).
- * Pass max_rows and gpw unchanged to sgg_pool_fwd.
+ * Pass max_rows and gpw unchanged to sgg_pool_fwd.  A chunk with i1 <= i0 is
+ * skipped.  nchunks_dev (optional, one device int32): the number of chunks
+ * the workgroups walk (grid-stride) is read on the device, while nchunks
+ * sizes the grid and picks the kernel form -- a fixed-capacity plan whose
+ * chunk count varies between graph replays (sgan.scene.PaddedScenes).
  */
 int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int target_chunks, int max_gpw,
                   int32_t* host_chunks, int cap, int* max_rows, int* gpw);
 int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2,
                  const float* b2, const int32_t* scene_off, const int32_t* chunks, int nchunks,
                  int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,
-                 void* stream);
+                 const int32_t* nchunks_dev, void* stream);
 
 /* Backward of sgg_pool_fwd.  Only the (i, argmax[i,c]) pairs carry gradient
  * (torch.max(dim) backward, models.py:541).  Writes dU (B x 512, every row),
@@ -296,10 +300,12 @@ int sgg_head_fwd(const float* X, int ldx, int M, int K, int N1, const float* W1,
 /* bce_g != NULL: dY is not read; the head's output gradient is formed in the
  * launch from the BCE loss on Y that sgg_bce_fwd computed (losses.py:5-21):
  * dY[m] = (bce_g * bce_w / count) * d bce(Y[m], m < bce_split ? ya : yb) / dY,
- * count = bce_split or M - bce_split -- sgg_bce_bwd's expression. */
+ * count = bce_split or M - bce_split -- sgg_bce_bwd's expression (with
+ * bce_nvalid, as sgg_bce_bwd: the real rows of each range only). */
 int sgg_head_bwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* w2, const float* hid,
                  const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, const float* bce_g,
-                 const float* bce_ya, const float* bce_yb, int bce_split, float bce_w, void* stream);
+                 const float* bce_ya, const float* bce_yb, int bce_split, float bce_w, const int32_t* bce_nvalid,
+                 void* stream);
 
 /* ------------------------------------------------------------------------
  * Input-embedding fold (a Linear(2, E) displacement embedding feeding a
@@ -421,14 +427,18 @@ int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float*
  * An empty range contributes 0.  ya, yb are device scalars (graph-capturable
  * label smoothing); loss is one device float.  total (optional, with the
  * device scalar addend): *total = *loss + *addend -- the generator's total
- * loss (gan_g_loss + the L2 term, train.py:471-474) in the same launch. */
+ * loss (gan_g_loss + the L2 term, train.py:471-474) in the same launch.
+ * nvalid (optional, one device int32): a padded batch (the fixed-capacity
+ * scene index of the graph-replayed real-data path): only the first *nvalid
+ * scores of each range are real; the means run over them. */
 int sgg_bce_fwd(const float* x, int n, int split, const float* ya, const float* yb, float w, float* loss,
-                const float* addend, float* total, void* stream);
+                const float* addend, float* total, const int32_t* nvalid, void* stream);
 
 /* dx_i = *gout * w / |range(i)| * df/dx(x_i, y_range(i)) with torch's
- * subgradients at 0 (clamp passes x >= 0, d|x| = sign(x) = 0 at 0). */
+ * subgradients at 0 (clamp passes x >= 0, d|x| = sign(x) = 0 at 0); with
+ * nvalid, |range| counts the real scores and the padding scores get 0. */
 int sgg_bce_bwd(const float* x, int n, int split, const float* ya, const float* yb, float w,
-                const float* gout, float* dx, void* stream);
+                const float* gout, float* dx, const int32_t* nvalid, void* stream);
 
 /* ------------------------------------------------------------------------
  * Optimizer step of the training loop (scripts/train.py:418-427 and :472-482:
@@ -623,6 +633,7 @@ int sgg_l2_select(const float* pred, const float* gt, const float* mask, int ldm
 
 /* sgg_l2_loss_fwd: loss = sum_s w * sum_{i in s, t} mask (gt - pred)^2 / msum_s,
  * msum_s = sum_{i in s, t} mask (train.py:459-464, losses.py:52-71 'raw');
+ * a scene with msum_s = 0 (only padding scenes) adds 0 and gets 0 gradient;
  * writes msum (S) and uses term_ws (S floats).  sgg_l2_loss_bwd: dpred =
  * gout * w * -2 mask (gt - pred) / msum_{s(i)}. */
 int sgg_l2_loss_fwd(const float* pred, int ldp, const float* gt, const float* mask, int ldm, const int32_t* scene_off,
@@ -640,7 +651,8 @@ int sgg_l2_loss_bwd(const float* pred, int ldp, const float* gt, const float* ma
  * (sgg_gather_batch_floats(B, ..) floats): obs_traj, pred_traj,
  * obs_traj_rel, pred_traj_rel, obs_vel, pred_vel ((T_part x B x 2) each;
  * velocity = 2.5 x displacement), obs_traj_g, pred_traj_g (T_part x B),
- * non_linear_ped (B), loss_mask (B x T).  seq_start_end stays on the host. */
+ * non_linear_ped (B), loss_mask (B x T).  seq_start_end stays on the host.
+ * rows[b] < 0: a padding ped, written as zeros (loss mask included). */
 long long sgg_gather_batch_floats(int B, int obs_len, int pred_len);
 int sgg_gather_batch(const float* table, int rec, const int32_t* rows, int B, int obs_len, int pred_len, float* out,
                      void* stream);

@@ -625,6 +625,67 @@ def test_real_data_training_device_path_equals_host_path():
         assert torch.equal(wa[k], wb[k]), k
 
 
+@pytest.mark.parametrize("graph", ["gat", "gcn"])
+def test_bucketed_graph_replay_equals_eager_on_real_batches(graph):
+    """configs[1] on real data through HIP-graph replays: the padded
+    capacity-bucket path (BucketedGraphTrainer, PaddedScenes) against eager
+    GanTrainer iterations on the same consecutive zara1-train batch pairs,
+    from the same seeds: every loss and every parameter after each of three
+    iterations.  The graphed run captures its bucket(s) inside the first
+    step (parameters / optimizer state / host RNGs restored after the
+    warm-up), so any trace of the capture would show here.  Padding changes
+    only reduction lengths (zero terms, split-K boundaries): 1e-6."""
+    from sgan.data.device import DeviceLoader, DeviceTrajectoryDataset
+    from sgan.data.trajectories_GCN import TrajectoryDataset
+    from sgan.train_step import BucketedGraphTrainer, GanTrainer
+    dd = DeviceTrajectoryDataset(TrajectoryDataset(os.path.join(GOLDEN, "datasets_group", "zara1", "train")), DEV)
+    torch.manual_seed(4)
+    sb = DeviceLoader(dd, batch_size=64, shuffle=True).scene_batches()
+    pairs = [(next(sb), next(sb)) for _ in range(3)]
+    # the last loader batch of the epoch (fewer scenes) as one more D batch
+    sb = DeviceLoader(dd, batch_size=64, shuffle=False).scene_batches()
+    last = list(sb)[-1]
+    assert len(last) < 64
+    pairs.append((last, pairs[0][1]))
+    res = []
+    for graphed in (False, True):
+        torch.manual_seed(0)   # the family's modules the fixture does not cover (unused ones) init alike
+        g, d = reference_gd(graph)
+        tr = GanTrainer(g, d, capturable=True)
+        bt = BucketedGraphTrainer(tr, dd) if graphed else None
+        torch.manual_seed(11)
+        random.seed(11)
+        losses, ws = [], []
+        for sd, sg in pairs:
+            if graphed:
+                ld, lg = bt.step(sd, sg)
+            else:
+                (bd, scd), (bg, scg) = dd.batch(sd), dd.batch(sg)
+                ld, lg = tr.step(bd, scd, bg, scg)
+            losses.append({k: float(v) for k, v in list(ld.items()) + list(lg.items())})
+            ws.append({k: v.detach().cpu().clone() for k, v in list(g.state_dict().items())
+                       + [("d." + k, v) for k, v in d.state_dict().items()]})
+        if graphed:
+            assert bt.eager_steps == 0 and len(bt.buckets) >= 1
+        res.append((losses, ws))
+    (la, wa), (lb, wb) = res
+    worst = {}
+    for it in range(len(pairs)):
+        for k in la[it]:
+            assert abs(la[it][k] - lb[it][k]) <= 1e-6 * max(1.0, abs(la[it][k])), (it, k, la[it][k], lb[it][k])
+        for k in wa[it]:
+            err = (wa[it][k] - wb[it][k]).abs().max().item()
+            worst[(it, k)] = err
+    top = sorted(worst.items(), key=lambda kv: -kv[1])[:8]
+    print("largest parameter differences:", top)
+    # Adam normalises each element's step to ~lr: an fp32 reduction-order
+    # difference in a near-zero gradient element can move that element's
+    # update by a fraction of lr (1e-4 for G, 1e-3 for D)
+    for (it, k), err in worst.items():
+        lr = 1e-3 if k.startswith("d.") else 1e-4
+        assert err <= 0.1 * lr * (it + 1), (it, k, err)
+
+
 # ---------------------------------------------------------------------------
 # configs[0] on TRAINED checkpoints through the reference's get_generator
 # ---------------------------------------------------------------------------

@@ -430,7 +430,7 @@ def test_pool_resident_equals_tiled(bn, form, monkeypatch):
         am = torch.empty(B, bn, device=DEV, dtype=torch.int32)
         N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(sc.scene_off),
                                  N.ptr(chunks), nchunks, max_rows, gpw, B, bn, sc.max_n, N.ptr(out), N.ptr(am),
-                                 N.stream_ptr()), "pool")
+                                 None, N.stream_ptr()), "pool")
         res.append((out.cpu(), am.cpu()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     # and against a torch restatement of the pair MLP

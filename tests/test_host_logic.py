@@ -1,6 +1,9 @@
 """Host-side logic of the product that needs no GPU: optimizer-state format,
 scene sharding, trainer guards, device-scalar cache, the vanilla family's
 module set.  (No kernel is launched here.)"""
+import os
+
+import numpy as np
 import pytest
 import torch
 
@@ -171,3 +174,72 @@ def test_family_switch_keeps_shared_modules_and_sgangat_shapes():
         bad = _family_state("gat")
         bad.pop("gatencoder.out_embedding.bias")
         _reference_style_gen().load_state_dict(bad)
+
+
+def test_padded_sizes_fit_rules():
+    """padded_sizes: exactly S_cap scenes / B_cap peds, real scenes first,
+    padding scenes non-empty and within np_cap; None when it cannot fit."""
+    from sgan.scene import padded_sizes
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        S = int(rng.integers(1, 65))
+        sizes = rng.integers(1, 58, size=S)
+        S_cap, np_cap = 96, 64
+        B_cap = int(-(-(sizes.sum() + S_cap - S) // 256) * 256)
+        out = padded_sizes(sizes, S_cap, B_cap, np_cap)
+        assert out is not None and len(out) == S_cap and out.sum() == B_cap
+        assert np.array_equal(out[:S], sizes) and out[S:].min() >= 1 and out.max() <= np_cap
+    assert padded_sizes([70], 8, 128, 64) is None           # a scene over np_cap
+    assert padded_sizes([5] * 9, 8, 128, 64) is None        # too many scenes
+    assert padded_sizes([5, 5], 8, 12, 64) is None          # fewer padding peds than padding scenes
+    assert padded_sizes([5, 5], 2, 11, 64) is None          # padding peds but no padding scene
+    assert list(padded_sizes([5, 5], 2, 10, 64)) == [5, 5]
+
+
+def test_padded_scenes_pack_layout():
+    """PaddedScenes.pack (host side, the layout one H2D copy moves): scene
+    offsets, ped -> scene map, gather rows (-1 = padding), the repeat's
+    offsets, and per pooling plan a chunk count + table of the fixed gpw that
+    covers every (scene, row) of the padded batch exactly once."""
+    from sgan import _native
+    if not os.path.exists(_native.lib_path()):
+        pytest.skip("libsgg.so not built")
+    from sgan.scene import PaddedScenes
+    rng = np.random.default_rng(1)
+    ps = PaddedScenes(96, 1024, "cpu", np_cap=64, reps=(2,))
+    sizes = np.minimum(rng.geometric(0.1, size=64), 57)
+    sizes[:3] = (57, 40, 1)
+    off_r = np.concatenate([[0], np.cumsum(sizes)])
+    rows_r = rng.integers(0, 10000, size=int(off_r[-1])).astype(np.int32)
+    ps.load(off_r, rows_r)
+    for rep, bn in ((1, 8), (1, 48), (2, 48)):
+        sub = ps if rep == 1 else ps.repeat(2)
+        tab, grid, mr, gpw, cnt = sub.pool_plan(bn)
+        assert tab.shape == (ps.pool_cap, 4) and int(cnt) == grid and mr == 64 and gpw in (1, 2, 4)
+    for trial in range(3):
+        sizes = np.minimum(rng.geometric(0.1, size=64 - trial * 10), 57)
+        off_r = np.concatenate([[0], np.cumsum(sizes)])
+        B_r = int(off_r[-1])
+        assert B_r + 96 - len(sizes) <= 1024
+        rows_r = rng.integers(0, 10000, size=B_r).astype(np.int32)
+        ps.load(off_r, rows_r)
+        buf = ps._dev.numpy()
+        L = ps._lay
+        off = buf[L["scene_off"]:L["scene_off"] + 97]
+        assert buf[0] == B_r and off[-1] == 1024 and np.array_equal(off[:len(off_r)], off_r)
+        assert np.array_equal(buf[L["rows"]:L["rows"] + B_r], rows_r) and (buf[L["rows"] + B_r:L["rows"] + 1024] == -1).all()
+        ped = buf[L["ped_scene"]:L["ped_scene"] + 1024]
+        assert np.array_equal(ped, np.repeat(np.arange(96), np.diff(off)))
+        r2 = buf[L["rep2"]:L["rep2"] + 2 * 96 + 1]
+        assert np.array_equal(r2, np.concatenate([off, off[1:] + 1024]))
+        for k, (rep, bn, gpw, _) in enumerate(ps._plans):
+            o = ps._plan_region(k)
+            tab = buf[o + 4:o + 4 + 4 * ps.pool_cap].reshape(-1, 4)[:buf[o]]
+            so = off if rep == 1 else r2
+            seen = set()
+            for s, i0, i1, g in tab:
+                assert g == gpw
+                for i in range(i0, i1):
+                    assert (s, i) not in seen
+                    seen.add((int(s), int(i)))
+            assert len(seen) == int(so[-1])

@@ -38,7 +38,7 @@ def run(S, n, hd, bn, gpws=(0,), reps=20):
         am = torch.empty(B, bn, device=dev, dtype=torch.int32)
         call = lambda: N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2c), N.ptr(b2),
                                                 N.ptr(sc.scene_off), N.ptr(chunks), nchunks, max_rows, g, B, bn,
-                                                sc.max_n, N.ptr(out), N.ptr(am), N.stream_ptr()), "pool")
+                                                sc.max_n, N.ptr(out), N.ptr(am), None, N.stream_ptr()), "pool")
         for _ in range(3):
             call()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

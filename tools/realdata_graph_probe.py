@@ -1,0 +1,52 @@
+"""Graph-replayed real-data training (BucketedGraphTrainer) alone, for a
+rocprofv3 kernel trace: one untimed epoch pass (bucket captures), then
+`iters` timed iterations over zara1 train, per-bucket iteration counts.
+usage: python tools/realdata_graph_probe.py [iters] [gran] [pad_scenes] [np_caps]"""
+import collections
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "group-gan-gcn-gat_amd")]
+import bench  # noqa: E402
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+    gran = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    pad = int(sys.argv[3]) if len(sys.argv) > 3 else 32
+    caps = tuple(int(x) for x in sys.argv[4].split(",")) if len(sys.argv) > 4 else (48, 64)
+    dev = torch.device("cuda", 0)
+    from sgan.data.device import DeviceLoader, DeviceTrajectoryDataset
+    from sgan.data.trajectories_GCN import TrajectoryDataset
+    from sgan.train_step import BucketedGraphTrainer, DataParallel, GanTrainer
+    dd = DeviceTrajectoryDataset(TrajectoryDataset(os.path.join(ROOT, "tests", "golden", "datasets_group", "zara1",
+                                                                "train")), dev)
+    g, d = bench.build_models(0)
+    tr = GanTrainer(g.to(dev), d.to(dev), dp=DataParallel(), capturable=True)
+    bt = BucketedGraphTrainer(tr, dd, batch_size=64, pad_scenes=pad, gran=gran, np_caps=caps)
+
+    def batches():
+        while True:
+            yield from DeviceLoader(dd, batch_size=64, shuffle=True).scene_batches()
+    it = batches()
+    for _ in range(len(dd) // 64 + 1):
+        bt.step(next(it), next(it))
+    torch.cuda.synchronize()
+    used = collections.Counter()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        sd, sg = next(it), next(it)
+        used[bt.bucket_of(dd.layout(sd)[0], dd.layout(sg)[0])] += 1
+        bt.step(sd, sg)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print("gran %d pad %d caps %s: %.3f ms / iteration, %.0f D-step scenes/s; buckets used %s"
+          % (gran, pad, caps, dt / iters * 1e3, 64 * iters / dt, dict(used)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
