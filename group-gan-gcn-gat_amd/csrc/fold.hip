@@ -65,11 +65,11 @@ __global__ void __launch_bounds__(512) fold_fwd_multi_kernel(FoldList L) {
 // of its column in registers), and its three column sums walk the group's
 // rows with the W loads all independent (many in flight); the groups are
 // summed in LDS in a fixed order.
-__global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__ W, int ldw, int R, int E,
-                                                       const float* __restrict__ We, const float* __restrict__ be,
-                                                       const float* __restrict__ dA, const float* __restrict__ dbias,
-                                                       float* __restrict__ dW, int lddw, float* __restrict__ dWe,
-                                                       float* __restrict__ dbe, float* __restrict__ dbias_copy) {
+__device__ __forceinline__ void fold_bwd_body(const float* __restrict__ W, int ldw, int R, int E,
+                                              const float* __restrict__ We, const float* __restrict__ be,
+                                              const float* __restrict__ dA, const float* __restrict__ dbias,
+                                              float* __restrict__ dW, int lddw, float* __restrict__ dWe,
+                                              float* __restrict__ dbe, float* __restrict__ dbias_copy) {
   __shared__ float g3[3 * 512];        // (dA_x, dA_y, dbias) per row, R <= 512
   __shared__ float part[3 * 512];      // per (group, column) sums
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
@@ -109,6 +109,31 @@ __global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__
     if (j < 2) dWe[2 * e + j] = s;
     else dbe[e] = s;
   }
+}
+
+__global__ void __launch_bounds__(512) fold_bwd_kernel(const float* __restrict__ W, int ldw, int R, int E,
+                                                       const float* __restrict__ We, const float* __restrict__ be,
+                                                       const float* __restrict__ dA, const float* __restrict__ dbias,
+                                                       float* __restrict__ dW, int lddw, float* __restrict__ dWe,
+                                                       float* __restrict__ dbe, float* __restrict__ dbias_copy) {
+  fold_bwd_body(W, ldw, R, E, We, be, dA, dbias, dW, lddw, dWe, dbe, dbias_copy);
+}
+
+// every fold backward of a grad finish in one launch: workgroup k runs fold k
+// on its summed (dA, dbias) (dA_src / db_src point at the sums)
+struct FoldBwdList {
+  SggFoldBwd f[SGG_FOLDB_MAX];
+};
+
+__global__ void __launch_bounds__(512) fold_bwd_multi_kernel(FoldBwdList L) {
+  const SggFoldBwd& d = L.f[blockIdx.x];
+  fold_bwd_body(d.W, d.ldw, d.R, d.E, d.We, d.be, d.dA_src, d.db_src, d.dW, d.lddw, d.dWe, d.dbe, d.dbias_copy);
+}
+
+void fold_bwd_multi(const SggFoldBwd* folds, int n, hipStream_t st) {
+  FoldBwdList L;
+  for (int k = 0; k < n; ++k) L.f[k] = folds[k];
+  hipLaunchKernelGGL(fold_bwd_multi_kernel, dim3(n), dim3(512), 0, st, L);
 }
 
 }  // namespace sgg

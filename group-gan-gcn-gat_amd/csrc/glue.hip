@@ -161,19 +161,18 @@ __global__ void __launch_bounds__(512) l2_select_kernel(const float* __restrict_
 // terms in scene order (lane-strided partials, a fixed shuffle tree).  A
 // scene without a masked step (only the padding scenes of a fixed-capacity
 // batch, PaddedScenes: real scenes always have one) adds 0 instead of 0 / 0.
-__global__ void __launch_bounds__(64) l2_terms_kernel(const float* __restrict__ pred, int ldp,
-                                                      const float* __restrict__ gt, const float* __restrict__ mask,
-                                                      int ldm, const int32_t* __restrict__ scene_off, int T, int B,
-                                                      float w, float* __restrict__ msum_out,
-                                                      float* __restrict__ term) {
-  __shared__ float msk[kL2MaxElems];
-  const int lane = threadIdx.x, s = blockIdx.x;
-  const float2* g2 = reinterpret_cast<const float2*>(gt);
-  const int o = scene_off[s], n = scene_off[s + 1] - o;
+// one wave: the (masked squared error, mask) sums of scene [o, o + n); msk is
+// the wave's own LDS staging buffer (kL2MaxElems)
+__device__ __forceinline__ void l2_scene(const float* __restrict__ pred, int ldp, const float2* __restrict__ g2,
+                                         const float* __restrict__ mask, int ldm, int o, int n, int T, int B,
+                                         float* msk, int lane, float& acc_out, float& ms_out) {
   const int tot = n * T;
   const bool staged = tot <= kL2MaxElems;   // uniform
   if (staged) stage_mask(msk, mask, ldm, o, n, T, lane, 64);
-  __syncthreads();   // lanes read entries other lanes wrote (one wave: costs nothing)
+  // lanes read entries other lanes wrote: a wavefront-scope release / acquire
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   float acc = 0.f, ms = 0.f;
   for (int e0 = lane; e0 < tot; e0 += 256) {
     float mk[4];
@@ -194,8 +193,23 @@ __global__ void __launch_bounds__(64) l2_terms_kernel(const float* __restrict__ 
         ms += mk[u];
       }
   }
-  acc = wave_sum(acc);
-  ms = wave_sum(ms);
+  acc_out = wave_sum(acc);
+  ms_out = wave_sum(ms);
+  // the staging buffer is rewritten by the wave's next scene: every lane's
+  // reads of it are done (wave_sum consumed them) before the next stores
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ void __launch_bounds__(64) l2_terms_kernel(const float* __restrict__ pred, int ldp,
+                                                      const float* __restrict__ gt, const float* __restrict__ mask,
+                                                      int ldm, const int32_t* __restrict__ scene_off, int T, int B,
+                                                      float w, float* __restrict__ msum_out,
+                                                      float* __restrict__ term) {
+  __shared__ float msk[kL2MaxElems];
+  const int lane = threadIdx.x, s = blockIdx.x;
+  const int o = scene_off[s], n = scene_off[s + 1] - o;
+  float acc, ms;
+  l2_scene(pred, ldp, reinterpret_cast<const float2*>(gt), mask, ldm, o, n, T, B, msk, lane, acc, ms);
   if (lane == 0) {
     msum_out[s] = ms;
     term[s] = ms > 0.f ? (w * acc) / ms : 0.f;
@@ -280,9 +294,11 @@ extern "C" int sgg_l2_loss_fwd(const float* pred, int ldp, const float* gt, cons
                                float* term_ws, void* stream) {
   SGG_CHECK_ARG(pred && gt && mask && scene_off && loss && msum && term_ws, "sgg_l2_loss_fwd: null pointer");
   SGG_CHECK_ARG(S >= 0 && T >= 1 && B >= 0 && ldm >= T && ldp >= 2 * B, "sgg_l2_loss_fwd: bad sizes");
+  // (one workgroup looping over the scenes in a single launch measured slower:
+  // its per-scene load latencies add up, ~50 us at 64 scenes vs ~10 us here)
   if (S > 0)
     hipLaunchKernelGGL(l2_terms_kernel, dim3(S), dim3(64), 0, (hipStream_t)stream, pred, ldp, gt, mask, ldm, scene_off,
-                       T, B, w, msum, term_ws);
+                     T, B, w, msum, term_ws);
   hipLaunchKernelGGL(l2_sum_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, term_ws, S, loss);
   SGG_RETURN_LAUNCH("sgg_l2_loss_fwd");
 }

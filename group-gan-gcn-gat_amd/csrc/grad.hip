@@ -1,7 +1,11 @@
-// Weight-gradient finish of one backward op in ONE launch (sgg_grad_finish,
-// include/sgg.h): the slab row sums (SggRed) and the input-embedding fold
-// backwards (SggFoldBwd) of the pooling backward (reference sgan/models.py:
-// 497-549) and of the LSTM backward (:62-92, :142-178).
+// Weight-gradient finish of a backward pass in TWO launches (sgg_grad_finish,
+// include/sgg.h): the slab row sums (SggRed) of every backward op -- the
+// pooling backward (reference sgan/models.py:497-549), the LSTM backward
+// (:62-92, :142-178), the discriminator head, the GAT encoder / GCN module
+// slabs -- then the input-embedding fold backwards (SggFoldBwd) of all of
+// them, one workgroup each.  (sgan.kernels defers the ops' finishes to the
+// end of the backward pass inside the training step and issues them here
+// together.)
 //
 // Before, the row sums took a sgg_slab_reduce and sgg_xtw's reduce pass per
 // op, launches of a few microseconds of work each behind the fixed per-
@@ -133,13 +137,16 @@ extern "C" int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* f
   a.blk0[nj] = blk;
   hipStream_t st = (hipStream_t)stream;
   if (blk > 0) hipLaunchKernelGGL(grad_finish_kernel, dim3(blk), dim3(1024), 0, st, a);
-  g = scratch;
-  for (int k = 0; k < nfold; ++k) {   // the fold backwards on the summed (dA, dbias)
-    const SggFoldBwd& d = folds[k];
-    const int rc = sgg_fold_bwd(d.W, d.ldw, d.R, d.E, d.We, d.be, g, g + 2 * d.R, d.dW, d.lddw, d.dWe, d.dbe,
-                                d.dbias_copy, stream);
-    if (rc != 0) return rc;
-    g += 3 * (size_t)d.R;
+  if (nfold > 0) {   // the fold backwards on the summed (dA, dbias), one workgroup each
+    SggFoldBwd f[SGG_FOLDB_MAX];
+    g = scratch;
+    for (int k = 0; k < nfold; ++k) {
+      f[k] = folds[k];
+      f[k].dA_src = g;              // (the row-sum launch's outputs: dA, then dbias)
+      f[k].db_src = g + 2 * folds[k].R;
+      g += 3 * (size_t)folds[k].R;
+    }
+    fold_bwd_multi(f, nfold, st);
   }
   SGG_RETURN_LAUNCH("sgg_grad_finish");
 }

@@ -101,6 +101,10 @@ __attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const floa
                                                       hipStream_t st, const float* dout2 = nullptr,
                                                       int bsplit = 0, int t_stop = 0);
 
+// fold.hip: the fold backwards of one sgg_grad_finish in one launch (a
+// workgroup each; dA_src / db_src point at the summed (dA, dbias)); internal
+__attribute__((visibility("hidden"))) void fold_bwd_multi(const SggFoldBwd* folds, int n, hipStream_t st);
+
 // v if keep else +0.f, as a bit mask: a plain `keep ? v : 0` lets the
 // compiler sink the load of v into an exec-masked branch that waits for it
 // (one memory latency per load); the mask keeps every load unconditional

@@ -57,8 +57,8 @@ class Fold(ctypes.Structure):
     _fields_ = [("W", _p), ("ldw", _i), ("R", _i), ("E", _i), ("We", _p), ("be", _p), ("b1", _p), ("b2", _p),
                 ("A", _p), ("bias", _p)]
 
-RED_MAX = 8     # SGG_RED_MAX
-FOLDB_MAX = 2   # SGG_FOLDB_MAX
+RED_MAX = 24    # SGG_RED_MAX
+FOLDB_MAX = 6   # SGG_FOLDB_MAX
 
 
 class Red(ctypes.Structure):

@@ -335,25 +335,34 @@ def xtw_partial(X, Y, colsum=False):
 
 class GradFinish:
     """Collects the row-sum jobs (SggRed) and fold backwards (SggFoldBwd) of
-    one backward op, then runs them through sgg_grad_finish: one launch for
-    every row sum, one per fold.  Results are bit-identical to
-    sgg_slab_reduce / sgg_xtw / sgg_fold_bwd in turn."""
+    one backward op and runs them through sgg_grad_finish: one launch for
+    every row sum, one for the folds.  Inside defer_grad_finish() (the
+    trainer's steps) run() only queues the jobs: grad_flush() issues the
+    queued jobs of the whole backward pass together.  Results are
+    bit-identical to sgg_slab_reduce / sgg_xtw / sgg_fold_bwd in turn."""
 
     def __init__(self):
         self.reds, self.folds, self.keep = [], [], []
+
+    def _hold(self, *ts):
+        """Keep the jobs' buffers alive until the launch -- by their STORAGE:
+        a queued reference to an output tensor itself would raise its use
+        count, and autograd's AccumulateGrad would then copy the (not yet
+        written) gradient into .grad instead of taking the tensor."""
+        self.keep += [t.untyped_storage() for t in ts if t is not None]
 
     def rowsum(self, src, rows, ld, col0, cols, out):
         """out[c] = sum over src's rows of src[:, col0 + c] (out contiguous)."""
         assert out.is_contiguous() and out.numel() == cols
         self.reds.append(N.Red(N.ptr(src), rows, ld, col0, cols, N.ptr(out), 0, 0, 0, 0))
-        self.keep += [src, out]
+        self._hold(src, out)
 
     def xtw_sums(self, ws, splits, M, Nn, C, trans_c=False, colsum=None):
         """C (M x Nn, or its transpose; row-strided view) and optionally the
         column sums from xtw_partial's workspace."""
         assert C.stride(1) == 1 and tuple(C.shape) == ((Nn, M) if trans_c else (M, Nn))
         self.reds.append(N.Red(N.ptr(ws), splits, M * Nn, 0, M * Nn, N.ptr(C), 1, Nn, C.stride(0), int(trans_c)))
-        self.keep += [ws, C]
+        self._hold(ws, C)
         if colsum is not None:
             self.rowsum(ws[splits * M * Nn:], splits, Nn, 0, Nn, colsum)
 
@@ -370,29 +379,72 @@ class GradFinish:
         self.folds.append(N.FoldBwd(N.ptr(W), W.stride(0), R, E, N.ptr(We), N.ptr(be),
                                     N.ptr(dA_src), dA_rows, dA_ld, dA_col0, N.ptr(db_src), db_rows, db_ld, db_col0,
                                     N.ptr(dW), dW.stride(0), N.ptr(dWe), N.ptr(dbe), N.ptr(dbias_copy)))
-        self.keep += [W, We, be, dA_src, db_src, dW, dWe, dbe, dbias_copy]
+        self._hold(W, We, be, dA_src, db_src, dW, dWe, dbe, dbias_copy)
         return dW, dWe, dbe
 
     def run(self):
         if not self.reds and not self.folds:
             return
-        lib = _lib()
-        assert len(self.reds) <= N.RED_MAX and len(self.folds) <= N.FOLDB_MAX
-        reds = (N.Red * max(1, len(self.reds)))(*self.reds)
-        folds = (N.FoldBwd * max(1, len(self.folds)))(*self.folds)
-        nr, nf = len(self.reds), len(self.folds)
-        dev = self.keep[0].device
-        scratch = torch.empty(max(1, sum(3 * f.R for f in self.folds)), device=dev, dtype=torch.float32)
+        if _DEFER[0] > 0:
+            _PENDING.append(self)
+            return
+        _finish_launch(self.reds, self.folds, self.keep)
 
-        def launch(reds=reds, folds=folds, nr=nr, nf=nf, keep=list(self.keep)):
-            N.check(lib.sgg_grad_finish(reds, nr, folds, nf, N.ptr(scratch), scratch.numel() * 4, N.stream_ptr()),
-                    "sgg_grad_finish")
-        launch()
-        if timer.active:
-            nb = sum(4.0 * r.rows * r.cols for r in self.reds) + sum(4.0 * 3 * f.R * max(f.dA_rows, f.db_rows)
-                                                                     for f in self.folds)
-            timer.add("sgg::grad_finish_kernel", (nr, nf, tuple((r.rows, r.cols) for r in self.reds)), nb / 4.0, nb,
-                      launch)
+
+_DEFER = [0]
+_PENDING = []
+
+
+@contextlib.contextmanager
+def defer_grad_finish():
+    """Scope in which the backward ops queue their weight-gradient finishes
+    (GradFinish) instead of launching them; grad_flush() -- the trainer's,
+    before the optimizer reads the gradients -- issues all of them in two
+    launches (every row sum, every fold backward) where the ops would issue
+    two each.  Leaving the scope flushes whatever is still queued."""
+    _DEFER[0] += 1
+    try:
+        yield
+    finally:
+        _DEFER[0] -= 1
+        if _DEFER[0] == 0:
+            grad_flush()
+
+
+def grad_flush():
+    """Issue every queued GradFinish (in queue order, as few sgg_grad_finish
+    calls as the job limits allow)."""
+    while _PENDING:
+        reds, folds, keep = [], [], []
+        while _PENDING and len(reds) + len(_PENDING[0].reds) <= N.RED_MAX \
+                and len(folds) + len(_PENDING[0].folds) <= N.FOLDB_MAX:
+            gf = _PENDING.pop(0)
+            reds += gf.reds
+            folds += gf.folds
+            keep += gf.keep
+        if not reds and not folds:   # one op alone over the limits: cannot happen (each op is within them)
+            raise N.NativeError("grad_flush: a queued finish exceeds the job limits")
+        _finish_launch(reds, folds, keep)
+
+
+def _finish_launch(reds_l, folds_l, keep):
+    lib = _lib()
+    assert len(reds_l) <= N.RED_MAX and len(folds_l) <= N.FOLDB_MAX
+    reds = (N.Red * max(1, len(reds_l)))(*reds_l)
+    folds = (N.FoldBwd * max(1, len(folds_l)))(*folds_l)
+    nr, nf = len(reds_l), len(folds_l)
+    dev = keep[0].device
+    scratch = torch.empty(max(1, sum(3 * f.R for f in folds_l)), device=dev, dtype=torch.float32)
+
+    def launch(reds=reds, folds=folds, nr=nr, nf=nf, keep=list(keep)):
+        N.check(lib.sgg_grad_finish(reds, nr, folds, nf, N.ptr(scratch), scratch.numel() * 4, N.stream_ptr()),
+                "sgg_grad_finish")
+    launch()
+    if timer.active:
+        nb = sum(4.0 * r.rows * r.cols for r in reds_l) + sum(4.0 * 3 * f.R * max(f.dA_rows, f.db_rows)
+                                                               for f in folds_l)
+        timer.add("sgg::grad_finish_kernel", (nr, nf, tuple((r.rows, r.cols) for r in reds_l)), nb / 4.0, nb,
+                  launch)
 
 
 class _XW(torch.autograd.Function):
@@ -1073,9 +1125,10 @@ class _GatEnc(torch.autograd.Function):
                       4.0 * (B * (40 + 1 + 24 + 40) + scenes.S * P) + _gatenc_saved_bytes(B, nh),
                       lambda a=a, keep=keep: N.check(lib.sgg_gatenc_bwd(N.ctypes.byref(a), N.stream_ptr()),
                                                      "sgg_gatenc_bwd"))
-        with side(slab):
-            flat = torch.empty(P, device=x.device, dtype=torch.float32)
-            N.check(lib.sgg_slab_reduce(N.ptr(slab), scenes.S, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+        flat = torch.empty(P, device=x.device, dtype=torch.float32)
+        gf = GradFinish()   # the scene-ordered slab sum (sgg_slab_reduce's order), deferred in the trainer
+        gf.rowsum(slab, scenes.S, P, 0, P, flat)
+        gf.run()
         grads, o = [], 0
         for q in ps:
             grads.append(flat[o:o + q.numel()].view_as(q))
@@ -1215,9 +1268,10 @@ class _GcnMod(torch.autograd.Function):
                       4.0 * (B * (a.fin + 1 + a.fe + a.fin) + rows * P),
                       lambda a=a, keep=keep: N.check(lib.sgg_gcnmod_bwd(N.ctypes.byref(a), N.stream_ptr()),
                                                      "sgg_gcnmod_bwd"))
-        with side(slab):
-            flat = torch.empty(P, device=x.device, dtype=torch.float32)
-            N.check(lib.sgg_slab_reduce(N.ptr(slab), rows, P, N.ptr(flat), N.stream_ptr()), "sgg_slab_reduce")
+        flat = torch.empty(P, device=x.device, dtype=torch.float32)
+        gf = GradFinish()   # the workgroup-ordered slab sum (sgg_slab_reduce's order), deferred in the trainer
+        gf.rowsum(slab, rows, P, 0, P, flat)
+        gf.run()
         grads, o = [], 0
         for q in ps:
             grads.append(flat[o:o + q.numel()].view_as(q))

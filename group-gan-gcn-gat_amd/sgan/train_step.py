@@ -141,6 +141,9 @@ class KernelOps:
     # the discriminator head forms the BCE gradient in its own backward
     # (kernels.BceLink) inside the steps only
     handoff = staticmethod(K.bce_handoff)
+    # the backward ops' weight-gradient finishes queued and issued together
+    # (two launches per backward pass instead of two per op)
+    defer_finish = staticmethod(K.defer_grad_finish)
 
 
 class GanTrainer:
@@ -183,6 +186,7 @@ class GanTrainer:
     def _finish(self, params, opt, loss_terms, clip):
         """all-reduce grads (+ loss values), clip, step."""
         K.side_join()   # the weight gradients of the side stream (normally joined at the end of backward)
+        K.grad_flush()  # the backward ops' queued weight-gradient finishes (KernelOps.defer_finish)
         grads = [p.grad for p in params if p.grad is not None]
         if self.dp.on and self.dp.world > 1:   # the loss values ride along with the gradients
             vals = torch.stack([t.detach().reshape(()) for t in loss_terms])
@@ -194,7 +198,10 @@ class GanTrainer:
 
     # -- steps ---------------------------------------------------------------
     def _scope(self):
-        return getattr(self.ops, "handoff", contextlib.nullcontext)()
+        st = contextlib.ExitStack()
+        st.enter_context(getattr(self.ops, "handoff", contextlib.nullcontext)())
+        st.enter_context(getattr(self.ops, "defer_finish", contextlib.nullcontext)())
+        return st
 
     def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """discriminator_step (train.py:395-429). `batch` holds this rank's

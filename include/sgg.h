@@ -224,8 +224,9 @@ int sgg_xtw_partial(const float* X, int ldx, const float* Y, int ldy, const floa
                     int N, int colsum, float* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
- * Weight-gradient finish of one backward op (the pooling
- * backward of models.py:497-549, the LSTM backward of :62-92 / :142-178):
+ * Weight-gradient finish of the backward ops of one backward pass (the
+ * pooling backward of models.py:497-549, the LSTM backward of :62-92 /
+ * :142-178, the discriminator head, the GAT encoder / GCN module slabs):
  * every slab row sum the op needs (SggRed: the kernels' per-workgroup slab
  * rows, sgg_xtw_partial's split partials) and the input-embedding fold
  * backwards (SggFoldBwd, the algebra of sgg_fold_bwd) whose (dA, dbias) are
@@ -237,8 +238,8 @@ int sgg_xtw_partial(const float* X, int ldx, const float* Y, int ldy, const floa
  * sgg_slab_reduce does (16 row phases, then the phases in order); map 0:
  * out[c]; map 1 (sgg_xtw's C, c = m * N + n): out[m * ldo + n], or
  * out[n * ldo + m] when trans != 0. */
-#define SGG_RED_MAX 8
-#define SGG_FOLDB_MAX 2
+#define SGG_RED_MAX 24
+#define SGG_FOLDB_MAX 6
 typedef struct {
   const float* src;
   int rows;
@@ -277,7 +278,8 @@ typedef struct {
   float* dbias_copy;
 } SggFoldBwd;
 /* scratch: 3 R floats per fold job (its (dA, dbias) row sums).  Launches:
- * one for all row sums, then one sgg_fold_bwd per fold job. */
+ * one for all row sums, then (with fold jobs) one for every fold backward
+ * (a workgroup per fold, fold_bwd's algebra and order). */
 int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* folds, int nfold, float* scratch,
                     size_t scratch_bytes, void* stream);
 

@@ -858,6 +858,40 @@ def test_gcn_module_fused_equals_per_op(prec, sizes):
         close(gf[k], gr[k].cpu().numpy(), rtol=t_dw, floor=fl, what="fused d" + k)
 
 
+@pytest.mark.parametrize("graph", ["gat", "sgangat"])
+def test_deferred_grad_finish_is_bit_identical(graph):
+    """The trainer's deferred weight-gradient finish (every backward op's
+    GradFinish queued, then issued together: defer_grad_finish / grad_flush)
+    against each op finishing in its own launches: every gradient of a D-step
+    and a G-step bit-identical."""
+    import contextlib
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, KernelOps
+    sizes = [20, 7, 13, 20, 2] if graph == "gat" else [64, 30, 5]
+    batch = synthetic_batch(sizes, seed=5, device=DEV)
+    sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+
+    class Immediate(KernelOps):
+        defer_finish = staticmethod(contextlib.nullcontext)
+    res = []
+    for ops in (KernelOps(), Immediate()):
+        g, d = build_models(graph)
+        tr = GanTrainer(g, d, ops=ops)
+        torch.manual_seed(3)
+        random.seed(3)
+        grads = {}
+        tr.d_step(batch, sc)
+        grads.update({"d." + k: p.grad.detach().clone() for k, p in d.named_parameters() if p.grad is not None})
+        tr.g_step(batch, sc)
+        grads.update({"g." + k: p.grad.detach().clone() for k, p in g.named_parameters() if p.grad is not None})
+        res.append(grads)
+    a, b = res
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+
+
 def test_step_glue_kernels_match_torch():
     """glue.hip (sgg_traj_cat, sgg_decoder_init, sgg_l2_select,
     sgg_l2_loss_fwd/bwd) against the reference's torch expressions

@@ -1,0 +1,30 @@
+"""The kernels of one graph-replayed training iteration from a rocprofv3
+kernel trace (bench.py's timed replays): the launches between two
+consecutive starts of the best-of-k rollout, with durations and gaps.
+usage: python tools/ktrace_iter.py TRACE_DIR [which replay, default: the middle one]"""
+import csv
+import os
+import re
+import sys
+
+
+def short(n):
+    n = n.replace("(anonymous namespace)::", "")
+    m = re.search(r"((sgg|at::native)::[A-Za-z_0-9:]+(<[^()]{0,40})?)", n)
+    return (m.group(1) if m else n)[:58]
+
+
+rows = list(csv.DictReader(open(os.path.join(sys.argv[1], "run_kernel_trace.csv"))))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if "lstm_fwd_mfma" in r["Kernel_Name"]]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) // 2
+a, b = idx[k], idx[k + 1]
+t0 = int(rows[a]["Start_Timestamp"])
+busy, prev = 0, None
+for r in rows[a:b]:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    print("%8.1f %6.1f %6.1f  %-58s grid=%s" % ((s - t0) / 1e3, (e - s) / 1e3, (s - prev) / 1e3 if prev else 0.0,
+                                                short(r["Kernel_Name"]), r.get("Grid_Size_X") or r.get("Grid_Size")))
+    busy += e - s
+    prev = e
+print("%d kernels, %.1f us busy, %.1f us period" % (b - a, busy / 1e3, (int(rows[b]["Start_Timestamp"]) - t0) / 1e3))
