@@ -6,17 +6,17 @@
 // is latency-bound and the per-ped gate GEMM (4H x H) is spread over all four
 // SIMDs of a CU.
 //
-// Forward step, wave g = gate block g (i | f | g | o):
-//   G_g^T (H x 16 peds) = [W_hh,g | A_g b_g] . [h_{t-1} | r_x r_y 1 0]^T
-// = MU = H / 16 tiles x (H / 4 + 1) k-steps of 16x16x4 per wave.  The D
-// layout puts (unit 16 mu + 4 q + r, ped c16) in lane (q << 4 | c16),
-// register r of tile mu: "slot" j = 4 mu + r of that lane.  The wave applies
-// its gate's activation and writes slot j to LDS gate[g][j][lane]; after a
-// barrier wave w runs the cell update of slots w MU .. w MU + MU - 1 (c in
-// registers) and writes h to hb[j][lane].  The next step's B operand for
-// k-step ks is h of unit 16 (ks >> 2) + 4 q + (ks & 3) -- exactly
-// hb[ks][lane], because W_hh's columns are loaded in that permuted order.
-// Two barriers per step; every LDS access is lane-linear (conflict-free).
+// "Slot" j of lane (q, c16) is unit slot_unit(j, q) = 16 (j >> 2) + 4 q +
+// (j & 3) of ped c16; wave w owns slots w MU .. w MU + MU - 1 (MU = H / 16).
+// Forward step: wave w's tile mu holds the four gates of its slot j = w MU +
+// mu, gate-interleaved -- D row 4 q + r is (gate r, unit slot_unit(j, q)):
+//   G^T (H rows x 16 peds) = [W_hh | A b] (those rows) . [h_{t-1} | r_x r_y 1 0]^T
+// = MU tiles x (H / 4 + 1) k-steps of 16x16x4 per wave, so a lane ends the
+// MFMAs holding i, f, g, o of its own slots: activations and the cell update
+// run in registers (c too) and h goes to hb[t & 1][j][lane].  The next step's
+// B operand for k-step ks is h of unit slot_unit(ks, q) -- exactly
+// hb[.][ks][lane], because W_hh's columns are loaded in that permuted order.
+// ONE barrier per step (hb double-buffered); every LDS access is lane-linear.
 // Decoder: the hidden2pos feedback r_t = Wp h_t + bp into step t+1 is folded
 // into the weights before step 1 (W_hh + A Wp, b' + A bp; lstm_unit.hip), so
 // r_t is off the critical path: wave partials in LDS, summed by wave 0 after
@@ -30,25 +30,25 @@
 // the recurrence.  h_all stays in the public (T+1) x B x H layout (it is the
 // encoder's output).
 //
-// Backward step t (reverse): the slot owners turn dh_t (four gate-block
-// partials of W^T dG_{t+1} from LDS, + Wp^T dout_t for the decoder) into dG_t
-// with the saved activations (loaded a step ahead), writing dG_t to LDS
-// dgb[t & 1][g][j][lane]; after a barrier wave g computes its gate block's
-// share of dh_{t-1}:
-//   P_g (H x 16) = W_hh,g^T (H x H) . dG_g^T       (MU tiles x H / 4 k-steps)
-// written to LDS for the next step's owners; second barrier.  The decoder
-// uses the folded W' for t >= 1 (its input r_{t-1} depends on h_{t-1}) and
-// plain W_hh at t = 0 (dh0).  drel_in = A^T dG_t is a slot partial reduced
-// over the q lanes and the waves off the critical path.
+// Backward step t (reverse): the slot owners turn dh_t (four wave partials of
+// W^T dG_{t+1} from LDS, + Wp^T dout_t for the decoder) into dG_t with the
+// saved activations (loaded a step ahead), and straight from registers run
+// their slots' share of dh_{t-1}:
+//   P_w (H x 16) = sum over the wave's slots j and gates r of
+//                  W_hh[r H + slot_unit(j, q)]^T . dG_r,j     (MU tiles x 4 MU k-steps)
+// -- k-step (j, r) takes lane quarter q's own dG value of gate r -- written
+// to LDS part[t & 1] for the next step's owners: ONE barrier per step.  The
+// decoder uses the folded W' for t >= 1 (its input r_{t-1} depends on
+// h_{t-1}) and plain W_hh at t = 0 (dh0).  drel_in = A^T dG_t is a slot
+// partial reduced over the q lanes and the waves off the critical path.
 //
 // Weight gradients in the kernel (wpart != NULL): wave g accumulates, on the
 // MFMA, its gate block's
 //   dW_hh,g += dG_g^T (H x 16 peds) . h_{t-1}
-// (MU x MU tiles, K = the block's 16 peds = 4 k-steps), the A operand read
-// straight from the double-buffered dG image in LDS, h_{t-1} staged from
-// h_all one step ahead.  The MFMAs of step t + 1 are issued at the top of
-// step t, ahead of that step's VALU work, so the matrix core runs them in the
-// shadow of the cell-gradient arithmetic.  The slot owners sum db += dG and
+// (MU x MU tiles, K = the block's 16 peds = 4 k-steps) in four helper waves,
+// the A operand read from the double-buffered dG image the owners leave in
+// LDS, h_{t-1} staged from h_all one step ahead; the helpers pass the owners'
+// one barrier per step, so they run beside the next step's owners.  The slot owners sum db += dG and
 // dA += dG r_in^T on the VALU (3 FMA per gate value; reduced over the 16 peds
 // by lane shuffles at the end).  dG never reaches HBM: the workgroup writes
 // one slab row [dW_hh (4H x H) | db (4H) | dA (4H x 2)] that sgg_slab_reduce
@@ -107,9 +107,8 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     const float* __restrict__ Wu, int ldwu, const float* __restrict__ cu, int NU, float* __restrict__ U) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS;
   constexpr bool decoder = DEC, save = SAVE;
-  __shared__ float gate[4][KS][64];
-  __shared__ float hb[KS][64];
-  __shared__ float2 rpart[4][kMwPeds];
+  __shared__ float hb[2][KS][64];
+  __shared__ float2 rpart[2][4][kMwPeds];
   __shared__ float relseq[kMwMaxT][kMwPeds][2];
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -118,12 +117,14 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
   const int ped = blk * kMwPeds + c16;
   const int pc = ped < B ? ped : B - 1;   // clamped: every load and store unconditional and in bounds
 
-  // [W_hh,g | A_g b_g] in registers, W_hh's columns in the permuted k order
-  // (slot_unit(4 m + i, q) = 16 m + 4 q + i: one 16-byte load per block m)
+  // [W_hh | A b] rows of tile mu in registers: A-operand row c16 is gate
+  // c16 & 3 of unit slot_unit(g MU + mu, c16 >> 2); W_hh's columns in the
+  // permuted k order (slot_unit(4 m + i, q) = 16 m + 4 q + i: one 16-byte load
+  // per block m)
   float w[MU][KS + 1], ak0[MU], ak1[MU];
 #pragma unroll
   for (int mu = 0; mu < MU; ++mu) {
-    const int row = g * H + 16 * mu + c16;
+    const int row = (c16 & 3) * H + slot_unit(g * MU + mu, c16 >> 2);
 #pragma unroll
     for (int m = 0; m < KS / 4; ++m) {
       const float4 v = *reinterpret_cast<const float4*>(Whh + row * H + 16 * m + 4 * q);
@@ -142,7 +143,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     const int j = g * MU + i, u = slot_unit(j, q);
     const float hv = h0 ? h0[(size_t)pc * H + u] : 0.f;
     c[i] = c0 ? c0[(size_t)pc * H + u] : 0.f;
-    hb[j][lane] = hv;
+    hb[0][j][lane] = hv;
     if (save) {
       h_all[(size_t)pc * H + u] = hv;
       c_tile[((size_t)blk * (T + 1) * KS + j) * 64 + lane] = c[i];
@@ -166,8 +167,6 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     return q < 2 ? v : (q == 2 ? 1.f : 0.f);
   };
   float xin = input(0);
-  const float s = g == 2 ? 2.f : 1.f;   // g: tanh, i f o: sigmoid
-  const float nsl = s * kNegLog2e;
 
   for (int t = 0; t < T; ++t) {
     if (decoder && t == 1) {
@@ -184,55 +183,56 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
         if (q == 2) w[mu][KS] = fmaf(ak1[mu], bp1, fmaf(ak0[mu], bp0, w[mu][KS]));
       xin = q == 2 ? 1.f : 0.f;
     }
+    const int rb = t & 1;   // h_{t-1} is in hb[rb]; h_t goes to hb[rb ^ 1]
     floatx4 acc[MU];
 #pragma unroll
     for (int mu = 0; mu < MU; ++mu)
       acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][KS], xin, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     float hk[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[ks][lane];
+    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[rb][ks][lane];
     if (!decoder && t + 1 < T) xin = input(t + 1);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][ks], hk[ks], acc[mu], 0, 0, 0);
 
-    float* at = save ? act_tile + (((size_t)blk * T + t) * 4 + g) * KS * 64 + lane : nullptr;
-#pragma unroll
-    for (int mu = 0; mu < MU; ++mu) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float a = gate_act(acc[mu][r], s, nsl);
-        gate[g][4 * mu + r][lane] = a;
-        if (save) at[(4 * mu + r) * 64] = a;   // lane-linear 256-byte line per slot
-      }
-    }
-    lds_barrier();
-
-    // cell update of this wave's slots
+    // activations (r = 2: tanh, else sigmoid) and the cell update of this
+    // wave's slots, in registers
     float px = 0.f, py = 0.f;
 #pragma unroll
-    for (int i = 0; i < MU; ++i) {
-      const int j = g * MU + i;
-      const float ig = gate[0][j][lane], fg = gate[1][j][lane], gg = gate[2][j][lane], og = gate[3][j][lane];
-      c[i] = fmaf(fg, c[i], ig * gg);
-      const float h = og * tanh_m(c[i]);
-      hb[j][lane] = h;
+    for (int mu = 0; mu < MU; ++mu) {
+      const int j = g * MU + mu;
+      float a[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = r == 2 ? 2.f : 1.f;
+        a[r] = gate_act(acc[mu][r], s, s * kNegLog2e);
+      }
+      if (save) {   // tile-native: gate r, slot j, one lane-linear 256-byte line each
+        float* at = act_tile + (((size_t)blk * T + t) * 4 * KS + j) * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) at[r * KS * 64] = a[r];
+      }
+      c[mu] = fmaf(a[1], c[mu], a[0] * a[2]);
+      const float h = a[3] * tanh_m(c[mu]);
+      hb[rb ^ 1][j][lane] = h;
       if (save || t == T - 1) h_all[((size_t)(save ? t + 1 : T) * B + pc) * H + slot_unit(j, q)] = h;
-      if (save) c_tile[(((size_t)blk * (T + 1) + t + 1) * KS + j) * 64 + lane] = c[i];
-      px = fmaf(wp0[i], h, px);
-      py = fmaf(wp1[i], h, py);
+      if (save) c_tile[(((size_t)blk * (T + 1) + t + 1) * KS + j) * 64 + lane] = c[mu];
+      px = fmaf(wp0[mu], h, px);
+      py = fmaf(wp1[mu], h, py);
     }
     if (decoder) {
       px += __shfl_xor(px, 16);
       px += __shfl_xor(px, 32);
       py += __shfl_xor(py, 16);
       py += __shfl_xor(py, 32);
-      if (q == 0) rpart[g][c16] = make_float2(px, py);
+      if (q == 0) rpart[t & 1][g][c16] = make_float2(px, py);
     }
     lds_barrier();
     if (decoder && g == 0 && q == 0) {   // r_t = Wp h_t + bp
-      const float2 r0 = rpart[0][c16], r1 = rpart[1][c16], r2 = rpart[2][c16], r3 = rpart[3][c16];
+      const float2 r0 = rpart[t & 1][0][c16], r1 = rpart[t & 1][1][c16], r2 = rpart[t & 1][2][c16],
+                   r3 = rpart[t & 1][3][c16];
       *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + pc) * 2) =
           make_float2(((r0.x + r1.x) + (r2.x + r3.x)) + bp0, ((r0.y + r1.y) + (r2.y + r3.y)) + bp1);
     }
@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     // takes tiles g, g + 4, ...
     float hk[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[ks][lane];
+    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[T & 1][ks][lane];
     const int ntile = NU >> 4;
     // tiles in pairs (two independent accumulation chains); the next pair's
     // Wu fragments are in flight during the current pair's MFMAs
@@ -316,8 +316,8 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   // decoder slab rows carry [dWp (2 x H) | dbp (2)] after [dW_hh | db | dA]
   constexpr int NHS = MwCfg<H>::NHS, P0 = MwCfg<H>::P, P = P0 + (DEC ? 2 * H + 2 : 0);
   __shared__ float dgb[2][4][KS][kDgPitch];
-  __shared__ float part[4][KS][64];
-  __shared__ float2 fbp[4][kMwPeds];
+  __shared__ float part[2][4][KS][64];
+  __shared__ float2 fbp[2][4][kMwPeds];
   __shared__ float hs[2][kMwPeds][HP];
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -347,10 +347,12 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   };
   if (wgrad && g >= 4) {
     // helper waves 4..7: the weight gradient of gate block hg, off the
-    // recurrence's critical path.  They pass the same two barriers per step:
-    // after barrier A(t) dG_t is in dgb[t & 1] and h_{t-1} in hs[t & 1]; the
-    // MFMAs run while the owners compute dh_{t-1}, then h_{t-2} is staged into
-    // the other buffer (its last reader, step t + 1, finished before B(t + 1)).
+    // recurrence's critical path.  They pass the owners' barrier of each step:
+    // after barrier (t) dG_t is in dgb[t & 1] and h_{t-1} in hs[t & 1]; the
+    // MFMAs run while the owners compute step t - 1, then h_{t-2} is staged
+    // into the other buffer (its last readers, step t + 1, all passed barrier
+    // (t)).  dgb[t & 1] is rewritten at step t - 2, after barrier (t - 1),
+    // which a helper reaches only once its step-t MFMAs are issued.
     const int hg = g - 4;
     floatx4 dw[MU][MU];
 #pragma unroll
@@ -379,13 +381,12 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     if (T >= 2) stage_load(T - 2);
     for (int t = T - 1; t >= 0; --t) {
       const int cur = t & 1;
-      lds_barrier();   // A(t)
+      lds_barrier();   // (t)
       dw_accum(cur);
       if (t > 0) {
         stage_store(cur ^ 1);
         if (t > 1) stage_load(t - 2);
       }
-      lds_barrier();   // B(t)
     }
     // slab row of this workgroup: D tile (mu, nu) holds rows hg H + 16 mu + 4 q + r, cols 16 nu + c16
     float* row = wpart + (size_t)blk * P;
@@ -400,21 +401,27 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     return;
   }
 
-  // W_hh,g^T in registers: wt[mu][ks] = W_hh[g H + slot_unit(ks, q)][16 mu + c16]
-  // (decoder: the folded W' = W_hh + A Wp for t >= 1, plain W_hh kept for t = 0)
-  float wt[MU][KS], wt0[MU][KS];
+  // the wave's rows of W_hh^T in registers, k-step (i, r) = gate r of slot
+  // g MU + i: wt[mu][i][r] = W_hh[r H + slot_unit(g MU + i, q)][16 mu + c16]
+  // (decoder: the folded W' = W_hh + A Wp for t >= 1, plain W_hh for t = 0 --
+  // kept in registers for H <= 32, reloaded at t = 0 above that, where a
+  // second copy would spill)
+  constexpr bool wt0_reg = MU <= 2;
+  float wt[MU][MU][4], wt0[MU][MU][4];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int row = g * H + slot_unit(ks, q);
-    const float a0 = decoder ? A[2 * row] : 0.f, a1 = decoder ? A[2 * row + 1] : 0.f;
+  for (int i = 0; i < MU; ++i)
 #pragma unroll
-    for (int mu = 0; mu < MU; ++mu) {
-      const int col = 16 * mu + c16;
-      const float v = Whh[row * H + col];
-      wt0[mu][ks] = v;
-      wt[mu][ks] = decoder ? fmaf(a1, Wp[H + col], fmaf(a0, Wp[col], v)) : v;
+    for (int r = 0; r < 4; ++r) {
+      const int row = r * H + slot_unit(g * MU + i, q);
+      const float a0 = decoder ? A[2 * row] : 0.f, a1 = decoder ? A[2 * row + 1] : 0.f;
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu) {
+        const int col = 16 * mu + c16;
+        const float v = Whh[row * H + col];
+        wt0[mu][i][r] = v;
+        wt[mu][i][r] = decoder ? fmaf(a1, Wp[H + col], fmaf(a0, Wp[col], v)) : v;
+      }
     }
-  }
   // per owned slot: rows of A for the four gates (A^T dG), Wp columns, dc
   float aa0[MU][4], aa1[MU][4], wp0[MU], wp1[MU], dc[MU], dh[MU];
 #pragma unroll
@@ -505,11 +512,24 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       dbp0 += rtx;
       dbp1 += rty;
     }
+    if (decoder && t == 0) {
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+        for (int i = 0; i < MU; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            wt[mu][i][r] = wt0_reg ? wt0[mu][i][r] : Whh[(r * H + slot_unit(g * MU + i, q)) * H + 16 * mu + c16];
+    }
+    floatx4 acc[MU];
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu) acc[mu] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
       const int j = g * MU + i;
       float dhv = dh[i];
-      if (t < T - 1) dhv = (part[0][j][lane] + part[1][j][lane]) + (part[2][j][lane] + part[3][j][lane]);
+      if (t < T - 1)
+        dhv = (part[cur ^ 1][0][j][lane] + part[cur ^ 1][1][j][lane]) + (part[cur ^ 1][2][j][lane] + part[cur ^ 1][3][j][lane]);
       if (decoder) dhv = fmaf(wp0[i], d0, fmaf(wp1[i], d1, dhv));
       const float ig = ci[i], fg = cf[i], gg = cg[i], og = co[i];
       const float tc = tanh_m(cc[i]);
@@ -523,52 +543,38 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       dc[i] = dct * fg;
       // a padded ped (last block) carries no gradient: its dG is zero, so it
       // adds nothing to the weight gradients
-      const float vi = keep_if(dct * gg * ig * (1.f - ig), valid);
-      const float vf = keep_if(dct * ccp[i] * fg * (1.f - fg), valid);
-      const float vg = keep_if(dct * ig * (1.f - gg * gg), valid);
-      const float vo = keep_if(d_o * og * (1.f - og), valid);
-      dgb[cur][0][j][lane] = vi;
-      dgb[cur][1][j][lane] = vf;
-      dgb[cur][2][j][lane] = vg;
-      dgb[cur][3][j][lane] = vo;
+      const float vv[4] = {keep_if(dct * gg * ig * (1.f - ig), valid), keep_if(dct * ccp[i] * fg * (1.f - fg), valid),
+                           keep_if(dct * ig * (1.f - gg * gg), valid), keep_if(d_o * og * (1.f - og), valid)};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[mu][i][r], vv[r], acc[mu], 0, 0, 0);
       if (wgrad) {
-        const float vv[4] = {vi, vf, vg, vo};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          dgb[cur][k][j][lane] = vv[k];
           db[i][k] += vv[k];
           dax[i][k] = fmaf(vv[k], r0, dax[i][k]);
           day[i][k] = fmaf(vv[k], r1, day[i][k]);
         }
       }
-      f0 = fmaf(aa0[i][3], vo, fmaf(aa0[i][2], vg, fmaf(aa0[i][1], vf, fmaf(aa0[i][0], vi, f0))));
-      f1 = fmaf(aa1[i][3], vo, fmaf(aa1[i][2], vg, fmaf(aa1[i][1], vf, fmaf(aa1[i][0], vi, f1))));
+      f0 = fmaf(aa0[i][3], vv[3], fmaf(aa0[i][2], vv[2], fmaf(aa0[i][1], vv[1], fmaf(aa0[i][0], vv[0], f0))));
+      f1 = fmaf(aa1[i][3], vv[3], fmaf(aa1[i][2], vv[2], fmaf(aa1[i][1], vv[1], fmaf(aa1[i][0], vv[0], f1))));
     }
     f0 += __shfl_xor(f0, 16);
     f0 += __shfl_xor(f0, 32);
     f1 += __shfl_xor(f1, 16);
     f1 += __shfl_xor(f1, 32);
-    if (q == 0) fbp[g][c16] = make_float2(f0, f1);
+    if (q == 0) fbp[cur][g][c16] = make_float2(f0, f1);
+    // this wave's share of dh_{t-1}: D row 4 q + r of tile mu is unit
+    // slot_unit(4 mu + r, q), i.e. slot 4 mu + r of the next step's owners
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[cur][g][4 * mu + r][lane] = acc[mu][r];
     lds_barrier();
-
-    // gate block g of dG_t: its share of dh_{t-1}
-    float bk[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) bk[ks] = dgb[cur][g][ks][lane];
-    if (decoder && t == 0) {
-#pragma unroll
-      for (int mu = 0; mu < MU; ++mu)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) wt[mu][ks] = wt0[mu][ks];
-    }
-    floatx4 acc[MU];
-#pragma unroll
-    for (int mu = 0; mu < MU; ++mu) acc[mu] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[mu][ks], bk[ks], acc[mu], 0, 0, 0);
     if (pgrad || (g == 0 && q == 0)) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
-      const float2 r0 = fbp[0][c16], r1 = fbp[1][c16], r2 = fbp[2][c16], r3 = fbp[3][c16];
+      const float2 r0 = fbp[cur][0][c16], r1 = fbp[cur][1][c16], r2 = fbp[cur][2][c16], r3 = fbp[cur][3][c16];
       const float sx = (r0.x + r1.x) + (r2.x + r3.x), sy = (r0.y + r1.y) + (r2.y + r3.y);
       if (valid && g == 0 && q == 0) {
         *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(sx, sy);
@@ -577,11 +583,6 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       din_x = sx;
       din_y = sy;
     }
-#pragma unroll
-    for (int mu = 0; mu < MU; ++mu)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) part[g][4 * mu + r][lane] = acc[mu][r];
-    lds_barrier();
   }
   if (t_stop > 0 && valid && g == 0 && q == 0) {   // the skipped steps' input gradients are defined as zero
     for (int t = 0; t < t_stop; ++t) *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(0.f, 0.f);
@@ -590,7 +591,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
       const int j = g * MU + i;
-      dh0[(size_t)ped * H + slot_unit(j, q)] = (part[0][j][lane] + part[1][j][lane]) + (part[2][j][lane] + part[3][j][lane]);
+      dh0[(size_t)ped * H + slot_unit(j, q)] = (part[0][0][j][lane] + part[0][1][j][lane]) + (part[0][2][j][lane] + part[0][3][j][lane]);
     }
   }
   if (wgrad) {
@@ -718,6 +719,8 @@ int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* 
                 const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
                 int T, int B, int H, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart,
                 hipStream_t st, const float* dout2, int bsplit, int t_stop) {
+  // the helper waves pass one barrier per step of ALL T steps
+  SGG_CHECK_ARG(!wpart || t_stop == 0, "sgg_lstm_bwd: weight gradients need every step (t_stop=%d)", t_stop);
   switch (H) {
     case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
     case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
