@@ -333,6 +333,34 @@ extern "C" int sgg_lstm_bwd_tail(const float* A, const float* Whh, const float* 
                      drel_in, nullptr, nullptr, (hipStream_t)stream, nullptr, 0, t_stop);
 }
 
+static MwSeg to_mw(const SggLstmSeg& s) {
+  return MwSeg{s.rel, s.A, s.Whh, s.bias, s.h0, s.c0, nullptr, nullptr, s.T, s.B, s.Bl, s.t0, s.Tl, s.Bsrc,
+               s.h_all, s.c_all, s.act_all, nullptr, s.Wu, s.ldwu, s.cu, s.NU, s.U};
+}
+
+extern "C" int sgg_lstm_fwd_seg(const SggLstmSeg* seg, int H, void* stream) {
+  SGG_CHECK_ARG(seg, "sgg_lstm_fwd_seg: null segment");
+  SGG_CHECK_ARG(lstm_mw_ok(H, seg->B), "sgg_lstm_fwd_seg: no four-wave kernel for H=%d", H);
+  return lstm_mw_fwd_seg(to_mw(*seg), H, (hipStream_t)stream);
+}
+
+extern "C" int sgg_lstm_fwd_seg2(const SggLstmSeg* a, int Ha, const SggLstmSeg* b, int Hb, void* stream) {
+  SGG_CHECK_ARG(a && b, "sgg_lstm_fwd_seg2: null segment");
+  SGG_CHECK_ARG(lstm_mw_ok(Ha, a->B) && lstm_mw_ok(Hb, b->B), "sgg_lstm_fwd_seg2: no four-wave kernel (Ha=%d Hb=%d)",
+                Ha, Hb);
+  return lstm_mw_fwd_seg2(to_mw(*a), Ha, to_mw(*b), Hb, (hipStream_t)stream);
+}
+
+extern "C" int sgg_lstm_bwd_shared(const float* A, const float* Whh, const float* h_all, const float* c_all,
+                                   const float* act_all, const float* rel, const float* dh_last, int T, int B, int H,
+                                   int t_sh, int Bsrc, float* drel_in, float* wpart, void* stream) {
+  SGG_CHECK_ARG(A && Whh && h_all && c_all && act_all && rel && drel_in, "sgg_lstm_bwd_shared: null pointer");
+  SGG_CHECK_ARG(T >= 1 && B >= 1 && t_sh >= 1 && lstm_mw_ok(H, B),
+                "sgg_lstm_bwd_shared: bad sizes or no four-wave kernel (T=%d B=%d H=%d t_sh=%d)", T, B, H, t_sh);
+  return lstm_mw_bwd(A, Whh, nullptr, h_all, c_all, act_all, rel, nullptr, dh_last, nullptr, T, B, H, 0, nullptr,
+                     drel_in, nullptr, wpart, (hipStream_t)stream, nullptr, 0, 0, t_sh, Bsrc);
+}
+
 extern "C" int sgg_lstm_wpart_rows(int H, int B) {
   if (B < 0) return -1;
   return lstm_mw_ok(H, B) ? lstm_mw_wpart_rows(H, B) : 0;

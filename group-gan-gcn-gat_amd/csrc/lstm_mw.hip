@@ -23,12 +23,13 @@
 // the step's second barrier.
 //
 // Saved states for the backward are TILE-NATIVE (this family's private
-// layout, sized by sgg_lstm_state_floats): the gate activations of block b,
-// step t, gate g, slot j are the 64 floats act[((b T + t) 4 + g) KS + j][lane]
-// and the cells c[(b (T+1) + t) KS + j][lane] -- each a 256-byte line written
-// and read by one lane-linear instruction, i.e. exactly the LDS images of
-// the recurrence.  h_all stays in the public (T+1) x B x H layout (it is the
-// encoder's output).
+// layout, sized by sgg_lstm_state_floats): the four gate activations of
+// block b, step t, slot j are one float4 per lane, act[(b T + t) KS + j][lane],
+// and the cells of wave g's MU slots MU consecutive floats per lane,
+// c[((b (T+1) + t) 4 + g)][lane][MU] -- one vector store per slot (act) and
+// per wave (c) and step, read back by the slot's owner in the backward with
+// the same instruction count.  h_all stays in the public (T+1) x B x H
+// layout (it is the encoder's output).
 //
 // Backward step t (reverse): the slot owners turn dh_t (four wave partials of
 // W^T dG_{t+1} from LDS, + Wp^T dout_t for the decoder) into dG_t with the
@@ -81,6 +82,41 @@ __device__ __forceinline__ float tanh_m(float x) {
   return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * (2.f * kNegLog2e))), -1.f);
 }
 
+// MU consecutive floats in one vector access (the cell layout of a lane)
+template <int MU>
+__device__ __forceinline__ void store_vec(float* p, const float (&v)[MU]) {
+  if constexpr (MU == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (MU == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+  } else if constexpr (MU == 3) {
+    typedef float f3 __attribute__((ext_vector_type(3)));
+    f3 x = {v[0], v[1], v[2]};
+    __builtin_memcpy(p, &x, 12);
+  } else {
+#pragma unroll
+    for (int i = 0; i < MU; ++i) p[i] = v[i];
+  }
+}
+template <int MU>
+__device__ __forceinline__ void load_vec(const float* p, float (&v)[MU]) {
+  if constexpr (MU == 4) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else if constexpr (MU == 2) {
+    const float2 x = *reinterpret_cast<const float2*>(p);
+    v[0] = x.x; v[1] = x.y;
+  } else if constexpr (MU == 3) {
+    typedef float f3 __attribute__((ext_vector_type(3)));
+    f3 x;
+    __builtin_memcpy(&x, p, 12);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z;
+  } else {
+#pragma unroll
+    for (int i = 0; i < MU; ++i) v[i] = p[i];
+  }
+}
+
 // unit held by slot j of lane quarter q
 __device__ __forceinline__ int slot_unit(int j, int q) { return 16 * (j >> 2) + 4 * q + (j & 3); }
 
@@ -94,28 +130,56 @@ struct MwCfg {
   static constexpr int P = G4 * H + G4 + 2 * G4;                           // slab row floats
 };
 
+}  // namespace
+
+// One sequence segment of the forward (MwSeg, sgg_common.h; sgg.h
+// SggLstmSeg): steps t0 .. t0 + T - 1 of a Tl-step sequence.  rel holds B
+// rows per step and is read at steps t0 + t; h_all rows are Bl apart; the
+// saved states sit at their Tl-layout positions.  t0 > 0: the state entering
+// step t0 is ped (p mod Bsrc)'s, read from h_all[t0] and the tile-native c
+// at t0 (written by the segment that ran steps 0 .. t0 - 1 on Bsrc peds, e.g.
+// the discriminator's observed-steps prefix shared by its real and fake
+// halves).
+
+#ifdef SGG_LSTM_PROF
+// phase timestamps of workgroup 0 (tools/lstm_mw_probe.hip; diagnostic builds only)
+__device__ long long g_lstm_prof[64];
+#define LMARK(i) \
+  if (threadIdx.x == 0 && blk == 0) g_lstm_prof[i] = wall_clock64();
+#else
+#define LMARK(i)
+#endif
+
+namespace {
+
 // DEC / SAVE are compile-time, so the step loop carries no per-store
 // branches.  A padded lane (ped >= B, last block) runs on the clamped ped's
 // inputs, so it computes bit-identical values and its stores to that ped's
 // rows (h_all, rel_out) are benign duplicates: no store needs a guard.
 template <int H, bool DEC, bool SAVE>
-__global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
-    const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
-    const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
-    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B,
-    float* __restrict__ h_all, float* __restrict__ c_tile, float* __restrict__ act_tile, float* __restrict__ rel_out,
-    const float* __restrict__ Wu, int ldwu, const float* __restrict__ cu, int NU, float* __restrict__ U) {
+__device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS;
   constexpr bool decoder = DEC, save = SAVE;
+  const float* __restrict__ rel = sg.rel;
+  const float* __restrict__ A = sg.A;
+  const float* __restrict__ Whh = sg.Whh;
+  const float* __restrict__ bias = sg.bias;
+  const float* __restrict__ Wp = sg.Wp;
+  const float* __restrict__ bp = sg.bp;
+  float* __restrict__ h_all = sg.h_all;
+  float* __restrict__ c_tile = sg.c_tile;
+  float* __restrict__ act_tile = sg.act_tile;
+  float* __restrict__ rel_out = sg.rel_out;
+  const int T = sg.T, B = sg.B, Bl = sg.Bl, t0 = sg.t0, Tl = sg.Tl;
   __shared__ float hb[2][KS][64];
   __shared__ float2 rpart[2][4][kMwPeds];
   __shared__ float relseq[kMwMaxT][kMwPeds][2];
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, c16 = lane & 15;
-  const int blk = blockIdx.x;
   const int ped = blk * kMwPeds + c16;
   const int pc = ped < B ? ped : B - 1;   // clamped: every load and store unconditional and in bounds
+  LMARK(0);
 
   // [W_hh | A b] rows of tile mu in registers: A-operand row c16 is gate
   // c16 & 3 of unit slot_unit(g MU + mu, c16 >> 2); W_hh's columns in the
@@ -138,27 +202,94 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     w[mu][KS] = q == 0 ? ak0[mu] : q == 1 ? ak1[mu] : q == 2 ? bias[row] : 0.f;
   }
   float c[MU], wp0[MU], wp1[MU];
+  // t0 > 0: the source block / row of the state entering step t0
+  const int nsrc = (sg.Bsrc + kMwPeds - 1) / kMwPeds;
+  const int sblk = t0 > 0 ? blk % nsrc : blk;
+  const int spc = t0 > 0 ? pc % sg.Bsrc : pc;
 #pragma unroll
   for (int i = 0; i < MU; ++i) {
     const int j = g * MU + i, u = slot_unit(j, q);
-    const float hv = h0 ? h0[(size_t)pc * H + u] : 0.f;
-    c[i] = c0 ? c0[(size_t)pc * H + u] : 0.f;
-    hb[0][j][lane] = hv;
-    if (save) {
-      h_all[(size_t)pc * H + u] = hv;
-      c_tile[((size_t)blk * (T + 1) * KS + j) * 64 + lane] = c[i];
+    float hv, cv;
+    if (t0 > 0) {
+      hv = h_all[((size_t)t0 * Bl + spc) * H + u];
+      cv = c_tile[((((size_t)sblk * (Tl + 1) + t0) * 4 + g) * 64 + lane) * MU + i];
+    } else {
+      hv = sg.h0 ? sg.h0[(size_t)pc * H + u] : 0.f;
+      cv = sg.c0 ? sg.c0[(size_t)pc * H + u] : 0.f;
+      if (save) {
+        h_all[(size_t)pc * H + u] = hv;
+        c_tile[(((size_t)blk * (Tl + 1) * 4 + g) * 64 + lane) * MU + i] = cv;
+      }
     }
+    c[i] = cv;
+    hb[0][j][lane] = hv;
     wp0[i] = decoder ? Wp[u] : 0.f;
     wp1[i] = decoder ? Wp[H + u] : 0.f;
   }
   const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
-  if (!decoder)
-    for (int e = threadIdx.x; e < 2 * kMwPeds * T; e += kMwThreads) {
-      const int t = e / (2 * kMwPeds), p = (e >> 1) & (kMwPeds - 1), k = e & 1;
-      const int pp = min(blk * kMwPeds + p, B - 1);   // padded lanes see the clamped ped's inputs
-      relseq[t][p][k] = rel[((size_t)t * B + pp) * 2 + k];
+  // the encoder's inputs of all T steps: loaded into registers here, written
+  // to LDS after the epilogue's prefetch below is issued (so the LDS writes
+  // wait for these loads only)
+  constexpr int kRelPer = 2 * kMwPeds * kMwMaxT / kMwThreads;
+  float rv[kRelPer];
+  if (!decoder) {
+#pragma unroll
+    for (int m = 0; m < kRelPer; ++m) {
+      const int e = threadIdx.x + m * kMwThreads;
+      if (e < 2 * kMwPeds * T) {
+        const int t = e / (2 * kMwPeds), p = (e >> 1) & (kMwPeds - 1), k = e & 1;
+        const int pp = min(blk * kMwPeds + p, B - 1);   // padded lanes see the clamped ped's inputs
+        rv[m] = rel[((size_t)(t0 + t) * B + pp) * 2 + k];
+      }
     }
-  __syncthreads();
+  }
+
+  // the projection epilogue's Wu fragments (see below), fetched now so their
+  // latency hides under the recurrence: all of this wave's <= 8 tiles in
+  // registers (NU <= 512, H <= 48, 16-byte aligned rows)
+  constexpr bool kUPre = !DEC && H <= 48;
+  constexpr int kUT = 8;
+  const float* __restrict__ Wu = sg.Wu;
+  const int ldwu = sg.ldwu, NU = sg.NU;
+  const bool upre = kUPre && sg.U && NU <= 16 * 4 * kUT &&
+                    ((reinterpret_cast<uintptr_t>(Wu) | ((uintptr_t)ldwu * 4)) & 15) == 0;
+  float wu[kUPre ? kUT : 1][KS];
+  float cuv[kUPre ? kUT : 1][4];
+  if (upre) {
+    const int ntile = NU >> 4;
+#pragma unroll
+    for (int i = 0; i < kUT; ++i) {
+      const float4 v = *reinterpret_cast<const float4*>(sg.cu + 16 * min(g + 4 * i, ntile - 1) + 4 * q);
+      cuv[i][0] = v.x;
+      cuv[i][1] = v.y;
+      cuv[i][2] = v.z;
+      cuv[i][3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < kUT; ++i) {
+      const float* wr = Wu + (size_t)(min(g + 4 * i, ntile - 1) * 16 + c16) * ldwu;
+#pragma unroll
+      for (int m = 0; m < KS / 4; ++m) {
+        const float4 v = *reinterpret_cast<const float4*>(wr + 16 * m + 4 * q);
+        wu[i][4 * m] = v.x;
+        wu[i][4 * m + 1] = v.y;
+        wu[i][4 * m + 2] = v.z;
+        wu[i][4 * m + 3] = v.w;
+      }
+    }
+  }
+
+  if (!decoder) {
+#pragma unroll
+    for (int m = 0; m < kRelPer; ++m) {
+      const int e = threadIdx.x + m * kMwThreads;
+      if (e < 2 * kMwPeds * T) relseq[e / (2 * kMwPeds)][(e >> 1) & (kMwPeds - 1)][e & 1] = rv[m];
+    }
+  }
+  // LDS only: the prologue's global stores (saved initial state) need not
+  // complete before the recurrence
+  lds_barrier();
+  LMARK(1);
 
   // input k-step operand: r_x (q = 0), r_y (q = 1), 1 (q = 2), 0 (q = 3)
   // (loads unconditional, the constant lanes selected after)
@@ -167,7 +298,6 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
     return q < 2 ? v : (q == 2 ? 1.f : 0.f);
   };
   float xin = input(0);
-
   for (int t = 0; t < T; ++t) {
     if (decoder && t == 1) {
       // fold the hidden2pos feedback into the recurrence (see header)
@@ -209,19 +339,18 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
         const float s = r == 2 ? 2.f : 1.f;
         a[r] = gate_act(acc[mu][r], s, s * kNegLog2e);
       }
-      if (save) {   // tile-native: gate r, slot j, one lane-linear 256-byte line each
-        float* at = act_tile + (((size_t)blk * T + t) * 4 * KS + j) * 64 + lane;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) at[r * KS * 64] = a[r];
-      }
+      if (save)   // tile-native: slot j's four gates as one 16-byte value per lane
+        reinterpret_cast<float4*>(act_tile)[(((size_t)blk * Tl + t0 + t) * KS + j) * 64 + lane] =
+            make_float4(a[0], a[1], a[2], a[3]);
       c[mu] = fmaf(a[1], c[mu], a[0] * a[2]);
       const float h = a[3] * tanh_m(c[mu]);
       hb[rb ^ 1][j][lane] = h;
-      if (save || t == T - 1) h_all[((size_t)(save ? t + 1 : T) * B + pc) * H + slot_unit(j, q)] = h;
-      if (save) c_tile[(((size_t)blk * (T + 1) + t + 1) * KS + j) * 64 + lane] = c[mu];
+      if (save || t == T - 1) h_all[((size_t)(t0 + (save ? t + 1 : T)) * Bl + pc) * H + slot_unit(j, q)] = h;
       px = fmaf(wp0[mu], h, px);
       py = fmaf(wp1[mu], h, py);
     }
+    if (save)   // the wave's MU cells of this lane, contiguous
+      store_vec<MU>(c_tile + ((((size_t)blk * (Tl + 1) + t0 + t + 1) * 4 + g) * 64 + lane) * MU, c);
     if (decoder) {
       px += __shfl_xor(px, 16);
       px += __shfl_xor(px, 32);
@@ -230,6 +359,7 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
       if (q == 0) rpart[t & 1][g][c16] = make_float2(px, py);
     }
     lds_barrier();
+    if (t < 60) LMARK(t + 2);
     if (decoder && g == 0 && q == 0) {   // r_t = Wp h_t + bp
       const float2 r0 = rpart[t & 1][0][c16], r1 = rpart[t & 1][1][c16], r2 = rpart[t & 1][2][c16],
                    r3 = rpart[t & 1][3][c16];
@@ -237,7 +367,30 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
           make_float2(((r0.x + r1.x) + (r2.x + r3.x)) + bp0, ((r0.y + r1.y) + (r2.y + r3.y)) + bp1);
     }
   }
-  if (!decoder && U) {
+  const float* __restrict__ cu = sg.cu;
+  float* __restrict__ U = sg.U;
+  if (kUPre && upre) {
+    // U^T tiles g + 4 i from the prefetched fragments: eight independent
+    // accumulation chains
+    float hk[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[T & 1][ks][lane];
+    const int ntile = NU >> 4;
+    floatx4 acc[kUT];
+#pragma unroll
+    for (int i = 0; i < kUT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < kUT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wu[i][ks], hk[ks], acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < kUT; ++i) {
+      const int nt = g + 4 * i;
+      if (nt < ntile)
+        *reinterpret_cast<float4*>(U + (size_t)pc * NU + 16 * nt + 4 * q) =
+            make_float4(acc[i][0] + cuv[i][0], acc[i][1] + cuv[i][1], acc[i][2] + cuv[i][2], acc[i][3] + cuv[i][3]);
+    }
+  } else if (!decoder && U) {
     // projection epilogue: U = h_T Wu^T + cu (B x NU; the pooling MLP's h-half
     // of its first layer, models.py:538) while h_T is still in LDS, in the
     // recurrence's own operand layout: U^T tile (16 units x 16 peds) =
@@ -301,6 +454,23 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(
       }
     }
   }
+  LMARK(63);
+}
+
+template <int H, bool DEC, bool SAVE>
+__global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd_kernel(MwSeg sg) {
+  mw_fwd_body<H, DEC, SAVE>(sg, blockIdx.x);
+}
+
+// two independent encoder segments in ONE launch: workgroups [0, nblk_a) run
+// segment a, the rest segment b (e.g. the generator's encoder beside the
+// discriminator's observed-steps prefix: both read only the observed steps)
+template <int HA, bool SA, int HB, bool SB>
+__global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd2_kernel(MwSeg a, MwSeg b, int nblk_a) {
+  if ((int)blockIdx.x < nblk_a)
+    mw_fwd_body<HA, false, SA>(a, blockIdx.x);
+  else
+    mw_fwd_body<HB, false, SB>(b, blockIdx.x - nblk_a);
 }
 
 template <int H, bool DEC, bool WGRAD>
@@ -310,7 +480,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     const float* __restrict__ rel, const float* __restrict__ rel_out, const float* __restrict__ dh_last,
     const float* __restrict__ dout, int T, int B, float* __restrict__ dh0, float* __restrict__ drel_in,
     float* __restrict__ drel_tot, float* __restrict__ wpart, const float* __restrict__ dout2, int bsplit,
-    int t_stop) {
+    int t_stop, int t_sh, int Bsrc) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
   constexpr bool decoder = DEC, wgrad = WGRAD;
   // decoder slab rows carry [dWp (2 x H) | dbp (2)] after [dW_hh | db | dA]
@@ -326,6 +496,11 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   const int ped = blk * kMwPeds + c16;
   const bool valid = ped < B;
   const int pc = valid ? ped : B - 1;
+  // t_sh > 0: the states of steps < t_sh (cells / h up to index t_sh) of ped
+  // p are ped (p mod Bsrc)'s -- a prefix shared by the halves of the batch
+  // and saved once (MwSeg t0); Bsrc is a multiple of 16 there
+  const int nsrc = t_sh > 0 ? Bsrc / kMwPeds : 1;
+  auto sblk = [&](bool shared_at) { return shared_at ? blk % nsrc : blk; };
 
   // weight-gradient operand of step t: h_{t-1} = h_all[t] of the block's 16
   // peds, fetched one step ahead, staged in LDS
@@ -335,7 +510,9 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
     for (int m = 0; m < NHS; ++m) {
       const int e = ht + m * kMwThreads;   // < 16 H exactly (NHS = 16 H / 256)
-      hv[m] = h_all[((size_t)t * B + min(blk * kMwPeds + e / H, B - 1)) * H + e % H];
+      int r = min(blk * kMwPeds + e / H, B - 1);
+      if (t <= t_sh && t_sh > 0) r %= Bsrc;
+      hv[m] = h_all[((size_t)t * B + r) * H + e % H];
     }
   };
   auto stage_store = [&](int buf) {
@@ -450,18 +627,17 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       nr0 = rv.x;
       nr1 = rv.y;
     }
-    const float* ab = act_tile + ((size_t)blk * T + t) * 4 * KS * 64 + lane;
-    const float* cb = c_tile + ((size_t)blk * (T + 1) + t) * KS * 64 + lane;
+    const float4* ab = reinterpret_cast<const float4*>(act_tile) + ((size_t)sblk(t < t_sh) * T + t) * KS * 64 + lane;
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
-      const int j = g * MU + i;
-      ni[i] = ab[(0 * KS + j) * 64];
-      nf[i] = ab[(1 * KS + j) * 64];
-      ng[i] = ab[(2 * KS + j) * 64];
-      no[i] = ab[(3 * KS + j) * 64];
-      nc[i] = cb[(KS + j) * 64];
-      ncp[i] = cb[j * 64];
+      const float4 v = ab[(g * MU + i) * 64];
+      ni[i] = v.x;
+      nf[i] = v.y;
+      ng[i] = v.z;
+      no[i] = v.w;
     }
+    load_vec<MU>(c_tile + ((((size_t)sblk(t + 1 <= t_sh) * (T + 1) + t + 1) * 4 + g) * 64 + lane) * MU, nc);
+    load_vec<MU>(c_tile + ((((size_t)sblk(t <= t_sh) * (T + 1) + t) * 4 + g) * 64 + lane) * MU, ncp);
     if (decoder) {
       // dout2: the output gradient of peds >= bsplit is a separate (T x (B - bsplit) x 2) block
       const float* dp = (dout2 && pc >= bsplit) ? dout2 + ((size_t)t * (B - bsplit) + (pc - bsplit)) * 2
@@ -648,27 +824,33 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 }
 
 template <int H>
-int launch_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0, const float* c0,
-               const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
-               float* rel_out, const float* Wu, int ldwu, const float* cu, int NU, float* U, hipStream_t st) {
-  const int grid = (B + kMwPeds - 1) / kMwPeds;
-  auto k = decoder ? (act_all ? lstm_mw_fwd_kernel<H, true, true> : lstm_mw_fwd_kernel<H, true, false>)
-                   : (act_all ? lstm_mw_fwd_kernel<H, false, true> : lstm_mw_fwd_kernel<H, false, false>);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kMwThreads), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B, h_all, c_all,
-                     act_all, rel_out, Wu, ldwu, cu, NU, U);
+int launch_seg(const MwSeg& sg, bool decoder, hipStream_t st) {
+  const int grid = (sg.B + kMwPeds - 1) / kMwPeds;
+  auto k = decoder ? (sg.act_tile ? lstm_mw_fwd_kernel<H, true, true> : lstm_mw_fwd_kernel<H, true, false>)
+                   : (sg.act_tile ? lstm_mw_fwd_kernel<H, false, true> : lstm_mw_fwd_kernel<H, false, false>);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kMwThreads), 0, st, sg);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
+}
+
+int launch_seg_h(const MwSeg& sg, int H, bool decoder, hipStream_t st) {
+  switch (H) {
+    case 16: return launch_seg<16>(sg, decoder, st);
+    case 32: return launch_seg<32>(sg, decoder, st);
+    case 48: return launch_seg<48>(sg, decoder, st);
+    default: return launch_seg<64>(sg, decoder, st);
+  }
 }
 
 template <int H>
 int launch_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
                int T, int B, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart, hipStream_t st,
-               const float* dout2, int bsplit, int t_stop) {
+               const float* dout2, int bsplit, int t_stop, int t_sh, int Bsrc) {
   const int grid = (B + kMwPeds - 1) / kMwPeds;
   auto k = decoder ? (wpart ? lstm_mw_bwd_kernel<H, true, true> : lstm_mw_bwd_kernel<H, true, false>)
                    : (wpart ? lstm_mw_bwd_kernel<H, false, true> : lstm_mw_bwd_kernel<H, false, false>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(wpart ? 2 * kMwThreads : kMwThreads), 0, st, A, Whh, Wp, h_all, c_all, act_all, rel, rel_out,
-                     dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart, dout2, bsplit, t_stop);
+                     dh_last, dout, T, B, dh0, drel_in, drel_tot, wpart, dout2, bsplit, t_stop, t_sh, Bsrc);
   SGG_RETURN_LAUNCH("sgg_lstm_bwd");
 }
 
@@ -707,25 +889,58 @@ int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float*
                 const float* cu, int NU, float* U) {
   SGG_CHECK_ARG(decoder || T <= kMwMaxT, "sgg_lstm_fwd: encoder sequences of the H=%d kernels hold <= %d steps (T=%d)",
                 H, kMwMaxT, T);
-  switch (H) {
-    case 16: return launch_fwd<16>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
-    case 32: return launch_fwd<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
-    case 48: return launch_fwd<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
-    default: return launch_fwd<64>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U, st);
+  const MwSeg sg{rel, A, Whh, bias, h0, c0, Wp, bp, T, B, B, 0, T, B, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U};
+  return launch_seg_h(sg, H, decoder != 0, st);
+}
+
+// checks of one encoder segment (sgg.h SggLstmSeg)
+static int seg_check(const MwSeg& s, int H, const char* fn) {
+  SGG_CHECK_ARG(s.rel && s.A && s.Whh && s.bias && s.h_all && (s.c_tile || !s.act_tile), "%s: null pointer", fn);
+  SGG_CHECK_ARG(H == 16 || H == 32 || H == 48 || H == 64, "%s: hidden size %d (16/32/48/64)", fn, H);
+  SGG_CHECK_ARG(s.T >= 1 && s.T <= kMwMaxT && s.B >= 1 && s.Bl >= s.B && s.t0 >= 0 && s.t0 + s.T <= s.Tl,
+                "%s: bad sizes T=%d B=%d Bl=%d t0=%d Tl=%d", fn, s.T, s.B, s.Bl, s.t0, s.Tl);
+  SGG_CHECK_ARG(s.t0 == 0 || (s.c_tile && s.Bsrc >= 1 && s.Bsrc <= s.Bl &&
+                              (s.Bsrc == s.B || (s.Bsrc % kMwPeds == 0 && s.B % s.Bsrc == 0))),
+                "%s: a segment from step t0=%d needs the saved cells and Bsrc = B or a multiple of 16 dividing B "
+                "(B=%d Bsrc=%d)", fn, s.t0, s.B, s.Bsrc);
+  SGG_CHECK_ARG(s.t0 == 0 || (!s.h0 && !s.c0), "%s: t0 > 0 takes its state from h_all / c_all, not h0 / c0", fn);
+  SGG_CHECK_ARG(!s.U || (s.Wu && s.cu && s.NU >= 16 && s.NU % 16 == 0 && s.ldwu >= H), "%s: bad projection", fn);
+  return 0;
+}
+
+int lstm_mw_fwd_seg(const MwSeg& s, int H, hipStream_t st) {
+  if (int rc = seg_check(s, H, "sgg_lstm_fwd_seg")) return rc;
+  return launch_seg_h(s, H, false, st);
+}
+
+int lstm_mw_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb, hipStream_t st) {
+  if (int rc = seg_check(a, Ha, "sgg_lstm_fwd_seg2 (a)")) return rc;
+  if (int rc = seg_check(b, Hb, "sgg_lstm_fwd_seg2 (b)")) return rc;
+  const int na = (a.B + kMwPeds - 1) / kMwPeds, nb = (b.B + kMwPeds - 1) / kMwPeds;
+  if (Ha == 32 && Hb == 48 && b.act_tile) {   // the generator encoder + the discriminator prefix
+    auto k = a.act_tile ? lstm_mw_fwd2_kernel<32, true, 48, true> : lstm_mw_fwd2_kernel<32, false, 48, true>;
+    hipLaunchKernelGGL(k, dim3(na + nb), dim3(kMwThreads), 0, st, a, b, na);
+    SGG_RETURN_LAUNCH("sgg_lstm_fwd_seg2");
   }
+  // other hidden-size pairs: two launches
+  if (int rc = launch_seg_h(a, Ha, false, st)) return rc;
+  return launch_seg_h(b, Hb, false, st);
 }
 
 int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                 const float* act_all, const float* rel, const float* rel_out, const float* dh_last, const float* dout,
                 int T, int B, int H, int decoder, float* dh0, float* drel_in, float* drel_tot, float* wpart,
-                hipStream_t st, const float* dout2, int bsplit, int t_stop) {
+                hipStream_t st, const float* dout2, int bsplit, int t_stop, int t_sh, int Bsrc) {
   // the helper waves pass one barrier per step of ALL T steps
   SGG_CHECK_ARG(!wpart || t_stop == 0, "sgg_lstm_bwd: weight gradients need every step (t_stop=%d)", t_stop);
+  SGG_CHECK_ARG(t_sh == 0 || (!decoder && t_sh < T && Bsrc >= kMwPeds && Bsrc % kMwPeds == 0 && B % Bsrc == 0),
+                "sgg_lstm_bwd: a shared prefix needs an encoder, t_sh < T and Bsrc a multiple of 16 dividing B "
+                "(t_sh=%d T=%d B=%d Bsrc=%d)", t_sh, T, B, Bsrc);
   switch (H) {
-    case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
-    case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
-    case 48: return launch_bwd<48>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
-    default: return launch_bwd<64>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop);
+    case 16: return launch_bwd<16>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop, t_sh, Bsrc);
+    case 32: return launch_bwd<32>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop, t_sh, Bsrc);
+    case 48: return launch_bwd<48>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop, t_sh, Bsrc);
+    default: return launch_bwd<64>(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, decoder, dh0, drel_in, drel_tot, wpart, st, dout2, bsplit, t_stop, t_sh, Bsrc);
   }
 }
 

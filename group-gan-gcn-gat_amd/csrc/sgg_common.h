@@ -99,7 +99,21 @@ __attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const floa
                                                       const float* dout, int T, int B, int H, int decoder,
                                                       float* dh0, float* drel_in, float* drel_tot, float* wpart,
                                                       hipStream_t st, const float* dout2 = nullptr,
-                                                      int bsplit = 0, int t_stop = 0);
+                                                      int bsplit = 0, int t_stop = 0, int t_sh = 0, int Bsrc = 0);
+// one encoder / decoder sequence segment of the four-wave forward (lstm_mw.hip)
+struct MwSeg {
+  const float *rel, *A, *Whh, *bias, *h0, *c0, *Wp, *bp;
+  int T, B, Bl, t0, Tl, Bsrc;
+  float *h_all, *c_tile, *act_tile, *rel_out;
+  const float* Wu;
+  int ldwu;
+  const float* cu;
+  int NU;
+  float* U;
+};
+__attribute__((visibility("hidden"))) int lstm_mw_fwd_seg(const MwSeg& s, int H, hipStream_t st);
+__attribute__((visibility("hidden"))) int lstm_mw_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
+                                                           hipStream_t st);
 
 // fold.hip: the fold backwards of one sgg_grad_finish in one launch (a
 // workgroup each; dA_src / db_src point at the summed (dA, dbias)); internal

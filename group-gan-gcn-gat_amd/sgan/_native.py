@@ -49,6 +49,16 @@ class GcnModArgs(ctypes.Structure):
 
 _gargs = ctypes.POINTER(GcnModArgs)
 
+
+class LstmSeg(ctypes.Structure):
+    """SggLstmSeg (include/sgg.h): one encoder sequence segment."""
+    _fields_ = [("rel", _p), ("A", _p), ("Whh", _p), ("bias", _p), ("h0", _p), ("c0", _p), ("T", _i), ("B", _i),
+                ("Bl", _i), ("t0", _i), ("Tl", _i), ("Bsrc", _i), ("h_all", _p), ("c_all", _p), ("act_all", _p),
+                ("Wu", _p), ("ldwu", _i), ("cu", _p), ("NU", _i), ("U", _p)]
+
+
+_sargs = ctypes.POINTER(LstmSeg)
+
 FOLD_MAX = 8   # SGG_FOLD_MAX
 
 
@@ -96,6 +106,9 @@ SIGNATURES = {
     "sgg_xtw_splits": (_i, [_i, _i, _i]),
     "sgg_lstm_bwd_split": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_lstm_bwd_tail": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p]),
+    "sgg_lstm_fwd_seg": (_i, [_sargs, _i, _p]),
+    "sgg_lstm_fwd_seg2": (_i, [_sargs, _i, _sargs, _i, _p]),
+    "sgg_lstm_bwd_shared": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_lstm_u_ok": (_i, [_i, _i, _i, _i, _i, _i]),
     "sgg_lstm_fwd_u": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p]),
     "sgg_head_ok": (_i, [_i, _i]),

@@ -1452,6 +1452,94 @@ def scene_mean_over_groups(gx, groups):
 # ---------------------------------------------------------------------------
 # fused LSTM sequences (encoder / decoder rollout)
 # ---------------------------------------------------------------------------
+def _tkey(t):
+    return (t.data_ptr(), tuple(t.shape), tuple(t.stride()))
+
+
+class SharedPrefix:
+    """The discriminator encoder's observed steps, run once (sgg.h
+    SggLstmSeg).  Its input traj_rel = cat(obs_rel, pred) (train.py:404-407,
+    456-459) starts with obs_rel for the real and the fake half alike, and
+    obs_rel is exactly what the generator's encoder reads first: the
+    generator's encoder launch on obs_rel also runs the discriminator's first
+    obs_len steps on obs_rel's Bsrc peds (sgg_lstm_fwd_seg2), saving them at
+    their positions of the discriminator's (T, copies Bsrc) state layout, and
+    the discriminator's forward on traj_rel then runs the remaining steps on
+    every column from there (sgg_lstm_fwd_seg, t0 = obs_len).  The backward
+    reads the shared steps of column p from column p mod Bsrc
+    (sgg_lstm_bwd_shared), so every result is the one of the full sequence.
+
+    Armed by `shared_prefix(...)` around a training step; the two halves only
+    meet when the generator's encoder runs on obs_rel itself and the
+    discriminator on a traj_cat whose head was obs_rel (same tensor), with the
+    discriminator's weights unchanged in between (fold versions)."""
+
+    def __init__(self, lstm, emb, obs_rel, T, copies, fold_specs=None):
+        self.lstm, self.emb, self.fold_specs = lstm, emb, fold_specs
+        self.key = _tkey(obs_rel)
+        self.T_pre, self.Bsrc = int(obs_rel.shape[0]), int(obs_rel.shape[1])
+        self.T, self.B = int(T), copies * self.Bsrc
+        self.H = int(lstm.weight_hh_l0.shape[1])
+        self.ran = self.used = False
+        lib = _lib()
+        self.ok = (lstm.num_layers == 1 and 0 < self.T_pre < self.T and self.Bsrc > 0
+                   and (copies == 1 or self.Bsrc % 16 == 0)
+                   and bool(lib.sgg_lstm_u_ok(self.T, self.B, self.H, 0, 1, 16))
+                   and bool(lib.sgg_lstm_u_ok(self.T_pre, self.Bsrc, self.H, 0, 1, 16)))
+
+    def arm(self, rel, H_g):
+        """The generator encoder's launch on `rel`: the prefix rides along iff
+        rel is obs_rel and the kernel pair is one launch (H_g = 32, H = 48)."""
+        return self.ok and not self.ran and H_g == 32 and self.H == 48 and _tkey(rel) == self.key
+
+    def segment(self, rel):
+        """-> SggLstmSeg of the prefix (state buffers allocated here)."""
+        lib = _lib()
+        dev = rel.device
+        T, B, H = self.T, self.B, self.H
+        self.h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
+        self.c_all = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 1)), device=dev, dtype=torch.float32)
+        self.act = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 0)), device=dev, dtype=torch.float32)
+        l = self.lstm
+        if self.fold_specs is not None:   # all of the module's folds in one launch, as its forward would
+            prefold(self.fold_specs())
+        self.A, self.bias = fold_fwd(l.weight_ih_l0, self.emb.weight, self.emb.bias, l.bias_ih_l0, l.bias_hh_l0)
+        self.Whh = l.weight_hh_l0.contiguous()
+        self.fold_ver = _fold_key(*lstm_fold_spec(l, self.emb))[1]
+        self.whh_ver = (l.weight_hh_l0._version, _EPOCH.get(l.weight_hh_l0.data_ptr(), 0))
+        return N.LstmSeg(N.ptr(rel), N.ptr(self.A), N.ptr(self.Whh), N.ptr(self.bias), None, None, self.T_pre,
+                         self.Bsrc, B, 0, T, self.Bsrc, N.ptr(self.h_all), N.ptr(self.c_all), N.ptr(self.act),
+                         None, 0, None, 0, None)
+
+    def matches(self, rel, W_hh, T, save):
+        """The discriminator's forward on `rel` may continue from the prefix."""
+        if not (self.ran and not self.used and save and T == self.T and W_hh is self.lstm.weight_hh_l0):
+            return False
+        if tuple(rel.shape) != (self.T, self.B, 2) or getattr(rel, "_sgg_head_key", None) != self.key:
+            return False
+        l = self.lstm
+        return (_fold_key(*lstm_fold_spec(l, self.emb))[1] == self.fold_ver
+                and (l.weight_hh_l0._version, _EPOCH.get(l.weight_hh_l0.data_ptr(), 0)) == self.whh_ver)
+
+
+_PREFIX = [None]
+
+
+@contextlib.contextmanager
+def shared_prefix(D, obs_rel, T, copies):
+    """Arm a SharedPrefix of the discriminator D's encoder for the duration of
+    one step (see SharedPrefix); D's forward on traj_cat(obs_rel, ...) of T
+    steps and copies x obs_rel's peds may then continue from it."""
+    prev = _PREFIX[0]
+    enc = D.encoder
+    _PREFIX[0] = SharedPrefix(enc.encoder, enc.spatial_embedding, obs_rel, T, copies,
+                              getattr(D, "fold_specs", None))
+    try:
+        yield _PREFIX[0]
+    finally:
+        _PREFIX[0] = prev
+
+
 class _LSTMSeq(torch.autograd.Function):
     """Fused LSTM sequence on the raw parameters of Linear(2, E) + LSTM(E, H)
     (+ hidden2pos for the decoder): the embedding fold is one launch
@@ -1466,22 +1554,35 @@ class _LSTMSeq(torch.autograd.Function):
     def forward(ctx, rel, W_ih, W_hh, b_ih, b_hh, We, be, h0, c0, Wp, bp, decoder, T, save, u=None, slink=None):
         lib = _lib()
         ctx.t_stop = int(getattr(rel, "_sgg_grad_from", 0))
+        pfx = _PREFIX[0]
+        rel_in = rel
         rel = _req(rel, "rel").contiguous()
         H = W_hh.shape[1]
         B = rel.shape[-2]
         dev = rel.device
         A, bias = fold_fwd(W_ih, We, be, b_ih, b_hh)
-        h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
-        # saved states in the layout of the kernel family (H, B) picks
-        c_all = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 1)), device=dev, dtype=torch.float32)
-        act = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 0)), device=dev, dtype=torch.float32) \
-            if save else None
+        # the discriminator's shared observed-steps prefix: this launch carries
+        # it (generator encoder), or this sequence continues from it
+        carry = pfx is not None and not decoder and h0 is None and c0 is None and pfx.arm(rel_in, H)
+        cont = (pfx is not None and not decoder and h0 is None and c0 is None and not carry
+                and pfx.matches(rel_in, W_hh, T, save))
+        ctx.t_sh, ctx.bsrc = (pfx.T_pre, pfx.Bsrc) if cont and pfx.Bsrc < B else (0, 0)
+        if cont:
+            h_all, c_all, act = pfx.h_all, pfx.c_all, pfx.act
+            pfx.used = True
+        else:
+            h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
+            # saved states in the layout of the kernel family (H, B) picks
+            c_all = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 1)), device=dev, dtype=torch.float32)
+            act = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 0)), device=dev, dtype=torch.float32) \
+                if save else None
         rel_out = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
         Whh = W_hh.contiguous()
         h0c = h0.contiguous() if h0 is not None else None
         c0c = c0.contiguous() if c0 is not None else None
         Wpc = Wp.contiguous() if Wp is not None else None
         U = None
+        Wu = cu = None
         if u is not None:
             # the pooling MLP's U = h_T Wu^T + cu from the kernel's epilogue
             Wu, cu = u
@@ -1489,6 +1590,28 @@ class _LSTMSeq(torch.autograd.Function):
             cu = cu.contiguous()
             U = torch.empty(B, Wu.shape[0], device=dev, dtype=torch.float32)
 
+        def seg(t0, Tn, Bsrc):
+            return N.LstmSeg(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), Tn, B, B, t0, T,
+                             Bsrc, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu),
+                             Wu.stride(0) if Wu is not None else 0, N.ptr(cu), Wu.shape[0] if Wu is not None else 0,
+                             N.ptr(U))
+        pfx_seg = pfx.segment(rel) if carry else None
+        if carry:
+            pfx.ran = True
+        kname = None
+        if carry:
+            ga, gb = seg(0, T, B), pfx_seg
+            kname = "sgg::lstm_mw_fwd2_kernel<32, %s, 48, true>" % ("true" if save else "false")
+
+            def launch():
+                N.check(lib.sgg_lstm_fwd_seg2(N.ctypes.byref(ga), H, N.ctypes.byref(gb), pfx.H, N.stream_ptr()),
+                        "sgg_lstm_fwd_seg2")
+        elif cont:
+            gs = seg(pfx.T_pre, T - pfx.T_pre, pfx.Bsrc)
+
+            def launch():
+                N.check(lib.sgg_lstm_fwd_seg(N.ctypes.byref(gs), H, N.stream_ptr()), "sgg_lstm_fwd_seg")
+        elif u is not None:
             def launch():
                 N.check(lib.sgg_lstm_fwd_u(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), T,
                                            B, H, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu), Wu.stride(0),
@@ -1501,11 +1624,17 @@ class _LSTMSeq(torch.autograd.Function):
         launch()
         if timer.active:
             # per ped-step: gates 2 4H (H + 3) FLOP + ~12 H cell / activation; bytes: inputs, saved states
-            fl = T * B * (8.0 * H * (H + 3) + 12.0 * H) + (2.0 * B * H * U.shape[1] if U is not None else 0.0)
-            nb = 4.0 * (T * B * 2 + (act.numel() + c_all.numel() + (T + 1) * B * H if save else B * H)
+            Ts = T - pfx.T_pre if cont else T    # the steps this launch runs
+            fl = Ts * B * (8.0 * H * (H + 3) + 12.0 * H) + (2.0 * B * H * U.shape[1] if U is not None else 0.0)
+            nb = 4.0 * (Ts * B * 2 + ((act.numel() + c_all.numel()) * Ts / T + (Ts + 1) * B * H if save else B * H)
                         + 4 * H * (H + 3) + (T * B * 2 if decoder else 0) + (U.numel() if U is not None else 0))
-            timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), int(save), 0).decode(),
-                      (T, B, int(decoder), int(save)), fl, nb, launch)
+            if carry:   # + the prefix: T_pre steps of Bsrc peds, states saved
+                Hp, Tp, Bp = pfx.H, pfx.T_pre, pfx.Bsrc
+                fl += Tp * Bp * (8.0 * Hp * (Hp + 3) + 12.0 * Hp)
+                nb += 4.0 * (Tp * Bp * 2 + Tp * Bp * 5 * Hp + (Tp + 1) * Bp * Hp + 4 * Hp * (Hp + 3))
+            name = kname or lib.sgg_lstm_kernel_name(H, B, int(decoder), int(save), 0).decode()
+            timer.add(name, (Ts, B, int(decoder), int(save)) + ((pfx.T_pre,) if (carry or cont) else ()), fl, nb,
+                      launch)
         ctx.meta = (decoder, T, B, H, h0 is not None)
         ctx.slink = slink
         ctx.set_materialize_grads(False)   # unused outputs (the decoder's h_last) get None, not a zero fill
@@ -1558,7 +1687,12 @@ class _LSTMSeq(torch.autograd.Function):
             dout = None
             dhl = dh_last.contiguous() if dh_last is not None else None
         tail = (not decoder and not wgrad and not has_h0 and rows > 0 and 0 < ctx.t_stop < T)
-        if tail:   # input gradients of steps t_stop .. T-1 only (the rest are not wanted)
+        if ctx.t_sh > 0:   # steps < t_sh saved once for column p mod bsrc (SharedPrefix)
+            def launch():
+                N.check(lib.sgg_lstm_bwd_shared(N.ptr(A), N.ptr(Whh), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
+                                                N.ptr(rel), N.ptr(dhl), T, B, H, ctx.t_sh, ctx.bsrc, N.ptr(drel_in),
+                                                N.ptr(wpart), N.stream_ptr()), "sgg_lstm_bwd_shared")
+        elif tail:   # input gradients of steps t_stop .. T-1 only (the rest are not wanted)
             def launch():
                 N.check(lib.sgg_lstm_bwd_tail(N.ptr(A), N.ptr(Whh), N.ptr(h_all), N.ptr(c_all), N.ptr(act),
                                               N.ptr(rel), N.ptr(dhl), T, B, H, ctx.t_stop, N.ptr(drel_in),
@@ -1799,6 +1933,7 @@ class _TrajCat(torch.autograd.Function):
     @staticmethod
     def forward(ctx, head, a, b, pos0):
         T0, B = head.shape[0], head.shape[1]
+        head_key = _tkey(head)
         T1 = a.shape[0]
         # rows of (x, y) pairs with a free step stride; anything else (e.g. the
         # permuted views seq_collate yields, trajectories_GCN.py:33) is copied
@@ -1819,6 +1954,7 @@ class _TrajCat(torch.autograd.Function):
         ctx.dims = (T0, B)
         if not head.requires_grad:
             out._sgg_grad_from = T0   # the consumer's backward may skip the head steps' input gradients
+        out._sgg_head_key = head_key   # every column starts with `head` (SharedPrefix)
         if start is None:
             return out
         ctx.mark_non_differentiable(start)

@@ -39,6 +39,7 @@ The result equals single-GPU training on the global batch up to summation
 order.
 """
 import contextlib
+import os
 import random
 
 import numpy as np
@@ -144,6 +145,9 @@ class KernelOps:
     # the backward ops' weight-gradient finishes queued and issued together
     # (two launches per backward pass instead of two per op)
     defer_finish = staticmethod(K.defer_grad_finish)
+    # the discriminator encoder's observed steps run once, in the generator
+    # encoder's launch (kernels.SharedPrefix)
+    shared_prefix = staticmethod(K.shared_prefix)
 
 
 class GanTrainer:
@@ -197,6 +201,14 @@ class GanTrainer:
         return vals
 
     # -- steps ---------------------------------------------------------------
+    def _prefix(self, obs_rel, copies):
+        """The discriminator encoder's observed steps run once, beside the
+        generator's encoder (ops.shared_prefix; a no-op without it)."""
+        sp = getattr(self.ops, "shared_prefix", None)
+        if sp is None or getattr(self.D, "encoder", None) is None or os.environ.get("SGG_NO_SHARED_PREFIX"):
+            return contextlib.nullcontext()
+        return sp(self.D, obs_rel, self.args.obs_len + self.args.pred_len, copies)
+
     def _scope(self):
         st = contextlib.ExitStack()
         st.enter_context(getattr(self.ops, "handoff", contextlib.nullcontext)())
@@ -223,13 +235,14 @@ class GanTrainer:
             # G's folds (stale since the last G-step) and D's (since the last
             # D-step) in ONE launch; the forwards below find them cached
             prefold(self.G.fold_specs() + self.D.fold_specs())
-        with torch.no_grad():
-            fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
-        # D reads traj[0] (the start positions, models.py:989) and traj_rel
-        # only: [fake | real] side by side, no relative_to_abs needed
-        traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
-        sc2 = sc.repeat(2)
-        scores = self.D(start, traj_rel, _sse_of(sc2), scenes=sc2)
+        with self._prefix(obs_rel, 2):
+            with torch.no_grad():
+                fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
+            # D reads traj[0] (the start positions, models.py:989) and traj_rel
+            # only: [fake | real] side by side, no relative_to_abs needed
+            traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
+            sc2 = sc.repeat(2)
+            scores = self.D(start, traj_rel, _sse_of(sc2), scenes=sc2)
         if inputs is not None:
             y_real = inputs.y[0]
         else:
@@ -265,7 +278,13 @@ class GanTrainer:
         # the k samples differ only in the noise appended after the graph
         # module: the encoder / pooling / GAT context runs once (with autograd)
         # and only the decoder rolls out k times
-        ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
+        pfx = self._prefix(obs_rel, 1)
+        pfx.__enter__()
+        try:
+            ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
+        except BaseException:
+            pfx.__exit__(None, None, None)
+            raise
         if self.selective_backward and k > 1:
             best = None
             if use_l2:
@@ -306,6 +325,7 @@ class GanTrainer:
         try:
             scores = D(obs[:1], ops.traj_cat(obs_rel, fake_rel_last), sse, scenes=sc)
         finally:
+            pfx.__exit__(None, None, None)
             for p in self.d_params:
                 p.requires_grad_(True)
         y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)

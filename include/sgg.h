@@ -421,6 +421,54 @@ int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float*
                  const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,
                  float* drel_in, float* drel_tot, float* wpart, void* stream);
 
+/* Encoder sequence SEGMENTS of the four-wave family (sgg_lstm_u_ok's family,
+ * T <= 64): steps t0 .. t0 + T - 1 of a Tl-step sequence whose states are
+ * saved at their Tl-layout positions -- the discriminator encoder's observed
+ * steps (models.py:976-980: Encoder(traj_rel), whose first obs_len inputs are
+ * obs_rel for the real and the fake trajectories alike) run ONCE, beside the
+ * generator's encoder of the same obs_rel (sgg_lstm_fwd_seg2: one launch),
+ * and the discriminator's forward runs only the remaining steps on both
+ * halves (sgg_lstm_fwd_seg with t0 = obs_len, Bsrc = the prefix's peds).
+ *   rel      (rows t0 .. t0+T-1 of a (t0+T) x B x 2 input; t0 = 0: T x B x 2)
+ *   A, Whh, bias, h0, c0 (t0 = 0 only), Wu / ldwu / cu / NU / U: as sgg_lstm_fwd_u (U NULL: none)
+ *   h_all    (Tl + 1) x Bl x H, rows Bl apart (Bl >= B); c_all / act_all the
+ *            tile-native saved states sized sgg_lstm_state_floats(Tl, Bl, H, .)
+ *            (act_all NULL: no saved states; only h_all[t0 + T] is written)
+ *   t0 > 0:  the state entering step t0 of ped p is ped (p mod Bsrc)'s,
+ *            read from h_all[t0] and c_all (Bsrc = B, or a multiple of 16
+ *            dividing B); h0 / c0 must be NULL.
+ * The backward of the whole Tl-step sequence is sgg_lstm_bwd_shared (or
+ * sgg_lstm_bwd / _tail when Bsrc = B: the layout is then complete). */
+typedef struct {
+  const float* rel;
+  const float* A;
+  const float* Whh;
+  const float* bias;
+  const float* h0;
+  const float* c0;
+  int T, B, Bl, t0, Tl, Bsrc;
+  float* h_all;
+  float* c_all;
+  float* act_all;
+  const float* Wu;
+  int ldwu;
+  const float* cu;
+  int NU;
+  float* U;
+} SggLstmSeg;
+int sgg_lstm_fwd_seg(const SggLstmSeg* seg, int H, void* stream);
+/* Two independent segments in ONE launch (a's workgroups first); one launch
+ * for (Ha, Hb) = (32, 48) with b saving states, two launches otherwise. */
+int sgg_lstm_fwd_seg2(const SggLstmSeg* a, int Ha, const SggLstmSeg* b, int Hb, void* stream);
+/* sgg_lstm_bwd (encoder) of a Tl = T step sequence whose steps < t_sh were
+ * saved once for Bsrc peds (sgg_lstm_fwd_seg with t0 = t_sh): ped p reads the
+ * saved states of steps < t_sh (cells and h up to t_sh) of ped p mod Bsrc.
+ * Bsrc a multiple of 16 dividing B; results identical to sgg_lstm_bwd on the
+ * complete layout. */
+int sgg_lstm_bwd_shared(const float* A, const float* Whh, const float* h_all, const float* c_all,
+                        const float* act_all, const float* rel, const float* dh_last, int T, int B, int H,
+                        int t_sh, int Bsrc, float* drel_in, float* wpart, void* stream);
+
 /* ------------------------------------------------------------------------
  * Adversarial loss (losses.py:5-21 bce_loss; gan_d_loss :36-49 sums two of
  * them, gan_g_loss :24-33 is one), shard-weighted:

@@ -892,6 +892,112 @@ def test_deferred_grad_finish_is_bit_identical(graph):
         assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
 
 
+@pytest.mark.parametrize("graph,sizes", [("gat", [20, 7, 13, 20, 4]), ("gat", [20, 7, 13, 20, 2]),
+                                         ("gcn", [64, 30, 2])])
+def test_shared_prefix_is_bit_identical(graph, sizes):
+    """The discriminator encoder's observed steps run once beside the
+    generator's encoder (kernels.SharedPrefix: sgg_lstm_fwd_seg2, the
+    suffix from step obs_len by sgg_lstm_fwd_seg, the D-step backward through
+    sgg_lstm_bwd_shared) against the full 20-step sequences: losses and every
+    gradient of a D-step and a G-step bit-identical.  B = 64 takes the shared
+    path in both steps; B = 62 (not a multiple of 16) only in the G-step."""
+    import contextlib
+    from sgan import kernels as K
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, KernelOps
+    batch = synthetic_batch(sizes, seed=5, device=DEV)
+    sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+    seen = []
+
+    class Probe(KernelOps):
+        @staticmethod
+        @contextlib.contextmanager
+        def shared_prefix(*a):
+            with K.shared_prefix(*a) as p:
+                yield p
+            seen.append((p.ok, p.ran, p.used))
+
+    class Full(KernelOps):
+        shared_prefix = None
+    res = []
+    for ops in (Probe(), Full()):
+        g, d = build_models(graph)
+        tr = GanTrainer(g, d, ops=ops)
+        torch.manual_seed(3)
+        random.seed(3)
+        out = {}
+        ld = tr.d_step(batch, sc)
+        out.update({"d." + k: p.grad.detach().clone() for k, p in d.named_parameters() if p.grad is not None})
+        lg = tr.g_step(batch, sc)
+        out.update({"g." + k: p.grad.detach().clone() for k, p in g.named_parameters() if p.grad is not None})
+        out.update({"loss." + k: torch.tensor(float(v)) for k, v in list(ld.items()) + list(lg.items())})
+        res.append(out)
+    B = sum(sizes)
+    assert seen == [(B % 16 == 0, B % 16 == 0, B % 16 == 0), (True, True, True)], seen
+    a, b = res
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+
+
+def test_lstm_segments_equal_full_sequence():
+    """C ABI: a 3-copy batch whose first 5 steps are shared -- prefix on 32
+    peds beside another encoder in one launch (sgg_lstm_fwd_seg2), suffix on
+    96 peds (sgg_lstm_fwd_seg, t0 = 5, Bsrc = 32), backward with weight
+    gradients (sgg_lstm_bwd_shared) -- against sgg_lstm_fwd / sgg_lstm_bwd of
+    the full sequence: h, U, drel_in and the slab bit-identical."""
+    from sgan import _native as N
+    lib = N.load()
+    torch.manual_seed(2)
+    T, T0, Bs, C, H, NU = 11, 5, 32, 3, 48, 64
+    B = Bs * C
+    f = lambda *s, sc=0.3: (torch.randn(*s, device=DEV) * sc).contiguous()
+    A, Whh, bias = f(4 * H, 2), f(4 * H, H, sc=0.2), f(4 * H)
+    Wu, cu = f(NU, H), f(NU)
+    head = f(T0, Bs, 2)
+    rel = torch.cat([head.repeat(1, C, 1), f(T - T0, B, 2)], 0).contiguous()
+    sf = lambda w: torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, w)), device=DEV)
+    P = 4 * H * H + 4 * H + 8 * H
+    rows = int(lib.sgg_lstm_wpart_rows(H, B))
+    dh_last = f(B, H)
+
+    def run(shared):
+        h_all, c_all, act = torch.empty(T + 1, B, H, device=DEV), sf(1), sf(0)
+        U = torch.empty(B, NU, device=DEV)
+        if shared:
+            # another encoder (H = 32, 32 peds, 5 steps) in the same launch as the prefix
+            A2, W2, b2 = f(128, 2), f(128, 32, sc=0.2), f(128)
+            h2 = torch.empty(T0 + 1, Bs, 32, device=DEV)
+            g2 = N.LstmSeg(N.ptr(head), N.ptr(A2), N.ptr(W2), N.ptr(b2), None, None, T0, Bs, Bs, 0, T0, Bs,
+                           N.ptr(h2), None, None, None, 0, None, 0, None)
+            pre = N.LstmSeg(N.ptr(head), N.ptr(A), N.ptr(Whh), N.ptr(bias), None, None, T0, Bs, B, 0, T, Bs,
+                            N.ptr(h_all), N.ptr(c_all), N.ptr(act), None, 0, None, 0, None)
+            N.check(lib.sgg_lstm_fwd_seg2(N.ctypes.byref(g2), 32, N.ctypes.byref(pre), H, N.stream_ptr()), "seg2")
+            suf = N.LstmSeg(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), None, None, T - T0, B, B, T0, T, Bs,
+                            N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu), Wu.stride(0), N.ptr(cu), NU, N.ptr(U))
+            N.check(lib.sgg_lstm_fwd_seg(N.ctypes.byref(suf), H, N.stream_ptr()), "seg")
+        else:
+            N.check(lib.sgg_lstm_fwd_u(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), None, None, T, B, H,
+                                       N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu), Wu.stride(0), N.ptr(cu),
+                                       NU, N.ptr(U), N.stream_ptr()), "fwd_u")
+        drel = torch.empty(T, B, 2, device=DEV)
+        wpart = torch.empty(rows, P, device=DEV)
+        if shared:
+            N.check(lib.sgg_lstm_bwd_shared(N.ptr(A), N.ptr(Whh), N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel),
+                                            N.ptr(dh_last), T, B, H, T0, Bs, N.ptr(drel), N.ptr(wpart),
+                                            N.stream_ptr()), "bwd_shared")
+        else:
+            N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), None, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel),
+                                     None, N.ptr(dh_last), None, T, B, H, 0, None, None, N.ptr(drel), None,
+                                     N.ptr(wpart), N.stream_ptr()), "bwd")
+        torch.cuda.synchronize()
+        return h_all[T0 + 1:].clone(), U, drel, wpart
+
+    for x, y, nm in zip(run(True), run(False), ("h", "U", "drel_in", "slab")):
+        assert torch.equal(x, y), (nm, (x - y).abs().max().item())
+
+
 def test_step_glue_kernels_match_torch():
     """glue.hip (sgg_traj_cat, sgg_decoder_init, sgg_l2_select,
     sgg_l2_loss_fwd/bwd) against the reference's torch expressions
