@@ -1060,7 +1060,7 @@ class _GatEnc(torch.autograd.Function):
     the inter GAT, out_embedding weight, bias -- the slab order of sgg.h."""
 
     @staticmethod
-    def forward(ctx, x, labels, scenes, nh, alpha, x2, link, dy_link, *params):
+    def forward(ctx, x, labels, scenes, nh, alpha, x2, link, dy_link, save, *params):
         lib = _lib()
         ctx.link = link
         ctx.dy_link = dy_link
@@ -1074,7 +1074,7 @@ class _GatEnc(torch.autograd.Function):
         a = _gatenc_args(x, labels, scenes, nh, alpha, ps, x2)
         a.y, a.ldy = N.ptr(y), 24
         saved = None
-        if any(ctx.needs_input_grad) and GATENC_SAVE:
+        if save and any(ctx.needs_input_grad) and GATENC_SAVE:
             nf = int(lib.sgg_gatenc_saved_floats(max(scenes.S, 1), a.np, nh))
             saved = torch.empty(max(nf, 1), device=x.device, dtype=torch.float32)
             a.saved = N.ptr(saved)
@@ -1136,7 +1136,7 @@ class _GatEnc(torch.autograd.Function):
         if ctx.link is not None and ctx.needs_input_grad[0]:
             ctx.link.put(dx)   # added by the pooling backward (the other consumer of x), which runs next
             dx = None
-        return (dx, None, None, None, None, dx2, None, None) + tuple(grads)
+        return (dx, None, None, None, None, dx2, None, None, None) + tuple(grads)
 
 
 def _gatenc_flops(scenes, nh):
@@ -1190,7 +1190,9 @@ def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None, link=None):
     (x's other consumer, the pooling net, adds it in its own backward)."""
     lab = _req(labels, "labels").contiguous().view(-1)
     dl = CopiesLink() if torch.is_grad_enabled() else None
-    y = _GatEnc.apply(x, lab, scenes, nh, alpha, x2, link, dl, *params)
+    # the forward state is saved only when a backward can follow (not under
+    # no_grad, e.g. the generator inside the discriminator step)
+    y = _GatEnc.apply(x, lab, scenes, nh, alpha, x2, link, dl, torch.is_grad_enabled(), *params)
     if dl is not None:
         y._sgg_copies_link = dl   # found by decoder_init (its only consumer in the generator)
     return y

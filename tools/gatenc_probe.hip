@@ -6,6 +6,9 @@
 //     -I group-gan-gcn-gat_amd/csrc -I include tools/gatenc_probe.hip -o gatenc_probe
 #include "../group-gan-gcn-gat_amd/csrc/gat_encoder.hip"
 #include "../group-gan-gcn-gat_amd/csrc/runtime.hip"
+#ifndef SGG_GATENC_PROF
+namespace sgg { __device__ long long g_gatenc_prof[2][64]; }   // (the un-instrumented build: launch times only)
+#endif
 
 #include <cstdio>
 #include <cstdlib>
@@ -92,6 +95,8 @@ int main(int argc, char** argv) {
     const long long t0 = pr[bwd][40];
     printf("  staged %.2f  scene-start %.2f\n", (pr[bwd][41] - t0) * 0.01, (pr[bwd][0] - t0) * 0.01);
     long long prev = pr[bwd][0];
+    if (!bwd && pr[0][53] > pr[0][52])
+      printf("  shader clock %.2f GHz (F1..F7)\n", (double)(pr[0][51] - pr[0][50]) / ((pr[0][53] - pr[0][52]) * 10.0));
     for (int i = 1; i < 31; ++i) {
       if (pr[bwd][i] <= 0 || pr[bwd][i] < t0) continue;
       printf("  mark %2d  %7.2f  (+%.2f)\n", i, (pr[bwd][i] - t0) * 0.01, (pr[bwd][i] - prev) * 0.01);

@@ -31,4 +31,8 @@ print(d['roofline']['kernel'] if '$leg' == 'head' else legs['$leg']['roofline'][
   done
   python $R/tools/pmc_traffic.py $O/pmc_${leg}_fetch $O/pmc_${leg}_write $O/pmc_${leg}_fetch.json $O/pmc_traffic.json || { echo TRAFFIC_FAIL $leg; exit 1; }
 done
+# keep what is judged, drop the raw traces (gpurun copies back <= 64 MiB)
+python $R/tools/ktrace_iter.py $O/prof > $O/iteration_trace.txt 2>&1 || true
+cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv
+rm -rf $O/prof $O/pmc_*_fetch $O/pmc_*_write
 echo done
