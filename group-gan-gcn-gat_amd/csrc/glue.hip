@@ -242,6 +242,35 @@ __global__ void __launch_bounds__(256) l2_loss_bwd_kernel(const float* __restric
   }
 }
 
+// sgg_l2_loss_bwd_scenes: one 64-lane workgroup per scene forms the scene's
+// mask sum as l2_terms_kernel does (same per-lane order, the same bits as the
+// forward's msum), then the scene's rows of dpred with l2_loss_bwd_kernel's
+// expression
+__global__ void __launch_bounds__(64) l2_loss_bwd_scenes_kernel(const float* __restrict__ pred, int ldp,
+                                                                const float* __restrict__ gt,
+                                                                const float* __restrict__ mask, int ldm,
+                                                                const int32_t* __restrict__ scene_off, int T, int B,
+                                                                float w, const float* __restrict__ gout,
+                                                                float* __restrict__ dpred, int ldd,
+                                                                float* __restrict__ term) {
+  __shared__ float msk[kL2MaxElems];
+  const int lane = threadIdx.x, s = blockIdx.x;
+  const int o = scene_off[s], n = scene_off[s + 1] - o;
+  float acc, ms;
+  l2_scene(pred, ldp, reinterpret_cast<const float2*>(gt), mask, ldm, o, n, T, B, msk, lane, acc, ms);
+  if (term && lane == 0) term[s] = ms > 0.f ? (w * acc) / ms : 0.f;   // (l2_terms_kernel's value)
+  const float g = *gout * w * -2.f;
+  const float2* g2 = reinterpret_cast<const float2*>(gt);
+  for (int e = lane; e < n * T; e += 64) {
+    const int t = e / n, p = o + (e - t * n);
+    const float m = mask[(size_t)p * ldm + t];
+    const float2 gv = g2[(size_t)t * B + p];
+    const float2 q = *reinterpret_cast<const float2*>(pred + (size_t)t * ldp + 2 * p);
+    const float c = ms > 0.f ? g * m / ms : 0.f;
+    *reinterpret_cast<float2*>(dpred + (size_t)t * ldd + 2 * p) = make_float2(c * (gv.x - q.x), c * (gv.y - q.y));
+  }
+}
+
 int grid_for(long long n, int per) {
   const long long g = (n + per - 1) / per;
   return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
@@ -312,4 +341,16 @@ extern "C" int sgg_l2_loss_bwd(const float* pred, int ldp, const float* gt, cons
   hipLaunchKernelGGL(l2_loss_bwd_kernel, dim3(grid_for((long long)T * B, 256)), dim3(256), 0, (hipStream_t)stream,
                      pred, ldp, gt, mask, ldm, ped_scene, msum, T, B, w, gout, dpred, ldd);
   SGG_RETURN_LAUNCH("sgg_l2_loss_bwd");
+}
+
+extern "C" int sgg_l2_loss_bwd_scenes(const float* pred, int ldp, const float* gt, const float* mask, int ldm,
+                                      const int32_t* scene_off, int S, int T, int B, float w, const float* gout,
+                                      float* dpred, int ldd, float* term, void* stream) {
+  SGG_CHECK_ARG(pred && gt && mask && scene_off && gout && dpred, "sgg_l2_loss_bwd_scenes: null pointer");
+  SGG_CHECK_ARG(S >= 0 && T >= 1 && B >= 0 && ldm >= T && ldp >= 2 * B && ldd >= 2 * B,
+                "sgg_l2_loss_bwd_scenes: bad sizes");
+  if (S == 0) return 0;
+  hipLaunchKernelGGL(l2_loss_bwd_scenes_kernel, dim3(S), dim3(64), 0, (hipStream_t)stream, pred, ldp, gt, mask, ldm,
+                     scene_off, T, B, w, gout, dpred, ldd, term);
+  SGG_RETURN_LAUNCH("sgg_l2_loss_bwd_scenes");
 }

@@ -35,7 +35,10 @@ constexpr int kRedJobs = SGG_RED_MAX + 2 * SGG_FOLDB_MAX;   // + each fold's (dA
 struct FinishArgs {
   SggRed red[kRedJobs];
   int nred;
-  int blk0[kRedJobs + 1];   // first workgroup of red job j; blk0[nred] = the grid
+  int blk0[kRedJobs + 1];   // first workgroup of red job j (after the loss workgroup, if any); blk0[nred]: end
+  SggL2Job l2[SGG_LOSSJOB_MAX];
+  SggBceJob bce[SGG_LOSSJOB_MAX];
+  int nl2, nbce;
 };
 
 __device__ __forceinline__ float phase_sum(const float* __restrict__ src, int rows, int ld, int col, int ph) {
@@ -72,11 +75,123 @@ __device__ void red_job(const SggRed& d, int blk, float (*rpart)[64]) {
   }
 }
 
-// workgroups = the red jobs' 64-column blocks (1024 threads: 64 columns x 16
-// row phases)
+// ---- the loss values' workgroup (sgg_grad_finish_losses) -------------------
+constexpr int kLossThreads = 1024;
+constexpr int kLossMaxScores = 8 * kLossThreads;
+
+// *loss = the scene terms summed in scene order by lane-strided partials and a
+// shuffle tree (l2_sum_kernel's form); the value is also left in *lv (LDS)
+// for a BCE job's addend
+__device__ void l2_value(const SggL2Job& d, float* lv) {
+  if (threadIdx.x < 64) {
+    float a = 0.f;
+    for (int s = threadIdx.x; s < d.S; s += 64) a += d.term[s];
+    a = wave_sum(a);
+    if (threadIdx.x == 0) {
+      *d.loss = a;
+      *lv = a;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float bce_term(float x, float y) {   // as loss.hip
+  return fmaxf(x, 0.f) - x * y + logf(1.f + expf(-fabsf(x)));
+}
+
+// a BCE job's inputs, loaded before the L2 jobs run (one round trip for all)
+struct BceIn {
+  float v[8], a, b;
+  int nv;
+};
+__device__ __forceinline__ void bce_load(const SggBceJob& d, BceIn& in) {
+  in.a = *d.ya;
+  in.b = *d.yb;
+  in.nv = d.nvalid ? *d.nvalid : d.n;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int i = threadIdx.x + kLossThreads * m;
+    in.v[m] = i < d.n ? d.x[i] : 0.f;
+  }
+}
+
+// *loss = w (mean_{i < split} f(x_i, ya) + mean_{i >= split} f(x_i, yb)) over
+// the first nvalid scores of each half; *total = *loss + addend (addend: an
+// L2 job's value from LDS when it is that job's loss, else *d.addend)
+__device__ void bce_value(const SggBceJob& d, const BceIn& in, float addend, float (*red)[kLossThreads / 64]) {
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int i = threadIdx.x + kLossThreads * m;
+    const bool live = i < d.split ? i < in.nv : i - d.split < in.nv;
+    if (i < d.n && live) {
+      if (i < d.split) s0 += bce_term(in.v[m], in.a);
+      else s1 += bce_term(in.v[m], in.b);
+    }
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = s0;
+    red[1][wave] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < kLossThreads / 64; ++w) {
+      t0 += red[0][w];
+      t1 += red[1][w];
+    }
+    const int c0 = min(d.split, in.nv), c1 = min(d.n - d.split, in.nv);
+    const float m0 = c0 > 0 ? t0 / (float)c0 : 0.f;
+    const float m1 = c1 > 0 ? t1 / (float)c1 : 0.f;
+    const float l = d.w * (m0 + m1);
+    *d.loss = l;
+    if (d.total) *d.total = l + addend;
+  }
+  __syncthreads();
+}
+
+__device__ void loss_workgroup(const FinishArgs& a, float (*rpart)[64]) {
+  __shared__ float lv[SGG_LOSSJOB_MAX];
+  BceIn in[SGG_LOSSJOB_MAX];
+#pragma unroll
+  for (int j = 0; j < SGG_LOSSJOB_MAX; ++j)
+    if (j < a.nbce) bce_load(a.bce[j], in[j]);
+  // an addend that is not an L2 job's value: read with the inputs
+  float ad[SGG_LOSSJOB_MAX];
+#pragma unroll
+  for (int j = 0; j < SGG_LOSSJOB_MAX; ++j) {
+    ad[j] = 0.f;
+    if (j < a.nbce && a.bce[j].total) {
+      bool fromL2 = false;
+      for (int k = 0; k < a.nl2; ++k) fromL2 |= a.bce[j].addend == a.l2[k].loss;
+      if (!fromL2) ad[j] = *a.bce[j].addend;
+    }
+  }
+  for (int k = 0; k < a.nl2; ++k) l2_value(a.l2[k], lv + k);
+#pragma unroll
+  for (int j = 0; j < SGG_LOSSJOB_MAX; ++j)
+    if (j < a.nbce) {
+      float addend = ad[j];
+      for (int k = 0; k < a.nl2; ++k)
+        if (a.bce[j].total && a.bce[j].addend == a.l2[k].loss) addend = lv[k];
+      bce_value(a.bce[j], in[j], addend, reinterpret_cast<float(*)[kLossThreads / 64]>(&rpart[0][0]));
+    }
+}
+
+// workgroups = (with loss jobs) the loss workgroup, then the red jobs' 64-column
+// blocks (1024 threads: 64 columns x 16 row phases)
 __global__ void __launch_bounds__(1024) grad_finish_kernel(FinishArgs a) {
   __shared__ float rpart[16][64];
-  const int b = blockIdx.x;
+  const int lw = a.nl2 + a.nbce > 0;   // (the loss workgroup is block 0: dispatched first, beside the row sums)
+  const int b = (int)blockIdx.x - lw;
+  if (b < 0) {   // the loss values: every L2 job, then every BCE job (an addend may be an L2 loss)
+    loss_workgroup(a, rpart);
+    return;
+  }
   int j = 0;
   while (j + 1 < a.nred && b >= a.blk0[j + 1]) ++j;
   red_job(a.red[j], b - a.blk0[j], rpart);
@@ -90,6 +205,26 @@ using namespace sgg;
 
 extern "C" int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* folds, int nfold, float* scratch,
                                size_t scratch_bytes, void* stream) {
+  return sgg_grad_finish_losses(reds, nred, folds, nfold, scratch, scratch_bytes, nullptr, 0, nullptr, 0, stream);
+}
+
+extern "C" int sgg_grad_finish_losses(const SggRed* reds, int nred, const SggFoldBwd* folds, int nfold,
+                                      float* scratch, size_t scratch_bytes, const SggL2Job* l2, int nl2,
+                                      const SggBceJob* bce, int nbce, void* stream) {
+  SGG_CHECK_ARG(nl2 >= 0 && nl2 <= SGG_LOSSJOB_MAX && nbce >= 0 && nbce <= SGG_LOSSJOB_MAX &&
+                    (nl2 == 0 || l2) && (nbce == 0 || bce),
+                "sgg_grad_finish_losses: 0 <= nl2, nbce <= %d (got %d, %d)", SGG_LOSSJOB_MAX, nl2, nbce);
+  for (int j = 0; j < nl2; ++j) {
+    const SggL2Job& d = l2[j];
+    SGG_CHECK_ARG(d.loss && (d.S == 0 || d.term) && d.S >= 0, "sgg_grad_finish_losses: bad L2 job %d", j);
+  }
+  for (int j = 0; j < nbce; ++j) {
+    const SggBceJob& d = bce[j];
+    SGG_CHECK_ARG(d.ya && d.yb && d.loss && (d.n == 0 || d.x) && (!d.total || d.addend),
+                  "sgg_grad_finish_losses: null pointer in BCE job %d", j);
+    SGG_CHECK_ARG(d.n >= 0 && d.n <= kLossMaxScores && d.split >= 0 && d.split <= d.n,
+                  "sgg_grad_finish_losses: BCE job %d: %d scores (<= %d) / bad split", j, d.n, kLossMaxScores);
+  }
   SGG_CHECK_ARG(nred >= 0 && nred <= SGG_RED_MAX && nfold >= 0 && nfold <= SGG_FOLDB_MAX,
                 "sgg_grad_finish: 0 <= nred <= %d, 0 <= nfold <= %d (got %d, %d)", SGG_RED_MAX, SGG_FOLDB_MAX, nred,
                 nfold);
@@ -135,6 +270,11 @@ extern "C" int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* f
     blk += (a.red[j].cols + 63) / 64;
   }
   a.blk0[nj] = blk;
+  for (int j = 0; j < nl2; ++j) a.l2[j] = l2[j];
+  for (int j = 0; j < nbce; ++j) a.bce[j] = bce[j];
+  a.nl2 = nl2;
+  a.nbce = nbce;
+  if (nl2 + nbce > 0) ++blk;   // the loss workgroup
   hipStream_t st = (hipStream_t)stream;
   if (blk > 0) hipLaunchKernelGGL(grad_finish_kernel, dim3(blk), dim3(1024), 0, st, a);
   if (nfold > 0) {   // the fold backwards on the summed (dA, dbias), one workgroup each

@@ -85,6 +85,20 @@ class FoldBwd(ctypes.Structure):
                 ("dW", _p), ("lddw", _i), ("dWe", _p), ("dbe", _p), ("dbias_copy", _p)]
 
 
+LOSSJOB_MAX = 2   # SGG_LOSSJOB_MAX
+
+
+class L2Job(ctypes.Structure):
+    """SggL2Job (include/sgg.h): an L2 loss value of sgg_grad_finish_losses."""
+    _fields_ = [("term", _p), ("S", _i), ("loss", _p)]
+
+
+class BceJob(ctypes.Structure):
+    """SggBceJob (include/sgg.h): a BCE loss value of sgg_grad_finish_losses."""
+    _fields_ = [("x", _p), ("n", _i), ("split", _i), ("ya", _p), ("yb", _p), ("w", _f), ("loss", _p),
+                ("addend", _p), ("total", _p), ("nvalid", _p)]
+
+
 # name -> (restype, argtypes); must mirror include/sgg.h exactly
 SIGNATURES = {
     "sgg_version": (_i, []),
@@ -117,6 +131,8 @@ SIGNATURES = {
     "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _p, _i, _f, _p, _p]),
     "sgg_xtw_partial": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
+    "sgg_grad_finish_losses": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz,
+                                    ctypes.POINTER(L2Job), _i, ctypes.POINTER(BceJob), _i, _p]),
     "sgg_adam_parts": (_i, [ctypes.c_longlong]),
     "sgg_adam_step": (_i, [_p, _p, _p, _p, _p, _i, ctypes.c_double, ctypes.c_double, ctypes.c_double, _f, _f, _p, _p,
                           _sz, _p]),
@@ -149,6 +165,7 @@ SIGNATURES = {
     "sgg_l2_select": (_i, [_p, _p, _p, _i, _p, _i, _i, _i, _i, _p, _p]),
     "sgg_l2_loss_fwd": (_i, [_p, _i, _p, _p, _i, _p, _i, _i, _i, _f, _p, _p, _p, _p]),
     "sgg_l2_loss_bwd": (_i, [_p, _i, _p, _p, _i, _p, _p, _i, _i, _f, _p, _p, _i, _p]),
+    "sgg_l2_loss_bwd_scenes": (_i, [_p, _i, _p, _p, _i, _p, _i, _i, _i, _f, _p, _p, _i, _p, _p]),
 }
 
 _lib = None

@@ -393,6 +393,42 @@ class GradFinish:
 
 _DEFER = [0]
 _PENDING = []
+# loss VALUES queued inside defer_grad_finish() (SggL2Job / SggBceJob): the
+# training step only reports them, so they are formed in the flush's row-sum
+# launch (one extra workgroup) instead of launches of their own
+_LOSS = {"l2": [], "bce": [], "keep": [], "out": set()}
+_BCE_DEFER_MAX_SCORES = 8192   # sgg_grad_finish_losses' limit
+
+
+DEFER_LOSSES = os.environ.get("SGG_DEFER_LOSSES", "1") != "0"
+
+
+def _loss_deferrable():
+    return DEFER_LOSSES and _DEFER[0] > 0 and len(_LOSS["l2"]) + len(_LOSS["bce"]) < 2 * N.LOSSJOB_MAX
+
+
+def _queue_loss(kind, job, keep, outs):
+    _LOSS[kind].append(job)
+    _LOSS["keep"] += [t.untyped_storage() for t in keep if t is not None]
+    _LOSS["out"].update(t.data_ptr() for t in outs)
+
+
+def _loss_pending(t):
+    """Is t a queued (not yet written) loss value?"""
+    return t is not None and t.data_ptr() in _LOSS["out"]
+
+
+def _take_losses():
+    l2, bce, keep = _LOSS["l2"], _LOSS["bce"], _LOSS["keep"]
+    _LOSS.update(l2=[], bce=[], keep=[], out=set())
+    return l2, bce, keep
+
+
+def flush_losses():
+    """Form the queued loss values now (their own one-workgroup launch)."""
+    l2, bce, keep = _take_losses()
+    if l2 or bce:
+        _finish_launch([], [], keep, l2, bce)
 
 
 @contextlib.contextmanager
@@ -413,7 +449,10 @@ def defer_grad_finish():
 
 def grad_flush():
     """Issue every queued GradFinish (in queue order, as few sgg_grad_finish
-    calls as the job limits allow)."""
+    calls as the job limits allow); the queued loss values ride in the last
+    one."""
+    if not _PENDING:
+        flush_losses()
     while _PENDING:
         reds, folds, keep = [], [], []
         while _PENDING and len(reds) + len(_PENDING[0].reds) <= N.RED_MAX \
@@ -424,21 +463,28 @@ def grad_flush():
             keep += gf.keep
         if not reds and not folds:   # one op alone over the limits: cannot happen (each op is within them)
             raise N.NativeError("grad_flush: a queued finish exceeds the job limits")
-        _finish_launch(reds, folds, keep)
+        l2, bce = [], []
+        if not _PENDING:
+            l2, bce, lkeep = _take_losses()
+            keep = keep + lkeep
+        _finish_launch(reds, folds, keep, l2, bce)
 
 
-def _finish_launch(reds_l, folds_l, keep):
+def _finish_launch(reds_l, folds_l, keep, l2_l=(), bce_l=()):
     lib = _lib()
     assert len(reds_l) <= N.RED_MAX and len(folds_l) <= N.FOLDB_MAX
+    assert len(l2_l) <= N.LOSSJOB_MAX and len(bce_l) <= N.LOSSJOB_MAX
     reds = (N.Red * max(1, len(reds_l)))(*reds_l)
     folds = (N.FoldBwd * max(1, len(folds_l)))(*folds_l)
-    nr, nf = len(reds_l), len(folds_l)
+    l2 = (N.L2Job * max(1, len(l2_l)))(*l2_l)
+    bce = (N.BceJob * max(1, len(bce_l)))(*bce_l)
+    nr, nf, nl, nb = len(reds_l), len(folds_l), len(l2_l), len(bce_l)
     dev = keep[0].device
     scratch = torch.empty(max(1, sum(3 * f.R for f in folds_l)), device=dev, dtype=torch.float32)
 
-    def launch(reds=reds, folds=folds, nr=nr, nf=nf, keep=list(keep)):
-        N.check(lib.sgg_grad_finish(reds, nr, folds, nf, N.ptr(scratch), scratch.numel() * 4, N.stream_ptr()),
-                "sgg_grad_finish")
+    def launch(reds=reds, folds=folds, nr=nr, nf=nf, l2=l2, bce=bce, nl=nl, nb=nb, keep=list(keep)):
+        N.check(lib.sgg_grad_finish_losses(reds, nr, folds, nf, N.ptr(scratch), scratch.numel() * 4, l2, nl, bce, nb,
+                                           N.stream_ptr()), "sgg_grad_finish")
     launch()
     if timer.active:
         nb = sum(4.0 * r.rows * r.cols for r in reds_l) + sum(4.0 * 3 * f.R * max(f.dA_rows, f.db_rows)
@@ -1823,8 +1869,12 @@ class _Bce(torch.autograd.Function):
         ctx.bce_link = getattr(x, "_sgg_bce_link", None)
         x = _req(x, "scores").contiguous().view(-1)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
-        N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss), None,
-                                   None, N.ptr(nvalid), N.stream_ptr()), "sgg_bce_fwd")
+        if _loss_deferrable() and x.numel() <= _BCE_DEFER_MAX_SCORES:   # formed with the weight gradients
+            _queue_loss("bce", N.BceJob(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss), None,
+                                        None, N.ptr(nvalid)), (x, ya, yb, loss, nvalid), (loss,))
+        else:
+            N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
+                                       None, None, N.ptr(nvalid), N.stream_ptr()), "sgg_bce_fwd")
         ctx.meta = (split, float(w), nvalid)
         ctx.save_for_backward(x, ya, yb)
         return loss
@@ -1881,8 +1931,15 @@ class _BceTotal(torch.autograd.Function):
         addend = _req(addend, "addend").reshape(())
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         total = torch.empty((), device=x.device, dtype=torch.float32)
-        N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
-                                   N.ptr(addend), N.ptr(total), N.ptr(nvalid), N.stream_ptr()), "sgg_bce_fwd")
+        if _loss_deferrable() and x.numel() <= _BCE_DEFER_MAX_SCORES:   # after a queued L2 addend, in one workgroup
+            _queue_loss("bce", N.BceJob(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
+                                        N.ptr(addend), N.ptr(total), N.ptr(nvalid)),
+                        (x, ya, yb, loss, addend, total, nvalid), (loss, total))
+        else:
+            if _loss_pending(addend):   # the addend is a queued value: form it first
+                flush_losses()
+            N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
+                                       N.ptr(addend), N.ptr(total), N.ptr(nvalid), N.stream_ptr()), "sgg_bce_fwd")
         ctx.meta = (split, float(w), nvalid)
         ctx.save_for_backward(x, ya, yb)
         ctx.set_materialize_grads(False)
@@ -2028,24 +2085,41 @@ class _L2Loss(torch.autograd.Function):
         gt = _req(gt, "gt").contiguous()
         T, B = gt.shape[0], gt.shape[1]
         loss = torch.empty((), device=pred.device, dtype=torch.float32)
-        msum = torch.empty(scenes.S, device=pred.device, dtype=torch.float32)
-        term = torch.empty(scenes.S, device=pred.device, dtype=torch.float32)
-        N.check(_lib().sgg_l2_loss_fwd(N.ptr(pred), pred.stride(0), N.ptr(gt), N.ptr(mask), mask.stride(0),
-                                       N.ptr(scenes.scene_off), scenes.S, T, B, float(w), N.ptr(loss), N.ptr(msum),
-                                       N.ptr(term), N.stream_ptr()), "sgg_l2_loss_fwd")
-        ctx.save_for_backward(pred, gt, mask, msum)
+        term = None
+        if _loss_deferrable():
+            # the backward forms the mask sums and the per-scene terms itself
+            # (sgg_l2_loss_bwd_scenes); the value is their sum, formed with the
+            # weight gradients (SggL2Job) -- inside the trainer's step, whose
+            # backward always runs
+            term = torch.empty(max(scenes.S, 1), device=pred.device, dtype=torch.float32)
+            _queue_loss("l2", N.L2Job(N.ptr(term), scenes.S, N.ptr(loss)), (term, loss), (loss,))
+            msum = None
+        else:
+            msum = torch.empty(scenes.S, device=pred.device, dtype=torch.float32)
+            term = torch.empty(scenes.S, device=pred.device, dtype=torch.float32)
+            N.check(_lib().sgg_l2_loss_fwd(N.ptr(pred), pred.stride(0), N.ptr(gt), N.ptr(mask), mask.stride(0),
+                                           N.ptr(scenes.scene_off), scenes.S, T, B, float(w), N.ptr(loss),
+                                           N.ptr(msum), N.ptr(term), N.stream_ptr()), "sgg_l2_loss_fwd")
+        ctx.save_for_backward(pred, gt, mask, msum, term)
         ctx.meta = (scenes, float(w))
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        pred, gt, mask, msum = ctx.saved_tensors
+        pred, gt, mask, msum, term = ctx.saved_tensors
         scenes, w = ctx.meta
         T, B = gt.shape[0], gt.shape[1]
         dpred = torch.empty(T, B, 2, device=pred.device, dtype=torch.float32)
-        N.check(_lib().sgg_l2_loss_bwd(N.ptr(pred), pred.stride(0), N.ptr(gt), N.ptr(mask), mask.stride(0),
-                                       N.ptr(scenes.ped_scene_i32()), N.ptr(msum), T, B, w, N.ptr(g.contiguous()),
-                                       N.ptr(dpred), 2 * B, N.stream_ptr()), "sgg_l2_loss_bwd")
+        if msum is None:   # (the value was queued: the scenes' mask sums are formed here)
+            N.check(_lib().sgg_l2_loss_bwd_scenes(N.ptr(pred), pred.stride(0), N.ptr(gt), N.ptr(mask), mask.stride(0),
+                                                  N.ptr(scenes.scene_off), scenes.S, T, B, w, N.ptr(g.contiguous()),
+                                                  N.ptr(dpred), 2 * B, N.ptr(term), N.stream_ptr()),
+                    "sgg_l2_loss_bwd_scenes")
+        else:
+            N.check(_lib().sgg_l2_loss_bwd(N.ptr(pred), pred.stride(0), N.ptr(gt), N.ptr(mask), mask.stride(0),
+                                           N.ptr(scenes.ped_scene_i32()), N.ptr(msum), T, B, w,
+                                           N.ptr(g.contiguous()), N.ptr(dpred), 2 * B, N.stream_ptr()),
+                    "sgg_l2_loss_bwd")
         return dpred, None, None, None, None
 
 

@@ -283,6 +283,42 @@ typedef struct {
 int sgg_grad_finish(const SggRed* reds, int nred, const SggFoldBwd* folds, int nfold, float* scratch,
                     size_t scratch_bytes, void* stream);
 
+/* Loss VALUES of a training step, formed in the row-sum launch of
+ * sgg_grad_finish (one extra workgroup) instead of launches of their own: in
+ * the step the values are only reported (the gradients come from the
+ * backward kernels), so they are due with the weight gradients, before the
+ * optimizer and the data-parallel all-reduce.
+ * SggL2Job: *loss = the value of sgg_l2_loss_fwd (the best-of-k L2 term,
+ *   train.py:459-464): the sum in scene order of the per-scene terms
+ *   w * masked SE / mask sum that sgg_l2_loss_bwd_scenes wrote (term != NULL)
+ *   in the backward -- no second pass over the predictions.
+ * SggBceJob: *loss = the value of sgg_bce_fwd (gan_d_loss / gan_g_loss,
+ *   losses.py:24-49), *total = *loss + *addend when total != NULL.
+ * The workgroup runs every L2 job, then every BCE job (an addend may be an L2
+ * job's loss).  The sums keep the separate kernels' orders (bit-identical
+ * values). */
+#define SGG_LOSSJOB_MAX 2
+typedef struct {
+  const float* term;
+  int S;
+  float* loss;
+} SggL2Job;
+typedef struct {
+  const float* x;
+  int n;
+  int split;
+  const float* ya;
+  const float* yb;
+  float w;
+  float* loss;
+  const float* addend;
+  float* total;
+  const int32_t* nvalid;
+} SggBceJob;
+int sgg_grad_finish_losses(const SggRed* reds, int nred, const SggFoldBwd* folds, int nfold, float* scratch,
+                           size_t scratch_bytes, const SggL2Job* l2, int nl2, const SggBceJob* bce, int nbce,
+                           void* stream);
+
 /* ------------------------------------------------------------------------
  * The discriminator's scoring head real_classifier = make_mlp([K, N1, 1])
  * (models.py:958-965 with make_mlp :7-20, applied at :991):
@@ -690,6 +726,14 @@ int sgg_l2_loss_fwd(const float* pred, int ldp, const float* gt, const float* ma
                     int S, int T, int B, float w, float* loss, float* msum, float* term_ws, void* stream);
 int sgg_l2_loss_bwd(const float* pred, int ldp, const float* gt, const float* mask, int ldm, const int32_t* ped_scene,
                     const float* msum, int T, int B, float w, const float* gout, float* dpred, int ldd, void* stream);
+/* sgg_l2_loss_bwd without the forward: one workgroup per scene forms the
+ * scene's masked squared error and mask sum (sgg_l2_loss_fwd's order) and
+ * writes the scene's rows of dpred and, when term != NULL, the scene's loss
+ * term (sgg_l2_loss_fwd's term_ws values), which a SggL2Job of
+ * sgg_grad_finish_losses sums into the loss value. */
+int sgg_l2_loss_bwd_scenes(const float* pred, int ldp, const float* gt, const float* mask, int ldm,
+                           const int32_t* scene_off, int S, int T, int B, float w, const float* gout, float* dpred,
+                           int ldd, float* term, void* stream);
 
 /* ------------------------------------------------------------------------
  * Device-resident data path (sgan/data/device.py): a split's peds live in
