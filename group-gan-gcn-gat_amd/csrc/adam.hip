@@ -148,13 +148,27 @@ __global__ void __launch_bounds__(kAdamThreads) adam_prep_kernel(AdamList L, int
   if (threadIdx.x == 0) partial[blockIdx.x] = s;
 }
 
+// fused (no clipping): the step scalars are formed here from step + 1 (lane t
+// of every wave: tensor t, adam_prep's expressions), and the LAST workgroup to
+// finish -- an atomic ticket in ws, left at 0 -- writes the incremented step
+// counters: every workgroup has read them (and used the values) before
+// taking its ticket, so none sees the new value.  One launch instead of two.
 __global__ void __launch_bounds__(kAdamThreads) adam_update_kernel(AdamList L, int nparts, float max_norm,
                                                                    const float* __restrict__ partial,
                                                                    const float* __restrict__ scal, float beta2,
-                                                                   float w1, float w2, float eps) {
+                                                                   float w1, float w2, float eps,
+                                                                   unsigned* __restrict__ ticket, double lr,
+                                                                   double beta1d, double beta2d) {
   __shared__ float red[kAdamThreads / 64];
+  __shared__ int last;
   const long long e0 = (long long)blockIdx.x * kAdamChunk;
   const Tab T = lane_tab(L);
+  float tstep = 0.f, lss = 0.f, lbc = 1.f;   // fused: lane t's step + 1 and step scalars
+  if (ticket && (int)(threadIdx.x & 63) < L.n) {
+    tstep = L.step[threadIdx.x & 63][0] + 1.f;
+    lss = (float)(lr / (1.0 - pow(beta1d, (double)tstep)));
+    lbc = (float)sqrt(1.0 - pow(beta2d, (double)tstep));
+  }
   int ek[kAdamPer];
   long long ei[kAdamPer];
   chunk_elems(L, T, e0, ek, ei);
@@ -178,8 +192,13 @@ __global__ void __launch_bounds__(kAdamThreads) adam_update_kernel(AdamList L, i
     gp[u] = reinterpret_cast<float*>(shfl64(T.g, k)) + i;
     mp[u] = reinterpret_cast<float*>(shfl64(T.m, k)) + i;
     vp[u] = reinterpret_cast<float*>(shfl64(T.v, k)) + i;
-    ss[u] = scal[2 * k];
-    bc[u] = scal[2 * k + 1];
+    if (ticket) {
+      ss[u] = __shfl(lss, k);
+      bc[u] = __shfl(lbc, k);
+    } else {
+      ss[u] = scal[2 * k];
+      bc[u] = scal[2 * k + 1];
+    }
   }
   // every load of the thread's elements first, then the updates
 #pragma unroll
@@ -203,15 +222,26 @@ __global__ void __launch_bounds__(kAdamThreads) adam_update_kernel(AdamList L, i
     *vp[u] = vi;
     *pp[u] = p0[u] + -ss[u] * (mi / (sqrtf(vi) / bc[u] + eps));   // addcdiv_(m, denom, -step_size)
   }
+  if (ticket) {
+    __syncthreads();   // (every lane's step read has been consumed above)
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (last) {
+      if ((int)threadIdx.x < L.n) L.step[threadIdx.x][0] = tstep;
+      if (threadIdx.x == 0) *ticket = 0u;
+    }
+  }
 }
 
 }  // namespace sgg
 
 using namespace sgg;
 
-// workspace floats: one partial per workgroup + 2 step scalars per tensor
+// workspace floats: one partial per workgroup + 2 step scalars per tensor +
+// the fused launch's ticket (zero when the workspace is first used; every
+// call leaves it at zero)
 extern "C" int sgg_adam_parts(long long total) {
-  return (int)((total + kAdamChunk - 1) / kAdamChunk) + 2 * kAdamMaxTensors;
+  return (int)((total + kAdamChunk - 1) / kAdamChunk) + 2 * kAdamMaxTensors + 1;
 }
 
 extern "C" int sgg_adam_step(float* const* params, float* const* grads, float* const* exp_avg,
@@ -233,15 +263,18 @@ extern "C" int sgg_adam_step(float* const* params, float* const* grads, float* c
     L.step[i] = step[i];
     L.off[i + 1] = L.off[i] + numel[i];
   }
-  const int parts = sgg_adam_parts(L.off[n]) - 2 * kAdamMaxTensors;
+  const int parts = sgg_adam_parts(L.off[n]) - 2 * kAdamMaxTensors - 1;
   if (parts == 0) return 0;
   const int clip = max_norm > 0.f;
-  SGG_CHECK_ARG(ws && ws_bytes >= sizeof(float) * ((size_t)parts + 2 * kAdamMaxTensors), "sgg_adam_step: workspace");
+  SGG_CHECK_ARG(ws && ws_bytes >= sizeof(float) * ((size_t)parts + 2 * kAdamMaxTensors + 1),
+                "sgg_adam_step: workspace");
   hipStream_t st = (hipStream_t)stream;
   float* scal = ws + parts;
-  hipLaunchKernelGGL(adam_prep_kernel, dim3(clip ? parts : 1), dim3(kAdamThreads), 0, st, L, clip, ws, scal, lr,
-                     beta1, beta2);
+  unsigned* ticket = reinterpret_cast<unsigned*>(scal + 2 * kAdamMaxTensors);
+  if (clip)   // the norm's partials need every workgroup: a launch of their own
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(parts), dim3(kAdamThreads), 0, st, L, clip, ws, scal, lr, beta1, beta2);
   hipLaunchKernelGGL(adam_update_kernel, dim3(parts), dim3(kAdamThreads), 0, st, L, parts, clip ? max_norm : 0.f,
-                     ws, scal, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps);
+                     ws, scal, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps, clip ? nullptr : ticket,
+                     lr, beta1, beta2);
   SGG_RETURN_LAUNCH("sgg_adam_step");
 }

@@ -77,7 +77,6 @@ __device__ void red_job(const SggRed& d, int blk, float (*rpart)[64]) {
 
 // ---- the loss values' workgroup (sgg_grad_finish_losses) -------------------
 constexpr int kLossThreads = 1024;
-constexpr int kLossMaxScores = 8 * kLossThreads;
 
 // *loss = the scene terms summed in scene order by lane-strided partials and a
 // shuffle tree (l2_sum_kernel's form); the value is also left in *lv (LDS)
@@ -127,6 +126,13 @@ __device__ void bce_value(const SggBceJob& d, const BceIn& in, float addend, flo
     if (i < d.n && live) {
       if (i < d.split) s0 += bce_term(in.v[m], in.a);
       else s1 += bce_term(in.v[m], in.b);
+    }
+  }
+  for (int i = threadIdx.x + 8 * kLossThreads; i < d.n; i += kLossThreads) {   // past the prefetched scores
+    const bool live = i < d.split ? i < in.nv : i - d.split < in.nv;
+    if (live) {
+      if (i < d.split) s0 += bce_term(d.x[i], in.a);
+      else s1 += bce_term(d.x[i], in.b);
     }
   }
   s0 = wave_sum(s0);
@@ -222,8 +228,7 @@ extern "C" int sgg_grad_finish_losses(const SggRed* reds, int nred, const SggFol
     const SggBceJob& d = bce[j];
     SGG_CHECK_ARG(d.ya && d.yb && d.loss && (d.n == 0 || d.x) && (!d.total || d.addend),
                   "sgg_grad_finish_losses: null pointer in BCE job %d", j);
-    SGG_CHECK_ARG(d.n >= 0 && d.n <= kLossMaxScores && d.split >= 0 && d.split <= d.n,
-                  "sgg_grad_finish_losses: BCE job %d: %d scores (<= %d) / bad split", j, d.n, kLossMaxScores);
+    SGG_CHECK_ARG(d.n >= 0 && d.split >= 0 && d.split <= d.n, "sgg_grad_finish_losses: BCE job %d: bad sizes", j);
   }
   SGG_CHECK_ARG(nred >= 0 && nred <= SGG_RED_MAX && nfold >= 0 && nfold <= SGG_FOLDB_MAX,
                 "sgg_grad_finish: 0 <= nred <= %d, 0 <= nfold <= %d (got %d, %d)", SGG_RED_MAX, SGG_FOLDB_MAX, nred,

@@ -397,7 +397,6 @@ _PENDING = []
 # training step only reports them, so they are formed in the flush's row-sum
 # launch (one extra workgroup) instead of launches of their own
 _LOSS = {"l2": [], "bce": [], "keep": [], "out": set()}
-_BCE_DEFER_MAX_SCORES = 8192   # sgg_grad_finish_losses' limit
 
 
 DEFER_LOSSES = os.environ.get("SGG_DEFER_LOSSES", "1") != "0"
@@ -761,7 +760,7 @@ class ClipAdam:
         total = sum(p.numel() for p in act)
         parts = lib.sgg_adam_parts(total)
         if self._ws is None or self._ws.numel() < parts:
-            self._ws = torch.empty(parts, device=act[0].device, dtype=torch.float32)
+            self._ws = torch.zeros(parts, device=act[0].device, dtype=torch.float32)   # (the ticket word: 0)
         b1, b2 = grp["betas"]
         N.check(lib.sgg_adam_step(arr(act), arr([p.grad for p in act]), arr([s["exp_avg"] for s in st]),
                                   arr([s["exp_avg_sq"] for s in st]), numel, n, float(grp["lr"]), float(b1),
@@ -1869,7 +1868,7 @@ class _Bce(torch.autograd.Function):
         ctx.bce_link = getattr(x, "_sgg_bce_link", None)
         x = _req(x, "scores").contiguous().view(-1)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
-        if _loss_deferrable() and x.numel() <= _BCE_DEFER_MAX_SCORES:   # formed with the weight gradients
+        if _loss_deferrable():   # formed with the weight gradients
             _queue_loss("bce", N.BceJob(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss), None,
                                         None, N.ptr(nvalid)), (x, ya, yb, loss, nvalid), (loss,))
         else:
@@ -1931,13 +1930,13 @@ class _BceTotal(torch.autograd.Function):
         addend = _req(addend, "addend").reshape(())
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         total = torch.empty((), device=x.device, dtype=torch.float32)
-        if _loss_deferrable() and x.numel() <= _BCE_DEFER_MAX_SCORES:   # after a queued L2 addend, in one workgroup
+        if _loss_deferrable():   # after a queued L2 addend, in the same workgroup
             _queue_loss("bce", N.BceJob(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
                                         N.ptr(addend), N.ptr(total), N.ptr(nvalid)),
                         (x, ya, yb, loss, addend, total, nvalid), (loss, total))
         else:
-            if _loss_pending(addend):   # the addend is a queued value: form it first
-                flush_losses()
+            if _loss_pending(addend):   # (a queued L2 value exists only after the backward)
+                raise N.NativeError("bce total: the addend is a queued loss value")
             N.check(_lib().sgg_bce_fwd(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
                                        N.ptr(addend), N.ptr(total), N.ptr(nvalid), N.stream_ptr()), "sgg_bce_fwd")
         ctx.meta = (split, float(w), nvalid)

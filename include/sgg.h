@@ -534,8 +534,9 @@ int sgg_bce_bwd(const float* x, int n, int split, const float* ya, const float* 
  * tensor's device fp32 step counter (torch's capturable Adam state['step']),
  * incremented first (host arrays of n <= 48 pointers).  max_norm <= 0: no clipping; otherwise the
  * clipped gradient is written back, as clip_grad_norm_ does.  ws holds
- * sgg_adam_parts(sum numel) floats (partial norms + per-tensor step scalars).
- * Two launches, graph-capturable. */
+ * sgg_adam_parts(sum numel) floats (partial norms + per-tensor step scalars +
+ * a ticket word that must be zero when ws is first used; every call leaves
+ * it at zero).  Two launches with clipping, one without; graph-capturable. */
 int sgg_adam_parts(long long total);
 int sgg_adam_step(float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
                   const long long* numel, int n, double lr, double beta1, double beta2, float eps, float max_norm,
