@@ -391,11 +391,16 @@ class GraphedTrainer:
     device)."""
 
     def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2, batch_g=None,
-                 sc_g=None, draw=None, prologue=None):
+                 sc_g=None, draw=None, prologue=None, iters=1):
         """draw: () -> (z_d, z_g, y) host tensors of the staging shapes (default:
         trainer.draw_inputs over this rank's span); prologue: launches captured
-        ahead of the step (the padded real-data path's batch gathers)."""
+        ahead of the step (the padded real-data path's batch gathers).
+        iters (one rank): iterations per graph -- a replay runs `iters`
+        consecutive iterations on the same batches (their host draws made in
+        order before it), so the per-replay graph launch is paid once per
+        `iters` iterations; step() then advances `iters` iterations."""
         self.t = trainer
+        self.iters = iters = max(1, int(iters))
         self.prologue = prologue or (lambda: None)
         self.batch, self.sc = batch, sc
         self.batch_g, self.sc_g = batch_g, sc_g
@@ -415,14 +420,18 @@ class GraphedTrainer:
         # copy is still pending
         shp = [(sc.S,) + (nd or ()), (k, sc.S) + (nd or ()), (3,)] if nd else [(3,)]
         sizes = [int(np.prod(x)) for x in shp]
+        per = sum(sizes)   # floats per iteration; iteration j's block at j * per
         views = lambda flat: [flat[o:o + n].view(x) for o, n, x in zip(np.cumsum([0] + sizes[:-1]), sizes, shp)]
-        self.stage_flat = [torch.empty(sum(sizes)).pin_memory() for _ in range(2)]
-        self.stage = [tuple(views(f)) if nd else (None, None, views(f)[0]) for f in self.stage_flat]
+        blocks = lambda flat: [views(flat[j * per:(j + 1) * per]) for j in range(iters)]
+        self.stage_flat = [torch.empty(iters * per).pin_memory() for _ in range(2)]
+        self.stage = [[tuple(v) if nd else (None, None, v[0]) for v in blocks(f)] for f in self.stage_flat]
         self.stage_ev = [None, None]
         self.cur = 0
-        self.inp_flat = torch.zeros(sum(sizes), device=dev)
-        dv = views(self.inp_flat)
-        self.inp = StepInputs(dv[0], dv[1], dv[2]) if nd else StepInputs(None, None, dv[0])
+        self.inp_flat = torch.zeros(iters * per, device=dev)
+        self.inps = [StepInputs(v[0], v[1], v[2]) if nd else StepInputs(None, None, v[0]) for v in blocks(self.inp_flat)]
+        self.inp = self.inps[0]
+        if iters > 1 and trainer.dp.on and trainer.dp.world > 1:
+            raise ValueError("GraphedTrainer: iters > 1 needs one rank (the collectives cut the graph)")
         # warm-up and capture on the same side stream: the parameters'
         # AccumulateGrad nodes (created by the first backward, kept alive by
         # the captured graph) are bound to the stream that created them
@@ -462,8 +471,9 @@ class GraphedTrainer:
                     g = torch.cuda.CUDAGraph()
                     g.capture_begin(pool=torch.cuda.graph_pool_handle())
                     self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
-                    self.prologue()
-                    losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
+                    for j in range(iters):
+                        self.prologue()
+                        losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inps[j], **self.kw)
                     g.capture_end()
                 self.pair.append((g, losses, [(p, p.grad) for p in params]))
             torch.cuda.current_stream().wait_stream(cap)
@@ -501,7 +511,7 @@ class GraphedTrainer:
         self.cur ^= 1
         if self.stage_ev[i] is not None:
             self.stage_ev[i].synchronize()        # that set's previous copies are done
-        h_zd, h_zg, h_y = self.stage[i]
+        h_zd, h_zg, h_y = self.stage[i][0]
         if z_d is not None:
             h_zd.copy_(z_d)
         if z_g is not None:
@@ -520,13 +530,14 @@ class GraphedTrainer:
             self.cur ^= 1
             if self.done_ev[i] is not None:
                 self.done_ev[i].synchronize()     # graph i's previous replay has read buffer i
-            z_d, z_g, y = self.draw()
-            h_zd, h_zg, h_y = self.stage[i]
-            if z_d is not None:
-                h_zd.copy_(z_d)
-            if z_g is not None:
-                h_zg.copy_(z_g)
-            h_y.copy_(y)
+            for j in range(self.iters):           # the replay's iterations' draws, in order
+                z_d, z_g, y = self.draw()
+                h_zd, h_zg, h_y = self.stage[i][j]
+                if z_d is not None:
+                    h_zd.copy_(z_d)
+                if z_g is not None:
+                    h_zg.copy_(z_g)
+                h_y.copy_(y)
             g, self.losses, grads = self.pair[i]
             g.replay()
             ev = torch.cuda.Event()

@@ -748,6 +748,43 @@ def test_graphed_trainer_equals_eager(replays):
     assert (sa - sb).abs().max().item() <= 1e-5 + 1e-5 * sa.abs().max().item(), "eager D forward after replays"
 
 
+def test_graphed_trainer_multi_iteration_equals_eager():
+    """A graph of two iterations (GraphedTrainer(iters=2), the bench's form:
+    the per-replay launch paid once per two iterations) replayed twice ==
+    four eager iterations: the host draws of both iterations are made in
+    order before each replay."""
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, GraphedTrainer
+    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
+    batch_g = synthetic_batch([20, 7, 13, 20, 2], seed=4, device=DEV)
+    res = []
+    for graphed in (False, True):
+        g, d = build_models()
+        tr = GanTrainer(g, d, capturable=True)
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
+        torch.manual_seed(11)
+        random.seed(11)
+        if graphed:
+            gt = GraphedTrainer(tr, batch, sc, warmup=1, batch_g=batch_g, sc_g=scg, iters=2)
+            for _ in range(2):
+                ld, lg = gt.step()
+        else:
+            for _ in range(5):
+                ld, lg = tr.step(batch, sc, batch_g, scg)
+        torch.cuda.synchronize()
+        ws = {"g." + k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
+        ws.update({"d." + k: v.detach().cpu().clone() for k, v in d.state_dict().items()})
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws))
+    (la, wa), (lb, wb) = res
+    for k in la:
+        assert abs(la[k] - lb[k]) <= 1e-5 * max(1.0, abs(la[k])), (k, la[k], lb[k])
+    for k in wa:
+        err = (wa[k] - wb[k]).abs().max().item()
+        assert err <= 1e-5 + 1e-5 * wa[k].abs().max().item(), (k, err)
+
+
 @pytest.mark.parametrize("nh,sizes", [(1, [1, 2, 20, 48, 13, 5]), (1, [20] * 70), (2, [20, 7, 24, 1])])
 def test_gat_encoder_fused_equals_per_layer(nh, sizes):
     """The one-launch GATEncoder (sgg_gatenc_fwd / _bwd + sgg_slab_reduce)
