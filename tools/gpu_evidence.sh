@@ -18,7 +18,7 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -3 $O/smoke.log
 timeout -k 10 400 python bench.py --steps 100 --warmup 10 > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-real-data --no-scaling-reference > $O/prof_bench.json 2> $O/prof.err || { echo PROF_FAIL; tail -20 $O/prof.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-real-data --no-scaling-reference --no-legs > $O/prof_bench.json 2> $O/prof.err || { echo PROF_FAIL; tail -20 $O/prof.err; exit 1; }
 for leg in head configs3_shard512 configs2_gcn_fp32 configs2_gcn_bf16 configs4_sgangat_bf16; do
   K=$(python -c "
 import json; d = json.loads(open('$O/bench.json').read().strip().splitlines()[-1])
