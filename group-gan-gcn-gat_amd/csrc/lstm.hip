@@ -395,6 +395,30 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   }
 }
 
+extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias,
+                                const float* Wp, const float* bp, int T, int B, int H, float* h_all, float* c_all,
+                                float* act_all, float* rel_out, float* rel0_out, void* stream) {
+  SGG_CHECK_ARG(di && di->ctx && di->ped_scene && di->last_rel && (di->nz == 0 || di->z) && A && Whh && bias &&
+                    h_all && c_all && Wp && bp && rel_out,
+                "sgg_lstm_fwd_dec: null pointer");
+  SGG_CHECK_ARG(T >= 1 && B >= 0 && di->Bper >= 1 && B % di->Bper == 0 && di->Dc >= 1 && di->nz >= 0 &&
+                    di->Dc + di->nz == H && di->ldc >= di->Dc && di->S >= 1,
+                "sgg_lstm_fwd_dec: bad sizes (T=%d B=%d Bper=%d Dc=%d nz=%d H=%d)", T, B, di->Bper, di->Dc, di->nz, H);
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const bool mw = lstm_mw_ok(H, B);
+  if (act_all && mw)
+    return lstm_mw_fwd(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, act_all, rel_out,
+                       st, nullptr, 0, nullptr, 0, nullptr, di, rel0_out);
+  if (!act_all && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
+    return lstm_fwd_mfma(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, nullptr, rel_out,
+                         st, di);
+  if (!act_all && mw)
+    return lstm_mw_fwd(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, nullptr, rel_out, st,
+                       nullptr, 0, nullptr, 0, nullptr, di, nullptr);
+  SGG_CHECK_ARG(false, "sgg_lstm_fwd_dec: no fused decoder start for H=%d B=%d (use sgg_decoder_init)", H, B);
+}
+
 extern "C" int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,
                             const float* act_all, const float* rel, const float* rel_out, const float* dh_last,
                             const float* dout, int T, int B, int H, int decoder, float* dG, float* dh0,

@@ -45,7 +45,8 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
     const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
-    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out) {
+    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out,
+    SggDecInit di) {
   constexpr int G4 = 4 * H;
   constexpr int MT = G4 / 16;     // gate-row tiles
   constexpr int MU = H / 16;      // unit tiles (i/f/g/o blocks are MU tiles apart)
@@ -85,7 +86,12 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
   for (int mu = 0; mu < MU; ++mu) {
     const size_t o = (size_t)ped * H + 16 * mu + 4 * q;
     float4 hv = make_float4(0.f, 0.f, 0.f, 0.f), cv = hv;
-    if (valid && h0) hv = *reinterpret_cast<const float4*>(h0 + o);
+    if (valid && di.ctx) {   // add_noise in the prologue (sgg_lstm_fwd_dec)
+      const int u = 16 * mu + 4 * q;
+      hv = make_float4(dec_h0(di, ped, u), dec_h0(di, ped, u + 1), dec_h0(di, ped, u + 2), dec_h0(di, ped, u + 3));
+    } else if (valid && h0) {
+      hv = *reinterpret_cast<const float4*>(h0 + o);
+    }
     if (valid && c0) cv = *reinterpret_cast<const float4*>(c0 + o);
     h[4 * mu] = hv.x; h[4 * mu + 1] = hv.y; h[4 * mu + 2] = hv.z; h[4 * mu + 3] = hv.w;
     c[4 * mu] = cv.x; c[4 * mu + 1] = cv.y; c[4 * mu + 2] = cv.z; c[4 * mu + 3] = cv.w;
@@ -98,6 +104,7 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
   auto load_in = [&](int t) -> float {
     if (q >= 2) return q == 2 ? 1.f : 0.f;
     if (!valid) return 0.f;
+    if (decoder && di.ctx) return dec_rel0(di, ped, q);
     return decoder ? rel[(size_t)ped * 2 + q] : rel[((size_t)t * B + ped) * 2 + q];
   };
   float xin = load_in(0);
@@ -162,10 +169,12 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
 template <int H>
 int launch(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0, const float* c0,
            const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
-           float* rel_out, hipStream_t st) {
+           float* rel_out, hipStream_t st, const SggDecInit* di) {
   const int grid = (B + 63) / 64;
+  SggDecInit d = {};
+  if (di) d = *di;
   hipLaunchKernelGGL(lstm_fwd_mfma_kernel<H>, dim3(grid), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B,
-                     decoder, h_all, c_all, act_all, rel_out);
+                     decoder, h_all, c_all, act_all, rel_out, d);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
 }
 
@@ -178,9 +187,10 @@ bool lstm_fwd_mfma_ok(int H, int B) { return H == 32 && B >= kLstmMfmaMinPeds; }
 
 int lstm_fwd_mfma(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
                   const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
-                  float* c_all, float* act_all, float* rel_out, hipStream_t st) {
-  if (H == 32) return launch<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
-  return launch<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st);
+                  float* c_all, float* act_all, float* rel_out, hipStream_t st, const SggDecInit* di) {
+  if (H == 32)
+    return launch<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st, di);
+  return launch<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st, di);
 }
 
 }  // namespace sgg

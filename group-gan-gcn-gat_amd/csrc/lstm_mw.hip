@@ -214,7 +214,7 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
       hv = h_all[((size_t)t0 * Bl + spc) * H + u];
       cv = c_tile[((((size_t)sblk * (Tl + 1) + t0) * 4 + g) * 64 + lane) * MU + i];
     } else {
-      hv = sg.h0 ? sg.h0[(size_t)pc * H + u] : 0.f;
+      hv = sg.di.ctx ? dec_h0(sg.di, pc, u) : sg.h0 ? sg.h0[(size_t)pc * H + u] : 0.f;
       cv = sg.c0 ? sg.c0[(size_t)pc * H + u] : 0.f;
       if (save) {
         h_all[(size_t)pc * H + u] = hv;
@@ -294,10 +294,12 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   // input k-step operand: r_x (q = 0), r_y (q = 1), 1 (q = 2), 0 (q = 3)
   // (loads unconditional, the constant lanes selected after)
   auto input = [&](int t) -> float {
-    const float v = decoder ? rel[(size_t)pc * 2 + (q & 1)] : relseq[t][c16][q & 1];
+    const float v = decoder ? (sg.di.ctx ? dec_rel0(sg.di, pc, q & 1) : rel[(size_t)pc * 2 + (q & 1)])
+                            : relseq[t][c16][q & 1];
     return q < 2 ? v : (q == 2 ? 1.f : 0.f);
   };
   float xin = input(0);
+  if (decoder && sg.rel0_out && g == 0 && q < 2) sg.rel0_out[(size_t)pc * 2 + q] = xin;   // (the backward's x_0)
   for (int t = 0; t < T; ++t) {
     if (decoder && t == 1) {
       // fold the hidden2pos feedback into the recurrence (see header)
@@ -886,10 +888,14 @@ int lstm_mw_wpart_rows(int H, int B) {
 int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
                 const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
                 float* c_all, float* act_all, float* rel_out, hipStream_t st, const float* Wu, int ldwu,
-                const float* cu, int NU, float* U) {
+                const float* cu, int NU, float* U, const SggDecInit* di, float* rel0_out) {
   SGG_CHECK_ARG(decoder || T <= kMwMaxT, "sgg_lstm_fwd: encoder sequences of the H=%d kernels hold <= %d steps (T=%d)",
                 H, kMwMaxT, T);
-  const MwSeg sg{rel, A, Whh, bias, h0, c0, Wp, bp, T, B, B, 0, T, B, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U};
+  MwSeg sg{rel, A, Whh, bias, h0, c0, Wp, bp, T, B, B, 0, T, B, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U};
+  if (di) {
+    sg.di = *di;
+    sg.rel0_out = rel0_out;
+  }
   return launch_seg_h(sg, H, decoder != 0, st);
 }
 

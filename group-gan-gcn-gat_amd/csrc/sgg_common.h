@@ -64,7 +64,8 @@ __attribute__((visibility("hidden"))) int lstm_fwd_mfma(const float* rel, const 
                                                         const float* bias, const float* h0, const float* c0,
                                                         const float* Wp, const float* bp, int T, int B, int H,
                                                         int decoder, float* h_all, float* c_all, float* act_all,
-                                                        float* rel_out, hipStream_t st);
+                                                        float* rel_out, hipStream_t st,
+                                                        const SggDecInit* di = nullptr);
 
 // lstm_unit.hip: unit-per-thread LSTM sequence kernels (one barrier per
 // step), dispatched by sgg_lstm_fwd / sgg_lstm_bwd; internal
@@ -92,7 +93,8 @@ __attribute__((visibility("hidden"))) int lstm_mw_fwd(const float* rel, const fl
                                                       int decoder, float* h_all, float* c_all, float* act_all,
                                                       float* rel_out, hipStream_t st, const float* Wu = nullptr,
                                                       int ldwu = 0, const float* cu = nullptr, int NU = 0,
-                                                      float* U = nullptr);
+                                                      float* U = nullptr, const SggDecInit* di = nullptr,
+                                                      float* rel0_out = nullptr);
 __attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp,
                                                       const float* h_all, const float* c_all, const float* act_all,
                                                       const float* rel, const float* rel_out, const float* dh_last,
@@ -110,7 +112,20 @@ struct MwSeg {
   const float* cu;
   int NU;
   float* U;
+  SggDecInit di;      // decoder: di.ctx != NULL builds h0 / rel0 in the prologue (sgg_lstm_fwd_dec)
+  float* rel0_out;    // (with di) receives rel0 when saving
 };
+// h0[p][u] and rel0[p][k] of a SggDecInit (sgg_decoder_init's values)
+__device__ __forceinline__ float dec_h0(const SggDecInit& d, int p, int u) {
+  const int r = p / d.Bper, i = p - r * d.Bper;
+  if (u < d.Dc) return d.ctx[(size_t)i * d.ldc + u];
+  const int s = d.ped_scene[i];
+  const int k = (d.best && r == 0) ? (int)d.best[s] : d.first_k + r - (d.best ? 1 : 0);
+  return d.z[((size_t)k * d.S + s) * d.nz + (u - d.Dc)];
+}
+__device__ __forceinline__ float dec_rel0(const SggDecInit& d, int p, int k) {
+  return d.last_rel[(size_t)(p % d.Bper) * 2 + k];
+}
 __attribute__((visibility("hidden"))) int lstm_mw_fwd_seg(const MwSeg& s, int H, hipStream_t st);
 __attribute__((visibility("hidden"))) int lstm_mw_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
                                                            hipStream_t st);

@@ -85,6 +85,12 @@ class FoldBwd(ctypes.Structure):
                 ("dW", _p), ("lddw", _i), ("dWe", _p), ("dbe", _p), ("dbias_copy", _p)]
 
 
+class DecInit(ctypes.Structure):
+    """SggDecInit (include/sgg.h): the decoder's h0 / rel0 built in the LSTM prologue."""
+    _fields_ = [("ctx", _p), ("ldc", _i), ("Dc", _i), ("z", _p), ("nz", _i), ("best", _p), ("first_k", _i),
+                ("ped_scene", _p), ("S", _i), ("Bper", _i), ("last_rel", _p)]
+
+
 LOSSJOB_MAX = 2   # SGG_LOSSJOB_MAX
 
 
@@ -131,6 +137,7 @@ SIGNATURES = {
     "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _p, _i, _f, _p, _p]),
     "sgg_xtw_partial": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
+    "sgg_lstm_fwd_dec": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
     "sgg_grad_finish_losses": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz,
                                     ctypes.POINTER(L2Job), _i, ctypes.POINTER(BceJob), _i, _p]),
     "sgg_adam_parts": (_i, [ctypes.c_longlong]),

@@ -1646,6 +1646,7 @@ class _LSTMSeq(torch.autograd.Function):
         if carry:
             pfx.ran = True
         kname = None
+        launch_done = False
         if carry:
             ga, gb = seg(0, T, B), pfx_seg
             kname = "sgg::lstm_mw_fwd2_kernel<32, %s, 48, true>" % ("true" if save else "false")
@@ -1668,7 +1669,31 @@ class _LSTMSeq(torch.autograd.Function):
                 N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c),
                                          N.ptr(Wpc), N.ptr(bp), T, B, H, int(decoder), N.ptr(h_all), N.ptr(c_all),
                                          N.ptr(act), N.ptr(rel_out), N.stream_ptr()), "sgg_lstm_fwd")
-        launch()
+            dinit = getattr(h0, "_sgg_dinit", None) if (decoder and h0 is not None and c0 is None) else None
+            if dinit is not None:
+                # the decoder's h0 / rel0 built in the kernel's prologue (one
+                # launch fewer); where no kernel takes it, materialise them first
+                di, dkeep, materialize = dinit
+                # the closure holds every buffer the descriptor and the
+                # arguments point to (the bench's timer re-issues it later)
+                fkeep = (dkeep, A, Whh, bias, Wpc, bp, h_all, c_all, act, rel_out, rel)
+                fused = lambda k=fkeep: lib.sgg_lstm_fwd_dec(N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias),
+                                                             N.ptr(Wpc), N.ptr(bp), T, B, H, N.ptr(h_all),
+                                                             N.ptr(c_all), N.ptr(act), N.ptr(rel_out),
+                                                             N.ptr(rel) if save else None, N.stream_ptr())
+                if fused() == 0:
+                    launch = lambda: N.check(fused(), "sgg_lstm_fwd_dec")
+                else:
+                    h0d, r0d = h0.detach(), rel
+                    materialize(h0d, r0d)
+                    plain = launch
+                    launch = lambda: (materialize(h0d, r0d), plain())
+                    plain()
+                launch_done = True
+            else:
+                launch_done = False
+        if not launch_done:
+            launch()
         if timer.active:
             # per ped-step: gates 2 4H (H + 3) FLOP + ~12 H cell / activation; bytes: inputs, saved states
             Ts = T - pfx.T_pre if cont else T    # the steps this launch runs
@@ -2029,9 +2054,14 @@ def traj_cat(head, a, b=None, pos0=None):
     return _TrajCat.apply(head, a, b, pos0)
 
 
+# the decoder's h0 / rel0 built in the decoder LSTM's prologue
+# (sgg_lstm_fwd_dec) instead of by a sgg_decoder_init launch; "0" disables
+DEC_INIT_FUSED = os.environ.get("SGG_DEC_INIT_FUSED", "1") != "0"
+
+
 class _DecoderInit(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cvec, z, best, first_k, copies, scenes, last_rel):
+    def forward(ctx, cvec, z, best, first_k, copies, scenes, last_rel, lazy):
         ctx.dy_link = getattr(cvec, "_sgg_copies_link", None)
         cvec = _rows(cvec, "ctx")
         B, Dc = cvec.shape
@@ -2039,10 +2069,28 @@ class _DecoderInit(torch.autograd.Function):
         h0 = torch.empty(copies * B, Dc + nz, device=cvec.device, dtype=torch.float32)
         rel0 = torch.empty(copies * B, 2, device=cvec.device, dtype=torch.float32)
         zc = _req(z, "z").contiguous() if z is not None else None
-        N.check(_lib().sgg_decoder_init(N.ptr(cvec), cvec.stride(0), Dc, N.ptr(zc), nz, N.ptr(best), int(first_k),
-                                        int(copies), N.ptr(scenes.ped_scene_i32()), scenes.S, B,
-                                        N.ptr(_req(last_rel, "last_rel").contiguous()), N.ptr(h0), N.ptr(rel0),
-                                        N.stream_ptr()), "sgg_decoder_init")
+        last = _req(last_rel, "last_rel").contiguous()
+        ps = scenes.ped_scene_i32()
+        args = (N.ptr(cvec), cvec.stride(0), Dc, N.ptr(zc), nz, N.ptr(best), int(first_k), int(copies), N.ptr(ps),
+                scenes.S, B, N.ptr(last), N.ptr(h0), N.ptr(rel0))
+
+        # every buffer the launches read, held by storage only (no autograd
+        # graph kept alive, no reference back to h0: a cycle through h0 would
+        # keep this iteration's graph alive into the next one)
+        keep = tuple(t.detach() for t in (cvec, zc, best, ps, last) if t is not None)
+
+        def materialize(h0_buf, rel0_buf, keep=keep):
+            N.check(_lib().sgg_decoder_init(*args[:-2], N.ptr(h0_buf), N.ptr(rel0_buf), N.stream_ptr()),
+                    "sgg_decoder_init")
+        if lazy:
+            # h0 / rel0 stay unwritten: the decoder LSTM (their one consumer)
+            # builds them in its prologue from this descriptor, or calls
+            # materialize(h0, rel0) first where its kernel family cannot
+            di = N.DecInit(N.ptr(cvec), cvec.stride(0), Dc, N.ptr(zc), nz, N.ptr(best), int(first_k), N.ptr(ps),
+                           scenes.S, B, N.ptr(last))
+            h0._sgg_dinit = (di, keep, materialize)
+        else:
+            materialize(h0, rel0)
         ctx.dims = (copies, B, Dc)
         ctx.mark_non_differentiable(rel0)
         ctx.set_materialize_grads(False)   # no zero-filled gradient for rel0
@@ -2055,15 +2103,17 @@ class _DecoderInit(torch.autograd.Function):
         if copies > 1 and ctx.dy_link is not None and dh0.is_contiguous():
             # the GAT encoder's backward sums the copies while loading dy
             ctx.dy_link.put(dh0, copies, B * dh0.shape[1], dh0.shape[1])
-            return d[0], None, None, None, None, None, None
-        return (d[0] if copies == 1 else d.sum(0)), None, None, None, None, None, None
+            return d[0], None, None, None, None, None, None, None
+        return (d[0] if copies == 1 else d.sum(0)), None, None, None, None, None, None, None
 
 
-def decoder_init(cvec, z, best, first_k, copies, scenes, last_rel):
+def decoder_init(cvec, z, best, first_k, copies, scenes, last_rel, lazy=False):
     """add_noise (global mix) + the decoder's first input for `copies` samples:
     z is (K, S, nz); copy r takes sample best[s] (r = 0, when best is given)
-    or first_k + r (- 1 with best).  -> (h0 (copies*B, Dc+nz), rel0)."""
-    return _DecoderInit.apply(cvec, z, best, first_k, copies, scenes, last_rel)
+    or first_k + r (- 1 with best).  -> (h0 (copies*B, Dc+nz), rel0).
+    lazy: h0 / rel0 are left for the decoder LSTM (lstm_sequence) to build in
+    its prologue -- pass them to nothing else."""
+    return _DecoderInit.apply(cvec, z, best, first_k, copies, scenes, last_rel, bool(lazy and DEC_INIT_FUSED))
 
 
 def l2_select(pred, gt, mask, scenes, k):

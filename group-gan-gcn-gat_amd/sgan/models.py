@@ -707,7 +707,7 @@ class TrajectoryGenerator(nn.Module):
             else:
                 (best, first_k), z = noise_index, user_noise
             z = z.to(noise_input.device, non_blocking=True)
-            h0, rel0 = K.decoder_init(noise_input, z, best, first_k, copies, sc, obs_traj_rel[-1])
+            h0, rel0 = K.decoder_init(noise_input, z, best, first_k, copies, sc, obs_traj_rel[-1], lazy=True)
             h, rel = K.lstm_sequence(rel0, self.decoder.decoder, self.decoder.spatial_embedding, h0=h0, c0=None,
                                      proj=self.decoder.hidden2pos, decoder=True, T=self.pred_len)
             return rel

@@ -398,6 +398,34 @@ int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float
                  const float* h0, const float* c0, const float* Wp, const float* bp, int T, int B, int H,
                  int decoder, float* h_all, float* c_all, float* act_all, float* rel_out,
                  void* stream);
+/* The decoder's initial state built in the sequence kernel's prologue
+ * instead of by sgg_decoder_init (add_noise, 'global' mix, models.py:827-850,
+ * and the decoder's first input, :909-925; one launch fewer per rollout):
+ * column p = r Bper + i (copy r, ped i) starts from
+ *   h0[p] = [ctx[i] (Dc floats, row stride ldc) | z[k][scene(i)] (nz floats)],
+ *   k = best[scene(i)] for r == 0 when best != NULL, else first_k + r - (best ? 1 : 0)
+ *   (z: K x S x nz), rel0[p] = last_rel[i];
+ * ped_scene: Bper int32 scene indices.  Everything else as sgg_lstm_fwd with
+ * decoder = 1, c0 = 0; rel0_out (may be NULL) receives rel0 (B x 2) -- the
+ * backward's first input -- when act_all != NULL.  Returns SGG_E_ARG where
+ * no kernel family takes the fused start (the caller then runs
+ * sgg_decoder_init + sgg_lstm_fwd). */
+typedef struct {
+  const float* ctx;
+  int ldc;
+  int Dc;
+  const float* z;
+  int nz;
+  const int64_t* best;
+  int first_k;
+  const int32_t* ped_scene;
+  int S;
+  int Bper;
+  const float* last_rel;
+} SggDecInit;
+int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias, const float* Wp,
+                     const float* bp, int T, int B, int H, float* h_all, float* c_all, float* act_all,
+                     float* rel_out, float* rel0_out, void* stream);
 
 /* Encoder sequence (decoder = 0) with the pooling MLP's h-half fused into the
  * kernel's epilogue (models.py:538): also writes U = h_T Wu^T + cu (B x NU,

@@ -6,6 +6,9 @@
 //     -I group-gan-gcn-gat_amd/csrc -I include tools/lstm_mw_probe.hip -o tools/lstm_mw_probe
 #include "../group-gan-gcn-gat_amd/csrc/lstm_mw.hip"
 #include "../group-gan-gcn-gat_amd/csrc/runtime.hip"
+#ifndef SGG_LSTM_PROF
+namespace sgg { __device__ long long g_lstm_prof[64]; }   // (the un-instrumented build: launch times only)
+#endif
 
 #include <cstdio>
 #include <cstdlib>
