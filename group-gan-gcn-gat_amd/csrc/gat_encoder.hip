@@ -161,6 +161,66 @@ __device__ inline void stage_weights(float* base, const StageTab& T, LW& lw) {
   }
 }
 
+// stage_weights for a kernel built for NH heads: only the NH-head table's
+// segments are looked up (fewer scalar registers than the 4-head table)
+template <int NH>
+__host__ __device__ constexpr int live_slot(int q) {
+  return q < 2 * NH ? q
+         : q < 2 * NH + 2 ? 2 * kGatEncMaxHeads + (q - 2 * NH)
+         : q < 4 * NH + 2 ? 2 * kGatEncMaxHeads + 2 + (q - 2 * NH - 2)
+                          : 4 * kGatEncMaxHeads + 2 + (q - 4 * NH - 2);
+}
+template <int NH>
+__device__ inline void stage_weights_t(float* base, const StageTab& T, LW& lw) {
+  constexpr int NL = 4 * NH + 6;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    lw.Wi[h] = base + T.dst[2 * h];
+    lw.ai[h] = base + T.dst[2 * h + 1];
+    lw.Wg[h] = base + T.dst[2 * kGatEncMaxHeads + 2 + 2 * h];
+    lw.ag[h] = base + T.dst[2 * kGatEncMaxHeads + 3 + 2 * h];
+  }
+  lw.Wio = base + T.dst[2 * kGatEncMaxHeads];
+  lw.aio = base + T.dst[2 * kGatEncMaxHeads + 1];
+  lw.Wgo = base + T.dst[4 * kGatEncMaxHeads + 2];
+  lw.ago = base + T.dst[4 * kGatEncMaxHeads + 3];
+  lw.Woe = base + T.dst[4 * kGatEncMaxHeads + 4];
+  lw.boe = base + T.dst[4 * kGatEncMaxHeads + 5];
+  for (int c = threadIdx.x; c < T.nchunks; c += blockDim.x) {
+    int q = 0;
+#pragma unroll
+    for (int k = 1; k < NL; ++k)
+      if (c >= T.coff[live_slot<NH>(k)]) q = k;
+    const float* sp = T.src[0];
+    int len = 0, dst = 0, N = 0, c0 = 0;
+#pragma unroll
+    for (int k = 0; k < NL; ++k)
+      if (q == k) {
+        const int sl = live_slot<NH>(k);
+        sp = T.src[sl];
+        len = T.len[sl];
+        dst = T.dst[sl];
+        N = T.rowN[sl];
+        c0 = T.coff[sl];
+      }
+    const int r0 = (c - c0) * kChunk;
+    float v[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u) v[u] = r0 + u < len ? sp[r0 + u] : 0.f;
+    int row = N ? r0 / N : 0, col = N ? r0 - row * N : r0;
+    int d = dst + (N ? row * (N + 1) + col : r0);
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u)
+      if (r0 + u < len) {
+        base[d++] = v[u];
+        if (N && ++col == N) {
+          col = 0;
+          ++d;
+        }
+      }
+  }
+}
+
 // int region of a scene: lab (float), gidl, grank, cnt, ginv (float), M, then
 // the groups' member masks (64-bit, 8-byte aligned)
 __host__ __device__ inline int gm_offset(int np) { return (5 * np + 4 + 1) & ~1; }
@@ -613,37 +673,12 @@ __device__ long long g_gatenc_prof[2][64];
 #define PMARK(i)
 #endif
 
-template <bool BWD>
+template <bool BWD, int NH>
 __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel(GatEncArgs p, StageTab tab) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const Layout L = make_layout(p.np, p.nh, BWD);
-  const PLayout PL = make_playout(p.nh);
-  const SLayout SL = make_slayout(p.np, p.nh);
-  const int nh = p.nh, PH = L.PH, NP = L.NP, NPP = L.NPP;
+  constexpr int nh = NH;
   // per-head strides of the weight image, the slab row and the saved state
   constexpr int SEGI = FI * PW72 + 2 * FH, SEGG = FO * PW72 + 2 * FH, PLI = FI * FH + 2 * FH, PLG = FO * FH + 2 * FH;
-  const int SLH = NP * FH + 2 * NP;
-  float* X = sm + L.X;
-  float* H1 = sm + L.H1;
-  float* yI = sm + L.yI;
-  float* preI = sm + L.preI;
-  float* gin = sm + L.gin;
-  float* G1 = sm + L.G1;
-  float* preG = sm + L.preG;
-  float* gout = sm + L.gout;
-  float* Wh = sm + L.Wh;
-  float* s = sm + L.s;
-  float* t = sm + L.t;
-  float* sp = sm + L.sp;
-  float* tp = sm + L.tp;
-  float* attm = sm + L.attm;
-  float* lab = sm + L.ints;
-  int* gidl = reinterpret_cast<int*>(lab + NP);
-  int* grank = gidl + NP;
-  int* cnt = grank + NP;
-  float* ginv = reinterpret_cast<float*>(cnt + NP);
-  int* Mp = reinterpret_cast<int*>(ginv + NP);
-  unsigned long long* gm = reinterpret_cast<unsigned long long*>(lab + gm_offset(NP));
   const int tid = threadIdx.x;
   // element e = r * FI + k of a scene's input rows (the split input: X2)
   auto xval = [&](int o, int e) -> float {
@@ -667,11 +702,41 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
   }
   PMARK(40);
   LW lw;
-  stage_weights(sm + L.wts, tab, lw);
+  stage_weights_t<NH>(sm + make_layout(p.np, NH, BWD).wts, tab, lw);
   // (the first scene's input stores are followed by a barrier before any use)
   PMARK(41);
 
   for (int sc = blockIdx.x; sc < p.S; sc += gridDim.x) {
+    // the LDS plan derived per scene from an opaque copy of np: hoisted out
+    // of the scene loop, the per-lane addresses spill to scratch
+    int NPo = p.np;
+    __asm__ volatile("" : "+s"(NPo));
+    const Layout L = make_layout(NPo, NH, BWD);
+    const PLayout PL = make_playout(NH);
+    const SLayout SL = make_slayout(NPo, NH);
+    const int PH = L.PH, NP = L.NP, NPP = L.NPP;
+    const int SLH = NP * FH + 2 * NP;
+    float* X = sm + L.X;
+    float* H1 = sm + L.H1;
+    float* yI = sm + L.yI;
+    float* preI = sm + L.preI;
+    float* gin = sm + L.gin;
+    float* G1 = sm + L.G1;
+    float* preG = sm + L.preG;
+    float* gout = sm + L.gout;
+    float* Wh = sm + L.Wh;
+    float* s = sm + L.s;
+    float* t = sm + L.t;
+    float* sp = sm + L.sp;
+    float* tp = sm + L.tp;
+    float* attm = sm + L.attm;
+    float* lab = sm + L.ints;
+    int* gidl = reinterpret_cast<int*>(lab + NP);
+    int* grank = gidl + NP;
+    int* cnt = grank + NP;
+    float* ginv = reinterpret_cast<float*>(cnt + NP);
+    int* Mp = reinterpret_cast<int*>(ginv + NP);
+    unsigned long long* gm = reinterpret_cast<unsigned long long*>(lab + gm_offset(NP));
     const int o = p.scene_off[sc];
     const int n = p.scene_off[sc + 1] - o;
     if (n <= 0) continue;   // uniform over the workgroup
@@ -1075,8 +1140,15 @@ extern "C" int sgg_gatenc_fwd(const GatEncArgs* args, void* stream) {
   if (rc) return rc;
   if (args->S == 0) return 0;
   const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 0);
-  hipLaunchKernelGGL(gatenc_kernel<false>, dim3(args->S < kGridCap ? args->S : kGridCap), dim3(kFwdThreads), lds,
-                     (hipStream_t)stream, *args, make_stage_tab(args->w, args->nh));
+  const dim3 grid(args->S < kGridCap ? args->S : kGridCap);
+  const StageTab tab = make_stage_tab(args->w, args->nh);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (args->nh) {
+    case 1: hipLaunchKernelGGL((gatenc_kernel<false, 1>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
+    case 2: hipLaunchKernelGGL((gatenc_kernel<false, 2>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
+    case 3: hipLaunchKernelGGL((gatenc_kernel<false, 3>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
+    default: hipLaunchKernelGGL((gatenc_kernel<false, 4>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
+  }
   SGG_RETURN_LAUNCH("sgg_gatenc_fwd");
 }
 
@@ -1085,8 +1157,15 @@ extern "C" int sgg_gatenc_bwd(const GatEncArgs* args, void* stream) {
   if (rc) return rc;
   if (args->S == 0) return 0;
   const size_t lds = (size_t)sgg_gatenc_lds_bytes(args->np, args->nh, 1);
-  hipLaunchKernelGGL(gatenc_kernel<true>, dim3(args->S < kGridCap ? args->S : kGridCap), dim3(kBwdThreads), lds,
-                     (hipStream_t)stream, *args, make_stage_tab(args->w, args->nh));
+  const dim3 grid(args->S < kGridCap ? args->S : kGridCap);
+  const StageTab tab = make_stage_tab(args->w, args->nh);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (args->nh) {
+    case 1: hipLaunchKernelGGL((gatenc_kernel<true, 1>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
+    case 2: hipLaunchKernelGGL((gatenc_kernel<true, 2>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
+    case 3: hipLaunchKernelGGL((gatenc_kernel<true, 3>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
+    default: hipLaunchKernelGGL((gatenc_kernel<true, 4>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
+  }
   SGG_RETURN_LAUNCH("sgg_gatenc_bwd");
 }
 
