@@ -234,6 +234,7 @@ struct Layout {
   // float offsets into the workgroup's LDS
   int X, H1, yI, preI, gin, G1, preG, gout, Wh, s, t, sp, tp, attm;   // forward
   int dWh, dH, dI, dG, dpre, dz, ds, dt;                             // backward
+  int WhIs, stIs, WhIOs, stIOs, WhGs, stGs, WhGOs, stGOs;              // backward: the saved layer state
   int ints;       // see ints_floats
   int wts;        // the module's weights, staged once per workgroup (odd row pitches)
   int total;      // floats
@@ -270,8 +271,26 @@ __host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
     L.dz = take(np * L.NPP);
     L.ds = take(np);
     L.dt = take(np);
+    // every layer's Wh and scores s | t, loaded with the inputs (one round
+    // trip per scene instead of one per layer) -- when they fit beside the
+    // rest of the plan (else 0: loaded per layer into the Wh scratch)
+    const int rest = ((ints_floats(np) + 3) & ~3) + ((weights_floats(nh) + 3) & ~3);
+    const int pre = 2 * (((nh * np * P72 + 3) & ~3) + ((nh * 2 * np + 3) & ~3) + ((np * P16 + 3) & ~3) + ((2 * np + 3) & ~3));
+    if (o + pre + rest <= 160 * 1024 / 4) {
+      L.WhIs = take(nh * np * P72);
+      L.stIs = take(nh * 2 * np);
+      L.WhIOs = take(np * P16);
+      L.stIOs = take(2 * np);
+      L.WhGs = take(nh * np * P72);
+      L.stGs = take(nh * 2 * np);
+      L.WhGOs = take(np * P16);
+      L.stGOs = take(2 * np);
+    } else {
+      L.WhIs = L.stIs = L.WhIOs = L.stIOs = L.WhGs = L.stGs = L.WhGOs = L.stGOs = 0;
+    }
   } else {
     L.dWh = L.dH = L.dI = L.dG = L.dpre = L.dz = L.ds = L.dt = 0;
+    L.WhIs = L.stIs = L.WhIOs = L.stIOs = L.WhGs = L.stGs = L.WhGOs = L.stGOs = 0;
   }
   L.ints = take(ints_floats(np));
   L.wts = take(weights_floats(nh));
@@ -759,9 +778,41 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         X[r * P40 + (e - r * FI)] = xval(o, e);
       }
     }
-    if (BWD && saved) {
-      rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
-    } else {
+    const bool preload = BWD && saved && L.WhIs > 0;   // uniform
+    if (BWD && saved) rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
+    if (preload) {
+      // the backward's whole input in ONE memory round trip: group structure,
+      // activations, every layer's Wh / scores (n rows: the group-side rows
+      // past M are never read), dy (+ its copies)
+      rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
+      rows_from_global(yI, P16, saved + SL.yI, n, FO);
+      rows_from_global(preI, P16, saved + SL.preI, n, FO);
+      rows_from_global(gin, P16, saved + SL.gin, n, FO);
+      rows_from_global(G1, PH, saved + SL.G1, n, FH * nh);
+      rows_from_global(preG, P16, saved + SL.preG, n, FO);
+      rows_from_global(gout, P16, saved + SL.gout, n, FO);
+      for (int h = 0; h < nh; ++h) {
+        rows_from_global(sm + L.WhIs + h * NP * P72, P72, saved + (SL.Whi[0] + h * SLH), n, FH);
+        rows_from_global(sm + L.stIs + h * 2 * NP, 0, saved + (SL.sti[0] + h * SLH), 1, 2 * NP);
+        rows_from_global(sm + L.WhGs + h * NP * P72, P72, saved + (SL.Whg[0] + h * SLH), n, FH);
+        rows_from_global(sm + L.stGs + h * 2 * NP, 0, saved + (SL.stg[0] + h * SLH), 1, 2 * NP);
+      }
+      rows_from_global(sm + L.WhIOs, P16, saved + SL.Whio, n, FO);
+      rows_from_global(sm + L.stIOs, 0, saved + SL.stio, 1, 2 * NP);
+      rows_from_global(sm + L.WhGOs, P16, saved + SL.Whgo, n, FO);
+      rows_from_global(sm + L.stGOs, 0, saved + SL.stgo, 1, 2 * NP);
+      {
+        constexpr int PDY = FE + 1;
+        const float* dyg = p.dy + (size_t)o * p.lddy;
+        const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
+        for (int e = tid; e < n * FE; e += blockDim.x) {
+          const int i = e / FE, k = e - i * FE;
+          float v = dyg[(size_t)i * p.lddy + k];
+          for (int c = 1; c < ncp; ++c) v += dyg[(size_t)c * p.dy_cstride + (size_t)i * p.lddy + k];
+          Wh[i * PDY + k] = v;   // dy (see below)
+        }
+      }
+    } else if (!(BWD && saved)) {
       // group structure (models.py:263-278) in ONE wave, lane = ped (n <= 64),
       // from the labels in global memory (no barrier after the X stores):
       // the lowest ungrouped ped leads the next group, its members are the
@@ -857,7 +908,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         rows_to_global(saved + SL.gout, gout, P16, M, FO);
         rows_to_global(saved + SL.ints, lab, 0, 1, ints_floats(NP));
       }
-    } else {
+    } else if (!preload) {
       // backward with the forward's saved state: no recompute
       rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
       rows_from_global(yI, P16, saved + SL.yI, n, FO);
@@ -867,7 +918,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       rows_from_global(preG, P16, saved + SL.preG, M, FO);
       rows_from_global(gout, P16, saved + SL.gout, M, FO);
       lds_barrier();
-    }
+    }   // (preload: everything came with the inputs)
 
     if (!BWD) {
       // ---- out = Woe [intra, gout[g(i)] / |g(i)|] + boe on the MFMA ------
@@ -917,13 +968,15 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     float* dy = Wh;
     float* v = Wh + NP * PDY;
     {
-      const float* dyg = p.dy + (size_t)o * p.lddy;
-      const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
-      for (int e = tid; e < n * FE; e += blockDim.x) {
-        const int i = e / FE, k = e - i * FE;
-        float v = dyg[(size_t)i * p.lddy + k];
-        for (int c = 1; c < ncp; ++c) v += dyg[(size_t)c * p.dy_cstride + (size_t)i * p.lddy + k];
-        dy[i * PDY + k] = v;
+      if (!preload) {   // (preload: dy came with the inputs)
+        const float* dyg = p.dy + (size_t)o * p.lddy;
+        const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
+        for (int e = tid; e < n * FE; e += blockDim.x) {
+          const int i = e / FE, k = e - i * FE;
+          float v = dyg[(size_t)i * p.lddy + k];
+          for (int c = 1; c < ncp; ++c) v += dyg[(size_t)c * p.dy_cstride + (size_t)i * p.lddy + k];
+          dy[i * PDY + k] = v;
+        }
       }
       for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
         const int i = e / (2 * FO), c = e - i * 2 * FO;
@@ -956,7 +1009,15 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     lds_barrier(); PMARK(19);
     // ---- inter out layer ----
     epi_bwd(dG, P16, preG, P16, M, FO, 2);
-    if (saved) {
+    const float* WhL = Wh;   // the layer's Wh / s / t: the preloaded copies, or the Wh scratch
+    int ldL = P72;
+    const float *sL = s, *tL = t;
+    if (preload) {
+      WhL = sm + L.WhGOs;
+      ldL = P16;
+      sL = sm + L.stGOs;
+      tL = sL + NP;
+    } else if (saved) {
       rows_from_global(Wh, P72, saved + SL.Whgo, M, FO);
       rows_from_global(s, 0, saved + SL.stgo, 1, M);
       rows_from_global(t, 0, saved + SL.stgo + NP, 1, M);
@@ -969,7 +1030,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       }
     }
     lds_barrier(); PMARK(20);
-    att_bwd(Wh, P72, M, FO, nullptr, s, t, p.alpha, lw.ago, dG, P16, dWh, P72, ds, dt, attm, dz, NPP, slab + PL.ago);
+    att_bwd(WhL, ldL, M, FO, nullptr, sL, tL, p.alpha, lw.ago, dG, P16, dWh, P72, ds, dt, attm, dz, NPP, slab + PL.ago);
     wgrad(G1, PH, M, FH * nh, dWh, P72, FO, slab + PL.Wgo, FO, 0);
     lin_t(dWh, P72, M, FO, lw.Wgo, PW16, FH * nh, dH, PH, false, 8);
     lds_barrier(); PMARK(21);
@@ -982,7 +1043,13 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         const float yv = G1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      if (saved) {
+      const float* WhH = Wh;
+      const float *sH = s, *tH = t;
+      if (preload) {
+        WhH = sm + L.WhGs + h * NP * P72;
+        sH = sm + L.stGs + h * 2 * NP;
+        tH = sH + NP;
+      } else if (saved) {
         rows_from_global(Wh, P72, saved + (SL.Whg[0] + h * SLH), M, FH);
         rows_from_global(s, 0, saved + (SL.stg[0] + h * SLH), 1, M);
         rows_from_global(t, 0, saved + (SL.stg[0] + h * SLH) + NP, 1, M);
@@ -995,7 +1062,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         }
       }
       lds_barrier(); PMARK(22);
-      att_bwd(Wh, P72, M, FH, nullptr, s, t, p.alpha, (lw.ag[0] + h * SEGG), dH + h * FH, PH, dWh, P72, ds, dt, attm, dz, NPP,
+      att_bwd(WhH, P72, M, FH, nullptr, sH, tH, p.alpha, (lw.ag[0] + h * SEGG), dH + h * FH, PH, dWh, P72, ds, dt, attm, dz, NPP,
               slab + (PL.ag[0] + h * PLG));
       wgrad(gin, P16, M, FO, dWh, P72, FH, slab + (PL.Wg[0] + h * PLG), FH, 0);
       lin_t(dWh, P72, M, FH, (lw.Wg[0] + h * SEGG), PW72, FO, dG, P16, true, 8);
@@ -1009,7 +1076,16 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     lds_barrier(); PMARK(24);
     // ---- intra out layer ----
     epi_bwd(dI, P16, preI, P16, n, FO, 2);
-    if (saved) {
+    WhL = Wh;
+    ldL = P72;
+    sL = s;
+    tL = t;
+    if (preload) {
+      WhL = sm + L.WhIOs;
+      ldL = P16;
+      sL = sm + L.stIOs;
+      tL = sL + NP;
+    } else if (saved) {
       rows_from_global(Wh, P72, saved + SL.Whio, n, FO);
       rows_from_global(s, 0, saved + SL.stio, 1, n);
       rows_from_global(t, 0, saved + SL.stio + NP, 1, n);
@@ -1022,7 +1098,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       }
     }
     lds_barrier(); PMARK(25);
-    att_bwd(Wh, P72, n, FO, gidl, s, t, p.alpha, lw.aio, dI, P16, dWh, P72, ds, dt, attm, dz, NPP, slab + PL.aio);
+    att_bwd(WhL, ldL, n, FO, gidl, sL, tL, p.alpha, lw.aio, dI, P16, dWh, P72, ds, dt, attm, dz, NPP, slab + PL.aio);
     wgrad(H1, PH, n, FH * nh, dWh, P72, FO, slab + PL.Wio, FO, 0);
     lin_t(dWh, P72, n, FO, lw.Wio, PW16, FH * nh, dH, PH, false, 8);
     lds_barrier(); PMARK(26);
@@ -1035,7 +1111,13 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         const float yv = H1[r * PH + h * FH + f];
         dH[r * PH + h * FH + f] *= yv > 0.f ? 1.f : yv + 1.f;
       }
-      if (saved) {
+      const float* WhH = Wh;
+      const float *sH = s, *tH = t;
+      if (preload) {
+        WhH = sm + L.WhIs + h * NP * P72;
+        sH = sm + L.stIs + h * 2 * NP;
+        tH = sH + NP;
+      } else if (saved) {
         rows_from_global(Wh, P72, saved + (SL.Whi[0] + h * SLH), n, FH);
         rows_from_global(s, 0, saved + (SL.sti[0] + h * SLH), 1, n);
         rows_from_global(t, 0, saved + (SL.sti[0] + h * SLH) + NP, 1, n);
@@ -1048,7 +1130,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         }
       }
       lds_barrier(); PMARK(27);
-      att_bwd(Wh, P72, n, FH, gidl, s, t, p.alpha, (lw.ai[0] + h * SEGI), dH + h * FH, PH, dWh, P72, ds, dt, attm, dz, NPP,
+      att_bwd(WhH, P72, n, FH, gidl, sH, tH, p.alpha, (lw.ai[0] + h * SEGI), dH + h * FH, PH, dWh, P72, ds, dt, attm, dz, NPP,
               slab + (PL.ai[0] + h * PLI));
       wgrad(X, P40, n, FI, dWh, P72, FH, slab + (PL.Wi[0] + h * PLI), FH, 0);
       // dX (global) accumulates over heads in a fixed order
