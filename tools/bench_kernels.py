@@ -167,6 +167,10 @@ if __name__ == "__main__":
             lstm_ab(*args)
         dense()
         sys.exit(0)
+    if what == "roll":    # the no-grad decoder rollout against its batch (waves per SIMD)
+        for B in (4096, 8192, 16384, 20480, 25600, 32768, 49152):
+            lstm(B, 12, 32, True, reps=20)
+        sys.exit(0)
     if what == "lstm":
         for B in (1280, 2560, 4096, 25600):
             for save in (False, True):
