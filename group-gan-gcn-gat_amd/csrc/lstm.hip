@@ -397,25 +397,36 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
 
 extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias,
                                 const float* Wp, const float* bp, int T, int B, int H, float* h_all, float* c_all,
-                                float* act_all, float* rel_out, float* rel0_out, void* stream) {
+                                float* act_all, float* rel_out, float* rel0_out, const SggTrajOut* to,
+                                void* stream) {
   SGG_CHECK_ARG(di && di->ctx && di->ped_scene && di->last_rel && (di->nz == 0 || di->z) && A && Whh && bias &&
                     h_all && c_all && Wp && bp && rel_out,
                 "sgg_lstm_fwd_dec: null pointer");
   SGG_CHECK_ARG(T >= 1 && B >= 0 && di->Bper >= 1 && B % di->Bper == 0 && di->Dc >= 1 && di->nz >= 0 &&
                     di->Dc + di->nz == H && di->ldc >= di->Dc && di->S >= 1,
                 "sgg_lstm_fwd_dec: bad sizes (T=%d B=%d Bper=%d Dc=%d nz=%d H=%d)", T, B, di->Bper, di->Dc, di->nz, H);
+  if (to) {
+    SGG_CHECK_ARG(to->out && to->head && (!to->start || to->pos0), "sgg_lstm_fwd_dec: null pointer in SggTrajOut");
+    SGG_CHECK_ARG(to->T0 >= 0 && to->ncol >= 1 && to->col0 >= 0 && to->col0 + to->ncol <= B &&
+                      to->NB == (to->b ? 2 : 1) * to->ncol && to->ldh >= 2 * to->ncol &&
+                      (!to->b || to->ldb >= 2 * to->ncol),
+                  "sgg_lstm_fwd_dec: bad SggTrajOut sizes (NB=%d T0=%d col0=%d ncol=%d B=%d)", to->NB, to->T0,
+                  to->col0, to->ncol, B);
+  }
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const bool mw = lstm_mw_ok(H, B);
   if (act_all && mw)
     return lstm_mw_fwd(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, act_all, rel_out,
-                       st, nullptr, 0, nullptr, 0, nullptr, di, rel0_out);
+                       st, nullptr, 0, nullptr, 0, nullptr, di, rel0_out, to);
+  SGG_CHECK_ARG(!to || (mw && !(lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))),
+                "sgg_lstm_fwd_dec: the discriminator input is written by the four-wave family only (H=%d B=%d)", H, B);
   if (!act_all && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
     return lstm_fwd_mfma(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, nullptr, rel_out,
                          st, di);
   if (!act_all && mw)
     return lstm_mw_fwd(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, nullptr, rel_out, st,
-                       nullptr, 0, nullptr, 0, nullptr, di, nullptr);
+                       nullptr, 0, nullptr, 0, nullptr, di, nullptr, to);
   SGG_CHECK_ARG(false, "sgg_lstm_fwd_dec: no fused decoder start for H=%d B=%d (use sgg_decoder_init)", H, B);
 }
 

@@ -227,6 +227,50 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
     wp1[i] = decoder ? Wp[H + u] : 0.f;
   }
   const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
+  // the discriminator input's entries of this workgroup's peds that do not
+  // come from the recurrence (head steps, the b half, start positions;
+  // SggTrajOut): loaded with the weights, stored after the prologue
+  constexpr int kTo = 4;
+  float2 tov[kTo];
+  float2* tod[kTo];
+  int nto = 0;
+  if (DEC && sg.to.out != nullptr) {
+    const SggTrajOut& to = sg.to;
+    const int dup = to.b ? 2 : 1;
+    const int nh = to.T0 * dup, nb = to.b ? T : 0, ns = to.start ? dup : 0;
+    nto = kMwPeds * (nh + nb + ns);
+    auto entry = [&](int e, float2*& d) -> float2 {
+      const int i = e % kMwPeds, w = e / kMwPeds;
+      const int col = min(blk * kMwPeds + i, B - 1) - to.col0;
+      d = nullptr;
+      if (col < 0 || col >= to.ncol) return make_float2(0.f, 0.f);
+      float2* o2 = reinterpret_cast<float2*>(to.out);
+      if (w < nh) {   // head step t (either half)
+        const int t = w / dup, half = w - t * dup;
+        d = o2 + (size_t)t * to.NB + col + half * to.ncol;
+        return reinterpret_cast<const float2*>(to.head + (size_t)t * to.ldh)[col];
+      }
+      if (w < nh + nb) {   // the b half's step T0 + t
+        const int t = w - nh;
+        d = o2 + (size_t)(to.T0 + t) * to.NB + to.ncol + col;
+        return reinterpret_cast<const float2*>(to.b + (size_t)t * to.ldb)[col];
+      }
+      d = reinterpret_cast<float2*>(to.start) + col + (w - nh - nb) * to.ncol;
+      return reinterpret_cast<const float2*>(to.pos0)[col];
+    };
+#pragma unroll
+    for (int m = 0; m < kTo; ++m) {
+      const int e = threadIdx.x + m * kMwThreads;
+      tod[m] = nullptr;
+      if (e < nto) tov[m] = entry(e, tod[m]);
+    }
+    for (int e = threadIdx.x + kTo * kMwThreads; e < nto; e += kMwThreads) {   // (longer heads: rare)
+      float2* d;
+      const float2 v = entry(e, d);
+      if (d) *d = v;
+    }
+  }
+
   // the encoder's inputs of all T steps: loaded into registers here, written
   // to LDS after the epilogue's prefetch below is issued (so the LDS writes
   // wait for these loads only)
@@ -286,6 +330,11 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
       if (e < 2 * kMwPeds * T) relseq[e / (2 * kMwPeds)][(e >> 1) & (kMwPeds - 1)][e & 1] = rv[m];
     }
   }
+  if (DEC && nto > 0) {
+#pragma unroll
+    for (int m = 0; m < kTo; ++m)
+      if (tod[m]) *tod[m] = tov[m];
+  }
   // LDS only: the prologue's global stores (saved initial state) need not
   // complete before the recurrence
   lds_barrier();
@@ -300,6 +349,9 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   };
   float xin = input(0);
   if (decoder && sg.rel0_out && g == 0 && q < 2) sg.rel0_out[(size_t)pc * 2 + q] = xin;   // (the backward's x_0)
+  const SggTrajOut& to = sg.to;
+  const int tcol = pc - to.col0;   // this lane's column of the discriminator input
+  const bool tlive = decoder && to.out != nullptr && tcol >= 0 && tcol < to.ncol;
   for (int t = 0; t < T; ++t) {
     if (decoder && t == 1) {
       // fold the hidden2pos feedback into the recurrence (see header)
@@ -365,8 +417,26 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
     if (decoder && g == 0 && q == 0) {   // r_t = Wp h_t + bp
       const float2 r0 = rpart[t & 1][0][c16], r1 = rpart[t & 1][1][c16], r2 = rpart[t & 1][2][c16],
                    r3 = rpart[t & 1][3][c16];
-      *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + pc) * 2) =
-          make_float2(((r0.x + r1.x) + (r2.x + r3.x)) + bp0, ((r0.y + r1.y) + (r2.y + r3.y)) + bp1);
+      const float2 rv2 = make_float2(((r0.x + r1.x) + (r2.x + r3.x)) + bp0, ((r0.y + r1.y) + (r2.y + r3.y)) + bp1);
+      *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + pc) * 2) = rv2;
+      if (tlive) {   // staged in LDS (the decoder's relseq is free), stored after the loop
+        if (T <= kMwMaxT) {
+          relseq[t][c16][0] = rv2.x;
+          relseq[t][c16][1] = rv2.y;
+        } else {
+          reinterpret_cast<float2*>(to.out)[(size_t)(to.T0 + t) * to.NB + tcol] = rv2;
+        }
+      }
+    }
+  }
+  if (DEC && to.out != nullptr && T <= kMwMaxT) {   // the generated steps of the discriminator input
+    lds_barrier();
+    for (int e = threadIdx.x; e < T * kMwPeds; e += kMwThreads) {
+      const int t = e / kMwPeds, i = e - t * kMwPeds;
+      const int col = min(blk * kMwPeds + i, B - 1) - to.col0;
+      if (col >= 0 && col < to.ncol)
+        reinterpret_cast<float2*>(to.out)[(size_t)(to.T0 + t) * to.NB + col] =
+            make_float2(relseq[t][i][0], relseq[t][i][1]);
     }
   }
   const float* __restrict__ cu = sg.cu;
@@ -888,7 +958,7 @@ int lstm_mw_wpart_rows(int H, int B) {
 int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
                 const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
                 float* c_all, float* act_all, float* rel_out, hipStream_t st, const float* Wu, int ldwu,
-                const float* cu, int NU, float* U, const SggDecInit* di, float* rel0_out) {
+                const float* cu, int NU, float* U, const SggDecInit* di, float* rel0_out, const SggTrajOut* to) {
   SGG_CHECK_ARG(decoder || T <= kMwMaxT, "sgg_lstm_fwd: encoder sequences of the H=%d kernels hold <= %d steps (T=%d)",
                 H, kMwMaxT, T);
   MwSeg sg{rel, A, Whh, bias, h0, c0, Wp, bp, T, B, B, 0, T, B, h_all, c_all, act_all, rel_out, Wu, ldwu, cu, NU, U};
@@ -896,6 +966,7 @@ int lstm_mw_fwd(const float* rel, const float* A, const float* Whh, const float*
     sg.di = *di;
     sg.rel0_out = rel0_out;
   }
+  if (to) sg.to = *to;
   return launch_seg_h(sg, H, decoder != 0, st);
 }
 

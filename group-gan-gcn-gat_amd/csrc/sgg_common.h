@@ -94,7 +94,7 @@ __attribute__((visibility("hidden"))) int lstm_mw_fwd(const float* rel, const fl
                                                       float* rel_out, hipStream_t st, const float* Wu = nullptr,
                                                       int ldwu = 0, const float* cu = nullptr, int NU = 0,
                                                       float* U = nullptr, const SggDecInit* di = nullptr,
-                                                      float* rel0_out = nullptr);
+                                                      float* rel0_out = nullptr, const SggTrajOut* to = nullptr);
 __attribute__((visibility("hidden"))) int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp,
                                                       const float* h_all, const float* c_all, const float* act_all,
                                                       const float* rel, const float* rel_out, const float* dh_last,
@@ -114,6 +114,7 @@ struct MwSeg {
   float* U;
   SggDecInit di;      // decoder: di.ctx != NULL builds h0 / rel0 in the prologue (sgg_lstm_fwd_dec)
   float* rel0_out;    // (with di) receives rel0 when saving
+  SggTrajOut to;      // decoder: to.out != NULL writes the discriminator input (sgg_lstm_fwd_dec)
 };
 // h0[p][u] and rel0[p][k] of a SggDecInit (sgg_decoder_init's values)
 __device__ __forceinline__ float dec_h0(const SggDecInit& d, int p, int u) {

@@ -94,6 +94,12 @@ class DecInit(ctypes.Structure):
 LOSSJOB_MAX = 2   # SGG_LOSSJOB_MAX
 
 
+class TrajOut(ctypes.Structure):
+    """SggTrajOut (include/sgg.h): the discriminator input written by the decoder launch."""
+    _fields_ = [("out", _p), ("NB", _i), ("T0", _i), ("col0", _i), ("ncol", _i), ("head", _p), ("ldh", _i),
+                ("b", _p), ("ldb", _i), ("pos0", _p), ("start", _p)]
+
+
 class L2Job(ctypes.Structure):
     """SggL2Job (include/sgg.h): an L2 loss value of sgg_grad_finish_losses."""
     _fields_ = [("term", _p), ("S", _i), ("loss", _p)]
@@ -137,7 +143,8 @@ SIGNATURES = {
     "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _p, _i, _f, _p, _p]),
     "sgg_xtw_partial": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
-    "sgg_lstm_fwd_dec": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
+    "sgg_lstm_fwd_dec": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
+                              ctypes.POINTER(TrajOut), _p]),
     "sgg_grad_finish_losses": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz,
                                     ctypes.POINTER(L2Job), _i, ctypes.POINTER(BceJob), _i, _p]),
     "sgg_adam_parts": (_i, [ctypes.c_longlong]),

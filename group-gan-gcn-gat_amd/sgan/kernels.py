@@ -6,6 +6,7 @@ all nodes (X^T dY, column sums) included (sgg_xtw, xtw.hip).  No op has a CPU
 path.
 """
 import contextlib
+import functools
 import os
 import weakref
 
@@ -1674,14 +1675,24 @@ class _LSTMSeq(torch.autograd.Function):
                 # the decoder's h0 / rel0 built in the kernel's prologue (one
                 # launch fewer); where no kernel takes it, materialise them first
                 di, dkeep, materialize = dinit
-                # the closure holds every buffer the descriptor and the
+                ta = _TRAJ[0]
+                to = ta.desc(T, B) if ta is not None else None
+                # the closure holds every buffer the descriptors and the
                 # arguments point to (the bench's timer re-issues it later)
-                fkeep = (dkeep, A, Whh, bias, Wpc, bp, h_all, c_all, act, rel_out, rel)
-                fused = lambda k=fkeep: lib.sgg_lstm_fwd_dec(N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias),
-                                                             N.ptr(Wpc), N.ptr(bp), T, B, H, N.ptr(h_all),
-                                                             N.ptr(c_all), N.ptr(act), N.ptr(rel_out),
-                                                             N.ptr(rel) if save else None, N.stream_ptr())
-                if fused() == 0:
+                fkeep = (dkeep, A, Whh, bias, Wpc, bp, h_all, c_all, act, rel_out, rel,
+                         (ta.out, ta.start, ta.head, ta.b, ta.pos0) if to is not None else None)
+                fused = lambda k=fkeep, to=to: lib.sgg_lstm_fwd_dec(
+                    N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wpc), N.ptr(bp), T, B, H,
+                    N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out), N.ptr(rel) if save else None,
+                    N.ctypes.byref(to) if to is not None else None, N.stream_ptr())
+                rc = fused()
+                if rc != 0 and to is not None:   # no family writes the discriminator input here
+                    to = None
+                    fused = functools.partial(fused, to=None)
+                    rc = fused()
+                if rc == 0:
+                    if to is not None:   # traj_cat on these columns finds them written
+                        ta.filled = (rel_out.data_ptr() + 8 * ta.col0, rel_out.stride(0))
                     launch = lambda: N.check(fused(), "sgg_lstm_fwd_dec")
                 else:
                     h0d, r0d = h0.detach(), rel
@@ -2006,6 +2017,68 @@ def bce_pair(scores, split, y_a, y_b, w=1.0, nvalid=None):
 # ---------------------------------------------------------------------------
 # training-step glue (glue.hip)
 # ---------------------------------------------------------------------------
+# the discriminator input written by the decoder launch that produces its
+# generated half (SggTrajOut, sgg_lstm_fwd_dec): armed by traj_ahead around
+# the decoder's call, taken by traj_cat when its arguments are the armed ones
+# (one launch fewer per step); "0" disables
+TRAJ_AHEAD = os.environ.get("SGG_TRAJ_AHEAD", "1") != "0"
+_TRAJ = [None]
+
+
+def _pairs_rows(t):
+    """t is rows of (x, y) pairs with a free step stride (sgg_traj_cat's layout)."""
+    return t is not None and t.dim() == 3 and t.stride(1) == 2 and t.stride(2) == 1
+
+
+class TrajAhead:
+    """traj_cat(head, <decoder output columns col0 .. col0 + ncol>, b, pos0),
+    allocated before the decoder runs (see traj_ahead)."""
+
+    def __init__(self, head, T1, ncol, col0=0, b=None, pos0=None):
+        self.head, self.b, self.pos0 = head, b, pos0
+        self.T0, self.T1, self.ncol, self.col0 = int(head.shape[0]), int(T1), int(ncol), int(col0)
+        NB = 2 * self.ncol if b is not None else self.ncol
+        dev = head.device
+        self.out = torch.empty(self.T0 + self.T1, NB, 2, device=dev, dtype=torch.float32)
+        self.start = torch.empty(1, NB, 2, device=dev, dtype=torch.float32) if pos0 is not None else None
+        self.filled = None   # (address, step stride) of the decoder output columns it holds
+        self.ok = (head.is_cuda and head.dtype == torch.float32 and _pairs_rows(head)
+                   and tuple(head.shape[1:]) == (self.ncol, 2)
+                   and (b is None or (b.dtype == torch.float32 and _pairs_rows(b)
+                                      and tuple(b.shape) == (self.T1, self.ncol, 2)))
+                   and (pos0 is None or (pos0.dtype == torch.float32 and pos0.is_contiguous()
+                                         and pos0.numel() == 2 * self.ncol)))
+
+    def desc(self, T, B):
+        """-> N.TrajOut for a decoder launch of T steps x B columns, or None."""
+        if not self.ok or self.filled is not None or T != self.T1 or self.col0 + self.ncol > B:
+            return None
+        b, p0 = self.b, self.pos0
+        return N.TrajOut(N.ptr(self.out), self.out.shape[1], self.T0, self.col0, self.ncol, N.ptr(self.head),
+                         self.head.stride(0), N.ptr(b), b.stride(0) if b is not None else 0, N.ptr(p0),
+                         N.ptr(self.start))
+
+    def taken_by(self, head, a, b, pos0):
+        key = lambda t: None if t is None else _tkey(t)
+        if (self.filled is None or key(head) != key(self.head) or key(b) != key(self.b)
+                or key(pos0) != key(self.pos0)):
+            return False
+        return (tuple(a.shape) == (self.T1, self.ncol, 2) and (a.data_ptr(), a.stride(0)) == self.filled
+                and a.stride(1) == 2 and a.stride(2) == 1)
+
+
+@contextlib.contextmanager
+def traj_ahead(head, T1, ncol, col0=0, b=None, pos0=None):
+    """Arm a TrajAhead for the decoder launch inside the block; traj_cat(head,
+    a, b, pos0) on that launch's output columns then returns it unlaunched."""
+    prev = _TRAJ[0]
+    _TRAJ[0] = TrajAhead(head, T1, ncol, col0, b, pos0) if TRAJ_AHEAD else None
+    try:
+        yield _TRAJ[0]
+    finally:
+        _TRAJ[0] = prev
+
+
 class _TrajCat(torch.autograd.Function):
     """cat over time of head (T0 x B x 2, repeated for both halves when b is
     given) and a | b (T1 x B x 2 each, side by side); a may be a batch slice
@@ -2018,6 +2091,18 @@ class _TrajCat(torch.autograd.Function):
         T0, B = head.shape[0], head.shape[1]
         head_key = _tkey(head)
         T1 = a.shape[0]
+        ta = _TRAJ[0]
+        if ta is not None and ta.taken_by(head, a, b, pos0):   # written by the decoder launch
+            out, start = ta.out, ta.start
+            ta.filled = ()   # taken once
+            ctx.dims = (T0, B)
+            if not head.requires_grad:
+                out._sgg_grad_from = T0
+            out._sgg_head_key = head_key
+            if start is None:
+                return out
+            ctx.mark_non_differentiable(start)
+            return out, start
         # rows of (x, y) pairs with a free step stride; anything else (e.g. the
         # permuted views seq_collate yields, trajectories_GCN.py:33) is copied
         fix = lambda t: t if t is None or (t.stride(1) == 2 and t.stride(2) == 1) else t.contiguous()

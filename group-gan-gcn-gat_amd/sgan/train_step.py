@@ -148,6 +148,7 @@ class KernelOps:
     # the discriminator encoder's observed steps run once, in the generator
     # encoder's launch (kernels.SharedPrefix)
     shared_prefix = staticmethod(K.shared_prefix)
+    traj_ahead = staticmethod(K.traj_ahead)
 
 
 class GanTrainer:
@@ -209,6 +210,14 @@ class GanTrainer:
             return contextlib.nullcontext()
         return sp(self.D, obs_rel, self.args.obs_len + self.args.pred_len, copies)
 
+    def _traj_ahead(self, head, T1, ncol, col0=0, b=None, pos0=None):
+        """The discriminator input written by the next decoder launch
+        (ops.traj_ahead; a no-op without it)."""
+        ta = getattr(self.ops, "traj_ahead", None)
+        if ta is None:
+            return contextlib.nullcontext()
+        return ta(head, T1, ncol, col0, b, pos0)
+
     def _scope(self):
         st = contextlib.ExitStack()
         st.enter_context(getattr(self.ops, "handoff", contextlib.nullcontext)())
@@ -235,11 +244,12 @@ class GanTrainer:
             # G's folds (stale since the last G-step) and D's (since the last
             # D-step) in ONE launch; the forwards below find them cached
             prefold(self.G.fold_specs() + self.D.fold_specs())
-        with self._prefix(obs_rel, 2):
+        with self._prefix(obs_rel, 2), self._traj_ahead(obs_rel, pred_gt_rel.shape[0], sc.B, 0, pred_gt_rel, obs[0]):
             with torch.no_grad():
                 fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
             # D reads traj[0] (the start positions, models.py:989) and traj_rel
-            # only: [fake | real] side by side, no relative_to_abs needed
+            # only: [fake | real] side by side, no relative_to_abs needed (the
+            # decoder launch writes it: ops.traj_ahead)
             traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
             sc2 = sc.repeat(2)
             scores = self.D(start, traj_rel, _sse_of(sc2), scenes=sc2)
@@ -293,13 +303,21 @@ class GanTrainer:
                                         noise_index=(None, 0))
                     best = ops.l2_select(pred_all, pred_gt_rel, mask, sc, k)   # (S,) int64
             copies = 2 if use_l2 else 1
-            out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=copies,
-                           noise_index=(best, k - 1))
+            # the last sample's columns become the discriminator input below
+            tah = self._traj_ahead(obs_rel, a.pred_len, B, (copies - 1) * B)
+            tah.__enter__()
+            try:
+                out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=copies,
+                               noise_index=(best, k - 1))
+            except BaseException:
+                tah.__exit__(None, None, None)
+                raise
             if use_l2:
                 fake_rel_best, fake_rel_last = ops.split2(out, B)
             else:
                 fake_rel_best, fake_rel_last = None, out
         else:
+            tah = contextlib.nullcontext()
             out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k, noise_index=(None, 0))
             fake_rel_last = out[:, (k - 1) * B:]
             fake_rel_best = None
@@ -325,6 +343,7 @@ class GanTrainer:
         try:
             scores = D(obs[:1], ops.traj_cat(obs_rel, fake_rel_last), sse, scenes=sc)
         finally:
+            tah.__exit__(None, None, None)
             pfx.__exit__(None, None, None)
             for p in self.d_params:
                 p.requires_grad_(True)

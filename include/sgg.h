@@ -423,9 +423,32 @@ typedef struct {
   int Bper;
   const float* last_rel;
 } SggDecInit;
+/* The discriminator input traj_rel = cat(head, the decoder's output) (and the
+ * start positions) written by the same decoder launch (SggTrajOut, may be
+ * NULL): sgg_traj_cat's result (train.py:409-415, 468-470) without its own
+ * launch.  out is (T0 + T) x NB x 2; decoder columns col0 .. col0 + ncol - 1
+ * become out's columns 0 .. ncol - 1 at steps T0 .. T0 + T - 1, head (T0
+ * steps of ncol peds, step stride ldh floats) fills their first T0 steps;
+ * with b != NULL (NB = 2 ncol) columns ncol .. 2 ncol - 1 hold head again,
+ * then b (T steps, stride ldb); with start != NULL, start (1 x NB x 2) gets
+ * pos0 (ncol x 2) for either half.  Taken by the four-wave decoder family
+ * only (SGG_E_ARG otherwise, as for a start no family takes). */
+typedef struct {
+  float* out;
+  int NB;
+  int T0;
+  int col0;
+  int ncol;
+  const float* head;
+  int ldh;
+  const float* b;
+  int ldb;
+  const float* pos0;
+  float* start;
+} SggTrajOut;
 int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias, const float* Wp,
                      const float* bp, int T, int B, int H, float* h_all, float* c_all, float* act_all,
-                     float* rel_out, float* rel0_out, void* stream);
+                     float* rel_out, float* rel0_out, const SggTrajOut* to, void* stream);
 
 /* Encoder sequence (decoder = 0) with the pooling MLP's h-half fused into the
  * kernel's epilogue (models.py:538): also writes U = h_T Wu^T + cu (B x NU,
