@@ -11,7 +11,8 @@ import os
 
 import torch  # noqa: F401  (must precede the dlopen below)
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libsgg.so")
+# SGG_LIB: another build of the same library (A/B runs of kernel variants, tools/)
+_LIB_PATH = os.environ.get("SGG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libsgg.so")
 
 _i = ctypes.c_int
 _f = ctypes.c_float
