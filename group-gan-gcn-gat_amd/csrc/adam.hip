@@ -237,9 +237,10 @@ __global__ void __launch_bounds__(kAdamThreads) adam_update_kernel(AdamList L, i
 
 using namespace sgg;
 
-// workspace floats: one partial per workgroup + 2 step scalars per tensor +
-// the fused launch's ticket (zero when the workspace is first used; every
-// call leaves it at zero)
+// workspace floats: the fused launch's ticket at the FIXED word ws[0] (zero
+// when the workspace is first used, every call leaves it at zero, and nothing
+// else ever writes it -- whatever the parameter count or clipping of the
+// call), then one partial per workgroup, then 2 step scalars per tensor
 extern "C" int sgg_adam_parts(long long total) {
   return (int)((total + kAdamChunk - 1) / kAdamChunk) + 2 * kAdamMaxTensors + 1;
 }
@@ -269,12 +270,14 @@ extern "C" int sgg_adam_step(float* const* params, float* const* grads, float* c
   SGG_CHECK_ARG(ws && ws_bytes >= sizeof(float) * ((size_t)parts + 2 * kAdamMaxTensors + 1),
                 "sgg_adam_step: workspace");
   hipStream_t st = (hipStream_t)stream;
-  float* scal = ws + parts;
-  unsigned* ticket = reinterpret_cast<unsigned*>(scal + 2 * kAdamMaxTensors);
+  unsigned* ticket = reinterpret_cast<unsigned*>(ws);
+  float* partial = ws + 1;
+  float* scal = partial + parts;
   if (clip)   // the norm's partials need every workgroup: a launch of their own
-    hipLaunchKernelGGL(adam_prep_kernel, dim3(parts), dim3(kAdamThreads), 0, st, L, clip, ws, scal, lr, beta1, beta2);
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(parts), dim3(kAdamThreads), 0, st, L, clip, partial, scal, lr, beta1,
+                       beta2);
   hipLaunchKernelGGL(adam_update_kernel, dim3(parts), dim3(kAdamThreads), 0, st, L, parts, clip ? max_norm : 0.f,
-                     ws, scal, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps, clip ? nullptr : ticket,
+                     partial, scal, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps, clip ? nullptr : ticket,
                      lr, beta1, beta2);
   SGG_RETURN_LAUNCH("sgg_adam_step");
 }

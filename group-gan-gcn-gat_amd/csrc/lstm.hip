@@ -400,7 +400,7 @@ extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const floa
                                 float* act_all, float* rel_out, float* rel0_out, const SggTrajOut* to,
                                 void* stream) {
   SGG_CHECK_ARG(di && di->ctx && di->ped_scene && di->last_rel && (di->nz == 0 || di->z) && A && Whh && bias &&
-                    h_all && c_all && Wp && bp && rel_out,
+                    ((h_all && c_all) || (!h_all && !c_all && !act_all)) && Wp && bp && rel_out,
                 "sgg_lstm_fwd_dec: null pointer");
   SGG_CHECK_ARG(T >= 1 && B >= 0 && di->Bper >= 1 && B % di->Bper == 0 && di->Dc >= 1 && di->nz >= 0 &&
                     di->Dc + di->nz == H && di->ldc >= di->Dc && di->S >= 1,

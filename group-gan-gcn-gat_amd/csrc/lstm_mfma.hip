@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
         *reinterpret_cast<float4*>(act_all + ab + 2 * H) = make_float4(ag[0], ag[1], ag[2], ag[3]);
         *reinterpret_cast<float4*>(act_all + ab + 3 * H) = make_float4(ao[0], ao[1], ao[2], ao[3]);
       }
-      if (valid && (save || t == T - 1)) {
+      if (valid && (save || (t == T - 1 && h_all))) {   // (no-grad rollout: h_all NULL, final state unwanted)
         const size_t o = ((size_t)(save ? t + 1 : T) * B + ped) * H + 16 * mu + 4 * q;
         *reinterpret_cast<float4*>(h_all + o) = make_float4(h[4 * mu], h[4 * mu + 1], h[4 * mu + 2], h[4 * mu + 3]);
         *reinterpret_cast<float4*>(c_all + o) = make_float4(c[4 * mu], c[4 * mu + 1], c[4 * mu + 2], c[4 * mu + 3]);

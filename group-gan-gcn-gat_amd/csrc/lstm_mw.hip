@@ -399,7 +399,7 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
       c[mu] = fmaf(a[1], c[mu], a[0] * a[2]);
       const float h = a[3] * tanh_m(c[mu]);
       hb[rb ^ 1][j][lane] = h;
-      if (save || t == T - 1) h_all[((size_t)(t0 + (save ? t + 1 : T)) * Bl + pc) * H + slot_unit(j, q)] = h;
+      if (save || (t == T - 1 && h_all)) h_all[((size_t)(t0 + (save ? t + 1 : T)) * Bl + pc) * H + slot_unit(j, q)] = h;
       px = fmaf(wp0[mu], h, px);
       py = fmaf(wp1[mu], h, py);
     }

@@ -403,8 +403,28 @@ _LOSS = {"l2": [], "bce": [], "keep": [], "out": set()}
 DEFER_LOSSES = os.environ.get("SGG_DEFER_LOSSES", "1") != "0"
 
 
-def _loss_deferrable():
-    return DEFER_LOSSES and _DEFER[0] > 0 and len(_LOSS["l2"]) + len(_LOSS["bce"]) < 2 * N.LOSSJOB_MAX
+def _loss_deferrable(kind):
+    """May one more loss value of `kind` ("l2" / "bce") be queued?  The finish
+    launch takes at most SGG_LOSSJOB_MAX jobs of EACH kind; past that the op
+    forms its value in a launch of its own."""
+    return DEFER_LOSSES and _DEFER[0] > 0 and not _NO_DEFER[0] and len(_LOSS[kind]) < N.LOSSJOB_MAX
+
+
+@contextlib.contextmanager
+def eager_losses():
+    """Scope in which no loss value is queued: every loss op writes its value
+    at once.  For callers that read a loss value before the backward (an
+    eager add of two values): a queued value is formed only after the
+    backward (the L2 value from the per-scene terms its backward writes)."""
+    prev = _NO_DEFER[0]
+    _NO_DEFER[0] = True
+    try:
+        yield
+    finally:
+        _NO_DEFER[0] = prev
+
+
+_NO_DEFER = [False]
 
 
 def _queue_loss(kind, job, keep, outs):
@@ -437,7 +457,20 @@ def defer_grad_finish():
     (GradFinish) instead of launching them; grad_flush() -- the trainer's,
     before the optimizer reads the gradients -- issues all of them in two
     launches (every row sum, every fold backward) where the ops would issue
-    two each.  Leaving the scope flushes whatever is still queued."""
+    two each.  Leaving the scope flushes whatever is still queued.
+
+    Invariant: inside the scope, the gradient tensors a backward op returns
+    (views of its slab sums, dW / dWe / dbe) are NOT written until
+    grad_flush().  Nothing may read them before that: not autograd's
+    InputBuffer summing two contributions to one parameter (no parameter of
+    the models feeds two ops), not a tensor / post-accumulate hook,
+    retain_grad or an all-reduce hook during the backward.  GanTrainer leaves
+    the scope out when a parameter has such a reader (_grad_observed); with
+    SGG_CHECK_DEFER=1 every op flushes right after its backward (the deferred
+    == immediate comparison of tests/test_gpu_parity.py runs both)."""
+    if os.environ.get("SGG_CHECK_DEFER") == "1":
+        yield
+        return
     _DEFER[0] += 1
     try:
         yield
@@ -772,6 +805,126 @@ class ClipAdam:
 # ---------------------------------------------------------------------------
 # social pooling
 # ---------------------------------------------------------------------------
+class OwnershipError(N.NativeError):
+    """A re-issuable launch holds a raw device pointer (inside a ctypes
+    descriptor) to memory it does not keep alive."""
+
+
+def _storage_span(obj):
+    """(begin, end) device address range of a tensor's / storage's memory."""
+    s = obj.untyped_storage() if isinstance(obj, torch.Tensor) else obj
+    b = s.data_ptr()
+    return (b, b + s.nbytes())
+
+
+def _walk_held(obj, spans, descs, seen, depth=0):
+    """Everything a closure holds: memory spans of tensors / storages, and the
+    ctypes descriptors (structs, arrays of them) whose pointer fields the
+    launch hands to the device."""
+    import ctypes
+    if obj is None or isinstance(obj, (int, float, str, bytes, bool)) or depth > 6 or id(obj) in seen:
+        return
+    seen.add(id(obj))
+    if isinstance(obj, (torch.Tensor, torch.UntypedStorage)):
+        sp = _storage_span(obj)
+        if sp is not None:
+            spans.append(sp)
+        return
+    if isinstance(obj, (ctypes.Structure, ctypes.Array)):
+        descs.append(obj)
+        for v in getattr(obj, "__dict__", {}).values():   # an owned descriptor's kept buffers
+            _walk_held(v, spans, descs, seen, depth + 1)
+        return
+    if isinstance(obj, (list, tuple, set, frozenset)):
+        for v in obj:
+            _walk_held(v, spans, descs, seen, depth + 1)
+        return
+    if isinstance(obj, dict):
+        for v in obj.values():
+            _walk_held(v, spans, descs, seen, depth + 1)
+        return
+    if isinstance(obj, functools.partial):
+        for v in (obj.func, obj.args, obj.keywords):
+            _walk_held(v, spans, descs, seen, depth + 1)
+        return
+    code = getattr(obj, "__code__", None)
+    if code is not None:   # a function: its closure cells and bound defaults
+        for c in obj.__closure__ or ():
+            try:
+                _walk_held(c.cell_contents, spans, descs, seen, depth + 1)
+            except ValueError:   # an empty cell
+                pass
+        _walk_held(obj.__defaults__, spans, descs, seen, depth + 1)
+        _walk_held(obj.__kwdefaults__, spans, descs, seen, depth + 1)
+        return
+    if hasattr(obj, "__self__") and hasattr(obj, "__func__"):   # a bound method
+        _walk_held(obj.__self__, spans, descs, seen, depth + 1)
+        return
+    d = getattr(obj, "__dict__", None)
+    if d is not None and not isinstance(obj, (type, torch.nn.Module)):
+        _walk_held(d, spans, descs, seen, depth + 1)
+
+
+def _desc_pointers(desc, path="", out=None):
+    """[(field path, address)] of every non-null pointer field of a ctypes
+    struct / array (nested structs and pointer arrays included)."""
+    import ctypes
+    out = [] if out is None else out
+    if isinstance(desc, ctypes.Array):
+        for i in range(len(desc)):
+            v = desc[i]
+            if isinstance(v, (ctypes.Structure, ctypes.Array)):
+                _desc_pointers(v, "%s[%d]" % (path, i), out)
+            elif desc._type_ is ctypes.c_void_p and v:
+                out.append(("%s[%d]" % (path, i), v))
+        return out
+    for fname, ftype in desc._fields_:
+        v = getattr(desc, fname)
+        if isinstance(v, (ctypes.Structure, ctypes.Array)):
+            _desc_pointers(v, path + "." + fname, out)
+        elif ftype is ctypes.c_void_p and v:
+            out.append((path + "." + fname, v))
+    return out
+
+
+def check_ownership(fn, name="launch"):
+    """Assert that every device pointer a re-issuable launch `fn` passes
+    through a ctypes descriptor lies in memory that `fn` itself keeps alive
+    (a tensor or storage reachable from its closure, its bound defaults, or
+    the descriptor's own kept buffers).  Arguments passed as N.ptr(t) are
+    re-evaluated on tensors the closure holds, so they are owned by
+    construction; a descriptor's pointers are raw integers, and a buffer that
+    only the descriptor names can be freed and reused before a re-issue (the
+    round-3 hipErrorIllegalAddress)."""
+    spans, descs = [], []
+    _walk_held(fn, spans, descs, set())
+    spans.sort()
+    for d in descs:
+        for path, p in _desc_pointers(d, type(d).__name__):
+            if not any(b <= p < e for b, e in spans):
+                raise OwnershipError("%s: descriptor field %s points to 0x%x, which the re-issuable launch does "
+                                     "not keep alive" % (name, path, p))
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """Around a HIP-graph capture: collect garbage first and keep the cyclic
+    garbage collector off until the capture ends.  A CUDAGraph reachable only
+    through a reference cycle is destroyed whenever the collector happens to
+    run; if that is inside another capture, ~CUDAGraph's synchronisation is
+    illegal on the capturing stream and the process aborts (the round-3
+    hipErrorStreamCaptureUnsupported)."""
+    import gc
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
 class LaunchTimer:
     """Per-kernel device timing of the hot ops (bench.py's roofline).
 
@@ -780,13 +933,16 @@ class LaunchTimer:
     its kernel name (as rocprofv3 lists it), its algorithmic FLOP and HBM
     bytes (work models in DESIGN.md section 4) and a closure that re-issues
     the identical launch on the same buffers (every instrumented op is
-    idempotent: it rewrites its outputs from its inputs; the closure keeps the
-    tensors alive).  `replay()` captures `reps` back-to-back re-issues of each
-    distinct launch into a HIP graph and replays it between two HIP events on
-    the current stream, so the device never
-    waits for the host and elapsed / reps is the kernel's average device
-    duration (an event pair around one eager launch would also count host
-    launch latency)."""
+    idempotent: it rewrites its outputs from its inputs).  The closure must
+    own every buffer it launches on: `add` checks that each pointer inside
+    its ctypes descriptors lies in a tensor / storage reachable from the
+    closure (check_ownership) and raises OwnershipError otherwise, so a
+    recorded launch stays valid after the step's own tensors are dropped.
+    `replay()` captures `reps` back-to-back re-issues of each distinct launch
+    into a HIP graph and replays it between two HIP events on the current
+    stream, so the device never waits for the host and elapsed / reps is the
+    kernel's average device duration (an event pair around one eager launch
+    would also count host launch latency)."""
 
     def __init__(self):
         self.active = False
@@ -803,12 +959,18 @@ class LaunchTimer:
 
     def add(self, name, key, flop, nbytes, relaunch):
         if self.active:
+            check_ownership(relaunch, name)
             self.rec.append((name, (name,) + tuple(key), float(flop), float(nbytes), relaunch))
 
     @staticmethod
     def replay(records, reps=20):
         """records -> {key: dict(name, launches, flop, bytes, ms)} with ms the
         average device time of one launch."""
+        with capture_guard():   # (one collection for all the captures below)
+            return LaunchTimer._replay(records, reps)
+
+    @staticmethod
+    def _replay(records, reps):
         res = {}
         cur = torch.cuda.current_stream()
         for name, key, fl, nb, fn in records:
@@ -1625,6 +1787,12 @@ class _LSTMSeq(torch.autograd.Function):
             act = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 0)), device=dev, dtype=torch.float32) \
                 if save else None
         rel_out = torch.empty(T, B, 2, device=dev, dtype=torch.float32) if decoder else None
+        # a no-grad decoder rollout whose final state nobody reads
+        # (final_state_unused(): the best-of-k samples) writes rel_out only
+        no_final = (_NO_FINAL[0] and decoder and not save and not cont and h0 is not None and c0 is None
+                    and getattr(h0, "_sgg_dinit", None) is not None)
+        if no_final:
+            h_all = c_all = None
         Whh = W_hh.contiguous()
         h0c = h0.contiguous() if h0 is not None else None
         c0c = c0.contiguous() if c0 is not None else None
@@ -1695,6 +1863,10 @@ class _LSTMSeq(torch.autograd.Function):
                         ta.filled = (rel_out.data_ptr() + 8 * ta.col0, rel_out.stride(0))
                     launch = lambda: N.check(fused(), "sgg_lstm_fwd_dec")
                 else:
+                    if h_all is None:   # (sgg_lstm_fwd writes the final state)
+                        h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
+                        c_all = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 1)), device=dev,
+                                            dtype=torch.float32)
                     h0d, r0d = h0.detach(), rel
                     materialize(h0d, r0d)
                     plain = launch
@@ -1709,7 +1881,8 @@ class _LSTMSeq(torch.autograd.Function):
             # per ped-step: gates 2 4H (H + 3) FLOP + ~12 H cell / activation; bytes: inputs, saved states
             Ts = T - pfx.T_pre if cont else T    # the steps this launch runs
             fl = Ts * B * (8.0 * H * (H + 3) + 12.0 * H) + (2.0 * B * H * U.shape[1] if U is not None else 0.0)
-            nb = 4.0 * (Ts * B * 2 + ((act.numel() + c_all.numel()) * Ts / T + (Ts + 1) * B * H if save else B * H)
+            nb = 4.0 * (Ts * B * 2 + ((act.numel() + c_all.numel()) * Ts / T + (Ts + 1) * B * H if save else
+                                      (0 if no_final else 2 * B * H))
                         + 4 * H * (H + 3) + (T * B * 2 if decoder else 0) + (U.numel() if U is not None else 0))
             if carry:   # + the prefix: T_pre steps of Bsrc peds, states saved
                 Hp, Tp, Bp = pfx.H, pfx.T_pre, pfx.Bsrc
@@ -1723,7 +1896,7 @@ class _LSTMSeq(torch.autograd.Function):
         ctx.set_materialize_grads(False)   # unused outputs (the decoder's h_last) get None, not a zero fill
         if save:
             ctx.save_for_backward(rel, W_ih, We, be, A, Whh, Wpc, h_all, c_all, act, rel_out)
-        h_last = h_all[T]
+        h_last = h_all[T] if h_all is not None else rel.new_empty(0, H)
         if U is not None:
             ctx.mark_non_differentiable(U)   # its gradient is the pooling backward's business (dh = dU Wu)
             return h_last, U
@@ -1904,7 +2077,7 @@ class _Bce(torch.autograd.Function):
         ctx.bce_link = getattr(x, "_sgg_bce_link", None)
         x = _req(x, "scores").contiguous().view(-1)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
-        if _loss_deferrable():   # formed with the weight gradients
+        if _loss_deferrable("bce"):   # formed with the weight gradients
             _queue_loss("bce", N.BceJob(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss), None,
                                         None, N.ptr(nvalid)), (x, ya, yb, loss, nvalid), (loss,))
         else:
@@ -1966,7 +2139,7 @@ class _BceTotal(torch.autograd.Function):
         addend = _req(addend, "addend").reshape(())
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         total = torch.empty((), device=x.device, dtype=torch.float32)
-        if _loss_deferrable():   # after a queued L2 addend, in the same workgroup
+        if _loss_deferrable("bce"):   # after a queued L2 addend, in the same workgroup
             _queue_loss("bce", N.BceJob(N.ptr(x), x.numel(), split, N.ptr(ya), N.ptr(yb), float(w), N.ptr(loss),
                                         N.ptr(addend), N.ptr(total), N.ptr(nvalid)),
                         (x, ya, yb, loss, addend, total, nvalid), (loss, total))
@@ -2139,6 +2312,21 @@ def traj_cat(head, a, b=None, pos0=None):
     return _TrajCat.apply(head, a, b, pos0)
 
 
+_NO_FINAL = [False]
+
+
+@contextlib.contextmanager
+def final_state_unused():
+    """The no-grad decoder rollouts inside skip their final-state stores
+    (h_T, c_T): the caller reads the predicted displacements only."""
+    prev = _NO_FINAL[0]
+    _NO_FINAL[0] = True
+    try:
+        yield
+    finally:
+        _NO_FINAL[0] = prev
+
+
 # the decoder's h0 / rel0 built in the decoder LSTM's prologue
 # (sgg_lstm_fwd_dec) instead of by a sgg_decoder_init launch; "0" disables
 DEC_INIT_FUSED = os.environ.get("SGG_DEC_INIT_FUSED", "1") != "0"
@@ -2220,7 +2408,7 @@ class _L2Loss(torch.autograd.Function):
         T, B = gt.shape[0], gt.shape[1]
         loss = torch.empty((), device=pred.device, dtype=torch.float32)
         term = None
-        if _loss_deferrable():
+        if _loss_deferrable("l2"):
             # the backward forms the mask sums and the per-scene terms itself
             # (sgg_l2_loss_bwd_scenes); the value is their sum, formed with the
             # weight gradients (SggL2Job) -- inside the trainer's step, whose

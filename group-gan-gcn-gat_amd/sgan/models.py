@@ -708,8 +708,9 @@ class TrajectoryGenerator(nn.Module):
                 (best, first_k), z = noise_index, user_noise
             z = z.to(noise_input.device, non_blocking=True)
             h0, rel0 = K.decoder_init(noise_input, z, best, first_k, copies, sc, obs_traj_rel[-1], lazy=True)
-            h, rel = K.lstm_sequence(rel0, self.decoder.decoder, self.decoder.spatial_embedding, h0=h0, c0=None,
-                                     proj=self.decoder.hidden2pos, decoder=True, T=self.pred_len)
+            with K.final_state_unused():   # (the decoder state is discarded, models.py:925)
+                _h, rel = K.lstm_sequence(rel0, self.decoder.decoder, self.decoder.spatial_embedding, h0=h0, c0=None,
+                                          proj=self.decoder.hidden2pos, decoder=True, T=self.pred_len)
             return rel
         if noise_index is not None and user_noise is not None:
             best, first_k = noise_index

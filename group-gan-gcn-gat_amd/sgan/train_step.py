@@ -39,6 +39,7 @@ The result equals single-GPU training on the global batch up to summation
 order.
 """
 import contextlib
+import functools
 import os
 import random
 
@@ -149,6 +150,9 @@ class KernelOps:
     # encoder's launch (kernels.SharedPrefix)
     shared_prefix = staticmethod(K.shared_prefix)
     traj_ahead = staticmethod(K.traj_ahead)
+    # loss ops inside this scope write their values at once (not queued for
+    # the finish launch): for values read before the backward
+    eager_losses = staticmethod(K.eager_losses)
 
 
 class GanTrainer:
@@ -221,8 +225,21 @@ class GanTrainer:
     def _scope(self):
         st = contextlib.ExitStack()
         st.enter_context(getattr(self.ops, "handoff", contextlib.nullcontext)())
-        st.enter_context(getattr(self.ops, "defer_finish", contextlib.nullcontext)())
+        if not self._grad_observed():
+            st.enter_context(getattr(self.ops, "defer_finish", contextlib.nullcontext)())
         return st
+
+    def _grad_observed(self):
+        """Does anything read a parameter gradient DURING the backward (a
+        tensor hook, a post-accumulate hook, retain_grad)?  Deferred finishes
+        (kernels.defer_grad_finish) write the weight gradients only at
+        grad_flush(), before the optimizer: such a reader would see unwritten
+        memory, so the step then lets every op finish its own gradients."""
+        for p in self.g_params + self.d_params:
+            if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None) \
+                    or p.retains_grad:
+                return True
+        return False
 
     def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """discriminator_step (train.py:395-429). `batch` holds this rank's
@@ -329,9 +346,16 @@ class GanTrainer:
                 scene_l2 = torch.zeros(k, S, device=obs.device).index_add_(1, seg, l2s)
                 mask_sum = torch.zeros(S, device=obs.device).index_add_(0, seg, mask.sum(1))
         terms = []
+        total = getattr(self.ops, "bce_pair_total", None)
+        fused_total = use_l2 and total is not None and self._bce_override is None
+        # without the one-launch total below, the loss values are read by an
+        # eager add before the backward: they must not be queued (a queued L2
+        # value is formed from terms its backward writes)
+        eager = contextlib.nullcontext if fused_total else getattr(self.ops, "eager_losses", contextlib.nullcontext)
         if use_l2:
             if fake_rel_best is not None:
-                g_l2 = ops.l2_loss(fake_rel_best, pred_gt_rel, mask, sc, a.l2_loss_weight)
+                with eager():
+                    g_l2 = ops.l2_loss(fake_rel_best, pred_gt_rel, mask, sc, a.l2_loss_weight)
             else:
                 g_l2 = (a.l2_loss_weight * scene_l2.min(0)[0] / mask_sum).sum()
             terms.append(g_l2)
@@ -348,12 +372,12 @@ class GanTrainer:
             for p in self.d_params:
                 p.requires_grad_(True)
         y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)
-        total = getattr(self.ops, "bce_pair_total", None)
-        if terms and total is not None and self._bce_override is None:
+        if terms and fused_total:
             # gan_g_loss and the total loss with the L2 term from one launch
             adv, loss = total(scores, scores.shape[0], y, y, sc.B / B_global, terms[0], **_valid(sc))
         else:
-            adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global, **_valid(sc))    # gan_g_loss
+            with eager():
+                adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global, **_valid(sc))    # gan_g_loss
             loss = adv + (terms[0] if terms else 0.0)
         self.opt_g.zero_grad(set_to_none=True)
         torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self._g_inputs())
@@ -429,7 +453,9 @@ class GraphedTrainer:
         dev = batch[0].device
         s0 = shard[0]
         self.span = (self.kw["S_global"], s0, s0 + sc.S)
-        self.draw = draw or (lambda: trainer.draw_inputs(*self.span))
+        # (no closure over self anywhere in this object: a GraphedTrainer must
+        # never sit in a reference cycle, see kernels.capture_guard)
+        self.draw = draw or functools.partial(trainer.draw_inputs, *self.span)
         G = trainer.G
         nd = tuple(G.noise_dim) if G.noise_dim else None
         k = trainer.args.best_k
@@ -486,7 +512,7 @@ class GraphedTrainer:
             # stay intact while the other graph replays.
             for i in range(2):
                 K.clear_fold_cache()   # every fold the replays need must be a node of this graph
-                with torch.cuda.stream(cap):
+                with torch.cuda.stream(cap), K.capture_guard():
                     g = torch.cuda.CUDAGraph()
                     g.capture_begin(pool=torch.cuda.graph_pool_handle())
                     self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
@@ -503,7 +529,7 @@ class GraphedTrainer:
             return
         K.clear_fold_cache()   # every fold the replays need must be a node of the graph
         pool = torch.cuda.graph_pool_handle()   # the segments replay in capture order: one shared pool
-        with torch.cuda.stream(cap):
+        with torch.cuda.stream(cap), K.capture_guard():
             g = torch.cuda.CUDAGraph()
             g.capture_begin(pool=pool)
 
@@ -624,6 +650,11 @@ class BucketedGraphTrainer:
         if trainer.dp.on and trainer.dp.world > 1:
             raise NotImplementedError("BucketedGraphTrainer: one rank (the padded batches are not sharded)")
         self.t, self.dd = trainer, ddset
+        if pad_scenes < 1:
+            # a full batch (S == batch_size) still needs one padding scene to
+            # absorb the bucket's spare peds (padded_sizes): without it every
+            # such iteration would silently run eagerly
+            raise ValueError("BucketedGraphTrainer: pad_scenes must be >= 1 (got %d)" % pad_scenes)
         self.S_cap = batch_size + pad_scenes
         self.gran, self.np_caps, self.pool_cap = gran, tuple(sorted(np_caps)), pool_cap
         self.buckets = {}
@@ -664,20 +695,22 @@ class BucketedGraphTrainer:
             ent = self.buckets[key] = self._capture(key, off_d, rows_d, off_g, rows_g)
         ent["sc_d"].load(off_d, rows_d)
         ent["sc_g"].load(off_g, rows_g)
-        ent["S_real"] = (len(off_d) - 1, len(off_g) - 1)
+        ent["state"]["S_real"] = (len(off_d) - 1, len(off_g) - 1)
         return ent["gt"].step()
 
-    def _draw(self, ent):
+    @staticmethod
+    def _draw(t, S_cap, state):
         """The host RNG draws of one iteration in the reference's order
         (StepInputs; TrainArgs.draw_inputs with the two batches' own scene
-        counts), zero-padded to S_cap rows."""
-        t = self.t
-        S_d, S_g = ent["S_real"]
+        counts), zero-padded to S_cap rows.  (A static function over the
+        trainer and the bucket's state, not a closure over the bucket: the
+        bucket holds the GraphedTrainer holding this draw.)"""
+        S_d, S_g = state["S_real"]
 
         def pad(z):
             if z is None:
                 return None
-            out = torch.zeros((self.S_cap,) + tuple(z.shape[1:]), dtype=z.dtype)
+            out = torch.zeros((S_cap,) + tuple(z.shape[1:]), dtype=z.dtype)
             out[:z.shape[0]] = z
             return out
         z_d = pad(t._noise(S_d, 0, S_d))
@@ -702,7 +735,7 @@ class BucketedGraphTrainer:
         dev = self.dd.device
         dd = self.dd
         To, Tp = dd.obs_len, dd.pred_len
-        ent = {"S_real": (len(off_d) - 1, len(off_g) - 1)}
+        ent = {"state": {"S_real": (len(off_d) - 1, len(off_g) - 1)}}
         ent["sc_d"] = PaddedScenes(self.S_cap, B_cap, dev, np_cap, reps=(2,), pool_cap=self.pool_cap)
         ent["sc_g"] = PaddedScenes(self.S_cap, B_cap, dev, np_cap, reps=(), pool_cap=self.pool_cap)
         ent["sc_d"].load(off_d, rows_d)
@@ -711,8 +744,8 @@ class BucketedGraphTrainer:
         bufs = [torch.empty(nf, device=dev, dtype=torch.float32) for _ in range(2)]
         batches = [dd.views(b, B_cap, sc.host_off) for b, sc in zip(bufs, (ent["sc_d"], ent["sc_g"]))]
 
-        def prologue():
-            for b, sc in zip(bufs, (ent["sc_d"], ent["sc_g"])):
+        def prologue(bufs=bufs, scs=(ent["sc_d"], ent["sc_g"])):   # (no reference to ent: no cycle)
+            for b, sc in zip(bufs, scs):
                 dd.gather_into(sc.rows, B_cap, b)
         # the warm-up iterations must leave no trace: parameters, optimizer
         # state (created here where missing: zeros == torch Adam's fresh
@@ -721,7 +754,8 @@ class BucketedGraphTrainer:
         rng = (torch.get_rng_state(), random.getstate())
         try:
             gt = GraphedTrainer(self.t, batches[0], ent["sc_d"], warmup=2, batch_g=batches[1], sc_g=ent["sc_g"],
-                                draw=lambda: self._draw(ent), prologue=prologue)
+                                draw=functools.partial(self._draw, self.t, self.S_cap, ent["state"]),
+                                prologue=prologue)
         finally:
             with torch.no_grad():
                 for t in self._state():

@@ -407,7 +407,10 @@ int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float
  *   (z: K x S x nz), rel0[p] = last_rel[i];
  * ped_scene: Bper int32 scene indices.  Everything else as sgg_lstm_fwd with
  * decoder = 1, c0 = 0; rel0_out (may be NULL) receives rel0 (B x 2) -- the
- * backward's first input -- when act_all != NULL.  Returns SGG_E_ARG where
+ * backward's first input -- when act_all != NULL.  Without act_all (no
+ * saved states) h_all and c_all may both be NULL: the final state (h_T, c_T)
+ * is then not written -- the best-of-k rollout's consumers read rel_out only
+ * (models.py:925 discards the decoder state).  Returns SGG_E_ARG where
  * no kernel family takes the fused start (the caller then runs
  * sgg_decoder_init + sgg_lstm_fwd). */
 typedef struct {
@@ -585,9 +588,10 @@ int sgg_bce_bwd(const float* x, int n, int split, const float* ya, const float* 
  * tensor's device fp32 step counter (torch's capturable Adam state['step']),
  * incremented first (host arrays of n <= 48 pointers).  max_norm <= 0: no clipping; otherwise the
  * clipped gradient is written back, as clip_grad_norm_ does.  ws holds
- * sgg_adam_parts(sum numel) floats (partial norms + per-tensor step scalars +
- * a ticket word that must be zero when ws is first used; every call leaves
- * it at zero).  Two launches with clipping, one without; graph-capturable. */
+ * sgg_adam_parts(sum numel) floats: ws[0] is the one-launch path's ticket
+ * word (zero when ws is first used; every call leaves it at zero and nothing
+ * else writes it, whatever the tensor list or clipping of a call), then the
+ * partial norms and the per-tensor step scalars.  Two launches with clipping, one without; graph-capturable. */
 int sgg_adam_parts(long long total);
 int sgg_adam_step(float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
                   const long long* numel, int n, double lr, double beta1, double beta2, float eps, float max_norm,

@@ -243,3 +243,86 @@ def test_padded_scenes_pack_layout():
                     assert (s, i) not in seen
                     seen.add((int(s), int(i)))
             assert len(seen) == int(so[-1])
+
+
+def test_check_ownership_walks_closures_and_descriptors():
+    """kernels.check_ownership (the launch timer's record-time check): every
+    pointer inside a re-issuable launch's ctypes descriptors must lie in a
+    tensor / storage the closure itself keeps alive -- found through closure
+    cells, bound defaults, functools.partial, nested closures, arrays of
+    descriptors and pointer arrays of nested structs."""
+    import functools
+    from sgan import _native as N
+    from sgan import kernels as K
+    a, b = torch.zeros(32), torch.zeros(16)
+    job = N.L2Job(N.ptr(a), 3, N.ptr(b[4:]))          # a view: its storage counts
+    K.check_ownership(lambda k=(a, b): job)
+    K.check_ownership(functools.partial(lambda j, s: j, job, [a.untyped_storage(), b.untyped_storage()]))
+    inner = lambda: (a, b)   # noqa: E731
+    K.check_ownership(lambda: (inner(), job))          # nested closure holds them
+    with pytest.raises(K.OwnershipError):
+        K.check_ownership(lambda k=(a,): job, "l2")      # b only named by the descriptor
+    arr = (N.L2Job * 2)(job, N.L2Job(N.ptr(a), 1, None))
+    K.check_ownership(lambda: (arr, a, b))
+    with pytest.raises(K.OwnershipError):
+        K.check_ownership(lambda: (arr, a))
+    ge = N.GatEncArgs()
+    ge.w.Wi[1] = N.ptr(b).value
+    with pytest.raises(K.OwnershipError):
+        K.check_ownership(lambda: (ge, a))
+    K.check_ownership(lambda: (ge, b))
+    # an owned descriptor: its kept buffers ride on the instance
+    job2 = N.L2Job(N.ptr(a), 1, N.ptr(b))
+    job2._keep = (a, b)
+    K.check_ownership(lambda: job2)
+
+
+def test_loss_deferral_limit_is_per_kind():
+    """The finish launch takes SGG_LOSSJOB_MAX jobs of EACH kind: a third BCE
+    value is not queued even while the L2 list is empty (it would fail the
+    launch's job check), and eager_losses() turns queueing off."""
+    from sgan import _native as N
+    from sgan import kernels as K
+    K._DEFER[0] += 1
+    saved = dict(K._LOSS)
+    try:
+        K._LOSS.update(l2=[], bce=[object()] * N.LOSSJOB_MAX, keep=[], out=set())
+        assert not K._loss_deferrable("bce")
+        assert K._loss_deferrable("l2")
+        with K.eager_losses():
+            assert not K._loss_deferrable("l2")
+        assert K._loss_deferrable("l2")
+    finally:
+        K._DEFER[0] -= 1
+        K._LOSS.clear()
+        K._LOSS.update(saved)
+
+
+def test_trainer_skips_deferred_finish_when_grads_are_observed():
+    """A parameter hook (or retain_grad) reads gradients during the backward:
+    the trainer's step scope then leaves the deferred finishes out."""
+    from sgan.models import TrajectoryDiscriminator
+    from sgan.train_step import GanTrainer, KernelOps
+
+    class Ops(KernelOps):
+        optimizer = staticmethod(lambda params, lr: torch.optim.Adam(params, lr=lr))
+    g = _gen()
+    d = TrajectoryDiscriminator(8, 12, embedding_dim=16, h_dim=48, mlp_dim=64, batch_norm=False, d_type="global")
+    tr = GanTrainer(g, d, ops=Ops())
+    assert not tr._grad_observed()
+    h = next(iter(d.parameters())).register_hook(lambda gr: gr)
+    assert tr._grad_observed()
+    h.remove()
+    assert not tr._grad_observed()
+
+
+def test_bucketed_trainer_requires_a_padding_scene():
+    from sgan.train_step import BucketedGraphTrainer
+
+    class _T:
+        class dp:
+            on = False
+            world = 1
+    with pytest.raises(ValueError):
+        BucketedGraphTrainer(_T(), None, batch_size=64, pad_scenes=0)
+    assert BucketedGraphTrainer(_T(), None, batch_size=64, pad_scenes=1).S_cap == 65
