@@ -212,6 +212,42 @@ def roofline_of(name, a):
                     "re-issues of each launch on its stream); traffic = PMC HBM bytes of the named launch (null if not profiled)"}
 
 
+# the reference's work per 20-ped scene and training
+# iteration (D-step 0.42 + G-step 1.87 GFLOP; context x 20, the unfolded
+# pooling MLP, every sample's backward)
+REFERENCE_FLOP_PER_SCENE = 2.29e9
+
+
+def iteration_roofline(agg, ms_step, scenes):
+    """The whole iteration against the roofline, from the executed-work model:
+    every instrumented launch's algorithmic FLOP and bytes (the work models
+    the per-kernel table divides by).  A launch cannot
+    finish faster than max(FLOP / fp32 peak, bytes / HBM peak); the sum of
+    those bounds over the iteration's launches is its roofline time, and
+    frac = roofline time / measured time per iteration."""
+    fl = by = t_roof = t_meas = 0.0
+    for a in agg.values():
+        for _key, r, per_it in a["shapes"]:
+            fl += per_it * r["flop"]
+            by += per_it * r["bytes"]
+            t_roof += per_it * max(r["flop"] / (FP32_PEAK_TFLOPS * 1e12), r["bytes"] / (HBM_PEAK_GBS * 1e9))
+            t_meas += per_it * r["ms"] * 1e-3
+    t = ms_step * 1e-3
+    return {"flop": fl, "bytes": by, "flop_per_scene": fl / scenes,
+            "achieved_tflops": round(fl / t / 1e12, 3), "achieved_gbs": round(by / t / 1e9, 1),
+            "roofline_us": round(t_roof * 1e6, 2), "instrumented_device_us": round(t_meas * 1e6, 1),
+            "measured_us": round(t * 1e6, 1), "frac": round(t_roof / t, 4),
+            "reference_flop_per_scene": REFERENCE_FLOP_PER_SCENE,
+            "reference_equivalent_tflops": round(REFERENCE_FLOP_PER_SCENE * scenes / t / 1e12, 2),
+            "note": "executed-work model: the algorithmic FLOP / bytes of every instrumented launch of one iteration "
+                    "(the per-kernel work models); roofline_us = sum over launches of max(FLOP / 157.3 TFLOP/s, "
+                    "bytes / 8 TB/s); frac = roofline_us / measured_us.  The reference's own work (2.29 GFLOP per "
+                    "scene, SURVEY.md 8d) is larger: the build computes the context once instead of best_k times, "
+                    "folds the input embeddings, rolls out the best_k samples without autograd and skips discarded "
+                    "gradients (DESIGN.md section 4, executed-work model); reference_equivalent_tflops is that work "
+                    "over the measured time (above the fp32 peak because of those de-duplications)"}
+
+
 def real_data_leg(dev, iters=20, warmup=3, batch=64):
     """configs[1] on REAL data: training iterations over the zara1 train split
     (tests/golden/datasets_group/zara1/train, the reference's datasets_group
@@ -323,7 +359,8 @@ def spawn(n):
 
 
 def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
-    """-> (run(k): k training iterations, graphed?).  Graphed on one rank: a
+    """-> (run(k): k training iterations, graphed?, the one-iteration
+    GraphedTrainer or None).  Graphed on one rank: a
     HIP graph of GRAPH_ITERS iterations replayed k // GRAPH_ITERS times (the
     per-replay graph launch paid once per GRAPH_ITERS iterations) and a
     one-iteration graph for the remainder, so run(k) does exactly k."""
@@ -346,22 +383,24 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
                     k %= GRAPH_ITERS
                 for _ in range(k):
                     g1.step()
-            return run, True
+            return run, True, g1
         except Exception as e:  # capture unsupported (e.g. a collective): eager
             print("bench: graph capture failed (%s: %s); running eager" % (type(e).__name__, e), file=sys.stderr)
             torch.cuda.synchronize()
     def eager(k):
         for _ in range(k):
             trainer.step(batch, sc, batch_g, sc_g, **kw)
-    return eager, False
+    return eager, False, None
 
 
-def timed_run(run, steps, warmup, world, dev):
+def timed_run(run, steps, warmup, world, dev, on_start=None):
     run(warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if on_start is not None:
+        on_start()
     t0 = time.perf_counter()
     run(steps)   # exactly `steps` iterations
     torch.cuda.synchronize()
@@ -403,8 +442,17 @@ def measure(spec, steps, warmup, rank, world, dev, graph_on, n_it=3):
     K.set_precision(spec["prec"])
     try:
         trainer, batch, sc, batch_g, sc_g, kw = setup(spec["per_gpu"], spec["peds"], rank, world, dev, spec["graph"])
-        step, graphed = make_step(trainer, batch, sc, batch_g, sc_g, kw, graph_on, world)
-        elapsed = timed_run(step, steps, warmup, world, dev)
+        step, graphed, gt = make_step(trainer, batch, sc, batch_g, sc_g, kw, graph_on, world)
+        comm = gt is not None and world > 1
+        elapsed = timed_run(step, steps, warmup, world, dev, on_start=gt.time_allreduce if comm else None)
+        # N > 1: HIP events around each eager gradient all-reduce between the
+        # graph segments, on this rank, max over ranks
+        ar_us = gt.allreduce_ms() * 1e3 / steps if comm else None
+        if ar_us is not None:
+            t = torch.tensor([ar_us], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ar_us = float(t)
+            gt.time_allreduce(False)
         n_it = max(1, min(steps, n_it))
         K.timer.start()
         for _ in range(n_it):
@@ -413,7 +461,8 @@ def measure(spec, steps, warmup, rank, world, dev, graph_on, n_it=3):
         timed = K.timer.replay(recs)
     finally:
         K.set_precision("fp32")
-    return dict(elapsed=elapsed, graphed=graphed, agg=kernel_table(timed, n_it), recs=recs, n_it=n_it)
+    return dict(elapsed=elapsed, graphed=graphed, agg=kernel_table(timed, n_it), recs=recs, n_it=n_it,
+                allreduce_us=ar_us)
 
 
 def top_kernels(agg, n=10):
@@ -434,7 +483,11 @@ def leg_line(name, spec, res, steps):
             "peds_per_scene": spec["peds"], "generator": spec["graph"], "dtype": spec["prec"],
             "hip_graph": res["graphed"],
             "instrumented_launches_per_iter": round(sum(a["launches_per_iter"] for a in agg.values()), 1),
-            "roofline": roofline_of(dom_name, dom), "kernels": top_kernels(agg, 5)}
+            "roofline": dict(roofline_of(dom_name, dom),
+                             # (fp32 legs: the bf16 node transforms would need their own peak)
+                             iteration=iteration_roofline(agg, ms, spec["per_gpu"]) if spec["prec"] == "fp32"
+                             else None),
+            "kernels": top_kernels(agg, 5)}
 
 
 def main():
@@ -482,7 +535,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-        assert dist.get_world_size() == args.gpus
+        # the collective library must see exactly the N ranks the line reports
+        if dist.get_world_size() != args.gpus or dist.get_backend() != backend:
+            raise SystemExit("bench: %s process group reports world size %d (backend %s), expected %d"
+                             % (backend, dist.get_world_size(), dist.get_backend(), args.gpus))
 
     if args.leg:
         head = dict(LEGS[args.leg])
@@ -530,7 +586,7 @@ def main():
         # of the strong-scaling curve the N > 1 runs measure
         from sgan import kernels as K
         tr4, b4, sc4, bg4, scg4, kw4 = setup(CONFIG4_GLOBAL, args.peds, 0, 1, dev, "gat")
-        st4, gr4 = make_step(tr4, b4, sc4, bg4, scg4, kw4, args.graph)
+        st4, gr4, _ = make_step(tr4, b4, sc4, bg4, scg4, kw4, args.graph)
         k4 = max(3, args.steps // 4)
         e4 = timed_run(st4, k4, 2, 1, dev)
         scaling_ref = {"global_batch": CONFIG4_GLOBAL, "n_gpus": 1, "steps": k4, "ms_per_step": round(e4 / k4 * 1e3, 3),
@@ -548,6 +604,7 @@ def main():
         top = sorted(agg.items(), key=lambda kv: -kv[1]["us_per_iter"])
         dom_name, dom = top[0]
         roofline = roofline_of(dom_name, dom)
+        roofline["iteration"] = iteration_roofline(agg, elapsed / args.steps * 1e3, per_gpu)
         launches = sorted(((r["launches"] / n_it * r["ms"] * 1e3, n, r, k) for n, a in agg.items()
                            for k, r, _ in a["shapes"]), key=lambda x: -x[0])
         launch_table = [{"kernel": n, "shape": list(k[1:]), "per_iter": round(r["launches"] / n_it, 2),
@@ -556,9 +613,13 @@ def main():
         total_launch_us = sum(x[0] for x in launches)
         if os.environ.get("SGG_BENCH_TABLE"):   # every instrumented launch (the JSON line keeps the top 30)
             with open(os.environ["SGG_BENCH_TABLE"], "w") as f:
+                f.write("# kernel | launch shape | launches per iteration | avg us | us per iteration | algorithmic "
+                        "FLOP per launch | algorithmic bytes per launch | roofline us per launch\n")
                 for us, n, r, k in launches:
-                    f.write("%-50s %-36s %5.2f %8.2f %8.1f\n" % (n[:50], str(list(k[1:]))[:36], r["launches"] / n_it,
-                                                              r["ms"] * 1e3, us))
+                    rl = max(r["flop"] / (FP32_PEAK_TFLOPS * 1e12), r["bytes"] / (HBM_PEAK_GBS * 1e9)) * 1e6
+                    f.write("%-50s %-36s %5.2f %8.2f %8.1f %12.4g %12.4g %8.3f\n" % (
+                        n[:50], str(list(k[1:]))[:36], r["launches"] / n_it, r["ms"] * 1e3, us, r["flop"],
+                        r["bytes"], rl))
         ms_step = elapsed / args.steps * 1e3
         value = world * per_gpu / (elapsed / args.steps)
         cpu = None
@@ -598,6 +659,16 @@ def main():
             line["real_data"] = real
         if pmc_target is not None:
             line["pmc_target"] = pmc_target
+        if world > 1:
+            ar = res["allreduce_us"]
+            line["communication"] = {
+                "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                "allreduce_us_per_iter": round(ar, 1) if ar is not None else None,
+                "compute_us_per_iter": round(ms_step * 1e3 - ar, 1) if ar is not None else None,
+                "allreduces_per_iter": 2,
+                "note": "HIP events around each eager gradient all-reduce (one flat SUM bucket per optimizer step, "
+                        "between the HIP-graph segments), summed per iteration, max over ranks; compute = "
+                        "ms_per_step - all-reduce time"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -239,13 +239,63 @@ struct Layout {
   int wts;        // the module's weights, staged once per workgroup (odd row pitches)
   int total;      // floats
   int PH, NP, NPP;
+  int compact;    // backward plan for scenes past the full plan (see make_compact_layout)
 };
 
-__host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
+constexpr int kLdsFloats = 160 * 1024 / 4;
+
+// The backward's plan when the full one (every forward activation resident
+// beside the gradients) exceeds the LDS -- scenes of 49 .. 64 peds with one
+// head.  It needs the forward's saved state and keeps only what the phase at
+// hand reads, aliased by lifetime:
+//   * yI / gout (the out embedding's input), preG / preI (the epilogue
+//     backwards) are read straight from the saved state in global memory,
+//     once per element;
+//   * one region U holds the inter layers' operands -- G1 | dH | gin | dpre --
+//     during the inter backward, then the intra layers' -- H1 | dH | X --
+//     loaded after the group-mean backward (H1 over the dead G1, X over the
+//     dead gin / dpre; dH at the same offset in both).  The extra memory
+//     round trip of H1 / X is the price (the inter operands arrive with dy).
+__host__ __device__ inline Layout make_compact_layout(int np, int nh) {
   Layout L;
   L.NP = np;
   L.PH = FH * nh + 1;
   L.NPP = att_pitch(np);
+  L.compact = 1;
+  int o = 0;
+  auto take = [&](int n) { const int r = o; o += (n + 3) & ~3; return r; };
+  L.s = take(np);
+  L.t = take(np);
+  L.ds = take(np);
+  L.dt = take(np);
+  L.attm = take(np * L.NPP);
+  L.dz = take(np * L.NPP);
+  L.Wh = take(np * P72);
+  L.dWh = take(np * P72);
+  L.dI = take(np * P16);
+  L.dG = take(np * P16);
+  const int ph = (np * L.PH + 3) & ~3, p16 = (np * P16 + 3) & ~3;
+  const int u = take(2 * ph + (np * P40 > 2 * p16 ? np * P40 : 2 * p16));
+  L.G1 = L.H1 = u;
+  L.dH = u + ph;
+  L.gin = L.X = u + 2 * ph;
+  L.dpre = u + 2 * ph + p16;
+  L.yI = L.preI = L.preG = L.gout = L.sp = L.tp = 0;   // (not resident)
+  L.WhIs = L.stIs = L.WhIOs = L.stIOs = L.WhGs = L.stGs = L.WhGOs = L.stGOs = 0;
+  L.ints = take(ints_floats(np));
+  L.wts = take(weights_floats(nh));
+  L.total = o;
+  return L;
+}
+
+// full: every buffer of either direction resident (bwd 2: this plan even
+// when it does not fit -- the recompute backward has no other)
+__host__ __device__ inline Layout make_layout(int np, int nh, int bwd) {
+  Layout L;
+  L.NP = np;
+  L.PH = FH * nh + 1;
+  L.NPP = att_pitch(np);
+  L.compact = 0;
   int o = 0;
   auto take = [&](int n) { const int r = o; o += (n + 3) & ~3; return r; };
   L.X = take(np * P40);
@@ -276,7 +326,7 @@ __host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
     // rest of the plan (else 0: loaded per layer into the Wh scratch)
     const int rest = ((ints_floats(np) + 3) & ~3) + ((weights_floats(nh) + 3) & ~3);
     const int pre = 2 * (((nh * np * P72 + 3) & ~3) + ((nh * 2 * np + 3) & ~3) + ((np * P16 + 3) & ~3) + ((2 * np + 3) & ~3));
-    if (o + pre + rest <= 160 * 1024 / 4) {
+    if (o + pre + rest <= kLdsFloats) {
       L.WhIs = take(nh * np * P72);
       L.stIs = take(nh * 2 * np);
       L.WhIOs = take(np * P16);
@@ -295,6 +345,7 @@ __host__ __device__ inline Layout make_layout(int np, int nh, bool bwd) {
   L.ints = take(ints_floats(np));
   L.wts = take(weights_floats(nh));
   L.total = o;
+  if (bwd == 1 && L.total > kLdsFloats) return make_compact_layout(np, nh);
   return L;
 }
 
@@ -734,6 +785,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     const PLayout PL = make_playout(NH);
     const SLayout SL = make_slayout(NPo, NH);
     const int PH = L.PH, NP = L.NP, NPP = L.NPP;
+    const bool compact = BWD && L.compact;   // uniform (the host requires the saved state for it)
     const int SLH = NP * FH + 2 * NP;
     float* X = sm + L.X;
     float* H1 = sm + L.H1;
@@ -763,7 +815,9 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     const bool first = pre && sc == (int)blockIdx.x;   // uniform
     float* saved = p.saved ? p.saved + (size_t)sc * SL.total : nullptr;
     // ---- inputs and group structure (one phase) ------------------------
-    if (first) {
+    if (compact) {
+      // (X arrives with H1 before the intra backward)
+    } else if (first) {
 #pragma unroll
       for (int m = 0; m < kXPre; ++m) {
         const int e = tid + m * (int)blockDim.x;
@@ -908,6 +962,11 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         rows_to_global(saved + SL.gout, gout, P16, M, FO);
         rows_to_global(saved + SL.ints, lab, 0, 1, ints_floats(NP));
       }
+    } else if (compact) {
+      // the inter backward's operands (the intra ones come after it)
+      rows_from_global(gin, P16, saved + SL.gin, M, FO);
+      rows_from_global(G1, PH, saved + SL.G1, M, FH * nh);
+      lds_barrier();
     } else if (!preload) {
       // backward with the forward's saved state: no recompute
       rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
@@ -978,9 +1037,18 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
           dy[i * PDY + k] = v;
         }
       }
-      for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
-        const int i = e / (2 * FO), c = e - i * 2 * FO;
-        v[i * PV + c] = c < FO ? yI[i * P16 + c] : gout[grank[i] * P16 + c - FO] * ginv[i];
+      if (compact) {   // yI / gout straight from the saved state
+        const float* yIg = saved + SL.yI;
+        const float* goutg = saved + SL.gout;
+        for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
+          const int i = e / (2 * FO), c = e - i * 2 * FO;
+          v[i * PV + c] = c < FO ? yIg[i * FO + c] : goutg[grank[i] * FO + c - FO] * ginv[i];
+        }
+      } else {
+        for (int e = tid; e < n * 2 * FO; e += blockDim.x) {
+          const int i = e / (2 * FO), c = e - i * 2 * FO;
+          v[i * PV + c] = c < FO ? yI[i * P16 + c] : gout[grank[i] * P16 + c - FO] * ginv[i];
+        }
       }
     }
     lds_barrier(); PMARK(17);
@@ -1008,7 +1076,10 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     }
     lds_barrier(); PMARK(19);
     // ---- inter out layer ----
-    epi_bwd(dG, P16, preG, P16, M, FO, 2);
+    if (compact)
+      epi_bwd(dG, P16, saved + SL.preG, FO, M, FO, 2);
+    else
+      epi_bwd(dG, P16, preG, P16, M, FO, 2);
     const float* WhL = Wh;   // the layer's Wh / s / t: the preloaded copies, or the Wh scratch
     int ldL = P72;
     const float *sL = s, *tL = t;
@@ -1073,9 +1144,19 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       const int i = e / FO, f = e - i * FO;
       dI[i * P16 + f] = fmaf(ginv[i], dG[grank[i] * P16 + f], dI[i * P16 + f]);
     }
+    if (compact) {   // the intra backward's operands, over the dead inter ones
+      rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
+      for (int e = tid; e < n * FI; e += blockDim.x) {
+        const int r = e / FI;
+        X[r * P40 + (e - r * FI)] = xval(o, e);
+      }
+    }
     lds_barrier(); PMARK(24);
     // ---- intra out layer ----
-    epi_bwd(dI, P16, preI, P16, n, FO, 2);
+    if (compact)
+      epi_bwd(dI, P16, saved + SL.preI, FO, n, FO, 2);
+    else
+      epi_bwd(dI, P16, preI, P16, n, FO, 2);
     WhL = Wh;
     ldL = P72;
     sL = s;
@@ -1188,8 +1269,8 @@ extern "C" long long sgg_gatenc_saved_floats(int S, int max_n, int nh) {
 }
 
 extern "C" long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd) {
-  if (max_n < 1 || nh < 1 || nh > kGatEncMaxHeads) return -1;
-  return 4ll * make_layout(max_n, nh, bwd != 0).total;
+  if (max_n < 1 || nh < 1 || nh > kGatEncMaxHeads || bwd < 0 || bwd > 2) return -1;
+  return 4ll * make_layout(max_n, nh, bwd).total;
 }
 
 static int gatenc_check(const char* who, const GatEncArgs* a, int bwd) {
@@ -1214,6 +1295,10 @@ static int gatenc_check(const char* who, const GatEncArgs* a, int bwd) {
   }
   const long long lds = sgg_gatenc_lds_bytes(a->np, a->nh, bwd);
   SGG_CHECK_ARG(lds <= 160 * 1024, "%s: %d peds x %d heads need %lld B of LDS (> 160 KiB)", who, a->np, a->nh, lds);
+  if (bwd)
+    SGG_CHECK_ARG(a->saved || sgg_gatenc_lds_bytes(a->np, a->nh, 2) <= 160 * 1024,
+                  "%s: %d peds x %d heads: the backward fits the LDS only with the forward's saved state", who, a->np,
+                  a->nh);
   return 0;
 }
 

@@ -1388,7 +1388,10 @@ def gat_encoder_fused_ok(scenes, nh, need_grad):
     """The fused GATEncoder path holds a scene in one workgroup's LDS."""
     if not GATENC_FUSED or nh < 1 or nh > N.MAX_HEADS or scenes.max_n > 64:
         return False
-    return _lib().sgg_gatenc_lds_bytes(max(scenes.max_n, 1), nh, int(bool(need_grad))) <= 160 * 1024
+    # the backward's plan: with the forward's saved state (compact for
+    # 49 .. 64-ped scenes) or, SGG_GATENC_SAVE=0, the recomputing one
+    plan = (1 if GATENC_SAVE else 2) if need_grad else 0
+    return _lib().sgg_gatenc_lds_bytes(max(scenes.max_n, 1), nh, plan) <= 160 * 1024
 
 
 def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None, link=None):

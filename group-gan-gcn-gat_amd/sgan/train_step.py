@@ -443,6 +443,7 @@ class GraphedTrainer:
         order before it), so the per-replay graph launch is paid once per
         `iters` iterations; step() then advances `iters` iterations."""
         self.t = trainer
+        self.ar_events = None   # time_allreduce()
         self.iters = iters = max(1, int(iters))
         self.prologue = prologue or (lambda: None)
         self.batch, self.sc = batch, sc
@@ -594,9 +595,28 @@ class GraphedTrainer:
         for g, tensors in self.segments:
             g.replay()
             if tensors is not None:
-                self.t.dp.allreduce_(tensors)
+                if self.ar_events is not None:   # HIP events around the collective (bench.py)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    self.t.dp.allreduce_(tensors)
+                    e1.record()
+                    self.ar_events.append((e0, e1))
+                else:
+                    self.t.dp.allreduce_(tensors)
         self._after_replay(None)
         return self.losses
+
+    def time_allreduce(self, on=True):
+        """Record HIP events around every gradient all-reduce of the following
+        replays (several ranks); allreduce_ms() sums them."""
+        self.ar_events = [] if on else None
+
+    def allreduce_ms(self):
+        """Device time of the recorded all-reduces (ms, summed); synchronises."""
+        if not self.ar_events:
+            return 0.0
+        self.ar_events[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.ar_events)
 
     @staticmethod
     def _after_replay(grads):
@@ -638,8 +658,8 @@ class BucketedGraphTrainer:
 
     A bucket is (B_cap, np_cap): np_cap, the largest scene it holds, is the
     smallest of `np_caps` that fits both batches (the kernels size their LDS
-    plans by it; the one-launch GAT encoder's backward holds scenes of <= 48
-    peds, larger ones take the per-layer GAT kernels).
+    plans by it; the one-launch GAT encoder takes scenes of up to 64 peds --
+    its backward past 49 on the compact LDS plan).
 
     Capturing a new bucket runs GraphedTrainer's warm-up iterations; the
     parameters, the optimizer state and the host RNG states are saved before

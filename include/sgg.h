@@ -673,6 +673,13 @@ int sgg_gatenc_param_size(int nh);
  * and the backward reads them instead of recomputing the forward (it must
  * then be called with the same saved buffer, np and nh). */
 long long sgg_gatenc_saved_floats(int S, int max_n, int nh);
+/* LDS bytes of a launch's plan (<= 160 KiB to run): bwd 0 the forward, 1 the
+ * backward with the forward's saved state (scenes past the full plan, e.g.
+ * 49 .. 64 peds with one head, take a compact plan that aliases the inter /
+ * intra layers' operands and reads the epilogue inputs from the saved
+ * state), 2 the backward without it (recomputing the forward: the full plan
+ * only).  sgg_gatenc_bwd refuses a launch whose plan needs the saved state
+ * when args->saved is NULL. */
 long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd);
 int sgg_gatenc_fwd(const SggGatEncArgs* args, void* stream);
 int sgg_gatenc_bwd(const SggGatEncArgs* args, void* stream);

@@ -429,6 +429,11 @@ def test_bench_gpus2_spawns_two_ranks():
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 32 and line["config"]["parallelism"] == "dp2"
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    # the N > 1 line separates communication from compute
+    comm = line["communication"]
+    assert comm["world_size"] == 2 and comm["backend"] == "gloo"
+    assert comm["allreduce_us_per_iter"] > 0 and comm["compute_us_per_iter"] > 0
+    assert comm["allreduce_us_per_iter"] < line["ms_per_step"] * 1e3
 
 
 # ---------------------------------------------------------------------------

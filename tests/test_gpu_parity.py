@@ -292,18 +292,34 @@ def test_train_step_vs_reference_fixture(selective):
     Adam, seeded host RNGs) reproduced by GanTrainer: losses within 1e-4 rel,
     the gradients each optimizer step consumed (D raw, G after the 2.0 clip)
     within 1e-3 of the tensor max (floor 1 % of the step's largest gradient),
-    weights within Adam's sign-flip bound on noise-level gradients."""
+    weights within Adam's sign-flip bound on noise-level gradients, and --
+    the update itself pinned -- within 1 % of lr of torch.optim.Adam on CPU
+    applied to the same pre-step weights with the gradients the step
+    consumed (a CPU twin of each optimizer, stepped alongside)."""
     from sgan.scene import SceneIndex
     from sgan.train_step import GanTrainer
     g, d = build_models()
     tr = GanTrainer(g, d, selective_backward=selective)
     f = npz("train_step.npz")
+    # CPU twins: copies of the weights, torch's Adam with the trainer's lrs
+    twins = {}
+    for mod, tag, lr in ((g, "g", 1e-4), (d, "d", 1e-3)):
+        cp = {k: p.detach().cpu().clone().requires_grad_(True) for k, p in mod.named_parameters()}
+        twins[tag] = (cp, torch.optim.Adam(list(cp.values()), lr=lr))
     torch.manual_seed(1234)
     random.seed(1234)
     for it in range(2):
         b = [T(f["b%d/%s" % (it, k)]) for k in KEYS]
         sc = SceneIndex.from_seq_start_end(b[-1], DEV)
         ld, lg = tr.step(b, sc)
+        for mod, tag, lr in ((g, "g", 1e-4), (d, "d", 1e-3)):
+            cp, opt = twins[tag]
+            for k, p in mod.named_parameters():
+                cp[k].grad = p.grad.detach().cpu().clone() if p.grad is not None else None
+            opt.step()
+            for k, p in mod.named_parameters():
+                err = (p.detach().cpu() - cp[k].detach()).abs().max().item()
+                assert err <= 1e-2 * lr + 1e-6 * cp[k].abs().max().item(), ("Adam update", it, tag, k, err)
         for k, v in list(ld.items()) + list(lg.items()):
             tag = "D" if k.startswith("D") else "G"
             ref = float(f["it%d/%s/%s" % (it, tag, k)])
@@ -785,12 +801,18 @@ def test_graphed_trainer_multi_iteration_equals_eager():
         assert err <= 1e-5 + 1e-5 * wa[k].abs().max().item(), (k, err)
 
 
-@pytest.mark.parametrize("nh,sizes", [(1, [1, 2, 20, 48, 13, 5]), (1, [20] * 70), (2, [20, 7, 24, 1])])
+@pytest.mark.parametrize("nh,sizes", [(1, [1, 2, 20, 48, 13, 5]), (1, [20] * 70), (2, [20, 7, 24, 1]),
+                                      # past the full backward plan: the compact one (57 / 64 peds), and
+                                      # 49 (the full plan's last size) -- real zara1 scenes reach 57
+                                      (1, [49, 57, 64, 20, 3]), (1, [64] * 40 + [57] * 7),
+                                      (2, [49, 57, 64, 20])])
 def test_gat_encoder_fused_equals_per_layer(nh, sizes):
     """The one-launch GATEncoder (sgg_gatenc_fwd / _bwd + sgg_slab_reduce)
     against the per-layer kernels on the same module: outputs, input and
     parameter gradients; label patterns with singletons (label 0), one big
-    group, mixed groups, one-ped scenes."""
+    group, mixed groups, one-ped scenes.  Two heads at 49+ peds exceed every
+    LDS plan: the module takes the per-layer kernels there (checked to be
+    refused, and the module's result checked against the oracle instead)."""
     from sgan import kernels as K
     from sgan.models import GATEncoder
     from sgan.scene import SceneIndex
@@ -805,6 +827,10 @@ def test_gat_encoder_fused_equals_per_layer(nh, sizes):
     lab = torch.from_numpy(np.concatenate(labs).astype(np.float32)).to(DEV).view(-1, 1)
     x = torch.randn(B, 40, device=DEV)
     dy = torch.randn(B, 24, device=DEV)
+    if nh > 1 and max(sizes) > 48:
+        assert not K.gat_encoder_fused_ok(sc, nh, True)
+        _gat_encoder_vs_oracle(mod, nh, x, lab, sc, dy)
+        return
     res = []
     for fused in (True, False):
         K.GATENC_FUSED = fused
@@ -832,6 +858,28 @@ def test_gat_encoder_fused_equals_per_layer(nh, sizes):
     fl = 1e-2 * max(float(g.abs().max()) for g in gr.values())
     for k in gr:
         close(gf[k], gr[k].cpu().numpy(), rtol=2e-4, floor=fl, what="fused d" + k)
+
+
+def _gat_encoder_vs_oracle(mod, nh, x, lab, sc, dy):
+    """The product GATEncoder (whatever path it takes) against the oracle's
+    reference-formulation module with the same weights: output, dx, grads."""
+    from oracle import sgan_oracle as O
+    ref = O.GATEncoder([40, 16, 40], nh, 0.0, 0.2)
+    ref.load_state_dict({k: v.detach().cpu() for k, v in mod.state_dict().items()})
+    sse = torch.tensor(np.stack([sc.host_off[:-1], sc.host_off[1:]], 1))
+    xr = x.detach().cpu().clone().requires_grad_(True)
+    yr = ref(xr, sse, None, lab.cpu())
+    (yr * dy.cpu()).sum().backward()
+    mod.zero_grad(set_to_none=True)
+    xi = x.clone().requires_grad_(True)
+    y = mod(xi, None, None, lab, scenes=sc)
+    (y * dy).sum().backward()
+    close(y, yr.detach().numpy(), rtol=2e-5, what="out vs oracle")
+    close(xi.grad, xr.grad.numpy(), rtol=1e-4, what="dx vs oracle")
+    gref = dict(ref.named_parameters())
+    fl = 1e-2 * max(float(g.grad.abs().max()) for g in gref.values())
+    for k, q in mod.named_parameters():
+        close(q.grad, gref[k].grad.numpy(), rtol=2e-4, floor=fl, what="d%s vs oracle" % k)
 
 
 @pytest.mark.parametrize("prec,sizes", [("fp32", [1, 2, 20, 48, 13, 5, 64]), ("fp32", [20] * 600),
