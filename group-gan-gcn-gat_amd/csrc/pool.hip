@@ -423,6 +423,207 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
   }
 }
 
+// ---- forward, bf16 layer 2 ----------------------------------------------------
+// The opt-in bf16 precision (sgg_pool_fwd_bf16; BASELINE configs 3 and 5): the
+// 512 -> bn contraction on v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+// The hidden unit is formed exactly as above in fp32 (2 FMA + max) and only
+// then rounded to bf16 (round-to-nearest-even) as the A operand; W2 is
+// rounded when its k-tile is staged.  A 32-deep k-step gives a lane 8
+// consecutive units 8 kq .. 8 kq + 7 of its pair (A[row = pair][k]) and of
+// its column (B[k][col] = W2[col][k]), so the U row, (A_x, A_y) and W2 reads
+// are 16-byte LDS reads; one bf16 MFMA replaces eight f32 ones (16 vs 8 x 32
+// cycles), and the VALU work of the hidden units becomes the step's cost.
+// Same chunks, XCD order, epilogue (max over j with the smallest j on ties)
+// as pool_fwd_kernel.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+constexpr int kBfUP = kKT + 4;   // U tile row pitch (floats; 16-B rows)
+constexpr int kBfWP = kKT + 8;   // W2 tile row pitch (bf16; 16-B rows)
+
+template <int BN, int GPW>
+__global__ void __launch_bounds__(256) pool_fwd_bf16_kernel(
+    const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
+    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
+    const int32_t* __restrict__ nchunks_dev, float* __restrict__ out, int32_t* __restrict__ argmax) {
+  constexpr int NT = PoolCfg<BN>::NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Us = reinterpret_cast<float*>(smem);                                   // 64 x kBfUP
+  float* As = Us + SGG_POOL_MAX_PEDS * kBfUP;                                   // 64 units x (A_x, A_y)
+  __bf16* W2s = reinterpret_cast<__bf16*>(As + 2 * kKT);                        // 16 NT rows x kBfWP
+  float2* ps = reinterpret_cast<float2*>(W2s + 16 * NT * kBfWP);                // scene positions (<= 64)
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // 64 x BN
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kq = lane >> 4;
+
+  const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);   // XCD-aware (pool_fwd_kernel)
+  const int nch = nchunks_dev ? *nchunks_dev : nchunks;
+  for (int ch = xb; ch < nch; ch += gridDim.x) {
+    const int4 cd = chunks[ch];
+    const int s = cd.x, i0 = cd.y, i1 = cd.z;
+    if (i1 <= i0) continue;
+    const int o = scene_off[s];
+    const int n = scene_off[s + 1] - o;
+    const int rows = i1 - i0;
+    const int npairs = rows * n;
+
+    for (int q = threadIdx.x; q < n; q += blockDim.x) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) keys[q] = 0ull;
+    __syncthreads();
+
+    int uoff[GPW];
+    float rx[GPW], ry[GPW];
+    floatx4 acc[GPW][NT];
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int p = (wave * GPW + g) * 16 + c16;
+      int il = 0, j = 0;
+      if (p < npairs) { il = p / n; j = p - il * n; }
+      uoff[g] = j * kBfUP + 8 * kq;
+      const float2 pj = ps[j], pi = ps[i0 + il];
+      rx[g] = p < npairs ? pj.x - pi.x : 0.f;
+      ry[g] = p < npairs ? pj.y - pi.y : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + 255) / 256;   // float4 of U per thread
+    constexpr int kWQ = (16 * NT * (kKT / 4) + 255) / 256;            // float4 of W2 per thread
+    float4 ureg[kUQ], wreg[kWQ];
+    float areg = 0.f;
+    auto load_tile = [&](int k0) {
+#pragma unroll
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n) ureg[e] = *reinterpret_cast<const float4*>(U + (size_t)(o + r) * kHidden + k0 + 4 * c4);
+      }
+#pragma unroll
+      for (int e = 0; e < kWQ; ++e) {   // W2 rows (nn.Linear layout), rows >= BN are zero
+        const int q = threadIdx.x + 256 * e;
+        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
+        wreg[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c < BN) wreg[e] = *reinterpret_cast<const float4*>(W2 + (size_t)c * kHidden + k0 + 4 * c4);
+      }
+      if (threadIdx.x < 2 * kKT) areg = A[2 * k0 + threadIdx.x];
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n) *reinterpret_cast<float4*>(Us + r * kBfUP + 4 * c4) = ureg[e];
+      }
+#pragma unroll
+      for (int e = 0; e < kWQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
+        if (c < 16 * NT) {
+          __bf16* d = W2s + c * kBfWP + 4 * c4;
+          d[0] = (__bf16)wreg[e].x;
+          d[1] = (__bf16)wreg[e].y;
+          d[2] = (__bf16)wreg[e].z;
+          d[3] = (__bf16)wreg[e].w;
+        }
+      }
+      if (threadIdx.x < 2 * kKT) As[threadIdx.x] = areg;   // (A_x, A_y) of unit k at 2 k, 2 k + 1
+    };
+    load_tile(0);
+    __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
+    store_tile();
+    __syncthreads();
+    for (int k0 = 0; k0 < kHidden; k0 += kKT) {
+      if (k0 + kKT < kHidden) load_tile(k0 + kKT);
+#pragma unroll
+      for (int s2 = 0; s2 < kKT / 32; ++s2) {
+        const int kb = 32 * s2 + 8 * kq;   // the lane's 8 units in this k-step
+        float av[16];
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          *reinterpret_cast<float4*>(&av[4 * v]) = *reinterpret_cast<const float4*>(As + 2 * kb + 4 * v);
+        bf16x8_t bfr[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bfr[t] = *reinterpret_cast<const bf16x8_t*>(W2s + (16 * t + c16) * kBfWP + kb);
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) {
+          float uv[8];
+          *reinterpret_cast<float4*>(&uv[0]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 32 * s2);
+          *reinterpret_cast<float4*>(&uv[4]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 32 * s2 + 4);
+          bf16x8_t h;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            h[e] = (__bf16)fmaxf(fmaf(av[2 * e + 1], ry[g], fmaf(av[2 * e], rx[g], uv[e])), 0.f);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bfr[t], acc[g][t], 0, 0, 0);
+        }
+      }
+      __syncthreads();  // tile consumed
+      if (k0 + kKT < kHidden) {
+        store_tile();
+        __syncthreads();
+      }
+    }
+
+    // epilogue: bias, ReLU, max over j (as pool_fwd_kernel)
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int grp = wave * GPW + g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = grp * 16 + kq * 4 + r;
+        if (p < npairs) {
+          const int il = p / n, j = p - il * n;
+          const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int cc = 16 * t + c16;
+            if (cc < BN) {
+              float v = acc[g][t][r] + b2[cc];
+              v = v > 0.f ? v : 0.f;
+              atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) {
+      const unsigned long long key = keys[q];
+      const size_t oi = (size_t)(o + i0) * BN + q;
+      out[oi] = __uint_as_float((unsigned)(key >> 32));
+      argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+    }
+    __syncthreads();
+  }
+}
+
+template <int BN>
+static size_t pool_fwd_bf16_lds(int max_rows) {
+  return sizeof(float) * ((size_t)SGG_POOL_MAX_PEDS * kBfUP + 2 * kKT) +
+         sizeof(__bf16) * (size_t)16 * PoolCfg<BN>::NT * kBfWP + sizeof(float2) * SGG_POOL_MAX_PEDS +
+         sizeof(unsigned long long) * (size_t)max_rows * BN;
+}
+
+template <int BN>
+static int launch_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
+                           const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int max_rows,
+                           int gpw, float* out, int32_t* am, hipStream_t st) {
+  const int grid = nchunks < 65536 ? (nchunks + 7) & ~7 : 65536;   // multiple of 8 (XCD-aware order)
+  const size_t lds = pool_fwd_bf16_lds<BN>(max_rows);
+  const int4* ck = reinterpret_cast<const int4*>(chunks);
+#define SGG_POOL_BF(G)                                                                                          \
+  hipLaunchKernelGGL((pool_fwd_bf16_kernel<BN, G>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off, ck, \
+                     nchunks, ncd, out, am)
+  switch (gpw) {
+    case 1: SGG_POOL_BF(1); break;
+    case 2: SGG_POOL_BF(2); break;
+    case 4: SGG_POOL_BF(4); break;
+    default: SGG_POOL_BF(8); break;
+  }
+#undef SGG_POOL_BF
+  SGG_RETURN_LAUNCH("sgg_pool_fwd_bf16");
+}
+
 // ---- forward, resident form -------------------------------------------------
 // When the whole W2^T (bn rows x 512, rows padded to 16 NT with zeros) and a
 // scene's U rows fit in LDS beside each other: the workgroup stages W2 and A
@@ -908,6 +1109,28 @@ extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, co
     case 32: return launch_fwd<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
     case 48: return launch_fwd<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
     default: return launch_fwd<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
+  }
+}
+
+extern "C" int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
+                                 const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
+                                 int B, int bn, int max_n, float* out, int32_t* argmax, const int32_t* nchunks_dev,
+                                 void* stream) {
+  SGG_CHECK_ARG(U && pos && A && W2 && b2 && scene_off && chunks && out && argmax, "sgg_pool_fwd_bf16: null pointer");
+  SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_fwd_bf16: bottleneck %d not built (8/16/32/48/64)", bn);
+  SGG_CHECK_ARG(nchunks >= 0 && B >= 0, "sgg_pool_fwd_bf16: bad sizes");
+  SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "sgg_pool_fwd_bf16: max scene size %d outside [1, %d]",
+                max_n, SGG_POOL_MAX_PEDS);
+  SGG_CHECK_ARG(max_rows >= 1 && max_rows <= 64, "sgg_pool_fwd_bf16: chunk rows %d outside [1, 64]", max_rows);
+  SGG_CHECK_ARG(gpw == 1 || gpw == 2 || gpw == 4 || gpw == 8, "sgg_pool_fwd_bf16: gpw %d not in {1,2,4,8}", gpw);
+  if (nchunks == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (bn) {
+    case 8: return launch_fwd_bf16<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
+    case 16: return launch_fwd_bf16<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
+    case 32: return launch_fwd_bf16<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
+    case 48: return launch_fwd_bf16<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
+    default: return launch_fwd_bf16<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
   }
 }
 

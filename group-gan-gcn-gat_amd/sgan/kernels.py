@@ -1049,15 +1049,21 @@ class _Pool(torch.autograd.Function):
         chunks, nchunks, max_rows, gpw = plan[:4]
         ncd = plan[4] if len(plan) > 4 else None    # a fixed-capacity plan's device chunk count
 
+        # the opt-in bf16 precision: the 512 -> bn contraction on bf16 MFMA
+        bf16 = _PRECISION == "bf16"
+        fwd = lib.sgg_pool_fwd_bf16 if bf16 else lib.sgg_pool_fwd
+
         def launch():
-            N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(scenes.scene_off),
-                                     N.ptr(chunks), nchunks, max_rows, gpw, B, bn, scenes.max_n, N.ptr(out),
-                                     N.ptr(am), N.ptr(ncd), N.stream_ptr()), "sgg_pool_fwd")
+            N.check(fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(scenes.scene_off),
+                        N.ptr(chunks), nchunks, max_rows, gpw, B, bn, scenes.max_n, N.ptr(out),
+                        N.ptr(am), N.ptr(ncd), N.stream_ptr()), "sgg_pool_fwd")
         launch()
         if timer.active:
             # the form the library picks (pool.hip launch_fwd_g)
             small = gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count
             name = "pool_fwd_v_kernel<%d, %d>" % (bn, gpw) if small else "pool_fwd_kernel<%d, %d, 2>" % (bn, gpw)
+            if bf16:
+                name = "pool_fwd_bf16_kernel<%d, %d>" % (bn, gpw)
             nb = 4.0 * (B * 512 + 2 * B + 1024 + bn * 512 + bn) + 8.0 * B * bn
             timer.add("sgg::" + name, (scenes.S, B), _pool_flops(scenes, bn), nb, launch)
         ctx.scenes = scenes

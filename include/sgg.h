@@ -97,6 +97,18 @@ int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* 
                  int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,
                  const int32_t* nchunks_dev, void* stream);
 
+/* sgg_pool_fwd in the opt-in bf16 precision (BASELINE configs 3 and 5,
+ * sgan.kernels.set_precision("bf16")): the same arguments, chunk plan and
+ * argmax contract; the 512 -> bn contraction runs on
+ * v_mfma_f32_16x16x32_bf16 with the hidden units (formed in fp32, 2 FMA + max)
+ * and W2 rounded to bf16 (round-to-nearest-even), fp32 accumulation, bias,
+ * ReLU and max.  The backward (sgg_pool_bwd) is the fp32 one at the argmax
+ * this forward chose. */
+int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2,
+                      const float* b2, const int32_t* scene_off, const int32_t* chunks, int nchunks,
+                      int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,
+                      const int32_t* nchunks_dev, void* stream);
+
 /* Backward of sgg_pool_fwd.  Only the (i, argmax[i,c]) pairs carry gradient
  * (torch.max(dim) backward, models.py:541).  Writes dU (B x 512, every row),
  * and one row per workgroup of the parameter-gradient slab `part`

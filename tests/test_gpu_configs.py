@@ -851,3 +851,51 @@ def test_every_family_strict_loads_through_get_generator(graph):
         y = g(T(f[pre + "obs_traj"]), T(f[pre + "obs_traj_rel"]), T(f[pre + "seq_start_end"]),
               T(f[pre + "obs_traj_g"]), user_noise=T(f[pre + "noise"]))
     close(y, f[pre + "out"], rtol=1e-4, what="%s via get_generator" % graph)
+
+
+@pytest.mark.parametrize("bn,sizes", [(48, [20] * 10 + [64, 57, 3, 1, 49]), (8, [20] * 64), (48, [64] * 24)])
+def test_pool_bf16_kernel_matches_rounded_reference(bn, sizes):
+    """sgg_pool_fwd_bf16 (the bf16 precision's 512 -> bn contraction): hidden
+    units formed in fp32, rounded to bf16, times the bf16-rounded W2, fp32
+    accumulation, bias, ReLU, max over j -- against a float64 evaluation of
+    the same rounded operands (the fp32 hidden differs from the float64 one
+    by an ulp, so a rare hidden unit rounds to the neighbouring bf16 value:
+    out within 2e-3 of the scale, argmax equal on >= 99 % of the entries).
+    The fp32 kernel on the same inputs stays bit-identical to itself."""
+    from sgan import _native as N
+    from sgan.scene import SceneIndex
+    lib = N.load()
+    torch.manual_seed(bn + len(sizes))
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    sc = SceneIndex(off, DEV)
+    B = int(off[-1])
+    U = torch.randn(B, 512, device=DEV) * 0.5
+    A = torch.randn(512, 2, device=DEV) * 0.3
+    pos = torch.rand(B, 2, device=DEV) * 15
+    W2 = torch.randn(bn, 512, device=DEV) * 0.05
+    b2 = torch.randn(bn, device=DEV) * 0.1
+    chunks, nchunks, max_rows, gpw = sc.pool_plan(bn)[:4]
+    outs = {}
+    for name in ("sgg_pool_fwd_bf16", "sgg_pool_fwd"):
+        out = torch.empty(B, bn, device=DEV)
+        am = torch.empty(B, bn, device=DEV, dtype=torch.int32)
+        N.check(getattr(lib, name)(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(sc.scene_off),
+                                   N.ptr(chunks), nchunks, max_rows, gpw, B, bn, sc.max_n, N.ptr(out), N.ptr(am),
+                                   None, N.stream_ptr()), name)
+        outs[name] = (out.cpu(), am.cpu())
+    Ud, Ad, pd = U.double().cpu(), A.double().cpu(), pos.double().cpu()
+    W2r = W2.to(torch.bfloat16).double().cpu()
+    ref = torch.empty(B, bn, dtype=torch.float64)
+    ref_am = torch.empty(B, bn, dtype=torch.int64)
+    for s in range(len(sizes)):
+        o, n = int(off[s]), int(off[s + 1] - off[s])
+        r = pd[o:o + n][None, :, :] - pd[o:o + n][:, None, :]          # (i, j, 2): p_j - p_i
+        hid = (Ud[o:o + n][None] + r @ Ad.t()).clamp(min=0)               # (i, j, 512)
+        z = (hid.float().to(torch.bfloat16).double() @ W2r.t() + b2.double().cpu()).clamp(min=0)
+        v, j = z.max(1)
+        ref[o:o + n], ref_am[o:o + n] = v, j + o
+    out, am = outs["sgg_pool_fwd_bf16"]
+    close(out, ref, rtol=2e-3, what="pool bf16 out")
+    assert (am.long() == ref_am).double().mean() >= 0.99
+    # the fp32 kernel is a different (exact f32) contraction: bf16 is within bf16 rounding of it
+    close(out, outs["sgg_pool_fwd"][0], rtol=2e-2, what="pool bf16 vs fp32")
