@@ -1726,9 +1726,11 @@ class SharedPrefix:
         self.Whh = l.weight_hh_l0.contiguous()
         self.fold_ver = _fold_key(*lstm_fold_spec(l, self.emb))[1]
         self.whh_ver = (l.weight_hh_l0._version, _EPOCH.get(l.weight_hh_l0.data_ptr(), 0))
-        return N.LstmSeg(N.ptr(rel), N.ptr(self.A), N.ptr(self.Whh), N.ptr(self.bias), None, None, self.T_pre,
-                         self.Bsrc, B, 0, T, self.Bsrc, N.ptr(self.h_all), N.ptr(self.c_all), N.ptr(self.act),
-                         None, 0, None, 0, None)
+        s = N.LstmSeg(N.ptr(rel), N.ptr(self.A), N.ptr(self.Whh), N.ptr(self.bias), None, None, self.T_pre,
+                      self.Bsrc, B, 0, T, self.Bsrc, N.ptr(self.h_all), N.ptr(self.c_all), N.ptr(self.act),
+                      None, 0, None, 0, None)
+        s._keep = (rel, self.A, self.Whh, self.bias, self.h_all, self.c_all, self.act)   # (check_ownership)
+        return s
 
     def matches(self, rel, W_hh, T, save):
         """The discriminator's forward on `rel` may continue from the prefix."""
@@ -1816,10 +1818,13 @@ class _LSTMSeq(torch.autograd.Function):
             U = torch.empty(B, Wu.shape[0], device=dev, dtype=torch.float32)
 
         def seg(t0, Tn, Bsrc):
-            return N.LstmSeg(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), Tn, B, B, t0, T,
-                             Bsrc, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu),
-                             Wu.stride(0) if Wu is not None else 0, N.ptr(cu), Wu.shape[0] if Wu is not None else 0,
-                             N.ptr(U))
+            s = N.LstmSeg(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0c), N.ptr(c0c), Tn, B, B, t0, T,
+                          Bsrc, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu),
+                          Wu.stride(0) if Wu is not None else 0, N.ptr(cu), Wu.shape[0] if Wu is not None else 0,
+                          N.ptr(U))
+            # the descriptor owns what it points to (a re-issue outlives this frame)
+            s._keep = (rel, A, Whh, bias, h0c, c0c, h_all, c_all, act, Wu, cu, U)
+            return s
         pfx_seg = pfx.segment(rel) if carry else None
         if carry:
             pfx.ran = True
@@ -2236,9 +2241,11 @@ class TrajAhead:
         if not self.ok or self.filled is not None or T != self.T1 or self.col0 + self.ncol > B:
             return None
         b, p0 = self.b, self.pos0
-        return N.TrajOut(N.ptr(self.out), self.out.shape[1], self.T0, self.col0, self.ncol, N.ptr(self.head),
-                         self.head.stride(0), N.ptr(b), b.stride(0) if b is not None else 0, N.ptr(p0),
-                         N.ptr(self.start))
+        t = N.TrajOut(N.ptr(self.out), self.out.shape[1], self.T0, self.col0, self.ncol, N.ptr(self.head),
+                      self.head.stride(0), N.ptr(b), b.stride(0) if b is not None else 0, N.ptr(p0),
+                      N.ptr(self.start))
+        t._keep = (self.out, self.head, b, p0, self.start)   # (check_ownership)
+        return t
 
     def taken_by(self, head, a, b, pos0):
         key = lambda t: None if t is None else _tkey(t)
@@ -2370,6 +2377,7 @@ class _DecoderInit(torch.autograd.Function):
             # materialize(h0, rel0) first where its kernel family cannot
             di = N.DecInit(N.ptr(cvec), cvec.stride(0), Dc, N.ptr(zc), nz, N.ptr(best), int(first_k), N.ptr(ps),
                            scenes.S, B, N.ptr(last))
+            di._keep = keep   # (check_ownership: the descriptor owns what it points to)
             h0._sgg_dinit = (di, keep, materialize)
         else:
             materialize(h0, rel0)
