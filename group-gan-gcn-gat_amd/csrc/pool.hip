@@ -426,205 +426,209 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
 // ---- forward, bf16 layer 2 ----------------------------------------------------
 // The opt-in bf16 precision (sgg_pool_fwd_bf16; BASELINE configs 3 and 5): the
 // 512 -> bn contraction on v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
-// The hidden unit is formed exactly as above in fp32 (2 FMA + max) and only
-// then rounded to bf16 (round-to-nearest-even) as the A operand; W2 is
-// rounded when its k-tile is staged.  A 32-deep k-step gives a lane 8
+// The hidden unit is formed exactly as in the fp32 kernels (2 FMA + max in
+// fp32) and only then rounded to bf16 (round-to-nearest-even) as the A
+// operand; W2 is rounded when it is staged.  A 32-deep k-step gives a lane 8
 // consecutive units 8 kq .. 8 kq + 7 of its pair (A[row = pair][k]) and of
-// its column (B[k][col] = W2[col][k]), so the U row, (A_x, A_y) and W2 reads
-// are 16-byte LDS reads; one bf16 MFMA replaces eight f32 ones (16 vs 8 x 32
-// cycles), and the VALU work of the hidden units becomes the step's cost.
-// Same chunks, XCD order, epilogue (max over j with the smallest j on ties)
-// as pool_fwd_kernel.
+// its column (B[k][col] = W2[col][k]): the U row, (A_x, A_y) and W2 reads
+// are 16-byte LDS reads, and one bf16 MFMA does the work of eight f32 ones.
+//
+// With the matrix cores 16x faster, what the fp32 kernels hide behind the
+// MFMA -- staging the scene's U rows and W2 once per few hundred pairs --
+// would dominate, so the form differs: 512-thread persistent workgroups stage
+// W2 (bf16) and A ONCE for their lifetime; a chunk of whole i-rows of one
+// scene (sgg_pool_plan_bf16: up to 1024 pairs) runs in passes of up to
+// 8 waves x GPW 16-pair groups, its U rows streamed through two LDS k-tile
+// buffers (one barrier per 64-unit tile; the next-but-one tile's global loads
+// in flight in registers).  Any chunk table works (a chunk larger than a pass
+// takes several); the chunk order, epilogue and argmax contract (max over j,
+// smallest j on ties) are the fp32 kernels'.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-constexpr int kBfUP = kKT + 4;   // U tile row pitch (floats; 16-B rows)
-constexpr int kBfWP = kKT + 8;   // W2 tile row pitch (bf16; 16-B rows)
+constexpr int kBfWaves = 8;
+constexpr int kBfThreads = 64 * kBfWaves;
+constexpr int kBfUP = kKT + 4;         // U tile row pitch (floats; 16-B rows)
+constexpr int kBfWP = kHidden + 8;     // W2 row pitch (bf16; 16-B rows, +4 banks per row)
+constexpr int kBfMaxRows = 64;         // i-rows of one pass (keys)
+
+template <int BN>
+__host__ __device__ constexpr size_t pool_bf16_lds_bytes() {
+  return sizeof(__bf16) * (size_t)16 * PoolCfg<BN>::NT * kBfWP + sizeof(float) * 2 * kHidden +
+         sizeof(float) * 2 * (size_t)SGG_POOL_MAX_PEDS * kBfUP + sizeof(float2) * SGG_POOL_MAX_PEDS +
+         sizeof(unsigned long long) * (size_t)kBfMaxRows * BN;
+}
 
 template <int BN, int GPW>
-__global__ void __launch_bounds__(256) pool_fwd_bf16_kernel(
+__global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
     const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
     const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
     const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
     const int32_t* __restrict__ nchunks_dev, float* __restrict__ out, int32_t* __restrict__ argmax) {
   constexpr int NT = PoolCfg<BN>::NT;
+  constexpr int CAP = kBfWaves * GPW * 16;   // pairs per pass
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* Us = reinterpret_cast<float*>(smem);                                   // 64 x kBfUP
-  float* As = Us + SGG_POOL_MAX_PEDS * kBfUP;                                   // 64 units x (A_x, A_y)
-  __bf16* W2s = reinterpret_cast<__bf16*>(As + 2 * kKT);                        // 16 NT rows x kBfWP
-  float2* ps = reinterpret_cast<float2*>(W2s + 16 * NT * kBfWP);                // scene positions (<= 64)
-  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // 64 x BN
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __bf16* W2s = reinterpret_cast<__bf16*>(smem);                                // 16 NT rows x kBfWP
+  float* As = reinterpret_cast<float*>(W2s + 16 * NT * kBfWP);                  // 512 units x (A_x, A_y)
+  float* Ut = As + 2 * kHidden;                                                 // 2 x 64 rows x kBfUP
+  float2* ps = reinterpret_cast<float2*>(Ut + 2 * SGG_POOL_MAX_PEDS * kBfUP);   // scene positions
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // rows x BN
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
+
+  // W2 (rounded to bf16; rows >= BN zero) and A, once per workgroup
+  for (int q = tid; q < 16 * NT * (kHidden / 4); q += kBfThreads) {
+    const int c = q / (kHidden / 4), c4 = q - c * (kHidden / 4);
+    float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < BN) w = *reinterpret_cast<const float4*>(W2 + (size_t)c * kHidden + 4 * c4);
+    __bf16* d = W2s + c * kBfWP + 4 * c4;
+    d[0] = (__bf16)w.x;
+    d[1] = (__bf16)w.y;
+    d[2] = (__bf16)w.z;
+    d[3] = (__bf16)w.w;
+  }
+  for (int q = tid; q < 2 * kHidden / 4; q += kBfThreads)
+    reinterpret_cast<float4*>(As)[q] = reinterpret_cast<const float4*>(A)[q];
 
   const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);   // XCD-aware (pool_fwd_kernel)
   const int nch = nchunks_dev ? *nchunks_dev : nchunks;
   for (int ch = xb; ch < nch; ch += gridDim.x) {
     const int4 cd = chunks[ch];
-    const int s = cd.x, i0 = cd.y, i1 = cd.z;
-    if (i1 <= i0) continue;
+    const int s = cd.x;
+    if (cd.z <= cd.y) continue;   // an empty padding chunk (fixed-capacity plan), uniform
     const int o = scene_off[s];
     const int n = scene_off[s + 1] - o;
-    const int rows = i1 - i0;
-    const int npairs = rows * n;
+    int rpp = CAP / n;
+    rpp = rpp < 1 ? 1 : (rpp > kBfMaxRows ? kBfMaxRows : rpp);
+    for (int i0 = cd.y; i0 < cd.z; i0 += rpp) {
+      const int rows = min(rpp, cd.z - i0);
+      const int npairs = rows * n;
+      __syncthreads();   // (W2s / As staged; the previous pass's readers of Ut, ps, keys done)
+      for (int q = tid; q < n; q += kBfThreads) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
+      for (int q = tid; q < rows * BN; q += kBfThreads) keys[q] = 0ull;
 
-    for (int q = threadIdx.x; q < n; q += blockDim.x) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
-    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) keys[q] = 0ull;
-    __syncthreads();
-
-    int uoff[GPW];
-    float rx[GPW], ry[GPW];
-    floatx4 acc[GPW][NT];
+      // U tiles of 64 units: n rows x 16 float4, two per thread (n <= 64)
+      constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + kBfThreads - 1) / kBfThreads;
+      float4 ra[kUQ], rb[kUQ];
+      auto load_tile = [&](float4 (&r)[kUQ], int k0) {
 #pragma unroll
-    for (int g = 0; g < GPW; ++g) {
-      const int p = (wave * GPW + g) * 16 + c16;
-      int il = 0, j = 0;
-      if (p < npairs) { il = p / n; j = p - il * n; }
-      uoff[g] = j * kBfUP + 8 * kq;
-      const float2 pj = ps[j], pi = ps[i0 + il];
-      rx[g] = p < npairs ? pj.x - pi.x : 0.f;
-      ry[g] = p < npairs ? pj.y - pi.y : 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-
-    constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + 255) / 256;   // float4 of U per thread
-    constexpr int kWQ = (16 * NT * (kKT / 4) + 255) / 256;            // float4 of W2 per thread
-    float4 ureg[kUQ], wreg[kWQ];
-    float areg = 0.f;
-    auto load_tile = [&](int k0) {
-#pragma unroll
-      for (int e = 0; e < kUQ; ++e) {
-        const int q = threadIdx.x + 256 * e;
-        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
-        if (r < n) ureg[e] = *reinterpret_cast<const float4*>(U + (size_t)(o + r) * kHidden + k0 + 4 * c4);
-      }
-#pragma unroll
-      for (int e = 0; e < kWQ; ++e) {   // W2 rows (nn.Linear layout), rows >= BN are zero
-        const int q = threadIdx.x + 256 * e;
-        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
-        wreg[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (c < BN) wreg[e] = *reinterpret_cast<const float4*>(W2 + (size_t)c * kHidden + k0 + 4 * c4);
-      }
-      if (threadIdx.x < 2 * kKT) areg = A[2 * k0 + threadIdx.x];
-    };
-    auto store_tile = [&]() {
-#pragma unroll
-      for (int e = 0; e < kUQ; ++e) {
-        const int q = threadIdx.x + 256 * e;
-        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
-        if (r < n) *reinterpret_cast<float4*>(Us + r * kBfUP + 4 * c4) = ureg[e];
-      }
-#pragma unroll
-      for (int e = 0; e < kWQ; ++e) {
-        const int q = threadIdx.x + 256 * e;
-        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
-        if (c < 16 * NT) {
-          __bf16* d = W2s + c * kBfWP + 4 * c4;
-          d[0] = (__bf16)wreg[e].x;
-          d[1] = (__bf16)wreg[e].y;
-          d[2] = (__bf16)wreg[e].z;
-          d[3] = (__bf16)wreg[e].w;
+        for (int e = 0; e < kUQ; ++e) {
+          const int q = tid + kBfThreads * e;
+          const int row = q / (kKT / 4), c4 = q - row * (kKT / 4);
+          if (row < n) r[e] = *reinterpret_cast<const float4*>(U + (size_t)(o + row) * kHidden + k0 + 4 * c4);
         }
-      }
-      if (threadIdx.x < 2 * kKT) As[threadIdx.x] = areg;   // (A_x, A_y) of unit k at 2 k, 2 k + 1
-    };
-    load_tile(0);
-    __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
-    store_tile();
-    __syncthreads();
-    for (int k0 = 0; k0 < kHidden; k0 += kKT) {
-      if (k0 + kKT < kHidden) load_tile(k0 + kKT);
+      };
+      auto store_tile = [&](const float4 (&r)[kUQ], int buf) {
+        float* d = Ut + buf * SGG_POOL_MAX_PEDS * kBfUP;
 #pragma unroll
-      for (int s2 = 0; s2 < kKT / 32; ++s2) {
-        const int kb = 32 * s2 + 8 * kq;   // the lane's 8 units in this k-step
-        float av[16];
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          *reinterpret_cast<float4*>(&av[4 * v]) = *reinterpret_cast<const float4*>(As + 2 * kb + 4 * v);
-        bf16x8_t bfr[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) bfr[t] = *reinterpret_cast<const bf16x8_t*>(W2s + (16 * t + c16) * kBfWP + kb);
-#pragma unroll
-        for (int g = 0; g < GPW; ++g) {
-          float uv[8];
-          *reinterpret_cast<float4*>(&uv[0]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 32 * s2);
-          *reinterpret_cast<float4*>(&uv[4]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 32 * s2 + 4);
-          bf16x8_t h;
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            h[e] = (__bf16)fmaxf(fmaf(av[2 * e + 1], ry[g], fmaf(av[2 * e], rx[g], uv[e])), 0.f);
-#pragma unroll
-          for (int t = 0; t < NT; ++t) acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bfr[t], acc[g][t], 0, 0, 0);
+        for (int e = 0; e < kUQ; ++e) {
+          const int q = tid + kBfThreads * e;
+          const int row = q / (kKT / 4), c4 = q - row * (kKT / 4);
+          if (row < n) *reinterpret_cast<float4*>(d + row * kBfUP + 4 * c4) = r[e];
         }
+      };
+      load_tile(ra, 0);
+      load_tile(rb, kKT);
+      __syncthreads();   // ps / keys visible
+      store_tile(ra, 0);
+
+      // the lane's pair of each group (padding pairs: j = 0, r = 0)
+      int uoff[GPW];
+      float rx[GPW], ry[GPW];
+      floatx4 acc[GPW][NT];
+#pragma unroll
+      for (int g = 0; g < GPW; ++g) {
+        const int p = (wave * GPW + g) * 16 + c16;
+        int il = 0, j = 0;
+        if (p < npairs) { il = p / n; j = p - il * n; }
+        uoff[g] = j * kBfUP + 8 * kq;
+        const float2 pj = ps[j], pi = ps[i0 + il];
+        rx[g] = p < npairs ? pj.x - pi.x : 0.f;
+        ry[g] = p < npairs ? pj.y - pi.y : 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
       }
-      __syncthreads();  // tile consumed
-      if (k0 + kKT < kHidden) {
-        store_tile();
+      const int ngr = (npairs + 15) >> 4;   // groups with pairs (wave-uniform tests below)
+      __syncthreads();   // tile 0 staged
+
+      constexpr int NKT = kHidden / kKT;
+#pragma unroll 1
+      for (int kt = 0; kt < NKT; ++kt) {
+        // registers: tile kt + 1 in rb (loaded a tile ago); issue tile kt + 2 into ra
+        if (kt + 2 < NKT) load_tile(ra, (kt + 2) * kKT);
+        const float* ut = Ut + (kt & 1) * SGG_POOL_MAX_PEDS * kBfUP;
+#pragma unroll 1
+        for (int s2 = 0; s2 < kKT / 32; ++s2) {
+          const int ku = kt * kKT + 32 * s2 + 8 * kq;   // the lane's 8 units of this k-step
+          float av[16];
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            *reinterpret_cast<float4*>(&av[4 * v]) = *reinterpret_cast<const float4*>(As + 2 * ku + 4 * v);
+          bf16x8_t bfr[NT];
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            bfr[t] = *reinterpret_cast<const bf16x8_t*>(W2s + (16 * t + c16) * kBfWP + ku);
+#pragma unroll
+          for (int g = 0; g < GPW; ++g) {
+            if (wave * GPW + g < ngr) {   // (wave-uniform)
+              float uv[8];
+              *reinterpret_cast<float4*>(&uv[0]) = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2);
+              *reinterpret_cast<float4*>(&uv[4]) = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2 + 4);
+              bf16x8_t h;
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                h[e] = (__bf16)fmaxf(fmaf(av[2 * e + 1], ry[g], fmaf(av[2 * e], rx[g], uv[e])), 0.f);
+#pragma unroll
+              for (int t = 0; t < NT; ++t)
+                acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bfr[t], acc[g][t], 0, 0, 0);
+            }
+          }
+        }
+        if (kt + 1 < NKT) store_tile(rb, (kt + 1) & 1);   // (buffer (kt + 1) & 1 was last read in tile kt - 1)
+#pragma unroll
+        for (int e = 0; e < kUQ; ++e) rb[e] = ra[e];
         __syncthreads();
       }
-    }
 
-    // epilogue: bias, ReLU, max over j (as pool_fwd_kernel)
+      // epilogue: bias, ReLU, max over j (LDS atomic max on (bits << 32 | ~j))
 #pragma unroll
-    for (int g = 0; g < GPW; ++g) {
-      const int grp = wave * GPW + g;
+      for (int g = 0; g < GPW; ++g) {
+        const int grp = wave * GPW + g;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int p = grp * 16 + kq * 4 + r;
-        if (p < npairs) {
-          const int il = p / n, j = p - il * n;
-          const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
+        for (int r = 0; r < 4; ++r) {
+          const int p = grp * 16 + kq * 4 + r;
+          if (p < npairs) {
+            const int il = p / n, j = p - il * n;
+            const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
 #pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            const int cc = 16 * t + c16;
-            if (cc < BN) {
-              float v = acc[g][t][r] + b2[cc];
-              v = v > 0.f ? v : 0.f;
-              atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
+            for (int t = 0; t < NT; ++t) {
+              const int cc = 16 * t + c16;
+              if (cc < BN) {
+                float v = acc[g][t][r] + b2[cc];
+                v = v > 0.f ? v : 0.f;
+                atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
+              }
             }
           }
         }
       }
+      __syncthreads();
+      for (int q = tid; q < rows * BN; q += kBfThreads) {
+        const unsigned long long key = keys[q];
+        const size_t oi = (size_t)(o + i0) * BN + q;
+        out[oi] = __uint_as_float((unsigned)(key >> 32));
+        argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+      }
     }
-    __syncthreads();
-    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) {
-      const unsigned long long key = keys[q];
-      const size_t oi = (size_t)(o + i0) * BN + q;
-      out[oi] = __uint_as_float((unsigned)(key >> 32));
-      argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
-    }
-    __syncthreads();
   }
-}
-
-template <int BN>
-static size_t pool_fwd_bf16_lds(int max_rows) {
-  return sizeof(float) * ((size_t)SGG_POOL_MAX_PEDS * kBfUP + 2 * kKT) +
-         sizeof(__bf16) * (size_t)16 * PoolCfg<BN>::NT * kBfWP + sizeof(float2) * SGG_POOL_MAX_PEDS +
-         sizeof(unsigned long long) * (size_t)max_rows * BN;
 }
 
 template <int BN>
 static int launch_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                           const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int max_rows,
-                           int gpw, float* out, int32_t* am, hipStream_t st) {
-  const int grid = nchunks < 65536 ? (nchunks + 7) & ~7 : 65536;   // multiple of 8 (XCD-aware order)
-  const size_t lds = pool_fwd_bf16_lds<BN>(max_rows);
-  const int4* ck = reinterpret_cast<const int4*>(chunks);
-#define SGG_POOL_BF(G)                                                                                          \
-  hipLaunchKernelGGL((pool_fwd_bf16_kernel<BN, G>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off, ck, \
-                     nchunks, ncd, out, am)
-  switch (gpw) {
-    case 1: SGG_POOL_BF(1); break;
-    case 2: SGG_POOL_BF(2); break;
-    case 4: SGG_POOL_BF(4); break;
-    default: SGG_POOL_BF(8); break;
-  }
-#undef SGG_POOL_BF
-  SGG_RETURN_LAUNCH("sgg_pool_fwd_bf16");
-}
+                           const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int gpw,
+                           float* out, int32_t* am, hipStream_t st);
 
-// ---- forward, resident form -------------------------------------------------
+// ---- forward, resident form -------------------------------------------------// ---- forward, resident form -------------------------------------------------
 // When the whole W2^T (bn rows x 512, rows padded to 16 NT with zeros) and a
 // scene's U rows fit in LDS beside each other: the workgroup stages W2 and A
 // once for its lifetime (persistent grid over the chunk table) and the U rows
@@ -1013,6 +1017,27 @@ static int launch_fwd(const float* U, const float* pos, const float* A, const fl
 }
 
 template <int BN>
+static int launch_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
+                           const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int gpw,
+                           float* out, int32_t* am, hipStream_t st) {
+  // persistent: one 512-thread workgroup per CU (its LDS plan), a multiple of 8 (XCD-aware order)
+  int grid = device_cus();
+  if (grid > nchunks) grid = nchunks;
+  grid = (grid + 7) & ~7;
+  const size_t lds = pool_bf16_lds_bytes<BN>();
+  const int4* ck = reinterpret_cast<const int4*>(chunks);
+#define SGG_POOL_BF(G)                                                                                                  hipLaunchKernelGGL((pool_fwd_bf16_kernel<BN, G>), dim3(grid), dim3(kBfThreads), lds, st, U, pos, A, W2, b2, off, ck,                      nchunks, ncd, out, am)
+  if (gpw >= 4 && BN <= 48)
+    SGG_POOL_BF(4);
+  else if (gpw >= 2)
+    SGG_POOL_BF(2);
+  else
+    SGG_POOL_BF(1);
+#undef SGG_POOL_BF
+  SGG_RETURN_LAUNCH("sgg_pool_fwd_bf16");
+}
+
+template <int BN>
 static int launch_bwd(const float* U, const float* pos, const float* A, const float* W2, const float* out,
                       const int32_t* am, const float* dout, const int32_t* off, int S, int max_n, float* dU,
                       float* part, hipStream_t st) {
@@ -1112,6 +1137,57 @@ extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, co
   }
 }
 
+extern "C" int sgg_pool_plan_bf16(const int32_t* host_scene_off, int S, int bn, int target_chunks, int32_t* chunks,
+                                  int cap, int* max_rows, int* gpw_out) {
+  // host helper for pool_fwd_bf16_kernel: chunks of whole i-rows of up to a
+  // pair budget Pb (the largest of 1024 .. 128 that still gives >= target_chunks
+  // chunks), rows spread evenly over a scene's chunks; gpw = the 16-pair groups
+  // per wave that one pass of the widest chunk needs (8 waves per workgroup)
+  if (!host_scene_off || !chunks || !max_rows || !gpw_out || S < 0 || cap < 0 || !pool_bn_ok(bn)) {
+    sgg::set_error("sgg_pool_plan_bf16: bad argument");
+    return SGG_E_ARG;
+  }
+  auto rows_of = [&](int n, int pb) { const int r = pb / n; return r < 1 ? 1 : (r > n ? n : r); };
+  int pb = 1024;
+  for (; pb > 128; pb >>= 1) {
+    long nc = 0;
+    for (int s = 0; s < S; ++s) {
+      const int n = host_scene_off[s + 1] - host_scene_off[s];
+      if (n > 0) nc += (n + rows_of(n, pb) - 1) / rows_of(n, pb);
+    }
+    if (nc >= target_chunks) break;
+  }
+  int nc = 0, mr = 1, mp = 1;
+  for (int s = 0; s < S; ++s) {
+    const int n = host_scene_off[s + 1] - host_scene_off[s];
+    if (n <= 0) continue;
+    const int rmax = rows_of(n, pb), nck = (n + rmax - 1) / rmax, rows = (n + nck - 1) / nck;
+    for (int i0 = 0; i0 < n; i0 += rows) {
+      const int i1 = i0 + rows < n ? i0 + rows : n;
+      if (nc >= cap) {
+        sgg::set_error("sgg_pool_plan_bf16: chunk table capacity %d exceeded", cap);
+        return SGG_E_ARG;
+      }
+      chunks[4 * nc + 0] = s;
+      chunks[4 * nc + 1] = i0;
+      chunks[4 * nc + 2] = i1;
+      chunks[4 * nc + 3] = 0;
+      if (i1 - i0 > mr) mr = i1 - i0;
+      if ((i1 - i0) * n > mp) mp = (i1 - i0) * n;
+      ++nc;
+    }
+  }
+  // (register budget at two waves per SIMD: gpw <= 4, and <= 2 at bn 64 --
+  // a chunk wider than one pass runs in several)
+  const int gmax = bn > 48 ? 2 : 4;
+  int gpw = 1;
+  while (gpw < gmax && 16 * kBfWaves * gpw < mp) gpw <<= 1;
+  for (int c = 0; c < nc; ++c) chunks[4 * c + 3] = gpw;
+  *max_rows = mr;
+  *gpw_out = gpw;
+  return nc;
+}
+
 extern "C" int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
                                  const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
                                  int B, int bn, int max_n, float* out, int32_t* argmax, const int32_t* nchunks_dev,
@@ -1126,11 +1202,11 @@ extern "C" int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* 
   if (nchunks == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (bn) {
-    case 8: return launch_fwd_bf16<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
-    case 16: return launch_fwd_bf16<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
-    case 32: return launch_fwd_bf16<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
-    case 48: return launch_fwd_bf16<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
-    default: return launch_fwd_bf16<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, gpw, out, argmax, st);
+    case 8: return launch_fwd_bf16<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
+    case 16: return launch_fwd_bf16<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
+    case 32: return launch_fwd_bf16<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
+    case 48: return launch_fwd_bf16<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
+    default: return launch_fwd_bf16<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
   }
 }
 

@@ -1045,13 +1045,14 @@ class _Pool(torch.autograd.Function):
             assert U.shape == (B, 512) and U.is_contiguous()
         out = torch.empty(B, bn, device=h.device, dtype=torch.float32)
         am = torch.empty(B, bn, device=h.device, dtype=torch.int32)
-        plan = scenes.pool_plan(bn)
-        chunks, nchunks, max_rows, gpw = plan[:4]
-        ncd = plan[4] if len(plan) > 4 else None    # a fixed-capacity plan's device chunk count
-
-        # the opt-in bf16 precision: the 512 -> bn contraction on bf16 MFMA
+        # the opt-in bf16 precision: the 512 -> bn contraction on bf16 MFMA (its own chunk plan)
         bf16 = _PRECISION == "bf16"
         fwd = lib.sgg_pool_fwd_bf16 if bf16 else lib.sgg_pool_fwd
+        plan = scenes.pool_plan(bn, bf16=bf16)
+        chunks, nchunks, max_rows, gpw = plan[:4]
+        ncd = plan[4] if len(plan) > 4 else None    # a fixed-capacity plan's device chunk count
+        if bf16 and ncd is not None:
+            gpw = 4   # (a fixed-capacity fp32 plan: its chunks run in passes of up to 512 pairs)
 
         def launch():
             N.check(fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(scenes.scene_off),

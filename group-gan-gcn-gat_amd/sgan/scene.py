@@ -68,12 +68,13 @@ class SceneIndex:
     POOL_TARGET_CHUNKS = 512
     POOL_MAX_GPW = int(__import__("os").environ.get("SGG_POOL_MAX_GPW", "0"))
 
-    def pool_plan(self, bn, target_chunks=None):
+    def pool_plan(self, bn, target_chunks=None, bf16=False):
         """Device chunk table for sgg_pool_fwd (built on the host by
-        sgg_pool_plan, cached per bottleneck width)."""
+        sgg_pool_plan, cached per bottleneck width); bf16: the table of
+        sgg_pool_fwd_bf16 (sgg_pool_plan_bf16: big chunks, one per CU)."""
         target_chunks = target_chunks or self.POOL_TARGET_CHUNKS
         plans = self.__dict__.setdefault("_pool_plans", {})
-        key = (bn, target_chunks, self.POOL_MAX_GPW)
+        key = (bn, target_chunks, self.POOL_MAX_GPW, bool(bf16))
         if key not in plans:
             import ctypes
             lib = N.load()
@@ -81,8 +82,16 @@ class SceneIndex:
             cap = int(self.B) + self.S + 1
             tab = np.zeros((cap, 4), dtype=np.int32)
             mr, gpw = ctypes.c_int(0), ctypes.c_int(0)
-            nc = lib.sgg_pool_plan(off.ctypes.data_as(ctypes.c_void_p), self.S, bn, target_chunks, self.POOL_MAX_GPW,
-                                   tab.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(mr), ctypes.byref(gpw))
+            if bf16:
+                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count \
+                    if torch.device(self.device).type == "cuda" else 256
+                nc = lib.sgg_pool_plan_bf16(off.ctypes.data_as(ctypes.c_void_p), self.S, bn, int(ncu),
+                                            tab.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(mr),
+                                            ctypes.byref(gpw))
+            else:
+                nc = lib.sgg_pool_plan(off.ctypes.data_as(ctypes.c_void_p), self.S, bn, target_chunks,
+                                       self.POOL_MAX_GPW, tab.ctypes.data_as(ctypes.c_void_p), cap,
+                                       ctypes.byref(mr), ctypes.byref(gpw))
             if nc < 0:
                 N.check(nc, "sgg_pool_plan")
             dev = torch.from_numpy(tab[:max(nc, 1)].copy()).to(self.device, non_blocking=True)
@@ -241,7 +250,7 @@ class PaddedScenes(SceneIndex):
         """Offset of plan k: [chunk count, 0, 0, 0 | pool_cap x (scene, i0, i1, gpw)]."""
         return self._plan_base + (4 + 4 * self.pool_cap) * k
 
-    def pool_plan(self, bn, target_chunks=None, rep=1):
+    def pool_plan(self, bn, target_chunks=None, rep=1, bf16=False):
         """(chunk table, grid basis, max rows, gpw, device chunk count): the
         table holds up to pool_cap chunks; the kernels walk the device count,
         the grid is sized by the chunk count of the batch that registered the
@@ -352,7 +361,8 @@ class _PaddedRepeat(SceneIndex):
     def ped_scene_long(self):
         raise NotImplementedError("PaddedScenes.repeat: no ped-scene map")
 
-    def pool_plan(self, bn, target_chunks=None):
+    def pool_plan(self, bn, target_chunks=None, bf16=False):
+        # (the fixed-capacity plan serves both precisions: the bf16 kernel takes any chunk table)
         return self.parent.pool_plan(bn, target_chunks, rep=self.k)
 
     def groups(self, labels):

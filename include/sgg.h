@@ -98,12 +98,16 @@ int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* 
                  const int32_t* nchunks_dev, void* stream);
 
 /* sgg_pool_fwd in the opt-in bf16 precision (BASELINE configs 3 and 5,
- * sgan.kernels.set_precision("bf16")): the same arguments, chunk plan and
- * argmax contract; the 512 -> bn contraction runs on
- * v_mfma_f32_16x16x32_bf16 with the hidden units (formed in fp32, 2 FMA + max)
- * and W2 rounded to bf16 (round-to-nearest-even), fp32 accumulation, bias,
- * ReLU and max.  The backward (sgg_pool_bwd) is the fp32 one at the argmax
- * this forward chose. */
+ * sgan.kernels.set_precision("bf16")): the same arguments and argmax
+ * contract; the 512 -> bn contraction runs on v_mfma_f32_16x16x32_bf16 with
+ * the hidden units (formed in fp32, 2 FMA + max) and W2 rounded to bf16
+ * (round-to-nearest-even), fp32 accumulation, bias, ReLU and max.  Any chunk
+ * table is accepted (a chunk runs in passes of up to 8 x 16 gpw pairs); the
+ * efficient one comes from sgg_pool_plan_bf16 (up to 1024 pairs per chunk,
+ * >= target_chunks chunks -- one per CU fills the persistent grid).  The
+ * backward (sgg_pool_bwd) is the fp32 one at the argmax this forward chose. */
+int sgg_pool_plan_bf16(const int32_t* host_scene_off, int S, int bn, int target_chunks, int32_t* host_chunks,
+                       int cap, int* max_rows, int* gpw);
 int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2,
                       const float* b2, const int32_t* scene_off, const int32_t* chunks, int nchunks,
                       int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,

@@ -874,15 +874,19 @@ def test_pool_bf16_kernel_matches_rounded_reference(bn, sizes):
     pos = torch.rand(B, 2, device=DEV) * 15
     W2 = torch.randn(bn, 512, device=DEV) * 0.05
     b2 = torch.randn(bn, device=DEV) * 0.1
-    chunks, nchunks, max_rows, gpw = sc.pool_plan(bn)[:4]
     outs = {}
-    for name in ("sgg_pool_fwd_bf16", "sgg_pool_fwd"):
+    # the bf16 kernel on its own plan (big chunks) and on the fp32 plan's small ones (passes per chunk)
+    for name, bfplan in (("sgg_pool_fwd_bf16", True), ("sgg_pool_fwd_bf16/fp32plan", False),
+                         ("sgg_pool_fwd", False)):
+        chunks, nchunks, max_rows, gpw = sc.pool_plan(bn, bf16=bfplan)[:4]
         out = torch.empty(B, bn, device=DEV)
         am = torch.empty(B, bn, device=DEV, dtype=torch.int32)
-        N.check(getattr(lib, name)(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(sc.scene_off),
-                                   N.ptr(chunks), nchunks, max_rows, gpw, B, bn, sc.max_n, N.ptr(out), N.ptr(am),
-                                   None, N.stream_ptr()), name)
+        N.check(getattr(lib, name.split("/")[0])(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2),
+                                                 N.ptr(sc.scene_off), N.ptr(chunks), nchunks, max_rows, gpw, B, bn,
+                                                 sc.max_n, N.ptr(out), N.ptr(am), None, N.stream_ptr()), name)
         outs[name] = (out.cpu(), am.cpu())
+    assert torch.equal(outs["sgg_pool_fwd_bf16"][0], outs["sgg_pool_fwd_bf16/fp32plan"][0]), "bf16 plan-independent"
+    assert torch.equal(outs["sgg_pool_fwd_bf16"][1], outs["sgg_pool_fwd_bf16/fp32plan"][1])
     Ud, Ad, pd = U.double().cpu(), A.double().cpu(), pos.double().cpu()
     W2r = W2.to(torch.bfloat16).double().cpu()
     ref = torch.empty(B, bn, dtype=torch.float64)

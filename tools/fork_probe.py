@@ -62,6 +62,38 @@ def main():
         torch.cuda.current_stream().wait_stream(s0)
         graphs[name] = g
     torch.cuda.synchronize()
+    # two graphs of 10 re-issues each (a: 10 x encoder, b: 10 x rollout),
+    # replayed one after the other on one stream vs on two streams at once
+    # (separate hardware queues, no dependency between them)
+    g10 = {}
+    for name, fn in (("a10", a), ("b10", b)):
+        g = torch.cuda.CUDAGraph()
+        s0.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s0):
+            g.capture_begin(pool=pool)
+            for _ in range(10):
+                fn()
+            g.capture_end()
+        torch.cuda.current_stream().wait_stream(s0)
+        g10[name] = g
+    torch.cuda.synchronize()
+    for rnd in range(2):
+        for mode in ("one-stream", "two-streams"):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            s0.wait_stream(torch.cuda.current_stream())
+            s1.wait_stream(torch.cuda.current_stream())
+            for _ in range(20):
+                with torch.cuda.stream(s0):
+                    g10["a10"].replay()
+                with torch.cuda.stream(s1 if mode == "two-streams" else s0):
+                    g10["b10"].replay()
+            torch.cuda.current_stream().wait_stream(s0)
+            torch.cuda.current_stream().wait_stream(s1)
+            e1.record()
+            e1.synchronize()
+            print("round %d %-11s %.1f us per (a + b) pair" % (rnd, mode, e0.elapsed_time(e1) / 200 * 1e3), flush=True)
     for rnd in range(2):
         for name, g in graphs.items():
             for _ in range(5):
