@@ -17,6 +17,7 @@
 #include <stdlib.h>
 
 #include "sgg_common.h"
+#include "xtw_body.h"
 
 namespace sgg {
 
@@ -211,17 +212,18 @@ __global__ void __launch_bounds__(256) xw_kernel(const float* __restrict__ X, in
   }
 }
 
+constexpr int kXwSplitLds = 4 * 16 * 65;   // LDS floats of one split-K workgroup
+
 template <bool TRANS_W>
-__global__ void __launch_bounds__(256) xw_splitk_kernel(const float* __restrict__ X, int ldx,
-                                                        const float* __restrict__ Xmask, int ldm,
-                                                        const float* __restrict__ W, int ldw,
-                                                        const float* __restrict__ bias, float* __restrict__ Y,
-                                                        int ldy, int M, int K, int N, int act) {
-  __shared__ float part[4][16][65];
+__device__ __forceinline__ void xw_splitk_body(const float* __restrict__ X, int ldx, const float* __restrict__ Xmask,
+                                               int ldm, const float* __restrict__ W, int ldw,
+                                               const float* __restrict__ bias, float* __restrict__ Y, int ldy, int M,
+                                               int K, int N, int act, int bx, int by, float* smem) {
+  float (*part)[16][65] = reinterpret_cast<float (*)[16][65]>(smem);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int row0 = blockIdx.x * 16;
-  const int col0 = blockIdx.y * 64;
+  const int row0 = bx * 16;
+  const int col0 = by * 64;
   const int ar = lane & 15, kq = lane >> 4;
   const int arow = row0 + ar;
   const bool arow_ok = arow < M;
@@ -256,6 +258,38 @@ __global__ void __launch_bounds__(256) xw_splitk_kernel(const float* __restrict_
       *py = xw_epi(((part[0][rr][cc] + part[1][rr][cc]) + part[2][rr][cc]) + part[3][rr][cc], bias, n, act) +
             ((act & 2) ? *py : 0.f);
     }
+  }
+}
+
+template <bool TRANS_W>
+__global__ void __launch_bounds__(256) xw_splitk_kernel(const float* __restrict__ X, int ldx,
+                                                        const float* __restrict__ Xmask, int ldm,
+                                                        const float* __restrict__ W, int ldw,
+                                                        const float* __restrict__ bias, float* __restrict__ Y,
+                                                        int ldy, int M, int K, int N, int act) {
+  __shared__ float part[kXwSplitLds];
+  xw_splitk_body<TRANS_W>(X, ldx, Xmask, ldm, W, ldw, bias, Y, ldy, M, K, N, act, blockIdx.x, blockIdx.y, part);
+}
+
+// The pooling backward's two independent products of dU (B x 512) in ONE
+// launch: dh (+)= dU W1h (split-K, as sgg_xw with K >= 256) and the split-K
+// partials of dW1h^T = h^T dU with the column sums of dU (as
+// sgg_xtw_partial); the first nxw workgroups take the former, the rest the
+// latter.  (Two launches of ~7-8 us each before.)
+template <int MT>
+__global__ void __launch_bounds__(256) xw_xtw_kernel(const float* __restrict__ dU, int ldu, const float* __restrict__ W,
+                                                     int ldw, float* __restrict__ dh, int ldh, int act, int B, int K,
+                                                     int H, int nxw_x, int nxw, const float* __restrict__ X, int ldx,
+                                                     int rows_per_split, int gx, int gy, float* __restrict__ slab,
+                                                     float* __restrict__ colslab) {
+  __shared__ float smem[kXwSplitLds > kXtwRedFloats ? kXwSplitLds : kXtwRedFloats];
+  const int b = blockIdx.x;
+  if (b < nxw) {
+    xw_splitk_body<false>(dU, ldu, nullptr, 0, W, ldw, nullptr, dh, ldh, B, K, H, act, b % nxw_x, b / nxw_x, smem);
+  } else {
+    const int q = b - nxw;
+    xtw_partial_body<MT>(X, ldx, dU, ldu, nullptr, 0, B, H, K, rows_per_split, slab, colslab, q % gx, (q / gx) % gy,
+                         q / (gx * gy), smem);
   }
 }
 
@@ -378,4 +412,35 @@ extern "C" int sgg_xw(const float* X, int ldx, const float* Xmask, int ldm, cons
     hipLaunchKernelGGL((sgg::xw_kernel<false, false>), grid, dim3(256), 0, s, X, ldx, Xmask, ldm, W, ldw, bias, Y,
                        ldy, M, K, N, act);
   SGG_RETURN_LAUNCH("sgg_xw");
+}
+
+extern "C" int sgg_xtw_splits(int R, int M, int N);
+using sgg::kHidden;
+
+extern "C" int sgg_pool_dh_dw(const float* dU, int ldu, const float* W, int ldw, float* dh, int ldh, int accumulate,
+                              const float* h, int ldx, int B, int H, float* ws, size_t ws_bytes, void* stream) {
+  SGG_CHECK_ARG(dU && W && dh && h && ws, "sgg_pool_dh_dw: null pointer");
+  SGG_CHECK_ARG(B >= 1 && H >= 1 && H <= 64 && ldu >= kHidden && ldw >= H && ldh >= H && ldx >= H,
+                "sgg_pool_dh_dw: bad sizes B=%d H=%d", B, H);
+  const int splits = sgg_xtw_splits(B, H, kHidden);
+  const size_t need = sizeof(float) * (size_t)splits * ((size_t)H * kHidden + kHidden);
+  SGG_CHECK_ARG(ws_bytes >= need, "sgg_pool_dh_dw: workspace %zu < %zu bytes", ws_bytes, need);
+  const int nxw_x = (B + 15) / 16, nxw = nxw_x * ((H + 63) / 64);
+  const int gx = (H + 63) / 64, gy = kHidden / 64;
+  const int rps = ((B + splits - 1) / splits + 63) & ~63;   // (xtw.hip launch_partial)
+  const dim3 grid(nxw + gx * gy * splits);
+  float* colslab = ws + (size_t)splits * H * kHidden;
+  hipStream_t st = (hipStream_t)stream;
+  const int act = accumulate ? 2 : 0;
+#define SGG_XWXTW(MT)                                                                                               \
+  hipLaunchKernelGGL(sgg::xw_xtw_kernel<MT>, grid, dim3(256), 0, st, dU, ldu, W, ldw, dh, ldh, act, B, kHidden, H, \
+                     nxw_x, nxw, h, ldx, rps, gx, gy, ws, colslab)
+  switch (H >= 64 ? 4 : (H + 15) / 16) {
+    case 1: SGG_XWXTW(1); break;
+    case 2: SGG_XWXTW(2); break;
+    case 3: SGG_XWXTW(3); break;
+    default: SGG_XWXTW(4); break;
+  }
+#undef SGG_XWXTW
+  SGG_RETURN_LAUNCH("sgg_pool_dh_dw");
 }

@@ -123,6 +123,7 @@ SIGNATURES = {
     "sgg_pool_plan_bf16": (_i, [_p, _i, _i, _i, _p, _i, _p, _p]),
     "sgg_pool_fwd_bf16": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
     "sgg_pool_bwd_grid": (_i, [_i]),
+    "sgg_pool_dh_dw": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _i, _i, _i, _p, _sz, _p]),
     "sgg_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_gat_fwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _i, _p]),
     "sgg_gat_bwd": (_i, [_p, _i, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _p, _i, _p, _p, _p, _p]),

@@ -18,6 +18,9 @@ from . import _native as N
 GATENC_FUSED = os.environ.get("SGG_GATENC_FUSED", "1") != "0"
 # the fused GATEncoder forward keeps its layer state for the backward (0: the backward recomputes it)
 GATENC_SAVE = os.environ.get("SGG_GATENC_SAVE", "1") != "0"
+# the pooling backward's dh = dU W1h and h^T dU partials in one launch
+# (sgg_pool_dh_dw); "0": two launches (sgg_xw + sgg_xtw_partial)
+DUAL_POOL_BWD = os.environ.get("SGG_DUAL_POOL_BWD", "1") != "0"
 # weight-gradient reductions of the backward on a side stream (needed only by
 # the optimizer step, which joins it).  Off by default: measured slower at
 # configs[1] (61.1k vs 68.9k scenes/s graph-replayed, 12.4k vs 14.8k eager
@@ -1099,19 +1102,40 @@ class _Pool(torch.autograd.Function):
                                                             "true" if stage else "false"), (sc.S, B),
                       8.0 * B * bn * 512, nb, launch)
         dh = None
+        H = h.shape[1]
+        dual = need[0] and wgrad and DUAL_POOL_BWD and not SIDE_STREAM and H <= 64
         if need[0]:
             base = ctx.link.take() if ctx.link is not None else None
-            # dh = dU W1h (+ the other consumer's gradient of h, accumulated in the same launch)
-            dh = xw_raw(dU, W1[:, E:], None, trans_w=False, prec="fp32", out=base, act=0 if base is None else 2)
+            if dual:
+                # dh = dU W1h (+ the other consumer's gradient of h) and the
+                # h^T dU partials (+ column sums) in ONE launch
+                dh = base if base is not None else torch.empty(B, H, device=h.device, dtype=torch.float32)
+                splits = lib.sgg_xtw_splits(B, H, 512)
+                ws = torch.empty(splits * (H * 512 + 512), device=h.device, dtype=torch.float32)
+                W1h = W1[:, E:]
+                acc = int(base is not None)
+
+                def launch2():
+                    N.check(lib.sgg_pool_dh_dw(N.ptr(dU), 512, N.ptr(W1h), W1h.stride(0), N.ptr(dh), dh.stride(0),
+                                               acc, N.ptr(h), h.stride(0), B, H, N.ptr(ws), ws.numel() * 4,
+                                               N.stream_ptr()), "sgg_pool_dh_dw")
+                launch2()
+                if timer.active:   # (re-issued like sgg_xw's accumulating launches: timing, not values)
+                    mt = 4 if H >= 64 else (H + 15) // 16
+                    timer.add("sgg::xw_xtw_kernel<%d>" % mt, (B, H), 4.0 * B * 512 * H,
+                              4.0 * (2 * B * 512 + 512 * H + 2 * B * H) + 4.0 * ws.numel(), launch2)
+            else:
+                # dh = dU W1h (+ the other consumer's gradient of h, accumulated in the same launch)
+                dh = xw_raw(dU, W1[:, E:], None, trans_w=False, prec="fp32", out=base, act=0 if base is None else 2)
         if not wgrad:
             return dh, None, None, None, None, None, None, None, None, None, None
         with side(part, h, dU, W1, We, be):
             # one launch after the dW1h partials: dW2, db2 (slab [dW2 | dA | db2]
             # row sums), dW1h = dU^T h, dc = sum_j dU_j, and the fold backward
             # of (dA, dc) -> dW1e, dWe, dbe
-            H = h.shape[1]
             rows = part.shape[0]
-            ws, splits = xtw_partial(h, dU, colsum=True)
+            if not dual:
+                ws, splits = xtw_partial(h, dU, colsum=True)
             dW1 = torch.empty_like(W1)
             dW2 = torch.empty(bn, 512, device=h.device, dtype=torch.float32)
             db2 = torch.empty(bn, device=h.device, dtype=torch.float32)

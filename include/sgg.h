@@ -113,6 +113,16 @@ int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* A, const fl
                       int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,
                       const int32_t* nchunks_dev, void* stream);
 
+/* The pooling backward's two products of dU (B x 512, row stride ldu) in ONE
+ * launch (models.py:538's Linear: the h half of the first layer): dh = dU W
+ * (W = W1[:, E:], 512 x H at row stride ldw; accumulate != 0 adds to dh) and
+ * the split-K partials of h^T dU plus the column sums of dU into ws, laid
+ * out exactly as sgg_xtw_partial(h, dU, colsum = 1) lays them out
+ * (sgg_xtw_splits(B, H, 512) splits; ws >= splits (512 H + 512) floats), for
+ * sgg_grad_finish to sum.  H <= 64. */
+int sgg_pool_dh_dw(const float* dU, int ldu, const float* W, int ldw, float* dh, int ldh, int accumulate,
+                   const float* h, int ldx, int B, int H, float* ws, size_t ws_bytes, void* stream);
+
 /* Backward of sgg_pool_fwd.  Only the (i, argmax[i,c]) pairs carry gradient
  * (torch.max(dim) backward, models.py:541).  Writes dU (B x 512, every row),
  * and one row per workgroup of the parameter-gradient slab `part`

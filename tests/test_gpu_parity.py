@@ -1190,3 +1190,37 @@ def test_graphed_trainer_two_ranks():
                        capture_output=True, text=True, timeout=110, env=env)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and out.count(" OK") == 2, out[-3000:]
+
+
+@pytest.mark.parametrize("bn,H,sizes", [(48, 48, [20] * 12 + [64, 3]), (8, 32, [20] * 40 + [57, 1])])
+def test_pool_backward_one_launch_equals_two(bn, H, sizes):
+    """The pooling backward's dh = dU W1h and h^T dU partials in one launch
+    (sgg_pool_dh_dw) are bit-identical to the two separate launches (sgg_xw,
+    sgg_xtw_partial): same bodies, same split order -- with and without the
+    accumulated gradient of h from the graph module (GradLink)."""
+    from sgan import kernels as K
+    from sgan.models import PoolHiddenNet
+    from sgan.scene import SceneIndex
+    torch.manual_seed(bn + H)
+    mod = PoolHiddenNet(embedding_dim=16, h_dim=H, mlp_dim=64, bottleneck_dim=bn, batch_norm=False).to(DEV)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    sc = SceneIndex(off, DEV)
+    B = int(off[-1])
+    h0 = torch.randn(B, H, device=DEV)
+    pos = torch.rand(B, 2, device=DEV) * 10
+    dout = torch.randn(B, bn, device=DEV)
+    res = []
+    for dual in (True, False):
+        K.DUAL_POOL_BWD = dual
+        try:
+            mod.zero_grad(set_to_none=True)
+            h = h0.clone().requires_grad_(True)
+            y = mod(h, None, pos, scenes=sc)
+            (y * dout).sum().backward()
+            res.append((h.grad.clone(), {k: p.grad.clone() for k, p in mod.named_parameters()}))
+        finally:
+            K.DUAL_POOL_BWD = True
+    (da, ga), (db, gb) = res
+    assert torch.equal(da, db), "dh"
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), "d" + k
