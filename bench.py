@@ -55,6 +55,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md
 RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)   # FLOP / byte
 CONFIG4_GLOBAL = 4096      # BASELINE configs[3]: synthetic 20-ped, batch 4096, 8 x MI355X
 GRAPH_ITERS = int(os.environ.get("SGG_GRAPH_ITERS", "4"))   # iterations per HIP-graph replay (one rank)
+# one rank: the G-step's prefix graph beside the D-step graph on a second
+# stream (GraphedTrainer(overlap=True))
+OVERLAP = os.environ.get("SGG_OVERLAP", "0") == "1"
 # PMC traffic tables (tools/pmc_traffic.py), newest first
 TRAFFIC_TABLES = [os.path.join(ROOT, "profiles", f) for f in ("r03_pmc_traffic.json", "r02_pmc_traffic.json")]
 # the reference's CPU path, train iteration at batch 64, 8 threads (the survey container)
@@ -367,10 +370,11 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
     from sgan.train_step import GraphedTrainer
     if graph:
         try:
-            g1 = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, **kw)
+            g1 = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, overlap=OVERLAP, **kw)
             gk = None
             if GRAPH_ITERS > 1 and world == 1:
-                gk = GraphedTrainer(trainer, batch, sc, warmup=0, batch_g=batch_g, sc_g=sc_g, iters=GRAPH_ITERS, **kw)
+                gk = GraphedTrainer(trainer, batch, sc, warmup=0, batch_g=batch_g, sc_g=sc_g, iters=GRAPH_ITERS,
+                                    overlap=OVERLAP, **kw)
 
             if gk is not None:   # both graphs replayed once before any timing (first-replay costs)
                 gk.step()

@@ -288,8 +288,35 @@ class GanTrainer:
             return self._g_step(batch, sc, S_global, B_global, shard, inputs)
 
     def _g_step(self, batch, sc, S_global, B_global, shard, inputs):
+        return self._g_rest(self._g_prefix(batch, sc, S_global, B_global, shard, inputs))
+
+    def g_prefix(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None, shared=False):
+        """The part of generator_step that reads G's weights and the G batch
+        only (train.py:441-455): the context (encoder, pooling, GAT, with
+        autograd), the no-grad best-of-k rollout and the per-scene argmin.
+        Nothing of the D-step before it changes its inputs, so it may run
+        beside the D-step (GraphedTrainer(overlap=True)); g_rest(prefix)
+        finishes the G-step after it.  shared=False: the discriminator's
+        observed steps are NOT run in the generator encoder's launch (D's
+        weights change in the D-step's Adam); the G-step's D forward then runs
+        its whole encoder."""
+        if shared:
+            return self._g_prefix(batch, sc, S_global, B_global, shard, inputs)
+        self._no_shared = True
+        try:
+            return self._g_prefix(batch, sc, S_global, B_global, shard, inputs)
+        finally:
+            self._no_shared = False
+
+    def g_rest(self, pre):
+        """The rest of generator_step after g_prefix: the two samples with
+        autograd, the losses, D's frozen forward, backward, clip, Adam."""
+        with self._scope():
+            return self._g_rest(pre)
+
+    def _g_prefix(self, batch, sc, S_global, B_global, shard, inputs):
         a = self.args
-        G, D, ops = self.G, self.D, self.ops
+        G, ops = self.G, self.ops
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, loss_mask, sse) = batch
         S_global = S_global or sc.S
         B_global = B_global or sc.B
@@ -305,20 +332,32 @@ class GanTrainer:
         # the k samples differ only in the noise appended after the graph
         # module: the encoder / pooling / GAT context runs once (with autograd)
         # and only the decoder rolls out k times
-        pfx = self._prefix(obs_rel, 1)
+        pfx = contextlib.nullcontext() if getattr(self, "_no_shared", False) else self._prefix(obs_rel, 1)
         pfx.__enter__()
         try:
             ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
-        except BaseException:
-            pfx.__exit__(None, None, None)
-            raise
-        if self.selective_backward and k > 1:
             best = None
-            if use_l2:
+            if self.selective_backward and k > 1 and use_l2:
                 with torch.no_grad():
                     pred_all = G.decode(ctx.detach(), obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k,
                                         noise_index=(None, 0))
                     best = ops.l2_select(pred_all, pred_gt_rel, mask, sc, k)   # (S,) int64
+        except BaseException:
+            pfx.__exit__(None, None, None)
+            raise
+        return dict(batch=batch, sc=sc, S_global=S_global, B_global=B_global, z_all=z_all, ctx=ctx, best=best,
+                    pfx=pfx, mask=mask, inputs=inputs)
+
+    def _g_rest(self, pre):
+        a = self.args
+        G, D, ops = self.G, self.D, self.ops
+        batch, sc, B_global, z_all, ctx, pfx, mask, inputs = (pre[n] for n in (
+            "batch", "sc", "B_global", "z_all", "ctx", "pfx", "mask", "inputs"))
+        (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, loss_mask, sse) = batch
+        S, B, k = sc.S, sc.B, a.best_k
+        use_l2 = a.l2_loss_weight > 0
+        if self.selective_backward and k > 1:
+            best = pre["best"]
             copies = 2 if use_l2 else 1
             # the last sample's columns become the discriminator input below
             tah = self._traj_ahead(obs_rel, a.pred_len, B, (copies - 1) * B)
@@ -409,6 +448,20 @@ class GanTrainer:
         lg = self.g_step(batch if batch_g is None else batch_g, sc if sc_g is None else sc_g, **kw)
         return ld, lg
 
+    def step_split(self, batch, sc, batch_g=None, sc_g=None, **kw):
+        """The same iteration in the order GraphedTrainer(overlap=True) issues
+        it: g_prefix (the G-step's context, rollout and argmin -- G's weights
+        and the G batch only), the D-step, then g_rest.  Needs pre-drawn host
+        RNG numbers (kw['inputs'], StepInputs): the noise of the G-step is
+        consumed before the D-step's, so the draws must already be in the
+        reference's order."""
+        if kw.get("inputs") is None and self.G.noise_dim:
+            raise ValueError("step_split: pass inputs=StepInputs (draw_inputs) -- the G-step's noise is used first")
+        pre = self.g_prefix(batch if batch_g is None else batch_g, sc if sc_g is None else sc_g, **kw)
+        ld = self.d_step(batch, sc, **kw)
+        lg = self.g_rest(pre)
+        return ld, lg
+
     def draw_inputs(self, S_global, s0, s1):
         """The host draws one iteration makes, in the reference's order (torch
         RNG: D-step noise, then best_k G-step noises; Python random: D real,
@@ -434,17 +487,25 @@ class GraphedTrainer:
     device)."""
 
     def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2, batch_g=None,
-                 sc_g=None, draw=None, prologue=None, iters=1):
+                 sc_g=None, draw=None, prologue=None, iters=1, overlap=False):
         """draw: () -> (z_d, z_g, y) host tensors of the staging shapes (default:
         trainer.draw_inputs over this rank's span); prologue: launches captured
         ahead of the step (the padded real-data path's batch gathers).
         iters (one rank): iterations per graph -- a replay runs `iters`
         consecutive iterations on the same batches (their host draws made in
         order before it), so the per-replay graph launch is paid once per
-        `iters` iterations; step() then advances `iters` iterations."""
+        `iters` iterations; step() then advances `iters` iterations.
+        overlap (one rank): each iteration as three graphs -- the G-step's
+        prefix (GanTrainer.g_prefix: context, best-of-k rollout, argmin),
+        the D-step, the rest of the G-step -- the first two replayed on two
+        streams at once (the prefix depends on G's weights and the G batch
+        only), the third after both.  Forked branches INSIDE one captured
+        graph do not overlap on this runtime (profiles/r04_graph_fork_probe);
+        separate graphs on separate streams do."""
         self.t = trainer
         self.ar_events = None   # time_allreduce()
         self.iters = iters = max(1, int(iters))
+        self.overlap = overlap = bool(overlap) and not (trainer.dp.on and trainer.dp.world > 1)
         self.prologue = prologue or (lambda: None)
         self.batch, self.sc = batch, sc
         self.batch_g, self.sc_g = batch_g, sc_g
@@ -487,7 +548,8 @@ class GraphedTrainer:
             for _ in range(warmup):
                 self._load(*self.draw())
                 self.prologue()
-                trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
+                (trainer.step_split if overlap else trainer.step)(batch, sc, batch_g, sc_g, inputs=self.inp,
+                                                                   **self.kw)
         torch.cuda.current_stream().wait_stream(cap)
         torch.cuda.synchronize()
         trainer.opt_g.zero_grad(set_to_none=True)
@@ -511,6 +573,9 @@ class GraphedTrainer:
             # memory pool: its outputs (the losses, every p.grad) can then
             # never share memory with the other graph's temporaries, so they
             # stay intact while the other graph replays.
+            if overlap:
+                self._capture_overlap(cap, params)
+                return
             for i in range(2):
                 K.clear_fold_cache()   # every fold the replays need must be a node of this graph
                 with torch.cuda.stream(cap), K.capture_guard():
@@ -552,6 +617,63 @@ class GraphedTrainer:
         torch.cuda.synchronize()
         K.clear_fold_cache()
 
+    def _capture_overlap(self, cap, params):
+        """The two alternating graph sets of the overlapped plan: per set a
+        head graph (the H2D copy of its staging buffer, the prologue) and per
+        iteration the prefix / D-step / rest graphs.  Pools: the prefix graphs
+        get their own (they replay beside the D-step, so nothing of theirs
+        may share memory with it), the head, D-step and rest graphs share one
+        (they replay in capture order on one stream).  The fold cache is
+        emptied before each prefix and D-step capture: each computes the
+        folds it reads itself, so no graph reads a fold another graph wrote
+        on the other stream."""
+        t = self.t
+        bg, scg = (self.batch, self.sc) if self.batch_g is None else (self.batch_g, self.sc_g)
+        self.side = torch.cuda.Stream()
+        for i in range(2):
+            pool_b, pool_a = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
+            parts = []
+            with torch.cuda.stream(cap), K.capture_guard():
+                head = torch.cuda.CUDAGraph()
+                head.capture_begin(pool=pool_a)
+                self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
+                self.prologue()
+                head.capture_end()
+                for j in range(self.iters):
+                    K.clear_fold_cache()
+                    gb = torch.cuda.CUDAGraph()
+                    gb.capture_begin(pool=pool_b)
+                    pre = t.g_prefix(bg, scg, inputs=self.inps[j], **self.kw)
+                    gb.capture_end()
+                    K.clear_fold_cache()
+                    ga = torch.cuda.CUDAGraph()
+                    ga.capture_begin(pool=pool_a)
+                    ld = t.d_step(self.batch, self.sc, inputs=self.inps[j], **self.kw)
+                    ga.capture_end()
+                    gc = torch.cuda.CUDAGraph()
+                    gc.capture_begin(pool=pool_a)
+                    lg = t.g_rest(pre)
+                    gc.capture_end()
+                    del pre
+                    parts.append((gb, ga, gc))
+            self.pair.append(((head, parts), (ld, lg), [(p, p.grad) for p in params]))
+        torch.cuda.current_stream().wait_stream(cap)
+        torch.cuda.synchronize()
+        K.clear_fold_cache()
+        self.done_ev = [None, None]
+        self.losses = self.pair[1][1]
+
+    def _replay_overlap(self, head, parts):
+        main = torch.cuda.current_stream()
+        head.replay()
+        for gb, ga, gc in parts:
+            self.side.wait_stream(main)      # G's weights of the previous G-step, the inputs
+            with torch.cuda.stream(self.side):
+                gb.replay()
+            ga.replay()
+            main.wait_stream(self.side)
+            gc.replay()
+
     def _load(self, z_d, z_g, y):
         i = self.cur
         self.cur ^= 1
@@ -585,7 +707,10 @@ class GraphedTrainer:
                     h_zg.copy_(z_g)
                 h_y.copy_(y)
             g, self.losses, grads = self.pair[i]
-            g.replay()
+            if self.overlap:
+                self._replay_overlap(*g)
+            else:
+                g.replay()
             ev = torch.cuda.Event()
             ev.record()
             self.done_ev[i] = ev

@@ -405,6 +405,102 @@ def test_no_grad_rollout_mfma_vs_oracle(T, decoder, B):
             close(mod(rel.to(DEV)), ref(rel).numpy(), rtol=1e-5, what="encoder h")
 
 
+@pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (48, 20, False, 37), (32, 12, True, 37),
+                                            (16, 5, True, 37), (64, 3, False, 37),
+                                            # batches that take the MFMA forward (lstm_mfma.hip)
+                                            (32, 8, False, 4133), (32, 12, True, 4133), (48, 20, False, 2085)])
+def test_fused_lstm_vs_oracle(H, T, decoder, B):
+    """sgg_lstm_fwd/bwd (Encoder / Decoder rollout) against the oracle's
+    torch-CPU modules: outputs and every parameter / input gradient."""
+    from oracle import sgan_oracle as O
+    from sgan import models as M
+    torch.manual_seed(H + T)
+    if decoder:
+        ref, mod = O.Decoder(T, 16, H, 64, 1, False), M.Decoder(T, 16, H, 64, 1, False)
+    else:
+        ref, mod = O.Encoder(16, H), M.Encoder(16, H)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(DEV)
+    if decoder:
+        last_pos, last_rel = torch.randn(B, 2), torch.randn(B, 2) * 0.3
+        h0 = (torch.randn(1, B, H) * 0.5).requires_grad_(True)
+        c0 = torch.zeros(1, B, H)
+        y_ref, _ = ref(last_pos, last_rel, (h0, c0), None)
+        h0d = h0.detach().to(DEV).requires_grad_(True)
+        y, _ = mod(last_pos.to(DEV), last_rel.to(DEV), (h0d, c0.to(DEV)), None)
+        dy = torch.randn_like(y_ref)
+        (y_ref * dy).sum().backward()
+        (y * dy.to(DEV)).sum().backward()
+        close(y, y_ref.detach().numpy(), rtol=1e-5, what="decoder out")
+        close(h0d.grad, h0.grad.numpy(), rtol=1e-4, what="decoder dh0")
+    else:
+        rel = (torch.randn(T, B, 2) * 0.3).requires_grad_(True)
+        y_ref = ref(rel)
+        reld = rel.detach().to(DEV).requires_grad_(True)
+        y = mod(reld)
+        dy = torch.randn_like(y_ref)
+        (y_ref * dy).sum().backward()
+        (y * dy.to(DEV)).sum().backward()
+        close(y, y_ref.detach().numpy(), rtol=1e-5, what="encoder h")
+        close(reld.grad, rel.grad.numpy(), rtol=1e-4, what="encoder drel")
+    for (k, p), (_, q) in zip(ref.named_parameters(), mod.named_parameters()):
+        close(q.grad, p.grad.numpy(), rtol=1e-4, floor=1e-6, what="lstm d" + k)
+
+
+@pytest.mark.parametrize("T,decoder,B", [(12, True, 25600), (8, False, 4133), (12, True, 4099)])
+def test_no_grad_rollout_mfma_vs_oracle(T, decoder, B):
+    """The no-grad batch-MFMA forward (lstm_fwd_mfma_kernel: the best-of-20
+    decoder rollout of the training step, 25,600 sequences) against the
+    oracle's modules."""
+    from oracle import sgan_oracle as O
+    from sgan import models as M
+    H = 32
+    torch.manual_seed(T + B)
+    if decoder:
+        ref, mod = O.Decoder(T, 16, H, 64, 1, False), M.Decoder(T, 16, H, 64, 1, False)
+    else:
+        ref, mod = O.Encoder(16, H), M.Encoder(16, H)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(DEV)
+    with torch.no_grad():
+        if decoder:
+            last_pos, last_rel = torch.randn(B, 2), torch.randn(B, 2) * 0.3
+            h0, c0 = torch.randn(1, B, H) * 0.5, torch.zeros(1, B, H)
+            y_ref, h_ref = ref(last_pos, last_rel, (h0, c0), None)
+            y, h = mod(last_pos.to(DEV), last_rel.to(DEV), (h0.to(DEV), c0.to(DEV)), None)
+            close(y, y_ref.numpy(), rtol=1e-5, what="rollout rel")
+            close(h, h_ref.numpy(), rtol=1e-5, what="rollout h_T")
+        else:
+            rel = torch.randn(T, B, 2) * 0.3
+            close(mod(rel.to(DEV)), ref(rel).numpy(), rtol=1e-5, what="encoder h")
+
+
+@pytest.mark.parametrize("B", [25600, 4099])
+def test_pipelined_rollout_equals_plain(B, monkeypatch):
+    """The software-pipelined no-grad rollout (lstm_roll_mfma_kernel) runs
+    every gate tile's MFMAs in the plain kernel's k order and the same cell
+    arithmetic: outputs and the final state are bitwise equal to
+    lstm_fwd_mfma_kernel's (SGG_ROLL_PLAIN=1)."""
+    from sgan import _native as N
+    from sgan import models as M
+    H, T = 32, 12
+    torch.manual_seed(B)
+    mod = M.Decoder(T, 16, H, 64, 1, False).to(DEV)
+    last_pos, last_rel = torch.randn(B, 2, device=DEV), torch.randn(B, 2, device=DEV) * 0.3
+    h0, c0 = torch.randn(1, B, H, device=DEV) * 0.5, torch.randn(1, B, H, device=DEV) * 0.2
+    lib = N.load()
+    outs = {}
+    for plain in (False, True):
+        if plain:
+            monkeypatch.setenv("SGG_ROLL_PLAIN", "1")
+        name = lib.sgg_lstm_kernel_name(H, B, 1, 0, 0).decode()
+        assert ("lstm_fwd_mfma_kernel" if plain else "lstm_roll_mfma_kernel") in name, name
+        with torch.no_grad():
+            outs[plain] = mod(last_pos, last_rel, (h0, c0), None)
+    assert torch.equal(outs[False][0], outs[True][0]), "rollout rel differs"
+    assert torch.equal(outs[False][1], outs[True][1]), "rollout h_T differs"
+
+
 @pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (32, 12, True, 37), (16, 5, True, 21),
                                             (48, 12, True, 37), (64, 3, True, 37), (48, 20, False, 2085)])
 def test_fused_lstm_other_families(H, T, decoder, B, monkeypatch):
@@ -762,6 +858,59 @@ def test_graphed_trainer_equals_eager(replays):
         err = (ga[k] - gb[k]).abs().max().item()
         assert err <= 1e-6 + 1e-5 * ga[k].abs().max().item(), ("grad", k, err)
     assert (sa - sb).abs().max().item() <= 1e-5 + 1e-5 * sa.abs().max().item(), "eager D forward after replays"
+
+
+@pytest.mark.parametrize("iters", [1, 2])
+def test_graphed_trainer_overlap_equals_eager(iters):
+    """The overlapped plan (GraphedTrainer(overlap=True): the G-step's prefix
+    graph replayed on a second stream beside the D-step graph, the rest of
+    the G-step after both) == the eager sequential iterations, after an odd
+    number of replays (both alternating graph sets used); and the eager
+    step_split order == step() bitwise."""
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, GraphedTrainer
+    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
+    batch_g = synthetic_batch([20, 7, 13, 20, 2], seed=4, device=DEV)
+    res = []
+    for mode in ("eager", "split", "overlap"):
+        g, d = build_models()
+        tr = GanTrainer(g, d, capturable=True)
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
+        torch.manual_seed(11)
+        random.seed(11)
+        n = 1 + 3 * iters
+        if mode == "overlap":
+            gt = GraphedTrainer(tr, batch, sc, warmup=1, batch_g=batch_g, sc_g=scg, iters=iters, overlap=True)
+            for _ in range(3):
+                ld, lg = gt.step()
+        elif mode == "split":
+            for _ in range(n):
+                ld, lg = tr.step_split(batch, sc, batch_g, scg, inputs=_inputs(tr, sc))
+        else:
+            for _ in range(n):
+                ld, lg = tr.step(batch, sc, batch_g, scg)
+        torch.cuda.synchronize()
+        ws = {"g." + k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
+        ws.update({"d." + k: v.detach().cpu().clone() for k, v in d.state_dict().items()})
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws))
+    # eager draws its label-smoothing numbers as Python floats, the other two
+    # take them from the float32 StepInputs: 1e-5 there, 1e-6 between those two
+    for (la, wa), (lb, wb), tol in ((res[1], res[2], 1e-6), (res[0], res[2], 1e-5)):
+        for k in la:
+            assert abs(la[k] - lb[k]) <= tol * max(1.0, abs(la[k])), (k, la[k], lb[k])
+        for k in wa:
+            err = (wa[k] - wb[k]).abs().max().item()
+            assert err <= tol * max(1.0, wa[k].abs().max().item()), (k, err)
+
+
+def _inputs(tr, sc):
+    """StepInputs of one iteration drawn in the reference's order (device)."""
+    from sgan.train_step import StepInputs
+    z_d, z_g, y = tr.draw_inputs(sc.S, 0, sc.S)
+    dv = lambda t: t.to(DEV) if t is not None else None
+    return StepInputs(dv(z_d), dv(z_g), dv(y))
 
 
 def test_graphed_trainer_multi_iteration_equals_eager():

@@ -20,11 +20,15 @@ idx = [i for i, r in enumerate(rows) if "lstm_fwd_mfma" in r["Kernel_Name"]]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) // 2
 a, b = idx[k], idx[k + 1]
 t0 = int(rows[a]["Start_Timestamp"])
-busy, prev = 0, None
+busy, prev, cover, reach = 0, None, 0, t0
 for r in rows[a:b]:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    print("%8.1f %6.1f %6.1f  %-58s grid=%s" % ((s - t0) / 1e3, (e - s) / 1e3, (s - prev) / 1e3 if prev else 0.0,
-                                                short(r["Kernel_Name"]), r.get("Grid_Size_X") or r.get("Grid_Size")))
+    print("%8.1f %6.1f %6.1f  %-58s grid=%s q=%s" % ((s - t0) / 1e3, (e - s) / 1e3, (s - prev) / 1e3 if prev else 0.0,
+                                                     short(r["Kernel_Name"]), r.get("Grid_Size_X") or r.get("Grid_Size"),
+                                                     r.get("Queue_Id", r.get("Stream_Id", "?"))))
     busy += e - s
     prev = e
-print("%d kernels, %.1f us busy, %.1f us period" % (b - a, busy / 1e3, (int(rows[b]["Start_Timestamp"]) - t0) / 1e3))
+    cover += max(0, e - max(s, reach))   # union of the kernels' intervals (two streams may overlap)
+    reach = max(reach, e)
+print("%d kernels, %.1f us busy, %.1f us covered, %.1f us period" % (
+    b - a, busy / 1e3, cover / 1e3, (int(rows[b]["Start_Timestamp"]) - t0) / 1e3))
