@@ -26,6 +26,8 @@
 // decomposition of the reference's (N, N, 2F) concatenation), masked to
 // -inf outside the graph, softmax over j; one wavefront per attention row
 // with lane j (n <= 64), row max / sum by wave shuffles.
+#include <string.h>
+
 #include "sgg_common.h"
 
 
@@ -73,6 +75,17 @@ struct LW {
 // into the LDS image (matrices at pitch N + 1, vectors packed).
 constexpr int kSegs = 4 * kGatEncMaxHeads + 6;
 constexpr int kChunk = 8;
+// the per-batch fields of a forward (the second batch of sgg_gatenc_fwd2)
+struct GatEncSet {
+  const float* X;
+  const float* X2;
+  const float* labels;
+  const int32_t* scene_off;
+  float* y;
+  float* saved;
+  int ldx, ldx2, kx1, S, ldy;
+};
+
 struct StageTab {
   const float* src[kSegs];
   int coff[kSegs];   // first chunk (non-decreasing)
@@ -743,22 +756,46 @@ __device__ long long g_gatenc_prof[2][64];
 #define PMARK(i)
 #endif
 
+// the scene set of virtual scene vs: p's scenes first, then s2's (a
+// forward over two independent batches with the same weights and np in one
+// launch, sgg_gatenc_fwd2); per-field uniform selects, no struct copy
+__device__ __forceinline__ GatEncSet pick_set(const GatEncArgs& p, const GatEncSet& s2, bool two) {
+  GatEncSet q;
+  q.X = two ? s2.X : p.X;
+  q.ldx = two ? s2.ldx : p.ldx;
+  q.X2 = two ? s2.X2 : p.X2;
+  q.ldx2 = two ? s2.ldx2 : p.ldx2;
+  q.kx1 = two ? s2.kx1 : p.kx1;
+  q.labels = two ? s2.labels : p.labels;
+  q.scene_off = two ? s2.scene_off : p.scene_off;
+  q.S = two ? s2.S : p.S;
+  q.y = two ? s2.y : p.y;
+  q.ldy = two ? s2.ldy : p.ldy;
+  q.saved = two ? s2.saved : p.saved;
+  return q;
+}
+
 template <bool BWD, int NH>
-__global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel(GatEncArgs p, StageTab tab) {
+__global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel(GatEncArgs p, StageTab tab,
+                                                                                  GatEncSet s2) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int nh = NH;
   // per-head strides of the weight image, the slab row and the saved state
   constexpr int SEGI = FI * PW72 + 2 * FH, SEGG = FO * PW72 + 2 * FH, PLI = FI * FH + 2 * FH, PLG = FO * FH + 2 * FH;
   const int tid = threadIdx.x;
   // element e = r * FI + k of a scene's input rows (the split input: X2)
-  auto xval = [&](int o, int e) -> float {
+  auto xval = [&](const GatEncSet& q, int o, int e) -> float {
     const int r = e / FI, k = e - r * FI;
-    return p.X2 && k >= p.kx1 ? p.X2[(size_t)(o + r) * p.ldx2 + (k - p.kx1)] : p.X[(size_t)(o + r) * p.ldx + k];
+    return q.X2 && k >= q.kx1 ? q.X2[(size_t)(o + r) * q.ldx2 + (k - q.kx1)] : q.X[(size_t)(o + r) * q.ldx + k];
   };
+  const int nvs = p.S + (BWD ? 0 : s2.S);   // virtual scenes (the backward: p's only)
   // the first scene's inputs are loaded before the weight staging so their
   // latency hides under it (registers; stored after the staging)
   constexpr int kXPre = 3;
-  const int o0 = p.scene_off[blockIdx.x], n0 = p.scene_off[blockIdx.x + 1] - o0;
+  const bool two0 = !BWD && (int)blockIdx.x >= p.S;
+  const GatEncSet q0 = pick_set(p, s2, two0);
+  const int sc0 = two0 ? (int)blockIdx.x - p.S : (int)blockIdx.x;
+  const int o0 = q0.scene_off[sc0], n0 = q0.scene_off[sc0 + 1] - o0;
   const bool pre = n0 > 0 && n0 * FI <= kXPre * (int)blockDim.x;   // uniform
   float xp[kXPre];
   float lp = 0.f;
@@ -766,9 +803,9 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
 #pragma unroll
     for (int m = 0; m < kXPre; ++m) {
       const int e = tid + m * (int)blockDim.x;
-      xp[m] = e < n0 * FI ? xval(o0, e) : 0.f;
+      xp[m] = e < n0 * FI ? xval(q0, o0, e) : 0.f;
     }
-    if (tid < n0) lp = p.labels[o0 + tid];
+    if (tid < n0) lp = q0.labels[o0 + tid];
   }
   PMARK(40);
   LW lw;
@@ -776,7 +813,10 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
   // (the first scene's input stores are followed by a barrier before any use)
   PMARK(41);
 
-  for (int sc = blockIdx.x; sc < p.S; sc += gridDim.x) {
+  for (int vs = blockIdx.x; vs < nvs; vs += gridDim.x) {
+    const bool two = !BWD && vs >= p.S;   // uniform
+    const GatEncSet q = pick_set(p, s2, two);
+    const int sc = two ? vs - p.S : vs;
     // the LDS plan derived per scene from an opaque copy of np: hoisted out
     // of the scene loop, the per-lane addresses spill to scratch
     int NPo = p.np;
@@ -808,12 +848,12 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     float* ginv = reinterpret_cast<float*>(cnt + NP);
     int* Mp = reinterpret_cast<int*>(ginv + NP);
     unsigned long long* gm = reinterpret_cast<unsigned long long*>(lab + gm_offset(NP));
-    const int o = p.scene_off[sc];
-    const int n = p.scene_off[sc + 1] - o;
+    const int o = q.scene_off[sc];
+    const int n = q.scene_off[sc + 1] - o;
     if (n <= 0) continue;   // uniform over the workgroup
     PMARK(0);
-    const bool first = pre && sc == (int)blockIdx.x;   // uniform
-    float* saved = p.saved ? p.saved + (size_t)sc * SL.total : nullptr;
+    const bool first = pre && vs == (int)blockIdx.x;   // uniform
+    float* saved = q.saved ? q.saved + (size_t)sc * SL.total : nullptr;
     // ---- inputs and group structure (one phase) ------------------------
     if (compact) {
       // (X arrives with H1 before the intra backward)
@@ -829,7 +869,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     } else {
       for (int e = tid; e < n * FI; e += blockDim.x) {
         const int r = e / FI;
-        X[r * P40 + (e - r * FI)] = xval(o, e);
+        X[r * P40 + (e - r * FI)] = xval(q, o, e);
       }
     }
     const bool preload = BWD && saved && L.WhIs > 0;   // uniform
@@ -875,7 +915,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       if (tid < 64) {
         const int i = tid;
         const bool in = i < n;
-        const float li = !in ? 0.f : first ? lp : p.labels[o + i];
+        const float li = !in ? 0.f : first ? lp : q.labels[o + i];
         if (in) lab[i] = li;
         unsigned long long rem = __ballot(in);
         int g = i, r = 0, c = 1, m = 0;
@@ -1003,7 +1043,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = r0 + 4 * kq + r;
-            if (row < n) p.y[(size_t)(o + row) * p.ldy + col] = acc[r] + bc;
+            if (row < n) q.y[(size_t)(o + row) * q.ldy + col] = acc[r] + bc;
           }
         }
       }
@@ -1148,7 +1188,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
       for (int e = tid; e < n * FI; e += blockDim.x) {
         const int r = e / FI;
-        X[r * P40 + (e - r * FI)] = xval(o, e);
+        X[r * P40 + (e - r * FI)] = xval(q, o, e);
       }
     }
     lds_barrier(); PMARK(24);
@@ -1310,13 +1350,37 @@ extern "C" int sgg_gatenc_fwd(const GatEncArgs* args, void* stream) {
   const dim3 grid(args->S < kGridCap ? args->S : kGridCap);
   const StageTab tab = make_stage_tab(args->w, args->nh);
   const hipStream_t st = (hipStream_t)stream;
+  const GatEncSet none = {};
   switch (args->nh) {
-    case 1: hipLaunchKernelGGL((gatenc_kernel<false, 1>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
-    case 2: hipLaunchKernelGGL((gatenc_kernel<false, 2>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
-    case 3: hipLaunchKernelGGL((gatenc_kernel<false, 3>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
-    default: hipLaunchKernelGGL((gatenc_kernel<false, 4>), grid, dim3(kFwdThreads), lds, st, *args, tab); break;
+    case 1: hipLaunchKernelGGL((gatenc_kernel<false, 1>), grid, dim3(kFwdThreads), lds, st, *args, tab, none); break;
+    case 2: hipLaunchKernelGGL((gatenc_kernel<false, 2>), grid, dim3(kFwdThreads), lds, st, *args, tab, none); break;
+    case 3: hipLaunchKernelGGL((gatenc_kernel<false, 3>), grid, dim3(kFwdThreads), lds, st, *args, tab, none); break;
+    default: hipLaunchKernelGGL((gatenc_kernel<false, 4>), grid, dim3(kFwdThreads), lds, st, *args, tab, none); break;
   }
   SGG_RETURN_LAUNCH("sgg_gatenc_fwd");
+}
+
+extern "C" int sgg_gatenc_fwd2(const GatEncArgs* a, const GatEncArgs* b, void* stream) {
+  if (int rc = gatenc_check("sgg_gatenc_fwd2 (a)", a, 0)) return rc;
+  if (int rc = gatenc_check("sgg_gatenc_fwd2 (b)", b, 0)) return rc;
+  SGG_CHECK_ARG(a->nh == b->nh && a->np == b->np && a->alpha == b->alpha &&
+                    memcmp(&a->w, &b->w, sizeof(a->w)) == 0,
+                "sgg_gatenc_fwd2: the two batches must share the weights, heads, alpha and np (np %d / %d)", a->np,
+                b->np);
+  const int S = a->S + b->S;
+  if (S == 0) return 0;
+  const size_t lds = (size_t)sgg_gatenc_lds_bytes(a->np, a->nh, 0);
+  const dim3 grid(S < kGridCap ? S : kGridCap);
+  const StageTab tab = make_stage_tab(a->w, a->nh);
+  const hipStream_t st = (hipStream_t)stream;
+  const GatEncSet s2 = {b->X, b->X2, b->labels, b->scene_off, b->y, b->saved, b->ldx, b->ldx2, b->kx1, b->S, b->ldy};
+  switch (a->nh) {
+    case 1: hipLaunchKernelGGL((gatenc_kernel<false, 1>), grid, dim3(kFwdThreads), lds, st, *a, tab, s2); break;
+    case 2: hipLaunchKernelGGL((gatenc_kernel<false, 2>), grid, dim3(kFwdThreads), lds, st, *a, tab, s2); break;
+    case 3: hipLaunchKernelGGL((gatenc_kernel<false, 3>), grid, dim3(kFwdThreads), lds, st, *a, tab, s2); break;
+    default: hipLaunchKernelGGL((gatenc_kernel<false, 4>), grid, dim3(kFwdThreads), lds, st, *a, tab, s2); break;
+  }
+  SGG_RETURN_LAUNCH("sgg_gatenc_fwd2");
 }
 
 extern "C" int sgg_gatenc_bwd(const GatEncArgs* args, void* stream) {
@@ -1327,11 +1391,12 @@ extern "C" int sgg_gatenc_bwd(const GatEncArgs* args, void* stream) {
   const dim3 grid(args->S < kGridCap ? args->S : kGridCap);
   const StageTab tab = make_stage_tab(args->w, args->nh);
   const hipStream_t st = (hipStream_t)stream;
+  const GatEncSet none = {};
   switch (args->nh) {
-    case 1: hipLaunchKernelGGL((gatenc_kernel<true, 1>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
-    case 2: hipLaunchKernelGGL((gatenc_kernel<true, 2>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
-    case 3: hipLaunchKernelGGL((gatenc_kernel<true, 3>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
-    default: hipLaunchKernelGGL((gatenc_kernel<true, 4>), grid, dim3(kBwdThreads), lds, st, *args, tab); break;
+    case 1: hipLaunchKernelGGL((gatenc_kernel<true, 1>), grid, dim3(kBwdThreads), lds, st, *args, tab, none); break;
+    case 2: hipLaunchKernelGGL((gatenc_kernel<true, 2>), grid, dim3(kBwdThreads), lds, st, *args, tab, none); break;
+    case 3: hipLaunchKernelGGL((gatenc_kernel<true, 3>), grid, dim3(kBwdThreads), lds, st, *args, tab, none); break;
+    default: hipLaunchKernelGGL((gatenc_kernel<true, 4>), grid, dim3(kBwdThreads), lds, st, *args, tab, none); break;
   }
   SGG_RETURN_LAUNCH("sgg_gatenc_bwd");
 }

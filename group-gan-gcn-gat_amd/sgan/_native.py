@@ -169,6 +169,7 @@ SIGNATURES = {
     "sgg_gatenc_lds_bytes": (ctypes.c_longlong, [_i, _i, _i]),
     "sgg_gatenc_saved_floats": (ctypes.c_longlong, [_i, _i, _i]),
     "sgg_gatenc_fwd": (_i, [_pargs, _p]),
+    "sgg_gatenc_fwd2": (_i, [_pargs, _pargs, _p]),
     "sgg_gatenc_bwd": (_i, [_pargs, _p]),
     "sgg_gcnmod_param_size": (_i, [_i, _i]),
     "sgg_gcnmod_slab_rows": (_i, [_i]),

@@ -1299,7 +1299,7 @@ class _GatEnc(torch.autograd.Function):
     the inter GAT, out_embedding weight, bias -- the slab order of sgg.h."""
 
     @staticmethod
-    def forward(ctx, x, labels, scenes, nh, alpha, x2, link, dy_link, save, *params):
+    def forward(ctx, x, labels, scenes, nh, alpha, x2, link, dy_link, save, comp, *params):
         lib = _lib()
         ctx.link = link
         ctx.dy_link = dy_link
@@ -1317,13 +1317,26 @@ class _GatEnc(torch.autograd.Function):
             nf = int(lib.sgg_gatenc_saved_floats(max(scenes.S, 1), a.np, nh))
             saved = torch.empty(max(nf, 1), device=x.device, dtype=torch.float32)
             a.saved = N.ptr(saved)
-        N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_fwd")
+        keep = (x, x2, y, labels, scenes, ps, saved)   # the replay closure holds every buffer `a` points to
+        flops = _gatenc_flops(scenes, nh)
+        nbytes = 4.0 * B * (40 + 1 + 24) + (_gatenc_saved_bytes(B, nh) if saved is not None else 0.0)
+        ac = comp.args(nh, alpha, ps, a.np) if comp is not None else None
+        if ac is not None:
+            # the companion batch's scenes first, then this one's (sgg_gatenc_fwd2)
+            keep = keep + comp.keep()
+            flops += _gatenc_flops(comp.scenes, nh)
+            nbytes += 4.0 * comp.x.shape[0] * (40 + 1 + 24)
+            launch = lambda a=a, ac=ac, keep=keep: N.check(
+                lib.sgg_gatenc_fwd2(N.ctypes.byref(ac), N.ctypes.byref(a), N.stream_ptr()), "sgg_gatenc_fwd2")
+        else:
+            if comp is not None:   # (different np: the companion runs alone, first)
+                comp.run_alone(nh, alpha, ps)
+            launch = lambda a=a, keep=keep: N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                    "sgg_gatenc_fwd")
+        launch()
         if timer.active:
-            keep = (x, x2, y, labels, scenes, ps, saved)   # the replay closure holds every buffer `a` points to
-            timer.add("sgg::gatenc_kernel<false>", (scenes.S, B, nh), _gatenc_flops(scenes, nh),
-                      4.0 * B * (40 + 1 + 24) + (_gatenc_saved_bytes(B, nh) if saved is not None else 0.0),
-                      lambda a=a, keep=keep: N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()),
-                                                     "sgg_gatenc_fwd"))
+            timer.add("sgg::gatenc_kernel<false>", (scenes.S, B, nh) + ((comp.scenes.S,) if ac is not None else ()),
+                      flops, nbytes, launch)
         ctx.meta = (labels, scenes, nh, alpha)
         ctx.save_for_backward(x, x2, saved, *ps)
         return y
@@ -1375,7 +1388,48 @@ class _GatEnc(torch.autograd.Function):
         if ctx.link is not None and ctx.needs_input_grad[0]:
             ctx.link.put(dx)   # added by the pooling backward (the other consumer of x), which runs next
             dx = None
-        return (dx, None, None, None, None, dx2, None, None, None) + tuple(grads)
+        return (dx, None, None, None, None, dx2, None, None, None, None) + tuple(grads)
+
+
+class GatEncCompanion:
+    """A second batch through the same GATEncoder forward, without autograd:
+    the discriminator step's generator forward, launched together with the
+    generator step's context (sgg_gatenc_fwd2; G's weights do not change
+    between the two steps, scripts/train.py:395-484).  Its output is `y`
+    once the launch carrying it has been issued."""
+
+    def __init__(self, x, labels, scenes, x2=None):
+        self.x = _rows(x, "x")
+        self.x2 = _rows(x2, "x2") if x2 is not None else None
+        self.labels = _req(labels, "labels").contiguous().view(-1)
+        self.scenes = scenes
+        self.y = None
+
+    def keep(self):
+        return (self.x, self.x2, self.labels, self.scenes, self.y)
+
+    def args(self, nh, alpha, ps, np_other):
+        """The companion's launch arguments when it can share the launch
+        (same np as the batch carrying it), else None."""
+        a = _gatenc_args(self.x, self.labels, self.scenes, nh, alpha, ps, self.x2)
+        if a.np != np_other:
+            return None
+        self.y = torch.empty(self.x.shape[0], 24, device=self.x.device, dtype=torch.float32)
+        a.y, a.ldy = N.ptr(self.y), 24
+        return a
+
+    def run_alone(self, nh, alpha, ps):
+        lib = _lib()
+        a = _gatenc_args(self.x, self.labels, self.scenes, nh, alpha, ps, self.x2)
+        self.y = torch.empty(self.x.shape[0], 24, device=self.x.device, dtype=torch.float32)
+        a.y, a.ldy = N.ptr(self.y), 24
+        keep = self.keep() + (ps,)
+        launch = lambda a=a, keep=keep: N.check(lib.sgg_gatenc_fwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                "sgg_gatenc_fwd")
+        launch()
+        if timer.active:
+            timer.add("sgg::gatenc_kernel<false>", (self.scenes.S, self.x.shape[0], nh),
+                      _gatenc_flops(self.scenes, nh), 4.0 * self.x.shape[0] * (40 + 1 + 24), launch)
 
 
 def _gatenc_flops(scenes, nh):
@@ -1425,16 +1479,17 @@ def gat_encoder_fused_ok(scenes, nh, need_grad):
     return _lib().sgg_gatenc_lds_bytes(max(scenes.max_n, 1), nh, plan) <= 160 * 1024
 
 
-def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None, link=None):
+def gat_encoder(x, labels, scenes, nh, alpha, params, x2=None, link=None, companion=None):
     """GATEncoder.forward (models.py:254-294) for all scenes: (B, 40) -> (B, 24).
     x2: the input as two column blocks [x | x2] (no concatenation copy).
     link: a GradLink that takes the gradient of x instead of returning it
-    (x's other consumer, the pooling net, adds it in its own backward)."""
+    (x's other consumer, the pooling net, adds it in its own backward).
+    companion: a GatEncCompanion whose batch runs in the same launch."""
     lab = _req(labels, "labels").contiguous().view(-1)
     dl = CopiesLink() if torch.is_grad_enabled() else None
     # the forward state is saved only when a backward can follow (not under
     # no_grad, e.g. the generator inside the discriminator step)
-    y = _GatEnc.apply(x, lab, scenes, nh, alpha, x2, link, dl, torch.is_grad_enabled(), *params)
+    y = _GatEnc.apply(x, lab, scenes, nh, alpha, x2, link, dl, torch.is_grad_enabled(), companion, *params)
     if dl is not None:
         y._sgg_copies_link = dl   # found by decoder_init (its only consumer in the generator)
     return y
@@ -2384,6 +2439,17 @@ class _DecoderInit(torch.autograd.Function):
         rel0 = torch.empty(copies * B, 2, device=cvec.device, dtype=torch.float32)
         zc = _req(z, "z").contiguous() if z is not None else None
         last = _req(last_rel, "last_rel").contiguous()
+        # the kernels index z[k][s] and last_rel[p] without bounds: shapes checked here
+        if B != scenes.B or tuple(last.shape) != (B, 2):
+            raise ValueError("decoder_init: context rows %d / last_rel %s vs the scenes' %d peds"
+                             % (B, tuple(last.shape), scenes.B))
+        if zc is not None:
+            need_k = first_k + copies - (1 if best is not None else 0)
+            if zc.dim() != 3 or zc.shape[1] != scenes.S or zc.shape[0] < max(need_k, 1):
+                raise ValueError("decoder_init: noise %s must be (>= %d draws, %d scenes, nz)"
+                                 % (tuple(zc.shape), need_k, scenes.S))
+            if best is not None and (best.numel() != scenes.S or best.dtype != torch.int64):
+                raise ValueError("decoder_init: best must be the %d scenes' int64 sample indices" % scenes.S)
         ps = scenes.ped_scene_i32()
         args = (N.ptr(cvec), cvec.stride(0), Dc, N.ptr(zc), nz, N.ptr(best), int(first_k), int(copies), N.ptr(ps),
                 scenes.S, B, N.ptr(last), N.ptr(h0), N.ptr(rel0))

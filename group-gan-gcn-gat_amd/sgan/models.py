@@ -282,10 +282,17 @@ class GATEncoder(nn.Module):
             ps += [gat.out_att.W, gat.out_att.a]
         return ps + [self.out_embedding.weight, self.out_embedding.bias]
 
-    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None, link=None):
+    def fused_ok(self, sc, need_grad):
+        """The one-launch path (sgg_gatenc_*) takes these scenes."""
+        return ((self.gat_intra.dropout == 0 or not self.training)
+                and K.gat_encoder_fused_ok(sc, len(self.gat_intra.attentions), need_grad))
+
+    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None, link=None, companion=None):
         """h_states: (B, 40), or the pair (encoder state, pooled vector) whose
         concatenation it is (the fused kernel reads both blocks in place).
-        link: GradLink shared with the pooling net (see kernels.GradLink)."""
+        link: GradLink shared with the pooling net (see kernels.GradLink).
+        companion: a kernels.GatEncCompanion (a no-grad batch through the
+        same module) run in the same launch; the fused path only."""
         x2 = None
         if isinstance(h_states, (tuple, list)):
             h_states, x2 = h_states
@@ -296,10 +303,12 @@ class GATEncoder(nn.Module):
         params = self.fused_params()
         need_grad = torch.is_grad_enabled() and (h_states.requires_grad or (x2 is not None and x2.requires_grad)
                                                  or any(p.requires_grad for p in params))
-        if (self.gat_intra.dropout == 0 or not self.training) and K.gat_encoder_fused_ok(sc, nh, need_grad):
+        if self.fused_ok(sc, need_grad):
             # one launch per direction for the whole module (sgg_gatenc_fwd / _bwd)
             return K.gat_encoder(h_states, end_group, sc, nh, self.gat_intra.attentions[0].alpha, params, x2=x2,
-                                 link=link)
+                                 link=link, companion=companion)
+        if companion is not None:
+            raise ValueError("GATEncoder: a companion batch needs the one-launch path (fused_ok)")
         if x2 is not None:
             h_states = torch.cat([h_states, x2], dim=1)
         g = sc.groups(end_group.reshape(-1))
@@ -687,6 +696,41 @@ class TrajectoryGenerator(nn.Module):
         else:
             noise_input = ctx
         return noise_input
+
+    def pair_ok(self, sc_a, sc_b):
+        """context_pair runs its two batches' GATEncoder in one launch."""
+        return (self.graph == "gat" and self.pooling_type == "pool_net" and self.num_layers == 1
+                and self.mlp_decoder_needed() and self.pool_net.fused_ok()
+                and self.gatencoder.fused_ok(sc_a, False) and self.gatencoder.fused_ok(sc_b, True))
+
+    def context_pair(self, a, b):
+        """context() of two batches: a = (obs_traj, obs_traj_rel, seq_start_end,
+        obs_traj_g, scenes) without autograd -- the discriminator step's
+        generator forward (scripts/train.py:400) -- and b with autograd -- the
+        generator step's (:443-455).  G's weights do not change between the
+        two steps (the discriminator step updates D only), so both contexts
+        can be formed at the discriminator step: the GATEncoder of both
+        batches runs in ONE launch (sgg_gatenc_fwd2), each result exactly as
+        context() computes it.  -> (context of a, context of b)."""
+        obs_a, rel_a, sse_a, g_a, sc_a = a
+        obs_b, rel_b, sse_b, g_b, sc_b = b
+        if not self.pair_ok(sc_a, sc_b):
+            with torch.no_grad():
+                ca = self.context(obs_a, rel_a, sse_a, g_a, scenes=sc_a)
+            return ca, self.context(obs_b, rel_b, sse_b, g_b, scenes=sc_b)
+        K.prefold(self.fold_specs())
+        u = K.pool_u_spec(self.pool_net)
+        H = self.encoder_h_dim
+        with torch.no_grad():
+            h_a, U_a = self.encoder(rel_a, proj_u=u)
+            pool_a = self.pool_net(h_a, sse_a, obs_a[-1], scenes=sc_a, U=U_a)
+        h_b, U_b = self.encoder(rel_b, proj_u=u)
+        link = K.GradLink() if torch.is_grad_enabled() else None
+        pool_b = self.pool_net(h_b, sse_b, obs_b[-1], scenes=sc_b, link=link, U=U_b)
+        comp = K.GatEncCompanion(h_a.view(-1, H), g_a[-1], sc_a, x2=pool_a)
+        y_b = self.gatencoder((h_b.view(-1, H), pool_b), sse_b, obs_b[-1], g_b[-1], scenes=sc_b, link=link,
+                              companion=comp)
+        return comp.y, y_b
 
     def decode(self, noise_input, obs_traj, obs_traj_rel, seq_start_end, user_noise=None, *, scenes=None,
                copies=1, noise_index=None):

@@ -52,6 +52,11 @@ from .models import get_noise
 from .scene import SceneIndex
 
 
+# step(): the G-step's generator context formed at the D-step beside the
+# D-step's own (G.context_pair: one GATEncoder launch for both batches)
+PAIR = os.environ.get("SGG_PAIR", "1") != "0"
+
+
 class TrainArgs:
     """scripts/train.py:29-124 defaults of the fields the steps read."""
 
@@ -241,33 +246,62 @@ class GanTrainer:
                 return True
         return False
 
-    def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
+    def d_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None, pair=None):
         """discriminator_step (train.py:395-429). `batch` holds this rank's
         scenes (device tensors), `sc` their SceneIndex.  `inputs` (StepInputs)
-        replaces the host RNG draws by pre-drawn device tensors (graph mode)."""
+        replaces the host RNG draws by pre-drawn device tensors (graph mode).
+        pair = (batch_g, sc_g): the next G-step's batch -- its generator
+        context is formed here beside this step's (G.context_pair: G's weights
+        do not change in between) together with its best-of-k rollout and
+        argmin; returns (losses, prefix) for g_rest(prefix)."""
         with self._scope():
-            return self._d_step(batch, sc, S_global, B_global, shard, inputs)
+            return self._d_step(batch, sc, S_global, B_global, shard, inputs, pair)
 
-    def _d_step(self, batch, sc, S_global, B_global, shard, inputs):
+    def _pairs(self, sc, sc_g):
+        """step() forms the G-step's context at the D-step (d_step pair=)."""
+        G = self.G
+        return (PAIR and self.selective_backward and self.args.best_k > 1 and self.args.l2_loss_weight > 0
+                and hasattr(G, "context_pair") and G.pair_ok(sc, sc_g))
+
+    def _d_step(self, batch, sc, S_global, B_global, shard, inputs, pair=None):
         a = self.args
+        G = self.G
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, _lm, sse) = batch
+        g_kw = (S_global, B_global)   # the G-step's own (None: its batch's sizes)
         S_global = S_global or sc.S
         B_global = B_global or sc.B
         s0 = shard[0]
         z = inputs.z_d if inputs is not None else self._noise(S_global, s0, s0 + sc.S)
         prefold = getattr(self.ops, "prefold", None)
-        if prefold is not None and hasattr(self.G, "fold_specs") and hasattr(self.D, "fold_specs") \
-                and self.G.num_layers == 1 and self.D.encoder.num_layers == 1:
+        if prefold is not None and hasattr(G, "fold_specs") and hasattr(self.D, "fold_specs") \
+                and G.num_layers == 1 and self.D.encoder.num_layers == 1:
             # G's folds (stale since the last G-step) and D's (since the last
             # D-step) in ONE launch; the forwards below find them cached
-            prefold(self.G.fold_specs() + self.D.fold_specs())
-        with self._prefix(obs_rel, 2), self._traj_ahead(obs_rel, pred_gt_rel.shape[0], sc.B, 0, pred_gt_rel, obs[0]):
-            with torch.no_grad():
-                fake_rel = self.G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
-            # D reads traj[0] (the start positions, models.py:989) and traj_rel
-            # only: [fake | real] side by side, no relative_to_abs needed (the
-            # decoder launch writes it: ops.traj_ahead)
-            traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
+            prefold(G.fold_specs() + self.D.fold_specs())
+        pre = None
+        with self._prefix(obs_rel, 2):
+            with self._traj_ahead(obs_rel, pred_gt_rel.shape[0], sc.B, 0, pred_gt_rel, obs[0]):
+                if pair is not None:
+                    # this step's generator context (no autograd) and the G-step's
+                    # (autograd) with one GATEncoder launch for both
+                    bg, scg = pair
+                    ctx_d, ctx_g = G.context_pair((obs, obs_rel, sse, obs_g, sc),
+                                                  (bg[0], bg[2], bg[10], bg[6], scg))
+                    with torch.no_grad():
+                        fake_rel = G.decode(ctx_d, obs, obs_rel, sse, user_noise=z, scenes=sc)
+                else:
+                    with torch.no_grad():
+                        fake_rel = G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
+                # D reads traj[0] (the start positions, models.py:989) and traj_rel
+                # only: [fake | real] side by side, no relative_to_abs needed (the
+                # decoder launch writes it: ops.traj_ahead)
+                traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
+            if pair is not None:   # the G-step's best-of-k rollout and argmin (its D input is not armed here)
+                self._no_shared = True
+                try:
+                    pre = self._g_prefix(bg, scg, g_kw[0], g_kw[1], shard, inputs, ctx=ctx_g)
+                finally:
+                    self._no_shared = False
             sc2 = sc.repeat(2)
             scores = self.D(start, traj_rel, _sse_of(sc2), scenes=sc2)
         if inputs is not None:
@@ -280,7 +314,8 @@ class GanTrainer:
         self.opt_d.zero_grad(set_to_none=True)
         torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device))
         vals = self._finish(self.d_params, self.opt_d, [loss], a.clipping_threshold_d)
-        return {"D_data_loss": vals[0], "D_total_loss": vals[0]}
+        out = {"D_data_loss": vals[0], "D_total_loss": vals[0]}
+        return out if pair is None else (out, pre)
 
     def g_step(self, batch, sc, S_global=None, B_global=None, shard=(0, None), inputs=None):
         """generator_step (train.py:432-484)."""
@@ -314,7 +349,7 @@ class GanTrainer:
         with self._scope():
             return self._g_rest(pre)
 
-    def _g_prefix(self, batch, sc, S_global, B_global, shard, inputs):
+    def _g_prefix(self, batch, sc, S_global, B_global, shard, inputs, ctx=None):
         a = self.args
         G, ops = self.G, self.ops
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, loss_mask, sse) = batch
@@ -335,7 +370,8 @@ class GanTrainer:
         pfx = contextlib.nullcontext() if getattr(self, "_no_shared", False) else self._prefix(obs_rel, 1)
         pfx.__enter__()
         try:
-            ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
+            if ctx is None:   # (else formed by the D-step: G.context_pair)
+                ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
             best = None
             if self.selective_backward and k > 1 and use_l2:
                 with torch.no_grad():
@@ -444,8 +480,12 @@ class GanTrainer:
         reference's loop feeds consecutive loader batches to the two steps
         (scripts/train.py:279-297); batch_g must have the same scene / ped
         counts when S_global / B_global are given."""
+        bg, scg = (batch, sc) if batch_g is None else (batch_g, sc_g)
+        if self._pairs(sc, scg):
+            ld, pre = self.d_step(batch, sc, pair=(bg, scg), **kw)
+            return ld, self.g_rest(pre)
         ld = self.d_step(batch, sc, **kw)
-        lg = self.g_step(batch if batch_g is None else batch_g, sc if sc_g is None else sc_g, **kw)
+        lg = self.g_step(bg, scg, **kw)
         return ld, lg
 
     def step_split(self, batch, sc, batch_g=None, sc_g=None, **kw):

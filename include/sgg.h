@@ -708,6 +708,14 @@ long long sgg_gatenc_saved_floats(int S, int max_n, int nh);
  * when args->saved is NULL. */
 long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd);
 int sgg_gatenc_fwd(const SggGatEncArgs* args, void* stream);
+/* Two independent batches through the same GATEncoder in ONE launch (a's
+ * scenes first, then b's): the discriminator step's generator forward (no
+ * saved state) beside the generator step's context (saved state for its
+ * backward) -- the weights do not change between them (scripts/train.py:
+ * 395-429 updates D only).  Both must have the same weights, heads, alpha
+ * and np; each batch keeps its own X / X2 / labels / scene_off / S / y /
+ * saved, exactly as two sgg_gatenc_fwd calls would write them. */
+int sgg_gatenc_fwd2(const SggGatEncArgs* a, const SggGatEncArgs* b, void* stream);
 int sgg_gatenc_bwd(const SggGatEncArgs* args, void* stream);
 
 /* ------------------------------------------------------------------------

@@ -475,32 +475,6 @@ def test_no_grad_rollout_mfma_vs_oracle(T, decoder, B):
             close(mod(rel.to(DEV)), ref(rel).numpy(), rtol=1e-5, what="encoder h")
 
 
-@pytest.mark.parametrize("B", [25600, 4099])
-def test_pipelined_rollout_equals_plain(B, monkeypatch):
-    """The software-pipelined no-grad rollout (lstm_roll_mfma_kernel) runs
-    every gate tile's MFMAs in the plain kernel's k order and the same cell
-    arithmetic: outputs and the final state are bitwise equal to
-    lstm_fwd_mfma_kernel's (SGG_ROLL_PLAIN=1)."""
-    from sgan import _native as N
-    from sgan import models as M
-    H, T = 32, 12
-    torch.manual_seed(B)
-    mod = M.Decoder(T, 16, H, 64, 1, False).to(DEV)
-    last_pos, last_rel = torch.randn(B, 2, device=DEV), torch.randn(B, 2, device=DEV) * 0.3
-    h0, c0 = torch.randn(1, B, H, device=DEV) * 0.5, torch.randn(1, B, H, device=DEV) * 0.2
-    lib = N.load()
-    outs = {}
-    for plain in (False, True):
-        if plain:
-            monkeypatch.setenv("SGG_ROLL_PLAIN", "1")
-        name = lib.sgg_lstm_kernel_name(H, B, 1, 0, 0).decode()
-        assert ("lstm_fwd_mfma_kernel" if plain else "lstm_roll_mfma_kernel") in name, name
-        with torch.no_grad():
-            outs[plain] = mod(last_pos, last_rel, (h0, c0), None)
-    assert torch.equal(outs[False][0], outs[True][0]), "rollout rel differs"
-    assert torch.equal(outs[False][1], outs[True][1]), "rollout h_T differs"
-
-
 @pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (32, 12, True, 37), (16, 5, True, 21),
                                             (48, 12, True, 37), (64, 3, True, 37), (48, 20, False, 2085)])
 def test_fused_lstm_other_families(H, T, decoder, B, monkeypatch):
@@ -905,6 +879,46 @@ def test_graphed_trainer_overlap_equals_eager(iters):
             assert err <= tol * max(1.0, wa[k].abs().max().item()), (k, err)
 
 
+@pytest.mark.parametrize("graphed", [False, True])
+def test_paired_context_step_is_bit_identical(graphed, monkeypatch):
+    """step() with the G-step's context formed at the D-step beside the
+    D-step's own (G.context_pair: one GATEncoder launch for both batches; the
+    G-step's D forward then runs its whole encoder) == the sequential steps
+    (SGG_PAIR=0), bitwise over three iterations, eager and graph-replayed."""
+    from sgan import train_step as TS
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
+    # eager: a G batch of other scene / ped counts (its own sizes, not the
+    # D batch's, must reach its losses and noise); graphed: the same sizes
+    batch_g = synthetic_batch([20, 7, 13, 20, 2] if graphed else [9, 20, 13, 20, 3, 5], seed=4, device=DEV)
+    res = []
+    for pair in (False, True):
+        monkeypatch.setattr(TS, "PAIR", pair)
+        g, d = build_models()
+        tr = TS.GanTrainer(g, d, capturable=True)
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
+        assert tr._pairs(sc, scg) == pair
+        torch.manual_seed(5)
+        random.seed(5)
+        if graphed:
+            gt = TS.GraphedTrainer(tr, batch, sc, warmup=1, batch_g=batch_g, sc_g=scg)
+            for _ in range(2):
+                ld, lg = gt.step()
+        else:
+            for _ in range(3):
+                ld, lg = tr.step(batch, sc, batch_g, scg)
+        torch.cuda.synchronize()
+        ws = {"g." + k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
+        ws.update({"d." + k: v.detach().cpu().clone() for k, v in d.state_dict().items()})
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws))
+    (la, wa), (lb, wb) = res
+    assert la == lb, (la, lb)
+    for k in wa:
+        assert torch.equal(wa[k], wb[k]), k
+
+
 def _inputs(tr, sc):
     """StepInputs of one iteration drawn in the reference's order (device)."""
     from sgan.train_step import StepInputs
@@ -1007,6 +1021,49 @@ def test_gat_encoder_fused_equals_per_layer(nh, sizes):
     fl = 1e-2 * max(float(g.abs().max()) for g in gr.values())
     for k in gr:
         close(gf[k], gr[k].cpu().numpy(), rtol=2e-4, floor=fl, what="fused d" + k)
+
+
+@pytest.mark.parametrize("nh,sizes_a,sizes_b", [(1, [20, 7, 13, 20, 2], [20, 20, 1, 9]),
+                                                  (2, [5, 31, 12], [12, 40, 3, 3]),
+                                                  (1, [57, 20, 64], [64, 1, 33])])
+def test_gat_encoder_pair_equals_two_launches(nh, sizes_a, sizes_b):
+    """sgg_gatenc_fwd2 (a no-grad batch beside one with autograd: the D-step's
+    generator and the G-step's context) == two sgg_gatenc_fwd launches,
+    bitwise: both outputs, and batch b's saved state through its backward
+    (input and parameter gradients)."""
+    from sgan import kernels as K
+    from sgan.models import GATEncoder
+    from sgan.scene import SceneIndex
+    torch.manual_seed(7 + nh)
+    mod = GATEncoder([40, 16, 40], nh, 0.0, 0.2).to(DEV)
+    sca, scb = (SceneIndex(np.concatenate([[0], np.cumsum(sz)]), DEV) for sz in (sizes_a, sizes_b))
+    sca.max_n = scb.max_n = max(sca.max_n, scb.max_n)   # one LDS plan for both (a capacity bucket's np_cap)
+    Ba, Bb = sum(sizes_a), sum(sizes_b)
+    lab_a = torch.randint(0, 4, (Ba,), device=DEV).float()
+    lab_b = torch.randint(0, 4, (Bb,), device=DEV).float()
+    xa, pa = torch.randn(Ba, 32, device=DEV), torch.randn(Ba, 8, device=DEV)
+    xb, pb = torch.randn(Bb, 32, device=DEV), torch.randn(Bb, 8, device=DEV)
+    dy = torch.randn(Bb, 24, device=DEV)
+    res = []
+    for paired in (False, True):
+        mod.zero_grad(set_to_none=True)
+        xbi, pbi = xb.clone().requires_grad_(True), pb.clone().requires_grad_(True)
+        if paired:
+            comp = K.GatEncCompanion(xa, lab_a, sca, x2=pa)
+            yb = mod((xbi, pbi), None, None, lab_b, scenes=scb, companion=comp)
+            ya = comp.y
+        else:
+            with torch.no_grad():
+                ya = mod((xa, pa), None, None, lab_a, scenes=sca)
+            yb = mod((xbi, pbi), None, None, lab_b, scenes=scb)
+        (yb * dy).sum().backward()
+        res.append((ya, yb.detach(), xbi.grad, pbi.grad, {k: q.grad.clone() for k, q in mod.named_parameters()}))
+    (a0, b0, dx0, dp0, g0), (a1, b1, dx1, dp1, g1) = res
+    assert torch.equal(a0, a1), "companion output"
+    assert torch.equal(b0, b1), "carrying batch output"
+    assert torch.equal(dx0, dx1) and torch.equal(dp0, dp1), "dx"
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), "d" + k
 
 
 def _gat_encoder_vs_oracle(mod, nh, x, lab, sc, dy):
