@@ -351,6 +351,14 @@ extern "C" int sgg_lstm_fwd_seg2(const SggLstmSeg* a, int Ha, const SggLstmSeg* 
   return lstm_mw_fwd_seg2(to_mw(*a), Ha, to_mw(*b), Hb, (hipStream_t)stream);
 }
 
+extern "C" int sgg_lstm_fwd_seg3(const SggLstmSeg* a, int Ha, const SggLstmSeg* b, int Hb, const SggLstmSeg* c, int Hc,
+                                 void* stream) {
+  SGG_CHECK_ARG(a && b && c, "sgg_lstm_fwd_seg3: null segment");
+  SGG_CHECK_ARG(lstm_mw_ok(Ha, a->B) && lstm_mw_ok(Hb, b->B) && lstm_mw_ok(Hc, c->B),
+                "sgg_lstm_fwd_seg3: no four-wave kernel (Ha=%d Hb=%d Hc=%d)", Ha, Hb, Hc);
+  return lstm_mw_fwd_seg3(to_mw(*a), Ha, to_mw(*b), Hb, to_mw(*c), Hc, (hipStream_t)stream);
+}
+
 extern "C" int sgg_lstm_bwd_shared(const float* A, const float* Whh, const float* h_all, const float* c_all,
                                    const float* act_all, const float* rel, const float* dh_last, int T, int B, int H,
                                    int t_sh, int Bsrc, float* drel_in, float* wpart, void* stream) {
@@ -395,10 +403,9 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   }
 }
 
-extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias,
-                                const float* Wp, const float* bp, int T, int B, int H, float* h_all, float* c_all,
-                                float* act_all, float* rel_out, float* rel0_out, const SggTrajOut* to,
-                                void* stream) {
+static int dec_check(const SggDecInit* di, const float* A, const float* Whh, const float* bias, const float* Wp,
+                     const float* bp, int T, int B, int H, float* h_all, float* c_all, float* act_all, float* rel_out,
+                     const SggTrajOut* to) {
   SGG_CHECK_ARG(di && di->ctx && di->ped_scene && di->last_rel && (di->nz == 0 || di->z) && A && Whh && bias &&
                     ((h_all && c_all) || (!h_all && !c_all && !act_all)) && Wp && bp && rel_out,
                 "sgg_lstm_fwd_dec: null pointer");
@@ -413,6 +420,26 @@ extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const floa
                   "sgg_lstm_fwd_dec: bad SggTrajOut sizes (NB=%d T0=%d col0=%d ncol=%d B=%d)", to->NB, to->T0,
                   to->col0, to->ncol, B);
   }
+  return 0;
+}
+
+extern "C" int sgg_lstm_fwd_dec_seg(const SggDecInit* di, const float* A, const float* Whh, const float* bias,
+                                    const float* Wp, const float* bp, int T, int B, int H, float* h_all, float* c_all,
+                                    float* act_all, float* rel_out, float* rel0_out, const SggTrajOut* to,
+                                    const SggLstmSeg* pre, int Hp, void* stream) {
+  if (int rc = dec_check(di, A, Whh, bias, Wp, bp, T, B, H, h_all, c_all, act_all, rel_out, to)) return rc;
+  SGG_CHECK_ARG(pre && B >= 1 && act_all && lstm_mw_ok(H, B) && lstm_mw_ok(Hp, pre->B),
+                "sgg_lstm_fwd_dec_seg: needs a saving four-wave decoder and a prefix segment (H=%d B=%d Hp=%d)", H, B,
+                Hp);
+  return lstm_mw_fwd_dec_seg(A, Whh, bias, Wp, bp, T, B, H, h_all, c_all, act_all, rel_out, di, rel0_out, to,
+                             to_mw(*pre), Hp, (hipStream_t)stream);
+}
+
+extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias,
+                                const float* Wp, const float* bp, int T, int B, int H, float* h_all, float* c_all,
+                                float* act_all, float* rel_out, float* rel0_out, const SggTrajOut* to,
+                                void* stream) {
+  if (int rc = dec_check(di, A, Whh, bias, Wp, bp, T, B, H, h_all, c_all, act_all, rel_out, to)) return rc;
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const bool mw = lstm_mw_ok(H, B);

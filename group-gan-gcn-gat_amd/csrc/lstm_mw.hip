@@ -545,6 +545,33 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd2_kernel(MwSeg a, MwSeg
     mw_fwd_body<HB, false, SB>(b, blockIdx.x - nblk_a);
 }
 
+// a decoder segment (the generator step's best / last samples with saved
+// states, decoder start and discriminator input built in the kernel) and an
+// independent encoder segment (the discriminator's observed-steps prefix of
+// the same step) in ONE launch
+template <int HA, bool SA, int HB, bool SB>
+__global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd2d_kernel(MwSeg a, MwSeg b, int nblk_a) {
+  if ((int)blockIdx.x < nblk_a)
+    mw_fwd_body<HA, true, SA>(a, blockIdx.x);
+  else
+    mw_fwd_body<HB, false, SB>(b, blockIdx.x - nblk_a);
+}
+
+// three independent encoder segments in ONE launch: the discriminator
+// step's generator encoder (a, no saved states) and the discriminator's
+// observed-steps prefix (b) beside the generator step's encoder (c, saved
+// states for its backward) -- G.context_pair
+template <int HA, bool SA, int HB, bool SB, int HC, bool SC>
+__global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd3_kernel(MwSeg a, MwSeg b, MwSeg c, int nblk_a, int nblk_b) {
+  const int blk = blockIdx.x;
+  if (blk < nblk_a)
+    mw_fwd_body<HA, false, SA>(a, blk);
+  else if (blk < nblk_a + nblk_b)
+    mw_fwd_body<HB, false, SB>(b, blk - nblk_a);
+  else
+    mw_fwd_body<HC, false, SC>(c, blk - nblk_a - nblk_b);
+}
+
 template <int H, bool DEC, bool WGRAD>
 __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_bwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Whh, const float* __restrict__ Wp,
@@ -1002,6 +1029,38 @@ int lstm_mw_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb, hipStream_t
   // other hidden-size pairs: two launches
   if (int rc = launch_seg_h(a, Ha, false, st)) return rc;
   return launch_seg_h(b, Hb, false, st);
+}
+
+int lstm_mw_fwd_dec_seg(const float* A, const float* Whh, const float* bias, const float* Wp, const float* bp, int T,
+                        int B, int H, float* h_all, float* c_all, float* act_all, float* rel_out, const SggDecInit* di,
+                        float* rel0_out, const SggTrajOut* to, const MwSeg& b, int Hb, hipStream_t st) {
+  if (int rc = seg_check(b, Hb, "sgg_lstm_fwd_dec_seg (prefix)")) return rc;
+  MwSeg a{nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, B, 0, T, B, h_all, c_all, act_all, rel_out};
+  a.di = *di;
+  a.rel0_out = rel0_out;
+  if (to) a.to = *to;
+  const int na = (B + kMwPeds - 1) / kMwPeds, nb = (b.B + kMwPeds - 1) / kMwPeds;
+  if (H == 32 && Hb == 48 && act_all && b.act_tile) {
+    hipLaunchKernelGGL((lstm_mw_fwd2d_kernel<32, true, 48, true>), dim3(na + nb), dim3(kMwThreads), 0, st, a, b, na);
+    SGG_RETURN_LAUNCH("sgg_lstm_fwd_dec_seg");
+  }
+  if (int rc = launch_seg_h(a, H, true, st)) return rc;   // other sizes: two launches
+  return launch_seg_h(b, Hb, false, st);
+}
+
+int lstm_mw_fwd_seg3(const MwSeg& a, int Ha, const MwSeg& b, int Hb, const MwSeg& c, int Hc, hipStream_t st) {
+  if (int rc = seg_check(a, Ha, "sgg_lstm_fwd_seg3 (a)")) return rc;
+  if (int rc = seg_check(b, Hb, "sgg_lstm_fwd_seg3 (b)")) return rc;
+  if (int rc = seg_check(c, Hc, "sgg_lstm_fwd_seg3 (c)")) return rc;
+  const int na = (a.B + kMwPeds - 1) / kMwPeds, nb = (b.B + kMwPeds - 1) / kMwPeds, nc = (c.B + kMwPeds - 1) / kMwPeds;
+  if (Ha == 32 && Hb == 48 && Hc == 32 && !a.act_tile && b.act_tile && c.act_tile) {
+    hipLaunchKernelGGL((lstm_mw_fwd3_kernel<32, false, 48, true, 32, true>), dim3(na + nb + nc), dim3(kMwThreads), 0, st,
+                       a, b, c, na, nb);
+    SGG_RETURN_LAUNCH("sgg_lstm_fwd_seg3");
+  }
+  // other combinations: the first two in one launch where seg2 has a kernel, then the third
+  if (int rc = lstm_mw_fwd_seg2(a, Ha, b, Hb, st)) return rc;
+  return launch_seg_h(c, Hc, false, st);
 }
 
 int lstm_mw_bwd(const float* A, const float* Whh, const float* Wp, const float* h_all, const float* c_all,

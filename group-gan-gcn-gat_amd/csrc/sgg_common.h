@@ -130,6 +130,14 @@ __device__ __forceinline__ float dec_rel0(const SggDecInit& d, int p, int k) {
 __attribute__((visibility("hidden"))) int lstm_mw_fwd_seg(const MwSeg& s, int H, hipStream_t st);
 __attribute__((visibility("hidden"))) int lstm_mw_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
                                                            hipStream_t st);
+__attribute__((visibility("hidden"))) int lstm_mw_fwd_dec_seg(const float* A, const float* Whh, const float* bias,
+                                                              const float* Wp, const float* bp, int T, int B, int H,
+                                                              float* h_all, float* c_all, float* act_all,
+                                                              float* rel_out, const SggDecInit* di, float* rel0_out,
+                                                              const SggTrajOut* to, const MwSeg& b, int Hb,
+                                                              hipStream_t st);
+__attribute__((visibility("hidden"))) int lstm_mw_fwd_seg3(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
+                                                           const MwSeg& c, int Hc, hipStream_t st);
 
 // fold.hip: the fold backwards of one sgg_grad_finish in one launch (a
 // workgroup each; dA_src / db_src point at the summed (dA, dbias)); internal

@@ -138,6 +138,7 @@ SIGNATURES = {
     "sgg_lstm_bwd_tail": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p]),
     "sgg_lstm_fwd_seg": (_i, [_sargs, _i, _p]),
     "sgg_lstm_fwd_seg2": (_i, [_sargs, _i, _sargs, _i, _p]),
+    "sgg_lstm_fwd_seg3": (_i, [_sargs, _i, _sargs, _i, _sargs, _i, _p]),
     "sgg_lstm_bwd_shared": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p]),
     "sgg_lstm_u_ok": (_i, [_i, _i, _i, _i, _i, _i]),
     "sgg_lstm_fwd_u": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p]),
@@ -149,6 +150,8 @@ SIGNATURES = {
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
     "sgg_lstm_fwd_dec": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
                               ctypes.POINTER(TrajOut), _p]),
+    "sgg_lstm_fwd_dec_seg": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
+                                  ctypes.POINTER(TrajOut), _sargs, _i, _p]),
     "sgg_grad_finish_losses": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz,
                                     ctypes.POINTER(L2Job), _i, ctypes.POINTER(BceJob), _i, _p]),
     "sgg_adam_parts": (_i, [ctypes.c_longlong]),

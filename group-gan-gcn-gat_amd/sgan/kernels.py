@@ -1775,6 +1775,7 @@ class SharedPrefix:
 
     def __init__(self, lstm, emb, obs_rel, T, copies, fold_specs=None):
         self.lstm, self.emb, self.fold_specs = lstm, emb, fold_specs
+        self.obs_rel = obs_rel
         self.key = _tkey(obs_rel)
         self.T_pre, self.Bsrc = int(obs_rel.shape[0]), int(obs_rel.shape[1])
         self.T, self.B = int(T), copies * self.Bsrc
@@ -1790,6 +1791,13 @@ class SharedPrefix:
         """The generator encoder's launch on `rel`: the prefix rides along iff
         rel is obs_rel and the kernel pair is one launch (H_g = 32, H = 48)."""
         return self.ok and not self.ran and H_g == 32 and self.H == 48 and _tkey(rel) == self.key
+
+    def arm_dec(self, H_dec):
+        """A saving decoder launch before the discriminator's forward (the
+        generator step's best / last samples, when no encoder launch of the
+        step carried the prefix: G.context_pair formed the context at the
+        discriminator step) carries it instead (sgg_lstm_fwd_dec_seg)."""
+        return self.ok and not self.ran and H_dec == 32 and self.H == 48
 
     def segment(self, rel):
         """-> SggLstmSeg of the prefix (state buffers allocated here)."""
@@ -1839,6 +1847,58 @@ def shared_prefix(D, obs_rel, T, copies):
         yield _PREFIX[0]
     finally:
         _PREFIX[0] = prev
+
+
+class EncoderRider:
+    """encoder_pair(): the block's first encoder launch that carries a shared
+    prefix (the discriminator step's generator encoder + the discriminator's
+    observed steps) is held instead of launched; the next encoder launch with
+    saved states (the generator step's encoder) issues all three segments in
+    one launch (sgg_lstm_fwd_seg3).  Nothing may read the held launch's
+    outputs before that; a held launch nobody carried is issued on exit."""
+
+    def __init__(self):
+        self.held = None     # ([(SggLstmSeg, H), ...], its own launch, its timer entry)
+        self.timing = None
+        self.done = False
+
+    def hold(self, segs, launch, timing):
+        self.held = (segs, launch)
+        self.timing = timing
+
+    def carry(self, own, H):
+        (a, Ha), (b, Hb) = self.held[0]
+        self.held = None
+        self.done = True
+        lib = _lib()
+        return lambda: N.check(lib.sgg_lstm_fwd_seg3(N.ctypes.byref(a), Ha, N.ctypes.byref(b), Hb,
+                                                     N.ctypes.byref(own), H, N.stream_ptr()), "sgg_lstm_fwd_seg3")
+
+    def flush(self):
+        if self.held is not None:
+            segs, launch = self.held
+            self.held = None
+            launch()
+            if timer.active:
+                name, key, fl, nb = self.timing
+                timer.add(name, key, fl, nb, launch)
+        self.done = True
+
+
+_RIDER = [None]
+
+
+@contextlib.contextmanager
+def encoder_pair():
+    """The first prefix-carrying encoder launch inside the block rides with
+    the next saved-state encoder launch (EncoderRider)."""
+    prev = _RIDER[0]
+    r = _RIDER[0] = EncoderRider()
+    try:
+        yield r
+    finally:
+        _RIDER[0] = prev
+        r.flush()
 
 
 class _LSTMSeq(torch.autograd.Function):
@@ -1943,11 +2003,24 @@ class _LSTMSeq(torch.autograd.Function):
                 # arguments point to (the bench's timer re-issues it later)
                 fkeep = (dkeep, A, Whh, bias, Wpc, bp, h_all, c_all, act, rel_out, rel,
                          (ta.out, ta.start, ta.head, ta.b, ta.pos0) if to is not None else None)
-                fused = lambda k=fkeep, to=to: lib.sgg_lstm_fwd_dec(
-                    N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wpc), N.ptr(bp), T, B, H,
-                    N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out), N.ptr(rel) if save else None,
-                    N.ctypes.byref(to) if to is not None else None, N.stream_ptr())
+                dcarry = pfx is not None and save and pfx.arm_dec(H)
+                if dcarry:
+                    # the discriminator's observed-steps prefix of this step rides along
+                    pseg = pfx.segment(pfx.obs_rel)
+                    pfx.ran = True
+                    kname = "sgg::lstm_mw_fwd2d_kernel<32, true, 48, true>"
+                    fused = lambda k=fkeep, to=to, pseg=pseg, Hp=pfx.H: lib.sgg_lstm_fwd_dec_seg(
+                        N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wpc), N.ptr(bp), T, B, H,
+                        N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out), N.ptr(rel),
+                        N.ctypes.byref(to) if to is not None else None, N.ctypes.byref(pseg), Hp, N.stream_ptr())
+                else:
+                    fused = lambda k=fkeep, to=to: lib.sgg_lstm_fwd_dec(
+                        N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wpc), N.ptr(bp), T, B, H,
+                        N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out), N.ptr(rel) if save else None,
+                        N.ctypes.byref(to) if to is not None else None, N.stream_ptr())
                 rc = fused()
+                if rc != 0 and dcarry:   # (the prefix is owed to the discriminator's forward: no fallback)
+                    N.check(rc, "sgg_lstm_fwd_dec_seg")
                 if rc != 0 and to is not None:   # no family writes the discriminator input here
                     to = None
                     fused = functools.partial(fused, to=None)
@@ -1969,22 +2042,41 @@ class _LSTMSeq(torch.autograd.Function):
                 launch_done = True
             else:
                 launch_done = False
-        if not launch_done:
+        # an encoder pair (encoder_pair(): G.context_pair): the first encoder
+        # launch of the block is held, the next one carries it
+        rider = _RIDER[0]
+        held = carried = False
+        if rider is not None and not launch_done and not decoder:
+            if carry and rider.held is None and not rider.done:
+                held = True
+            elif (u is not None and save and not carry and not cont and rider.held is not None
+                  and len(rider.held[0]) == 2):
+                own = seg(0, T, B)
+                launch = rider.carry(own, H)
+                carried = True
+        if not launch_done and not held:
             launch()
-        if timer.active:
+        if timer.active or held:
             # per ped-step: gates 2 4H (H + 3) FLOP + ~12 H cell / activation; bytes: inputs, saved states
             Ts = T - pfx.T_pre if cont else T    # the steps this launch runs
             fl = Ts * B * (8.0 * H * (H + 3) + 12.0 * H) + (2.0 * B * H * U.shape[1] if U is not None else 0.0)
             nb = 4.0 * (Ts * B * 2 + ((act.numel() + c_all.numel()) * Ts / T + (Ts + 1) * B * H if save else
                                       (0 if no_final else 2 * B * H))
                         + 4 * H * (H + 3) + (T * B * 2 if decoder else 0) + (U.numel() if U is not None else 0))
-            if carry:   # + the prefix: T_pre steps of Bsrc peds, states saved
+            if carry or (decoder and kname is not None):   # + the prefix: T_pre steps of Bsrc peds, states saved
                 Hp, Tp, Bp = pfx.H, pfx.T_pre, pfx.Bsrc
                 fl += Tp * Bp * (8.0 * Hp * (Hp + 3) + 12.0 * Hp)
                 nb += 4.0 * (Tp * Bp * 2 + Tp * Bp * 5 * Hp + (Tp + 1) * Bp * Hp + 4 * Hp * (Hp + 3))
             name = kname or lib.sgg_lstm_kernel_name(H, B, int(decoder), int(save), 0).decode()
-            timer.add(name, (Ts, B, int(decoder), int(save)) + ((pfx.T_pre,) if (carry or cont) else ()), fl, nb,
-                      launch)
+            key = (Ts, B, int(decoder), int(save)) + ((pfx.T_pre,) if (carry or cont) else ())
+            if held:
+                rider.hold([(ga, H), (gb, pfx.H)], launch, (name, key, fl, nb))
+            elif carried:
+                hname, hkey, hfl, hnb = rider.timing
+                timer.add("sgg::lstm_mw_fwd3_kernel<32, false, 48, true, 32, true>", hkey + key, hfl + fl, hnb + nb,
+                          launch)
+            else:
+                timer.add(name, key, fl, nb, launch)
         ctx.meta = (decoder, T, B, H, h0 is not None)
         ctx.slink = slink
         ctx.set_materialize_grads(False)   # unused outputs (the decoder's h_last) get None, not a zero fill

@@ -709,9 +709,11 @@ class TrajectoryGenerator(nn.Module):
         generator forward (scripts/train.py:400) -- and b with autograd -- the
         generator step's (:443-455).  G's weights do not change between the
         two steps (the discriminator step updates D only), so both contexts
-        can be formed at the discriminator step: the GATEncoder of both
-        batches runs in ONE launch (sgg_gatenc_fwd2), each result exactly as
-        context() computes it.  -> (context of a, context of b)."""
+        can be formed at the discriminator step: the encoders of both batches
+        run in ONE launch (sgg_lstm_fwd_seg3, with the discriminator's
+        observed-steps prefix when it is armed on a's input) and so does the
+        GATEncoder (sgg_gatenc_fwd2), each result exactly as context()
+        computes it.  -> (context of a, context of b)."""
         obs_a, rel_a, sse_a, g_a, sc_a = a
         obs_b, rel_b, sse_b, g_b, sc_b = b
         if not self.pair_ok(sc_a, sc_b):
@@ -721,10 +723,14 @@ class TrajectoryGenerator(nn.Module):
         K.prefold(self.fold_specs())
         u = K.pool_u_spec(self.pool_net)
         H = self.encoder_h_dim
+        # both encoders (+ a discriminator prefix armed on a's input) in one
+        # launch: a's is held until b's carries it (kernels.encoder_pair)
+        with K.encoder_pair():
+            with torch.no_grad():
+                h_a, U_a = self.encoder(rel_a, proj_u=u)
+            h_b, U_b = self.encoder(rel_b, proj_u=u)
         with torch.no_grad():
-            h_a, U_a = self.encoder(rel_a, proj_u=u)
             pool_a = self.pool_net(h_a, sse_a, obs_a[-1], scenes=sc_a, U=U_a)
-        h_b, U_b = self.encoder(rel_b, proj_u=u)
         link = K.GradLink() if torch.is_grad_enabled() else None
         pool_b = self.pool_net(h_b, sse_b, obs_b[-1], scenes=sc_b, link=link, U=U_b)
         comp = K.GatEncCompanion(h_a.view(-1, H), g_a[-1], sc_a, x2=pool_a)

@@ -367,8 +367,10 @@ class GanTrainer:
         # the k samples differ only in the noise appended after the graph
         # module: the encoder / pooling / GAT context runs once (with autograd)
         # and only the decoder rolls out k times
-        pfx = contextlib.nullcontext() if getattr(self, "_no_shared", False) else self._prefix(obs_rel, 1)
-        pfx.__enter__()
+        # (no shared prefix here: g_rest arms it for its decoder launch)
+        pfx = None if getattr(self, "_no_shared", False) else self._prefix(obs_rel, 1)
+        if pfx is not None:
+            pfx.__enter__()
         try:
             if ctx is None:   # (else formed by the D-step: G.context_pair)
                 ctx = G.context(obs, obs_rel, sse, obs_g, scenes=sc)
@@ -379,7 +381,8 @@ class GanTrainer:
                                         noise_index=(None, 0))
                     best = ops.l2_select(pred_all, pred_gt_rel, mask, sc, k)   # (S,) int64
         except BaseException:
-            pfx.__exit__(None, None, None)
+            if pfx is not None:
+                pfx.__exit__(None, None, None)
             raise
         return dict(batch=batch, sc=sc, S_global=S_global, B_global=B_global, z_all=z_all, ctx=ctx, best=best,
                     pfx=pfx, mask=mask, inputs=inputs)
@@ -390,78 +393,88 @@ class GanTrainer:
         batch, sc, B_global, z_all, ctx, pfx, mask, inputs = (pre[n] for n in (
             "batch", "sc", "B_global", "z_all", "ctx", "pfx", "mask", "inputs"))
         (obs, pred_gt, obs_rel, pred_gt_rel, _ov, _pv, obs_g, _pg, _nl, loss_mask, sse) = batch
-        S, B, k = sc.S, sc.B, a.best_k
-        use_l2 = a.l2_loss_weight > 0
-        if self.selective_backward and k > 1:
-            best = pre["best"]
-            copies = 2 if use_l2 else 1
-            # the last sample's columns become the discriminator input below
-            tah = self._traj_ahead(obs_rel, a.pred_len, B, (copies - 1) * B)
-            tah.__enter__()
-            try:
-                out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=copies,
-                               noise_index=(best, k - 1))
-            except BaseException:
-                tah.__exit__(None, None, None)
-                raise
+        # the shared prefix stays armed until D's forward, and is disarmed on
+        # any exception before it
+        with contextlib.ExitStack() as stack:
+            S, B, k = sc.S, sc.B, a.best_k
+            use_l2 = a.l2_loss_weight > 0
+            if pfx is None:
+                # the context was formed without the discriminator's observed-steps
+                # prefix (G.context_pair / g_prefix): it rides with the decoder
+                # launch below (D's weights are final by now)
+                stack.enter_context(self._prefix(obs_rel, 1))
+            else:
+                stack.push(pfx)   # (entered by _g_prefix)
+            if self.selective_backward and k > 1:
+                best = pre["best"]
+                copies = 2 if use_l2 else 1
+                # the last sample's columns become the discriminator input below
+                tah = self._traj_ahead(obs_rel, a.pred_len, B, (copies - 1) * B)
+                tah.__enter__()
+                try:
+                    out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=copies,
+                                   noise_index=(best, k - 1))
+                except BaseException:
+                    tah.__exit__(None, None, None)
+                    raise
+                if use_l2:
+                    fake_rel_best, fake_rel_last = ops.split2(out, B)
+                else:
+                    fake_rel_best, fake_rel_last = None, out
+            else:
+                tah = contextlib.nullcontext()
+                out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k, noise_index=(None, 0))
+                fake_rel_last = out[:, (k - 1) * B:]
+                fake_rel_best = None
+                if use_l2:   # every sample in the graph: min over k of the per-scene terms
+                    seg = sc.ped_scene_long()
+                    m = mask.t().unsqueeze(2)
+                    l2s = torch.stack([(m * (pred_gt_rel - out[:, i * B:(i + 1) * B]) ** 2).sum((0, 2))
+                                       for i in range(k)], 0)                       # (k, B)
+                    scene_l2 = torch.zeros(k, S, device=obs.device).index_add_(1, seg, l2s)
+                    mask_sum = torch.zeros(S, device=obs.device).index_add_(0, seg, mask.sum(1))
+            terms = []
+            total = getattr(self.ops, "bce_pair_total", None)
+            fused_total = use_l2 and total is not None and self._bce_override is None
+            # without the one-launch total below, the loss values are read by an
+            # eager add before the backward: they must not be queued (a queued L2
+            # value is formed from terms its backward writes)
+            eager = contextlib.nullcontext if fused_total else getattr(self.ops, "eager_losses", contextlib.nullcontext)
             if use_l2:
-                fake_rel_best, fake_rel_last = ops.split2(out, B)
-            else:
-                fake_rel_best, fake_rel_last = None, out
-        else:
-            tah = contextlib.nullcontext()
-            out = G.decode(ctx, obs, obs_rel, sse, user_noise=z_all, scenes=sc, copies=k, noise_index=(None, 0))
-            fake_rel_last = out[:, (k - 1) * B:]
-            fake_rel_best = None
-            if use_l2:   # every sample in the graph: min over k of the per-scene terms
-                seg = sc.ped_scene_long()
-                m = mask.t().unsqueeze(2)
-                l2s = torch.stack([(m * (pred_gt_rel - out[:, i * B:(i + 1) * B]) ** 2).sum((0, 2))
-                                   for i in range(k)], 0)                       # (k, B)
-                scene_l2 = torch.zeros(k, S, device=obs.device).index_add_(1, seg, l2s)
-                mask_sum = torch.zeros(S, device=obs.device).index_add_(0, seg, mask.sum(1))
-        terms = []
-        total = getattr(self.ops, "bce_pair_total", None)
-        fused_total = use_l2 and total is not None and self._bce_override is None
-        # without the one-launch total below, the loss values are read by an
-        # eager add before the backward: they must not be queued (a queued L2
-        # value is formed from terms its backward writes)
-        eager = contextlib.nullcontext if fused_total else getattr(self.ops, "eager_losses", contextlib.nullcontext)
-        if use_l2:
-            if fake_rel_best is not None:
-                with eager():
-                    g_l2 = ops.l2_loss(fake_rel_best, pred_gt_rel, mask, sc, a.l2_loss_weight)
-            else:
-                g_l2 = (a.l2_loss_weight * scene_l2.min(0)[0] / mask_sum).sum()
-            terms.append(g_l2)
-        # the reference back-propagates into D's weights here and discards the
-        # result (optimizer_d never sees it, train.py:478-482): freeze them for
-        # this forward so D's backward produces input gradients only
-        for p in self.d_params:
-            p.requires_grad_(False)
-        try:
-            scores = D(obs[:1], ops.traj_cat(obs_rel, fake_rel_last), sse, scenes=sc)
-        finally:
-            tah.__exit__(None, None, None)
-            pfx.__exit__(None, None, None)
+                if fake_rel_best is not None:
+                    with eager():
+                        g_l2 = ops.l2_loss(fake_rel_best, pred_gt_rel, mask, sc, a.l2_loss_weight)
+                else:
+                    g_l2 = (a.l2_loss_weight * scene_l2.min(0)[0] / mask_sum).sum()
+                terms.append(g_l2)
+            # the reference back-propagates into D's weights here and discards the
+            # result (optimizer_d never sees it, train.py:478-482): freeze them for
+            # this forward so D's backward produces input gradients only
             for p in self.d_params:
-                p.requires_grad_(True)
-        y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)
-        if terms and fused_total:
-            # gan_g_loss and the total loss with the L2 term from one launch
-            adv, loss = total(scores, scores.shape[0], y, y, sc.B / B_global, terms[0], **_valid(sc))
-        else:
-            with eager():
-                adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global, **_valid(sc))    # gan_g_loss
-            loss = adv + (terms[0] if terms else 0.0)
-        self.opt_g.zero_grad(set_to_none=True)
-        torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self._g_inputs())
-        vals = self._finish(self.g_params, self.opt_g, [terms[0] if terms else adv * 0, adv, loss],
-                            a.clipping_threshold_g)
-        out = {"G_discriminator_loss": vals[1], "G_total_loss": vals[2]}
-        if use_l2:
-            out["G_l2_loss_rel"] = vals[0]
-        return out
+                p.requires_grad_(False)
+            try:
+                scores = D(obs[:1], ops.traj_cat(obs_rel, fake_rel_last), sse, scenes=sc)
+            finally:
+                tah.__exit__(None, None, None)
+                stack.close()   # the prefix is spent once D has run
+                for p in self.d_params:
+                    p.requires_grad_(True)
+            y = inputs.y[2] if inputs is not None else random.uniform(0.7, 1.2)
+            if terms and fused_total:
+                # gan_g_loss and the total loss with the L2 term from one launch
+                adv, loss = total(scores, scores.shape[0], y, y, sc.B / B_global, terms[0], **_valid(sc))
+            else:
+                with eager():
+                    adv = self.bce_pair(scores, scores.shape[0], y, y, sc.B / B_global, **_valid(sc))    # gan_g_loss
+                loss = adv + (terms[0] if terms else 0.0)
+            self.opt_g.zero_grad(set_to_none=True)
+            torch.autograd.backward(loss, grad_tensors=self.ops.one(loss.device), inputs=self._g_inputs())
+            vals = self._finish(self.g_params, self.opt_g, [terms[0] if terms else adv * 0, adv, loss],
+                                a.clipping_threshold_g)
+            out = {"G_discriminator_loss": vals[1], "G_total_loss": vals[2]}
+            if use_l2:
+                out["G_l2_loss_rel"] = vals[0]
+            return out
 
     def _g_inputs(self):
         """G parameters on the forward's path (the family's unused graph

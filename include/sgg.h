@@ -576,6 +576,26 @@ int sgg_lstm_fwd_seg(const SggLstmSeg* seg, int H, void* stream);
 /* Two independent segments in ONE launch (a's workgroups first); one launch
  * for (Ha, Hb) = (32, 48) with b saving states, two launches otherwise. */
 int sgg_lstm_fwd_seg2(const SggLstmSeg* a, int Ha, const SggLstmSeg* b, int Hb, void* stream);
+/* Three independent segments in ONE launch (a's workgroups, then b's, then
+ * c's): the discriminator step's generator encoder (a, no saved states), the
+ * discriminator's observed-steps prefix (b) and the generator step's encoder
+ * (c, saved states) -- G.context_pair forms both steps' contexts at the
+ * discriminator step (G's weights do not change in between).  One launch
+ * for (Ha, Hb, Hc) = (32, 48, 32) with a not saving and b, c saving; else
+ * sgg_lstm_fwd_seg2(a, b) + c. */
+int sgg_lstm_fwd_seg3(const SggLstmSeg* a, int Ha, const SggLstmSeg* b, int Hb, const SggLstmSeg* c, int Hc,
+                      void* stream);
+/* sgg_lstm_fwd_dec (saving, four-wave family) with an independent encoder
+ * segment in the same launch: the generator step's best / last samples
+ * beside the discriminator's observed-steps prefix of that step (pre: the
+ * SggLstmSeg sgg_lstm_fwd_seg2 would carry as b; it needs D's weights after
+ * the discriminator step, so it rides with the first launch of the
+ * generator step that follows them).  One launch for (H, Hp) = (32, 48),
+ * two otherwise. */
+int sgg_lstm_fwd_dec_seg(const SggDecInit* di, const float* A, const float* Whh, const float* bias, const float* Wp,
+                         const float* bp, int T, int B, int H, float* h_all, float* c_all, float* act_all,
+                         float* rel_out, float* rel0_out, const SggTrajOut* to, const SggLstmSeg* pre, int Hp,
+                         void* stream);
 /* sgg_lstm_bwd (encoder) of a Tl = T step sequence whose steps < t_sh were
  * saved once for Bsrc peds (sgg_lstm_fwd_seg with t0 = t_sh): ped p reads the
  * saved states of steps < t_sh (cells and h up to t_sh) of ped p mod Bsrc.
