@@ -435,6 +435,16 @@ extern "C" int sgg_lstm_fwd_dec_seg(const SggDecInit* di, const float* A, const 
                              to_mw(*pre), Hp, (hipStream_t)stream);
 }
 
+extern "C" int sgg_lstm_fwd_dec2(const SggDecInit* di, const SggDecInit* di2, const float* A, const float* Whh,
+                                 const float* bias, const float* Wp, const float* bp, int T, int B, int B2, int H,
+                                 float* rel_out, float* rel_out2, const SggTrajOut* to2, void* stream) {
+  if (int rc = dec_check(di, A, Whh, bias, Wp, bp, T, B, H, nullptr, nullptr, nullptr, rel_out, nullptr)) return rc;
+  if (int rc = dec_check(di2, A, Whh, bias, Wp, bp, T, B2, H, nullptr, nullptr, nullptr, rel_out2, to2)) return rc;
+  SGG_CHECK_ARG(B >= 1 && B2 >= 1 && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"),
+                "sgg_lstm_fwd_dec2: the batch-MFMA rollout family only (H=%d B=%d)", H, B);
+  return lstm_fwd_mfma_dec2(di, di2, A, Whh, bias, Wp, bp, T, B, B2, H, rel_out, rel_out2, to2, (hipStream_t)stream);
+}
+
 extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias,
                                 const float* Wp, const float* bp, int T, int B, int H, float* h_all, float* c_all,
                                 float* act_all, float* rel_out, float* rel0_out, const SggTrajOut* to,

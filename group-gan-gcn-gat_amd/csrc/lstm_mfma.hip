@@ -40,23 +40,75 @@ constexpr float kNegLog2e = -1.4426950408889634f;
 __device__ __forceinline__ float sigm_pre(float y) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y)); }
 __device__ __forceinline__ float tanh_pre(float y) { return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y)), -1.f); }
 
+// a second no-grad decoder segment of the same decoder weights in the same
+// launch (sgg_lstm_fwd_dec2): workgroups from nblk1 on run it -- the
+// discriminator step's generator decoder beside the generator step's
+// best-of-k rollout; its discriminator input (SggTrajOut) written here too
+struct RollSeg2 {
+  SggDecInit di;
+  float* rel_out;
+  SggTrajOut to;
+  int B, nblk1;
+};
+
+__device__ __forceinline__ SggDecInit pick_di(const SggDecInit& a, const SggDecInit& b, bool two) {
+  SggDecInit d;
+  d.ctx = two ? b.ctx : a.ctx;
+  d.ldc = two ? b.ldc : a.ldc;
+  d.Dc = two ? b.Dc : a.Dc;
+  d.z = two ? b.z : a.z;
+  d.nz = two ? b.nz : a.nz;
+  d.best = two ? b.best : a.best;
+  d.first_k = two ? b.first_k : a.first_k;
+  d.ped_scene = two ? b.ped_scene : a.ped_scene;
+  d.S = two ? b.S : a.S;
+  d.Bper = two ? b.Bper : a.Bper;
+  d.last_rel = two ? b.last_rel : a.last_rel;
+  return d;
+}
+
 template <int H>
 __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
-    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B, int decoder,
-    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out,
-    SggDecInit di) {
+    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B1, int decoder,
+    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out1,
+    SggDecInit di1, RollSeg2 s2) {
   constexpr int G4 = 4 * H;
   constexpr int MT = G4 / 16;     // gate-row tiles
   constexpr int MU = H / 16;      // unit tiles (i/f/g/o blocks are MU tiles apart)
   constexpr int KSH = H / 4;      // k-steps over h_{t-1}
   constexpr int NU = H / 4;       // units per lane
-  const bool save = act_all != nullptr;
+  const bool two = s2.B > 0 && (int)blockIdx.x >= s2.nblk1;   // uniform: the second segment's workgroup
+  const bool save = act_all != nullptr && !two;
+  const SggDecInit di = pick_di(di1, s2.di, two);
+  const int B = two ? s2.B : B1;
+  float* __restrict__ rel_out = two ? s2.rel_out : rel_out1;
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, c16 = lane & 15;
-  const int ped = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + c16;
+  const int ped = (((int)blockIdx.x - (two ? s2.nblk1 : 0)) * 4 + (threadIdx.x >> 6)) * 16 + c16;
   const bool valid = ped < B;
+  // the second segment's discriminator input: head steps (both halves), the
+  // real half's steps and the start positions of this lane's column copied
+  // in the prologue; the generated steps stored as they are formed
+  const SggTrajOut& to = s2.to;
+  const int tcol = ped - to.col0;
+  const bool tlive = two && valid && to.out != nullptr && tcol >= 0 && tcol < to.ncol;
+  if (tlive && q == 0) {
+    float2* o2 = reinterpret_cast<float2*>(to.out);
+    const int dup = to.b ? 2 : 1;
+    for (int t = 0; t < to.T0; ++t) {
+      const float2 v = reinterpret_cast<const float2*>(to.head + (size_t)t * to.ldh)[tcol];
+      for (int hf = 0; hf < dup; ++hf) o2[(size_t)t * to.NB + tcol + hf * to.ncol] = v;
+    }
+    if (to.b)
+      for (int t = 0; t < T; ++t)
+        o2[(size_t)(to.T0 + t) * to.NB + to.ncol + tcol] = reinterpret_cast<const float2*>(to.b + (size_t)t * to.ldb)[tcol];
+    if (to.start) {
+      const float2 p0 = reinterpret_cast<const float2*>(to.pos0)[tcol];
+      for (int hf = 0; hf < dup; ++hf) reinterpret_cast<float2*>(to.start)[tcol + hf * to.ncol] = p0;
+    }
+  }
 
   // W_ext in registers, columns in the permuted k order
   float w[MT][KSH + 1];
@@ -159,6 +211,8 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
       px += bp0;
       py += bp1;
       if (valid && q == 0) *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + ped) * 2) = make_float2(px, py);
+      if (tlive && q == 0)
+        reinterpret_cast<float2*>(to.out)[(size_t)(to.T0 + t) * to.NB + tcol] = make_float2(px, py);
       xin = q == 0 ? px : q == 1 ? py : xin;
     } else {
       xin = xnext;
@@ -169,12 +223,16 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
 template <int H>
 int launch(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0, const float* c0,
            const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
-           float* rel_out, hipStream_t st, const SggDecInit* di) {
+           float* rel_out, hipStream_t st, const SggDecInit* di, const RollSeg2* seg2 = nullptr) {
   const int grid = (B + 63) / 64;
   SggDecInit d = {};
   if (di) d = *di;
-  hipLaunchKernelGGL(lstm_fwd_mfma_kernel<H>, dim3(grid), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B,
-                     decoder, h_all, c_all, act_all, rel_out, d);
+  RollSeg2 s2 = {};
+  if (seg2) s2 = *seg2;
+  s2.nblk1 = grid;
+  const int grid2 = s2.B > 0 ? (s2.B + 63) / 64 : 0;
+  hipLaunchKernelGGL(lstm_fwd_mfma_kernel<H>, dim3(grid + grid2), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T,
+                     B, decoder, h_all, c_all, act_all, rel_out, d, s2);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
 }
 
@@ -191,6 +249,21 @@ int lstm_fwd_mfma(const float* rel, const float* A, const float* Whh, const floa
   if (H == 32)
     return launch<32>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st, di);
   return launch<48>(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all, c_all, act_all, rel_out, st, di);
+}
+
+int lstm_fwd_mfma_dec2(const SggDecInit* di, const SggDecInit* di2, const float* A, const float* Whh,
+                       const float* bias, const float* Wp, const float* bp, int T, int B, int B2, int H,
+                       float* rel_out, float* rel_out2, const SggTrajOut* to2, hipStream_t st) {
+  RollSeg2 s2 = {};
+  s2.di = *di2;
+  s2.rel_out = rel_out2;
+  if (to2) s2.to = *to2;
+  s2.B = B2;
+  if (H == 32)
+    return launch<32>(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, 1, nullptr, nullptr, nullptr, rel_out, st,
+                      di, &s2);
+  return launch<48>(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, 1, nullptr, nullptr, nullptr, rel_out, st,
+                    di, &s2);
 }
 
 }  // namespace sgg

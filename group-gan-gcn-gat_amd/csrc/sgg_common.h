@@ -67,6 +67,13 @@ __attribute__((visibility("hidden"))) int lstm_fwd_mfma(const float* rel, const 
                                                         float* rel_out, hipStream_t st,
                                                         const SggDecInit* di = nullptr);
 
+// the rollout with a second no-grad decoder segment (+ its discriminator input) in one launch
+__attribute__((visibility("hidden"))) int lstm_fwd_mfma_dec2(const SggDecInit* di, const SggDecInit* di2,
+                                                             const float* A, const float* Whh, const float* bias,
+                                                             const float* Wp, const float* bp, int T, int B, int B2,
+                                                             int H, float* rel_out, float* rel_out2,
+                                                             const SggTrajOut* to2, hipStream_t st);
+
 // lstm_unit.hip: unit-per-thread LSTM sequence kernels (one barrier per
 // step), dispatched by sgg_lstm_fwd / sgg_lstm_bwd; internal
 __attribute__((visibility("hidden"))) bool lstm_unit_ok(int H, int decoder);

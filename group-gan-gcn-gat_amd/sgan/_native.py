@@ -150,6 +150,8 @@ SIGNATURES = {
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
     "sgg_lstm_fwd_dec": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
                               ctypes.POINTER(TrajOut), _p]),
+    "sgg_lstm_fwd_dec2": (_i, [ctypes.POINTER(DecInit), ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _i,
+                               _p, _p, ctypes.POINTER(TrajOut), _p]),
     "sgg_lstm_fwd_dec_seg": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
                                   ctypes.POINTER(TrajOut), _sargs, _i, _p]),
     "sgg_grad_finish_losses": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz,

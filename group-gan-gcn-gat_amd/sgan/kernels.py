@@ -916,7 +916,15 @@ def capture_guard():
     through a reference cycle is destroyed whenever the collector happens to
     run; if that is inside another capture, ~CUDAGraph's synchronisation is
     illegal on the capturing stream and the process aborts (the round-3
-    hipErrorStreamCaptureUnsupported)."""
+    hipErrorStreamCaptureUnsupported).
+
+    After a capture every object alive is moved to the collector's permanent
+    generation (gc.freeze): the captured graphs and the step state they keep
+    (autograd nodes, staging buffers) live as long as the trainer, and a full
+    collection re-scanning them costs milliseconds on the host while the
+    replayed iterations take a fraction of one (the real-data leg's slow
+    iterations, DESIGN.md section 5).  Reference counting still frees them;
+    only cyclic garbage among them would wait for gc.unfreeze()."""
     import gc
     gc.collect()
     was = gc.isenabled()
@@ -924,6 +932,7 @@ def capture_guard():
     try:
         yield
     finally:
+        gc.freeze()
         if was:
             gc.enable()
 
@@ -1888,6 +1897,65 @@ class EncoderRider:
 _RIDER = [None]
 
 
+class DecoderRider:
+    """decoder_pair(): the block's first no-grad four-wave decoder launch
+    with a fused start that writes the discriminator input (the
+    discriminator step's generator decoder) is held; the next no-grad
+    decoder launch of the same weights on the batch-MFMA family (the
+    generator step's best-of-k rollout) issues both (sgg_lstm_fwd_dec2).
+    Nothing may read the held launch's outputs before that -- its
+    discriminator input is taken by traj_cat without a launch; a held launch
+    nobody carried is issued on exit."""
+
+    def __init__(self):
+        self.held = None
+        self.timing = None
+        self.done = False
+
+    def hold(self, di, rel_out, to, B, H, T, weights, keep, launch):
+        self.held = (di, rel_out, to, B, H, T, weights, keep, launch)
+
+    def fits(self, H, T, *weights):
+        if self.held is None:
+            return False
+        _, _, _, _, Hh, Th, wh, _, _ = self.held
+        return Hh == H and Th == T and all(a is b for a, b in zip(wh, weights))
+
+    def carry(self, di, A, Whh, bias, Wp, bp, T, B, H, rel_out, keep):
+        di2, rel2, to2, B2, _, _, _, keep2, _ = self.held
+        self.held = None
+        self.done = True
+        lib = _lib()
+        return lambda k=(keep, keep2): lib.sgg_lstm_fwd_dec2(
+            N.ctypes.byref(di), N.ctypes.byref(di2), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wp), N.ptr(bp), T, B,
+            B2, H, N.ptr(rel_out), N.ptr(rel2), N.ctypes.byref(to2) if to2 is not None else None, N.stream_ptr())
+
+    def flush(self):
+        if self.held is not None:
+            launch = self.held[-1]
+            self.held = None
+            launch()
+            if timer.active:
+                timer.add(*self.timing, launch)
+        self.done = True
+
+
+_DRIDER = [None]
+
+
+@contextlib.contextmanager
+def decoder_pair():
+    """The discriminator step's decoder launch rides with the rollout's
+    (DecoderRider)."""
+    prev = _DRIDER[0]
+    r = _DRIDER[0] = DecoderRider()
+    try:
+        yield r
+    finally:
+        _DRIDER[0] = prev
+        r.flush()
+
+
 @contextlib.contextmanager
 def encoder_pair():
     """The first prefix-carrying encoder launch inside the block rides with
@@ -1970,6 +2038,7 @@ class _LSTMSeq(torch.autograd.Function):
             pfx.ran = True
         kname = None
         launch_done = False
+        dheld = dcarried = False
         if carry:
             ga, gb = seg(0, T, B), pfx_seg
             kname = "sgg::lstm_mw_fwd2_kernel<32, %s, 48, true>" % ("true" if save else "false")
@@ -2018,9 +2087,21 @@ class _LSTMSeq(torch.autograd.Function):
                         N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wpc), N.ptr(bp), T, B, H,
                         N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out), N.ptr(rel) if save else None,
                         N.ctypes.byref(to) if to is not None else None, N.stream_ptr())
-                rc = fused()
-                if rc != 0 and dcarry:   # (the prefix is owed to the discriminator's forward: no fallback)
-                    N.check(rc, "sgg_lstm_fwd_dec_seg")
+                drider = _DRIDER[0]
+                if drider is not None and not save and not dcarry and h_all is None and Wpc is not None:
+                    mfma = "mfma" in lib.sgg_lstm_kernel_name(H, B, 1, 0, 0).decode()
+                    if not mfma and to is not None and drider.held is None and not drider.done:
+                        # the discriminator step's decoder: held for the rollout's launch
+                        dheld = True
+                    elif mfma and drider.fits(H, T, A, Whh, bias, Wpc, bp):
+                        fused = drider.carry(di, A, Whh, bias, Wpc, bp, T, B, H, rel_out, fkeep)
+                        dcarried = True
+                if dheld:
+                    rc = 0
+                else:
+                    rc = fused()
+                if rc != 0 and (dcarry or dcarried):   # (owed to a later consumer: no fallback)
+                    N.check(rc, "sgg_lstm_fwd_dec_seg" if dcarry else "sgg_lstm_fwd_dec2")
                 if rc != 0 and to is not None:   # no family writes the discriminator input here
                     to = None
                     fused = functools.partial(fused, to=None)
@@ -2029,6 +2110,8 @@ class _LSTMSeq(torch.autograd.Function):
                     if to is not None:   # traj_cat on these columns finds them written
                         ta.filled = (rel_out.data_ptr() + 8 * ta.col0, rel_out.stride(0))
                     launch = lambda: N.check(fused(), "sgg_lstm_fwd_dec")
+                    if dheld:
+                        drider.hold(di, rel_out, to, B, H, T, (A, Whh, bias, Wpc, bp), fkeep, launch)
                 else:
                     if h_all is None:   # (sgg_lstm_fwd writes the final state)
                         h_all = torch.empty(T + 1, B, H, device=dev, dtype=torch.float32)
@@ -2056,7 +2139,7 @@ class _LSTMSeq(torch.autograd.Function):
                 carried = True
         if not launch_done and not held:
             launch()
-        if timer.active or held:
+        if timer.active or held or dheld:
             # per ped-step: gates 2 4H (H + 3) FLOP + ~12 H cell / activation; bytes: inputs, saved states
             Ts = T - pfx.T_pre if cont else T    # the steps this launch runs
             fl = Ts * B * (8.0 * H * (H + 3) + 12.0 * H) + (2.0 * B * H * U.shape[1] if U is not None else 0.0)
@@ -2069,7 +2152,12 @@ class _LSTMSeq(torch.autograd.Function):
                 nb += 4.0 * (Tp * Bp * 2 + Tp * Bp * 5 * Hp + (Tp + 1) * Bp * Hp + 4 * Hp * (Hp + 3))
             name = kname or lib.sgg_lstm_kernel_name(H, B, int(decoder), int(save), 0).decode()
             key = (Ts, B, int(decoder), int(save)) + ((pfx.T_pre,) if (carry or cont) else ())
-            if held:
+            if dheld:
+                drider.timing = (name, key, fl, nb)
+            elif dcarried:
+                hname, hkey, hfl, hnb = drider.timing
+                timer.add(name, key + hkey, fl + hfl, nb + hnb, launch)
+            elif held:
                 rider.hold([(ga, H), (gb, pfx.H)], launch, (name, key, fl, nb))
             elif carried:
                 hname, hkey, hfl, hnb = rider.timing

@@ -55,6 +55,9 @@ from .scene import SceneIndex
 # step(): the G-step's generator context formed at the D-step beside the
 # D-step's own (G.context_pair: one GATEncoder launch for both batches)
 PAIR = os.environ.get("SGG_PAIR", "1") != "0"
+# with PAIR: the D-step's generator decoder launched together with the
+# G-step's best-of-k rollout (kernels.decoder_pair: one batch-MFMA launch)
+DEC_PAIR = os.environ.get("SGG_DEC_PAIR", "1") != "0"
 
 
 class TrainArgs:
@@ -155,6 +158,7 @@ class KernelOps:
     # encoder's launch (kernels.SharedPrefix)
     shared_prefix = staticmethod(K.shared_prefix)
     traj_ahead = staticmethod(K.traj_ahead)
+    decoder_pair = staticmethod(K.decoder_pair)
     # loss ops inside this scope write their values at once (not queued for
     # the finish launch): for values read before the backward
     eager_losses = staticmethod(K.eager_losses)
@@ -279,29 +283,34 @@ class GanTrainer:
             # D-step) in ONE launch; the forwards below find them cached
             prefold(G.fold_specs() + self.D.fold_specs())
         pre = None
+        dpair = getattr(self.ops, "decoder_pair", None)
+        dpair = dpair() if (pair is not None and DEC_PAIR and dpair is not None) else contextlib.nullcontext()
         with self._prefix(obs_rel, 2):
-            with self._traj_ahead(obs_rel, pred_gt_rel.shape[0], sc.B, 0, pred_gt_rel, obs[0]):
+            with dpair:
+                with self._traj_ahead(obs_rel, pred_gt_rel.shape[0], sc.B, 0, pred_gt_rel, obs[0]):
+                    if pair is not None:
+                        # this step's generator context (no autograd) and the G-step's
+                        # (autograd) with one GATEncoder launch for both
+                        bg, scg = pair
+                        ctx_d, ctx_g = G.context_pair((obs, obs_rel, sse, obs_g, sc),
+                                                      (bg[0], bg[2], bg[10], bg[6], scg))
+                        with torch.no_grad():
+                            fake_rel = G.decode(ctx_d, obs, obs_rel, sse, user_noise=z, scenes=sc)
+                    else:
+                        with torch.no_grad():
+                            fake_rel = G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
+                    # D reads traj[0] (the start positions, models.py:989) and traj_rel
+                    # only: [fake | real] side by side, no relative_to_abs needed (the
+                    # decoder launch writes it: ops.traj_ahead)
+                    traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
                 if pair is not None:
-                    # this step's generator context (no autograd) and the G-step's
-                    # (autograd) with one GATEncoder launch for both
-                    bg, scg = pair
-                    ctx_d, ctx_g = G.context_pair((obs, obs_rel, sse, obs_g, sc),
-                                                  (bg[0], bg[2], bg[10], bg[6], scg))
-                    with torch.no_grad():
-                        fake_rel = G.decode(ctx_d, obs, obs_rel, sse, user_noise=z, scenes=sc)
-                else:
-                    with torch.no_grad():
-                        fake_rel = G(obs, obs_rel, sse, obs_g, user_noise=z, scenes=sc)
-                # D reads traj[0] (the start positions, models.py:989) and traj_rel
-                # only: [fake | real] side by side, no relative_to_abs needed (the
-                # decoder launch writes it: ops.traj_ahead)
-                traj_rel, start = self.ops.traj_cat(obs_rel, fake_rel, pred_gt_rel, obs[0])
-            if pair is not None:   # the G-step's best-of-k rollout and argmin (its D input is not armed here)
-                self._no_shared = True
-                try:
-                    pre = self._g_prefix(bg, scg, g_kw[0], g_kw[1], shard, inputs, ctx=ctx_g)
-                finally:
-                    self._no_shared = False
+                    # the G-step's best-of-k rollout (its launch also runs this
+                    # step's decoder, held since above: decoder_pair) and argmin
+                    self._no_shared = True
+                    try:
+                        pre = self._g_prefix(bg, scg, g_kw[0], g_kw[1], shard, inputs, ctx=ctx_g)
+                    finally:
+                        self._no_shared = False
             sc2 = sc.repeat(2)
             scores = self.D(start, traj_rel, _sse_of(sc2), scenes=sc2)
         if inputs is not None:

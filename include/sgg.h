@@ -478,6 +478,17 @@ typedef struct {
 int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, const float* bias, const float* Wp,
                      const float* bp, int T, int B, int H, float* h_all, float* c_all, float* act_all,
                      float* rel_out, float* rel0_out, const SggTrajOut* to, void* stream);
+/* Two no-grad decoder rollouts of the same decoder weights in ONE launch on
+ * the batch-MFMA family (no saved or final states): di's B sequences (the
+ * generator step's best-of-k samples, B >= the family's minimum) and di2's
+ * B2 (the discriminator step's generator decoder), the latter also writing
+ * its discriminator input (to2, may be NULL) as sgg_lstm_fwd_dec would.  The
+ * hidden2pos feedback is formed per step (rel_t = Wp h_t + bp) as in the
+ * rollout, not folded into the recurrence as in the four-wave family: the
+ * same values up to fp32 reassociation. */
+int sgg_lstm_fwd_dec2(const SggDecInit* di, const SggDecInit* di2, const float* A, const float* Whh,
+                      const float* bias, const float* Wp, const float* bp, int T, int B, int B2, int H,
+                      float* rel_out, float* rel_out2, const SggTrajOut* to2, void* stream);
 
 /* Encoder sequence (decoder = 0) with the pooling MLP's h-half fused into the
  * kernel's epilogue (models.py:538): also writes U = h_T Wu^T + cu (B x NU,

@@ -892,6 +892,7 @@ def test_paired_context_step_is_bit_identical(graphed, monkeypatch):
     # eager: a G batch of other scene / ped counts (its own sizes, not the
     # D batch's, must reach its losses and noise); graphed: the same sizes
     batch_g = synthetic_batch([20, 7, 13, 20, 2] if graphed else [9, 20, 13, 20, 3, 5], seed=4, device=DEV)
+    monkeypatch.setattr(TS, "DEC_PAIR", False)   # (test_decoder_pair_step_close: another kernel family)
     res = []
     for pair in (False, True):
         monkeypatch.setattr(TS, "PAIR", pair)
@@ -917,6 +918,105 @@ def test_paired_context_step_is_bit_identical(graphed, monkeypatch):
     assert la == lb, (la, lb)
     for k in wa:
         assert torch.equal(wa[k], wb[k]), k
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_decoder_pair_step_close(graphed, monkeypatch):
+    """The D-step's generator decoder launched with the G-step's best-of-k
+    rollout (kernels.decoder_pair, sgg_lstm_fwd_dec2: the batch-MFMA family,
+    whose hidden2pos feedback is formed per step where the four-wave family
+    folds it into the recurrence) against the separate launches: the same
+    iterations up to fp32 reassociation (losses 1e-5, weights within 0.1 lr
+    per step: Adam normalises near-zero gradient elements)."""
+    from sgan import train_step as TS
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
+    batch_g = synthetic_batch([20, 7, 13, 20, 2], seed=4, device=DEV)
+    res = []
+    for dec_pair in (False, True):
+        monkeypatch.setattr(TS, "DEC_PAIR", dec_pair)
+        g, d = build_models()
+        tr = TS.GanTrainer(g, d, capturable=True)
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
+        torch.manual_seed(5)
+        random.seed(5)
+        if graphed:
+            gt = TS.GraphedTrainer(tr, batch, sc, warmup=1, batch_g=batch_g, sc_g=scg)
+            for _ in range(2):
+                ld, lg = gt.step()
+        else:
+            for _ in range(3):
+                ld, lg = tr.step(batch, sc, batch_g, scg)
+        torch.cuda.synchronize()
+        ws = {"g." + k: v.detach().cpu().clone() for k, v in g.state_dict().items()}
+        ws.update({"d." + k: v.detach().cpu().clone() for k, v in d.state_dict().items()})
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws))
+    (la, wa), (lb, wb) = res
+    for k in la:
+        assert abs(la[k] - lb[k]) <= 1e-5 * max(1.0, abs(la[k])), (k, la[k], lb[k])
+    for k in wa:
+        lr = 1e-3 if k.startswith("d.") else 1e-4
+        err = (wa[k] - wb[k]).abs().max().item()
+        assert err <= 0.1 * lr * 3, (k, err)
+
+
+def test_rollout_with_second_decoder_segment():
+    """sgg_lstm_fwd_dec2: the rollout's sequences bitwise as its own launch
+    (sgg_lstm_fwd_dec), the second segment's within 2e-6 of the four-wave
+    decoder (another fp32 evaluation order), and its discriminator input
+    exactly [head | its own output] (+ [head | b], start positions)."""
+    from sgan import _native as N
+    lib = N.load()
+    torch.manual_seed(21)
+    H, T, T0, nz, Dc = 32, 12, 8, 8, 24
+    Sc, per, copies = 64, 20, 10
+    B1, B2 = copies * Sc * per, Sc * per   # rollout: 10 copies of 64 scenes x 20 peds = 12,800; decoder 1,280
+    A, Whh, bias = torch.randn(4 * H, 2, device=DEV) * .3, torch.randn(4 * H, H, device=DEV) * .2, \
+        torch.randn(4 * H, device=DEV) * .1
+    Wp, bp = torch.randn(2, H, device=DEV) * .3, torch.randn(2, device=DEV) * .1
+
+    def dinit(copies):
+        Bper = Sc * per
+        ctx = torch.randn(Bper, Dc, device=DEV)
+        z = torch.randn(copies, Sc, nz, device=DEV)
+        ps = torch.arange(Bper, device=DEV, dtype=torch.int32) // per
+        last = torch.randn(Bper, 2, device=DEV) * .3
+        d = N.DecInit(N.ptr(ctx), Dc, Dc, N.ptr(z), nz, None, 0, N.ptr(ps), Sc, Bper, N.ptr(last))
+        d._keep = (ctx, z, ps, last)
+        return d
+    d1, d2 = dinit(copies), dinit(1)
+    head = torch.randn(T0, B2, 2, device=DEV)
+    bgt = torch.randn(T, B2, 2, device=DEV)
+    pos0 = torch.randn(B2, 2, device=DEV)
+    outs = {}
+    for mode in ("two", "one"):
+        r1 = torch.full((T, B1, 2), float("nan"), device=DEV)
+        r2 = torch.full((T, B2, 2), float("nan"), device=DEV)
+        trj = torch.full((T0 + T, 2 * B2, 2), float("nan"), device=DEV)
+        st = torch.full((1, 2 * B2, 2), float("nan"), device=DEV)
+        to = N.TrajOut(N.ptr(trj), 2 * B2, T0, 0, B2, N.ptr(head), head.stride(0), N.ptr(bgt), bgt.stride(0),
+                       N.ptr(pos0), N.ptr(st))
+        if mode == "two":
+            N.check(lib.sgg_lstm_fwd_dec2(N.ctypes.byref(d1), N.ctypes.byref(d2), N.ptr(A), N.ptr(Whh), N.ptr(bias),
+                                          N.ptr(Wp), N.ptr(bp), T, B1, B2, H, N.ptr(r1), N.ptr(r2),
+                                          N.ctypes.byref(to), N.stream_ptr()), "dec2")
+        else:
+            N.check(lib.sgg_lstm_fwd_dec(N.ctypes.byref(d1), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wp),
+                                         N.ptr(bp), T, B1, H, None, None, None, N.ptr(r1), None, None,
+                                         N.stream_ptr()), "dec rollout")
+            N.check(lib.sgg_lstm_fwd_dec(N.ctypes.byref(d2), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wp),
+                                         N.ptr(bp), T, B2, H, None, None, None, N.ptr(r2), None, N.ctypes.byref(to),
+                                         N.stream_ptr()), "dec four-wave")
+        torch.cuda.synchronize()
+        outs[mode] = (r1, r2, trj, st)
+    (a1, a2, at, ast), (b1, b2, bt, bst) = outs["two"], outs["one"]
+    assert torch.equal(a1, b1), "rollout segment"
+    close(a2, b2.cpu().numpy(), rtol=2e-6, what="second segment vs four-wave decoder")
+    assert torch.equal(at[:T0, :B2], head) and torch.equal(at[:T0, B2:], head), "head steps"
+    assert torch.equal(at[T0:, :B2], a2) and torch.equal(at[T0:, B2:], bgt), "generated / real steps"
+    assert torch.equal(ast[0, :B2], pos0) and torch.equal(ast[0, B2:], pos0), "start positions"
 
 
 def _inputs(tr, sc):

@@ -7,6 +7,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,15 +38,34 @@ def main():
         bt.step(next(it), next(it))
     torch.cuda.synchronize()
     used = collections.Counter()
+    import gc
+    gcs = [0]
+    gc.callbacks.append(lambda phase, info: gcs.__setitem__(0, gcs[0] + (phase == "start")))
+    caps0 = len(bt.buckets)
     t0 = time.perf_counter()
+    marks = [t0]
     for _ in range(iters):
         sd, sg = next(it), next(it)
         used[bt.bucket_of(dd.layout(sd)[0], dd.layout(sg)[0])] += 1
         bt.step(sd, sg)
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    host = np.diff(marks) * 1e3
+    print("host ms per iteration: median %.3f max %.3f; gc collections %d; buckets captured in the loop %d"
+          % (np.median(host), host.max(), gcs[0], len(bt.buckets) - caps0))
     print("gran %d pad %d caps %s: %.3f ms / iteration, %.0f D-step scenes/s; buckets used %s"
           % (gran, pad, caps, dt / iters * 1e3, 64 * iters / dt, dict(used)), flush=True)
+    if os.environ.get("SGG_PROBE_CPROFILE"):   # where the host's share of an iteration goes
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(iters):
+            bt.step(next(it), next(it))
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(25)
 
 
 if __name__ == "__main__":
