@@ -313,12 +313,34 @@ __device__ void stage_weights(const SggGcnModArgs& a, float* lds, const Geo& L) 
   put(a.boe, 1, a.fe, L.boe, 0);
 }
 
+// the per-batch fields of a forward: batch a's, or (two) the second batch's
+// of sgg_gcnmod_fwd2 -- per-field uniform selects (weights, np, fin, fe, bf16
+// are shared)
+__device__ __forceinline__ SggGcnModArgs pick_batch(const SggGcnModArgs& a, const SggGcnModArgs& b, bool two) {
+  SggGcnModArgs q = a;
+  q.X = two ? b.X : a.X;
+  q.ldx = two ? b.ldx : a.ldx;
+  q.X2 = two ? b.X2 : a.X2;
+  q.ldx2 = two ? b.ldx2 : a.ldx2;
+  q.kx1 = two ? b.kx1 : a.kx1;
+  q.labels = two ? b.labels : a.labels;
+  q.scene_off = two ? b.scene_off : a.scene_off;
+  q.S = two ? b.S : a.S;
+  q.y = two ? b.y : a.y;
+  q.ldy = two ? b.ldy : a.ldy;
+  return q;
+}
+
 template <bool BF>
-__global__ void __launch_bounds__(kThreads) gcnmod_fwd_kernel(const SggGcnModArgs a) {
+__global__ void __launch_bounds__(kThreads) gcnmod_fwd_kernel(const SggGcnModArgs a1, const SggGcnModArgs a2,
+                                                              int S2) {
   extern __shared__ float lds[];
-  const Geo L = make_geo(a.np, a.fin, a.fe, false);
-  stage_weights<BF>(a, lds, L);
-  for (int s = blockIdx.x; s < a.S; s += gridDim.x) {
+  const Geo L = make_geo(a1.np, a1.fin, a1.fe, false);
+  stage_weights<BF>(a1, lds, L);
+  for (int vs = blockIdx.x; vs < a1.S + S2; vs += gridDim.x) {
+    const bool two = vs >= a1.S;   // uniform
+    const SggGcnModArgs a = pick_batch(a1, a2, two);
+    const int s = two ? vs - a1.S : vs;
     const int p0 = a.scene_off[s], n = a.scene_off[s + 1] - p0;
     if (n <= 0) continue;
     if (threadIdx.x < 64) groups(a.labels, p0, n, lds, L);
@@ -534,10 +556,27 @@ extern "C" int sgg_gcnmod_fwd(const SggGcnModArgs* a, void* stream) {
   const size_t lds = 4 * (size_t)make_geo(a->np, a->fin, a->fe, false).total;
   const dim3 grid(a->S < kFwdGridCap ? a->S : kFwdGridCap);
   if (a->bf16)
-    hipLaunchKernelGGL(gcnmod_fwd_kernel<true>, grid, dim3(kThreads), lds, (hipStream_t)stream, *a);
+    hipLaunchKernelGGL(gcnmod_fwd_kernel<true>, grid, dim3(kThreads), lds, (hipStream_t)stream, *a, *a, 0);
   else
-    hipLaunchKernelGGL(gcnmod_fwd_kernel<false>, grid, dim3(kThreads), lds, (hipStream_t)stream, *a);
+    hipLaunchKernelGGL(gcnmod_fwd_kernel<false>, grid, dim3(kThreads), lds, (hipStream_t)stream, *a, *a, 0);
   SGG_RETURN_LAUNCH("sgg_gcnmod_fwd");
+}
+
+extern "C" int sgg_gcnmod_fwd2(const SggGcnModArgs* a, const SggGcnModArgs* b, void* stream) {
+  if (int rc = gcnmod_check("sgg_gcnmod_fwd2 (a)", a, 0)) return rc;
+  if (int rc = gcnmod_check("sgg_gcnmod_fwd2 (b)", b, 0)) return rc;
+  SGG_CHECK_ARG(a->np == b->np && a->fin == b->fin && a->fe == b->fe && a->bf16 == b->bf16 && a->W0i == b->W0i &&
+                    a->W1i == b->W1i && a->W0g == b->W0g && a->W1g == b->W1g && a->Woe == b->Woe && a->boe == b->boe,
+                "sgg_gcnmod_fwd2: the two batches must share the weights, np, fin, fe and precision");
+  const int S = a->S + b->S;
+  if (S == 0) return 0;
+  const size_t lds = 4 * (size_t)make_geo(a->np, a->fin, a->fe, false).total;
+  const dim3 grid(S < kFwdGridCap ? S : kFwdGridCap);
+  if (a->bf16)
+    hipLaunchKernelGGL(gcnmod_fwd_kernel<true>, grid, dim3(kThreads), lds, (hipStream_t)stream, *a, *b, b->S);
+  else
+    hipLaunchKernelGGL(gcnmod_fwd_kernel<false>, grid, dim3(kThreads), lds, (hipStream_t)stream, *a, *b, b->S);
+  SGG_RETURN_LAUNCH("sgg_gcnmod_fwd2");
 }
 
 extern "C" int sgg_gcnmod_bwd(const SggGcnModArgs* a, void* stream) {

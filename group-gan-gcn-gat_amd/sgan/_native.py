@@ -180,6 +180,7 @@ SIGNATURES = {
     "sgg_gcnmod_slab_rows": (_i, [_i]),
     "sgg_gcnmod_lds_bytes": (ctypes.c_longlong, [_i, _i, _i, _i]),
     "sgg_gcnmod_fwd": (_i, [_gargs, _p]),
+    "sgg_gcnmod_fwd2": (_i, [_gargs, _gargs, _p]),
     "sgg_gcnmod_bwd": (_i, [_gargs, _p]),
     "sgg_slab_reduce": (_i, [_p, _i, _i, _p, _p]),
     "sgg_gather_batch_floats": (ctypes.c_longlong, [_i, _i, _i]),

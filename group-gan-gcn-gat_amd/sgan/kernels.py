@@ -1516,7 +1516,7 @@ class _GcnMod(torch.autograd.Function):
     out_embedding weight, bias -- the slab order of sgg.h."""
 
     @staticmethod
-    def forward(ctx, x, labels, scenes, x2, link, dy_link, bf16, *params):
+    def forward(ctx, x, labels, scenes, x2, link, dy_link, bf16, comp, *params):
         lib = _lib()
         ctx.link, ctx.dy_link = link, dy_link
         x = _rows(x, "x")
@@ -1529,13 +1529,26 @@ class _GcnMod(torch.autograd.Function):
         y = torch.empty(B, fe, device=x.device, dtype=torch.float32)
         a = _gcnmod_args(x, x2, labels, scenes, ps, bf16)
         a.y, a.ldy = N.ptr(y), fe
-        N.check(lib.sgg_gcnmod_fwd(N.ctypes.byref(a), N.stream_ptr()), "sgg_gcnmod_fwd")
+        keep = (x, x2, y, labels, scenes, ps)
+        flops = _gcnmod_flops(scenes, labels, a.fin, fe)
+        nbytes = 4.0 * B * (a.fin + 1 + fe)
+        ac = comp.args(ps, bf16, fe, a.np, a.fin) if comp is not None else None
+        if ac is not None:
+            # the companion batch's scenes first, then this one's (sgg_gcnmod_fwd2)
+            keep = keep + comp.keep()
+            flops += _gcnmod_flops(comp.scenes, comp.labels, a.fin, fe)
+            nbytes += 4.0 * comp.x.shape[0] * (a.fin + 1 + fe)
+            launch = lambda a=a, ac=ac, keep=keep: N.check(
+                lib.sgg_gcnmod_fwd2(N.ctypes.byref(ac), N.ctypes.byref(a), N.stream_ptr()), "sgg_gcnmod_fwd2")
+        else:
+            if comp is not None:   # (different np: the companion runs alone, first)
+                comp.run_alone(ps, bf16, fe)
+            launch = lambda a=a, keep=keep: N.check(lib.sgg_gcnmod_fwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                    "sgg_gcnmod_fwd")
+        launch()
         if timer.active:
-            keep = (x, x2, y, labels, scenes, ps)
-            timer.add("sgg::gcnmod_fwd_kernel<%s>" % ("true" if bf16 else "false"), (scenes.S, B, a.fin),
-                      _gcnmod_flops(scenes, labels, a.fin, fe), 4.0 * B * (a.fin + 1 + fe),
-                      lambda a=a, keep=keep: N.check(lib.sgg_gcnmod_fwd(N.ctypes.byref(a), N.stream_ptr()),
-                                                     "sgg_gcnmod_fwd"))
+            timer.add("sgg::gcnmod_fwd_kernel<%s>" % ("true" if bf16 else "false"),
+                      (scenes.S, B, a.fin) + ((comp.scenes.S,) if ac is not None else ()), flops, nbytes, launch)
         ctx.meta = (labels, scenes, bf16)
         ctx.save_for_backward(x, x2, *ps)
         return y
@@ -1587,7 +1600,47 @@ class _GcnMod(torch.autograd.Function):
         if ctx.link is not None and ctx.needs_input_grad[0]:
             ctx.link.put(dx)   # added by the pooling backward (the other consumer of x), which runs next
             dx = None
-        return (dx, None, None, dx2, None, None, None) + tuple(grads)
+        return (dx, None, None, dx2, None, None, None, None) + tuple(grads)
+
+
+class GcnModCompanion:
+    """A second batch through the same GCNModule forward without autograd,
+    launched with the batch that carries it (sgg_gcnmod_fwd2); see
+    GatEncCompanion.  Its output is `y` once that launch is issued."""
+
+    def __init__(self, x, labels, scenes, x2=None):
+        self.x = _rows(x, "x")
+        self.x2 = _rows(x2, "x2") if x2 is not None else None
+        self.labels = _req(labels, "labels").contiguous().view(-1)
+        self.scenes = scenes
+        self.y = None
+
+    def keep(self):
+        return (self.x, self.x2, self.labels, self.scenes, self.y)
+
+    def _args(self, ps, bf16, fe):
+        a = _gcnmod_args(self.x, self.x2, self.labels, self.scenes, ps, bf16)
+        self.y = torch.empty(self.x.shape[0], fe, device=self.x.device, dtype=torch.float32)
+        a.y, a.ldy = N.ptr(self.y), fe
+        return a
+
+    def args(self, ps, bf16, fe, np_other, fin_other):
+        a = _gcnmod_args(self.x, self.x2, self.labels, self.scenes, ps, bf16)
+        if a.np != np_other or a.fin != fin_other:
+            return None
+        return self._args(ps, bf16, fe)
+
+    def run_alone(self, ps, bf16, fe):
+        lib = _lib()
+        a = self._args(ps, bf16, fe)
+        keep = self.keep() + (ps,)
+        launch = lambda a=a, keep=keep: N.check(lib.sgg_gcnmod_fwd(N.ctypes.byref(a), N.stream_ptr()),
+                                                "sgg_gcnmod_fwd")
+        launch()
+        if timer.active:
+            timer.add("sgg::gcnmod_fwd_kernel<%s>" % ("true" if bf16 else "false"),
+                      (self.scenes.S, self.x.shape[0], a.fin), _gcnmod_flops(self.scenes, self.labels, a.fin, fe),
+                      4.0 * self.x.shape[0] * (a.fin + 1 + fe), launch)
 
 
 def _gcnmod_flops(scenes, labels, fin, fe):
@@ -1621,12 +1674,13 @@ def gcn_module_fused_ok(scenes, fin, fe, params_ok=True):
     return 0 <= _lib().sgg_gcnmod_lds_bytes(scenes.max_n, fin, fe, 1) <= 160 * 1024
 
 
-def gcn_module(x, labels, scenes, params, x2=None, link=None):
+def gcn_module(x, labels, scenes, params, x2=None, link=None, companion=None):
     """GCNModule.forward (models.py:628-712) for all scenes: (B, fin) -> (B, fe),
-    the input optionally as two column blocks [x | x2]; link as gat_encoder."""
+    the input optionally as two column blocks [x | x2]; link as gat_encoder;
+    companion: a GcnModCompanion whose batch runs in the same launch."""
     lab = _req(labels, "labels").contiguous().view(-1)
     dl = CopiesLink() if torch.is_grad_enabled() else None
-    y = _GcnMod.apply(x, lab, scenes, x2, link, dl, _PRECISION == "bf16", *params)
+    y = _GcnMod.apply(x, lab, scenes, x2, link, dl, _PRECISION == "bf16", companion, *params)
     if dl is not None:
         y._sgg_copies_link = dl   # found by decoder_init (its only consumer in the generator)
     return y

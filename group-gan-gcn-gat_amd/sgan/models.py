@@ -451,20 +451,28 @@ class GCNModule(nn.Module):
             return None
         return [gi[0], gi[1], gg[0], gg[1], self.out_embedding.weight, self.out_embedding.bias]
 
-    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None, link=None):
+    def fused_ok(self, sc, fin):
+        """The one-launch path (sgg_gcnmod_*) takes these scenes and inputs."""
+        params = self.fused_params()
+        return (params is not None and params[0].shape[0] == fin
+                and K.gcn_module_fused_ok(sc, fin, self.out_embedding.out_features))
+
+    def forward(self, h_states, seq_start_end, end_pos, end_group, scenes=None, link=None, companion=None):
         """h_states: (B, 40), or the pair (encoder state, pooled vector) whose
         concatenation it is (the fused kernel reads both blocks in place).
-        link: GradLink shared with the pooling net (see kernels.GradLink)."""
+        link: GradLink shared with the pooling net (see kernels.GradLink).
+        companion: a kernels.GcnModCompanion run in the same launch (fused path)."""
         x2 = None
         if isinstance(h_states, (tuple, list)):
             h_states, x2 = h_states
         sc = _scenes(seq_start_end, h_states.device, scenes)
         params = self.fused_params()
         fin = h_states.shape[1] + (x2.shape[1] if x2 is not None else 0)
-        if params is not None and params[0].shape[0] == fin and K.gcn_module_fused_ok(
-                sc, fin, self.out_embedding.out_features):
+        if self.fused_ok(sc, fin):
             # one launch per direction for the whole module (sgg_gcnmod_fwd / _bwd)
-            return K.gcn_module(h_states, end_group, sc, params, x2=x2, link=link)
+            return K.gcn_module(h_states, end_group, sc, params, x2=x2, link=link, companion=companion)
+        if companion is not None:
+            raise ValueError("GCNModule: a companion batch needs the one-launch path (fused_ok)")
         if x2 is not None:
             h_states = torch.cat([h_states, x2], dim=1)
         g = sc.groups(end_group.reshape(-1))
@@ -698,10 +706,15 @@ class TrajectoryGenerator(nn.Module):
         return noise_input
 
     def pair_ok(self, sc_a, sc_b):
-        """context_pair runs its two batches' GATEncoder in one launch."""
-        return (self.graph == "gat" and self.pooling_type == "pool_net" and self.num_layers == 1
-                and self.mlp_decoder_needed() and self.pool_net.fused_ok()
-                and self.gatencoder.fused_ok(sc_a, False) and self.gatencoder.fused_ok(sc_b, True))
+        """context_pair runs its two batches' graph module (GATEncoder or
+        GCNModule, two-block input) in one launch."""
+        if not (self.graph in ("gat", "gcn") and self.pooling_type == "pool_net" and self.num_layers == 1
+                and self.mlp_decoder_needed() and self.pool_net.fused_ok()):
+            return False
+        if self.graph == "gat":
+            return self.gatencoder.fused_ok(sc_a, False) and self.gatencoder.fused_ok(sc_b, True)
+        fin = self.encoder_h_dim + self.pool_net.bottleneck_dim
+        return self.gcn_module.fused_ok(sc_a, fin) and self.gcn_module.fused_ok(sc_b, fin)
 
     def context_pair(self, a, b):
         """context() of two batches: a = (obs_traj, obs_traj_rel, seq_start_end,
@@ -712,8 +725,9 @@ class TrajectoryGenerator(nn.Module):
         can be formed at the discriminator step: the encoders of both batches
         run in ONE launch (sgg_lstm_fwd_seg3, with the discriminator's
         observed-steps prefix when it is armed on a's input) and so does the
-        GATEncoder (sgg_gatenc_fwd2), each result exactly as context()
-        computes it.  -> (context of a, context of b)."""
+        graph module (GATEncoder: sgg_gatenc_fwd2; GCNModule: sgg_gcnmod_fwd2),
+        each result exactly as context() computes it.
+        -> (context of a, context of b)."""
         obs_a, rel_a, sse_a, g_a, sc_a = a
         obs_b, rel_b, sse_b, g_b, sc_b = b
         if not self.pair_ok(sc_a, sc_b):
@@ -733,9 +747,13 @@ class TrajectoryGenerator(nn.Module):
             pool_a = self.pool_net(h_a, sse_a, obs_a[-1], scenes=sc_a, U=U_a)
         link = K.GradLink() if torch.is_grad_enabled() else None
         pool_b = self.pool_net(h_b, sse_b, obs_b[-1], scenes=sc_b, link=link, U=U_b)
-        comp = K.GatEncCompanion(h_a.view(-1, H), g_a[-1], sc_a, x2=pool_a)
-        y_b = self.gatencoder((h_b.view(-1, H), pool_b), sse_b, obs_b[-1], g_b[-1], scenes=sc_b, link=link,
-                              companion=comp)
+        if self.graph == "gat":
+            comp = K.GatEncCompanion(h_a.view(-1, H), g_a[-1], sc_a, x2=pool_a)
+            module = self.gatencoder
+        else:
+            comp = K.GcnModCompanion(h_a.view(-1, H), g_a[-1], sc_a, x2=pool_a)
+            module = self.gcn_module
+        y_b = module((h_b.view(-1, H), pool_b), sse_b, obs_b[-1], g_b[-1], scenes=sc_b, link=link, companion=comp)
         return comp.y, y_b
 
     def decode(self, noise_input, obs_traj, obs_traj_rel, seq_start_end, user_noise=None, *, scenes=None,

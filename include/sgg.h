@@ -809,6 +809,12 @@ int sgg_gcnmod_param_size(int fin, int fe);
 int sgg_gcnmod_slab_rows(int S);
 long long sgg_gcnmod_lds_bytes(int max_n, int fin, int fe, int bwd);
 int sgg_gcnmod_fwd(const SggGcnModArgs* args, void* stream);
+/* Two independent batches through the same GCNModule in ONE launch (a's
+ * scenes first): the discriminator step's generator forward beside the
+ * generator step's context (G's weights do not change in between).  Same
+ * weights, np, fin, fe and precision; each batch's own X / X2 / labels /
+ * scene_off / S / y, exactly as two sgg_gcnmod_fwd calls would write them. */
+int sgg_gcnmod_fwd2(const SggGcnModArgs* a, const SggGcnModArgs* b, void* stream);
 int sgg_gcnmod_bwd(const SggGcnModArgs* args, void* stream);
 
 /* out[c] = sum_r slab[r][c] (rows x cols, row-major), rows summed in order. */

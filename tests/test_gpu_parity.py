@@ -879,8 +879,8 @@ def test_graphed_trainer_overlap_equals_eager(iters):
             assert err <= tol * max(1.0, wa[k].abs().max().item()), (k, err)
 
 
-@pytest.mark.parametrize("graphed", [False, True])
-def test_paired_context_step_is_bit_identical(graphed, monkeypatch):
+@pytest.mark.parametrize("graphed,family", [(False, "gat"), (True, "gat"), (False, "gcn"), (True, "gcn")])
+def test_paired_context_step_is_bit_identical(graphed, family, monkeypatch):
     """step() with the G-step's context formed at the D-step beside the
     D-step's own (G.context_pair: one GATEncoder launch for both batches; the
     G-step's D forward then runs its whole encoder) == the sequential steps
@@ -896,7 +896,8 @@ def test_paired_context_step_is_bit_identical(graphed, monkeypatch):
     res = []
     for pair in (False, True):
         monkeypatch.setattr(TS, "PAIR", pair)
-        g, d = build_models()
+        torch.manual_seed(0)   # (the family's modules the fixture does not cover init alike)
+        g, d = build_models(family)
         tr = TS.GanTrainer(g, d, capturable=True)
         sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
         scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
@@ -1161,6 +1162,50 @@ def test_gat_encoder_pair_equals_two_launches(nh, sizes_a, sizes_b):
     (a0, b0, dx0, dp0, g0), (a1, b1, dx1, dp1, g1) = res
     assert torch.equal(a0, a1), "companion output"
     assert torch.equal(b0, b1), "carrying batch output"
+    assert torch.equal(dx0, dx1) and torch.equal(dp0, dp1), "dx"
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), "d" + k
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_gcn_module_pair_equals_two_launches(bf16):
+    """sgg_gcnmod_fwd2 (a no-grad batch beside one with autograd) == two
+    sgg_gcnmod_fwd launches, bitwise: both outputs and batch b's gradients."""
+    from sgan import kernels as K
+    from sgan.models import GCNModule
+    from sgan.scene import SceneIndex
+    torch.manual_seed(3)
+    mod = GCNModule(input_dim=40, hidden_dim=72, out_dim=16, gcn_layers=2, final_dim=24).to(DEV)
+    sizes_a, sizes_b = [20, 7, 13, 20, 2], [20, 1, 20, 9, 33]
+    sca, scb = (SceneIndex(np.concatenate([[0], np.cumsum(sz)]), DEV) for sz in (sizes_a, sizes_b))
+    sca.max_n = scb.max_n = max(sca.max_n, scb.max_n)
+    Ba, Bb = sum(sizes_a), sum(sizes_b)
+    lab_a = torch.randint(0, 4, (Ba,), device=DEV).float()
+    lab_b = torch.randint(0, 4, (Bb,), device=DEV).float()
+    xa, pa = torch.randn(Ba, 32, device=DEV), torch.randn(Ba, 8, device=DEV)
+    xb, pb = torch.randn(Bb, 32, device=DEV), torch.randn(Bb, 8, device=DEV)
+    dy = torch.randn(Bb, 24, device=DEV)
+    prev = K.precision()
+    K.set_precision("bf16" if bf16 else "fp32")
+    try:
+        res = []
+        for paired in (False, True):
+            mod.zero_grad(set_to_none=True)
+            xbi, pbi = xb.clone().requires_grad_(True), pb.clone().requires_grad_(True)
+            if paired:
+                comp = K.GcnModCompanion(xa, lab_a, sca, x2=pa)
+                yb = mod((xbi, pbi), None, None, lab_b, scenes=scb, companion=comp)
+                ya = comp.y
+            else:
+                with torch.no_grad():
+                    ya = mod((xa, pa), None, None, lab_a, scenes=sca)
+                yb = mod((xbi, pbi), None, None, lab_b, scenes=scb)
+            (yb * dy).sum().backward()
+            res.append((ya, yb.detach(), xbi.grad, pbi.grad, {k: q.grad.clone() for k, q in mod.named_parameters()}))
+    finally:
+        K.set_precision(prev)
+    (a0, b0, dx0, dp0, g0), (a1, b1, dx1, dp1, g1) = res
+    assert torch.equal(a0, a1) and torch.equal(b0, b1), "outputs"
     assert torch.equal(dx0, dx1) and torch.equal(dp0, dp1), "dx"
     for k in g0:
         assert torch.equal(g0[k], g1[k]), "d" + k
