@@ -444,6 +444,9 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
 // takes several); the chunk order, epilogue and argmax contract (max over j,
 // smallest j on ties) are the fp32 kernels'.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef short short2v __attribute__((ext_vector_type(2)));
 constexpr int kBfWaves = 8;
 constexpr int kBfThreads = 64 * kBfWaves;
 constexpr int kBfUP = kKT + 4;         // U tile row pitch (floats; 16-B rows)
@@ -487,8 +490,13 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
     d[2] = (__bf16)w.z;
     d[3] = (__bf16)w.w;
   }
-  for (int q = tid; q < 2 * kHidden / 4; q += kBfThreads)
-    reinterpret_cast<float4*>(As)[q] = reinterpret_cast<const float4*>(A)[q];
+  // A planar (A_x of the 512 units, then A_y): a lane's consecutive units are
+  // adjacent registers, the operand pairs of v_pk_fma_f32
+  for (int q = tid; q < kHidden; q += kBfThreads) {
+    const float2 a = reinterpret_cast<const float2*>(A)[q];
+    As[q] = a.x;
+    As[kHidden + q] = a.y;
+  }
 
   const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);   // XCD-aware (pool_fwd_kernel)
   const int nch = nchunks_dev ? *nchunks_dev : nchunks;
@@ -534,7 +542,7 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
 
       // the lane's pair of each group (padding pairs: j = 0, r = 0)
       int uoff[GPW];
-      float rx[GPW], ry[GPW];
+      float2v rxy[GPW];
       floatx4 acc[GPW][NT];
 #pragma unroll
       for (int g = 0; g < GPW; ++g) {
@@ -543,8 +551,7 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
         if (p < npairs) { il = p / n; j = p - il * n; }
         uoff[g] = j * kBfUP + 8 * kq;
         const float2 pj = ps[j], pi = ps[i0 + il];
-        rx[g] = p < npairs ? pj.x - pi.x : 0.f;
-        ry[g] = p < npairs ? pj.y - pi.y : 0.f;
+        rxy[g] = p < npairs ? float2v{pj.x - pi.x, pj.y - pi.y} : float2v{0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
       }
@@ -560,10 +567,16 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
 #pragma unroll 1
         for (int s2 = 0; s2 < kKT / 32; ++s2) {
           const int ku = kt * kKT + 32 * s2 + 8 * kq;   // the lane's 8 units of this k-step
-          float av[16];
+          float2v ax[4], ay[4];
 #pragma unroll
-          for (int v = 0; v < 4; ++v)
-            *reinterpret_cast<float4*>(&av[4 * v]) = *reinterpret_cast<const float4*>(As + 2 * ku + 4 * v);
+          for (int v = 0; v < 2; ++v) {
+            const float4 x = *reinterpret_cast<const float4*>(As + ku + 4 * v);
+            const float4 y = *reinterpret_cast<const float4*>(As + kHidden + ku + 4 * v);
+            ax[2 * v] = float2v{x.x, x.y};
+            ax[2 * v + 1] = float2v{x.z, x.w};
+            ay[2 * v] = float2v{y.x, y.y};
+            ay[2 * v + 1] = float2v{y.z, y.w};
+          }
           bf16x8_t bfr[NT];
 #pragma unroll
           for (int t = 0; t < NT; ++t)
@@ -571,16 +584,30 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
 #pragma unroll
           for (int g = 0; g < GPW; ++g) {
             if (wave * GPW + g < ngr) {   // (wave-uniform)
-              float uv[8];
-              *reinterpret_cast<float4*>(&uv[0]) = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2);
-              *reinterpret_cast<float4*>(&uv[4]) = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2 + 4);
-              bf16x8_t h;
+              const float4 u0 = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2);
+              const float4 u1 = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2 + 4);
+              const float2v uv[4] = {{u0.x, u0.y}, {u0.z, u0.w}, {u1.x, u1.y}, {u1.z, u1.w}};
+              const float2v rx2 = rxy[g].xx, ry2 = rxy[g].yy;   // (op_sel broadcasts of one register pair)
+              // two units per instruction: fma(A_y, r_y, fma(A_x, r_x, U)) in fp32
+              // (v_pk_fma_f32), rounded to bf16 (v_cvt_pk_bf16_f32), then the
+              // ReLU on the bf16 bits as signed 16-bit max with 0
+              // (v_pk_max_i16: a negative value's sign bit makes it < 0) --
+              // the same bits as rounding max(x, 0), in 16 instead of 28
+              // vector instructions per 8 units
+              union {
+                bf16x8_t v;
+                bf16x2v b[4];
+                short2v i[4];
+              } h;
 #pragma unroll
-              for (int e = 0; e < 8; ++e)
-                h[e] = (__bf16)fmaxf(fmaf(av[2 * e + 1], ry[g], fmaf(av[2 * e], rx[g], uv[e])), 0.f);
+              for (int m = 0; m < 4; ++m) {
+                const float2v pre = __builtin_elementwise_fma(ay[m], ry2, __builtin_elementwise_fma(ax[m], rx2, uv[m]));
+                h.b[m] = __builtin_convertvector(pre, bf16x2v);
+                h.i[m] = __builtin_elementwise_max(h.i[m], short2v{0, 0});
+              }
 #pragma unroll
               for (int t = 0; t < NT; ++t)
-                acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bfr[t], acc[g][t], 0, 0, 0);
+                acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h.v, bfr[t], acc[g][t], 0, 0, 0);
             }
           }
         }
