@@ -43,6 +43,36 @@ constexpr int kKT = 64;          // hidden units per LDS k-tile
 constexpr int kKTP = kKT + 2;    // U tile row stride: (2j + k) mod 32 -> conflict-free b32 reads
 constexpr int kPoolWaves = 4;
 
+// One batch of a forward launch.  A launch serves one batch, or two of the
+// same pooling net (sgg_pool_fwd2, weights shared): workgroups [0, g1) walk
+// s1's chunks and [g1, grid) s2's (g1 a multiple of 8, so each range keeps
+// the XCD-aware chunk order); the set is picked once per workgroup.
+struct PoolSet {
+  const float* U;
+  const float* pos;
+  const int32_t* scene_off;
+  const int4* chunks;
+  int nchunks;
+  const int32_t* nchunks_dev;   // a fixed-capacity plan: the count is device data
+  float* out;
+  int32_t* argmax;
+};
+
+// this workgroup's batch: its pointers, chunk count, first chunk and stride
+#define SGG_POOL_PICK(s1, s2, g1)                                                       \
+  const bool two_ = (int)blockIdx.x >= (g1);                                            \
+  const float* __restrict__ U = two_ ? s2.U : s1.U;                                     \
+  const float* __restrict__ pos = two_ ? s2.pos : s1.pos;                               \
+  const int32_t* __restrict__ scene_off = two_ ? s2.scene_off : s1.scene_off;           \
+  const int4* __restrict__ chunks = two_ ? s2.chunks : s1.chunks;                       \
+  float* __restrict__ out = two_ ? s2.out : s1.out;                                     \
+  int32_t* __restrict__ argmax = two_ ? s2.argmax : s1.argmax;                          \
+  const int32_t* ncd_ = two_ ? s2.nchunks_dev : s1.nchunks_dev;                         \
+  const int nch = ncd_ ? *ncd_ : (two_ ? s2.nchunks : s1.nchunks);                      \
+  const int gb_ = (int)blockIdx.x - (two_ ? (g1) : 0);                                  \
+  const int gstride = two_ ? (int)gridDim.x - (g1) : (g1);                              \
+  const int xb = (gb_ & 7) * (gstride >> 3) + (gb_ >> 3)   /* XCD-aware (pool_fwd_kernel) */
+
 template <int BN>
 struct PoolCfg {
   static constexpr int NT = (BN + 15) / 16;                      // 16-wide column tiles
@@ -54,12 +84,12 @@ struct PoolCfg {
 // but the wave holds ~40 % more VGPRs; that pays only while the grid is at
 // most a couple of workgroups per CU (occupancy does not matter then): the
 // host picks it for small grids (launch_fwd).
+// (occupancy hint: <8, 1> keeps 5 waves per SIMD without spilling)
 template <int BN, int GPW, int UNR>
-__global__ void __launch_bounds__(256) pool_fwd_kernel(
-    const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
-    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
-    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks, const int32_t* __restrict__ nchunks_dev,
-    float* __restrict__ out, int32_t* __restrict__ argmax) {
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(BN == 8 && GPW == 1 ? 5 : 1))) pool_fwd_kernel(
+    const PoolSet s1, const PoolSet s2, int g1, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2) {
   using C = PoolCfg<BN>;
   constexpr int NT = C::NT, BNP = C::BNP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -77,9 +107,8 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(
   // correctness), so they take CONSECUTIVE chunks -- the chunks of one scene,
   // which all stage the same U rows, then hit one XCD's L2 instead of
   // fetching those rows once per XCD.
-  const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  const int nch = nchunks_dev ? *nchunks_dev : nchunks;   // a fixed-capacity plan: the count is device data
-  for (int ch = xb; ch < nch; ch += gridDim.x) {
+  SGG_POOL_PICK(s1, s2, g1);
+  for (int ch = xb; ch < nch; ch += gstride) {
     const int4 cd = chunks[ch];
     const int s = cd.x, i0 = cd.y, i1 = cd.z;
     if (i1 <= i0) continue;   // an empty padding chunk (fixed-capacity plan), uniform over the workgroup
@@ -235,10 +264,8 @@ __device__ __forceinline__ int perm16(int k) { return (k & 3) * 16 + (k >> 2); }
 
 template <int BN, int GPW>
 __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
-    const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
-    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
-    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks, const int32_t* __restrict__ nchunks_dev,
-    float* __restrict__ out, int32_t* __restrict__ argmax) {
+    const PoolSet s1, const PoolSet s2, int g1, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2) {
   constexpr int NT = PoolCfg<BN>::NT;
   constexpr int TB = (SGG_POOL_MAX_PEDS + 16 * NT) * kVP + 2 * kKT;   // one tile buffer: U | W2 | A
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -250,9 +277,8 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
 
-  const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);   // XCD-aware (pool_fwd_kernel)
-  const int nch = nchunks_dev ? *nchunks_dev : nchunks;   // a fixed-capacity plan: the count is device data
-  for (int ch = xb; ch < nch; ch += gridDim.x) {
+  SGG_POOL_PICK(s1, s2, g1);
+  for (int ch = xb; ch < nch; ch += gstride) {
     const int4 cd = chunks[ch];
     const int s = cd.x, i0 = cd.y, i1 = cd.z;
     if (i1 <= i0) continue;   // an empty padding chunk (fixed-capacity plan), uniform over the workgroup
@@ -462,10 +488,8 @@ __host__ __device__ constexpr size_t pool_bf16_lds_bytes() {
 
 template <int BN, int GPW>
 __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
-    const float* __restrict__ U, const float* __restrict__ pos, const float* __restrict__ A,
-    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2,
-    const int32_t* __restrict__ scene_off, const int4* __restrict__ chunks, int nchunks,
-    const int32_t* __restrict__ nchunks_dev, float* __restrict__ out, int32_t* __restrict__ argmax) {
+    const PoolSet s1, const PoolSet s2, int g1, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2) {
   constexpr int NT = PoolCfg<BN>::NT;
   constexpr int CAP = kBfWaves * GPW * 16;   // pairs per pass
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -498,9 +522,8 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
     As[kHidden + q] = a.y;
   }
 
-  const int xb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);   // XCD-aware (pool_fwd_kernel)
-  const int nch = nchunks_dev ? *nchunks_dev : nchunks;
-  for (int ch = xb; ch < nch; ch += gridDim.x) {
+  SGG_POOL_PICK(s1, s2, g1);
+  for (int ch = xb; ch < nch; ch += gstride) {
     const int4 cd = chunks[ch];
     const int s = cd.x;
     if (cd.z <= cd.y) continue;   // an empty padding chunk (fixed-capacity plan), uniform
@@ -565,8 +588,8 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
         if (kt + 2 < NKT) load_tile(ra, (kt + 2) * kKT);
         const float* ut = Ut + (kt & 1) * SGG_POOL_MAX_PEDS * kBfUP;
 #pragma unroll 1
-        for (int s2 = 0; s2 < kKT / 32; ++s2) {
-          const int ku = kt * kKT + 32 * s2 + 8 * kq;   // the lane's 8 units of this k-step
+        for (int sk = 0; sk < kKT / 32; ++sk) {
+          const int ku = kt * kKT + 32 * sk + 8 * kq;   // the lane's 8 units of this k-step
           float2v ax[4], ay[4];
 #pragma unroll
           for (int v = 0; v < 2; ++v) {
@@ -584,8 +607,8 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
 #pragma unroll
           for (int g = 0; g < GPW; ++g) {
             if (wave * GPW + g < ngr) {   // (wave-uniform)
-              const float4 u0 = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2);
-              const float4 u1 = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * s2 + 4);
+              const float4 u0 = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * sk);
+              const float4 u1 = *reinterpret_cast<const float4*>(ut + uoff[g] + 32 * sk + 4);
               const float2v uv[4] = {{u0.x, u0.y}, {u0.z, u0.w}, {u1.x, u1.y}, {u1.z, u1.w}};
               const float2v rx2 = rxy[g].xx, ry2 = rxy[g].yy;   // (op_sel broadcasts of one register pair)
               // two units per instruction: fma(A_y, r_y, fma(A_x, r_x, U)) in fp32
@@ -650,10 +673,6 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
   }
 }
 
-template <int BN>
-static int launch_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                           const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int gpw,
-                           float* out, int32_t* am, hipStream_t st);
 
 // ---- forward, resident form -------------------------------------------------// ---- forward, resident form -------------------------------------------------
 // When the whole W2^T (bn rows x 512, rows padded to 16 NT with zeros) and a
@@ -953,14 +972,16 @@ static size_t pool_fwd_lds(int max_rows) {
 
 static int device_cus();
 
+// workgroups of one batch's range: a multiple of 8 (XCD-aware order), <= 32768
+static int pool_range(int nchunks) { return nchunks < 32768 ? (nchunks + 7) & ~7 : 32768; }
+
 template <int BN, int GPW>
-static void launch_fwd_g(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                         const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int max_rows,
-                         float* out,
-                         int32_t* am, hipStream_t st) {
-  const int grid = nchunks < 65536 ? (nchunks + 7) & ~7 : 65536;   // multiple of 8 (XCD-aware order)
+static void launch_fwd_g(const PoolSet& s1, const PoolSet& s2, const float* A, const float* W2, const float* b2,
+                         int max_rows, hipStream_t st) {
+  // one workgroup per chunk (host counts) in each batch's range
+  const int g1 = pool_range(s1.nchunks), grid = g1 + (s2.chunks ? pool_range(s2.nchunks) : 0);
+  const int nchunks = s1.nchunks + (s2.chunks ? s2.nchunks : 0);
   const size_t lds = pool_fwd_lds<BN>(max_rows);
-  const int4* ck = reinterpret_cast<const int4*>(chunks);
   // small grids (<= 4 chunks per CU, <= 2 pair groups per wave): the
   // fragment-native tiles (measured 1.25-1.45x faster at 64-128 scenes;
   // slower at gpw 4 / >= 1024 scenes, where occupancy hides the LDS latency)
@@ -969,13 +990,11 @@ static void launch_fwd_g(const float* U, const float* pos, const float* A, const
     if (nchunks <= 4 * device_cus() && !(vv && vv[0] == '0')) {
       const size_t lv = sizeof(float) * 2 * ((size_t)(SGG_POOL_MAX_PEDS + 16 * PoolCfg<BN>::NT) * kVP + 2 * kKT) +
                         sizeof(float2) * SGG_POOL_MAX_PEDS + sizeof(unsigned long long) * (size_t)max_rows * BN;
-      hipLaunchKernelGGL((pool_fwd_v_kernel<BN, GPW>), dim3(grid), dim3(256), lv, st, U, pos, A, W2, b2, off, ck,
-                         nchunks, ncd, out, am);
+      hipLaunchKernelGGL((pool_fwd_v_kernel<BN, GPW>), dim3(grid), dim3(256), lv, st, s1, s2, g1, A, W2, b2);
       return;
     }
   }
-  hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW, 2>), dim3(grid), dim3(256), lds, st, U, pos, A, W2, b2, off, ck,
-                     nchunks, ncd, out, am);
+  hipLaunchKernelGGL((pool_fwd_kernel<BN, GPW, 2>), dim3(grid), dim3(256), lds, st, s1, s2, g1, A, W2, b2);
 }
 // j ranges per scene of the backward: S x jq units ~ one round of the chip
 static int pool_bwd_jq(int S) {
@@ -1015,45 +1034,58 @@ static void launch_fwd_res(const float* U, const float* pos, const float* A, con
 }
 
 template <int BN>
-static int launch_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                      const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int max_rows,
-                      int max_n, int gpw,
-                      float* out, int32_t* am, hipStream_t st) {
+static int launch_fwd(const PoolSet& s1, const PoolSet& s2, const float* A, const float* W2, const float* b2,
+                      int max_rows, int max_n, int gpw, hipStream_t st) {
   const size_t res = pool_res_lds<BN>(max_n, max_rows);
   // measured (tools/bench_kernels.py, round 1): the resident form is slower
   // than the tiled one at the training shapes (one workgroup of four waves
   // per CU cannot hide its LDS latency; the tiled form runs two per CU), so
-  // it is opt-in (SGG_POOL_RESIDENT=1)
+  // it is opt-in (SGG_POOL_RESIDENT=1; single-batch launches)
   const char* rs = getenv("SGG_POOL_RESIDENT");
-  if (res <= 160u * 1024u && rs && rs[0] == '1') {
+  if (res <= 160u * 1024u && rs && rs[0] == '1' && !s2.chunks) {
+    const int32_t* ck = reinterpret_cast<const int32_t*>(s1.chunks);
+#define SGG_POOL_RES(G) launch_fwd_res<BN, G>(s1.U, s1.pos, A, W2, b2, s1.scene_off, ck, s1.nchunks, s1.nchunks_dev, \
+                                              max_n, res, s1.out, s1.argmax, st)
     switch (gpw) {
-      case 1: launch_fwd_res<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
-      case 2: launch_fwd_res<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
-      case 4: launch_fwd_res<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
-      default: launch_fwd_res<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_n, res, out, am, st); break;
+      case 1: SGG_POOL_RES(1); break;
+      case 2: SGG_POOL_RES(2); break;
+      case 4: SGG_POOL_RES(4); break;
+      default: SGG_POOL_RES(8); break;
     }
+#undef SGG_POOL_RES
     SGG_RETURN_LAUNCH("sgg_pool_fwd");
   }
   switch (gpw) {
-    case 1: launch_fwd_g<BN, 1>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
-    case 2: launch_fwd_g<BN, 2>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
-    case 4: launch_fwd_g<BN, 4>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
-    default: launch_fwd_g<BN, 8>(U, pos, A, W2, b2, off, chunks, nchunks, ncd, max_rows, out, am, st); break;
+    case 1: launch_fwd_g<BN, 1>(s1, s2, A, W2, b2, max_rows, st); break;
+    case 2: launch_fwd_g<BN, 2>(s1, s2, A, W2, b2, max_rows, st); break;
+    case 4: launch_fwd_g<BN, 4>(s1, s2, A, W2, b2, max_rows, st); break;
+    default: launch_fwd_g<BN, 8>(s1, s2, A, W2, b2, max_rows, st); break;
   }
   SGG_RETURN_LAUNCH("sgg_pool_fwd");
 }
 
 template <int BN>
-static int launch_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                           const int32_t* off, const int32_t* chunks, int nchunks, const int32_t* ncd, int gpw,
-                           float* out, int32_t* am, hipStream_t st) {
-  // persistent: one 512-thread workgroup per CU (its LDS plan), a multiple of 8 (XCD-aware order)
+static int launch_fwd_bf16(const PoolSet& s1, const PoolSet& s2, const float* A, const float* W2, const float* b2,
+                           int gpw, hipStream_t st) {
+  // persistent: one 512-thread workgroup per CU (its LDS plan), each batch's
+  // range a multiple of 8 (XCD-aware order) sized by its share of the chunks
+  const int n1 = s1.nchunks, n2 = s2.chunks ? s2.nchunks : 0;
   int grid = device_cus();
-  if (grid > nchunks) grid = nchunks;
+  if (grid > n1 + n2) grid = n1 + n2;
   grid = (grid + 7) & ~7;
+  int g1 = grid;
+  if (n2 > 0) {
+    if (n1 == 0) {
+      g1 = 0;
+    } else {
+      if (grid < 16) grid = 16;
+      g1 = (int)(((long long)grid * n1 / (n1 + n2) + 4) & ~7LL);
+      g1 = g1 < 8 ? 8 : (g1 > grid - 8 ? grid - 8 : g1);
+    }
+  }
   const size_t lds = pool_bf16_lds_bytes<BN>();
-  const int4* ck = reinterpret_cast<const int4*>(chunks);
-#define SGG_POOL_BF(G)                                                                                                  hipLaunchKernelGGL((pool_fwd_bf16_kernel<BN, G>), dim3(grid), dim3(kBfThreads), lds, st, U, pos, A, W2, b2, off, ck,                      nchunks, ncd, out, am)
+#define SGG_POOL_BF(G) \
+  hipLaunchKernelGGL((pool_fwd_bf16_kernel<BN, G>), dim3(grid), dim3(kBfThreads), lds, st, s1, s2, g1, A, W2, b2)
   if (gpw >= 4 && BN <= 48)
     SGG_POOL_BF(4);
   else if (gpw >= 2)
@@ -1142,28 +1174,6 @@ extern "C" int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int t
   return nc;
 }
 
-extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
-                            const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
-                            int B, int bn, int max_n, float* out, int32_t* argmax, const int32_t* nchunks_dev,
-                            void* stream) {
-  SGG_CHECK_ARG(U && pos && A && W2 && b2 && scene_off && chunks && out && argmax, "sgg_pool_fwd: null pointer");
-  SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_fwd: bottleneck %d not built (8/16/32/48/64)", bn);
-  SGG_CHECK_ARG(nchunks >= 0 && B >= 0, "sgg_pool_fwd: bad sizes");
-  SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "sgg_pool_fwd: max scene size %d outside [1, %d]",
-                max_n, SGG_POOL_MAX_PEDS);
-  SGG_CHECK_ARG(max_rows >= 1 && max_rows <= 64, "sgg_pool_fwd: chunk rows %d outside [1, 64]", max_rows);
-  SGG_CHECK_ARG(gpw == 1 || gpw == 2 || gpw == 4 || gpw == 8, "sgg_pool_fwd: gpw %d not in {1,2,4,8}", gpw);
-  if (nchunks == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  switch (bn) {
-    case 8: return launch_fwd<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
-    case 16: return launch_fwd<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
-    case 32: return launch_fwd<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
-    case 48: return launch_fwd<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
-    default: return launch_fwd<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, max_rows, max_n, gpw, out, argmax, st);
-  }
-}
-
 extern "C" int sgg_pool_plan_bf16(const int32_t* host_scene_off, int S, int bn, int target_chunks, int32_t* chunks,
                                   int cap, int* max_rows, int* gpw_out) {
   // host helper for pool_fwd_bf16_kernel: chunks of whole i-rows of up to a
@@ -1215,26 +1225,88 @@ extern "C" int sgg_pool_plan_bf16(const int32_t* host_scene_off, int S, int bn, 
   return nc;
 }
 
+// the checks every forward entry makes on one batch
+static int pool_batch_check(const char* fn, const float* U, const float* pos, const int32_t* scene_off,
+                            const int32_t* chunks, int nchunks, int max_rows, int gpw, int B, int max_n,
+                            const float* out, const int32_t* argmax) {
+  SGG_CHECK_ARG(U && pos && scene_off && chunks && out && argmax, "%s: null pointer", fn);
+  SGG_CHECK_ARG(nchunks >= 0 && B >= 0, "%s: bad sizes", fn);
+  SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "%s: max scene size %d outside [1, %d]", fn, max_n,
+                SGG_POOL_MAX_PEDS);
+  SGG_CHECK_ARG(max_rows >= 1 && max_rows <= 64, "%s: chunk rows %d outside [1, 64]", fn, max_rows);
+  SGG_CHECK_ARG(gpw == 1 || gpw == 2 || gpw == 4 || gpw == 8, "%s: gpw %d not in {1,2,4,8}", fn, gpw);
+  return 0;
+}
+
+// one forward launch over one or two batches (nchunks: their total)
+static int pool_fwd_sets(const PoolSet& s1, const PoolSet& s2, const float* A, const float* W2, const float* b2,
+                         int max_rows, int max_n, int gpw, int bn, bool bf16, hipStream_t st) {
+  if (s1.nchunks + (s2.chunks ? s2.nchunks : 0) == 0) return 0;
+  if (bf16) {
+    switch (bn) {
+      case 8: return launch_fwd_bf16<8>(s1, s2, A, W2, b2, gpw, st);
+      case 16: return launch_fwd_bf16<16>(s1, s2, A, W2, b2, gpw, st);
+      case 32: return launch_fwd_bf16<32>(s1, s2, A, W2, b2, gpw, st);
+      case 48: return launch_fwd_bf16<48>(s1, s2, A, W2, b2, gpw, st);
+      default: return launch_fwd_bf16<64>(s1, s2, A, W2, b2, gpw, st);
+    }
+  }
+  switch (bn) {
+    case 8: return launch_fwd<8>(s1, s2, A, W2, b2, max_rows, max_n, gpw, st);
+    case 16: return launch_fwd<16>(s1, s2, A, W2, b2, max_rows, max_n, gpw, st);
+    case 32: return launch_fwd<32>(s1, s2, A, W2, b2, max_rows, max_n, gpw, st);
+    case 48: return launch_fwd<48>(s1, s2, A, W2, b2, max_rows, max_n, gpw, st);
+    default: return launch_fwd<64>(s1, s2, A, W2, b2, max_rows, max_n, gpw, st);
+  }
+}
+
+static int pool_fwd_one(const char* fn, bool bf16, const float* U, const float* pos, const float* A, const float* W2,
+                        const float* b2, const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows,
+                        int gpw, int B, int bn, int max_n, float* out, int32_t* argmax, const int32_t* nchunks_dev,
+                        void* stream) {
+  SGG_CHECK_ARG(A && W2 && b2, "%s: null pointer", fn);
+  SGG_CHECK_ARG(pool_bn_ok(bn), "%s: bottleneck %d not built (8/16/32/48/64)", fn, bn);
+  const int rc = pool_batch_check(fn, U, pos, scene_off, chunks, nchunks, max_rows, gpw, B, max_n, out, argmax);
+  if (rc != 0) return rc;
+  const PoolSet s1 = {U, pos, scene_off, reinterpret_cast<const int4*>(chunks), nchunks, nchunks_dev, out, argmax};
+  const PoolSet none = {};
+  return pool_fwd_sets(s1, none, A, W2, b2, max_rows, max_n, gpw, bn, bf16, (hipStream_t)stream);
+}
+
+extern "C" int sgg_pool_fwd(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
+                            const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
+                            int B, int bn, int max_n, float* out, int32_t* argmax, const int32_t* nchunks_dev,
+                            void* stream) {
+  return pool_fwd_one("sgg_pool_fwd", false, U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, B, bn,
+                      max_n, out, argmax, nchunks_dev, stream);
+}
+
 extern "C" int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* A, const float* W2, const float* b2,
                                  const int32_t* scene_off, const int32_t* chunks, int nchunks, int max_rows, int gpw,
                                  int B, int bn, int max_n, float* out, int32_t* argmax, const int32_t* nchunks_dev,
                                  void* stream) {
-  SGG_CHECK_ARG(U && pos && A && W2 && b2 && scene_off && chunks && out && argmax, "sgg_pool_fwd_bf16: null pointer");
-  SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_fwd_bf16: bottleneck %d not built (8/16/32/48/64)", bn);
-  SGG_CHECK_ARG(nchunks >= 0 && B >= 0, "sgg_pool_fwd_bf16: bad sizes");
-  SGG_CHECK_ARG(max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS, "sgg_pool_fwd_bf16: max scene size %d outside [1, %d]",
-                max_n, SGG_POOL_MAX_PEDS);
-  SGG_CHECK_ARG(max_rows >= 1 && max_rows <= 64, "sgg_pool_fwd_bf16: chunk rows %d outside [1, 64]", max_rows);
-  SGG_CHECK_ARG(gpw == 1 || gpw == 2 || gpw == 4 || gpw == 8, "sgg_pool_fwd_bf16: gpw %d not in {1,2,4,8}", gpw);
-  if (nchunks == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  switch (bn) {
-    case 8: return launch_fwd_bf16<8>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
-    case 16: return launch_fwd_bf16<16>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
-    case 32: return launch_fwd_bf16<32>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
-    case 48: return launch_fwd_bf16<48>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
-    default: return launch_fwd_bf16<64>(U, pos, A, W2, b2, scene_off, chunks, nchunks, nchunks_dev, gpw, out, argmax, st);
+  return pool_fwd_one("sgg_pool_fwd_bf16", true, U, pos, A, W2, b2, scene_off, chunks, nchunks, max_rows, gpw, B,
+                      bn, max_n, out, argmax, nchunks_dev, stream);
+}
+
+extern "C" int sgg_pool_fwd2(const SggPoolBatch* a, const SggPoolBatch* b, const float* A, const float* W2,
+                             const float* b2, int bn, int bf16, void* stream) {
+  SGG_CHECK_ARG(a && b && A && W2 && b2, "sgg_pool_fwd2: null pointer");
+  SGG_CHECK_ARG(pool_bn_ok(bn), "sgg_pool_fwd2: bottleneck %d not built (8/16/32/48/64)", bn);
+  for (const SggPoolBatch* p : {a, b}) {
+    const int rc = pool_batch_check("sgg_pool_fwd2", p->U, p->pos, p->scene_off, p->chunks, p->nchunks, p->max_rows,
+                                    p->gpw, p->B, p->max_n, p->out, p->argmax);
+    if (rc != 0) return rc;
   }
+  // one kernel instance (its pair groups per wave) serves both batches
+  SGG_CHECK_ARG(a->gpw == b->gpw, "sgg_pool_fwd2: the batches' plans differ in gpw (%d, %d)", a->gpw, b->gpw);
+  const PoolSet s1 = {a->U, a->pos, a->scene_off, reinterpret_cast<const int4*>(a->chunks), a->nchunks,
+                      a->nchunks_dev, a->out, a->argmax};
+  const PoolSet s2 = {b->U, b->pos, b->scene_off, reinterpret_cast<const int4*>(b->chunks), b->nchunks,
+                      b->nchunks_dev, b->out, b->argmax};
+  const int mr = a->max_rows > b->max_rows ? a->max_rows : b->max_rows;
+  const int mn = a->max_n > b->max_n ? a->max_n : b->max_n;
+  return pool_fwd_sets(s1, s2, A, W2, b2, mr, mn, a->gpw, bn, bf16 != 0, (hipStream_t)stream);
 }
 
 extern "C" int sgg_pool_bwd_grid(int S) {

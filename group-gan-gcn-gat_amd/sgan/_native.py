@@ -101,6 +101,12 @@ class TrajOut(ctypes.Structure):
                 ("b", _p), ("ldb", _i), ("pos0", _p), ("start", _p)]
 
 
+class PoolBatch(ctypes.Structure):
+    """SggPoolBatch (include/sgg.h): one batch of sgg_pool_fwd2."""
+    _fields_ = [("U", _p), ("pos", _p), ("scene_off", _p), ("chunks", _p), ("nchunks", _i), ("max_rows", _i),
+                ("gpw", _i), ("B", _i), ("max_n", _i), ("out", _p), ("argmax", _p), ("nchunks_dev", _p)]
+
+
 class L2Job(ctypes.Structure):
     """SggL2Job (include/sgg.h): an L2 loss value of sgg_grad_finish_losses."""
     _fields_ = [("term", _p), ("S", _i), ("loss", _p)]
@@ -122,6 +128,7 @@ SIGNATURES = {
     "sgg_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
     "sgg_pool_plan_bf16": (_i, [_p, _i, _i, _i, _p, _i, _p, _p]),
     "sgg_pool_fwd_bf16": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
+    "sgg_pool_fwd2": (_i, [ctypes.POINTER(PoolBatch), ctypes.POINTER(PoolBatch), _p, _p, _p, _i, _i, _p]),
     "sgg_pool_bwd_grid": (_i, [_i]),
     "sgg_pool_dh_dw": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _i, _i, _i, _p, _sz, _p]),
     "sgg_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]),
@@ -146,6 +153,7 @@ SIGNATURES = {
     "sgg_head_slab_cols": (_i, [_i, _i]),
     "sgg_head_fwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p]),
     "sgg_head_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _p, _i, _f, _p, _p]),
+    "sgg_head_fwdbwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _i, _p, _p, _p, _p, _i, _f, _p, _p]),
     "sgg_xtw_partial": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "sgg_grad_finish": (_i, [ctypes.POINTER(Red), _i, ctypes.POINTER(FoldBwd), _i, _p, _sz, _p]),
     "sgg_lstm_fwd_dec": (_i, [ctypes.POINTER(DecInit), _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,

@@ -597,6 +597,8 @@ class BceLink:
 
     def __init__(self):
         self.pending = None
+        self.forward_held = None   # the head's forward, waiting for the BCE forward (HEAD_FUSE)
+        self.fused = None          # (seed, dx, slab) of the fused launch, when it ran
 
     def put(self, g, ya, yb, split, w, placeholder, nvalid=None):
         self.pending = (g, ya, yb, split, w, placeholder, nvalid)
@@ -605,41 +607,104 @@ class BceLink:
         p, self.pending = self.pending, None
         return p
 
+    def run_fused(self, ya, yb, split, w, nvalid):
+        """The BCE forward's call: issue the held head forward together with
+        the head + BCE backward for the trainer's backward seed (the constant
+        1.0 of const()) -- sgg_head_fwdbwd.  The BCE backward later confirms
+        it received that seed (seed_ok); otherwise the head backward runs its
+        own launches."""
+        held, self.forward_held = self.forward_held, None
+        if held is None:
+            return
+        x, W1, b1, W2, b2, act, y, wgrad = held
+        lib = _lib()
+        M, Kd = x.shape
+        N1 = W1.shape[0]
+        seed = const(1.0, x.device)
+        dx = torch.empty(M, Kd, device=x.device, dtype=torch.float32)
+        P = lib.sgg_head_slab_cols(Kd, N1)
+        slab = torch.empty(max((M + 63) // 64, 1), P, device=x.device, dtype=torch.float32) if wgrad else None
+
+        def launch():
+            N.check(lib.sgg_head_fwdbwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(b1), N.ptr(W2), N.ptr(b2),
+                                        act, N.ptr(y), N.ptr(dx), dx.stride(0), N.ptr(slab), N.ptr(seed), N.ptr(ya),
+                                        N.ptr(yb), int(split), float(w), N.ptr(nvalid), N.stream_ptr()),
+                    "sgg_head_fwdbwd")
+        launch()
+        if timer.active and M > 0:
+            timer.add("sgg::head_fwdbwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1, wgrad),
+                      2.0 * M * N1 * (Kd + 1) + 2.0 * M * N1 * Kd * (2 if wgrad else 1),
+                      4.0 * (M * Kd * (2 if wgrad else 1) + N1 * Kd + 2 * M + M * Kd
+                             + (slab.numel() if wgrad else 0)), launch)
+        self.fused = (seed, dx, slab)
+
+    def flush_forward(self):
+        """The held forward alone (no BCE forward came): sgg_head_fwd."""
+        held, self.forward_held = self.forward_held, None
+        if held is not None:
+            x, W1, b1, W2, b2, act, y, _ = held
+            _head_fwd(x, W1, b1, W2, b2, act, y, record=True)
+
+
+HEAD_FUSE = os.environ.get("SGG_HEAD_FUSE", "1") != "0"
+_HELD_HEADS = []   # links whose head forward is held (flushed when the handoff scope ends)
+
+
+def _head_fwd(x, W1, b1, W2, b2, act, y, record=False):
+    """sgg_head_fwd -> hid (Y into y)."""
+    lib = _lib()
+    M, Kd = x.shape
+    N1 = W1.shape[0]
+    hid = torch.empty(M, N1, device=x.device, dtype=torch.float32)
+
+    def launch():
+        N.check(lib.sgg_head_fwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(b1), N.ptr(W2), N.ptr(b2),
+                                 act, N.ptr(hid), N.ptr(y), N.stream_ptr()), "sgg_head_fwd")
+    launch()
+    if record and timer.active and M > 0:
+        timer.add("sgg::head_fwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1), 2.0 * M * N1 * (Kd + 1),
+                  4.0 * (M * Kd + N1 * Kd + M * N1 + M), launch)
+    return hid
+
 
 class _Head(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W1, b1, W2, b2, act, bce_link=None):
-        lib = _lib()
         x = _rows(x, "x")
         if x.data_ptr() % 16 or x.stride(0) % 4:   # the kernel reads 16-byte blocks of a row
             x = x.contiguous()
         M, Kd = x.shape
-        N1 = W1.shape[0]
         W1, W2 = W1.contiguous(), W2.contiguous()
         b1, b2 = b1.contiguous(), b2.contiguous()
-        hid = torch.empty(M, N1, device=x.device, dtype=torch.float32)
         y = torch.empty(M, 1, device=x.device, dtype=torch.float32)
-
-        def launch():
-            N.check(lib.sgg_head_fwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(b1), N.ptr(W2), N.ptr(b2),
-                                     act, N.ptr(hid), N.ptr(y), N.stream_ptr()), "sgg_head_fwd")
-        launch()
-        if timer.active and M > 0:
-            timer.add("sgg::head_fwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1), 2.0 * M * N1 * (Kd + 1),
-                      4.0 * (M * Kd + N1 * Kd + M * N1 + M), launch)
+        wgrad = any(ctx.needs_input_grad[1:5])
+        if bce_link is not None and HEAD_FUSE and M > 0:
+            # held: the BCE forward on y issues it with the backward (BceLink.run_fused)
+            bce_link.forward_held = (x, W1, b1, W2, b2, act, y, wgrad)
+            _HELD_HEADS.append(bce_link)
+            hid = None
+        else:
+            hid = _head_fwd(x, W1, b1, W2, b2, act, y, record=True)
         ctx.act = act
         ctx.bce_link = bce_link
-        ctx.save_for_backward(x, W1, W2, hid, y)
+        ctx.hid = hid
+        ctx.save_for_backward(x, W1, b1, W2, b2, y)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = _lib()
-        x, W1, W2, hid, y = ctx.saved_tensors
+        x, W1, b1, W2, b2, y = ctx.saved_tensors
         need = ctx.needs_input_grad
         M, Kd = x.shape
         N1 = W1.shape[0]
-        pend = ctx.bce_link.take() if ctx.bce_link is not None else None
+        link = ctx.bce_link
+        pend = link.take() if link is not None else None
+        if link is not None and link.forward_held is not None:
+            link.flush_forward()
+        fused, hid = None, ctx.hid
+        if link is not None and link.fused is not None:
+            fused, link.fused = link.fused, None
         bce = None
         if pend is not None:
             g, ya, yb, split, w, ph, nvalid = pend
@@ -649,24 +714,30 @@ class _Head(torch.autograd.Function):
             bce = (g.contiguous(), ya, yb, int(split), float(w), nvalid)
         else:
             dy = dy.contiguous()
-        dx = torch.empty(M, Kd, device=x.device, dtype=torch.float32)
         wgrad = any(need[1:5])
         P = lib.sgg_head_slab_cols(Kd, N1)
         rows = (M + 63) // 64
-        slab = torch.empty(max(rows, 1), P, device=x.device, dtype=torch.float32) if wgrad else None
+        if fused is not None and bce is not None and bce[0].data_ptr() == fused[0].data_ptr():
+            # the BCE backward received the seed the fused launch assumed: dx and the slab are final
+            dx, slab = fused[1], fused[2]
+        else:
+            if hid is None:   # (the fused launch kept no hidden layer: recompute it)
+                hid = _head_fwd(x, W1, b1, W2, b2, ctx.act, torch.empty_like(y))
+            dx = torch.empty(M, Kd, device=x.device, dtype=torch.float32)
+            slab = torch.empty(max(rows, 1), P, device=x.device, dtype=torch.float32) if wgrad else None
+            bg, bya, byb, bsp, bw, bnv = (N.ptr(bce[0]), N.ptr(bce[1]), N.ptr(bce[2]), bce[3], bce[4],
+                                          N.ptr(bce[5])) if bce else (None, None, None, 0, 0.0, None)
 
-        bg, bya, byb, bsp, bw, bnv = (N.ptr(bce[0]), N.ptr(bce[1]), N.ptr(bce[2]), bce[3], bce[4],
-                                      N.ptr(bce[5])) if bce else (None, None, None, 0, 0.0, None)
-
-        def launch():
-            N.check(lib.sgg_head_bwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(W2), N.ptr(hid), N.ptr(y),
-                                     None if bce else N.ptr(dy), ctx.act, N.ptr(dx), dx.stride(0), N.ptr(slab),
-                                     bg, bya, byb, bsp, bw, bnv, N.stream_ptr()), "sgg_head_bwd")
-        launch()
-        if timer.active and M > 0:
-            timer.add("sgg::head_bwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1, wgrad),
-                      2.0 * M * N1 * Kd * (2 if wgrad else 1),
-                      4.0 * (M * Kd * (3 if wgrad else 2) + 2 * M * N1 + (slab.numel() if wgrad else 0)), launch)
+            def launch():
+                N.check(lib.sgg_head_bwd(N.ptr(x), x.stride(0), M, Kd, N1, N.ptr(W1), N.ptr(W2), N.ptr(hid),
+                                         N.ptr(y), None if bce else N.ptr(dy), ctx.act, N.ptr(dx), dx.stride(0),
+                                         N.ptr(slab), bg, bya, byb, bsp, bw, bnv, N.stream_ptr()), "sgg_head_bwd")
+            launch()
+            if timer.active and M > 0:
+                timer.add("sgg::head_bwd_kernel<%d, %d>" % (N1 // 16, Kd // 16), (M, Kd, N1, wgrad),
+                          2.0 * M * N1 * Kd * (2 if wgrad else 1),
+                          4.0 * (M * Kd * (3 if wgrad else 2) + 2 * M * N1 + (slab.numel() if wgrad else 0)), launch)
+        ctx.hid = None
         if not wgrad:
             return dx, None, None, None, None, None, None
         dW1 = torch.empty(N1, Kd, device=x.device, dtype=torch.float32)
@@ -702,6 +773,9 @@ def bce_handoff():
         yield
     finally:
         _BCE_HANDOFF[0] -= 1
+        if _BCE_HANDOFF[0] == 0:   # a held head forward no BCE forward took: issue it now
+            while _HELD_HEADS:
+                _HELD_HEADS.pop().flush_forward()
 
 
 def head(x, spec):
@@ -1028,6 +1102,79 @@ def _pool_flops(scenes, bn):
     return float((sz * sz).sum()) * 512.0 * (4 + 2 * bn)
 
 
+def _pool_kname(bn, gpw, nchunks, bf16, dev):
+    """The forward kernel the library picks (pool.hip launch_fwd_g / launch_fwd_bf16)."""
+    if bf16:
+        return "sgg::pool_fwd_bf16_kernel<%d, %d>" % (bn, 4 if gpw >= 4 and bn <= 48 else (2 if gpw >= 2 else 1))
+    small = gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+    return "sgg::" + ("pool_fwd_v_kernel<%d, %d>" % (bn, gpw) if small else "pool_fwd_kernel<%d, %d, 2>" % (bn, gpw))
+
+
+def _pool_wbytes(bn):
+    return 4.0 * (1024 + bn * 512 + bn)     # A, W2, b2
+
+
+class PoolRider:
+    """pool_pair(): the block's first pooling forward (the discriminator
+    step's generator pooling, scripts/train.py:400) is held; the next one of
+    the same net and plan width (the generator step's, :443) issues both in
+    ONE launch (sgg_pool_fwd2).  Nothing may read the held forward's outputs
+    before that; a held forward nobody carried is issued on exit."""
+
+    def __init__(self):
+        self.held = None
+        self.done = False
+        self.carried = False
+
+    def hold(self, batch, keep, weights, bn, bf16, gpw, nchunks, work, launch):
+        self.held = (batch, keep, weights, bn, bf16, gpw, nchunks, work, launch)
+
+    def fits(self, weights, bn, bf16, gpw):
+        if self.held is None:
+            return False
+        _, _, wh, bnh, bfh, gph, _, _, _ = self.held
+        return bnh == bn and bfh == bf16 and gph == gpw and all(a is b for a, b in zip(wh, weights))
+
+    def carry(self, batch, keep, nchunks, work):
+        """-> (the paired launch, (kernel name, S, B, flop, bytes, chunks) of both)."""
+        a, keep_a, (A, W2, b2), bn, bf16, gpw, nch_a, work_a, _ = self.held
+        self.held = None
+        self.done = self.carried = True
+        lib = _lib()
+        b = batch
+
+        def pl(k=(keep_a, keep, A, W2, b2)):
+            N.check(lib.sgg_pool_fwd2(N.ctypes.byref(a), N.ctypes.byref(b), N.ptr(A), N.ptr(W2), N.ptr(b2), bn,
+                                      int(bf16), N.stream_ptr()), "sgg_pool_fwd2")
+        S2, B2 = work_a[0] + work[0], work_a[1] + work[1]
+        return pl, (None, S2, B2, work_a[2] + work[2], work_a[3] + work[3], nch_a + nchunks)
+
+    def flush(self):
+        if self.held is not None:
+            _, _, (A, W2, b2), bn, bf16, gpw, nch, work, launch = self.held
+            self.held = None
+            launch()
+            if timer.active:
+                timer.add(_pool_kname(bn, gpw, nch, bf16, A.device), work[:2], work[2], work[3] + _pool_wbytes(bn),
+                          launch)
+        self.done = True
+
+
+_PRIDER = [None]
+
+
+@contextlib.contextmanager
+def pool_pair():
+    """The block's first pooling forward rides with the next one (PoolRider)."""
+    prev = _PRIDER[0]
+    r = _PRIDER[0] = PoolRider()
+    try:
+        yield r
+    finally:
+        _PRIDER[0] = prev
+        r.flush()
+
+
 class _Pool(torch.autograd.Function):
     """PoolHiddenNet on raw parameters: W1 (512 x (E + Hd)) = [W1e | W1h], the
     spatial embedding (We, be), b1, W2 (bn x 512), b2.  Forward: one fold
@@ -1070,15 +1217,31 @@ class _Pool(torch.autograd.Function):
             N.check(fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(scenes.scene_off),
                         N.ptr(chunks), nchunks, max_rows, gpw, B, bn, scenes.max_n, N.ptr(out),
                         N.ptr(am), N.ptr(ncd), N.stream_ptr()), "sgg_pool_fwd")
-        launch()
-        if timer.active:
-            # the form the library picks (pool.hip launch_fwd_g)
-            small = gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(h.device).multi_processor_count
-            name = "pool_fwd_v_kernel<%d, %d>" % (bn, gpw) if small else "pool_fwd_kernel<%d, %d, 2>" % (bn, gpw)
-            if bf16:
-                name = "pool_fwd_bf16_kernel<%d, %d>" % (bn, gpw)
-            nb = 4.0 * (B * 512 + 2 * B + 1024 + bn * 512 + bn) + 8.0 * B * bn
-            timer.add("sgg::" + name, (scenes.S, B), _pool_flops(scenes, bn), nb, launch)
+        nb = 4.0 * (B * 512 + 2 * B) + 8.0 * B * bn     # + the weights, once per launch (_pool_timing)
+        work = (scenes.S, B, _pool_flops(scenes, bn), nb)
+        rider = _PRIDER[0]
+        if rider is not None and not rider.done and rider.held is None:
+            # the block's first pooling forward: held until the next one carries it
+            batch = N.PoolBatch(N.ptr(U), N.ptr(pos), N.ptr(scenes.scene_off), N.ptr(chunks), nchunks, max_rows,
+                                gpw, B, scenes.max_n, N.ptr(out), N.ptr(am), N.ptr(ncd))
+            rider.hold(batch, (U, pos, scenes.scene_off, chunks, out, am, ncd), (A, W2, b2), bn, bf16, gpw,
+                       nchunks, work, launch)
+        elif rider is not None and rider.fits((A, W2, b2), bn, bf16, gpw):
+            batch = N.PoolBatch(N.ptr(U), N.ptr(pos), N.ptr(scenes.scene_off), N.ptr(chunks), nchunks, max_rows,
+                                gpw, B, scenes.max_n, N.ptr(out), N.ptr(am), N.ptr(ncd))
+            pl, (name, S2, B2, fl2, nb2, nch2) = rider.carry(batch, (U, pos, scenes.scene_off, chunks, out, am, ncd),
+                                                             nchunks, work)
+            pl()
+            if timer.active:
+                timer.add(_pool_kname(bn, gpw, nch2, bf16, h.device), (S2, B2, "pair"), fl2, nb2 + _pool_wbytes(bn),
+                          pl)
+        else:
+            if rider is not None:
+                rider.flush()
+            launch()
+            if timer.active:
+                timer.add(_pool_kname(bn, gpw, nchunks, bf16, h.device), (scenes.S, B), work[2],
+                          nb + _pool_wbytes(bn), launch)
         ctx.scenes = scenes
         ctx.E = E
         ctx.save_for_backward(h, pos, W1, We, be, A, W2, U, out, am)
@@ -2403,6 +2566,8 @@ class _Bce(torch.autograd.Function):
     def forward(ctx, x, ya, yb, split, w, nvalid):
         ctx.shape = x.shape
         ctx.bce_link = getattr(x, "_sgg_bce_link", None)
+        if ctx.bce_link is not None:   # the held head forward + its backward, one launch
+            ctx.bce_link.run_fused(ya, yb, split, w, nvalid)
         x = _req(x, "scores").contiguous().view(-1)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         if _loss_deferrable("bce"):   # formed with the weight gradients
@@ -2463,6 +2628,8 @@ class _BceTotal(torch.autograd.Function):
     def forward(ctx, x, ya, yb, split, w, addend, nvalid):
         ctx.shape = x.shape
         ctx.bce_link = getattr(x, "_sgg_bce_link", None)
+        if ctx.bce_link is not None:   # the held head forward + its backward, one launch
+            ctx.bce_link.run_fused(ya, yb, split, w, nvalid)
         x = _req(x, "scores").contiguous().view(-1)
         addend = _req(addend, "addend").reshape(())
         loss = torch.empty((), device=x.device, dtype=torch.float32)

@@ -724,9 +724,9 @@ class TrajectoryGenerator(nn.Module):
         two steps (the discriminator step updates D only), so both contexts
         can be formed at the discriminator step: the encoders of both batches
         run in ONE launch (sgg_lstm_fwd_seg3, with the discriminator's
-        observed-steps prefix when it is armed on a's input) and so does the
-        graph module (GATEncoder: sgg_gatenc_fwd2; GCNModule: sgg_gcnmod_fwd2),
-        each result exactly as context() computes it.
+        observed-steps prefix when it is armed on a's input), so do the
+        poolings (sgg_pool_fwd2) and the graph module (GATEncoder:
+        sgg_gatenc_fwd2; GCNModule: sgg_gcnmod_fwd2), each result exactly as context() computes it.
         -> (context of a, context of b)."""
         obs_a, rel_a, sse_a, g_a, sc_a = a
         obs_b, rel_b, sse_b, g_b, sc_b = b
@@ -743,10 +743,12 @@ class TrajectoryGenerator(nn.Module):
             with torch.no_grad():
                 h_a, U_a = self.encoder(rel_a, proj_u=u)
             h_b, U_b = self.encoder(rel_b, proj_u=u)
-        with torch.no_grad():
-            pool_a = self.pool_net(h_a, sse_a, obs_a[-1], scenes=sc_a, U=U_a)
         link = K.GradLink() if torch.is_grad_enabled() else None
-        pool_b = self.pool_net(h_b, sse_b, obs_b[-1], scenes=sc_b, link=link, U=U_b)
+        # both poolings in one launch (sgg_pool_fwd2): a's is held until b's carries it
+        with K.pool_pair():
+            with torch.no_grad():
+                pool_a = self.pool_net(h_a, sse_a, obs_a[-1], scenes=sc_a, U=U_a)
+            pool_b = self.pool_net(h_b, sse_b, obs_b[-1], scenes=sc_b, link=link, U=U_b)
         if self.graph == "gat":
             comp = K.GatEncCompanion(h_a.view(-1, H), g_a[-1], sc_a, x2=pool_a)
             module = self.gatencoder

@@ -113,6 +113,31 @@ int sgg_pool_fwd_bf16(const float* U, const float* pos, const float* A, const fl
                       int max_rows, int gpw, int B, int bn, int max_n, float* out, int32_t* argmax,
                       const int32_t* nchunks_dev, void* stream);
 
+/* Two batches through ONE pooling net in one launch: sgg_pool_fwd (bf16 = 0)
+ * or sgg_pool_fwd_bf16 (bf16 != 0) of batch a and of batch b, the same
+ * weights (A, W2, b2, bn) -- the discriminator step's generator pooling
+ * (scripts/train.py:400, no autograd) and the generator step's (:443) run
+ * together (sgan.models.TrajectoryGenerator.context_pair).  Each batch's
+ * fields are sgg_pool_fwd's arguments of the same name; both plans must have
+ * the same gpw.  The workgroups walk a's chunks, then b's: each output is
+ * bitwise what the single-batch call writes. */
+typedef struct SggPoolBatch {
+  const float* U;
+  const float* pos;
+  const int32_t* scene_off;
+  const int32_t* chunks;
+  int nchunks;
+  int max_rows;
+  int gpw;
+  int B;
+  int max_n;
+  float* out;
+  int32_t* argmax;
+  const int32_t* nchunks_dev;
+} SggPoolBatch;
+int sgg_pool_fwd2(const SggPoolBatch* a, const SggPoolBatch* b, const float* A, const float* W2, const float* b2,
+                  int bn, int bf16, void* stream);
+
 /* The pooling backward's two products of dU (B x 512, row stride ldu) in ONE
  * launch (models.py:538's Linear: the h half of the first layer): dh = dU W
  * (W = W1[:, E:], 512 x H at row stride ldw; accumulate != 0 adds to dh) and
@@ -370,6 +395,17 @@ int sgg_head_bwd(const float* X, int ldx, int M, int K, int N1, const float* W1,
                  const float* Y, const float* dY, int act, float* dX, int lddx, float* wslab, const float* bce_g,
                  const float* bce_ya, const float* bce_yb, int bce_split, float bce_w, const int32_t* bce_nvalid,
                  void* stream);
+/* sgg_head_fwd and sgg_head_bwd with the BCE loss's gradient (bce_g != NULL
+ * required) in ONE launch: Y is written (the loss value's input), hid is not
+ * (the backward's ReLU masks come from the forward's own registers), dX and
+ * the slab row are what the two calls write, bitwise, when *bce_g holds the
+ * same value.  The trainer issues it at the BCE forward with bce_g = its
+ * backward seed (1.0), which the loss's backward then confirms it received
+ * (sgan.kernels.BceLink). */
+int sgg_head_fwdbwd(const float* X, int ldx, int M, int K, int N1, const float* W1, const float* b1, const float* w2,
+                    const float* b2, int act, float* Y, float* dX, int lddx, float* wslab, const float* bce_g,
+                    const float* bce_ya, const float* bce_yb, int bce_split, float bce_w, const int32_t* bce_nvalid,
+                    void* stream);
 
 /* ------------------------------------------------------------------------
  * Input-embedding fold (a Linear(2, E) displacement embedding feeding a

@@ -1,6 +1,7 @@
 """GPU parity: the HIP path (through the C ABI) against the reference's golden
 fixtures and the CPU oracle.  Tolerances are fp32 reassociation bounds
 (north_star: outputs within 1e-3 relative on fp32)."""
+import contextlib
 import json
 import os
 import random
@@ -1211,6 +1212,51 @@ def test_gcn_module_pair_equals_two_launches(bf16):
         assert torch.equal(g0[k], g1[k]), "d" + k
 
 
+@pytest.mark.parametrize("bn,prec,sizes_a,sizes_b", [
+    (8, "fp32", [20, 7, 13, 20, 2, 33], [20, 1, 20, 9, 33, 17]),
+    (48, "fp32", [20, 20, 20, 20], [20, 20, 20, 20]),
+    (48, "fp32", [64, 3, 57], [64, 64, 1, 12]),
+    (8, "bf16", [20, 7, 13, 20, 2, 33], [20, 1, 20, 9, 33, 17]),
+    (48, "bf16", [64, 3, 57], [64, 64, 1, 12]),
+])
+def test_pool_pair_equals_two_launches(bn, prec, sizes_a, sizes_b):
+    """sgg_pool_fwd2 (pool_pair: a no-grad batch held, carried by the next
+    forward of the same net) == two single-batch launches, bitwise: both
+    outputs, batch b's dh and parameter gradients."""
+    from sgan import kernels as K
+    from sgan.models import PoolHiddenNet
+    from sgan.scene import SceneIndex
+    torch.manual_seed(bn + len(sizes_a))
+    mod = PoolHiddenNet(embedding_dim=16, h_dim=32, mlp_dim=64, bottleneck_dim=bn, batch_norm=False).to(DEV)
+    sca, scb = (SceneIndex(np.concatenate([[0], np.cumsum(sz)]), DEV) for sz in (sizes_a, sizes_b))
+    Ba, Bb = sum(sizes_a), sum(sizes_b)
+    ha, hb0 = torch.randn(Ba, 32, device=DEV), torch.randn(Bb, 32, device=DEV)
+    pa, pb = torch.rand(Ba, 2, device=DEV) * 10, torch.rand(Bb, 2, device=DEV) * 10
+    dout = torch.randn(Bb, bn, device=DEV)
+    prev = K.precision()
+    K.set_precision(prec)
+    try:
+        res = []
+        for paired in (False, True):
+            mod.zero_grad(set_to_none=True)
+            hb = hb0.clone().requires_grad_(True)
+            with (K.pool_pair() if paired else contextlib.nullcontext()) as r:
+                with torch.no_grad():
+                    ya = mod(ha, None, pa, scenes=sca)
+                yb = mod(hb, None, pb, scenes=scb)
+            if paired:
+                assert r.carried, "the second forward did not carry the first"
+            (yb * dout).sum().backward()
+            res.append((ya, yb.detach(), hb.grad, {k: q.grad.clone() for k, q in mod.named_parameters()}))
+    finally:
+        K.set_precision(prev)
+    (a0, b0, d0, g0), (a1, b1, d1, g1) = res
+    assert torch.equal(a0, a1) and torch.equal(b0, b1), "outputs"
+    assert torch.equal(d0, d1), "dh"
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), "d" + k
+
+
 def _gat_encoder_vs_oracle(mod, nh, x, lab, sc, dy):
     """The product GATEncoder (whatever path it takes) against the oracle's
     reference-formulation module with the same weights: output, dx, grads."""
@@ -1322,6 +1368,48 @@ def test_deferred_grad_finish_is_bit_identical(graph):
         tr.g_step(batch, sc)
         grads.update({"g." + k: p.grad.detach().clone() for k, p in g.named_parameters() if p.grad is not None})
         res.append(grads)
+    a, b = res
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+
+
+@pytest.mark.parametrize("graph", ["gat", "sgangat"])
+def test_head_fused_is_bit_identical(graph, monkeypatch):
+    """The discriminator head's forward held until the BCE forward and issued
+    with its backward for the backward seed (sgg_head_fwdbwd, BceLink.run_fused)
+    against the two launches: losses and every gradient of a D-step and a
+    G-step bit-identical; the fused runs issue no separate head forward and
+    accept the seed (no fallback recompute)."""
+    from sgan import kernels as K
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer
+    sizes = [20, 7, 13, 20, 2] if graph == "gat" else [64, 30, 5]
+    batch = synthetic_batch(sizes, seed=5, device=DEV)
+    sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+    calls = [0]
+    plain = K._head_fwd
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return plain(*a, **k)
+    monkeypatch.setattr(K, "_head_fwd", counted)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(K, "HEAD_FUSE", fuse)
+        calls[0] = 0
+        g, d = build_models(graph)
+        tr = GanTrainer(g, d)
+        torch.manual_seed(3)
+        random.seed(3)
+        out = {}
+        out.update({"loss." + k: torch.tensor(float(v)) for k, v in tr.d_step(batch, sc).items()})
+        out.update({"d." + k: p.grad.detach().clone() for k, p in d.named_parameters() if p.grad is not None})
+        out.update({"loss." + k: torch.tensor(float(v)) for k, v in tr.g_step(batch, sc).items()})
+        out.update({"g." + k: p.grad.detach().clone() for k, p in g.named_parameters() if p.grad is not None})
+        res.append(out)
+        assert (calls[0] == 0) == fuse, (fuse, calls[0])
     a, b = res
     assert sorted(a) == sorted(b)
     for k in a:
