@@ -373,8 +373,9 @@ __global__ void __launch_bounds__(64 * (H / 16)) q4_bwd_kernel(
 #pragma unroll
   for (int r = 0; r < 4; ++r) db[r] = dax[r] = day[r] = 0.f;
   load_step(T - 1);
-  if (WGRAD) {   // h_{T-2} of step T - 1 into its buffer
+  if (WGRAD) {   // h_{T-2} of step T - 1 into its buffer (read by every wave)
     hst[(T - 1) & 1][j][u & 3][u >> 2] = nh;
+    __syncthreads();
   }
   for (int t = T - 1; t >= t_stop; --t) {
     const int cur = t & 1;
