@@ -599,7 +599,9 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   // p are ped (p mod Bsrc)'s -- a prefix shared by the halves of the batch
   // and saved once (MwSeg t0); Bsrc is a multiple of 16 there
   const int nsrc = t_sh > 0 ? Bsrc / kMwPeds : 1;
-  auto sblk = [&](bool shared_at) { return shared_at ? blk % nsrc : blk; };
+  // (t_sh == 0: no shared prefix -- every step reads its own block, the
+  // initial cell c_{-1} at index 0 included)
+  auto sblk = [&](bool shared_at) { return (shared_at && t_sh > 0) ? blk % nsrc : blk; };
 
   // weight-gradient operand of step t: h_{t-1} = h_all[t] of the block's 16
   // peds, fetched one step ahead, staged in LDS
