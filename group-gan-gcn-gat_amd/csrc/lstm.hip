@@ -329,9 +329,6 @@ extern "C" int sgg_lstm_bwd_tail(const float* A, const float* Whh, const float* 
   SGG_CHECK_ARG(A && Whh && h_all && c_all && act_all && rel && drel_in, "sgg_lstm_bwd_tail: null pointer");
   SGG_CHECK_ARG(T >= 1 && B >= 1 && t_stop >= 0 && t_stop < T && lstm_mw_ok(H, B),
                 "sgg_lstm_bwd_tail: bad sizes or no four-wave kernel (T=%d B=%d H=%d t_stop=%d)", T, B, H, t_stop);
-  if (lstm_q4_ok(H, B))   // (four peds per workgroup, the same saved states)
-    return lstm_q4_bwd(A, Whh, h_all, c_all, act_all, rel, dh_last, T, B, H, t_stop, 0, 0, nullptr, drel_in, nullptr,
-                       (hipStream_t)stream);
   return lstm_mw_bwd(A, Whh, nullptr, h_all, c_all, act_all, rel, nullptr, dh_last, nullptr, T, B, H, 0, nullptr,
                      drel_in, nullptr, nullptr, (hipStream_t)stream, nullptr, 0, t_stop);
 }
@@ -346,10 +343,6 @@ extern "C" int sgg_lstm_fwd_seg(const SggLstmSeg* seg, int H, void* stream) {
   SGG_CHECK_ARG(lstm_mw_ok(H, seg->B), "sgg_lstm_fwd_seg: no four-wave kernel for H=%d", H);
   return lstm_mw_fwd_seg(to_mw(*seg), H, (hipStream_t)stream);
 }
-
-extern "C" int sgg_lstm_fwd_seg_q4(int H, int B) { return lstm_q4_ok(H, B) ? 1 : 0; }
-
-extern "C" int sgg_lstm_q4_enable(int on) { return lstm_q4_enable(on); }
 
 extern "C" int sgg_lstm_fwd_seg2(const SggLstmSeg* a, int Ha, const SggLstmSeg* b, int Hb, void* stream) {
   SGG_CHECK_ARG(a && b, "sgg_lstm_fwd_seg2: null segment");
@@ -372,20 +365,14 @@ extern "C" int sgg_lstm_bwd_shared(const float* A, const float* Whh, const float
   SGG_CHECK_ARG(A && Whh && h_all && c_all && act_all && rel && drel_in, "sgg_lstm_bwd_shared: null pointer");
   SGG_CHECK_ARG(T >= 1 && B >= 1 && t_sh >= 1 && lstm_mw_ok(H, B),
                 "sgg_lstm_bwd_shared: bad sizes or no four-wave kernel (T=%d B=%d H=%d t_sh=%d)", T, B, H, t_sh);
-  if (lstm_q4_ok(H, B))   // (four peds per workgroup; wpart rows: sgg_lstm_wpart_rows2)
-    return lstm_q4_bwd(A, Whh, h_all, c_all, act_all, rel, dh_last, T, B, H, 0, t_sh, Bsrc, nullptr, drel_in, wpart,
-                       (hipStream_t)stream);
   return lstm_mw_bwd(A, Whh, nullptr, h_all, c_all, act_all, rel, nullptr, dh_last, nullptr, T, B, H, 0, nullptr,
                      drel_in, nullptr, wpart, (hipStream_t)stream, nullptr, 0, 0, t_sh, Bsrc);
 }
 
-extern "C" int sgg_lstm_wpart_rows2(int H, int B, int decoder) {
+extern "C" int sgg_lstm_wpart_rows(int H, int B) {
   if (B < 0) return -1;
-  if (!decoder && lstm_mw_ok(H, B) && lstm_q4_ok(H, B)) return lstm_q4_wpart_rows(B);
   return lstm_mw_ok(H, B) ? lstm_mw_wpart_rows(H, B) : 0;
 }
-
-extern "C" int sgg_lstm_wpart_rows(int H, int B) { return sgg_lstm_wpart_rows2(H, B, 0); }
 
 extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0,
                             const float* c0, const float* Wp, const float* bp, int T, int B, int H, int decoder, float* h_all,
@@ -492,8 +479,6 @@ extern "C" int sgg_lstm_bwd(const float* A, const float* Whh, const float* Wp, c
   if (lstm_mw_ok(H, B)) {
     SGG_CHECK_ARG(!wpart || (h_all && rel && (!decoder || rel_out)),
                   "sgg_lstm_bwd: weight gradients need h_all, rel (and rel_out for the decoder)");
-    if (!decoder && lstm_q4_ok(H, B))   // (four peds per workgroup; wpart rows: sgg_lstm_wpart_rows2)
-      return lstm_q4_bwd(A, Whh, h_all, c_all, act_all, rel, dh_last, T, B, H, 0, 0, 0, dh0, drel_in, wpart, st);
     return lstm_mw_bwd(A, Whh, Wp, h_all, c_all, act_all, rel, rel_out, dh_last, dout, T, B, H, decoder, dh0, drel_in,
                        drel_tot, wpart, st);
   }

@@ -1016,17 +1016,12 @@ static int seg_check(const MwSeg& s, int H, const char* fn) {
 
 int lstm_mw_fwd_seg(const MwSeg& s, int H, hipStream_t st) {
   if (int rc = seg_check(s, H, "sgg_lstm_fwd_seg")) return rc;
-  if (lstm_q4_ok(H, s.B)) return lstm_q4_fwd_seg(s, H, st);   // (an encoder segment: four peds per workgroup)
   return launch_seg_h(s, H, false, st);
 }
 
 int lstm_mw_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb, hipStream_t st) {
   if (int rc = seg_check(a, Ha, "sgg_lstm_fwd_seg2 (a)")) return rc;
   if (int rc = seg_check(b, Hb, "sgg_lstm_fwd_seg2 (b)")) return rc;
-  if (lstm_q4_ok(Ha, a.B) && lstm_q4_ok(Hb, b.B)) {   // (four peds per workgroup)
-    const int rc = lstm_q4_fwd_seg2(a, Ha, b, Hb, st);
-    if (rc != 1) return rc;
-  }
   const int na = (a.B + kMwPeds - 1) / kMwPeds, nb = (b.B + kMwPeds - 1) / kMwPeds;
   if (Ha == 32 && Hb == 48 && b.act_tile) {   // the generator encoder + the discriminator prefix
     auto k = a.act_tile ? lstm_mw_fwd2_kernel<32, true, 48, true> : lstm_mw_fwd2_kernel<32, false, 48, true>;
@@ -1046,10 +1041,6 @@ int lstm_mw_fwd_dec_seg(const float* A, const float* Whh, const float* bias, con
   a.di = *di;
   a.rel0_out = rel0_out;
   if (to) a.to = *to;
-  if (lstm_q4_ok(H, B) && lstm_q4_ok(Hb, b.B)) {   // (four peds per workgroup)
-    const int rc = lstm_q4_fwd_dec_seg(a, H, b, Hb, st);
-    if (rc != 1) return rc;
-  }
   const int na = (B + kMwPeds - 1) / kMwPeds, nb = (b.B + kMwPeds - 1) / kMwPeds;
   if (H == 32 && Hb == 48 && act_all && b.act_tile) {
     hipLaunchKernelGGL((lstm_mw_fwd2d_kernel<32, true, 48, true>), dim3(na + nb), dim3(kMwThreads), 0, st, a, b, na);
@@ -1063,10 +1054,6 @@ int lstm_mw_fwd_seg3(const MwSeg& a, int Ha, const MwSeg& b, int Hb, const MwSeg
   if (int rc = seg_check(a, Ha, "sgg_lstm_fwd_seg3 (a)")) return rc;
   if (int rc = seg_check(b, Hb, "sgg_lstm_fwd_seg3 (b)")) return rc;
   if (int rc = seg_check(c, Hc, "sgg_lstm_fwd_seg3 (c)")) return rc;
-  if (lstm_q4_ok(Ha, a.B) && lstm_q4_ok(Hb, b.B) && lstm_q4_ok(Hc, c.B)) {   // (four peds per workgroup)
-    const int rc = lstm_q4_fwd_seg3(a, Ha, b, Hb, c, Hc, st);
-    if (rc != 1) return rc;
-  }
   const int na = (a.B + kMwPeds - 1) / kMwPeds, nb = (b.B + kMwPeds - 1) / kMwPeds, nc = (c.B + kMwPeds - 1) / kMwPeds;
   if (Ha == 32 && Hb == 48 && Hc == 32 && !a.act_tile && b.act_tile && c.act_tile) {
     hipLaunchKernelGGL((lstm_mw_fwd3_kernel<32, false, 48, true, 32, true>), dim3(na + nb + nc), dim3(kMwThreads), 0, st,

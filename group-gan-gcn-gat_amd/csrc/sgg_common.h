@@ -135,24 +135,6 @@ __device__ __forceinline__ float dec_rel0(const SggDecInit& d, int p, int k) {
   return d.last_rel[(size_t)(p % d.Bper) * 2 + k];
 }
 __attribute__((visibility("hidden"))) int lstm_mw_fwd_seg(const MwSeg& s, int H, hipStream_t st);
-// lstm_q4.hip: encoder segments with four peds per workgroup (4x4x1 MFMA),
-// the four-wave family's tile-native saved states
-__attribute__((visibility("hidden"))) bool lstm_q4_ok(int H, int B);
-__attribute__((visibility("hidden"))) int lstm_q4_enable(int on);
-__attribute__((visibility("hidden"))) int lstm_q4_fwd_seg(const MwSeg& s, int H, hipStream_t st);
-// (1: no four-peds kernel for this combination -- nothing launched)
-__attribute__((visibility("hidden"))) int lstm_q4_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
-                                                           hipStream_t st);
-__attribute__((visibility("hidden"))) int lstm_q4_fwd_dec_seg(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
-                                                              hipStream_t st);
-__attribute__((visibility("hidden"))) int lstm_q4_wpart_rows(int B);
-__attribute__((visibility("hidden"))) int lstm_q4_bwd(const float* A, const float* Whh, const float* h_all,
-                                                      const float* c_all, const float* act_all, const float* rel,
-                                                      const float* dh_last, int T, int B, int H, int t_stop,
-                                                      int t_sh, int Bsrc, float* dh0, float* drel_in, float* wpart,
-                                                      hipStream_t st);
-__attribute__((visibility("hidden"))) int lstm_q4_fwd_seg3(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
-                                                           const MwSeg& c, int Hc, hipStream_t st);
 __attribute__((visibility("hidden"))) int lstm_mw_fwd_seg2(const MwSeg& a, int Ha, const MwSeg& b, int Hb,
                                                            hipStream_t st);
 __attribute__((visibility("hidden"))) int lstm_mw_fwd_dec_seg(const float* A, const float* Whh, const float* bias,

@@ -143,8 +143,6 @@ SIGNATURES = {
     "sgg_xtw_splits": (_i, [_i, _i, _i]),
     "sgg_lstm_bwd_split": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_lstm_bwd_tail": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p]),
-    "sgg_lstm_fwd_seg_q4": (_i, [_i, _i]),
-    "sgg_lstm_q4_enable": (_i, [_i]),
     "sgg_lstm_fwd_seg": (_i, [_sargs, _i, _p]),
     "sgg_lstm_fwd_seg2": (_i, [_sargs, _i, _sargs, _i, _p]),
     "sgg_lstm_fwd_seg3": (_i, [_sargs, _i, _sargs, _i, _sargs, _i, _p]),
@@ -176,7 +174,6 @@ SIGNATURES = {
     "sgg_lstm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "sgg_lstm_state_floats": (ctypes.c_longlong, [_i, _i, _i, _i]),
     "sgg_lstm_wpart_rows": (_i, [_i, _i]),
-    "sgg_lstm_wpart_rows2": (_i, [_i, _i, _i]),
     "sgg_lstm_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
     "sgg_lstm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
     "sgg_bce_fwd": (_i, [_p, _i, _i, _p, _p, _f, _p, _p, _p, _p, _p]),

@@ -2258,16 +2258,13 @@ class _LSTMSeq(torch.autograd.Function):
         dheld = dcarried = False
         if carry:
             ga, gb = seg(0, T, B), pfx_seg
-            q4 = lib.sgg_lstm_fwd_seg_q4(H, B) and lib.sgg_lstm_fwd_seg_q4(pfx.H, pfx.Bsrc) and H == 32
-            kname = "sgg::%s_fwd2_kernel<32, %s, 48, true>" % ("q4" if q4 else "lstm_mw", "true" if save else "false")
+            kname = "sgg::lstm_mw_fwd2_kernel<32, %s, 48, true>" % ("true" if save else "false")
 
             def launch():
                 N.check(lib.sgg_lstm_fwd_seg2(N.ctypes.byref(ga), H, N.ctypes.byref(gb), pfx.H, N.stream_ptr()),
                         "sgg_lstm_fwd_seg2")
         elif cont:
             gs = seg(pfx.T_pre, T - pfx.T_pre, pfx.Bsrc)
-            if lib.sgg_lstm_fwd_seg_q4(H, B):
-                kname = "sgg::q4_fwd_seg_kernel<%d, %s>" % (H, "true" if save else "false")
 
             def launch():
                 N.check(lib.sgg_lstm_fwd_seg(N.ctypes.byref(gs), H, N.stream_ptr()), "sgg_lstm_fwd_seg")
@@ -2297,8 +2294,7 @@ class _LSTMSeq(torch.autograd.Function):
                     # the discriminator's observed-steps prefix of this step rides along
                     pseg = pfx.segment(pfx.obs_rel)
                     pfx.ran = True
-                    q4 = H == 32 and lib.sgg_lstm_fwd_seg_q4(H, B) and lib.sgg_lstm_fwd_seg_q4(pfx.H, pfx.Bsrc)
-                    kname = "sgg::%s_fwd2d_kernel<32, true, 48, true>" % ("q4" if q4 else "lstm_mw")
+                    kname = "sgg::lstm_mw_fwd2d_kernel<32, true, 48, true>"
                     fused = lambda k=fkeep, to=to, pseg=pseg, Hp=pfx.H: lib.sgg_lstm_fwd_dec_seg(
                         N.ctypes.byref(di), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(Wpc), N.ptr(bp), T, B, H,
                         N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel_out), N.ptr(rel),
@@ -2382,9 +2378,8 @@ class _LSTMSeq(torch.autograd.Function):
                 rider.hold([(ga, H), (gb, pfx.H)], launch, (name, key, fl, nb))
             elif carried:
                 hname, hkey, hfl, hnb = rider.timing
-                q4 = lib.sgg_lstm_fwd_seg_q4(H, B) and lib.sgg_lstm_fwd_seg_q4(48, B)
-                timer.add("sgg::%s_fwd3_kernel<32, false, 48, true, 32, true>" % ("q4" if q4 else "lstm_mw"),
-                          hkey + key, hfl + fl, hnb + nb, launch)
+                timer.add("sgg::lstm_mw_fwd3_kernel<32, false, 48, true, 32, true>", hkey + key, hfl + fl, hnb + nb,
+                          launch)
             else:
                 timer.add(name, key, fl, nb, launch)
         ctx.meta = (decoder, T, B, H, h0 is not None)
@@ -2408,7 +2403,7 @@ class _LSTMSeq(torch.autograd.Function):
         dev = rel.device
         need = ctx.needs_input_grad
         wgrad = any(need[1:7])
-        rows = int(lib.sgg_lstm_wpart_rows2(H, B, int(decoder)))
+        rows = int(lib.sgg_lstm_wpart_rows(H, B))
         G4 = 4 * H
         P = G4 * H + G4 + 2 * G4
         # the decoder's rows also carry [dWp (2 x H) | dbp (2)] (lstm_mw.hip)
@@ -2470,10 +2465,8 @@ class _LSTMSeq(torch.autograd.Function):
             nb = 4.0 * (act.numel() + c_all.numel() + T * B * 2 + (B * H if has_h0 else 0)
                         + ((T * B * (H + 2) + wpart.numel()) if wpart is not None else 0)
                         + (dG.numel() if dG is not None else 0) + (T * B * 4 if decoder else 0))
-            bname = lib.sgg_lstm_kernel_name(H, B, int(decoder), int(wpart is not None), 1).decode()
-            if not decoder and split is None and lib.sgg_lstm_fwd_seg_q4(H, B):
-                bname = "sgg::q4_bwd_kernel<%d, %s>" % (H, "true" if wpart is not None else "false")
-            timer.add(bname, (T, B, int(decoder), int(wpart is not None)), fl, nb, launch)
+            timer.add(lib.sgg_lstm_kernel_name(H, B, int(decoder), int(wpart is not None), 1).decode(),
+                      (T, B, int(decoder), int(wpart is not None)), fl, nb, launch)
         dW_ih = dW_hh = db_ih = db_hh = dWe = dbe = dWp = dbp = None
         side_ctx = side(wpart, dG, h_all, rel, rel_out, drel_tot, W_ih, We, be) if wgrad or decoder \
             else contextlib.nullcontext()

@@ -543,9 +543,8 @@ int sgg_lstm_fwd_u(const float* rel, const float* A, const float* Whh, const flo
  * step inputs), dh0 (B x H, may be NULL; no gradient is produced for c0)
  * and, for the decoder, drel_tot (T x B x 2, total dL/d rel_out[t]).
  * Weight gradients, two forms:
- *  - sgg_lstm_wpart_rows2(H, B, decoder) > 0 (the four-wave MFMA family and,
- *    for encoders, the four-peds kernels): pass wpart (that many rows x
- *    (4H*H + 4H + 8H) floats; the decoder's rows are 2H + 2 wider)
+ *  - sgg_lstm_wpart_rows(H, B) > 0 (the four-wave MFMA family): pass wpart
+ *    (rows x (4H*H + 4H + 8H) floats; the decoder's rows are 2H + 2 wider)
  *    and the kernel accumulates, per workgroup, one slab row [dW_hh (4H x H)
  *    | dbias (4H) | dA (4H x 2)] = sum over its peds and all steps of
  *    dG_t^T [h_{t-1} | 1 | r_in(t)] (h_all and rel -- and rel_out for the
@@ -558,11 +557,6 @@ int sgg_lstm_fwd_u(const float* rel, const float* A, const float* Whh, const flo
  *    must be NULL.
  * In the dG form dWp / dbp of the decoder are X^T sums of drel_tot and h_all,
  * left to the caller. */
-/* The slab rows of the backward of an encoder (decoder = 0) or decoder
- * sequence of (H, B): an encoder on the four-peds kernels (sgg_lstm_fwd_seg_q4)
- * writes one row per four peds, the four-wave kernels one per 16.
- * sgg_lstm_wpart_rows(H, B) = sgg_lstm_wpart_rows2(H, B, 0). */
-int sgg_lstm_wpart_rows2(int H, int B, int decoder);
 int sgg_lstm_wpart_rows(int H, int B);
 /* Name of the kernel sgg_lstm_fwd (bwd = 0; save = act_all != NULL) or
  * sgg_lstm_bwd (bwd = 1) launches for these sizes, as rocprofv3 lists it
@@ -626,13 +620,6 @@ typedef struct {
   float* U;
 } SggLstmSeg;
 int sgg_lstm_fwd_seg(const SggLstmSeg* seg, int H, void* stream);
-/* 1 when sgg_lstm_fwd_seg runs (H, B) on the four-peds-per-workgroup
- * kernels (H = 32 / 48; v_mfma_f32_4x4x1_16b_f32, the same saved-state
- * layout; SGG_LSTM_Q4=0 turns them off), else 0. */
-int sgg_lstm_fwd_seg_q4(int H, int B);
-/* Turn the four-peds-per-workgroup segments on (1) or off (0) for the
- * process; returns the previous setting (kernel comparisons, tests). */
-int sgg_lstm_q4_enable(int on);
 /* Two independent segments in ONE launch (a's workgroups first); one launch
  * for (Ha, Hb) = (32, 48) with b saving states, two launches otherwise. */
 int sgg_lstm_fwd_seg2(const SggLstmSeg* a, int Ha, const SggLstmSeg* b, int Hb, void* stream);

@@ -592,7 +592,6 @@ def test_encoder_projection_epilogue(H, T, B, save):
     net's first layer, Wu = W1[:, E:] in place) equals the sgg_xw form, and
     h_T is unchanged by the epilogue."""
     from sgan import kernels as K
-    lstm_q4.sgg_lstm_q4_enable(q4)
     torch.manual_seed(H + B)
     lstm = torch.nn.LSTM(16, H).to(DEV)
     emb = torch.nn.Linear(2, 16).to(DEV)
@@ -647,8 +646,7 @@ def test_fused_head_matches_torch(M, Kd, N1, relu1, relu2):
 
 @pytest.mark.parametrize("H,B", [(48, 1280), (48, 37), (32, 100)])
 @pytest.mark.parametrize("proj", [False, True])
-@pytest.mark.parametrize("q4", [0, 1])
-def test_encoder_backward_tail_equals_full(H, B, proj, q4, lstm_q4):
+def test_encoder_backward_tail_equals_full(H, B, proj):
     """Frozen-weight encoder backward over the steps whose input gradients are
     wanted (sgg_lstm_bwd_tail, the generator step's pass through D: traj_cat
     marks the observed steps as not needing a gradient) is bit-identical to
@@ -677,12 +675,7 @@ def test_encoder_backward_tail_equals_full(H, B, proj, q4, lstm_q4):
         (h * dh).sum().backward()
         grads.append(pred.grad.clone())
         outs.append((h.detach().clone(), U.clone() if U is not None else None))
-    # q4: the tail on the four-peds backward (the full BPTT stays on the 16-ped
-    # kernel): equal up to fp32 reassociation
-    if q4:
-        assert close_to(grads[0], grads[1]), (grads[0] - grads[1]).abs().max().item()
-    else:
-        torch.testing.assert_close(grads[0], grads[1], rtol=0, atol=0)
+    torch.testing.assert_close(grads[0], grads[1], rtol=0, atol=0)
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)
     if proj:
         assert outs[0][1] is not None
@@ -1423,29 +1416,9 @@ def test_head_fused_is_bit_identical(graph, monkeypatch):
         assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
 
 
-@pytest.fixture
-def lstm_q4():
-    """Sets the four-peds-per-workgroup LSTM segments on / off (request.param)
-    for one test and restores the previous setting."""
-    from sgan import _native as N
-    lib = N.load()
-    prev = lib.sgg_lstm_q4_enable(1)
-    try:
-        yield lib
-    finally:
-        lib.sgg_lstm_q4_enable(prev)
-
-
-def close_to(x, y, rel=2e-5):
-    """max |x - y| <= rel * max(1, max |y|): fp32 reassociation bounds."""
-    scale = max(1.0, y.abs().max().item()) if y.numel() else 1.0
-    return (x - y).abs().max().item() <= rel * scale if x.numel() else True
-
-
 @pytest.mark.parametrize("graph,sizes", [("gat", [20, 7, 13, 20, 4]), ("gat", [20, 7, 13, 20, 2]),
                                          ("gcn", [64, 30, 2])])
-@pytest.mark.parametrize("q4", [0, 1])
-def test_shared_prefix_is_bit_identical(graph, sizes, q4, lstm_q4):
+def test_shared_prefix_is_bit_identical(graph, sizes):
     """The discriminator encoder's observed steps run once beside the
     generator's encoder (kernels.SharedPrefix: sgg_lstm_fwd_seg2, the
     suffix from step obs_len by sgg_lstm_fwd_seg, the D-step backward through
@@ -1457,7 +1430,6 @@ def test_shared_prefix_is_bit_identical(graph, sizes, q4, lstm_q4):
     from sgan.data.synthetic import synthetic_batch
     from sgan.scene import SceneIndex
     from sgan.train_step import GanTrainer, KernelOps
-    lstm_q4.sgg_lstm_q4_enable(q4)
     batch = synthetic_batch(sizes, seed=5, device=DEV)
     sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
     seen = []
@@ -1490,70 +1462,51 @@ def test_shared_prefix_is_bit_identical(graph, sizes, q4, lstm_q4):
     a, b = res
     assert sorted(a) == sorted(b)
     for k in a:
-        # q4: the discriminator's continuation (sgg_lstm_fwd_seg) runs on the
-        # four-peds kernels, whose sums round differently from the full
-        # sequence's 16-ped kernel -- equal up to fp32 reassociation
-        if q4:
-            assert close_to(a[k], b[k], 1e-4), (k, (a[k] - b[k]).abs().max().item())
-        else:
-            assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
 
 
-@pytest.mark.parametrize("H,B,T", [(48, 1280, 12), (48, 37, 20), (32, 100, 8)])
-@pytest.mark.parametrize("wgrad", [False, True])
-def test_q4_lstm_equals_four_wave(H, B, T, wgrad, lstm_q4):
-    """The four-peds encoder kernels (lstm_q4.hip) against the four-wave
-    ones on the same inputs: a forward segment (sgg_lstm_fwd_seg, with the
-    projection epilogue) -- h, U and the tile-native saved states -- and the
-    backward from the four-wave saved states (sgg_lstm_bwd: drel_in, dh0, the
-    slab's row sums), equal up to fp32 reassociation."""
+@pytest.mark.parametrize("H", [32, 48])
+def test_lstm_backward_nonzero_c0_per_block(H):
+    """C ABI: a batch of three 16-ped blocks with a nonzero initial cell c0
+    (sgg_lstm_fwd / sgg_lstm_bwd with weight gradients and dh0) equals the
+    three blocks run one at a time, bitwise: drel_in, dh0 and each block's
+    slab row.  (Regression: the four-wave backward once read block 0's
+    c_{-1} for every block.)"""
     from sgan import _native as N
-    lib = lstm_q4
-    torch.manual_seed(H + B + T)
+    lib = N.load()
+    torch.manual_seed(H)
+    T, B = 6, 48
     f = lambda *s, sc=0.3: (torch.randn(*s, device=DEV) * sc).contiguous()
-    A, Whh, bias, NU = f(4 * H, 2), f(4 * H, H, sc=0.2), f(4 * H), 64
-    Wu, cu = f(NU, H), f(NU)
+    A, Whh, bias = f(4 * H, 2), f(4 * H, H, sc=0.2), f(4 * H)
     rel, h0, c0, dh_last = f(T, B, 2), f(B, H), f(B, H), f(B, H)
-    sf = lambda w: torch.zeros(int(lib.sgg_lstm_state_floats(T, B, H, w)), device=DEV)
     P = 4 * H * H + 4 * H + 8 * H
 
-    def fwd(q4):
-        lib.sgg_lstm_q4_enable(q4)
-        h_all, c_all, act = torch.zeros(T + 1, B, H, device=DEV), sf(1), sf(0)
-        U = torch.empty(B, NU, device=DEV)
-        sg = N.LstmSeg(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0), N.ptr(c0), T, B, B, 0, T, B,
-                       N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(Wu), Wu.stride(0), N.ptr(cu), NU, N.ptr(U))
-        N.check(lib.sgg_lstm_fwd_seg(N.ctypes.byref(sg), H, N.stream_ptr()), "seg")
+    def run(lo, hi):
+        n = hi - lo
+        r, h, c, d = (rel[:, lo:hi].contiguous(), h0[lo:hi].contiguous(), c0[lo:hi].contiguous(),
+                      dh_last[lo:hi].contiguous())
+        sf = lambda w: torch.empty(int(lib.sgg_lstm_state_floats(T, n, H, w)), device=DEV)
+        h_all, c_all, act = torch.empty(T + 1, n, H, device=DEV), sf(1), sf(0)
+        N.check(lib.sgg_lstm_fwd(N.ptr(r), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h), N.ptr(c), None, None, T, n,
+                                 H, 0, N.ptr(h_all), N.ptr(c_all), N.ptr(act), None, N.stream_ptr()), "fwd")
+        rows = int(lib.sgg_lstm_wpart_rows(H, n))
+        assert rows == n // 16
+        wpart = torch.empty(rows, P, device=DEV)
+        drel, dh0 = torch.empty(T, n, 2, device=DEV), torch.empty(n, H, device=DEV)
+        N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), None, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(r), None,
+                                 N.ptr(d), None, T, n, H, 0, None, N.ptr(dh0), N.ptr(drel), None, N.ptr(wpart),
+                                 N.stream_ptr()), "bwd")
         torch.cuda.synchronize()
-        return h_all, c_all, act, U
+        return drel, dh0, wpart
 
-    def bwd(q4, st):
-        lib.sgg_lstm_q4_enable(q4)
-        h_all, c_all, act = st[:3]
-        rows = int(lib.sgg_lstm_wpart_rows2(H, B, 0))
-        wpart = torch.empty(rows, P, device=DEV) if wgrad else None
-        drel, dh0 = torch.empty(T, B, 2, device=DEV), torch.empty(B, H, device=DEV)
-        N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), None, N.ptr(h_all), N.ptr(c_all), N.ptr(act), N.ptr(rel),
-                                 None, N.ptr(dh_last), None, T, B, H, 0, None, N.ptr(dh0), N.ptr(drel), None,
-                                 N.ptr(wpart), N.stream_ptr()), "bwd")
-        torch.cuda.synchronize()
-        return drel, dh0, (wpart.double().sum(0) if wgrad else torch.zeros(1, device=DEV))
-
-    s4, s16 = fwd(1), fwd(0)
-    for x, y, nm in zip(s4, s16, ("h_all", "c (tile)", "act (tile)", "U")):
-        if nm.endswith("(tile)") and B % 16:   # (the four-wave kernel also fills its padded lanes' slots)
-            continue
-        assert close_to(x, y), (nm, (x - y).abs().max().item())
-    ref = bwd(0, s16)
-    # the four-peds backward on the four-wave states, and the four-wave
-    # backward on the four-peds states (the layouts are interchangeable)
-    for got in (bwd(1, s16), bwd(0, s4)):
-        for x, y, nm in zip(got, ref, ("drel_in", "dh0", "slab sums")):
-            assert close_to(x.float(), y.float(), 5e-5), (nm, (x - y).abs().max().item())
+    full = run(0, B)
+    parts = [run(16 * k, 16 * k + 16) for k in range(3)]
+    assert torch.equal(full[0], torch.cat([p[0] for p in parts], 1)), "drel_in"
+    assert torch.equal(full[1], torch.cat([p[1] for p in parts], 0)), "dh0"
+    assert torch.equal(full[2], torch.cat([p[2] for p in parts], 0)), "slab rows"
 
 
-@pytest.mark.parametrize("q4", [0, 1])
-def test_lstm_segments_equal_full_sequence(q4, lstm_q4):
+def test_lstm_segments_equal_full_sequence():
     """C ABI: a 3-copy batch whose first 5 steps are shared -- prefix on 32
     peds beside another encoder in one launch (sgg_lstm_fwd_seg2), suffix on
     96 peds (sgg_lstm_fwd_seg, t0 = 5, Bsrc = 32), backward with weight
@@ -1561,7 +1514,6 @@ def test_lstm_segments_equal_full_sequence(q4, lstm_q4):
     the full sequence: h, U, drel_in and the slab bit-identical."""
     from sgan import _native as N
     lib = N.load()
-    lib.sgg_lstm_q4_enable(q4)
     torch.manual_seed(2)
     T, T0, Bs, C, H, NU = 11, 5, 32, 3, 48, 64
     B = Bs * C
@@ -1607,13 +1559,8 @@ def test_lstm_segments_equal_full_sequence(q4, lstm_q4):
         torch.cuda.synchronize()
         return h_all[T0 + 1:].clone(), U, drel, wpart
 
-    # q4: the suffix on the four-peds kernel (its saved states feed the 16-ped
-    # backward): equal to the full 16-ped sequence up to fp32 reassociation
     for x, y, nm in zip(run(True), run(False), ("h", "U", "drel_in", "slab")):
-        if q4:
-            assert close_to(x, y), (nm, (x - y).abs().max().item())
-        else:
-            assert torch.equal(x, y), (nm, (x - y).abs().max().item())
+        assert torch.equal(x, y), (nm, (x - y).abs().max().item())
 
 
 def test_step_glue_kernels_match_torch():
