@@ -17,48 +17,24 @@
 
 namespace sgg {
 
-// One row of a fold.  E <= kFoldE: the row's W entries, We and be are all
-// requested before the first FMA -- one memory round trip per launch (the
-// weights were just written by the optimizer: the reads come from HBM);
-// wider E walks the row in blocks of kFoldE.
-constexpr int kFoldE = 32;
-
-__device__ __forceinline__ void fold_row(const float* __restrict__ W, int ldw, int E, const float* __restrict__ We,
-                                         const float* __restrict__ be, const float* __restrict__ b1,
-                                         const float* __restrict__ b2, float* __restrict__ A,
-                                         float* __restrict__ bias, int r) {
-  float a0 = 0.f, a1 = 0.f, bb = 0.f;
-  const float* w = W + (size_t)r * ldw;
-  const float c1 = b1[r], c2 = b2 ? b2[r] : 0.f;
-  for (int e0 = 0; e0 < E; e0 += kFoldE) {
-    float wv[kFoldE], x0[kFoldE], x1[kFoldE], xb[kFoldE];
-#pragma unroll
-    for (int u = 0; u < kFoldE; ++u) {
-      const bool ok = e0 + u < E;
-      wv[u] = ok ? w[e0 + u] : 0.f;
-      x0[u] = ok ? We[2 * (e0 + u)] : 0.f;
-      x1[u] = ok ? We[2 * (e0 + u) + 1] : 0.f;
-      xb[u] = ok ? be[e0 + u] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < kFoldE; ++u) {   // (the same fmaf chain in e order as before)
-      if (e0 + u < E) {
-        a0 = fmaf(wv[u], x0[u], a0);
-        a1 = fmaf(wv[u], x1[u], a1);
-        bb = fmaf(wv[u], xb[u], bb);
-      }
-    }
-  }
-  A[2 * r] = a0;
-  A[2 * r + 1] = a1;
-  bias[r] = bb + c1 + c2;
-}
-
 __global__ void __launch_bounds__(512) fold_fwd_kernel(const float* __restrict__ W, int ldw, int R, int E,
                                                        const float* __restrict__ We, const float* __restrict__ be,
                                                        const float* __restrict__ b1, const float* __restrict__ b2,
                                                        float* __restrict__ A, float* __restrict__ bias) {
-  for (int r = threadIdx.x; r < R; r += blockDim.x) fold_row(W, ldw, E, We, be, b1, b2, A, bias, r);
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f, bb = 0.f;
+    const float* w = W + (size_t)r * ldw;
+#pragma unroll 8
+    for (int e = 0; e < E; ++e) {
+      const float we = w[e];
+      a0 = fmaf(we, We[2 * e], a0);
+      a1 = fmaf(we, We[2 * e + 1], a1);
+      bb = fmaf(we, be[e], bb);
+    }
+    A[2 * r] = a0;
+    A[2 * r + 1] = a1;
+    bias[r] = bb + b1[r] + (b2 ? b2[r] : 0.f);
+  }
 }
 
 // every fold of a module set in one launch: workgroup k computes fold k
@@ -68,7 +44,20 @@ struct FoldList {
 
 __global__ void __launch_bounds__(512) fold_fwd_multi_kernel(FoldList L) {
   const SggFold& d = L.f[blockIdx.x];
-  for (int r = threadIdx.x; r < d.R; r += blockDim.x) fold_row(d.W, d.ldw, d.E, d.We, d.be, d.b1, d.b2, d.A, d.bias, r);
+  for (int r = threadIdx.x; r < d.R; r += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f, bb = 0.f;
+    const float* w = d.W + (size_t)r * d.ldw;
+#pragma unroll 8
+    for (int e = 0; e < d.E; ++e) {
+      const float we = w[e];
+      a0 = fmaf(we, d.We[2 * e], a0);
+      a1 = fmaf(we, d.We[2 * e + 1], a1);
+      bb = fmaf(we, d.be[e], bb);
+    }
+    d.A[2 * r] = a0;
+    d.A[2 * r + 1] = a1;
+    d.bias[r] = bb + d.b1[r] + (d.b2 ? d.b2[r] : 0.f);
+  }
 }
 
 // (dA, dbias) staged in LDS once; thread t owns column e = t % E of row group
@@ -76,11 +65,6 @@ __global__ void __launch_bounds__(512) fold_fwd_multi_kernel(FoldList L) {
 // of its column in registers), and its three column sums walk the group's
 // rows with the W loads all independent (many in flight); the groups are
 // summed in LDS in a fixed order.
-// The thread's W entries (its column, every ng-th row: R / ng <= kFoldRows
-// of them for E >= 16) are requested before the (dA, dbias) staging, so the
-// launch waits on one memory round trip, not two.
-constexpr int kFoldRows = 16;
-
 __device__ __forceinline__ void fold_bwd_body(const float* __restrict__ W, int ldw, int R, int E,
                                               const float* __restrict__ We, const float* __restrict__ be,
                                               const float* __restrict__ dA, const float* __restrict__ dbias,
@@ -88,17 +72,6 @@ __device__ __forceinline__ void fold_bwd_body(const float* __restrict__ W, int l
                                               float* __restrict__ dbe, float* __restrict__ dbias_copy) {
   __shared__ float g3[3 * 512];        // (dA_x, dA_y, dbias) per row, R <= 512
   __shared__ float part[3 * 512];      // per (group, column) sums
-  const int ng = blockDim.x / E;
-  const int t = threadIdx.x;
-  const bool owner = t < ng * E;
-  const int e = owner ? t % E : 0, g = owner ? t / E : 0;
-  float wv[kFoldRows];
-#pragma unroll
-  for (int i = 0; i < kFoldRows; ++i) {
-    const int r = g + i * ng;
-    wv[i] = (owner && r < R) ? W[(size_t)r * ldw + e] : 0.f;
-  }
-  const float we0 = owner ? We[2 * e] : 0.f, we1 = owner ? We[2 * e + 1] : 0.f, bee = owner ? be[e] : 0.f;
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
     const float2 a = reinterpret_cast<const float2*>(dA)[r];
     const float b = dbias[r];
@@ -109,30 +82,32 @@ __device__ __forceinline__ void fold_bwd_body(const float* __restrict__ W, int l
     if (dbias_copy) dbias_copy[r] = b;
   }
   __syncthreads();
-  if (owner) {
+  const int ng = blockDim.x / E;
+  const int t = threadIdx.x;
+  if (t < ng * E) {
+    const int e = t % E, g = t / E;
+    const float we0 = We[2 * e], we1 = We[2 * e + 1], bee = be[e];
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    auto row = [&](int r, float w) {
+#pragma unroll 8
+    for (int r = g; r < R; r += ng) {
       const float a0 = g3[3 * r], a1 = g3[3 * r + 1], b = g3[3 * r + 2];
       dW[(size_t)r * lddw + e] = fmaf(a0, we0, fmaf(a1, we1, b * bee));
+      const float w = W[(size_t)r * ldw + e];
       s0 = fmaf(w, a0, s0);
       s1 = fmaf(w, a1, s1);
       s2 = fmaf(w, b, s2);
-    };
-#pragma unroll
-    for (int i = 0; i < kFoldRows; ++i)   // (rows in the same order as before)
-      if (g + i * ng < R) row(g + i * ng, wv[i]);
-    for (int r = g + kFoldRows * ng; r < R; r += ng) row(r, W[(size_t)r * ldw + e]);
+    }
     part[3 * t] = s0;
     part[3 * t + 1] = s1;
     part[3 * t + 2] = s2;
   }
   __syncthreads();
   if (t < 3 * E) {   // output (e, j): dWe[e][j] (j < 2) or dbe[e] (j = 2)
-    const int e2 = t / 3, j = t - 3 * e2;
+    const int e = t / 3, j = t - 3 * e;
     float s = 0.f;
-    for (int g2 = 0; g2 < ng; ++g2) s += part[3 * (g2 * E + e2) + j];
-    if (j < 2) dWe[2 * e2 + j] = s;
-    else dbe[e2] = s;
+    for (int g = 0; g < ng; ++g) s += part[3 * (g * E + e) + j];
+    if (j < 2) dWe[2 * e + j] = s;
+    else dbe[e] = s;
   }
 }
 
