@@ -378,7 +378,10 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
             g1 = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, overlap=OVERLAP, **kw)
             gk = None
             if GRAPH_ITERS > 1 and world == 1:
+                # (the timed trainer draws each replay's host RNG numbers
+                # while the previous replay runs: GraphedTrainer draw_ahead)
                 gk = GraphedTrainer(trainer, batch, sc, warmup=0, batch_g=batch_g, sc_g=sc_g, iters=GRAPH_ITERS,
+                                    draw_ahead=True,
                                     overlap=OVERLAP, **kw)
 
             if gk is not None:   # both graphs replayed once before any timing (first-replay costs)
@@ -502,7 +505,7 @@ def leg_line(name, spec, res, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None,
                     help="scenes per GPU (default: 64 at N = 1, BASELINE configs[1]; 4096 / N at N > 1, configs[3])")

@@ -549,7 +549,7 @@ class GraphedTrainer:
     device)."""
 
     def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2, batch_g=None,
-                 sc_g=None, draw=None, prologue=None, iters=1, overlap=False):
+                 sc_g=None, draw=None, prologue=None, iters=1, overlap=False, draw_ahead=False):
         """draw: () -> (z_d, z_g, y) host tensors of the staging shapes (default:
         trainer.draw_inputs over this rank's span); prologue: launches captured
         ahead of the step (the padded real-data path's batch gathers).
@@ -596,6 +596,14 @@ class GraphedTrainer:
         self.stage = [[tuple(v) if nd else (None, None, v[0]) for v in blocks(f)] for f in self.stage_flat]
         self.stage_ev = [None, None]
         self.cur = 0
+        # draw_ahead (one rank): the host draws of the next replay are made
+        # right after this replay is queued (the same draw sequence of THIS
+        # trainer, one replay earlier in wall-clock time), so a replay never
+        # waits for the host RNG.  Off by default: with it, code that draws
+        # from the host RNG between steps (another trainer, e.g. the
+        # bucketed real-data one) sees the state one replay ahead
+        self.draw_ahead = draw_ahead
+        self.drawn = [False, False]
         self.inp_flat = torch.zeros(iters * per, device=dev)
         self.inps = [StepInputs(v[0], v[1], v[2]) if nd else StepInputs(None, None, v[0]) for v in blocks(self.inp_flat)]
         self.inp = self.inps[0]
@@ -752,22 +760,29 @@ class GraphedTrainer:
         ev.record()
         self.stage_ev[i] = ev
 
+    def _fill(self, i):
+        """The host draws of graph i's next replay into its staging buffer,
+        once graph i's previous replay (which read that buffer) is done."""
+        if self.done_ev[i] is not None:
+            self.done_ev[i].synchronize()
+        for j in range(self.iters):           # the replay's iterations' draws, in order
+            z_d, z_g, y = self.draw()
+            h_zd, h_zg, h_y = self.stage[i][j]
+            if z_d is not None:
+                h_zd.copy_(z_d)
+            if z_g is not None:
+                h_zg.copy_(z_g)
+            h_y.copy_(y)
+        self.drawn[i] = True
+
     def step(self):
         """Draw this iteration's host RNG numbers, replay the graph; returns the
         (device) loss dicts of the captured step."""
         if self.pair:
             i = self.cur
             self.cur ^= 1
-            if self.done_ev[i] is not None:
-                self.done_ev[i].synchronize()     # graph i's previous replay has read buffer i
-            for j in range(self.iters):           # the replay's iterations' draws, in order
-                z_d, z_g, y = self.draw()
-                h_zd, h_zg, h_y = self.stage[i][j]
-                if z_d is not None:
-                    h_zd.copy_(z_d)
-                if z_g is not None:
-                    h_zg.copy_(z_g)
-                h_y.copy_(y)
+            if not self.drawn[i]:
+                self._fill(i)
             g, self.losses, grads = self.pair[i]
             if self.overlap:
                 self._replay_overlap(*g)
@@ -776,6 +791,9 @@ class GraphedTrainer:
             ev = torch.cuda.Event()
             ev.record()
             self.done_ev[i] = ev
+            self.drawn[i] = False
+            if self.draw_ahead:   # the next replay's draws while this one runs
+                self._fill(i ^ 1)
             self._after_replay(grads)
             return self.losses
         self._load(*self.draw())

@@ -835,6 +835,37 @@ def test_graphed_trainer_equals_eager(replays):
     assert (sa - sb).abs().max().item() <= 1e-5 + 1e-5 * sa.abs().max().item(), "eager D forward after replays"
 
 
+@pytest.mark.parametrize("iters", [1, 4])
+def test_graphed_trainer_draw_ahead_is_bit_identical(iters):
+    """GraphedTrainer(draw_ahead=True) -- each replay's host draws made while
+    the previous replay runs -- against draw_ahead=False: the same losses and
+    weights after three replays, bitwise (the same draw sequence)."""
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, GraphedTrainer
+    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
+    batch_g = synthetic_batch([20, 7, 13, 20, 2], seed=4, device=DEV)
+    res = []
+    for ahead in (False, True):
+        g, d = build_models()
+        tr = GanTrainer(g, d, capturable=True)
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
+        torch.manual_seed(11)
+        random.seed(11)
+        gt = GraphedTrainer(tr, batch, sc, warmup=1, batch_g=batch_g, sc_g=scg, iters=iters, draw_ahead=ahead)
+        for _ in range(3):
+            ld, lg = gt.step()
+        torch.cuda.synchronize()
+        ws = {"g." + k: v.detach().clone() for k, v in g.state_dict().items()}
+        ws.update({"d." + k: v.detach().clone() for k, v in d.state_dict().items()})
+        res.append(({k: float(v) for k, v in list(ld.items()) + list(lg.items())}, ws))
+    (la, wa), (lb, wb) = res
+    assert la == lb
+    for k in wa:
+        assert torch.equal(wa[k], wb[k]), k
+
+
 @pytest.mark.parametrize("iters", [1, 2])
 def test_graphed_trainer_overlap_equals_eager(iters):
     """The overlapped plan (GraphedTrainer(overlap=True): the G-step's prefix
