@@ -309,9 +309,16 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
 
     constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + 255) / 256;   // float4 of U per thread
     constexpr int kWQ = (16 * NT * (kKT / 4) + 255) / 256;            // float4 of W2 per thread
-    float4 ureg[kUQ], wreg[kWQ];
-    float areg = 0.f;
-    auto load_tile = [&](int k0) {
+    // a register set of one staged tile (U rows, W2 rows, A)
+    struct Stage {
+      float4 u[kUQ], w[kWQ];
+      float a;
+    };
+    Stage sx;
+    auto load_tile = [&](Stage& st, int k0) {
+      float4 (&ureg)[kUQ] = st.u;
+      float4 (&wreg)[kWQ] = st.w;
+      float& areg = st.a;
 #pragma unroll
       for (int e = 0; e < kUQ; ++e) {
         const int q = threadIdx.x + 256 * e;
@@ -328,7 +335,10 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
       if (threadIdx.x < 2 * kKT) areg = A[2 * k0 + threadIdx.x];
     };
     // float4 c4 of a row holds units 4 c4 .. 4 c4 + 3 = k-step c4 of lane quarters 0..3
-    auto store_tile = [&](float* tb) {
+    auto store_tile = [&](const Stage& st, float* tb) {
+      const float4 (&ureg)[kUQ] = st.u;
+      const float4 (&wreg)[kWQ] = st.w;
+      const float areg = st.a;
       float* Us = tb;
       float* W2s = tb + SGG_POOL_MAX_PEDS * kVP;
       float* As = W2s + 16 * NT * kVP;
@@ -391,28 +401,29 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
     // fragments in registers), tile k + 1's fragments come in from the other
     // buffer and tile k + 2's global loads are in flight; tile k + 2 is then
     // stored over tile k (whose fragments every wave read before the last
-    // barrier)
+    // barrier).  (Two register sets -- loads two tiles ahead -- measured no
+    // faster for the small G tiles: 21.4 vs 21.3 us.)
     constexpr int NKT = kHidden / kKT;   // 8 (even)
     Frag F0, F1;
-    load_tile(0);
+    load_tile(sx, 0);
     __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
-    store_tile(tb0);
-    load_tile(kKT);
+    store_tile(sx, tb0);
+    load_tile(sx, kKT);
     __syncthreads();
     read_frag(tb0, F0);
-    store_tile(tb1);
+    store_tile(sx, tb1);
     __syncthreads();
 #pragma unroll
     for (int kt = 0; kt < NKT; kt += 2) {
-      if (kt + 2 < NKT) load_tile((kt + 2) * kKT);
+      if (kt + 2 < NKT) load_tile(sx, (kt + 2) * kKT);
       read_frag(tb1, F1);
       compute(F0);
-      if (kt + 2 < NKT) store_tile(tb0);
+      if (kt + 2 < NKT) store_tile(sx, tb0);
       __syncthreads();
-      if (kt + 3 < NKT) load_tile((kt + 3) * kKT);
+      if (kt + 3 < NKT) load_tile(sx, (kt + 3) * kKT);
       if (kt + 2 < NKT) read_frag(tb0, F0);
       compute(F1);
-      if (kt + 3 < NKT) store_tile(tb1);
+      if (kt + 3 < NKT) store_tile(sx, tb1);
       __syncthreads();
     }
 
@@ -581,11 +592,9 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
       const int ngr = (npairs + 15) >> 4;   // groups with pairs (wave-uniform tests below)
       __syncthreads();   // tile 0 staged
 
-      constexpr int NKT = kHidden / kKT;
-#pragma unroll 1
-      for (int kt = 0; kt < NKT; ++kt) {
-        // registers: tile kt + 1 in rb (loaded a tile ago); issue tile kt + 2 into ra
-        if (kt + 2 < NKT) load_tile(ra, (kt + 2) * kKT);
+      constexpr int NKT = kHidden / kKT;   // (even)
+      // the k-steps of tile kt from LDS buffer kt & 1
+      auto compute = [&](int kt) {
         const float* ut = Ut + (kt & 1) * SGG_POOL_MAX_PEDS * kBfUP;
 #pragma unroll 1
         for (int sk = 0; sk < kKT / 32; ++sk) {
@@ -634,9 +643,22 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
             }
           }
         }
-        if (kt + 1 < NKT) store_tile(rb, (kt + 1) & 1);   // (buffer (kt + 1) & 1 was last read in tile kt - 1)
-#pragma unroll
-        for (int e = 0; e < kUQ; ++e) rb[e] = ra[e];
+      };
+      // two register sets in turn (no copy between them): the loads of tile
+      // kt + 2, issued before tile kt's k-steps, are stored to LDS only after
+      // tile kt + 1's -- a whole tile of MFMAs in flight over their latency
+      // (a copy ra -> rb at the end of each tile waited for the loads just issued)
+#pragma unroll 1
+      for (int kt = 0; kt < NKT; kt += 2) {
+        // rb holds tile kt + 1 (loaded a tile ago); ra takes tile kt + 2
+        if (kt + 2 < NKT) load_tile(ra, (kt + 2) * kKT);
+        compute(kt);
+        store_tile(rb, (kt + 1) & 1);   // (buffer (kt + 1) & 1 was last read in tile kt - 1)
+        __syncthreads();
+        // ra holds tile kt + 2; rb takes tile kt + 3
+        if (kt + 3 < NKT) load_tile(rb, (kt + 3) * kKT);
+        compute(kt + 1);
+        if (kt + 2 < NKT) store_tile(ra, kt & 1);
         __syncthreads();
       }
 
