@@ -6,9 +6,9 @@
 // that decomposition directly (s_i + t_j, 2NF MACs instead of 2N^2F), which
 // is exact up to fp32 reassociation.  One workgroup (4 waves) per segment
 // (scene for the intra-group graph, the scene's groups for the inter-group
-// graph); Wh is LDS-resident with an odd row stride (F | 1) so column walks
-// across rows are bank-conflict free; one wave per attention row with lanes
-// over j: row max / row sum are wave shuffles (__shfl_xor over 64 lanes).
+// graph); Wh is LDS-resident (odd row stride), the attention of a 16-row
+// block lives in registers and both products (att @ Wh, and the backward's
+// dhp @ Wh^T / att^T @ dhp) run on fp32 MFMA tiles (below).
 //
 // Multi-head (the batched GAT of the sgangat family, sgan/GAT.py:6-55 text):
 // Wh holds all heads side by side (n x heads*F, the output of one X @ [w_0 |
@@ -23,110 +23,152 @@ namespace sgg {
 constexpr int kGatThreads = 256;
 constexpr int kGatWaves = kGatThreads / 64;
 
-__device__ __forceinline__ bool gat_edge(int mode, const float* lab, int i, int j) {
-  if (mode == 1 || i == j) return true;
-  const float li = lab[i];
-  return li != 0.f && li == lab[j];
-}
-
 __device__ __forceinline__ float lrelu(float x, float alpha) { return x > 0.f ? x : alpha * x; }
 
-// softmax row i over j into att[0..n) (one wave); returns nothing, writes LDS
-__device__ __forceinline__ void gat_row(int i, int n, int mode, const float* lab, const float* ss,
-                                        const float* ts, float alpha, float* att, int lane) {
-  const float si = ss[i];
-  float m = -INFINITY;
-  for (int j = lane; j < n; j += 64) {
-    if (gat_edge(mode, lab, i, j)) m = fmaxf(m, lrelu(si + ts[j], alpha));
-  }
-  m = wave_max(m);
-  float sum = 0.f;
-  for (int j = lane; j < n; j += 64) {
-    float p = 0.f;
-    if (gat_edge(mode, lab, i, j)) p = expf(lrelu(si + ts[j], alpha) - m);
-    att[j] = p;
-    sum += p;
-  }
-  sum = wave_sum(sum);
-  const float inv = 1.f / sum;
-  for (int j = lane; j < n; j += 64) att[j] *= inv;
-}
+// LDS row stride of a staged node tile: F rounded up to the 4-feature MFMA
+// k-step (the pad columns hold zeros), odd
+__host__ __device__ __forceinline__ int gat_fs(int F) { return ((F + 3) & ~3) | 1; }
+__host__ __device__ __forceinline__ int gat_r16(int n) { return (n + 15) & ~15; }
 
+// Both kernels work on 16 x 16 x 4 fp32 MFMA tiles (exact fp32 products;
+// v_mfma_f32_16x16x4_f32: A[i = lane & 15][k = lane >> 4], B[k = lane >> 4][c
+// = lane & 15], C rows 4 (lane >> 4) + v, column lane & 15).  One workgroup
+// per (segment, head); wave w takes the 16-node row blocks w, w + 4, ...
+//
+// Forward: the attention rows of a row block are built directly in the A
+// operand layout (lane = row i, k-step m = nodes 4m + (lane >> 4)), so the
+// softmax needs two cross-lane steps per reduction and the aggregation
+// att @ Wh reads only Wh (LDS) -- no attention matrix is stored.
+template <int NM>   // 4-node k-steps held per lane: segments of <= 4 NM nodes
 __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
     const float* __restrict__ Wh, int heads, const float* __restrict__ a_all, const float* __restrict__ bias,
-    const float* __restrict__ labels, const int32_t* __restrict__ seg_off, int nseg, int F, float alpha, int mode,
-    int epi, int max_seg, float* __restrict__ hp, float* __restrict__ y, int ldy) {
+    const float* __restrict__ labels, const int32_t* __restrict__ seg_off, int nseg, int nrows, int F, float alpha,
+    int mode, int epi, int max_seg, float* __restrict__ hp, float* __restrict__ y, int ldy) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int Fp = F | 1;
-  float* Ws = reinterpret_cast<float*>(smem);       // max_seg x Fp
-  float* ss = Ws + max_seg * Fp;                    // max_seg
-  float* ts = ss + max_seg;                         // max_seg
-  float* lab = ts + max_seg;                        // max_seg
-  float* att = lab + max_seg;                       // kGatWaves x max_seg
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int Fs = gat_fs(F), F4 = (F + 3) & ~3;
+  const int nmax = gat_r16(max_seg);
   const int HF = heads * F;
+  // rows past the last segment (zero-padded group buffers): zero outputs
+  for (size_t e = (size_t)seg_off[nseg] * HF + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * HF;
+       e += (size_t)gridDim.x * kGatThreads) {
+    const size_t r = e / HF, c = e - r * HF;
+    y[r * ldy + c] = 0.f;
+    if (epi) hp[e] = 0.f;
+  }
+  float* Ws = reinterpret_cast<float*>(smem);   // nmax x Fs
+  float* ss = Ws + nmax * Fs;                   // nmax
+  float* ts = ss + nmax;                        // nmax
+  float* lab = ts + nmax;                       // nmax
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int nct = (F + 15) >> 4;
   for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
     const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
     const int n = seg_off[g + 1] - o;
+    if (n <= 0) continue;
     const float* a = a_all + 2 * F * hd;
     const int c0 = hd * F;
-    for (int q = threadIdx.x; q < n * F; q += blockDim.x) {
-      const int r = q / F, f = q - r * F;
-      Ws[r * Fp + f] = Wh[(size_t)(o + r) * HF + c0 + f];
+    const int nr = gat_r16(n);
+    for (int e = threadIdx.x; e < nr * F4; e += kGatThreads) {
+      const int r = e / F4, f = e - r * F4;
+      Ws[r * Fs + f] = (r < n && f < F) ? Wh[(size_t)(o + r) * HF + c0 + f] : 0.f;
     }
     __syncthreads();
-    for (int r = threadIdx.x; r < n; r += blockDim.x) {
+    for (int r = threadIdx.x; r < nr; r += kGatThreads) {
       float s = 0.f, t = 0.f;
       for (int f = 0; f < F; ++f) {
-        const float w = Ws[r * Fp + f];
+        const float w = Ws[r * Fs + f];
         s = fmaf(w, a[f], s);
         t = fmaf(w, a[F + f], t);
       }
       ss[r] = s;
       ts[r] = t;
-      lab[r] = mode == 0 ? labels[o + r] : 0.f;
+      lab[r] = (mode == 0 && r < n) ? labels[o + r] : 0.f;
     }
     __syncthreads();
-    float* arow = att + wave * max_seg;
-    for (int i = wave; i < n; i += kGatWaves) {
-      gat_row(i, n, mode, lab, ss, ts, alpha, arow, lane);
-      // the att row is written and read by this wave only: order its LDS
-      // writes before the cross-lane reads below
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // aggregate: lanes over features
-      float hv[2], zv[2];
-      float zmax = -INFINITY;
+    const int nm = nr >> 2;
+    for (int rb = wave; 16 * rb < n; rb += kGatWaves) {
+      const int i = 16 * rb + r16;
+      const bool iv = i < n;
+      const float si = ss[i], li = lab[i];
+      float p[NM];
+      float mx = -INFINITY;
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int f = lane + 64 * c;
-        float acc = 0.f;
-        if (f < F) {
-          for (int j = 0; j < n; ++j) acc = fmaf(arow[j], Ws[j * Fp + f], acc);
-          if (bias) acc += bias[f];
+      for (int m = 0; m < NM; ++m) {
+        p[m] = -INFINITY;
+        if (m < nm) {
+          const int j = 4 * m + q;
+          const bool edge = iv && j < n && (mode == 1 || i == j || (li != 0.f && li == lab[j]));
+          if (edge) {
+            p[m] = lrelu(si + ts[j], alpha);
+            mx = fmaxf(mx, p[m]);
+          }
         }
-        hv[c] = acc;
-        zv[c] = epi ? elu(acc) : acc;
-        if (f < F) zmax = fmaxf(zmax, zv[c]);
       }
-      float lse = 0.f;
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      float sum = 0.f;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const float e = p[m] == -INFINITY ? 0.f : expf(p[m] - mx);
+        p[m] = e;
+        sum += e;
+      }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      const float inv = iv ? 1.f / sum : 0.f;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) p[m] *= inv;
+      // out = att @ Wh (+ bias), 16-feature column tiles
+      floatx4 hv[8];
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        hv[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (ct < nct) {
+          const int fb = min(16 * ct + r16, F - 1);
+#pragma unroll
+          for (int m = 0; m < NM; ++m)
+            if (m < nm) hv[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[m], Ws[(4 * m + q) * Fs + fb], hv[ct], 0, 0, 0);
+          const float bv = (bias && 16 * ct + r16 < F) ? bias[16 * ct + r16] : 0.f;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) hv[ct][v] += bv;
+        }
+      }
+      // epilogue per output row 16 rb + 4 q + v, feature 16 ct + r16
+      float lse[4] = {0.f, 0.f, 0.f, 0.f};
       if (epi == 2) {
-        zmax = wave_max(zmax);
-        float se = 0.f;
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-          if (lane + 64 * c < F) se += expf(zv[c] - zmax);
-        se = wave_sum(se);
-        lse = zmax + logf(se);
+        for (int v = 0; v < 4; ++v) {
+          float zm = -INFINITY;
+#pragma unroll
+          for (int ct = 0; ct < 8; ++ct)
+            if (ct < nct && 16 * ct + r16 < F) zm = fmaxf(zm, elu(hv[ct][v]));
+#pragma unroll
+          for (int o2 = 1; o2 < 16; o2 <<= 1) zm = fmaxf(zm, __shfl_xor(zm, o2));
+          float se = 0.f;
+#pragma unroll
+          for (int ct = 0; ct < 8; ++ct)
+            if (ct < nct && 16 * ct + r16 < F) se += expf(elu(hv[ct][v]) - zm);
+#pragma unroll
+          for (int o2 = 1; o2 < 16; o2 <<= 1) se += __shfl_xor(se, o2);
+          lse[v] = zm + logf(se);
+        }
       }
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int f = lane + 64 * c;
-        if (f < F) {
-          if (epi) hp[(size_t)(o + i) * HF + c0 + f] = hv[c];
-          y[(size_t)(o + i) * ldy + c0 + f] = epi == 2 ? zv[c] - lse : zv[c];
+      for (int ct = 0; ct < 8; ++ct) {
+        const int f = 16 * ct + r16;
+        if (ct < nct && f < F) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int io = 16 * rb + 4 * q + v;
+            if (io < n) {
+              const float h = hv[ct][v];
+              const float z = epi ? elu(h) : h;
+              if (epi) hp[(size_t)(o + io) * HF + c0 + f] = h;
+              y[(size_t)(o + io) * ldy + c0 + f] = epi == 2 ? z - lse[v] : z;
+            }
+          }
         }
       }
     }
@@ -134,139 +176,221 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
   }
 }
 
+// Backward.  Per row block (in the C layout: lane = column j, rows 4 (lane >>
+// 4) + v): the attention recomputed, datt = dhp @ Wh^T on MFMA, the softmax
+// and LeakyReLU backward to dz, its row sums (ds) and per-block column sums
+// (dt, summed over the blocks in order afterwards); the attention goes to LDS
+// for dWh = att^T @ dhp (MFMA over the rows) + ds a_src + dt a_dst.
+template <int NJT>  // 16-node column tiles: segments of <= 16 NJT nodes
 __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
     const float* __restrict__ Wh, int heads, const float* __restrict__ a_all, const float* __restrict__ labels,
-    const int32_t* __restrict__ seg_off, int nseg, int F, float alpha, int mode, int epi, int max_seg,
+    const int32_t* __restrict__ seg_off, int nseg, int nrows, int F, float alpha, int mode, int epi, int max_seg,
     const float* __restrict__ hp, const float* __restrict__ y, const float* __restrict__ dy, int lddy,
     float* __restrict__ dWh, float* __restrict__ ds_out, float* __restrict__ dt_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int Fp = F | 1;
-  const int Np = max_seg | 1;
-  float* Ws = reinterpret_cast<float*>(smem);  // max_seg x Fp
-  float* Ds = Ws + max_seg * Fp;               // max_seg x Fp  (d hp)
-  float* At = Ds + max_seg * Fp;               // max_seg x Np  (att, then dz)
-  float* ss = At + max_seg * Np;
-  float* ts = ss + max_seg;
-  float* lab = ts + max_seg;
-  float* dss = lab + max_seg;
-  float* dts = dss + max_seg;
+  {  // rows past the last segment: zero gradients
+    const size_t r0 = seg_off[nseg], w = (size_t)heads * (F + 2);
+    for (size_t e = r0 * w + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * w;
+         e += (size_t)gridDim.x * kGatThreads) {
+      const size_t r = e / w, c = e - r * w;
+      if (c < (size_t)heads * F) dWh[r * heads * F + c] = 0.f;
+      else if (c < (size_t)heads * (F + 1)) ds_out[r * heads + c - (size_t)heads * F] = 0.f;
+      else dt_out[r * heads + c - (size_t)heads * (F + 1)] = 0.f;
+    }
+  }
+  const int Fs = gat_fs(F), F4 = (F + 3) & ~3;
+  const int nmax = gat_r16(max_seg), Na = nmax + 4;
+  float* Ws = reinterpret_cast<float*>(smem);  // nmax x Fs
+  float* Ds = Ws + nmax * Fs;                  // nmax x Fs  (d hp)
+  float* At = Ds + nmax * Fs;                  // nmax x Na  (att)
+  float* ss = At + nmax * Na;
+  float* ts = ss + nmax;
+  float* lab = ts + nmax;
+  float* dss = lab + nmax;
+  float* dts = dss + nmax;
+  float* rsum = dts + nmax;                    // epilogue 2: row sums of dy
+  float* dtp = rsum + nmax;                    // (nmax / 16) x nmax column partials of dz
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
   const int HF = heads * F;
+  const int nct = (F + 15) >> 4;
   for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
     const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
     const int n = seg_off[g + 1] - o;
+    if (n <= 0) continue;
     const float* a = a_all + 2 * F * hd;
     const int c0 = hd * F;
-    for (int q = threadIdx.x; q < n * F; q += blockDim.x) {
-      const int r = q / F, f = q - r * F;
-      Ws[r * Fp + f] = Wh[(size_t)(o + r) * HF + c0 + f];
+    const int nr = gat_r16(n), nrb = nr >> 4;
+    for (int e = threadIdx.x; e < nr * F4; e += kGatThreads) {
+      const int r = e / F4, f = e - r * F4;
+      float w = 0.f, d = 0.f;
+      if (r < n && f < F) {
+        const size_t row = (size_t)(o + r);
+        w = Wh[row * HF + c0 + f];
+        d = dy[row * lddy + c0 + f];
+        if (epi == 1) d *= elu_grad(hp[row * HF + c0 + f]);
+      }
+      Ws[r * Fs + f] = w;
+      Ds[r * Fs + f] = d;
     }
     __syncthreads();
-    for (int r = threadIdx.x; r < n; r += blockDim.x) {
-      float s = 0.f, t = 0.f;
+    for (int r = threadIdx.x; r < nr; r += kGatThreads) {
+      float s = 0.f, t = 0.f, sd = 0.f;
       for (int f = 0; f < F; ++f) {
-        const float w = Ws[r * Fp + f];
+        const float w = Ws[r * Fs + f];
         s = fmaf(w, a[f], s);
         t = fmaf(w, a[F + f], t);
+        sd += Ds[r * Fs + f];
       }
       ss[r] = s;
       ts[r] = t;
-      lab[r] = mode == 0 ? labels[o + r] : 0.f;
+      rsum[r] = sd;
+      lab[r] = (mode == 0 && r < n) ? labels[o + r] : 0.f;
     }
-    // d hp through the epilogue, one wave per row
-    for (int i = wave; i < n; i += kGatWaves) {
-      float d[2], h[2], sm[2];
-      float sdy = 0.f;
+    __syncthreads();
+    if (epi == 2) {   // d hp = (dy - softmax(y) sum(dy)) * ELU'(hp)
+      for (int e = threadIdx.x; e < n * F; e += kGatThreads) {
+        const int r = e / F, f = e - r * F;
+        const size_t row = (size_t)(o + r);
+        Ds[r * Fs + f] = (Ds[r * Fs + f] - expf(y[row * F + f]) * rsum[r]) * elu_grad(hp[row * HF + c0 + f]);
+      }
+      __syncthreads();
+    }
+    for (int rb = wave; rb < nrb; rb += kGatWaves) {
+      float sv[4], lv[4];
+      bool iv[4];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int f = lane + 64 * c;
-        d[c] = 0.f; h[c] = 0.f; sm[c] = 0.f;
-        if (f < F) {
-          d[c] = dy[(size_t)(o + i) * lddy + c0 + f];
-          if (epi) h[c] = hp[(size_t)(o + i) * HF + c0 + f];
-          if (epi == 2) sm[c] = expf(y[(size_t)(o + i) * F + f]);
-          sdy += d[c];
+      for (int v = 0; v < 4; ++v) {
+        const int i = 16 * rb + 4 * q + v;
+        iv[v] = i < n;
+        sv[v] = ss[i];
+        lv[v] = lab[i];
+      }
+      float tj[NJT], att[NJT][4];
+      float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        const int j = 16 * jt + r16;
+        const bool jv = jt < nrb && j < n;
+        tj[jt] = jt < nrb ? ts[j] : 0.f;
+        const float lj = jt < nrb ? lab[j] : 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int i = 16 * rb + 4 * q + v;
+          const bool edge = jv && iv[v] && (mode == 1 || i == j || (lv[v] != 0.f && lv[v] == lj));
+          att[jt][v] = edge ? lrelu(sv[v] + tj[jt], alpha) : -INFINITY;
+          mx[v] = fmaxf(mx[v], att[jt][v]);
         }
       }
-      if (epi == 2) sdy = wave_sum(sdy);
+      float inv[4];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int f = lane + 64 * c;
-        if (f < F) {
-          float v = d[c];
-          if (epi == 2) v = v - sm[c] * sdy;
-          if (epi) v *= elu_grad(h[c]);
-          Ds[i * Fp + f] = v;
+      for (int v = 0; v < 4; ++v) {
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) mx[v] = fmaxf(mx[v], __shfl_xor(mx[v], o2));
+        float sum = 0.f;
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt) {
+          const float e = att[jt][v] == -INFINITY ? 0.f : expf(att[jt][v] - mx[v]);
+          att[jt][v] = e;
+          sum += e;
         }
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) sum += __shfl_xor(sum, o2);
+        inv[v] = iv[v] ? 1.f / sum : 0.f;
+      }
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) att[jt][v] *= inv[v];
+      // datt_ij = dhp_i . Wh_j
+      floatx4 da[NJT];
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) da[jt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      const float* Dr = Ds + (16 * rb + r16) * Fs + q;
+      for (int k = 0; k < F4; k += 4) {
+        const float av = Dr[k];
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt)
+          if (jt < nrb) da[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Ws[(16 * jt + r16) * Fs + k + q], da[jt], 0, 0, 0);
+      }
+      float dot[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dot[v] = fmaf(att[jt][v], da[jt][v], dot[v]);
+      float dsr[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) dot[v] += __shfl_xor(dot[v], o2);
+        dsr[v] = 0.f;
+      }
+#pragma unroll
+      for (int jt = 0; jt < NJT; ++jt) {
+        if (jt < nrb) {
+          float cp = 0.f;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const float de = att[jt][v] * (da[jt][v] - dot[v]);
+            const float dz = (sv[v] + tj[jt]) > 0.f ? de : alpha * de;
+            dsr[v] += dz;
+            cp += dz;
+            At[(16 * rb + 4 * q + v) * Na + 16 * jt + r16] = att[jt][v];
+          }
+          cp += __shfl_xor(cp, 16);
+          cp += __shfl_xor(cp, 32);
+          if (q == 0) dtp[rb * nmax + 16 * jt + r16] = cp;
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) dsr[v] += __shfl_xor(dsr[v], o2);
+        if (r16 == 0) dss[16 * rb + 4 * q + v] = dsr[v];
       }
     }
     __syncthreads();
-    for (int i = wave; i < n; i += kGatWaves) gat_row(i, n, mode, lab, ss, ts, alpha, At + i * Np, lane);
-    __syncthreads();
-    // dWh_j (attention-weighted part) = sum_i att_ij dhp_i
-    for (int q = threadIdx.x; q < n * F; q += blockDim.x) {
-      const int j = q / F, f = q - j * F;
+    for (int j = threadIdx.x; j < nr; j += kGatThreads) {
       float acc = 0.f;
-      for (int i = 0; i < n; ++i) acc = fmaf(At[i * Np + j], Ds[i * Fp + f], acc);
-      dWh[(size_t)(o + j) * HF + c0 + f] = acc;
-    }
-    __syncthreads();
-    // per row: datt_ij = dhp_i . Wh_j ; softmax + LeakyReLU backward -> dz (in place of att)
-    for (int i = wave; i < n; i += kGatWaves) {
-      float* arow = At + i * Np;
-      const float si = ss[i];
-      float dot = 0.f;
-      float datt[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = lane + 64 * c;
-        datt[c] = 0.f;
-        if (j < n) {
-          float acc = 0.f;
-          for (int f = 0; f < F; ++f) acc = fmaf(Ds[i * Fp + f], Ws[j * Fp + f], acc);
-          datt[c] = acc;
-          dot = fmaf(arow[j], acc, dot);
-        }
-      }
-      dot = wave_sum(dot);
-      float dsum = 0.f;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = lane + 64 * c;
-        if (j < n) {
-          const float at = arow[j];
-          const float de = at * (datt[c] - dot);
-          const float dz = (si + ts[j]) > 0.f ? de : alpha * de;
-          arow[j] = dz;
-          dsum += dz;
-        }
-      }
-      dsum = wave_sum(dsum);
-      if (lane == 0) dss[i] = dsum;
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      float acc = 0.f;
-      for (int i = 0; i < n; ++i) acc += At[i * Np + j];
+      for (int rb = 0; rb < nrb; ++rb) acc += dtp[rb * nmax + j];
       dts[j] = acc;
-      ds_out[(size_t)(o + j) * heads + hd] = dss[j];
-      dt_out[(size_t)(o + j) * heads + hd] = acc;
+      if (j < n) {
+        ds_out[(size_t)(o + j) * heads + hd] = dss[j];
+        dt_out[(size_t)(o + j) * heads + hd] = acc;
+      }
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < n * F; q += blockDim.x) {
-      const int j = q / F, f = q - j * F;
-      dWh[(size_t)(o + j) * HF + c0 + f] += dss[j] * a[f] + dts[j] * a[F + f];
+    // dWh_j = sum_i att_ij dhp_i + ds_j a_src + dt_j a_dst
+    for (int jb = wave; jb < nrb; jb += kGatWaves) {
+      for (int ct = 0; ct < nct; ++ct) {
+        const int fb = min(16 * ct + r16, F - 1);
+        floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int m = 0; m < nr; m += 4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(At[(m + q) * Na + 16 * jb + r16], Ds[(m + q) * Fs + fb], acc, 0,
+                                                     0, 0);
+        const int f = 16 * ct + r16;
+        if (f < F) {
+          const float as = a[f], ad = a[F + f];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int j = 16 * jb + 4 * q + v;
+            if (j < n) dWh[(size_t)(o + j) * HF + c0 + f] = acc[v] + (dss[j] * as + dts[j] * ad);
+          }
+        }
+      }
     }
-    __syncthreads();
+    __syncthreads();  // LDS reused by the next segment
   }
 }
 
 static size_t gat_fwd_lds(int F, int max_seg) {
-  return sizeof(float) * ((size_t)max_seg * (F | 1) + 3 * (size_t)max_seg + (size_t)kGatWaves * max_seg) + 16;
+  const size_t nm = gat_r16(max_seg);
+  return sizeof(float) * (nm * gat_fs(F) + 3 * nm) + 16;
 }
 static size_t gat_bwd_lds(int F, int max_seg) {
-  return sizeof(float) * (2 * (size_t)max_seg * (F | 1) + (size_t)max_seg * (max_seg | 1) + 5 * (size_t)max_seg) + 16;
+  const size_t nm = gat_r16(max_seg);
+  return sizeof(float) * (2 * nm * gat_fs(F) + nm * (nm + 4) + 6 * nm + (nm / 16) * nm) + 16;
 }
 
 }  // namespace sgg
@@ -302,9 +426,9 @@ extern "C" int sgg_gat_fwd(const float* Wh, int heads, const float* a, const flo
   SGG_CHECK_ARG(ldy >= heads * F, "sgg_gat_fwd: ldy < heads * F");
   SGG_CHECK_ARG(epilogue != 2 || ldy == F, "sgg_gat_fwd: log_softmax epilogue needs a dense y (ldy == F)");
   if (nseg == 0) return 0;
-  hipLaunchKernelGGL(gat_fwd_kernel, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), gat_fwd_lds(F, max_seg),
-                     (hipStream_t)stream, Wh, heads, a, bias, labels, seg_off, nseg, F, alpha, mask_mode, epilogue,
-                     max_seg, hp, y, ldy);
+  auto k = max_seg <= 32 ? gat_fwd_kernel<8> : max_seg <= 64 ? gat_fwd_kernel<16> : gat_fwd_kernel<32>;
+  hipLaunchKernelGGL(k, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), gat_fwd_lds(F, max_seg), (hipStream_t)stream,
+                     Wh, heads, a, bias, labels, seg_off, nseg, n, F, alpha, mask_mode, epilogue, max_seg, hp, y, ldy);
   SGG_RETURN_LAUNCH("sgg_gat_fwd");
 }
 
@@ -321,8 +445,8 @@ extern "C" int sgg_gat_bwd(const float* Wh, int heads, const float* a, const flo
   if (nseg == 0) return 0;
   const size_t lds = gat_bwd_lds(F, max_seg);
   SGG_CHECK_ARG(lds <= 160 * 1024, "sgg_gat_bwd: segment %d x F %d needs %zu B of LDS", max_seg, F, lds);
-  hipLaunchKernelGGL(gat_bwd_kernel, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), lds, (hipStream_t)stream, Wh,
-                     heads, a, labels, seg_off, nseg, F, alpha, mask_mode, epilogue, max_seg, hp, y, dy, lddy, dWh,
-                     ds, dt);
+  auto k = max_seg <= 32 ? gat_bwd_kernel<2> : max_seg <= 64 ? gat_bwd_kernel<4> : gat_bwd_kernel<8>;
+  hipLaunchKernelGGL(k, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), lds, (hipStream_t)stream, Wh, heads, a,
+                     labels, seg_off, nseg, n, F, alpha, mask_mode, epilogue, max_seg, hp, y, dy, lddy, dWh, ds, dt);
   SGG_RETURN_LAUNCH("sgg_gat_bwd");
 }

@@ -1406,10 +1406,9 @@ class _GatAttn(torch.autograd.Function):
         a = a.contiguous().view(-1)
         if bias is not None:
             bias = bias.contiguous()
-        # the complete-graph mode runs over zero-padded group buffers whose
-        # pad rows no segment covers: keep them zero for the reductions after
-        alloc = torch.zeros if mode == 1 else torch.empty
-        y = alloc(n, HF, device=wh.device, dtype=torch.float32)
+        # (rows past the last segment -- the zero-padded group buffers of the
+        # complete-graph mode -- are written zero by the kernel)
+        y = torch.empty(n, HF, device=wh.device, dtype=torch.float32)
         hp = torch.empty(n, HF, device=wh.device, dtype=torch.float32) if epi else None
         N.check(lib.sgg_gat_fwd(N.ptr(wh), heads, N.ptr(a), N.ptr(bias), N.ptr(labels), N.ptr(seg_off), nseg, n, F,
                                 float(alpha), mode, epi, max_seg, N.ptr(hp), N.ptr(y), HF, N.stream_ptr()),
@@ -1426,10 +1425,9 @@ class _GatAttn(torch.autograd.Function):
         n, HF = wh.shape
         F = HF // heads
         dy = dy.contiguous()
-        alloc = torch.zeros if mode == 1 else torch.empty
-        dWh = alloc(n, HF, device=wh.device, dtype=torch.float32)
-        ds = alloc(n, heads, device=wh.device, dtype=torch.float32)
-        dt = alloc(n, heads, device=wh.device, dtype=torch.float32)
+        dWh = torch.empty(n, HF, device=wh.device, dtype=torch.float32)
+        ds = torch.empty(n, heads, device=wh.device, dtype=torch.float32)
+        dt = torch.empty(n, heads, device=wh.device, dtype=torch.float32)
         N.check(lib.sgg_gat_bwd(N.ptr(wh), heads, N.ptr(a), N.ptr(labels), N.ptr(seg_off), nseg, n, F, alpha, mode,
                                 epi, max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), HF, N.ptr(dWh), N.ptr(ds), N.ptr(dt),
                                 N.stream_ptr()), "sgg_gat_bwd")

@@ -181,7 +181,8 @@ int sgg_pool_bwd(const float* U, const float* pos, const float* A, const float* 
  * group GAT write straight into their concat slot, models.py:234); hp
  * (n x heads*F, pre-epilogue, bias included) is written when epilogue != 0
  * (needed by the backward).  Epilogue 2 requires heads == 1 and ldy == F.
- * Segments larger than SGG_GAT_MAX_NODES are rejected.
+ * Rows [seg_off[nseg], n) (zero-padded group buffers no segment covers)
+ * get zero y / hp.  Segments larger than SGG_GAT_MAX_NODES are rejected.
  */
 int sgg_gat_fwd(const float* Wh, int heads, const float* a, const float* bias, const float* labels,
                 const int32_t* seg_off, int nseg, int n, int F, float alpha, int mask_mode,
@@ -190,7 +191,8 @@ int sgg_gat_fwd(const float* Wh, int heads, const float* a, const float* bias, c
 /* Backward of sgg_gat_fwd (bias excluded: its gradient is the column sum of
  * the pre-epilogue gradient, formed by the caller).  dy: head h at columns
  * [hF, hF + F) of row stride lddy; y / hp as written by the forward.  Writes
- * dWh (n x heads*F) and ds, dt (n x heads): the caller finishes
+ * dWh (n x heads*F) and ds, dt (n x heads), zero on the rows past the last
+ * segment; the caller finishes
  * da_h = [Wh_h^T ds_h ; Wh_h^T dt_h], dX = dWh W^T, dW = X^T dWh. */
 int sgg_gat_bwd(const float* Wh, int heads, const float* a, const float* labels, const int32_t* seg_off,
                 int nseg, int n, int F, float alpha, int mask_mode, int epilogue, int max_seg,

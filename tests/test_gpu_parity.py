@@ -1735,3 +1735,92 @@ def test_pool_backward_one_launch_equals_two(bn, H, sizes):
     assert torch.equal(da, db), "dh"
     for k in ga:
         assert torch.equal(ga[k], gb[k]), "d" + k
+
+
+def _gat_attention_ref(wh, a, bias, labels, seg_off, mode, epi, heads, alpha=0.2):
+    """fp64 torch restatement of the attention layer (models.py:184-220, the
+    multi-head GAT.py:6-55 text): per segment and head, masked softmax of
+    LeakyReLU(s_i + t_j), att @ Wh + bias, then the epilogue."""
+    n, HF = wh.shape
+    F = HF // heads
+    y = torch.zeros(n, HF, dtype=torch.float64, device=wh.device)
+    ys = []
+    so = seg_off.tolist()
+    for g in range(len(so) - 1):
+        o, e = so[g], so[g + 1]
+        if e == o:
+            continue
+        cols = []
+        for h in range(heads):
+            W = wh[o:e, h * F:(h + 1) * F]
+            s = W @ a[h, :F]
+            t = W @ a[h, F:]
+            z = torch.nn.functional.leaky_relu(s[:, None] + t[None, :], alpha)
+            if mode == 0:
+                lab = labels[o:e].view(-1)
+                m = (lab[:, None] == lab[None, :]) & (lab[:, None] != 0)
+                m = m | torch.eye(e - o, dtype=torch.bool, device=wh.device)
+                z = z.masked_fill(~m, float("-inf"))
+            out = torch.softmax(z, 1) @ W
+            if bias is not None:
+                out = out + bias
+            if epi:
+                out = torch.nn.functional.elu(out)
+            if epi == 2:
+                out = torch.log_softmax(out, 1)
+            cols.append(out)
+        ys.append((o, e, torch.cat(cols, 1)))
+    for o, e, v in ys:
+        y = torch.cat([y[:o], v, y[e:]], 0)
+    return y
+
+
+@pytest.mark.parametrize("heads,F,sizes,mode,epi,use_bias,pad", [
+    (4, 16, [64] * 9, 1, 1, True, 0),           # configs[4] batched GAT, layer 1
+    (1, 40, [64] * 9, 1, 0, True, 0),           # layer 2
+    (4, 16, [20, 1, 64, 7, 33], 1, 1, True, 3),  # ragged, pad rows past the last segment
+    (1, 16, [20, 7, 1, 33, 5], 0, 1, False, 0),  # GAT family layer 1, label mask
+    (1, 40, [5, 20, 64, 3], 0, 2, False, 0),     # layer 2: log_softmax epilogue
+    (2, 17, [100, 128, 9], 0, 1, False, 0),      # > 64 nodes, F not a multiple of 4
+    (1, 128, [30, 2], 1, 0, True, 0),            # widest F
+    (3, 1, [12, 40], 1, 1, True, 0),             # F = 1
+])
+def test_gat_attention_vs_torch(heads, F, sizes, mode, epi, use_bias, pad):
+    """sgg_gat_fwd / sgg_gat_bwd (MFMA tiles) against an fp64 torch
+    restatement: the output, and the gradients of Wh, a and the bias through
+    the kernel's dWh / ds / dt; pad rows past the last segment stay zero."""
+    from sgan import kernels as K
+    torch.manual_seed(heads * 100 + F)
+    n_seg = sum(sizes)
+    n = n_seg + pad
+    seg_off = torch.tensor(np.concatenate([[0], np.cumsum(sizes)]), dtype=torch.int32, device=DEV)
+    labels = None
+    if mode == 0:
+        rs = np.random.RandomState(F)
+        labels = torch.from_numpy(rs.randint(0, 4, n).astype(np.float32)).to(DEV).view(-1, 1)
+    graph = K.SegmentGraph(seg_off, len(sizes), max(sizes), mode, labels)
+    wh = torch.randn(n, heads * F, device=DEV)
+    if pad:
+        wh[n_seg:] = 0
+    a = torch.randn(heads, 2 * F, device=DEV) * 0.5
+    bias = torch.randn(F, device=DEV) * 0.1 if use_bias else None
+    dy = torch.randn(n, heads * F, device=DEV)
+    dy[n_seg:] = 0      # pad rows are read by no consumer
+    whg = wh.clone().requires_grad_(True)
+    ag = a.clone().requires_grad_(True)
+    bg = bias.clone().requires_grad_(True) if use_bias else None
+    y = K.gat_attention(whg, ag, 0.2, graph, epi, heads=heads, bias=bg)
+    (y * dy).sum().backward()
+    wr = wh.double().requires_grad_(True)
+    ar = a.double().requires_grad_(True)
+    br = bias.double().requires_grad_(True) if use_bias else None
+    yr = _gat_attention_ref(wr, ar, br, labels, seg_off, mode, epi, heads)
+    (yr * dy.double()).sum().backward()
+    close(y, yr.detach().cpu().numpy(), rtol=2e-5, what="y")
+    if pad:
+        assert torch.equal(y[n_seg:], torch.zeros_like(y[n_seg:]))
+        assert torch.equal(whg.grad[n_seg:], torch.zeros_like(whg.grad[n_seg:]))
+    close(whg.grad[:n_seg], wr.grad[:n_seg].cpu().numpy(), rtol=1e-4, what="dWh")
+    close(ag.grad, ar.grad.cpu().numpy(), rtol=1e-4, what="da")
+    if use_bias:
+        close(bg.grad, br.grad.cpu().numpy(), rtol=1e-4, what="dbias")

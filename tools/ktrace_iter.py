@@ -16,7 +16,15 @@ def short(n):
 
 rows = list(csv.DictReader(open(os.path.join(sys.argv[1], "run_kernel_trace.csv"))))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "lstm_fwd_mfma" in r["Kernel_Name"]]
+def grid(r):
+    return int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
+
+
+# the rollout: the largest-grid launch of the rollout kernel (configurations
+# whose decoder also runs lstm_fwd_mfma launch it with a smaller grid)
+mark = [i for i, r in enumerate(rows) if "lstm_fwd_mfma" in r["Kernel_Name"]]
+gmax = max(grid(rows[i]) for i in mark)
+idx = [i for i in mark if grid(rows[i]) == gmax]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) // 2
 a, b = idx[k], idx[k + 1]
 t0 = int(rows[a]["Start_Timestamp"])
