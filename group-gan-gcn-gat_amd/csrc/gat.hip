@@ -41,9 +41,10 @@ __host__ __device__ __forceinline__ int gat_r16(int n) { return (n + 15) & ~15; 
 // att @ Wh reads only Wh (LDS) -- no attention matrix is stored.
 template <int NM>   // 4-node k-steps held per lane: segments of <= 4 NM nodes
 __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
-    const float* __restrict__ Wh, int heads, const float* __restrict__ a_all, const float* __restrict__ bias,
-    const float* __restrict__ labels, const int32_t* __restrict__ seg_off, int nseg, int nrows, int F, float alpha,
-    int mode, int epi, int max_seg, float* __restrict__ hp, float* __restrict__ y, int ldy) {
+    const float* __restrict__ Wh, int heads, const float* __restrict__ a_src, const float* __restrict__ a_dst, int lda,
+    const float* __restrict__ bias, const float* __restrict__ labels, const int32_t* __restrict__ seg_off, int nseg,
+    int nrows, int F, float alpha, int mode, int epi, int max_seg, float* __restrict__ hp, float* __restrict__ y,
+    int ldy) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int Fs = gat_fs(F), F4 = (F + 3) & ~3;
   const int nmax = gat_r16(max_seg);
@@ -67,7 +68,8 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
     const int o = seg_off[g];
     const int n = seg_off[g + 1] - o;
     if (n <= 0) continue;
-    const float* a = a_all + 2 * F * hd;
+    const float* as = a_src + (size_t)lda * hd;
+    const float* ad = a_dst + (size_t)lda * hd;
     const int c0 = hd * F;
     const int nr = gat_r16(n);
     for (int e = threadIdx.x; e < nr * F4; e += kGatThreads) {
@@ -79,8 +81,8 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
       float s = 0.f, t = 0.f;
       for (int f = 0; f < F; ++f) {
         const float w = Ws[r * Fs + f];
-        s = fmaf(w, a[f], s);
-        t = fmaf(w, a[F + f], t);
+        s = fmaf(w, as[f], s);
+        t = fmaf(w, ad[f], t);
       }
       ss[r] = s;
       ts[r] = t;
@@ -181,12 +183,18 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
 // and LeakyReLU backward to dz, its row sums (ds) and per-block column sums
 // (dt, summed over the blocks in order afterwards); the attention goes to LDS
 // for dWh = att^T @ dhp (MFMA over the rows) + ds a_src + dt a_dst.
+// With the slabs (sgg_gat_bwd_ex) each (segment, head) also writes its
+// partials of the parameter gradients: da_src = Wh^T ds, da_dst = Wh^T dt
+// (pda, 2F floats) and the bias gradient's column sums of dhp (pdb, F doubles:
+// a near-cancelling sum, the next layer's instance norm removes each
+// feature's scene mean); gat_param_reduce_kernel sums them in a fixed order.
 template <int NJT>  // 16-node column tiles: segments of <= 16 NJT nodes
 __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
-    const float* __restrict__ Wh, int heads, const float* __restrict__ a_all, const float* __restrict__ labels,
-    const int32_t* __restrict__ seg_off, int nseg, int nrows, int F, float alpha, int mode, int epi, int max_seg,
-    const float* __restrict__ hp, const float* __restrict__ y, const float* __restrict__ dy, int lddy,
-    float* __restrict__ dWh, float* __restrict__ ds_out, float* __restrict__ dt_out) {
+    const float* __restrict__ Wh, int heads, const float* __restrict__ a_src, const float* __restrict__ a_dst, int lda,
+    const float* __restrict__ labels, const int32_t* __restrict__ seg_off, int nseg, int nrows, int F, float alpha,
+    int mode, int epi, int max_seg, const float* __restrict__ hp, const float* __restrict__ y,
+    const float* __restrict__ dy, int lddy, float* __restrict__ dWh, float* __restrict__ ds_out,
+    float* __restrict__ dt_out, float* __restrict__ pda, double* __restrict__ pdb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   {  // rows past the last segment: zero gradients
     const size_t r0 = seg_off[nseg], w = (size_t)heads * (F + 2);
@@ -194,6 +202,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
          e += (size_t)gridDim.x * kGatThreads) {
       const size_t r = e / w, c = e - r * w;
       if (c < (size_t)heads * F) dWh[r * heads * F + c] = 0.f;
+      else if (!ds_out) continue;
       else if (c < (size_t)heads * (F + 1)) ds_out[r * heads + c - (size_t)heads * F] = 0.f;
       else dt_out[r * heads + c - (size_t)heads * (F + 1)] = 0.f;
     }
@@ -218,8 +227,18 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
     const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
     const int n = seg_off[g + 1] - o;
-    if (n <= 0) continue;
-    const float* a = a_all + 2 * F * hd;
+    if (n <= 0) {
+      for (int c = threadIdx.x; c < 3 * F; c += kGatThreads) {
+        if (c < 2 * F) {
+          if (pda) pda[(size_t)gh * 2 * F + c] = 0.f;
+        } else if (pdb) {
+          pdb[(size_t)gh * F + c - 2 * F] = 0.0;
+        }
+      }
+      continue;
+    }
+    const float* as = a_src + (size_t)lda * hd;
+    const float* ad = a_dst + (size_t)lda * hd;
     const int c0 = hd * F;
     const int nr = gat_r16(n), nrb = nr >> 4;
     for (int e = threadIdx.x; e < nr * F4; e += kGatThreads) {
@@ -239,8 +258,8 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
       float s = 0.f, t = 0.f, sd = 0.f;
       for (int f = 0; f < F; ++f) {
         const float w = Ws[r * Fs + f];
-        s = fmaf(w, a[f], s);
-        t = fmaf(w, a[F + f], t);
+        s = fmaf(w, as[f], s);
+        t = fmaf(w, ad[f], t);
         sd += Ds[r * Fs + f];
       }
       ss[r] = s;
@@ -355,12 +374,29 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
       float acc = 0.f;
       for (int rb = 0; rb < nrb; ++rb) acc += dtp[rb * nmax + j];
       dts[j] = acc;
-      if (j < n) {
+      if (j < n && ds_out) {
         ds_out[(size_t)(o + j) * heads + hd] = dss[j];
         dt_out[(size_t)(o + j) * heads + hd] = acc;
       }
     }
     __syncthreads();
+    // parameter-gradient partials of this (segment, head): LDS reads only
+    for (int c = threadIdx.x; c < 3 * F; c += kGatThreads) {
+      if (c < 2 * F) {
+        if (pda) {
+          const int f = c < F ? c : c - F;
+          const float* wv = c < F ? dss : dts;
+          float acc = 0.f;
+          for (int i = 0; i < n; ++i) acc = fmaf(Ws[i * Fs + f], wv[i], acc);
+          pda[(size_t)gh * 2 * F + c] = acc;
+        }
+      } else if (pdb) {
+        const int f = c - 2 * F;
+        double acc = 0.0;
+        for (int i = 0; i < n; ++i) acc += (double)Ds[i * Fs + f];
+        pdb[(size_t)gh * F + f] = acc;
+      }
+    }
     // dWh_j = sum_i att_ij dhp_i + ds_j a_src + dt_j a_dst
     for (int jb = wave; jb < nrb; jb += kGatWaves) {
       for (int ct = 0; ct < nct; ++ct) {
@@ -371,16 +407,51 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
                                                      0, 0);
         const int f = 16 * ct + r16;
         if (f < F) {
-          const float as = a[f], ad = a[F + f];
+          const float sf = as[f], df = ad[f];
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int j = 16 * jb + 4 * q + v;
-            if (j < n) dWh[(size_t)(o + j) * HF + c0 + f] = acc[v] + (dss[j] * as + dts[j] * ad);
+            if (j < n) dWh[(size_t)(o + j) * HF + c0 + f] = acc[v] + (dss[j] * sf + dts[j] * df);
           }
         }
       }
     }
     __syncthreads();  // LDS reused by the next segment
+  }
+}
+
+// da_src / da_dst (heads x F each) and dbias (F, summed over the heads) from
+// the (segment, head) partials of gat_bwd_kernel: one workgroup per output,
+// a fixed-order fp64 tree over the segments
+__global__ void __launch_bounds__(256) gat_param_reduce_kernel(const float* __restrict__ pda,
+                                                               const double* __restrict__ pdb, int nseg, int heads,
+                                                               int F, float* __restrict__ da_src,
+                                                               float* __restrict__ da_dst, float* __restrict__ dbias) {
+  __shared__ double red[256];
+  const int e = blockIdx.x, na = heads * 2 * F;
+  const int t = threadIdx.x;
+  double acc = 0.0;
+  if (e < na) {
+    const int h = e / (2 * F), c = e - h * 2 * F;
+    for (int g = t; g < nseg; g += 256) acc += (double)pda[((size_t)g * heads + h) * 2 * F + c];
+  } else {
+    const int f = e - na;
+    for (int gh = t; gh < nseg * heads; gh += 256) acc += pdb[(size_t)gh * F + f];
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (int s2 = 128; s2 > 0; s2 >>= 1) {
+    if (t < s2) red[t] += red[t + s2];
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (e < na) {
+      const int h = e / (2 * F), c = e - h * 2 * F;
+      if (c < F) da_src[h * F + c] = (float)red[0];
+      else da_dst[h * F + c - F] = (float)red[0];
+    } else {
+      dbias[e - na] = (float)red[0];
+    }
   }
 }
 
@@ -414,39 +485,93 @@ static int gat_args_ok(const char* who, const float* Wh, int heads, const float*
 
 static int gat_grid(int nseg, int heads) {
   const long long w = (long long)nseg * heads;
-  return w < 16384 ? (int)w : 16384;
+  return w < 1 ? 1 : w < 16384 ? (int)w : 16384;
+}
+
+static int gat_fwd_launch(const char* who, const float* Wh, int heads, const float* as, const float* ad, int lda,
+                          const float* bias, const float* labels, const int32_t* seg_off, int nseg, int n, int F,
+                          float alpha, int mask_mode, int epilogue, int max_seg, float* hp, float* y, int ldy,
+                          void* stream) {
+  int rc = gat_args_ok(who, Wh, heads, as, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
+  if (rc) return rc;
+  SGG_CHECK_ARG(ad, "%s: null a_dst", who);
+  SGG_CHECK_ARG(y && (epilogue == 0 || hp), "%s: null output", who);
+  SGG_CHECK_ARG(ldy >= heads * F, "%s: ldy < heads * F", who);
+  SGG_CHECK_ARG(epilogue != 2 || ldy == F, "%s: log_softmax epilogue needs a dense y (ldy == F)", who);
+  if (nseg == 0 && n == 0) return 0;   // (rows but no segments: the kernel zeroes the rows)
+  auto k = max_seg <= 32 ? gat_fwd_kernel<8> : max_seg <= 64 ? gat_fwd_kernel<16> : gat_fwd_kernel<32>;
+  hipLaunchKernelGGL(k, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), gat_fwd_lds(F, max_seg), (hipStream_t)stream,
+                     Wh, heads, as, ad, lda, bias, labels, seg_off, nseg, n, F, alpha, mask_mode, epilogue, max_seg,
+                     hp, y, ldy);
+  SGG_RETURN_LAUNCH(who);
+}
+
+static int gat_bwd_launch(const char* who, const float* Wh, int heads, const float* as, const float* ad, int lda,
+                          const float* labels, const int32_t* seg_off, int nseg, int n, int F, float alpha,
+                          int mask_mode, int epilogue, int max_seg, const float* hp, const float* y, const float* dy,
+                          int lddy, float* dWh, float* ds, float* dt, float* pda, double* pdb, void* stream) {
+  int rc = gat_args_ok(who, Wh, heads, as, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
+  if (rc) return rc;
+  SGG_CHECK_ARG(ad && dy && dWh, "%s: null pointer", who);
+  SGG_CHECK_ARG(epilogue == 0 || hp, "%s: epilogue needs hp", who);
+  SGG_CHECK_ARG(epilogue != 2 || y, "%s: log_softmax epilogue needs y", who);
+  SGG_CHECK_ARG(lddy >= heads * F, "%s: lddy < heads * F", who);
+  if (nseg == 0 && n == 0) return 0;
+  const size_t lds = gat_bwd_lds(F, max_seg);
+  SGG_CHECK_ARG(lds <= 160 * 1024, "%s: segment %d x F %d needs %zu B of LDS", who, max_seg, F, lds);
+  auto k = max_seg <= 32 ? gat_bwd_kernel<2> : max_seg <= 64 ? gat_bwd_kernel<4> : gat_bwd_kernel<8>;
+  hipLaunchKernelGGL(k, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), lds, (hipStream_t)stream, Wh, heads, as, ad,
+                     lda, labels, seg_off, nseg, n, F, alpha, mask_mode, epilogue, max_seg, hp, y, dy, lddy, dWh, ds,
+                     dt, pda, pdb);
+  SGG_RETURN_LAUNCH(who);
 }
 
 extern "C" int sgg_gat_fwd(const float* Wh, int heads, const float* a, const float* bias, const float* labels,
                            const int32_t* seg_off, int nseg, int n, int F, float alpha, int mask_mode, int epilogue,
                            int max_seg, float* hp, float* y, int ldy, void* stream) {
-  int rc = gat_args_ok("sgg_gat_fwd", Wh, heads, a, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
-  if (rc) return rc;
-  SGG_CHECK_ARG(y && (epilogue == 0 || hp), "sgg_gat_fwd: null output");
-  SGG_CHECK_ARG(ldy >= heads * F, "sgg_gat_fwd: ldy < heads * F");
-  SGG_CHECK_ARG(epilogue != 2 || ldy == F, "sgg_gat_fwd: log_softmax epilogue needs a dense y (ldy == F)");
-  if (nseg == 0) return 0;
-  auto k = max_seg <= 32 ? gat_fwd_kernel<8> : max_seg <= 64 ? gat_fwd_kernel<16> : gat_fwd_kernel<32>;
-  hipLaunchKernelGGL(k, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), gat_fwd_lds(F, max_seg), (hipStream_t)stream,
-                     Wh, heads, a, bias, labels, seg_off, nseg, n, F, alpha, mask_mode, epilogue, max_seg, hp, y, ldy);
-  SGG_RETURN_LAUNCH("sgg_gat_fwd");
+  return gat_fwd_launch("sgg_gat_fwd", Wh, heads, a, a ? a + F : nullptr, 2 * F, bias, labels, seg_off, nseg, n, F,
+                        alpha, mask_mode, epilogue, max_seg, hp, y, ldy, stream);
 }
 
 extern "C" int sgg_gat_bwd(const float* Wh, int heads, const float* a, const float* labels, const int32_t* seg_off,
                            int nseg, int n, int F, float alpha, int mask_mode, int epilogue, int max_seg,
                            const float* hp, const float* y, const float* dy, int lddy, float* dWh, float* ds,
                            float* dt, void* stream) {
-  int rc = gat_args_ok("sgg_gat_bwd", Wh, heads, a, labels, seg_off, nseg, n, F, mask_mode, epilogue, max_seg);
+  SGG_CHECK_ARG(ds && dt, "sgg_gat_bwd: null pointer");
+  return gat_bwd_launch("sgg_gat_bwd", Wh, heads, a, a ? a + F : nullptr, 2 * F, labels, seg_off, nseg, n, F, alpha,
+                        mask_mode, epilogue, max_seg, hp, y, dy, lddy, dWh, ds, dt, nullptr, nullptr, stream);
+}
+
+static size_t gat_pda_bytes(int nseg, int heads, int F) {
+  return ((size_t)nseg * heads * 2 * F * sizeof(float) + 15) & ~(size_t)15;
+}
+
+extern "C" size_t sgg_gat_bwd_ex_work_bytes(int nseg, int heads, int F) {
+  if (nseg < 0 || heads < 1 || F < 1) return 0;
+  return gat_pda_bytes(nseg, heads, F) + (size_t)nseg * heads * F * sizeof(double);
+}
+
+extern "C" int sgg_gat_fwd_ex(const float* Wh, int heads, const float* a_src, const float* a_dst, const float* bias,
+                              const float* labels, const int32_t* seg_off, int nseg, int n, int F, float alpha,
+                              int mask_mode, int epilogue, int max_seg, float* hp, float* y, int ldy, void* stream) {
+  return gat_fwd_launch("sgg_gat_fwd_ex", Wh, heads, a_src, a_dst, F, bias, labels, seg_off, nseg, n, F, alpha,
+                        mask_mode, epilogue, max_seg, hp, y, ldy, stream);
+}
+
+extern "C" int sgg_gat_bwd_ex(const float* Wh, int heads, const float* a_src, const float* a_dst, const float* labels,
+                              const int32_t* seg_off, int nseg, int n, int F, float alpha, int mask_mode, int epilogue,
+                              int max_seg, const float* hp, const float* y, const float* dy, int lddy, float* dWh,
+                              float* da_src, float* da_dst, float* dbias, void* work, void* stream) {
+  SGG_CHECK_ARG(da_src && da_dst && work, "sgg_gat_bwd_ex: null pointer");
+  SGG_CHECK_ARG(((uintptr_t)work & 15) == 0, "sgg_gat_bwd_ex: work must be 16-byte aligned");
+  float* pda = reinterpret_cast<float*>(work);
+  double* pdb = dbias ? reinterpret_cast<double*>(reinterpret_cast<char*>(work) + gat_pda_bytes(nseg, heads, F))
+                      : nullptr;
+  int rc = gat_bwd_launch("sgg_gat_bwd_ex", Wh, heads, a_src, a_dst, F, labels, seg_off, nseg, n, F, alpha, mask_mode,
+                          epilogue, max_seg, hp, y, dy, lddy, dWh, nullptr, nullptr, pda, pdb, stream);
   if (rc) return rc;
-  SGG_CHECK_ARG(dy && dWh && ds && dt, "sgg_gat_bwd: null pointer");
-  SGG_CHECK_ARG(epilogue == 0 || hp, "sgg_gat_bwd: epilogue needs hp");
-  SGG_CHECK_ARG(epilogue != 2 || y, "sgg_gat_bwd: log_softmax epilogue needs y");
-  SGG_CHECK_ARG(lddy >= heads * F, "sgg_gat_bwd: lddy < heads * F");
-  if (nseg == 0) return 0;
-  const size_t lds = gat_bwd_lds(F, max_seg);
-  SGG_CHECK_ARG(lds <= 160 * 1024, "sgg_gat_bwd: segment %d x F %d needs %zu B of LDS", max_seg, F, lds);
-  auto k = max_seg <= 32 ? gat_bwd_kernel<2> : max_seg <= 64 ? gat_bwd_kernel<4> : gat_bwd_kernel<8>;
-  hipLaunchKernelGGL(k, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), lds, (hipStream_t)stream, Wh, heads, a,
-                     labels, seg_off, nseg, n, F, alpha, mask_mode, epilogue, max_seg, hp, y, dy, lddy, dWh, ds, dt);
-  SGG_RETURN_LAUNCH("sgg_gat_bwd");
+  // (no segments: the reduce writes zero gradients)
+  hipLaunchKernelGGL(gat_param_reduce_kernel, dim3(heads * 2 * F + (dbias ? F : 0)), dim3(256), 0,
+                     (hipStream_t)stream, pda, pdb, nseg, heads, F, da_src, da_dst, dbias);
+  SGG_RETURN_LAUNCH("sgg_gat_bwd_ex");
 }

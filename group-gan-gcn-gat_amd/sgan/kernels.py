@@ -1449,6 +1449,59 @@ class _GatAttn(torch.autograd.Function):
         return dWh, da, dbias, None, None, None, None, None, None, None, None
 
 
+class _GatAttnEx(torch.autograd.Function):
+    """The batched multi-head GAT's attention (sgg_gat_fwd_ex / _bwd_ex):
+    a_src / a_dst as the module holds them, and their gradients and the
+    bias's finished on the device (no host-side concatenation, products or
+    reductions)."""
+
+    @staticmethod
+    def forward(ctx, wh, a_src, a_dst, bias, labels, seg_off, nseg, max_seg, alpha, mode, epi, heads):
+        lib = _lib()
+        wh = _req(wh, "wh").contiguous()
+        n, HF = wh.shape
+        F = HF // heads
+        a_src, a_dst = a_src.contiguous(), a_dst.contiguous()
+        if a_src.numel() != heads * F or a_dst.numel() != heads * F:
+            raise ValueError("a_src / a_dst must hold heads x F = %d values" % (heads * F))
+        if bias is not None:
+            bias = bias.contiguous()
+        y = torch.empty(n, HF, device=wh.device, dtype=torch.float32)
+        hp = torch.empty(n, HF, device=wh.device, dtype=torch.float32) if epi else None
+        N.check(lib.sgg_gat_fwd_ex(N.ptr(wh), heads, N.ptr(a_src), N.ptr(a_dst), N.ptr(bias), N.ptr(labels),
+                                   N.ptr(seg_off), nseg, n, F, float(alpha), mode, epi, max_seg, N.ptr(hp), N.ptr(y),
+                                   HF, N.stream_ptr()), "sgg_gat_fwd_ex")
+        ctx.meta = (labels, seg_off, nseg, max_seg, float(alpha), mode, epi, heads, bias is not None, F)
+        ctx.save_for_backward(wh, a_src, a_dst, hp, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib()
+        wh, a_src, a_dst, hp, y = ctx.saved_tensors
+        labels, seg_off, nseg, max_seg, alpha, mode, epi, heads, has_bias, F = ctx.meta
+        n, HF = wh.shape
+        dy = dy.contiguous()
+        dWh = torch.empty(n, HF, device=wh.device, dtype=torch.float32)
+        da_s = torch.empty_like(a_src)
+        da_d = torch.empty_like(a_dst)
+        dbias = torch.empty(F, device=wh.device, dtype=torch.float32) if has_bias else None
+        work = torch.empty(max(16, int(lib.sgg_gat_bwd_ex_work_bytes(nseg, heads, F))), device=wh.device,
+                           dtype=torch.uint8)
+        N.check(lib.sgg_gat_bwd_ex(N.ptr(wh), heads, N.ptr(a_src), N.ptr(a_dst), N.ptr(labels), N.ptr(seg_off), nseg,
+                                   n, F, alpha, mode, epi, max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), HF, N.ptr(dWh),
+                                   N.ptr(da_s), N.ptr(da_d), N.ptr(dbias), N.ptr(work), N.stream_ptr()),
+                "sgg_gat_bwd_ex")
+        return dWh, da_s, da_d, dbias, None, None, None, None, None, None, None, None
+
+
+def gat_attention_ex(wh, a_src, a_dst, alpha, graph, epilogue, heads=1, bias=None):
+    """gat_attention with a_src / a_dst separate (heads x F each, any shape
+    of that size) and the parameter gradients finished in the kernels."""
+    return _GatAttnEx.apply(wh, a_src, a_dst, bias, graph.labels, graph.seg_off, graph.nseg, graph.max_seg, alpha,
+                            graph.mode, epilogue, heads)
+
+
 def gat_attention(wh, a, alpha, graph, epilogue, heads=1, bias=None):
     """Masked-softmax attention + aggregation + epilogue over `graph`
     (a SegmentGraph).  epilogue: 0 none, 1 ELU, 2 log_softmax(ELU).

@@ -356,8 +356,7 @@ class BatchMultiHeadGraphAttention(nn.Module):
         H, Fi, Fo = self.n_head, self.f_in, self.f_out
         w_all = self.w.permute(1, 0, 2).reshape(Fi, H * Fo)                 # [w_0 | .. | w_{H-1}]
         wh = K.xw(x, w_all)                                                  # n x H*Fo
-        a_all = torch.cat([self.a_src.view(H, Fo), self.a_dst.view(H, Fo)], dim=1)
-        return K.gat_attention(wh, a_all, 0.2, graph, epilogue, heads=H, bias=self.bias)
+        return K.gat_attention_ex(wh, self.a_src, self.a_dst, 0.2, graph, epilogue, heads=H, bias=self.bias)
 
     def __repr__(self):
         return "%s (%d -> %d -> %d)" % (self.__class__.__name__, self.n_head, self.f_in, self.f_out)

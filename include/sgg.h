@@ -199,6 +199,26 @@ int sgg_gat_bwd(const float* Wh, int heads, const float* a, const float* labels,
                 const float* hp, const float* y, const float* dy, int lddy,
                 float* dWh, float* ds, float* dt, void* stream);
 
+/* sgg_gat_fwd with the attention vectors as the module holds them: a_src
+ * and a_dst heads x F each (the batched GAT's (heads, F, 1) parameters,
+ * GAT.py:38-39 text) instead of one heads x 2F array -- no concatenation. */
+int sgg_gat_fwd_ex(const float* Wh, int heads, const float* a_src, const float* a_dst, const float* bias,
+                   const float* labels, const int32_t* seg_off, int nseg, int n, int F, float alpha, int mask_mode,
+                   int epilogue, int max_seg, float* hp, float* y, int ldy, void* stream);
+
+/* Backward of sgg_gat_fwd_ex with the parameter gradients finished on the
+ * device: dWh (n x heads*F, zero past the last segment), da_src / da_dst
+ * (heads x F: Wh_h^T ds_h, Wh_h^T dt_h) and, when dbias != NULL, dbias (F:
+ * the column sum over nodes and heads of the pre-epilogue gradient,
+ * accumulated in fp64).  Per-(segment, head) partials go to `work` (16-byte
+ * aligned, sgg_gat_bwd_ex_work_bytes) and a second launch sums them in a
+ * fixed order (deterministic). */
+size_t sgg_gat_bwd_ex_work_bytes(int nseg, int heads, int F);
+int sgg_gat_bwd_ex(const float* Wh, int heads, const float* a_src, const float* a_dst, const float* labels,
+                   const int32_t* seg_off, int nseg, int n, int F, float alpha, int mask_mode, int epilogue,
+                   int max_seg, const float* hp, const float* y, const float* dy, int lddy, float* dWh,
+                   float* da_src, float* da_dst, float* dbias, void* work, void* stream);
+
 /* ------------------------------------------------------------------------
  * Instance normalisation over the rows of each segment (InstanceNorm1d,
  * affine = False, of the sgangat GAT, GAT.py:71-74, 80: each scene's

@@ -1788,7 +1788,9 @@ def _gat_attention_ref(wh, a, bias, labels, seg_off, mode, epi, heads, alpha=0.2
 def test_gat_attention_vs_torch(heads, F, sizes, mode, epi, use_bias, pad):
     """sgg_gat_fwd / sgg_gat_bwd (MFMA tiles) against an fp64 torch
     restatement: the output, and the gradients of Wh, a and the bias through
-    the kernel's dWh / ds / dt; pad rows past the last segment stay zero."""
+    the kernel's dWh / ds / dt; pad rows past the last segment stay zero.
+    The same for sgg_gat_fwd_ex / _bwd_ex (a_src / a_dst apart, da and dbias
+    reduced on the device)."""
     from sgan import kernels as K
     torch.manual_seed(heads * 100 + F)
     n_seg = sum(sizes)
@@ -1806,21 +1808,29 @@ def test_gat_attention_vs_torch(heads, F, sizes, mode, epi, use_bias, pad):
     bias = torch.randn(F, device=DEV) * 0.1 if use_bias else None
     dy = torch.randn(n, heads * F, device=DEV)
     dy[n_seg:] = 0      # pad rows are read by no consumer
-    whg = wh.clone().requires_grad_(True)
-    ag = a.clone().requires_grad_(True)
-    bg = bias.clone().requires_grad_(True) if use_bias else None
-    y = K.gat_attention(whg, ag, 0.2, graph, epi, heads=heads, bias=bg)
-    (y * dy).sum().backward()
     wr = wh.double().requires_grad_(True)
     ar = a.double().requires_grad_(True)
     br = bias.double().requires_grad_(True) if use_bias else None
     yr = _gat_attention_ref(wr, ar, br, labels, seg_off, mode, epi, heads)
     (yr * dy.double()).sum().backward()
-    close(y, yr.detach().cpu().numpy(), rtol=2e-5, what="y")
-    if pad:
-        assert torch.equal(y[n_seg:], torch.zeros_like(y[n_seg:]))
-        assert torch.equal(whg.grad[n_seg:], torch.zeros_like(whg.grad[n_seg:]))
-    close(whg.grad[:n_seg], wr.grad[:n_seg].cpu().numpy(), rtol=1e-4, what="dWh")
-    close(ag.grad, ar.grad.cpu().numpy(), rtol=1e-4, what="da")
-    if use_bias:
-        close(bg.grad, br.grad.cpu().numpy(), rtol=1e-4, what="dbias")
+    for ex in (False, True):
+        whg = wh.clone().requires_grad_(True)
+        bg = bias.clone().requires_grad_(True) if use_bias else None
+        if ex:    # sgg_gat_fwd_ex / _bwd_ex: a_src, a_dst apart, parameter gradients on the device
+            asg = a[:, :F].clone().view(heads, F, 1).requires_grad_(True)
+            adg = a[:, F:].clone().view(heads, F, 1).requires_grad_(True)
+            y = K.gat_attention_ex(whg, asg, adg, 0.2, graph, epi, heads=heads, bias=bg)
+        else:
+            ag = a.clone().requires_grad_(True)
+            y = K.gat_attention(whg, ag, 0.2, graph, epi, heads=heads, bias=bg)
+        (y * dy).sum().backward()
+        w = "ex " if ex else ""
+        close(y, yr.detach().cpu().numpy(), rtol=2e-5, what=w + "y")
+        if pad:
+            assert torch.equal(y[n_seg:], torch.zeros_like(y[n_seg:]))
+            assert torch.equal(whg.grad[n_seg:], torch.zeros_like(whg.grad[n_seg:]))
+        close(whg.grad[:n_seg], wr.grad[:n_seg].cpu().numpy(), rtol=1e-4, what=w + "dWh")
+        da = torch.cat([asg.grad.view(heads, F), adg.grad.view(heads, F)], 1) if ex else ag.grad
+        close(da, ar.grad.cpu().numpy(), rtol=1e-4, what=w + "da")
+        if use_bias:
+            close(bg.grad, br.grad.cpu().numpy(), rtol=1e-4, what=w + "dbias")
