@@ -22,6 +22,7 @@ namespace sgg {
 
 constexpr int kGatThreads = 256;
 constexpr int kGatWaves = kGatThreads / 64;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float lrelu(float x, float alpha) { return x > 0.f ? x : alpha * x; }
 
@@ -39,6 +40,133 @@ __host__ __device__ __forceinline__ int gat_r16(int n) { return (n + 15) & ~15; 
 // operand layout (lane = row i, k-step m = nodes 4m + (lane >> 4)), so the
 // softmax needs two cross-lane steps per reduction and the aggregation
 // att @ Wh reads only Wh (LDS) -- no attention matrix is stored.
+
+// s_i = Wh_i . a_src, t_i = Wh_i . a_dst and the labels of rows [0, nr)
+// (Ws rows >= n are zero); the caller barriers after
+__device__ __forceinline__ void gat_scores(const float* Ws, int Fs, const float* as, const float* ad, int F,
+                                           const float* labels, int mode, int o, int n, int nr, float* ss, float* ts,
+                                           float* lab) {
+  for (int r = threadIdx.x; r < nr; r += kGatThreads) {
+    float s = 0.f, t = 0.f;
+    for (int f = 0; f < F; ++f) {
+      const float w = Ws[r * Fs + f];
+      s = fmaf(w, as[f], s);
+      t = fmaf(w, ad[f], t);
+    }
+    ss[r] = s;
+    ts[r] = t;
+    lab[r] = (mode == 0 && r < n) ? labels[o + r] : 0.f;
+  }
+}
+
+// softmax attention + aggregation + bias + epilogue of one (segment, head)
+// from the LDS tile Ws (nr x Fs, zero rows past n) and its scores
+template <int NM>
+__device__ __forceinline__ void gat_attend(const float* Ws, int Fs, const float* ss, const float* ts,
+                                           const float* lab, int o, int n, int nr, int F, int HF, int c0, float alpha,
+                                           int mode, int epi, const float* __restrict__ bias, float* __restrict__ hp,
+                                           float* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int nct = (F + 15) >> 4;
+  const int nm = nr >> 2;
+  for (int rb = wave; 16 * rb < n; rb += kGatWaves) {
+    const int i = 16 * rb + r16;
+    const bool iv = i < n;
+    const float si = ss[i], li = lab[i];
+    float p[NM];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      p[m] = -INFINITY;
+      if (m < nm) {
+        const int j = 4 * m + q;
+        const bool edge = iv && j < n && (mode == 1 || i == j || (li != 0.f && li == lab[j]));
+        if (edge) {
+          p[m] = lrelu(si + ts[j], alpha);
+          mx = fmaxf(mx, p[m]);
+        }
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const float e = p[m] == -INFINITY ? 0.f : expf(p[m] - mx);
+      p[m] = e;
+      sum += e;
+    }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float inv = iv ? 1.f / sum : 0.f;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) p[m] *= inv;
+    // out = att @ Wh (+ bias), 16-feature column tiles
+    floatx4 hv[8];
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+      hv[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (ct < nct) {
+        const int fb = min(16 * ct + r16, F - 1);
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+          if (m < nm) hv[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[m], Ws[(4 * m + q) * Fs + fb], hv[ct], 0, 0, 0);
+        const float bv = (bias && 16 * ct + r16 < F) ? bias[16 * ct + r16] : 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) hv[ct][v] += bv;
+      }
+    }
+    // epilogue per output row 16 rb + 4 q + v, feature 16 ct + r16
+    float lse[4] = {0.f, 0.f, 0.f, 0.f};
+    if (epi == 2) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float zm = -INFINITY;
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct)
+          if (ct < nct && 16 * ct + r16 < F) zm = fmaxf(zm, elu(hv[ct][v]));
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) zm = fmaxf(zm, __shfl_xor(zm, o2));
+        float se = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct)
+          if (ct < nct && 16 * ct + r16 < F) se += expf(elu(hv[ct][v]) - zm);
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) se += __shfl_xor(se, o2);
+        lse[v] = zm + logf(se);
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+      const int f = 16 * ct + r16;
+      if (ct < nct && f < F) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int io = 16 * rb + 4 * q + v;
+          if (io < n) {
+            const float h = hv[ct][v];
+            const float z = epi ? elu(h) : h;
+            if (epi) hp[(size_t)(o + io) * HF + c0 + f] = h;
+            y[(size_t)(o + io) * ldy + c0 + f] = epi == 2 ? z - lse[v] : z;
+          }
+        }
+      }
+    }
+  }
+}
+
+// rows past the last segment (zero-padded group buffers): zero outputs
+__device__ __forceinline__ void gat_zero_pad_rows(const int32_t* seg_off, int nseg, int nrows, int HF, float* y,
+                                                  int ldy, float* hp) {
+  for (size_t e = (size_t)seg_off[nseg] * HF + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * HF;
+       e += (size_t)gridDim.x * kGatThreads) {
+    const size_t r = e / HF, c = e - r * HF;
+    y[r * ldy + c] = 0.f;
+    if (hp) hp[e] = 0.f;
+  }
+}
+
 template <int NM>   // 4-node k-steps held per lane: segments of <= 4 NM nodes
 __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
     const float* __restrict__ Wh, int heads, const float* __restrict__ a_src, const float* __restrict__ a_dst, int lda,
@@ -49,27 +177,16 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
   const int Fs = gat_fs(F), F4 = (F + 3) & ~3;
   const int nmax = gat_r16(max_seg);
   const int HF = heads * F;
-  // rows past the last segment (zero-padded group buffers): zero outputs
-  for (size_t e = (size_t)seg_off[nseg] * HF + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * HF;
-       e += (size_t)gridDim.x * kGatThreads) {
-    const size_t r = e / HF, c = e - r * HF;
-    y[r * ldy + c] = 0.f;
-    if (epi) hp[e] = 0.f;
-  }
+  gat_zero_pad_rows(seg_off, nseg, nrows, HF, y, ldy, epi ? hp : nullptr);
   float* Ws = reinterpret_cast<float*>(smem);   // nmax x Fs
   float* ss = Ws + nmax * Fs;                   // nmax
   float* ts = ss + nmax;                        // nmax
   float* lab = ts + nmax;                       // nmax
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, q = lane >> 4;
-  const int nct = (F + 15) >> 4;
   for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
     const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
     const int n = seg_off[g + 1] - o;
     if (n <= 0) continue;
-    const float* as = a_src + (size_t)lda * hd;
-    const float* ad = a_dst + (size_t)lda * hd;
     const int c0 = hd * F;
     const int nr = gat_r16(n);
     for (int e = threadIdx.x; e < nr * F4; e += kGatThreads) {
@@ -77,105 +194,156 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
       Ws[r * Fs + f] = (r < n && f < F) ? Wh[(size_t)(o + r) * HF + c0 + f] : 0.f;
     }
     __syncthreads();
-    for (int r = threadIdx.x; r < nr; r += kGatThreads) {
-      float s = 0.f, t = 0.f;
-      for (int f = 0; f < F; ++f) {
-        const float w = Ws[r * Fs + f];
-        s = fmaf(w, as[f], s);
-        t = fmaf(w, ad[f], t);
-      }
-      ss[r] = s;
-      ts[r] = t;
-      lab[r] = (mode == 0 && r < n) ? labels[o + r] : 0.f;
-    }
+    gat_scores(Ws, Fs, a_src + (size_t)lda * hd, a_dst + (size_t)lda * hd, F, labels, mode, o, n, nr, ss, ts, lab);
     __syncthreads();
-    const int nm = nr >> 2;
-    for (int rb = wave; 16 * rb < n; rb += kGatWaves) {
-      const int i = 16 * rb + r16;
-      const bool iv = i < n;
-      const float si = ss[i], li = lab[i];
-      float p[NM];
-      float mx = -INFINITY;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        p[m] = -INFINITY;
-        if (m < nm) {
-          const int j = 4 * m + q;
-          const bool edge = iv && j < n && (mode == 1 || i == j || (li != 0.f && li == lab[j]));
-          if (edge) {
-            p[m] = lrelu(si + ts[j], alpha);
-            mx = fmaxf(mx, p[m]);
-          }
-        }
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      float sum = 0.f;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const float e = p[m] == -INFINITY ? 0.f : expf(p[m] - mx);
-        p[m] = e;
-        sum += e;
-      }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
-      const float inv = iv ? 1.f / sum : 0.f;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) p[m] *= inv;
-      // out = att @ Wh (+ bias), 16-feature column tiles
-      floatx4 hv[8];
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) {
-        hv[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-        if (ct < nct) {
-          const int fb = min(16 * ct + r16, F - 1);
-#pragma unroll
-          for (int m = 0; m < NM; ++m)
-            if (m < nm) hv[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[m], Ws[(4 * m + q) * Fs + fb], hv[ct], 0, 0, 0);
-          const float bv = (bias && 16 * ct + r16 < F) ? bias[16 * ct + r16] : 0.f;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) hv[ct][v] += bv;
-        }
-      }
-      // epilogue per output row 16 rb + 4 q + v, feature 16 ct + r16
-      float lse[4] = {0.f, 0.f, 0.f, 0.f};
-      if (epi == 2) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          float zm = -INFINITY;
-#pragma unroll
-          for (int ct = 0; ct < 8; ++ct)
-            if (ct < nct && 16 * ct + r16 < F) zm = fmaxf(zm, elu(hv[ct][v]));
-#pragma unroll
-          for (int o2 = 1; o2 < 16; o2 <<= 1) zm = fmaxf(zm, __shfl_xor(zm, o2));
-          float se = 0.f;
-#pragma unroll
-          for (int ct = 0; ct < 8; ++ct)
-            if (ct < nct && 16 * ct + r16 < F) se += expf(elu(hv[ct][v]) - zm);
-#pragma unroll
-          for (int o2 = 1; o2 < 16; o2 <<= 1) se += __shfl_xor(se, o2);
-          lse[v] = zm + logf(se);
-        }
-      }
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) {
-        const int f = 16 * ct + r16;
-        if (ct < nct && f < F) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int io = 16 * rb + 4 * q + v;
-            if (io < n) {
-              const float h = hv[ct][v];
-              const float z = epi ? elu(h) : h;
-              if (epi) hp[(size_t)(o + io) * HF + c0 + f] = h;
-              y[(size_t)(o + io) * ldy + c0 + f] = epi == 2 ? z - lse[v] : z;
-            }
-          }
-        }
-      }
-    }
+    gat_attend<NM>(Ws, Fs, ss, ts, lab, o, n, nr, F, HF, c0, alpha, mode, epi, bias, hp, y, ldy);
     __syncthreads();  // LDS reused by the next segment
   }
+}
+
+// One batched-GAT layer of the sgangat family in one launch (GAT.py:71-86
+// text: InstanceNorm1d over the scene's nodes, then the multi-head attention
+// layer): per (segment, head) the segment's input rows (one or two column
+// blocks: [h | pool_h] without a concatenation) are staged in LDS, normalised
+// per feature (the two-pass fp64 statistics of seg_norm_fwd_kernel, norm.hip,
+// same row phases and combine order), transformed by the head's W (K x F, the
+// module's (heads, K, F) layout: no permuted copy) on the MFMA -- fp32 16x16x4,
+// or bf16 16x16x32 with xw_bf16_kernel's rounding and k order -- and attended.
+// When saving (training), head 0 writes the normalised rows and 1 / std and
+// every head its Wh block: the backward's operands.
+struct GatLayerArgs {
+  const float *x1, *x2;
+  int ld1, K1, ld2, K2;
+  const float *w, *a_src, *a_dst, *bias;
+  const int32_t* seg_off;
+  int nseg, nrows, heads, F, epi, max_seg;
+  float alpha, eps;
+  float *xn, *rstd, *wh, *hp, *y;
+  int ldy;
+};
+
+__host__ __device__ __forceinline__ int gat_layer_kp(int K) { return (K + 31) & ~31; }
+
+template <int NM, bool BF16>
+__global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLayerArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int F = p.F, K = p.K1 + p.K2, HF = p.heads * F;
+  const int Fs = gat_fs(F);
+  const int Kp = gat_layer_kp(K), Ks = Kp + 1;
+  const int F16 = (F + 15) & ~15, Wp = F16 + 1;
+  const int nmax = gat_r16(p.max_seg);
+  gat_zero_pad_rows(p.seg_off, p.nseg, p.nrows, HF, p.y, p.ldy, p.epi ? p.hp : nullptr);
+  if (p.wh) {   // the saved operands too (the backward's products run over all rows)
+    gat_zero_pad_rows(p.seg_off, p.nseg, p.nrows, HF, p.wh, HF, nullptr);
+    gat_zero_pad_rows(p.seg_off, p.nseg, p.nrows, K, p.xn, K, nullptr);
+  }
+  double(*red)[64] = reinterpret_cast<double(*)[64]>(smem);   // 4 x 64
+  float* Xs = reinterpret_cast<float*>(smem + 4 * 64 * sizeof(double));   // nmax x Ks
+  float* Wl = Xs + nmax * Ks;                   // Kp x Wp
+  float* Ws = Wl + Kp * Wp;                     // nmax x Fs
+  float* ss = Ws + nmax * Fs;
+  float* ts = ss + nmax;
+  float* lab = ts + nmax;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int fl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  for (int gh = blockIdx.x; gh < p.nseg * p.heads; gh += gridDim.x) {
+    const int g = gh / p.heads, hd = gh - g * p.heads;
+    const int o = p.seg_off[g];
+    const int n = p.seg_off[g + 1] - o;
+    if (n <= 0) continue;
+    const int c0 = hd * F;
+    const int nr = gat_r16(n);
+    const bool save = p.wh != nullptr;
+    for (int e = threadIdx.x; e < nr * Kp; e += kGatThreads) {
+      const int r = e / Kp, k = e - r * Kp;
+      float v = 0.f;
+      if (r < n && k < K)
+        v = k < p.K1 ? p.x1[(size_t)(o + r) * p.ld1 + k] : p.x2[(size_t)(o + r) * p.ld2 + (k - p.K1)];
+      Xs[r * Ks + k] = v;
+    }
+    const float* wg = p.w + (size_t)hd * K * F;
+    for (int e = threadIdx.x; e < Kp * F16; e += kGatThreads) {
+      const int k = e / F16, f = e - k * F16;
+      Wl[k * Wp + f] = (k < K && f < F) ? wg[(size_t)k * F + f] : 0.f;
+    }
+    __syncthreads();
+    // instance norm per feature over the segment's rows (in place)
+    for (int f0 = 0; f0 < K; f0 += 64) {
+      const int f = f0 + fl;
+      const bool fok = f < K;
+      double s = 0.0;
+      if (fok)
+        for (int r = ph; r < n; r += 4) s += (double)Xs[r * Ks + f];
+      red[ph][fl] = s;
+      __syncthreads();
+      const double meand = ((red[0][fl] + red[1][fl]) + (red[2][fl] + red[3][fl])) / n;
+      __syncthreads();
+      const float mean = (float)meand;
+      double qv = 0.0;
+      if (fok)
+        for (int r = ph; r < n; r += 4) {
+          const double d = (double)Xs[r * Ks + f] - meand;
+          qv = fma(d, d, qv);
+        }
+      red[ph][fl] = qv;
+      __syncthreads();
+      const double qs = (red[0][fl] + red[1][fl]) + (red[2][fl] + red[3][fl]);
+      __syncthreads();
+      const float rs = 1.f / sqrtf((float)(qs / n) + p.eps);
+      if (fok) {
+        for (int r = ph; r < n; r += 4) {
+          const float v = (Xs[r * Ks + f] - mean) * rs;
+          Xs[r * Ks + f] = v;
+          if (save && hd == 0) p.xn[(size_t)(o + r) * K + f] = v;
+        }
+        if (save && hd == 0 && ph == 0) p.rstd[(size_t)g * K + f] = rs;
+      }
+    }
+    __syncthreads();
+    // Wh = Xn W_h: (row block, column tile) MFMA tiles over the waves
+    const int nrb = nr >> 4, nct = F16 >> 4;
+    for (int tile = wave; tile < nrb * nct; tile += kGatWaves) {
+      const int rb = tile / nct, ct = tile - rb * nct;
+      floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+      const float* xr = Xs + (16 * rb + r16) * Ks;
+      if constexpr (BF16) {
+        for (int k0 = 0; k0 < Kp; k0 += 32) {
+          const int kb = k0 + 8 * q;
+          bf16x8 a, b;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            a[j] = (__bf16)xr[kb + j];
+            b[j] = (__bf16)Wl[(kb + j) * Wp + 16 * ct + r16];
+          }
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+        }
+      } else {
+        for (int k0 = 0; k0 < K; k0 += 4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[k0 + q], Wl[(k0 + q) * Wp + 16 * ct + r16], acc, 0, 0, 0);
+      }
+      const int f = 16 * ct + r16;
+      if (f < F) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int r = 16 * rb + 4 * q + v;
+          Ws[r * Fs + f] = acc[v];
+          if (save && r < n) p.wh[(size_t)(o + r) * HF + c0 + f] = acc[v];
+        }
+      }
+    }
+    __syncthreads();
+    gat_scores(Ws, Fs, p.a_src + (size_t)F * hd, p.a_dst + (size_t)F * hd, F, nullptr, 1, o, n, nr, ss, ts, lab);
+    __syncthreads();
+    gat_attend<NM>(Ws, Fs, ss, ts, lab, o, n, nr, F, HF, c0, p.alpha, 1, p.epi, p.bias, p.hp, p.y, p.ldy);
+    __syncthreads();  // LDS reused by the next segment
+  }
+}
+
+static size_t gat_layer_lds(int K, int F, int max_seg) {
+  const size_t nm = gat_r16(max_seg), Kp = gat_layer_kp(K);
+  return 4 * 64 * sizeof(double) +
+         sizeof(float) * (nm * (Kp + 1) + Kp * (((F + 15) & ~15) + 1) + nm * gat_fs(F) + 3 * nm) + 16;
 }
 
 // Backward.  Per row block (in the C layout: lane = column j, rows 4 (lane >>
@@ -574,4 +742,38 @@ extern "C" int sgg_gat_bwd_ex(const float* Wh, int heads, const float* a_src, co
   hipLaunchKernelGGL(gat_param_reduce_kernel, dim3(heads * 2 * F + (dbias ? F : 0)), dim3(256), 0,
                      (hipStream_t)stream, pda, pdb, nseg, heads, F, da_src, da_dst, dbias);
   SGG_RETURN_LAUNCH("sgg_gat_bwd_ex");
+}
+
+extern "C" size_t sgg_gat_layer_lds_bytes(int K, int F, int max_seg) {
+  if (K < 1 || F < 1 || max_seg < 1) return 0;
+  return gat_layer_lds(K, F, max_seg);
+}
+
+extern "C" int sgg_gat_layer_fwd(const float* x1, int ld1, int K1, const float* x2, int ld2, int K2, const float* w,
+                                 const float* a_src, const float* a_dst, const float* bias, const int32_t* seg_off,
+                                 int nseg, int n, int heads, int F, float alpha, float eps, int epilogue, int max_seg,
+                                 int bf16, float* xn, float* rstd, float* wh, float* hp, float* y, int ldy,
+                                 void* stream) {
+  const int K = K1 + (x2 ? K2 : 0);
+  SGG_CHECK_ARG(x1 && w && a_src && a_dst && seg_off && y, "sgg_gat_layer_fwd: null pointer");
+  SGG_CHECK_ARG(K1 >= 1 && ld1 >= K1 && (!x2 || (K2 >= 1 && ld2 >= K2)), "sgg_gat_layer_fwd: bad input blocks");
+  SGG_CHECK_ARG(K <= 256, "sgg_gat_layer_fwd: K=%d > 256", K);
+  SGG_CHECK_ARG(F >= 1 && F <= 128 && heads >= 1 && heads <= 64, "sgg_gat_layer_fwd: F=%d heads=%d", F, heads);
+  SGG_CHECK_ARG(epilogue == 0 || epilogue == 1, "sgg_gat_layer_fwd: epilogue must be 0 or 1");
+  SGG_CHECK_ARG(epilogue == 0 || hp, "sgg_gat_layer_fwd: the ELU epilogue needs hp");
+  SGG_CHECK_ARG(!wh || (xn && rstd), "sgg_gat_layer_fwd: saving needs xn, rstd and wh");
+  SGG_CHECK_ARG(ldy >= heads * F && nseg >= 0 && n >= 0, "sgg_gat_layer_fwd: bad sizes");
+  SGG_CHECK_ARG(max_seg >= 1 && max_seg <= SGG_GAT_MAX_NODES, "sgg_gat_layer_fwd: max segment %d outside [1, %d]",
+                max_seg, SGG_GAT_MAX_NODES);
+  const size_t lds = gat_layer_lds(K, F, max_seg);
+  SGG_CHECK_ARG(lds <= 160 * 1024, "sgg_gat_layer_fwd: K %d, F %d, %d nodes need %zu B of LDS", K, F, max_seg, lds);
+  if (nseg == 0 && n == 0) return 0;
+  GatLayerArgs p{x1, x2, ld1, K1, ld2, x2 ? K2 : 0, w, a_src, a_dst, bias, seg_off, nseg, n, heads, F, epilogue,
+                 max_seg, alpha, eps, xn, rstd, wh, hp, y, ldy};
+  auto k = bf16 ? (max_seg <= 32 ? gat_layer_fwd_kernel<8, true> : max_seg <= 64 ? gat_layer_fwd_kernel<16, true>
+                                                                                  : gat_layer_fwd_kernel<32, true>)
+                : (max_seg <= 32 ? gat_layer_fwd_kernel<8, false> : max_seg <= 64 ? gat_layer_fwd_kernel<16, false>
+                                                                                   : gat_layer_fwd_kernel<32, false>);
+  hipLaunchKernelGGL(k, dim3(gat_grid(nseg, heads)), dim3(kGatThreads), lds, (hipStream_t)stream, p);
+  SGG_RETURN_LAUNCH("sgg_gat_layer_fwd");
 }

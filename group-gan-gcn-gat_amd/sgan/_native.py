@@ -138,6 +138,9 @@ SIGNATURES = {
     "sgg_gat_bwd_ex": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _p, _p, _p, _i, _p, _p, _p, _p, _p,
                             _p]),
     "sgg_gat_bwd_ex_work_bytes": (_sz, [_i, _i, _i]),
+    "sgg_gat_layer_lds_bytes": (_sz, [_i, _i, _i]),
+    "sgg_gat_layer_fwd": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _f, _f, _i, _i, _i, _p, _p,
+                               _p, _p, _p, _i, _p]),
     "sgg_seg_norm_fwd": (_i, [_p, _i, _i, _p, _i, _f, _p, _i, _p, _p]),
     "sgg_seg_norm_bwd": (_i, [_p, _i, _p, _i, _i, _p, _i, _p, _p, _i, _p]),
     "sgg_group_index_ws": (_sz, [_i, _i]),

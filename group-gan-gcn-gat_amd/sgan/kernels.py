@@ -1488,11 +1488,28 @@ class _GatAttnEx(torch.autograd.Function):
         dbias = torch.empty(F, device=wh.device, dtype=torch.float32) if has_bias else None
         work = torch.empty(max(16, int(lib.sgg_gat_bwd_ex_work_bytes(nseg, heads, F))), device=wh.device,
                            dtype=torch.uint8)
+        _gat_bwd_ex_launch(wh, heads, a_src, a_dst, labels, seg_off, nseg, n, F, alpha, mode, epi, max_seg, hp, y, dy,
+                           dWh, da_s, da_d, dbias, work)
+        return dWh, da_s, da_d, dbias, None, None, None, None, None, None, None, None
+
+
+def _gat_bwd_ex_launch(wh, heads, a_src, a_dst, labels, seg_off, nseg, n, F, alpha, mode, epi, max_seg, hp, y, dy,
+                       dWh, da_s, da_d, dbias, work):
+    lib = _lib()
+    HF = heads * F
+
+    def launch():
         N.check(lib.sgg_gat_bwd_ex(N.ptr(wh), heads, N.ptr(a_src), N.ptr(a_dst), N.ptr(labels), N.ptr(seg_off), nseg,
                                    n, F, alpha, mode, epi, max_seg, N.ptr(hp), N.ptr(y), N.ptr(dy), HF, N.ptr(dWh),
                                    N.ptr(da_s), N.ptr(da_d), N.ptr(dbias), N.ptr(work), N.stream_ptr()),
                 "sgg_gat_bwd_ex")
-        return dWh, da_s, da_d, dbias, None, None, None, None, None, None, None, None
+    launch()
+    if timer.active and n > 0:
+        # per (segment, head): datt = dhp Wh^T, dWh = att^T dhp, the attention
+        # recompute ~ 3 x 2 n^2 F (n^2 bounded by n * max_seg); operands
+        # Wh, dy, hp (+ y) in, dWh out
+        timer.add("sgg::gat_bwd_kernel+gat_param_reduce_kernel", (n, HF, heads, max_seg),
+                  6.0 * n * max_seg * HF, 4.0 * n * HF * (4 if epi else 3), launch)
 
 
 def gat_attention_ex(wh, a_src, a_dst, alpha, graph, epilogue, heads=1, bias=None):
@@ -1500,6 +1517,112 @@ def gat_attention_ex(wh, a_src, a_dst, alpha, graph, epilogue, heads=1, bias=Non
     of that size) and the parameter gradients finished in the kernels."""
     return _GatAttnEx.apply(wh, a_src, a_dst, bias, graph.labels, graph.seg_off, graph.nseg, graph.max_seg, alpha,
                             graph.mode, epilogue, heads)
+
+
+class _GatLayer(torch.autograd.Function):
+    """One batched-GAT layer of the sgangat family (instance norm over each
+    segment's rows, then the multi-head attention layer) in one launch,
+    sgg_gat_layer_fwd: the input as one or two column blocks (x2: [h |
+    pool_h] without a concatenation), w in the module's (heads, K, F) layout.
+    Backward: sgg_gat_bwd_ex (dWh and the attention parameters' gradients),
+    the node transform's input / weight gradients as _XW's backward, then
+    sgg_seg_norm_bwd."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, w, a_src, a_dst, bias, seg_off, nseg, max_seg, eps, alpha, epi):
+        lib = _lib()
+        x1 = _rows(x1, "x1")
+        x2 = _rows(x2, "x2") if x2 is not None else None
+        n, K1 = x1.shape
+        K2 = x2.shape[1] if x2 is not None else 0
+        K = K1 + K2
+        H, Kw, F = w.shape
+        if Kw != K:
+            raise ValueError("gat_layer: w is (%d, %d, %d) for %d input features" % (H, Kw, F, K))
+        w = _req(w, "w").contiguous()
+        a_src, a_dst = a_src.contiguous(), a_dst.contiguous()
+        bias = bias.contiguous() if bias is not None else None
+        HF = H * F
+        dev = x1.device
+        save = any(ctx.needs_input_grad[:6])
+        y = torch.empty(n, HF, device=dev, dtype=torch.float32)
+        hp = torch.empty(n, HF, device=dev, dtype=torch.float32) if epi else None
+        xn = rstd = wh = None
+        if save:
+            xn = torch.empty(n, K, device=dev, dtype=torch.float32)
+            rstd = torch.empty(nseg, K, device=dev, dtype=torch.float32)
+            wh = torch.empty(n, HF, device=dev, dtype=torch.float32)
+        bf16 = _PRECISION == "bf16"
+
+        def launch():
+            N.check(lib.sgg_gat_layer_fwd(N.ptr(x1), x1.stride(0), K1, N.ptr(x2), x2.stride(0) if x2 is not None else 0,
+                                          K2, N.ptr(w), N.ptr(a_src), N.ptr(a_dst), N.ptr(bias), N.ptr(seg_off), nseg,
+                                          n, H, F, float(alpha), float(eps), epi, max_seg, int(bf16), N.ptr(xn),
+                                          N.ptr(rstd), N.ptr(wh), N.ptr(hp), N.ptr(y), HF, N.stream_ptr()),
+                    "sgg_gat_layer_fwd")
+        launch()
+        if timer.active and n > 0:
+            # norm 5 nK, transform 2 n K HF, attention 2 n^2 HF (n^2 bounded by
+            # n * max_seg); x in, W, y (+ hp) out, the saved xn / Wh
+            timer.add("sgg::gat_layer_fwd_kernel<%d, %s>" % (8 if max_seg <= 32 else 16 if max_seg <= 64 else 32,
+                                                             "true" if bf16 else "false"),
+                      (n, K, HF, H, max_seg, save), 5.0 * n * K + 2.0 * n * K * HF + 2.0 * n * max_seg * HF,
+                      4.0 * (n * K + H * K * F + n * HF * (2 if epi else 1) + (n * K + n * HF if save else 0)), launch)
+        ctx.meta = (seg_off, nseg, max_seg, float(alpha), epi, H, F, K1, K2, bias is not None)
+        ctx.save_for_backward(xn, rstd, wh, hp, y, w, a_src, a_dst)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib()
+        xn, rstd, wh, hp, y, w, a_src, a_dst = ctx.saved_tensors
+        seg_off, nseg, max_seg, alpha, epi, H, F, K1, K2, has_bias = ctx.meta
+        n = wh.shape[0]
+        K, HF = K1 + K2, H * F
+        dev = wh.device
+        dy = dy.contiguous()
+        dWh = torch.empty(n, HF, device=dev, dtype=torch.float32)
+        da_s = torch.empty_like(a_src)
+        da_d = torch.empty_like(a_dst)
+        dbias = torch.empty(F, device=dev, dtype=torch.float32) if has_bias else None
+        work = torch.empty(max(16, int(lib.sgg_gat_bwd_ex_work_bytes(nseg, H, F))), device=dev, dtype=torch.uint8)
+        _gat_bwd_ex_launch(wh, H, a_src, a_dst, None, seg_off, nseg, n, F, alpha, 1, epi, max_seg, hp, y, dy, dWh,
+                           da_s, da_d, dbias, work)
+        # the node transform Wh = xn [w_0 | .. | w_{H-1}] (as _XW's backward)
+        w_all = w.permute(1, 0, 2).reshape(K, HF)
+        dxn = xw_raw(dWh, w_all, None, True, 0, prec="fp32")
+        dw = None
+        if ctx.needs_input_grad[2]:
+            with side(xn, dWh):
+                dw_all = xtw(xn, dWh)
+            dw = dw_all.view(K, H, F).permute(1, 0, 2)
+        dx = torch.empty(n, K, device=dev, dtype=torch.float32)
+        N.check(lib.sgg_seg_norm_bwd(N.ptr(xn), K, N.ptr(dxn), K, K, N.ptr(seg_off), nseg, N.ptr(rstd), N.ptr(dx), K,
+                                     N.stream_ptr()), "sgg_seg_norm_bwd")
+        if timer.active and n > 0:
+            timer.add("sgg::seg_norm_bwd_kernel", (n, K), 8.0 * n * K, 4.0 * 4 * n * K,
+                      lambda: N.check(lib.sgg_seg_norm_bwd(N.ptr(xn), K, N.ptr(dxn), K, K, N.ptr(seg_off), nseg,
+                                                           N.ptr(rstd), N.ptr(dx), K, N.stream_ptr()),
+                                      "sgg_seg_norm_bwd"))
+        dx1 = dx[:, :K1] if K2 else dx
+        dx2 = dx[:, K1:] if K2 else None
+        return dx1, dx2, dw, da_s, da_d, dbias, None, None, None, None, None, None
+
+
+def gat_layer_ok(K, F, heads, max_seg, epi):
+    """sgg_gat_layer_fwd's limits: the LDS plan, F, heads, the epilogue."""
+    if not (1 <= F <= 128 and 1 <= heads <= 64 and epi in (0, 1) and 1 <= max_seg <= 128 and K <= 256):
+        return False
+    return int(_lib().sgg_gat_layer_lds_bytes(K, F, max_seg)) <= 160 * 1024
+
+
+def gat_layer(x, w, a_src, a_dst, bias, graph, epilogue, eps=1e-5, alpha=0.2):
+    """InstanceNorm1d over each segment's rows, then the multi-head attention
+    layer (w: (heads, K, F); x: a tensor or (x1, x2) column blocks) in one
+    launch (sgg_gat_layer_fwd); the complete graph of each segment."""
+    x1, x2 = x if isinstance(x, tuple) else (x, None)
+    return _GatLayer.apply(x1, x2, w, a_src, a_dst, bias, graph.seg_off, graph.nseg, graph.max_seg, eps, alpha,
+                           epilogue)
 
 
 def gat_attention(wh, a, alpha, graph, epilogue, heads=1, bias=None):

@@ -380,12 +380,23 @@ class BatchGAT(nn.Module):
             raise ValueError("the last batched GAT layer must have one head (GAT.py:83 squeezes it)")
 
     def forward(self, x, graph):
+        """x: (n, n_units[0]) or its two column blocks (h, pool_h).  Each layer
+        is one sgg_gat_layer_fwd launch (norm + node transform + attention)
+        when it fits the kernel (LAYER_FUSED), else the per-op path."""
         if self.dropout > 0 and self.training:
             raise NotImplementedError("dropout between GAT layers is not implemented (dropout1=0)")
         for i, layer in enumerate(self.layer_stack):
+            epi = 0 if i + 1 == self.n_layer else 1                          # ELU fused into the kernel
+            if BatchGAT.LAYER_FUSED and K.gat_layer_ok(layer.f_in, layer.f_out, layer.n_head, graph.max_seg, epi):
+                x = K.gat_layer(x, layer.w, layer.a_src, layer.a_dst, layer.bias, graph, epi)
+                continue
+            if isinstance(x, tuple):
+                x = torch.cat(x, dim=1)
             x = K.seg_instance_norm(x, graph.seg_off, graph.nseg)
-            x = layer(x, graph, 0 if i + 1 == self.n_layer else 1)          # ELU fused into the kernel
+            x = layer(x, graph, epi)
         return x
+
+    LAYER_FUSED = True
 
 
 class BatchGATEncoder(nn.Module):
@@ -397,7 +408,9 @@ class BatchGATEncoder(nn.Module):
         self.gat_net = BatchGAT(n_units, n_heads, dropout, alpha)
 
     def forward(self, h_states, seq_start_end, scenes=None):
-        sc = _scenes(seq_start_end, h_states.device, scenes)
+        """h_states: (B, n_units[0]) or its two column blocks (h, pool_h)."""
+        dev = (h_states[0] if isinstance(h_states, tuple) else h_states).device
+        sc = _scenes(seq_start_end, dev, scenes)
         if sc.max_n > 128:
             raise ValueError("GAT kernels hold <= 128 peds per scene (got %d)" % sc.max_n)
         return self.gat_net(h_states, K.SegmentGraph(sc.scene_off, sc.S, sc.max_n, 1, None))
@@ -688,7 +701,9 @@ class TrajectoryGenerator(nn.Module):
                 # the graph module reads [h | pool_h] as two blocks (no cat)
                 module = self.gatencoder if self.graph == "gat" else self.gcn_module
                 return module((ctx, pool_h), seq_start_end, end_pos, obs_traj_g[-1], scenes=sc, link=link)
-            ctx = torch.cat([ctx, pool_h], dim=1)
+            # (the batched GAT's first layer reads [h | pool_h] as two blocks)
+            ctx = (ctx, pool_h) if self.graph == "sgangat" and self.mlp_decoder_needed() else torch.cat(
+                [ctx, pool_h], dim=1)
         if self.mlp_decoder_needed():
             if self.graph == "gat":
                 noise_input = self.gatencoder(ctx, seq_start_end, end_pos, obs_traj_g[-1], scenes=sc)

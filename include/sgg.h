@@ -219,6 +219,25 @@ int sgg_gat_bwd_ex(const float* Wh, int heads, const float* a_src, const float* 
                    int max_seg, const float* hp, const float* y, const float* dy, int lddy, float* dWh,
                    float* da_src, float* da_dst, float* dbias, void* work, void* stream);
 
+/* One layer of the sgangat family's batched GAT in one launch (GAT.py:71-86
+ * text): InstanceNorm1d over each segment's rows (biased variance, eps; the
+ * statistics of sgg_seg_norm_fwd), Wh = xn [w_0 | .. | w_{H-1}] with w in
+ * the module's (heads, K, F) layout -- fp32, or with bf16 != 0 the operands
+ * rounded to bf16 as sgg_xw_bf16 does (fp32 accumulate) -- then the
+ * multi-head attention of sgg_gat_fwd_ex on the complete segment graph
+ * (epilogue 0 or 1).  The input is one row block x1 (n x K1, stride ld1) or
+ * two, [x1 | x2] (x2: n x K2, stride ld2; NULL for one): K = K1 + K2 <= 256.
+ * When wh != NULL (training) also writes the backward's operands: xn (n x
+ * K, the normalised input), rstd (nseg x K) and wh (n x heads*F) -- with
+ * them the backward is sgg_gat_bwd_ex, the transform's products and
+ * sgg_seg_norm_bwd.  Rows past the last segment get zeros.  The LDS plan
+ * (sgg_gat_layer_lds_bytes(K, F, max_seg)) must fit 160 KiB. */
+size_t sgg_gat_layer_lds_bytes(int K, int F, int max_seg);
+int sgg_gat_layer_fwd(const float* x1, int ld1, int K1, const float* x2, int ld2, int K2, const float* w,
+                      const float* a_src, const float* a_dst, const float* bias, const int32_t* seg_off, int nseg,
+                      int n, int heads, int F, float alpha, float eps, int epilogue, int max_seg, int bf16,
+                      float* xn, float* rstd, float* wh, float* hp, float* y, int ldy, void* stream);
+
 /* ------------------------------------------------------------------------
  * Instance normalisation over the rows of each segment (InstanceNorm1d,
  * affine = False, of the sgangat GAT, GAT.py:71-74, 80: each scene's
