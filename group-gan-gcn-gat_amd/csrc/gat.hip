@@ -31,6 +31,45 @@ __device__ __forceinline__ float lrelu(float x, float alpha) { return x > 0.f ? 
 __host__ __device__ __forceinline__ int gat_fs(int F) { return ((F + 3) & ~3) | 1; }
 __host__ __device__ __forceinline__ int gat_r16(int n) { return (n + 15) & ~15; }
 
+// A rows x cols block into LDS with 16 loads in flight per thread (a loop
+// of one load and one store per element waits a memory latency per
+// element): ld(r, c) is called with indices clamped into [0, nv) x [0, cv)
+// and its value masked to zero outside; st(r, c, v) stores it
+template <typename Ld, typename St>
+__device__ __forceinline__ void stage_block(int rows, int cols, int nv, int cv, Ld ld, St st) {
+  constexpr int kU = 16;
+  const int total = rows * cols;
+  const int dq = kGatThreads / cols, dr = kGatThreads - dq * cols;   // one step of kGatThreads elements
+  for (int base = 0; base < total; base += kU * kGatThreads) {
+    const int e0 = base + (int)threadIdx.x;
+    const int r0 = e0 / cols, c0 = e0 - r0 * cols;
+    float v[kU];
+    int r = r0, c = c0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {   // (slots past the block load a clamped element: no branch)
+      v[u] = keep_if(ld(min(r, nv - 1), min(c, cv - 1)), r < nv && c < cv);
+      r += dq;
+      c += dr;
+      if (c >= cols) {
+        c -= cols;
+        ++r;
+      }
+    }
+    r = r0;
+    c = c0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (e0 + u * kGatThreads < total) st(r, c, v[u]);
+      r += dq;
+      c += dr;
+      if (c >= cols) {
+        c -= cols;
+        ++r;
+      }
+    }
+  }
+}
+
 // Both kernels work on 16 x 16 x 4 fp32 MFMA tiles (exact fp32 products;
 // v_mfma_f32_16x16x4_f32: A[i = lane & 15][k = lane >> 4], B[k = lane >> 4][c
 // = lane & 15], C rows 4 (lane >> 4) + v, column lane & 15).  One workgroup
@@ -41,21 +80,37 @@ __host__ __device__ __forceinline__ int gat_r16(int n) { return (n + 15) & ~15; 
 // softmax needs two cross-lane steps per reduction and the aggregation
 // att @ Wh reads only Wh (LDS) -- no attention matrix is stored.
 
-// s_i = Wh_i . a_src, t_i = Wh_i . a_dst and the labels of rows [0, nr)
-// (Ws rows >= n are zero); the caller barriers after
-__device__ __forceinline__ void gat_scores(const float* Ws, int Fs, const float* as, const float* ad, int F,
+// s_i = Wh_i . a_src, t_i = Wh_i . a_dst (a_s / a_d: LDS copies) and the
+// labels of rows [0, nr) (Ws rows >= n are zero): each row's dot products
+// split over 256 / nr lanes (a shuffle tree joins them); the caller barriers
+__device__ __forceinline__ void gat_scores(const float* Ws, int Fs, const float* a_s, const float* a_d, int F,
                                            const float* labels, int mode, int o, int n, int nr, float* ss, float* ts,
-                                           float* lab) {
-  for (int r = threadIdx.x; r < nr; r += kGatThreads) {
-    float s = 0.f, t = 0.f;
-    for (int f = 0; f < F; ++f) {
-      const float w = Ws[r * Fs + f];
-      s = fmaf(w, as[f], s);
-      t = fmaf(w, ad[f], t);
+                                           float* lab, const float* Ds = nullptr, float* rsum = nullptr) {
+  int sp = 1;   // lanes per row: a power of 2 (groups of aligned lanes)
+  while (sp < 16 && 2 * sp * nr <= kGatThreads) sp *= 2;
+  const int part = threadIdx.x & (sp - 1);
+  for (int r = threadIdx.x / sp; r < nr; r += kGatThreads / sp) {
+    // (fp64: the products of two floats are exact, so the scores are the
+    // rounded exact dot products whatever the lane split)
+    double s = 0.0, t = 0.0;
+    float sd = 0.f;
+    for (int f = part; f < F; f += sp) {
+      const double w = Ws[r * Fs + f];
+      s = fma(w, (double)a_s[f], s);
+      t = fma(w, (double)a_d[f], t);
+      if (Ds) sd += Ds[r * Fs + f];
     }
-    ss[r] = s;
-    ts[r] = t;
-    lab[r] = (mode == 0 && r < n) ? labels[o + r] : 0.f;
+    for (int o2 = 1; o2 < sp; o2 <<= 1) {
+      s += __shfl_xor(s, o2);
+      t += __shfl_xor(t, o2);
+      sd += __shfl_xor(sd, o2);
+    }
+    if (part == 0) {
+      ss[r] = (float)s;
+      ts[r] = (float)t;
+      if (rsum) rsum[r] = sd;
+      lab[r] = (mode == 0 && r < n) ? labels[o + r] : 0.f;
+    }
   }
 }
 
@@ -182,6 +237,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
   float* ss = Ws + nmax * Fs;                   // nmax
   float* ts = ss + nmax;                        // nmax
   float* lab = ts + nmax;                       // nmax
+  float* al = lab + nmax;                       // 2F: the head's a_src | a_dst
   for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
     const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
@@ -189,12 +245,12 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
     if (n <= 0) continue;
     const int c0 = hd * F;
     const int nr = gat_r16(n);
-    for (int e = threadIdx.x; e < nr * F4; e += kGatThreads) {
-      const int r = e / F4, f = e - r * F4;
-      Ws[r * Fs + f] = (r < n && f < F) ? Wh[(size_t)(o + r) * HF + c0 + f] : 0.f;
-    }
+    stage_block(nr, F4, n, F, [&](int r, int f) { return Wh[(size_t)(o + r) * HF + c0 + f]; },
+                [&](int r, int f, float v) { Ws[r * Fs + f] = v; });
+    for (int f = threadIdx.x; f < 2 * F; f += kGatThreads)
+      al[f] = f < F ? a_src[(size_t)lda * hd + f] : a_dst[(size_t)lda * hd + f - F];
     __syncthreads();
-    gat_scores(Ws, Fs, a_src + (size_t)lda * hd, a_dst + (size_t)lda * hd, F, labels, mode, o, n, nr, ss, ts, lab);
+    gat_scores(Ws, Fs, al, al + F, F, labels, mode, o, n, nr, ss, ts, lab);
     __syncthreads();
     gat_attend<NM>(Ws, Fs, ss, ts, lab, o, n, nr, F, HF, c0, alpha, mode, epi, bias, hp, y, ldy);
     __syncthreads();  // LDS reused by the next segment
@@ -244,6 +300,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
   float* ss = Ws + nmax * Fs;
   float* ts = ss + nmax;
   float* lab = ts + nmax;
+  float* al = lab + nmax;                       // 2F: the head's a_src | a_dst
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int fl = threadIdx.x & 63, ph = threadIdx.x >> 6;
@@ -255,18 +312,17 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
     const int c0 = hd * F;
     const int nr = gat_r16(n);
     const bool save = p.wh != nullptr;
-    for (int e = threadIdx.x; e < nr * Kp; e += kGatThreads) {
-      const int r = e / Kp, k = e - r * Kp;
-      float v = 0.f;
-      if (r < n && k < K)
-        v = k < p.K1 ? p.x1[(size_t)(o + r) * p.ld1 + k] : p.x2[(size_t)(o + r) * p.ld2 + (k - p.K1)];
-      Xs[r * Ks + k] = v;
-    }
+    stage_block(
+        nr, Kp, n, K,
+        [&](int r, int k) {
+          return k < p.K1 ? p.x1[(size_t)(o + r) * p.ld1 + k] : p.x2[(size_t)(o + r) * p.ld2 + (k - p.K1)];
+        },
+        [&](int r, int k, float v) { Xs[r * Ks + k] = v; });
     const float* wg = p.w + (size_t)hd * K * F;
-    for (int e = threadIdx.x; e < Kp * F16; e += kGatThreads) {
-      const int k = e / F16, f = e - k * F16;
-      Wl[k * Wp + f] = (k < K && f < F) ? wg[(size_t)k * F + f] : 0.f;
-    }
+    stage_block(Kp, F16, K, F, [&](int k, int f) { return wg[(size_t)k * F + f]; },
+                [&](int k, int f, float v) { Wl[k * Wp + f] = v; });
+    for (int f = threadIdx.x; f < 2 * F; f += kGatThreads)
+      al[f] = f < F ? p.a_src[(size_t)F * hd + f] : p.a_dst[(size_t)F * hd + f - F];
     __syncthreads();
     // instance norm per feature over the segment's rows (in place)
     for (int f0 = 0; f0 < K; f0 += 64) {
@@ -333,7 +389,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
       }
     }
     __syncthreads();
-    gat_scores(Ws, Fs, p.a_src + (size_t)F * hd, p.a_dst + (size_t)F * hd, F, nullptr, 1, o, n, nr, ss, ts, lab);
+    gat_scores(Ws, Fs, al, al + F, F, nullptr, 1, o, n, nr, ss, ts, lab);
     __syncthreads();
     gat_attend<NM>(Ws, Fs, ss, ts, lab, o, n, nr, F, HF, c0, p.alpha, 1, p.epi, p.bias, p.hp, p.y, p.ldy);
     __syncthreads();  // LDS reused by the next segment
@@ -343,7 +399,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
 static size_t gat_layer_lds(int K, int F, int max_seg) {
   const size_t nm = gat_r16(max_seg), Kp = gat_layer_kp(K);
   return 4 * 64 * sizeof(double) +
-         sizeof(float) * (nm * (Kp + 1) + Kp * (((F + 15) & ~15) + 1) + nm * gat_fs(F) + 3 * nm) + 16;
+         sizeof(float) * (nm * (Kp + 1) + Kp * (((F + 15) & ~15) + 1) + nm * gat_fs(F) + 3 * nm + 2 * F) + 16;
 }
 
 // Backward.  Per row block (in the C layout: lane = column j, rows 4 (lane >>
@@ -387,6 +443,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
   float* dts = dss + nmax;
   float* rsum = dts + nmax;                    // epilogue 2: row sums of dy
   float* dtp = rsum + nmax;                    // (nmax / 16) x nmax column partials of dz
+  float* al = dtp + (nmax / 16) * nmax;        // 2F: the head's a_src | a_dst
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int HF = heads * F;
@@ -405,43 +462,33 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
       }
       continue;
     }
-    const float* as = a_src + (size_t)lda * hd;
-    const float* ad = a_dst + (size_t)lda * hd;
+    const float* as = al;
+    const float* ad = al + F;
     const int c0 = hd * F;
     const int nr = gat_r16(n), nrb = nr >> 4;
-    for (int e = threadIdx.x; e < nr * F4; e += kGatThreads) {
-      const int r = e / F4, f = e - r * F4;
-      float w = 0.f, d = 0.f;
-      if (r < n && f < F) {
-        const size_t row = (size_t)(o + r);
-        w = Wh[row * HF + c0 + f];
-        d = dy[row * lddy + c0 + f];
-        if (epi == 1) d *= elu_grad(hp[row * HF + c0 + f]);
-      }
-      Ws[r * Fs + f] = w;
-      Ds[r * Fs + f] = d;
-    }
+    for (int f = threadIdx.x; f < 2 * F; f += kGatThreads)
+      al[f] = f < F ? a_src[(size_t)lda * hd + f] : a_dst[(size_t)lda * hd + f - F];
+    stage_block(nr, F4, n, F, [&](int r, int f) { return Wh[(size_t)(o + r) * HF + c0 + f]; },
+                [&](int r, int f, float v) { Ws[r * Fs + f] = v; });
+    stage_block(
+        nr, F4, n, F,
+        [&](int r, int f) {
+          const size_t row = (size_t)(o + r);
+          const float d = dy[row * lddy + c0 + f];
+          return epi == 1 ? d * elu_grad(hp[row * HF + c0 + f]) : d;
+        },
+        [&](int r, int f, float v) { Ds[r * Fs + f] = v; });
     __syncthreads();
-    for (int r = threadIdx.x; r < nr; r += kGatThreads) {
-      float s = 0.f, t = 0.f, sd = 0.f;
-      for (int f = 0; f < F; ++f) {
-        const float w = Ws[r * Fs + f];
-        s = fmaf(w, as[f], s);
-        t = fmaf(w, ad[f], t);
-        sd += Ds[r * Fs + f];
-      }
-      ss[r] = s;
-      ts[r] = t;
-      rsum[r] = sd;
-      lab[r] = (mode == 0 && r < n) ? labels[o + r] : 0.f;
-    }
+    gat_scores(Ws, Fs, as, ad, F, labels, mode, o, n, nr, ss, ts, lab, Ds, rsum);
     __syncthreads();
     if (epi == 2) {   // d hp = (dy - softmax(y) sum(dy)) * ELU'(hp)
-      for (int e = threadIdx.x; e < n * F; e += kGatThreads) {
-        const int r = e / F, f = e - r * F;
-        const size_t row = (size_t)(o + r);
-        Ds[r * Fs + f] = (Ds[r * Fs + f] - expf(y[row * F + f]) * rsum[r]) * elu_grad(hp[row * HF + c0 + f]);
-      }
+      stage_block(
+          n, F, n, F,
+          [&](int r, int f) {
+            const size_t row = (size_t)(o + r);
+            return (Ds[r * Fs + f] - expf(y[row * F + f]) * rsum[r]) * elu_grad(hp[row * HF + c0 + f]);
+          },
+          [&](int r, int f, float v) { Ds[r * Fs + f] = v; });
       __syncthreads();
     }
     for (int rb = wave; rb < nrb; rb += kGatWaves) {
@@ -625,11 +672,11 @@ __global__ void __launch_bounds__(256) gat_param_reduce_kernel(const float* __re
 
 static size_t gat_fwd_lds(int F, int max_seg) {
   const size_t nm = gat_r16(max_seg);
-  return sizeof(float) * (nm * gat_fs(F) + 3 * nm) + 16;
+  return sizeof(float) * (nm * gat_fs(F) + 3 * nm + 2 * F) + 16;
 }
 static size_t gat_bwd_lds(int F, int max_seg) {
   const size_t nm = gat_r16(max_seg);
-  return sizeof(float) * (2 * nm * gat_fs(F) + nm * (nm + 4) + 6 * nm + (nm / 16) * nm) + 16;
+  return sizeof(float) * (2 * nm * gat_fs(F) + nm * (nm + 4) + 6 * nm + (nm / 16) * nm + 2 * F) + 16;
 }
 
 }  // namespace sgg
