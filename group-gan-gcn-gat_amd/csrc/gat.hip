@@ -20,6 +20,15 @@
 
 namespace sgg {
 
+// phase timestamps of workgroup 0's first (segment, head) (tools/gat_layer_probe.hip)
+#ifdef SGG_GAT_PROF
+__device__ long long g_gat_prof[64];
+#define GPMARK(i) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_gat_prof[i] = wall_clock64();
+#else
+#define GPMARK(i)
+#endif
+
 constexpr int kGatThreads = 256;
 constexpr int kGatWaves = kGatThreads / 64;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -79,6 +88,79 @@ __device__ __forceinline__ void stage_block(int rows, int cols, int nv, int cv, 
 // operand layout (lane = row i, k-step m = nodes 4m + (lane >> 4)), so the
 // softmax needs two cross-lane steps per reduction and the aggregation
 // att @ Wh reads only Wh (LDS) -- no attention matrix is stored.
+
+// two blocks staged together (both blocks' loads in flight before any store:
+// one memory round trip per batch instead of two)
+template <typename LdA, typename StA, typename LdB, typename StB>
+__device__ __forceinline__ void stage_pair(int rowsA, int colsA, int nvA, int cvA, LdA ldA, StA stA, int rowsB,
+                                           int colsB, int nvB, int cvB, LdB ldB, StB stB) {
+  constexpr int kU = 16;
+  const int totA = rowsA * colsA, totB = rowsB * colsB;
+  const int dqA = kGatThreads / colsA, drA = kGatThreads - dqA * colsA;
+  const int dqB = kGatThreads / colsB, drB = kGatThreads - dqB * colsB;
+  for (int base = 0; base < totA || base < totB; base += kU * kGatThreads) {
+    const int e0 = base + (int)threadIdx.x;
+    const int rA0 = e0 / colsA, cA0 = e0 - rA0 * colsA;
+    const int rB0 = e0 / colsB, cB0 = e0 - rB0 * colsB;
+    float va[kU], vb[kU];
+    int r = rA0, c = cA0;
+    const bool doA = base < totA, doB = base < totB;
+    if (doA) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        va[u] = keep_if(ldA(min(r, nvA - 1), min(c, cvA - 1)), r < nvA && c < cvA);
+        r += dqA;
+        c += drA;
+        if (c >= colsA) {
+          c -= colsA;
+          ++r;
+        }
+      }
+    }
+    r = rB0;
+    c = cB0;
+    if (doB) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        vb[u] = keep_if(ldB(min(r, nvB - 1), min(c, cvB - 1)), r < nvB && c < cvB);
+        r += dqB;
+        c += drB;
+        if (c >= colsB) {
+          c -= colsB;
+          ++r;
+        }
+      }
+    }
+    r = rA0;
+    c = cA0;
+    if (doA) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (e0 + u * kGatThreads < totA) stA(r, c, va[u]);
+        r += dqA;
+        c += drA;
+        if (c >= colsA) {
+          c -= colsA;
+          ++r;
+        }
+      }
+    }
+    r = rB0;
+    c = cB0;
+    if (doB) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (e0 + u * kGatThreads < totB) stB(r, c, vb[u]);
+        r += dqB;
+        c += drB;
+        if (c >= colsB) {
+          c -= colsB;
+          ++r;
+        }
+      }
+    }
+  }
+}
 
 // s_i = Wh_i . a_src, t_i = Wh_i . a_dst (a_s / a_d: LDS copies) and the
 // labels of rows [0, nr) (Ws rows >= n are zero): each row's dot products
@@ -212,9 +294,8 @@ __device__ __forceinline__ void gat_attend(const float* Ws, int Fs, const float*
 }
 
 // rows past the last segment (zero-padded group buffers): zero outputs
-__device__ __forceinline__ void gat_zero_pad_rows(const int32_t* seg_off, int nseg, int nrows, int HF, float* y,
-                                                  int ldy, float* hp) {
-  for (size_t e = (size_t)seg_off[nseg] * HF + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * HF;
+__device__ __forceinline__ void gat_zero_pad_rows(int tot, int nrows, int HF, float* y, int ldy, float* hp) {
+  for (size_t e = (size_t)tot * HF + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * HF;
        e += (size_t)gridDim.x * kGatThreads) {
     const size_t r = e / HF, c = e - r * HF;
     y[r * ldy + c] = 0.f;
@@ -232,7 +313,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
   const int Fs = gat_fs(F), F4 = (F + 3) & ~3;
   const int nmax = gat_r16(max_seg);
   const int HF = heads * F;
-  gat_zero_pad_rows(seg_off, nseg, nrows, HF, y, ldy, epi ? hp : nullptr);
+  gat_zero_pad_rows(seg_off[nseg], nrows, HF, y, ldy, epi ? hp : nullptr);
   float* Ws = reinterpret_cast<float*>(smem);   // nmax x Fs
   float* ss = Ws + nmax * Fs;                   // nmax
   float* ts = ss + nmax;                        // nmax
@@ -288,65 +369,88 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
   const int Kp = gat_layer_kp(K), Ks = Kp + 1;
   const int F16 = (F + 15) & ~15, Wp = F16 + 1;
   const int nmax = gat_r16(p.max_seg);
-  gat_zero_pad_rows(p.seg_off, p.nseg, p.nrows, HF, p.y, p.ldy, p.epi ? p.hp : nullptr);
+  GPMARK(0);
+  // the first work item's offsets with the total (independent loads)
+  const int gfirst = min((int)blockIdx.x / p.heads, p.nseg);
+  const int tot = p.seg_off[p.nseg], ofirst = p.seg_off[gfirst], efirst = p.seg_off[min(gfirst + 1, p.nseg)];
+  gat_zero_pad_rows(tot, p.nrows, HF, p.y, p.ldy, p.epi ? p.hp : nullptr);
   if (p.wh) {   // the saved operands too (the backward's products run over all rows)
-    gat_zero_pad_rows(p.seg_off, p.nseg, p.nrows, HF, p.wh, HF, nullptr);
-    gat_zero_pad_rows(p.seg_off, p.nseg, p.nrows, K, p.xn, K, nullptr);
+    gat_zero_pad_rows(tot, p.nrows, HF, p.wh, HF, nullptr);
+    gat_zero_pad_rows(tot, p.nrows, K, p.xn, K, nullptr);
   }
-  double(*red)[64] = reinterpret_cast<double(*)[64]>(smem);   // 4 x 64
-  float* Xs = reinterpret_cast<float*>(smem + 4 * 64 * sizeof(double));   // nmax x Ks
+  double(*red)[64] = reinterpret_cast<double(*)[64]>(smem);   // 8 x 64
+  float* Xs = reinterpret_cast<float*>(smem + 8 * 64 * sizeof(double));   // nmax x Ks
   float* Wl = Xs + nmax * Ks;                   // Kp x Wp
   float* Ws = Wl + Kp * Wp;                     // nmax x Fs
   float* ss = Ws + nmax * Fs;
   float* ts = ss + nmax;
   float* lab = ts + nmax;
-  float* al = lab + nmax;                       // 2F: the head's a_src | a_dst
+  float* al = lab + nmax;                       // 3F: the head's a_src | a_dst, the bias
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int fl = threadIdx.x & 63, ph = threadIdx.x >> 6;
   for (int gh = blockIdx.x; gh < p.nseg * p.heads; gh += gridDim.x) {
     const int g = gh / p.heads, hd = gh - g * p.heads;
-    const int o = p.seg_off[g];
-    const int n = p.seg_off[g + 1] - o;
+    const int o = gh == (int)blockIdx.x ? ofirst : p.seg_off[g];
+    const int n = (gh == (int)blockIdx.x ? efirst : p.seg_off[g + 1]) - o;
     if (n <= 0) continue;
     const int c0 = hd * F;
     const int nr = gat_r16(n);
     const bool save = p.wh != nullptr;
+    GPMARK(1);
+    const float* wg = p.w + (size_t)hd * K * F;
+    float av = 0.f;   // thread t < 3F: a_src | a_dst | bias entry t (issued with the tiles' loads)
+    {
+      const int t = threadIdx.x;
+      if (t < F) av = p.a_src[(size_t)F * hd + t];
+      else if (t < 2 * F) av = p.a_dst[(size_t)F * hd + t - F];
+      else if (t < 3 * F && p.bias) av = p.bias[t - 2 * F];
+    }
     stage_block(
         nr, Kp, n, K,
         [&](int r, int k) {
           return k < p.K1 ? p.x1[(size_t)(o + r) * p.ld1 + k] : p.x2[(size_t)(o + r) * p.ld2 + (k - p.K1)];
         },
         [&](int r, int k, float v) { Xs[r * Ks + k] = v; });
-    const float* wg = p.w + (size_t)hd * K * F;
     stage_block(Kp, F16, K, F, [&](int k, int f) { return wg[(size_t)k * F + f]; },
                 [&](int k, int f, float v) { Wl[k * Wp + f] = v; });
-    for (int f = threadIdx.x; f < 2 * F; f += kGatThreads)
-      al[f] = f < F ? p.a_src[(size_t)F * hd + f] : p.a_dst[(size_t)F * hd + f - F];
+    if ((int)threadIdx.x < 3 * F) al[threadIdx.x] = av;
+    for (int t = threadIdx.x + kGatThreads; t < 3 * F; t += kGatThreads)   // (F > 85)
+      al[t] = t < F ? p.a_src[(size_t)F * hd + t] : t < 2 * F ? p.a_dst[(size_t)F * hd + t - F]
+                                                             : (p.bias ? p.bias[t - 2 * F] : 0.f);
     __syncthreads();
+    GPMARK(2);
     // instance norm per feature over the segment's rows (in place)
+    // (one pass: fp64 sum and sum of squares -- exact enough for fp32 data
+    // that var = E[x^2] - mean^2 loses nothing at fp32 -- two chains each)
     for (int f0 = 0; f0 < K; f0 += 64) {
       const int f = f0 + fl;
       const bool fok = f < K;
-      double s = 0.0;
-      if (fok)
-        for (int r = ph; r < n; r += 4) s += (double)Xs[r * Ks + f];
-      red[ph][fl] = s;
+      double s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
+      if (fok) {
+        int r = ph;
+        for (; r + 4 < n; r += 8) {
+          const double x0 = Xs[r * Ks + f], x1 = Xs[(r + 4) * Ks + f];
+          s0 += x0;
+          s1 += x1;
+          q0 = fma(x0, x0, q0);
+          q1 = fma(x1, x1, q1);
+        }
+        if (r < n) {
+          const double x0 = Xs[r * Ks + f];
+          s0 += x0;
+          q0 = fma(x0, x0, q0);
+        }
+      }
+      red[ph][fl] = s0 + s1;
+      red[4 + ph][fl] = q0 + q1;
       __syncthreads();
       const double meand = ((red[0][fl] + red[1][fl]) + (red[2][fl] + red[3][fl])) / n;
+      const double sq = ((red[4][fl] + red[5][fl]) + (red[6][fl] + red[7][fl])) / n;
       __syncthreads();
       const float mean = (float)meand;
-      double qv = 0.0;
-      if (fok)
-        for (int r = ph; r < n; r += 4) {
-          const double d = (double)Xs[r * Ks + f] - meand;
-          qv = fma(d, d, qv);
-        }
-      red[ph][fl] = qv;
-      __syncthreads();
-      const double qs = (red[0][fl] + red[1][fl]) + (red[2][fl] + red[3][fl]);
-      __syncthreads();
-      const float rs = 1.f / sqrtf((float)(qs / n) + p.eps);
+      const double vard = sq - meand * meand;
+      const float rs = 1.f / sqrtf((float)(vard > 0.0 ? vard : 0.0) + p.eps);
       if (fok) {
         for (int r = ph; r < n; r += 4) {
           const float v = (Xs[r * Ks + f] - mean) * rs;
@@ -357,6 +461,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
       }
     }
     __syncthreads();
+    GPMARK(3);
     // Wh = Xn W_h: (row block, column tile) MFMA tiles over the waves
     const int nrb = nr >> 4, nct = F16 >> 4;
     for (int tile = wave; tile < nrb * nct; tile += kGatWaves) {
@@ -389,17 +494,22 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
       }
     }
     __syncthreads();
+    GPMARK(4);
     gat_scores(Ws, Fs, al, al + F, F, nullptr, 1, o, n, nr, ss, ts, lab);
     __syncthreads();
-    gat_attend<NM>(Ws, Fs, ss, ts, lab, o, n, nr, F, HF, c0, p.alpha, 1, p.epi, p.bias, p.hp, p.y, p.ldy);
+    GPMARK(5);
+    gat_attend<NM>(Ws, Fs, ss, ts, lab, o, n, nr, F, HF, c0, p.alpha, 1, p.epi, p.bias ? al + 2 * F : nullptr, p.hp,
+                   p.y, p.ldy);
+    GPMARK(6);
     __syncthreads();  // LDS reused by the next segment
+    GPMARK(7);
   }
 }
 
 static size_t gat_layer_lds(int K, int F, int max_seg) {
   const size_t nm = gat_r16(max_seg), Kp = gat_layer_kp(K);
-  return 4 * 64 * sizeof(double) +
-         sizeof(float) * (nm * (Kp + 1) + Kp * (((F + 15) & ~15) + 1) + nm * gat_fs(F) + 3 * nm + 2 * F) + 16;
+  return 8 * 64 * sizeof(double) +
+         sizeof(float) * (nm * (Kp + 1) + Kp * (((F + 15) & ~15) + 1) + nm * gat_fs(F) + 3 * nm + 3 * F) + 16;
 }
 
 // Backward.  Per row block (in the C layout: lane = column j, rows 4 (lane >>
@@ -420,8 +530,10 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
     const float* __restrict__ dy, int lddy, float* __restrict__ dWh, float* __restrict__ ds_out,
     float* __restrict__ dt_out, float* __restrict__ pda, double* __restrict__ pdb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int gfirst = min((int)blockIdx.x / heads, nseg);
+  const int tot = seg_off[nseg], ofirst = seg_off[gfirst], efirst = seg_off[min(gfirst + 1, nseg)];
   {  // rows past the last segment: zero gradients
-    const size_t r0 = seg_off[nseg], w = (size_t)heads * (F + 2);
+    const size_t r0 = tot, w = (size_t)heads * (F + 2);
     for (size_t e = r0 * w + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * w;
          e += (size_t)gridDim.x * kGatThreads) {
       const size_t r = e / w, c = e - r * w;
@@ -450,8 +562,8 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
   const int nct = (F + 15) >> 4;
   for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
     const int g = gh / heads, hd = gh - g * heads;
-    const int o = seg_off[g];
-    const int n = seg_off[g + 1] - o;
+    const int o = gh == (int)blockIdx.x ? ofirst : seg_off[g];
+    const int n = (gh == (int)blockIdx.x ? efirst : seg_off[g + 1]) - o;
     if (n <= 0) {
       for (int c = threadIdx.x; c < 3 * F; c += kGatThreads) {
         if (c < 2 * F) {
@@ -468,10 +580,9 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
     const int nr = gat_r16(n), nrb = nr >> 4;
     for (int f = threadIdx.x; f < 2 * F; f += kGatThreads)
       al[f] = f < F ? a_src[(size_t)lda * hd + f] : a_dst[(size_t)lda * hd + f - F];
-    stage_block(nr, F4, n, F, [&](int r, int f) { return Wh[(size_t)(o + r) * HF + c0 + f]; },
-                [&](int r, int f, float v) { Ws[r * Fs + f] = v; });
-    stage_block(
-        nr, F4, n, F,
+    stage_pair(
+        nr, F4, n, F, [&](int r, int f) { return Wh[(size_t)(o + r) * HF + c0 + f]; },
+        [&](int r, int f, float v) { Ws[r * Fs + f] = v; }, nr, F4, n, F,
         [&](int r, int f) {
           const size_t row = (size_t)(o + r);
           const float d = dy[row * lddy + c0 + f];
