@@ -220,14 +220,48 @@ __device__ void groups(const float* __restrict__ labels, int p0, int n, float* l
   if (lane == 0) ((int*)(lds + L.Mv))[0] = __popcll(lm);
 }
 
-// Xb[g][c] = (sum over g's members of X[p][c]) / |g|   (A X on the group rows)
-__device__ void group_mean_x(const SggGcnModArgs& a, int p0, int M, float* lds, const Geo& L) {
+// Xb[g][c] = (sum over g's members of X[p][c]) / |g|   (A X on the group rows).
+// The scene's X rows are first staged in the H1 region (free until
+// intra_fwd_h1) with 16 loads in flight per thread -- a member walk over
+// global rows waits a memory latency per load -- then summed from LDS.
+__device__ void group_mean_x(const SggGcnModArgs& a, int p0, int n, int M, float* lds, const Geo& L) {
   const int* goff = (const int*)(lds + L.goff);
   const int* gcnt = (const int*)(lds + L.gcnt);
   const int* mem = (const int*)(lds + L.mem);
   const float* inv = lds + L.inv;
   float* Xb = lds + L.Xb;
   const int fin = a.fin;
+  if (L.PX <= PH) {
+    float* Xs = lds + L.H1;   // n x fin at pitch PX (n PX <= np PH)
+    constexpr int kU = 16;
+    const int tot = n * fin;
+    for (int base = 0; base < tot; base += kU * kThreads) {
+      float v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = min(base + u * kThreads + (int)threadIdx.x, tot - 1);
+        const int r = e / fin, c = e - r * fin;
+        const bool second = a.X2 && c >= a.kx1;
+        v[u] = second ? a.X2[(size_t)(p0 + r) * a.ldx2 + (c - a.kx1)] : a.X[(size_t)(p0 + r) * a.ldx + c];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = base + u * kThreads + (int)threadIdx.x;
+        if (e < tot) {
+          const int r = e / fin, c = e - r * fin;
+          Xs[r * L.PX + c] = v[u];
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < M * fin; e += blockDim.x) {
+      const int g = e / fin, c = e - g * fin;
+      float s = 0.f;
+      for (int q = goff[g], qe = q + gcnt[g]; q < qe; ++q) s += Xs[mem[q] * L.PX + c];
+      Xb[g * L.PX + c] = s * inv[g];
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < M * fin; e += blockDim.x) {
     const int g = e / fin, c = e - g * fin;
     const bool second = a.X2 && c >= a.kx1;
@@ -297,20 +331,44 @@ __device__ __forceinline__ float cat_at(const float* lds, const Geo& L, int i, i
   return c < FO ? lds[L.H2 + g * PO + c] : lds[L.vG2 + c - FO] * lds[L.inv + g];
 }
 
+// the module's six weight arrays into LDS as one virtual concatenation, 16
+// loads in flight per thread (one load + one store per trip would wait a
+// memory latency per element)
 template <bool BF>
 __device__ void stage_weights(const SggGcnModArgs& a, float* lds, const Geo& L) {
-  auto put = [&](const float* src, int rows, int cols, int dst, int pitch) {
-    for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
-      const int r = e / cols, c = e - r * cols;
-      lds[dst + r * pitch + c] = src[e];
-    }
+  const int n0 = a.fin * FH, n1 = n0 + FH * FO, n2 = n1 + FO * FH, n3 = n2 + FH * FO, n4 = n3 + a.fe * FC,
+            tot = n4 + a.fe;
+  auto where = [&](int e, const float*& src, int& le, int& cols, int& dst, int& pitch) {
+    if (e < n0) { src = a.W0i; le = e; cols = FH; dst = L.W0i; pitch = PH; }
+    else if (e < n1) { src = a.W1i; le = e - n0; cols = FO; dst = L.W1i; pitch = PO; }
+    else if (e < n2) { src = a.W0g; le = e - n1; cols = FH; dst = L.W0g; pitch = PH; }
+    else if (e < n3) { src = a.W1g; le = e - n2; cols = FO; dst = L.W1g; pitch = PO; }
+    else if (e < n4) { src = a.Woe; le = e - n3; cols = FC; dst = L.Woe; pitch = PC; }
+    else { src = a.boe; le = e - n4; cols = a.fe; dst = L.boe; pitch = 0; }
   };
-  put(a.W0i, a.fin, FH, L.W0i, PH);
-  put(a.W1i, FH, FO, L.W1i, PO);
-  put(a.W0g, FO, FH, L.W0g, PH);
-  put(a.W1g, FH, FO, L.W1g, PO);
-  put(a.Woe, a.fe, FC, L.Woe, PC);
-  put(a.boe, 1, a.fe, L.boe, 0);
+  constexpr int kU = 16;
+  for (int base = 0; base < tot; base += kU * kThreads) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = min(base + u * kThreads + (int)threadIdx.x, tot - 1);
+      const float* src;
+      int le, cols, dst, pitch;
+      where(e, src, le, cols, dst, pitch);
+      v[u] = src[le];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = base + u * kThreads + (int)threadIdx.x;
+      if (e < tot) {
+        const float* src;
+        int le, cols, dst, pitch;
+        where(e, src, le, cols, dst, pitch);
+        const int r = le / cols, c = le - r * cols;
+        lds[dst + r * pitch + c] = v[u];
+      }
+    }
+  }
 }
 
 // the per-batch fields of a forward: batch a's, or (two) the second batch's
@@ -346,7 +404,7 @@ __global__ void __launch_bounds__(kThreads) gcnmod_fwd_kernel(const SggGcnModArg
     if (threadIdx.x < 64) groups(a.labels, p0, n, lds, L);
     __syncthreads();
     const int M = ((const int*)(lds + L.Mv))[0];
-    group_mean_x(a, p0, M, lds, L);
+    group_mean_x(a, p0, n, M, lds, L);
     __syncthreads();
     intra_fwd_h1<BF>(M, a.fin, lds, L);
     __syncthreads();
@@ -390,17 +448,37 @@ __global__ void __launch_bounds__(kThreads) gcnmod_bwd_kernel(const SggGcnModArg
     if (wave == 0) {
       groups(a.labels, p0, n, lds, L);
     } else {
-      for (int e = threadIdx.x - 64; e < n * fe; e += blockDim.x - 64) {
-        const int r = e / fe, c = e - r * fe;
-        const float* src = a.dy + (size_t)(p0 + r) * a.lddy + c;
-        float v = src[0];
-        for (int k = 1; k < copies; ++k) v += src[(size_t)k * a.dy_cstride];
-        dY[r * L.PE + c] = v;
+      // 8 elements per thread in flight, one copy at a time (the copies
+      // summed in order, as one element at a time did)
+      constexpr int kU = 8;
+      const int tot = n * fe, nt = kThreads - 64, t = threadIdx.x - 64;
+      for (int base = 0; base < tot; base += kU * nt) {
+        const float* src[kU];
+        float v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int e = min(base + u * nt + t, tot - 1);
+          const int r = e / fe, c = e - r * fe;
+          src[u] = a.dy + (size_t)(p0 + r) * a.lddy + c;
+          v[u] = src[u][0];
+        }
+        for (int k = 1; k < copies; ++k) {
+#pragma unroll
+          for (int u = 0; u < kU; ++u) v[u] += src[u][(size_t)k * a.dy_cstride];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int e = base + u * nt + t;
+          if (e < tot) {
+            const int r = e / fe, c = e - r * fe;
+            dY[r * L.PE + c] = v[u];
+          }
+        }
       }
     }
     __syncthreads();
     const int M = ((const int*)(lds + L.Mv))[0];
-    group_mean_x(a, p0, M, lds, L);
+    group_mean_x(a, p0, n, M, lds, L);
     __syncthreads();
     intra_fwd_h1<BF>(M, fin, lds, L);
     __syncthreads();
