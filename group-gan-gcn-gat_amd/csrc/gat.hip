@@ -89,79 +89,6 @@ __device__ __forceinline__ void stage_block(int rows, int cols, int nv, int cv, 
 // softmax needs two cross-lane steps per reduction and the aggregation
 // att @ Wh reads only Wh (LDS) -- no attention matrix is stored.
 
-// two blocks staged together (both blocks' loads in flight before any store:
-// one memory round trip per batch instead of two)
-template <typename LdA, typename StA, typename LdB, typename StB>
-__device__ __forceinline__ void stage_pair(int rowsA, int colsA, int nvA, int cvA, LdA ldA, StA stA, int rowsB,
-                                           int colsB, int nvB, int cvB, LdB ldB, StB stB) {
-  constexpr int kU = 16;
-  const int totA = rowsA * colsA, totB = rowsB * colsB;
-  const int dqA = kGatThreads / colsA, drA = kGatThreads - dqA * colsA;
-  const int dqB = kGatThreads / colsB, drB = kGatThreads - dqB * colsB;
-  for (int base = 0; base < totA || base < totB; base += kU * kGatThreads) {
-    const int e0 = base + (int)threadIdx.x;
-    const int rA0 = e0 / colsA, cA0 = e0 - rA0 * colsA;
-    const int rB0 = e0 / colsB, cB0 = e0 - rB0 * colsB;
-    float va[kU], vb[kU];
-    int r = rA0, c = cA0;
-    const bool doA = base < totA, doB = base < totB;
-    if (doA) {
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        va[u] = keep_if(ldA(min(r, nvA - 1), min(c, cvA - 1)), r < nvA && c < cvA);
-        r += dqA;
-        c += drA;
-        if (c >= colsA) {
-          c -= colsA;
-          ++r;
-        }
-      }
-    }
-    r = rB0;
-    c = cB0;
-    if (doB) {
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        vb[u] = keep_if(ldB(min(r, nvB - 1), min(c, cvB - 1)), r < nvB && c < cvB);
-        r += dqB;
-        c += drB;
-        if (c >= colsB) {
-          c -= colsB;
-          ++r;
-        }
-      }
-    }
-    r = rA0;
-    c = cA0;
-    if (doA) {
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        if (e0 + u * kGatThreads < totA) stA(r, c, va[u]);
-        r += dqA;
-        c += drA;
-        if (c >= colsA) {
-          c -= colsA;
-          ++r;
-        }
-      }
-    }
-    r = rB0;
-    c = cB0;
-    if (doB) {
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        if (e0 + u * kGatThreads < totB) stB(r, c, vb[u]);
-        r += dqB;
-        c += drB;
-        if (c >= colsB) {
-          c -= colsB;
-          ++r;
-        }
-      }
-    }
-  }
-}
-
 // s_i = Wh_i . a_src, t_i = Wh_i . a_dst (a_s / a_d: LDS copies) and the
 // labels of rows [0, nr) (Ws rows >= n are zero): each row's dot products
 // split over 256 / nr lanes (a shuffle tree joins them); the caller barriers
@@ -580,9 +507,10 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
     const int nr = gat_r16(n), nrb = nr >> 4;
     for (int f = threadIdx.x; f < 2 * F; f += kGatThreads)
       al[f] = f < F ? a_src[(size_t)lda * hd + f] : a_dst[(size_t)lda * hd + f - F];
-    stage_pair(
-        nr, F4, n, F, [&](int r, int f) { return Wh[(size_t)(o + r) * HF + c0 + f]; },
-        [&](int r, int f, float v) { Ws[r * Fs + f] = v; }, nr, F4, n, F,
+    stage_block(nr, F4, n, F, [&](int r, int f) { return Wh[(size_t)(o + r) * HF + c0 + f]; },
+                [&](int r, int f, float v) { Ws[r * Fs + f] = v; });
+    stage_block(
+        nr, F4, n, F,
         [&](int r, int f) {
           const size_t row = (size_t)(o + r);
           const float d = dy[row * lddy + c0 + f];
