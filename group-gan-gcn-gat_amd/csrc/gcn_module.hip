@@ -28,6 +28,15 @@
 // sgg_slab_reduce sums in row order.
 #include "sgg_common.h"
 
+// phase timestamps of workgroup 0's first scene (tools/gcnmod_probe.hip)
+#ifdef SGG_GCN_PROF
+__device__ long long g_gcn_prof[64];
+#define CPMARK(i) \
+  if (threadIdx.x == 0 && blockIdx.x == 0 && first) g_gcn_prof[i] = wall_clock64();
+#else
+#define CPMARK(i)
+#endif
+
 namespace sgg {
 
 namespace {
@@ -186,8 +195,9 @@ __device__ void groups(const float* __restrict__ labels, int p0, int n, float* l
   const bool act = lane < n;
   const float li = act ? labels[p0 + lane] : 0.f;
   int l = lane;
+  // (j is uniform: readlane, a VALU read, instead of a shuffle's LDS round trip)
   for (int j = 0; j < n; ++j) {   // the first member with the same nonzero label (:651-657)
-    const float lj = __shfl(li, j);
+    const float lj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(li), j));
     if (j < lane && l == lane && li != 0.f && lj == li) l = j;
   }
   const bool lead = act && l == lane;
@@ -195,7 +205,7 @@ __device__ void groups(const float* __restrict__ labels, int p0, int n, float* l
   const int rank = __popcll(lm & ((1ull << lane) - 1ull));
   int cnt = 0, before = 0;
   for (int j = 0; j < n; ++j) {
-    const int lj = __shfl(l, j);
+    const int lj = __builtin_amdgcn_readlane(l, j);
     cnt += lj == lane;
     before += (j < lane) & (lj == l);
   }
@@ -430,10 +440,14 @@ __global__ void __launch_bounds__(kThreads) gcnmod_bwd_kernel(const SggGcnModArg
   float* slab = a.slab + (size_t)blockIdx.x * P.total;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fin = a.fin, fe = a.fe;
+#ifdef SGG_GCN_PROF
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_gcn_prof[0] = wall_clock64();
+#endif
   stage_weights<BF>(a, lds, L);
   bool first = true;   // the workgroup's first scene writes its slab row, later ones add
   auto acc = [&](int off, float v) { float* p = slab + off; *p = first ? v : *p + v; };
   const int copies = a.dy_copies > 1 ? a.dy_copies : 1;
+  CPMARK(1);
   for (int s = blockIdx.x; s < a.S; s += gridDim.x) {
     const int p0 = a.scene_off[s], n = a.scene_off[s + 1] - p0;
     if (n <= 0) continue;
@@ -477,19 +491,23 @@ __global__ void __launch_bounds__(kThreads) gcnmod_bwd_kernel(const SggGcnModArg
       }
     }
     __syncthreads();
+    CPMARK(2);
     const int M = ((const int*)(lds + L.Mv))[0];
     group_mean_x(a, p0, n, M, lds, L);
     __syncthreads();
+    CPMARK(3);
     intra_fwd_h1<BF>(M, fin, lds, L);
     __syncthreads();
     intra_fwd_h2<BF>(M, lds, L);
     __syncthreads();
+    CPMARK(4);
     // wave 0: the inter GCN; waves 1..3: dcat = dY Woe
     const float* Woe = lds + L.Woe;
     if (wave == 0) inter_fwd<BF>(M, lds, L);
     mm<false>(n, FC, fe, 1, kWaves - 1, [&](int r, int k) { return dY[min(r, n - 1) * L.PE + k]; },
               [&](int k, int c) { return Woe[k * PC + c]; }, [&](int r, int c, float v) { dcat[r * PC + c] = v; });
     __syncthreads();
+    CPMARK(5);
     const float* H1 = lds + L.H1;
     const float* H2 = lds + L.H2;
     const float* Xb = lds + L.Xb;
@@ -544,6 +562,7 @@ __global__ void __launch_bounds__(kThreads) gcnmod_bwd_kernel(const SggGcnModArg
       }
     }
     __syncthreads();
+    CPMARK(6);
     // Dg = (Sg + dgin) [H2 > 0] (each member's dintra plus its share of
     // dgin, summed over the group); dW1' += G1 (x) D2; dW0' += m (x) E1
     for (int e = threadIdx.x; e < M * FO + 2 * FH * FO; e += blockDim.x) {
@@ -559,6 +578,7 @@ __global__ void __launch_bounds__(kThreads) gcnmod_bwd_kernel(const SggGcnModArg
       }
     }
     __syncthreads();
+    CPMARK(7);
     // intra layer 2: dW1 += H1^T Dg; Eg = (Dg W1^T) [H1 > 0]
     float* Eg = lds + L.Eg;
     const float* W1i = lds + L.W1i;
@@ -568,6 +588,7 @@ __global__ void __launch_bounds__(kThreads) gcnmod_bwd_kernel(const SggGcnModArg
               [&](int c, int k) { return W1i[min(k, FH - 1) * PO + c]; },
               [&](int g, int k, float v) { Eg[g * PH + k] = H1[g * PH + k] > 0.f ? v : 0.f; });
     __syncthreads();
+    CPMARK(8);
     // intra layer 1: dW0 += Xb^T Eg; dX_p = (Eg W0^T)[g(p)] / |g(p)| for every member p
     const float* W0i = lds + L.W0i;
     mm<false>(fin, FH, M, 0, 2, [&](int k, int g) { return Xb[g * L.PX + min(k, fin - 1)]; },
@@ -582,8 +603,9 @@ __global__ void __launch_bounds__(kThreads) gcnmod_bwd_kernel(const SggGcnModArg
                 const int ld = second ? a.lddx2 : a.lddx;
                 for (int q = goff[g], qe = q + gcnt[g]; q < qe; ++q) dst[(size_t)(p0 + mem[q]) * ld] = d;
               });
-    first = false;
     __syncthreads();
+    CPMARK(9);
+    first = false;
   }
   if (first) {   // no non-empty scene: the row still enters the sum
     for (int e = threadIdx.x; e < P.total; e += blockDim.x) slab[e] = 0.f;
