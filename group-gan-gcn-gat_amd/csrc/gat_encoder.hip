@@ -921,7 +921,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         int g = i, r = 0, c = 1, m = 0;
         while (rem) {   // wave-uniform
           const int lead = __ffsll((long long)rem) - 1;
-          const float ll = __shfl(li, lead);
+          const float ll = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(li), lead));   // (lead: uniform)
           const unsigned long long same = ll != 0.f ? __ballot(in && li == ll) : (1ull << lead);
           if ((same >> i) & 1ull) {
             g = lead;
