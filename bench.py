@@ -319,10 +319,12 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
         t0 = time.perf_counter()
         scenes = 0
         marks = [t0]
+        steps_info = []
         for _ in range(iters):
             if mode == "graphed":
                 sd, sg = next(it), next(it)
                 bt.step(sd, sg)
+                steps_info.append(bt.last)
                 scenes += len(sd)
             else:
                 (bd, scd), (bg, scg) = next(it), next(it)
@@ -340,6 +342,12 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
         if bt is not None:
             out[mode].update(buckets=sorted([list(k) for k in bt.buckets]), eager_fallback_steps=bt.eager_steps,
                              warm_epoch_s=round(t_cap, 2), warm_iterations=n_warm)
+            # the slowest timed iteration: its bucket and that bucket's replays before it
+            its = [b - a for a, b in zip(marks, marks[1:])]
+            k = max(range(len(its)), key=lambda i: its[i])
+            out[mode]["slowest_iteration"] = {"index": k, "host_ms": round(its[k] * 1e3, 3),
+                                              "bucket": list(steps_info[k][0]),
+                                              "bucket_prior_replays": steps_info[k][1]}
         del tr, g, d, bt
     return {"metric": "train-scenes/s on real data (D-step scenes per second; the G-step takes the next loader "
                       "batch)", "split": "zara1 train",

@@ -918,6 +918,10 @@ class BucketedGraphTrainer:
         ent = self.buckets.get(key)
         if ent is None:
             ent = self.buckets[key] = self._capture(key, off_d, rows_d, off_g, rows_g)
+            ent["replays"] = 0
+        # (diagnostics: this step's bucket and its replays before this one)
+        self.last = (key, ent["replays"])
+        ent["replays"] += 1
         ent["sc_d"].load(off_d, rows_d)
         ent["sc_g"].load(off_g, rows_g)
         ent["state"]["S_real"] = (len(off_d) - 1, len(off_g) - 1)
