@@ -34,6 +34,7 @@ Prints ONE JSON line (rank 0).  Extra objects:
                (512 scenes).
 """
 import argparse
+import glob
 import json
 import os
 import socket
@@ -59,8 +60,9 @@ GRAPH_ITERS = int(os.environ.get("SGG_GRAPH_ITERS", "4"))   # iterations per HIP
 # one rank: the G-step's prefix graph beside the D-step graph on a second
 # stream (GraphedTrainer(overlap=True))
 OVERLAP = os.environ.get("SGG_OVERLAP", "0") == "1"
-# PMC traffic tables (tools/pmc_traffic.py), newest first
-TRAFFIC_TABLES = [os.path.join(ROOT, "profiles", f) for f in ("r03_pmc_traffic.json", "r02_pmc_traffic.json")]
+# PMC traffic tables (tools/pmc_traffic.py), every round's, newest first
+# (rNN[_x]_pmc_traffic.json sorts by round, then by the round's run letter)
+TRAFFIC_TABLES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")), reverse=True)
 # the reference's CPU path, train iteration at batch 64, 8 threads (the survey container)
 REFERENCE_CPU_SCENES_S = 13.9
 
@@ -316,6 +318,8 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
                 K.GATENC_FUSED = True
         torch.cuda.synchronize()
         t_cap = time.perf_counter() - t_cap
+        frozen = K.gc_frozen()   # the captured graphs' state out of the collector's scans (scoped)
+        frozen.__enter__()
         t0 = time.perf_counter()
         scenes = 0
         marks = [t0]
@@ -334,6 +338,7 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
             marks.append(time.perf_counter())
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        frozen.__exit__(None, None, None)
         # host-side iteration times (eager issue is host-bound; a first-use
         # stall -- a kernel's code object loaded at its first launch -- is an outlier)
         per = sorted(b - a for a, b in zip(marks, marks[1:]))
@@ -346,7 +351,8 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
             its = [b - a for a, b in zip(marks, marks[1:])]
             k = max(range(len(its)), key=lambda i: its[i])
             out[mode]["slowest_iteration"] = {"index": k, "host_ms": round(its[k] * 1e3, 3),
-                                              "bucket": list(steps_info[k][0]),
+                                              "bucket": (list(steps_info[k][0]) if steps_info[k][0] is not None
+                                                         else "eager"),
                                               "bucket_prior_replays": steps_info[k][1]}
         del tr, g, d, bt
     return {"metric": "train-scenes/s on real data (D-step scenes per second; the G-step takes the next loader "
@@ -387,9 +393,12 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
             gk = None
             if GRAPH_ITERS > 1 and world == 1:
                 # (the timed trainer draws each replay's host RNG numbers
-                # while the previous replay runs: GraphedTrainer draw_ahead)
+                # while the previous replay runs: GraphedTrainer draw_ahead;
+                # both trainers take their draws from ONE DrawSource, so the
+                # remainder iterations of g1 consume those draws in order and
+                # every iteration sees the reference's host RNG sequence)
                 gk = GraphedTrainer(trainer, batch, sc, warmup=0, batch_g=batch_g, sc_g=sc_g, iters=GRAPH_ITERS,
-                                    draw_ahead=True,
+                                    draw_ahead=True, draws=g1.draws,
                                     overlap=OVERLAP, **kw)
 
             if gk is not None:   # both graphs replayed once before any timing (first-replay costs)
@@ -655,8 +664,14 @@ def main():
             "scaling": "weak" if world == 1 else "strong",
             "vs_baseline": round(value / REFERENCE_CPU_SCENES_S, 1) if is_c1 else None,
             "vs_baseline_basis": "value / 13.9 scenes/s: the reference's own CPU path on this workload (train "
-                                 "iteration, batch 64, 8 threads), BASELINE.md section 2 -- the reference publishes "
-                                 "no throughput" if is_c1 else None,
+                                 "iteration, batch 64, 8 threads of the SURVEY container's Xeon -- another machine), "
+                                 "BASELINE.md section 2; the reference publishes no throughput; vs_cpu_same_box is "
+                                 "the ratio on this box" if is_c1 else None,
+            # the same box: the GPU rate over the CPU baseline timed above on
+            # this machine's host cores, beside vs_baseline
+            "vs_cpu_same_box": round(value / cpu["value"], 1) if cpu else None,
+            "vs_cpu_same_box_basis": ("value / cpu_baseline.value: the oracle's reference formulation on %d host "
+                                      "cores of this box (%s)" % (cpu["cores"], cpu["cpu_model"])) if cpu else None,
             "dtype": head["prec"],
             "data": "synthetic (random-init weights, SURVEY.md 8d recipe)",
             "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam) of the %s generator "

@@ -249,7 +249,9 @@ __global__ void __launch_bounds__(kGatThreads) gat_fwd_kernel(
   for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
     const int g = gh / heads, hd = gh - g * heads;
     const int o = seg_off[g];
-    const int n = seg_off[g + 1] - o;
+    // (a segment larger than the caller's max_seg would overrun the LDS plan:
+    // clamped, memory-safe; the host builds max_seg from the same offsets)
+    const int n = min(seg_off[g + 1] - o, nmax);
     if (n <= 0) continue;
     const int c0 = hd * F;
     const int nr = gat_r16(n);
@@ -319,7 +321,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
   for (int gh = blockIdx.x; gh < p.nseg * p.heads; gh += gridDim.x) {
     const int g = gh / p.heads, hd = gh - g * p.heads;
     const int o = gh == (int)blockIdx.x ? ofirst : p.seg_off[g];
-    const int n = (gh == (int)blockIdx.x ? efirst : p.seg_off[g + 1]) - o;
+    const int n = min((gh == (int)blockIdx.x ? efirst : p.seg_off[g + 1]) - o, nmax);   // (LDS plan bound)
     if (n <= 0) continue;
     const int c0 = hd * F;
     const int nr = gat_r16(n);
@@ -490,7 +492,7 @@ __global__ void __launch_bounds__(kGatThreads) gat_bwd_kernel(
   for (int gh = blockIdx.x; gh < nseg * heads; gh += gridDim.x) {
     const int g = gh / heads, hd = gh - g * heads;
     const int o = gh == (int)blockIdx.x ? ofirst : seg_off[g];
-    const int n = (gh == (int)blockIdx.x ? efirst : seg_off[g + 1]) - o;
+    const int n = min((gh == (int)blockIdx.x ? efirst : seg_off[g + 1]) - o, nmax);   // (LDS plan bound)
     if (n <= 0) {
       for (int c = threadIdx.x; c < 3 * F; c += kGatThreads) {
         if (c < 2 * F) {

@@ -11,7 +11,11 @@ import os
 
 import torch  # noqa: F401  (must precede the dlopen below)
 
-# SGG_LIB: another build of the same library (A/B runs of kernel variants, tools/)
+from ._srchash import source_hash
+
+# SGG_LIB: another build of the same library (A/B runs of kernel variants,
+# tools/); only such an explicit choice skips the source-hash check in load()
+_LIB_EXPLICIT = bool(os.environ.get("SGG_LIB"))
 _LIB_PATH = os.environ.get("SGG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libsgg.so")
 
 _i = ctypes.c_int
@@ -122,6 +126,7 @@ class BceJob(ctypes.Structure):
 SIGNATURES = {
     "sgg_version": (_i, []),
     "sgg_last_error": (ctypes.c_char_p, []),
+    "sgg_source_hash": (ctypes.c_char_p, []),
     "sgg_xw": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
     "sgg_xw_bf16": (_i, [_p, _i, _p, _i, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _p]),
     "sgg_pool_plan": (_i, [_p, _i, _i, _i, _i, _p, _i, _p, _p]),
@@ -219,8 +224,15 @@ def lib_path():
     return _LIB_PATH
 
 
+def built_hash():
+    """The source hash compiled into the loaded library."""
+    return load(require_gpu=False).sgg_source_hash().decode()
+
+
 def load(require_gpu=True):
-    """Load libsgg.so (once).  Raises NativeError when it is missing or, with
+    """Load libsgg.so (once).  Raises NativeError when it is missing, when it
+    was built from other sources than this tree's (`sgg_source_hash()` vs
+    `_srchash.source_hash()`; skipped only for an explicit SGG_LIB) or, with
     require_gpu, when no HIP device is visible: there is no fallback."""
     global _lib
     if _lib is None:
@@ -232,6 +244,12 @@ def load(require_gpu=True):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if not _LIB_EXPLICIT:
+            built, tree = lib.sgg_source_hash().decode(), source_hash()
+            if built != tree:
+                raise NativeError("%s was built from other sources (hash %s) than this tree's csrc/ + "
+                                  "include/sgg.h (%s) -- rebuild with group-gan-gcn-gat_amd/build_native.py"
+                                  % (_LIB_PATH, built[:16], tree[:16]))
         _lib = lib
     if require_gpu and not torch.cuda.is_available():
         raise NativeError("sgan: no HIP device visible; the MI355X kernels have no CPU fallback")

@@ -28,6 +28,10 @@ DUAL_POOL_BWD = os.environ.get("SGG_DUAL_POOL_BWD", "1") != "0"
 SIDE_STREAM = os.environ.get("SGG_SIDE_STREAM", "0") == "1"
 
 
+# SGG_DEBUG=1: host-side consistency checks that cost a device read
+DEBUG = os.environ.get("SGG_DEBUG", "0") == "1"
+
+
 def _lib():
     return N.load()
 
@@ -990,15 +994,8 @@ def capture_guard():
     through a reference cycle is destroyed whenever the collector happens to
     run; if that is inside another capture, ~CUDAGraph's synchronisation is
     illegal on the capturing stream and the process aborts (the round-3
-    hipErrorStreamCaptureUnsupported).
-
-    After a capture every object alive is moved to the collector's permanent
-    generation (gc.freeze): the captured graphs and the step state they keep
-    (autograd nodes, staging buffers) live as long as the trainer, and a full
-    collection re-scanning them costs milliseconds on the host while the
-    replayed iterations take a fraction of one (the real-data leg's slow
-    iterations, DESIGN.md section 5).  Reference counting still frees them;
-    only cyclic garbage among them would wait for gc.unfreeze()."""
+    hipErrorStreamCaptureUnsupported).  Nothing outlives
+    the capture: the collector's state is restored as it was."""
     import gc
     gc.collect()
     was = gc.isenabled()
@@ -1006,9 +1003,29 @@ def capture_guard():
     try:
         yield
     finally:
-        gc.freeze()
         if was:
             gc.enable()
+
+
+@contextlib.contextmanager
+def gc_frozen():
+    """Scope in which every object alive at entry (captured graphs and the
+    step state they keep) sits in the collector's permanent generation, so a
+    full collection during a replay loop does not re-scan them (milliseconds
+    of host time against sub-millisecond replays).  Opt-in and scoped: the
+    objects frozen here are unfrozen at exit, so cyclic garbage among them is
+    collected as usual afterwards.  When the process already froze objects
+    itself, its freeze is left alone (nothing frozen or unfrozen here)."""
+    import gc
+    own = gc.get_freeze_count() == 0
+    if own:
+        gc.collect()
+        gc.freeze()
+    try:
+        yield
+    finally:
+        if own:
+            gc.unfreeze()
 
 
 class LaunchTimer:
@@ -2062,6 +2079,13 @@ class SegmentGraph:
 
     def __init__(self, seg_off, nseg, max_seg, mode, labels=None):
         self.seg_off, self.nseg, self.max_seg, self.mode, self.labels = seg_off, nseg, max_seg, mode, labels
+        # the kernels size their LDS plan by max_seg (and clamp a larger
+        # segment, memory-safe but wrong): SGG_DEBUG=1 checks it against the
+        # offsets (one device read per graph)
+        if DEBUG and nseg > 0:
+            big = int((seg_off[1:nseg + 1] - seg_off[:nseg]).max())
+            if big > max_seg:
+                raise ValueError("SegmentGraph: a segment of %d nodes exceeds max_seg %d" % (big, max_seg))
 
 
 # ---------------------------------------------------------------------------

@@ -39,6 +39,7 @@ The result equals single-GPU training on the global batch up to summation
 order.
 """
 import contextlib
+import collections
 import functools
 import os
 import random
@@ -536,6 +537,37 @@ class GanTrainer:
         return z_d, zg, torch.tensor([yr, yf, yg], dtype=torch.float32)
 
 
+class DrawSource:
+    """The host RNG draws of consecutive iterations, in order, with look-ahead.
+    `ahead(n)` makes sure the next n iterations' draws exist (drawing them now
+    if needed) and returns them with the sequence number of the first;
+    `pop(n)` consumes them.  Trainers replaying the same training run share
+    one source, so a draw made ahead by one (GraphedTrainer draw_ahead) is
+    the draw the next iteration uses whichever trainer runs it: the host RNG
+    streams are advanced exactly in the reference's iteration order."""
+
+    def __init__(self, draw):
+        self.draw = draw
+        self.pending = collections.deque()
+        self.seq = 0          # sequence number of pending[0]
+
+    def ahead(self, n):
+        while len(self.pending) < n:
+            self.pending.append(self.draw())
+        return self.seq, [self.pending[j] for j in range(n)]
+
+    def pop(self, n):
+        for _ in range(n):
+            self.pending.popleft()
+        self.seq += n
+
+    def take(self):
+        self.ahead(1)
+        item = self.pending[0]
+        self.pop(1)
+        return item
+
+
 class GraphedTrainer:
     """One full iteration (D-step + G-step, both Adam updates) captured once
     into a HIP graph and replayed; with several ranks, three graph segments
@@ -549,9 +581,11 @@ class GraphedTrainer:
     device)."""
 
     def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2, batch_g=None,
-                 sc_g=None, draw=None, prologue=None, iters=1, overlap=False, draw_ahead=False):
+                 sc_g=None, draw=None, prologue=None, iters=1, overlap=False, draw_ahead=False, draws=None):
         """draw: () -> (z_d, z_g, y) host tensors of the staging shapes (default:
-        trainer.draw_inputs over this rank's span); prologue: launches captured
+        trainer.draw_inputs over this rank's span); draws: a DrawSource shared
+        with other trainers of the same run (default: one over `draw`);
+        prologue: launches captured
         ahead of the step (the padded real-data path's batch gathers).
         iters (one rank): iterations per graph -- a replay runs `iters`
         consecutive iterations on the same batches (their host draws made in
@@ -579,7 +613,9 @@ class GraphedTrainer:
         self.span = (self.kw["S_global"], s0, s0 + sc.S)
         # (no closure over self anywhere in this object: a GraphedTrainer must
         # never sit in a reference cycle, see kernels.capture_guard)
-        self.draw = draw or functools.partial(trainer.draw_inputs, *self.span)
+        self.draws = draws if draws is not None else DrawSource(
+            draw or functools.partial(trainer.draw_inputs, *self.span))
+        self.draw = self.draws.take
         G = trainer.G
         nd = tuple(G.noise_dim) if G.noise_dim else None
         k = trainer.args.best_k
@@ -597,13 +633,15 @@ class GraphedTrainer:
         self.stage_ev = [None, None]
         self.cur = 0
         # draw_ahead (one rank): the host draws of the next replay are made
-        # right after this replay is queued (the same draw sequence of THIS
-        # trainer, one replay earlier in wall-clock time), so a replay never
-        # waits for the host RNG.  Off by default: with it, code that draws
-        # from the host RNG between steps (another trainer, e.g. the
-        # bucketed real-data one) sees the state one replay ahead
+        # right after this replay is queued (taken ahead from the DrawSource,
+        # so the sequence is unchanged), and a replay never waits for the
+        # host RNG.  A trainer sharing the source that runs an iteration in
+        # between consumes the first of those draws; the staged buffer is then
+        # refilled at the next replay.  Off by default: code that draws from
+        # the host RNG OUTSIDE the source between steps would see the state
+        # one replay ahead
         self.draw_ahead = draw_ahead
-        self.drawn = [False, False]
+        self.staged = [None, None]   # DrawSource sequence number each staging buffer holds
         self.inp_flat = torch.zeros(iters * per, device=dev)
         self.inps = [StepInputs(v[0], v[1], v[2]) if nd else StepInputs(None, None, v[0]) for v in blocks(self.inp_flat)]
         self.inp = self.inps[0]
@@ -761,19 +799,22 @@ class GraphedTrainer:
         self.stage_ev[i] = ev
 
     def _fill(self, i):
-        """The host draws of graph i's next replay into its staging buffer,
-        once graph i's previous replay (which read that buffer) is done."""
+        """The host draws of graph i's next replay (the next `iters` draws of
+        the source, in order) into its staging buffer, once graph i's previous
+        replay (which read that buffer) is done; nothing if it holds them."""
+        seq, items = self.draws.ahead(self.iters)
+        if self.staged[i] == seq:
+            return
         if self.done_ev[i] is not None:
             self.done_ev[i].synchronize()
-        for j in range(self.iters):           # the replay's iterations' draws, in order
-            z_d, z_g, y = self.draw()
+        for j, (z_d, z_g, y) in enumerate(items):
             h_zd, h_zg, h_y = self.stage[i][j]
             if z_d is not None:
                 h_zd.copy_(z_d)
             if z_g is not None:
                 h_zg.copy_(z_g)
             h_y.copy_(y)
-        self.drawn[i] = True
+        self.staged[i] = seq
 
     def step(self):
         """Draw this iteration's host RNG numbers, replay the graph; returns the
@@ -781,8 +822,8 @@ class GraphedTrainer:
         if self.pair:
             i = self.cur
             self.cur ^= 1
-            if not self.drawn[i]:
-                self._fill(i)
+            self._fill(i)
+            self.draws.pop(self.iters)
             g, self.losses, grads = self.pair[i]
             if self.overlap:
                 self._replay_overlap(*g)
@@ -791,7 +832,7 @@ class GraphedTrainer:
             ev = torch.cuda.Event()
             ev.record()
             self.done_ev[i] = ev
-            self.drawn[i] = False
+            self.staged[i] = None
             if self.draw_ahead:   # the next replay's draws while this one runs
                 self._fill(i ^ 1)
             self._after_replay(grads)
@@ -884,6 +925,9 @@ class BucketedGraphTrainer:
         self.gran, self.np_caps, self.pool_cap = gran, tuple(sorted(np_caps)), pool_cap
         self.buckets = {}
         self.eager_steps = 0
+        # (diagnostics: the last step's bucket and its replays before it, or
+        # (None, "eager") for a batch pair no bucket holds)
+        self.last = None
 
     def bucket_of(self, off_d, off_g):
         """(B_cap, np_cap) of the bucket holding both batches, or None."""
@@ -912,6 +956,7 @@ class BucketedGraphTrainer:
         key = self.bucket_of(off_d, off_g)
         if key is None:
             self.eager_steps += 1
+            self.last = (None, "eager")
             bd, scd = self.dd.batch(scenes_d)
             bg, scg = self.dd.batch(scenes_g)
             return self.t.step(bd, scd, bg, scg)
@@ -919,7 +964,6 @@ class BucketedGraphTrainer:
         if ent is None:
             ent = self.buckets[key] = self._capture(key, off_d, rows_d, off_g, rows_g)
             ent["replays"] = 0
-        # (diagnostics: this step's bucket and its replays before this one)
         self.last = (key, ent["replays"])
         ent["replays"] += 1
         ent["sc_d"].load(off_d, rows_d)

@@ -30,9 +30,13 @@ extern "C" {
 
 #define SGG_E_ARG (-1)
 
-/* Library version / self description. */
+/* Library version / self description.  sgg_source_hash(): SHA-256 (hex) of
+ * the csrc/*.hip, csrc/*.h and include/sgg.h the library was built from
+ * (build_native.py); the Python loader refuses a library whose hash differs
+ * from the tree it runs in. */
 int sgg_version(void);
 const char* sgg_last_error(void);
+const char* sgg_source_hash(void);
 
 /* Upper bounds the kernels are built for (checked on every call). */
 #define SGG_POOL_MAX_PEDS 64   /* peds per scene held LDS-resident by the pooling kernel      */

@@ -117,3 +117,66 @@ def test_custom_bce_pair_total_loss_equals_default():
     for k in a:
         assert abs(a[k] - c[k]) <= 1e-5 * max(1.0, abs(a[k])), (k, a[k], c[k])
     assert abs(c["G_total_loss"] - (c["G_l2_loss_rel"] + c["G_discriminator_loss"])) <= 1e-5 * abs(c["G_total_loss"])
+
+
+def test_decoder_init_rejects_mismatched_shapes_before_launch(monkeypatch):
+    """The round-4 fault: the eager real-data pairing
+    handed the G batch (more scenes) the D batch's noise, and the decoder's
+    prologue read z[k][s] past its scene count.  decoder_init checks noise,
+    context rows and last_rel against the scenes on the host: ValueError,
+    and no launch is attempted (the library is unreachable in this test)."""
+    from sgan import kernels as K
+    from sgan.scene import SceneIndex
+    sc = SceneIndex([0, 3, 7], DEV)                      # S = 2 scenes, B = 7 peds
+    ctx = torch.randn(7, 24, device=DEV)
+    last = torch.randn(7, 2, device=DEV)
+    z_ok = torch.randn(1, 2, 8, device=DEV)
+
+    def no_launch():
+        raise AssertionError("decoder_init reached the library with bad shapes")
+    monkeypatch.setattr(K, "_lib", no_launch)
+    bad = [
+        (ctx, torch.randn(1, 3, 8, device=DEV), None, last),      # noise of a batch with more scenes
+        (ctx, torch.randn(1, 1, 8, device=DEV), None, last),      # ... and with fewer
+        (ctx, torch.randn(2, 8, device=DEV), None, last),         # noise not (K, S, nz)
+        (torch.randn(9, 24, device=DEV), z_ok, None, last),       # context rows of another batch
+        (ctx, z_ok, None, torch.randn(9, 2, device=DEV)),         # last_rel rows of another batch
+        (ctx, z_ok, torch.zeros(3, dtype=torch.int64, device=DEV), last),   # best of another batch
+    ]
+    for i, (c, z, best, lr) in enumerate(bad):
+        with pytest.raises(ValueError, match="decoder_init"):
+            K.decoder_init(c, z, best, 0, 1, sc, lr)
+    with pytest.raises(ValueError, match="decoder_init"):     # fewer draws than the copies need
+        K.decoder_init(ctx, z_ok, None, 0, 3, sc, last)
+
+
+def test_dropped_graphed_trainer_in_a_cycle_is_reclaimed():
+    """capture_guard leaves no process-wide trace (it used to
+    gc.freeze() every live object after each capture, so cyclic garbage
+    among them was never collected): a GraphedTrainer captured, then dropped
+    while sitting in a reference cycle, is reclaimed by gc.collect(); and
+    gc_frozen() unfreezes what it froze."""
+    import weakref
+    from sgan import kernels as K
+    from sgan.train_step import GanTrainer, GraphedTrainer
+    g, d = build_models()
+    tr = GanTrainer(g, d, capturable=True)
+    b, sc, bg, scg = _batches()
+    torch.manual_seed(3)
+    random.seed(3)
+    gt = GraphedTrainer(tr, b, sc, warmup=1, batch_g=bg, sc_g=scg)
+    gt.step()
+    torch.cuda.synchronize()
+    assert gc.get_freeze_count() == 0
+
+    class Holder:
+        pass
+    h = Holder()
+    h.me, h.gt = h, gt                      # a cycle holding the trainer
+    ref = weakref.ref(gt)
+    del gt, h
+    gc.collect()
+    assert ref() is None, "GraphedTrainer in a dropped cycle was not collected"
+    with K.gc_frozen():
+        assert gc.get_freeze_count() > 0
+    assert gc.get_freeze_count() == 0

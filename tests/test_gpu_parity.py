@@ -58,10 +58,13 @@ def build_models(graph="gat"):
 
 def test_native_loaded_on_gpu():
     from sgan import _native
+    from sgan._srchash import source_hash
     lib = _native.load()
     assert lib.sgg_version() >= 1
     maps = open("/proc/self/maps").read()
     assert "libsgg.so" in maps
+    # the binary under test was built from this tree's kernel sources (HEAD)
+    assert lib.sgg_source_hash().decode() == source_hash()
 
 
 def test_xw_matches_torch():
@@ -864,6 +867,48 @@ def test_graphed_trainer_draw_ahead_is_bit_identical(iters):
     assert la == lb
     for k in wa:
         assert torch.equal(wa[k], wb[k]), k
+
+
+def test_shared_draw_source_keeps_reference_order():
+    """bench.py's timed pattern: a draw-ahead multi-iteration trainer and a
+    one-iteration trainer over ONE DrawSource, interleaved (the remainder
+    iterations run between draw-ahead replays) == the one-iteration trainer
+    alone over the same number of iterations: the host RNG draws reach the
+    iterations in the reference's order (draw-ahead before a
+    remainder replay had reordered them)."""
+    from sgan.data.synthetic import synthetic_batch
+    from sgan.scene import SceneIndex
+    from sgan.train_step import GanTrainer, GraphedTrainer
+    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
+    batch_g = synthetic_batch([20, 7, 13, 20, 2], seed=4, device=DEV)
+    res = []
+    for mixed in (False, True):
+        g, d = build_models()
+        tr = GanTrainer(g, d, capturable=True)
+        sc = SceneIndex.from_seq_start_end(batch[-1], DEV)
+        scg = SceneIndex.from_seq_start_end(batch_g[-1], DEV)
+        torch.manual_seed(11)
+        random.seed(11)
+        g1 = GraphedTrainer(tr, batch, sc, warmup=1, batch_g=batch_g, sc_g=scg)
+        if mixed:
+            gk = GraphedTrainer(tr, batch, sc, warmup=0, batch_g=batch_g, sc_g=scg, iters=2, draw_ahead=True,
+                                draws=g1.draws)
+            plan = [gk, g1, gk, g1, g1]          # 2 + 1 + 2 + 1 + 1 iterations
+        else:
+            plan = [g1] * 7
+        for t in plan:
+            t.step()
+        torch.cuda.synchronize()
+        res.append((float(torch.randn(1)), random.random(),
+                    {k: v.detach().clone() for k, v in list(g.state_dict().items()) + list(d.state_dict().items())}))
+    (ra, pa, wa), (rb, pb, wb) = res
+    # the last draw-ahead (iterations 6, 7) was consumed by the two g1 steps:
+    # nothing pending, and both host streams end in the same state
+    assert not g1.draws.pending
+    assert (ra, pa) == (rb, pb)
+    for k in wa:
+        err = (wa[k] - wb[k]).abs().max().item()
+        assert err <= 1e-6 * max(1.0, wa[k].abs().max().item()), (k, err)
 
 
 @pytest.mark.parametrize("iters", [1, 2])

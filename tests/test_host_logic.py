@@ -326,3 +326,20 @@ def test_bucketed_trainer_requires_a_padding_scene():
     with pytest.raises(ValueError):
         BucketedGraphTrainer(_T(), None, batch_size=64, pad_scenes=0)
     assert BucketedGraphTrainer(_T(), None, batch_size=64, pad_scenes=1).S_cap == 65
+
+
+def test_draw_source_orders_draws_across_trainers():
+    """DrawSource (sgan/train_step.py): a look-ahead does not consume, the
+    sequence number names the first pending draw, and take() after a
+    look-ahead returns the draw made ahead (no second RNG draw)."""
+    import itertools
+    from sgan.train_step import DrawSource
+    c = itertools.count()
+    src = DrawSource(lambda: next(c))
+    seq, items = src.ahead(3)
+    assert (seq, items) == (0, [0, 1, 2])
+    assert src.take() == 0            # the other trainer consumes the head
+    seq, items = src.ahead(3)
+    assert (seq, items) == (1, [1, 2, 3])
+    src.pop(3)
+    assert src.take() == 4 and src.seq == 5 and not src.pending

@@ -39,6 +39,29 @@ def test_library_exports_header_symbols():
     assert lib.sgg_pool_bwd_grid(100000) == 256 and lib.sgg_pool_bwd_grid(0) == 1
 
 
+def test_library_built_from_this_tree():
+    """sgg_source_hash() (compiled in by build_native.py) equals the hash of
+    the csrc/ + include/sgg.h sources here; load() refuses a stale binary."""
+    from sgan import _native
+    from sgan._srchash import source_files, source_hash
+    if not os.path.exists(_native.lib_path()):
+        pytest.skip("libsgg.so not built")
+    assert any(f.endswith("sgg.h") for f in source_files()) and len(source_files()) > 10
+    lib = _native.load(require_gpu=False)
+    assert lib.sgg_source_hash().decode() == source_hash()
+
+
+def test_load_refuses_stale_library(monkeypatch):
+    from sgan import _native
+    if not os.path.exists(_native.lib_path()):
+        pytest.skip("libsgg.so not built")
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "_LIB_EXPLICIT", False)
+    monkeypatch.setattr(_native, "source_hash", lambda: "0" * 64)
+    with pytest.raises(_native.NativeError, match="other sources"):
+        _native.load(require_gpu=False)
+
+
 def test_product_path_has_no_cpu_fallback():
     import torch
     from sgan import _native
