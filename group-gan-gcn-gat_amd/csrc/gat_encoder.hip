@@ -506,7 +506,7 @@ __device__ __forceinline__ int mm_wave(int first) {
 // With a (2N: a_src | a_dst), also the attention score partials of the tile:
 // sp[tile column][r] = sum over its 16 columns of out[r][c] a[c], tp the same
 // with a[N + c] (att_rows sums the column tiles).
-__device__ void lin(const float* in, int ldi, int rows, int K, const float* W, int ldw, int N, float* out, int ldo,
+__device__ __forceinline__ void lin(const float* in, int ldi, int rows, int K, const float* W, int ldw, int N, float* out, int ldo,
                     int first = 0, const float* a = nullptr, float* sp = nullptr, float* tp = nullptr, int np = 0) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
   const int ct = (N + 15) >> 4, nt = ((rows + 15) >> 4) * ct;
@@ -541,7 +541,7 @@ __device__ void lin(const float* in, int ldi, int rows, int K, const float* W, i
 // out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin; N % 4 == 0;
 // out may be global memory)
 // (out2: columns >= ksplit go to out2 at pitch ldo2 instead)
-__device__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, int ldw, int K, float* out, int ldo,
+__device__ __forceinline__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, int ldw, int K, float* out, int ldo,
                       bool accum, int first = 0, float* out2 = nullptr, int ldo2 = 0, int ksplit = 0) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
   const int ct = (K + 15) >> 4, nt = ((rows + 15) >> 4) * ct;
@@ -566,7 +566,7 @@ __device__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, 
 
 // dst[k][c] = sum_r x[r][k] d[r][c]  (weight gradient of lin: to the slab,
 // ldo = N; or an LDS image)
-__device__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, int ldd, int N, float* dst, int ldo,
+__device__ __forceinline__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, int ldd, int N, float* dst, int ldo,
                       int first = 0) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
   const int ct = (N + 15) >> 4, nt = ((K + 15) >> 4) * ct;
@@ -706,7 +706,7 @@ __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, 
 // (2F, to da) in the last phase WITHOUT a closing barrier: the caller adds
 // its weight / input gradient products to that phase.  attm, dz: scratch
 // rows x npp.
-__device__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gidl, const float* s, const float* t,
+__device__ __forceinline__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gidl, const float* s, const float* t,
                         float alpha, const float* a, const float* dpre, int ldd, float* dWh, int lddw, float* ds,
                         float* dt, float* attm, float* dz, int npp, float* da) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;

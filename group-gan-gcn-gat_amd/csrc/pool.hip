@@ -484,6 +484,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 typedef short short2v __attribute__((ext_vector_type(2)));
+typedef short short4v __attribute__((ext_vector_type(4)));
 constexpr int kBfWaves = 8;
 constexpr int kBfThreads = 64 * kBfWaves;
 constexpr int kBfUP = kKT + 4;         // U tile row pitch (floats; 16-B rows)
@@ -551,22 +552,24 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
 
       // U tiles of 64 units: n rows x 16 float4, two per thread (n <= 64)
       constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + kBfThreads - 1) / kBfThreads;
-      float4 ra[kUQ], rb[kUQ];
-      auto load_tile = [&](float4 (&r)[kUQ], int k0) {
+      // (native vector registers: HIP's float4 struct, copied under the row
+      // guard, was kept in scratch memory)
+      floatx4 ra[kUQ], rb[kUQ];
+      auto load_tile = [&](floatx4 (&r)[kUQ], int k0) __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < kUQ; ++e) {
           const int q = tid + kBfThreads * e;
           const int row = q / (kKT / 4), c4 = q - row * (kKT / 4);
-          if (row < n) r[e] = *reinterpret_cast<const float4*>(U + (size_t)(o + row) * kHidden + k0 + 4 * c4);
+          if (row < n) r[e] = *reinterpret_cast<const floatx4*>(U + (size_t)(o + row) * kHidden + k0 + 4 * c4);
         }
       };
-      auto store_tile = [&](const float4 (&r)[kUQ], int buf) {
+      auto store_tile = [&](const floatx4 (&r)[kUQ], int buf) __attribute__((always_inline)) {
         float* d = Ut + buf * SGG_POOL_MAX_PEDS * kBfUP;
 #pragma unroll
         for (int e = 0; e < kUQ; ++e) {
           const int q = tid + kBfThreads * e;
           const int row = q / (kKT / 4), c4 = q - row * (kKT / 4);
-          if (row < n) *reinterpret_cast<float4*>(d + row * kBfUP + 4 * c4) = r[e];
+          if (row < n) *reinterpret_cast<floatx4*>(d + row * kBfUP + 4 * c4) = r[e];
         }
       };
       load_tile(ra, 0);
@@ -594,7 +597,7 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
 
       constexpr int NKT = kHidden / kKT;   // (even)
       // the k-steps of tile kt from LDS buffer kt & 1
-      auto compute = [&](int kt) {
+      auto compute = [&](int kt) __attribute__((always_inline)) {
         const float* ut = Ut + (kt & 1) * SGG_POOL_MAX_PEDS * kBfUP;
 #pragma unroll 1
         for (int sk = 0; sk < kKT / 32; ++sk) {
@@ -626,20 +629,21 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
               // (v_pk_max_i16: a negative value's sign bit makes it < 0) --
               // the same bits as rounding max(x, 0), in 16 instead of 28
               // vector instructions per 8 units
-              union {
-                bf16x8_t v;
-                bf16x2v b[4];
-                short2v i[4];
-              } h;
+              // (register values combined by shuffles and bit casts: a union
+              // or an indexed array here lived in scratch memory)
+              short2v hi[4];
 #pragma unroll
               for (int m = 0; m < 4; ++m) {
                 const float2v pre = __builtin_elementwise_fma(ay[m], ry2, __builtin_elementwise_fma(ax[m], rx2, uv[m]));
-                h.b[m] = __builtin_convertvector(pre, bf16x2v);
-                h.i[m] = __builtin_elementwise_max(h.i[m], short2v{0, 0});
+                const short2v b = __builtin_bit_cast(short2v, __builtin_convertvector(pre, bf16x2v));
+                hi[m] = __builtin_elementwise_max(b, short2v{0, 0});
               }
+              const short4v h01 = __builtin_shufflevector(hi[0], hi[1], 0, 1, 2, 3);
+              const short4v h23 = __builtin_shufflevector(hi[2], hi[3], 0, 1, 2, 3);
+              const bf16x8_t hv = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(h01, h23, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
               for (int t = 0; t < NT; ++t)
-                acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h.v, bfr[t], acc[g][t], 0, 0, 0);
+                acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hv, bfr[t], acc[g][t], 0, 0, 0);
             }
           }
         }
@@ -662,15 +666,21 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
         __syncthreads();
       }
 
-      // epilogue: bias, ReLU, max over j (LDS atomic max on (bits << 32 | ~j))
+      // epilogue: bias, ReLU, max over j (LDS atomic max on (bits << 32 | ~j)).
+      // (ne: n through an empty asm, so the pairs' (il, j) are formed here and
+      // not hoisted ahead of the k-loop, where 16 x GPW of them sat in registers
+      // through it and pushed GPW 4 into scratch)
+      int ne = n;
+      asm volatile("" : "+s"(ne));
+      const int npe = rows * ne;
 #pragma unroll
       for (int g = 0; g < GPW; ++g) {
         const int grp = wave * GPW + g;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int p = grp * 16 + kq * 4 + r;
-          if (p < npairs) {
-            const int il = p / n, j = p - il * n;
+          if (p < npe) {
+            const int il = p / ne, j = p - il * ne;
             const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {

@@ -31,7 +31,7 @@ extern "C" {
 #define SGG_E_ARG (-1)
 
 /* Library version / self description.  sgg_source_hash(): SHA-256 (hex) of
- * the csrc/*.hip, csrc/*.h and include/sgg.h the library was built from
+ * the kernel sources (csrc: .hip and .h files) and this header the library was built from
  * (build_native.py); the Python loader refuses a library whose hash differs
  * from the tree it runs in. */
 int sgg_version(void);

@@ -25,12 +25,12 @@ def main():
         elif cur is not None and ":" in t:
             k, v = t.split(":", 1)
             cur[k.strip()] = v.strip()
-    print("%-6s %-6s %-6s %-5s %-6s %s" % ("VGPR", "AGPR", "spill", "occ", "LDS", "kernel"))
+    print("%-6s %-6s %-6s %-7s %-5s %-6s %s" % ("VGPR", "AGPR", "spill", "scratch", "occ", "LDS", "kernel"))
     for c in rows:
         n = subprocess.run(["c++filt"], input=c["name"], capture_output=True, text=True).stdout.strip()
         if filt not in n:
             continue
-        print("%-6s %-6s %-6s %-5s %-6s %s" % (c.get("VGPRs"), c.get("AGPRs"), c.get("VGPRs Spill"),
+        print("%-6s %-6s %-6s %-7s %-5s %-6s %s" % (c.get("VGPRs"), c.get("AGPRs"), c.get("VGPRs Spill"), c.get("ScratchSize [bytes/lane]"),
                                               c.get("Occupancy [waves/SIMD]"), c.get("LDS Size [bytes/block]"),
                                               n[:110]))
 
