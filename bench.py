@@ -391,7 +391,7 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
         try:
             g1 = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, overlap=OVERLAP, **kw)
             gk = None
-            if GRAPH_ITERS > 1 and world == 1:
+            if GRAPH_ITERS > 1 and not trainer.dp.segmented:
                 # (the timed trainer draws each replay's host RNG numbers
                 # while the previous replay runs: GraphedTrainer draw_ahead;
                 # both trainers take their draws from ONE DrawSource, so the
@@ -472,16 +472,21 @@ def measure(spec, steps, warmup, rank, world, dev, graph_on, n_it=3):
     try:
         trainer, batch, sc, batch_g, sc_g, kw = setup(spec["per_gpu"], spec["peds"], rank, world, dev, spec["graph"])
         step, graphed, gt = make_step(trainer, batch, sc, batch_g, sc_g, kw, graph_on, world)
-        comm = gt is not None and world > 1
+        # N > 1, segmented graphs (gloo): HIP events around each eager gradient
+        # all-reduce between the graph segments; captured collectives (RCCL,
+        # inside the graph): the same two flat buckets all-reduced eagerly
+        # after the timed run -- on this rank, max over ranks
+        comm = gt is not None and world > 1 and trainer.dp.segmented
         elapsed = timed_run(step, steps, warmup, world, dev, on_start=gt.time_allreduce if comm else None)
-        # N > 1: HIP events around each eager gradient all-reduce between the
-        # graph segments, on this rank, max over ranks
         ar_us = gt.allreduce_ms() * 1e3 / steps if comm else None
+        if comm:
+            gt.time_allreduce(False)
+        elif world > 1:
+            ar_us = bucket_allreduce_us(trainer, dev)
         if ar_us is not None:
             t = torch.tensor([ar_us], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ar_us = float(t)
-            gt.time_allreduce(False)
         n_it = max(1, min(steps, n_it))
         K.timer.start()
         for _ in range(n_it):
@@ -491,7 +496,27 @@ def measure(spec, steps, warmup, rank, world, dev, graph_on, n_it=3):
     finally:
         K.set_precision("fp32")
     return dict(elapsed=elapsed, graphed=graphed, agg=kernel_table(timed, n_it), recs=recs, n_it=n_it,
-                allreduce_us=ar_us)
+                allreduce_us=ar_us, captured=bool(graphed and world > 1 and not trainer.dp.segmented))
+
+
+def bucket_allreduce_us(trainer, dev, reps=20):
+    """Device time of one iteration's two gradient all-reduces (the G and D
+    flat buckets incl. the loss values), issued eagerly back to back between
+    HIP events: the collectives' cost when they are captured inside the
+    iteration's graph (no events there)."""
+    nums = [sum(p.numel() for p in ps) + 3 for ps in (trainer.g_params, trainer.d_params)]
+    bufs = [torch.zeros(n, device=dev) for n in nums]
+    for b in bufs:
+        dist.all_reduce(b)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        for b in bufs:
+            dist.all_reduce(b)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
 
 
 def top_kernels(agg, n=10):
@@ -704,8 +729,10 @@ def main():
                 "allreduce_us_per_iter": round(ar, 1) if ar is not None else None,
                 "compute_us_per_iter": round(ms_step * 1e3 - ar, 1) if ar is not None else None,
                 "allreduces_per_iter": 2,
-                "note": "HIP events around each eager gradient all-reduce (one flat SUM bucket per optimizer step, "
-                        "between the HIP-graph segments), summed per iteration, max over ranks; compute = "
+                "collectives": "captured in the HIP graph" if res.get("captured") else "eager between graph segments",
+                "note": "one flat SUM bucket per optimizer step; captured: the two buckets all-reduced eagerly "
+                        "between HIP events after the timed run; segmented: HIP events around each eager "
+                        "all-reduce between the graph segments; per iteration, max over ranks; compute = "
                         "ms_per_step - all-reduce time"}
         print(json.dumps(line), flush=True)
     if world > 1:

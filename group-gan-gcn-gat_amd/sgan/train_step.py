@@ -87,14 +87,38 @@ def _valid(sc):
 
 
 class DataParallel:
-    """Scene-sharded DP context (world 1 = plain single-GPU)."""
+    """Scene-sharded DP context (world 1 = plain single-GPU).
 
-    def __init__(self, group=None):
+    exercise: run the gradient all-reduce even at world size 1 (the DP code
+    path on one GPU: an RCCL SUM over one rank is the identity, so the step
+    must stay bitwise equal to the non-DP one).  capture: the all-reduces are
+    captured INSIDE GraphedTrainer's HIP graph (RCCL is stream-capturable:
+    one graph per replay); default on for the nccl (= RCCL) backend, off for
+    gloo (a host collective cannot be captured: the graph is then cut into
+    segments with the all-reduces run eagerly between them).
+    SGG_CAPTURE_COLLECTIVE=0 forces the segment form."""
+
+    def __init__(self, group=None, exercise=False, capture=None):
         self.on = dist.is_available() and dist.is_initialized()
         self.group = group
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
+        self.exercise = bool(exercise) and self.on
+        if capture is None:
+            capture = self.on and dist.get_backend(group) == "nccl" and \
+                os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0"
+        self.capture = bool(capture) and self.on
         self.cut = None   # set by GraphedTrainer while capturing: graph segment boundary
+
+    @property
+    def collective(self):
+        """Whether the steps issue gradient all-reduces at all."""
+        return self.on and (self.world > 1 or self.exercise)
+
+    @property
+    def segmented(self):
+        """Whether a captured iteration must be cut at each all-reduce."""
+        return self.collective and not self.capture
 
     def shard(self, S_global):
         """Contiguous scene range [s0, s1) of this rank: a balanced split
@@ -112,7 +136,7 @@ class DataParallel:
 
     def allreduce_(self, tensors):
         """SUM-all-reduce a list of tensors through one flat bucket."""
-        if not self.on or self.world == 1 or not tensors:
+        if not self.collective or not tensors:
             return
         if self.cut is not None:       # capturing: end the graph segment here
             self.cut(tensors)
@@ -207,7 +231,7 @@ class GanTrainer:
         K.side_join()   # the weight gradients of the side stream (normally joined at the end of backward)
         K.grad_flush()  # the backward ops' queued weight-gradient finishes (KernelOps.defer_finish)
         grads = [p.grad for p in params if p.grad is not None]
-        if self.dp.on and self.dp.world > 1:   # the loss values ride along with the gradients
+        if self.dp.collective:   # the loss values ride along with the gradients
             vals = torch.stack([t.detach().reshape(()) for t in loss_terms])
             self.dp.allreduce_(grads + [vals])
         else:                                  # one rank: no copy (callers index the values)
@@ -601,7 +625,7 @@ class GraphedTrainer:
         self.t = trainer
         self.ar_events = None   # time_allreduce()
         self.iters = iters = max(1, int(iters))
-        self.overlap = overlap = bool(overlap) and not (trainer.dp.on and trainer.dp.world > 1)
+        self.overlap = overlap = bool(overlap) and not trainer.dp.collective
         self.prologue = prologue or (lambda: None)
         self.batch, self.sc = batch, sc
         self.batch_g, self.sc_g = batch_g, sc_g
@@ -645,8 +669,9 @@ class GraphedTrainer:
         self.inp_flat = torch.zeros(iters * per, device=dev)
         self.inps = [StepInputs(v[0], v[1], v[2]) if nd else StepInputs(None, None, v[0]) for v in blocks(self.inp_flat)]
         self.inp = self.inps[0]
-        if iters > 1 and trainer.dp.on and trainer.dp.world > 1:
-            raise ValueError("GraphedTrainer: iters > 1 needs one rank (the collectives cut the graph)")
+        if iters > 1 and trainer.dp.segmented:
+            raise ValueError("GraphedTrainer: iters > 1 needs the collectives inside the graph (DataParallel "
+                             "capture=True: nccl) or one rank -- segmented collectives cut the graph")
         # warm-up and capture on the same side stream: the parameters'
         # AccumulateGrad nodes (created by the first backward, kept alive by
         # the captured graph) are bound to the stream that created them
@@ -662,18 +687,19 @@ class GraphedTrainer:
         torch.cuda.synchronize()
         trainer.opt_g.zero_grad(set_to_none=True)
         trainer.opt_d.zero_grad(set_to_none=True)
-        # One graph at world size 1.  With several ranks the capture is cut at
-        # each gradient all-reduce (DataParallel.cut): the collectives run
-        # eagerly between graph segments on the segments' static buffers, so
-        # the replay never depends on capturing a collective (gloo cannot be
-        # captured; a failed capture would poison the stream).
+        # One graph per replay when the collectives (if any) are captured with
+        # it (one rank, or RCCL: DataParallel.capture).  Otherwise (gloo) the
+        # capture is cut at each gradient all-reduce (DataParallel.cut): the
+        # collectives run eagerly between graph segments on the segments'
+        # static buffers (gloo cannot be captured; a failed capture would
+        # poison the stream).
         self.segments = []
         self.pair = []
         dp = trainer.dp
         params = trainer.g_params + trainer.d_params
         cap.wait_stream(torch.cuda.current_stream())
-        if not (dp.on and dp.world > 1):
-            # one rank: TWO graphs, each starting with the H2D copy of its own
+        if not dp.segmented:
+            # TWO graphs, each starting with the H2D copy of its own
             # pinned staging buffer, replayed alternately -- the next replay is
             # queued behind the running one with no host copy between them,
             # and the host fills buffer i while graph i's previous replay
@@ -713,7 +739,7 @@ class GraphedTrainer:
                 self.segments.append((g, list(tensors)))
                 g = torch.cuda.CUDAGraph()
                 g.capture_begin(pool=pool)
-            dp.cut = cut if (dp.on and dp.world > 1) else None
+            dp.cut = cut if dp.segmented else None
             try:
                 self.prologue()
                 self.losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inp, **self.kw)
