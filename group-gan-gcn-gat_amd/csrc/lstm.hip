@@ -282,7 +282,7 @@ extern "C" const char* sgg_lstm_kernel_name(int H, int B, int decoder, int save,
     return buf;
   }
   if (save && mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_fwd_kernel<%d, %s, true>", H, tf[decoder != 0]);
-  else if (lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) snprintf(buf, sizeof buf, "sgg::lstm_fwd_mfma_kernel<%d>", H);
+  else if (!save && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) snprintf(buf, sizeof buf, "sgg::lstm_fwd_mfma_kernel<%d>", H);
   else if (mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_fwd_kernel<%d, %s, %s>", H, tf[decoder != 0], tf[save != 0]);
   else if (H <= 32) snprintf(buf, sizeof buf, "sgg::lstm_unit_fwd_kernel<%d>", H);
   else snprintf(buf, sizeof buf, "sgg::lstm_fwd_kernel<%d>", H);
@@ -388,8 +388,8 @@ extern "C" int sgg_lstm_fwd(const float* rel, const float* A, const float* Whh, 
   const bool mw = lstm_mw_ok(H, B);
   if (act_all && mw)
     return lstm_mw_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
-  if (lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
-    return lstm_fwd_mfma(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
+  if (!act_all && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
+    return lstm_fwd_mfma(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, nullptr, rel_out, st);
   if (mw)
     return lstm_mw_fwd(rel, A, Whh, bias, h0, c0, Wp, bp, T, B, H, decoder, h_all, c_all, act_all, rel_out, st);
   if (lstm_unit_ok(H, decoder) && !getenv("SGG_LSTM_ROWS"))

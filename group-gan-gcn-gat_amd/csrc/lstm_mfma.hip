@@ -67,20 +67,69 @@ __device__ __forceinline__ SggDecInit pick_di(const SggDecInit& a, const SggDecI
   return d;
 }
 
+// Sum of a value over the four 16-lane rows of the wave (the four q lanes of a
+// ped), in every lane: two lane-swap moves (gfx950 v_permlane16_swap /
+// v_permlane32_swap, VALU) instead of two LDS-routed shuffles; the additions
+// pair (row 0 + row 1) + (row 2 + row 3) in every lane, as the xor-16 / xor-32
+// shuffle tree did.
+__device__ __forceinline__ float rows_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+typedef float float2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2v exp2v(float2v y) {
+  return float2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+}
+__device__ __forceinline__ float2v rcpv(float2v y) {
+  return float2v{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)};
+}
+// exponent arguments are clamped where an infinite exponential would meet a
+// zero (0 * inf): 2^64 keeps every product below finite range, and the
+// functions it feeds are saturated there to far below fp32 resolution
+constexpr float kExpArgMax = 64.f;
+__device__ __forceinline__ float2v clampv(float2v y) {
+  return float2v{__builtin_amdgcn_fmed3f(y.x, -kExpArgMax, kExpArgMax), __builtin_amdgcn_fmed3f(y.y, -kExpArgMax, kExpArgMax)};
+}
+
+// The cell update of two units at once from their gate pre-activations,
+// pre-scaled by -log2(e) (i, f, o) and -2 log2(e) (g):  with e_x = 2^{y_x},
+//   f c = c / (1 + e_f),   i g = (1 - e_g) / ((1 + e_i)(1 + e_g)),
+//   h   = o tanh(c') = (1 - e_c) / ((1 + e_o)(1 + e_c)),  e_c = 2^{-2 log2(e) c'}
+// -- five exponentials and three reciprocals per unit (the per-gate form
+// takes five of each), the rest as packed two-unit VALU operations.
+__device__ __forceinline__ void cell2(float2v yi, float2v yf, float2v yg, float2v yo, float2v& c, float2v& h) {
+  const float2v one = {1.f, 1.f};
+  const float2v ei = exp2v(yi), ef = exp2v(yf), eg = exp2v(clampv(yg)), eo = exp2v(yo);
+  const float2v rf = rcpv(one + ef);
+  const float2v rig = rcpv((one + ei) * (one + eg));
+  c = __builtin_elementwise_fma(c, rf, (one - eg) * rig);
+  const float2v ec = exp2v(clampv(c * float2v{-2.8853900817779268f, -2.8853900817779268f}));
+  h = (one - ec) * rcpv((one + eo) * (one + ec));
+}
+
+// DEC (runtime, uniform): the decoder's output feedback folded into the
+// recurrence.  The next input is rel_t = Wp h_t + bp, so for t >= 1
+//   W_hh h + A rel + b = (W_hh + A Wp) h + (b + A bp):
+// the lane's weight registers hold W' = W_hh + A Wp and its accumulators start
+// from b' = b + A bp (the first MFMA's C operand), so a step is 4H/16 x H/4
+// MFMAs with no input k-step.  Step 0 adds A (rel_0 - Wp h_0 - bp) through
+// the input k-step.  The encoder (no feedback) keeps the input k-step
+// [r_x r_y 0 0] every step.
 template <int H>
 __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
     const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B1, int decoder,
-    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ act_all, float* __restrict__ rel_out1,
-    SggDecInit di1, RollSeg2 s2) {
+    float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ rel_out1, SggDecInit di1, RollSeg2 s2) {
   constexpr int G4 = 4 * H;
   constexpr int MT = G4 / 16;     // gate-row tiles
   constexpr int MU = H / 16;      // unit tiles (i/f/g/o blocks are MU tiles apart)
   constexpr int KSH = H / 4;      // k-steps over h_{t-1}
   constexpr int NU = H / 4;       // units per lane
   const bool two = s2.B > 0 && (int)blockIdx.x >= s2.nblk1;   // uniform: the second segment's workgroup
-  const bool save = act_all != nullptr && !two;
   const SggDecInit di = pick_di(di1, s2.di, two);
   const int B = two ? s2.B : B1;
   float* __restrict__ rel_out = two ? s2.rel_out : rel_out1;
@@ -110,19 +159,8 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     }
   }
 
-  // W_ext in registers, columns in the permuted k order
-  float w[MT][KSH + 1];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = 16 * mt + c16;
-#pragma unroll
-    for (int ks = 0; ks < KSH; ++ks) w[mt][ks] = Whh[row * H + 16 * (ks >> 2) + 4 * q + (ks & 3)];
-    w[mt][KSH] = q == 0 ? A[2 * row] : q == 1 ? A[2 * row + 1] : q == 2 ? bias[row] : 0.f;
-    // gate of tile mt: i, f, g, o blocks of MU tiles; g (tanh) takes -2 log2(e)
-    const float sc = (mt / MU == 2 ? 2.f : 1.f) * kNegLog2e;
-#pragma unroll
-    for (int ks = 0; ks <= KSH; ++ks) w[mt][ks] *= sc;
-  }
+  // the lane's k-step units (k = 4 mu + r  <->  unit 16 mu + 4q + r, the
+  // permuted k order) and the decoder's Wp columns of them
   float wp0[NU], wp1[NU];
 #pragma unroll
   for (int k = 0; k < NU; ++k) {
@@ -131,9 +169,33 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     wp1[k] = decoder ? Wp[H + u] : 0.f;
   }
   const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
+  // W' (or W_hh) in registers, columns in the permuted k order; the input
+  // column [A_x A_y 0 0] by q; the accumulator start b' (or b) in the D layout
+  // (rows 16 mt + 4q + r); all pre-scaled for v_exp_f32
+  float w[MT][KSH + 1];
+  floatx4 b0[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = 16 * mt + c16;
+    // gate of tile mt: i, f, g, o blocks of MU tiles; g (tanh) takes -2 log2(e)
+    const float sc = (mt / MU == 2 ? 2.f : 1.f) * kNegLog2e;
+    const float ax = A[2 * row], ay = A[2 * row + 1];
+#pragma unroll
+    for (int ks = 0; ks < KSH; ++ks) {
+      const float wv = Whh[row * H + 16 * (ks >> 2) + 4 * q + (ks & 3)];
+      w[mt][ks] = sc * (decoder ? fmaf(ay, wp1[ks], fmaf(ax, wp0[ks], wv)) : wv);
+    }
+    w[mt][KSH] = q == 0 ? sc * ax : q == 1 ? sc * ay : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int brow = 16 * mt + 4 * q + r;
+      const float bv = bias[brow];
+      b0[mt][r] = sc * (decoder ? fmaf(A[2 * brow + 1], bp1, fmaf(A[2 * brow], bp0, bv)) : bv);
+    }
+  }
 
-  // state of the lane's NU units (k = 4 mu + r  <->  unit 16 mu + 4q + r)
-  float h[NU], c[NU];
+  // state of the lane's NU units, as unit pairs (k, k + 1)
+  float2v h[NU / 2], c[NU / 2];
 #pragma unroll
   for (int mu = 0; mu < MU; ++mu) {
     const size_t o = (size_t)ped * H + 16 * mu + 4 * q;
@@ -145,75 +207,74 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
       hv = *reinterpret_cast<const float4*>(h0 + o);
     }
     if (valid && c0) cv = *reinterpret_cast<const float4*>(c0 + o);
-    h[4 * mu] = hv.x; h[4 * mu + 1] = hv.y; h[4 * mu + 2] = hv.z; h[4 * mu + 3] = hv.w;
-    c[4 * mu] = cv.x; c[4 * mu + 1] = cv.y; c[4 * mu + 2] = cv.z; c[4 * mu + 3] = cv.w;
-    if (valid && save) {
-      *reinterpret_cast<float4*>(h_all + o) = hv;
-      *reinterpret_cast<float4*>(c_all + o) = cv;
-    }
+    h[2 * mu] = float2v{hv.x, hv.y};
+    h[2 * mu + 1] = float2v{hv.z, hv.w};
+    c[2 * mu] = float2v{cv.x, cv.y};
+    c[2 * mu + 1] = float2v{cv.z, cv.w};
   }
-  // input k-step operand: r_x (q = 0), r_y (q = 1), 1 (q = 2), 0 (q = 3)
+  // input k-step operand: r_x (q = 0), r_y (q = 1), 0 (q = 2, 3)
   auto load_in = [&](int t) -> float {
-    if (q >= 2) return q == 2 ? 1.f : 0.f;
-    if (!valid) return 0.f;
+    if (q >= 2 || !valid) return 0.f;
     if (decoder && di.ctx) return dec_rel0(di, ped, q);
     return decoder ? rel[(size_t)ped * 2 + q] : rel[((size_t)t * B + ped) * 2 + q];
   };
   float xin = load_in(0);
+  if (decoder) {   // step 0's input correction rel_0 - (Wp h_0 + bp)
+    float px = 0.f, py = 0.f;
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      const float hk = (k & 1) ? h[k >> 1].y : h[k >> 1].x;
+      px = fmaf(wp0[k], hk, px);
+      py = fmaf(wp1[k], hk, py);
+    }
+    px = rows_sum(px) + bp0;
+    py = rows_sum(py) + bp1;
+    xin = q == 0 ? xin - px : q == 1 ? xin - py : 0.f;
+  }
 
   for (int t = 0; t < T; ++t) {
     const float xnext = (!decoder && t + 1 < T) ? load_in(t + 1) : 0.f;   // prefetch
     floatx4 acc[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt)
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][0], h[0].x, b0[mt], 0, 0, 0);
 #pragma unroll
-    for (int ks = 0; ks < KSH; ++ks)
+    for (int ks = 1; ks < KSH; ++ks) {
+      const float hk = (ks & 1) ? h[ks >> 1].y : h[ks >> 1].x;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][ks], h[ks], acc[mt], 0, 0, 0);
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][ks], hk, acc[mt], 0, 0, 0);
+    }
+    if (!decoder || t == 0) {   // (uniform)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][KSH], xin, acc[mt], 0, 0, 0);
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][KSH], xin, acc[mt], 0, 0, 0);
+    }
 
-    // gate activations (i, f, o sigmoid; g tanh) and the cell update
+    // gate activations (i, f, o sigmoid; g tanh) and the cell update, two
+    // units at a time
     float px = 0.f, py = 0.f;
 #pragma unroll
     for (int mu = 0; mu < MU; ++mu) {
-      float ai[4], af[4], ag[4], ao[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ai[r] = sigm_pre(acc[mu][r]);
-        af[r] = sigm_pre(acc[MU + mu][r]);
-        ag[r] = tanh_pre(acc[2 * MU + mu][r]);
-        ao[r] = sigm_pre(acc[3 * MU + mu][r]);
-        const int k = 4 * mu + r;
-        c[k] = fmaf(af[r], c[k], ai[r] * ag[r]);
-        h[k] = ao[r] * tanh_fast(c[k]);
-        px = fmaf(wp0[k], h[k], px);
-        py = fmaf(wp1[k], h[k], py);
+      for (int r = 0; r < 4; r += 2) {
+        const int k2 = 2 * mu + (r >> 1);
+        cell2(float2v{acc[mu][r], acc[mu][r + 1]}, float2v{acc[MU + mu][r], acc[MU + mu][r + 1]},
+              float2v{acc[2 * MU + mu][r], acc[2 * MU + mu][r + 1]}, float2v{acc[3 * MU + mu][r], acc[3 * MU + mu][r + 1]},
+              c[k2], h[k2]);
+        px = fmaf(wp0[2 * k2], h[k2].x, fmaf(wp0[2 * k2 + 1], h[k2].y, px));
+        py = fmaf(wp1[2 * k2], h[k2].x, fmaf(wp1[2 * k2 + 1], h[k2].y, py));
       }
-      if (valid && save) {
-        const size_t ab = ((size_t)t * B + ped) * G4 + 16 * mu + 4 * q;
-        *reinterpret_cast<float4*>(act_all + ab) = make_float4(ai[0], ai[1], ai[2], ai[3]);
-        *reinterpret_cast<float4*>(act_all + ab + H) = make_float4(af[0], af[1], af[2], af[3]);
-        *reinterpret_cast<float4*>(act_all + ab + 2 * H) = make_float4(ag[0], ag[1], ag[2], ag[3]);
-        *reinterpret_cast<float4*>(act_all + ab + 3 * H) = make_float4(ao[0], ao[1], ao[2], ao[3]);
-      }
-      if (valid && (save || (t == T - 1 && h_all))) {   // (no-grad rollout: h_all NULL, final state unwanted)
-        const size_t o = ((size_t)(save ? t + 1 : T) * B + ped) * H + 16 * mu + 4 * q;
-        *reinterpret_cast<float4*>(h_all + o) = make_float4(h[4 * mu], h[4 * mu + 1], h[4 * mu + 2], h[4 * mu + 3]);
-        *reinterpret_cast<float4*>(c_all + o) = make_float4(c[4 * mu], c[4 * mu + 1], c[4 * mu + 2], c[4 * mu + 3]);
+      if (valid && t == T - 1 && h_all) {   // (no-grad rollout: h_all NULL, final state unwanted)
+        const size_t o = ((size_t)T * B + ped) * H + 16 * mu + 4 * q;
+        *reinterpret_cast<float4*>(h_all + o) = make_float4(h[2 * mu].x, h[2 * mu].y, h[2 * mu + 1].x, h[2 * mu + 1].y);
+        *reinterpret_cast<float4*>(c_all + o) = make_float4(c[2 * mu].x, c[2 * mu].y, c[2 * mu + 1].x, c[2 * mu + 1].y);
       }
     }
     if (decoder) {   // rel_t = Wp h_t + bp: sum the 4 q-lanes of the ped
-      px += __shfl_xor(px, 16);
-      px += __shfl_xor(px, 32);
-      py += __shfl_xor(py, 16);
-      py += __shfl_xor(py, 32);
-      px += bp0;
-      py += bp1;
+      px = rows_sum(px) + bp0;
+      py = rows_sum(py) + bp1;
       if (valid && q == 0) *reinterpret_cast<float2*>(rel_out + ((size_t)t * B + ped) * 2) = make_float2(px, py);
       if (tlive && q == 0)
         reinterpret_cast<float2*>(to.out)[(size_t)(to.T0 + t) * to.NB + tcol] = make_float2(px, py);
-      xin = q == 0 ? px : q == 1 ? py : xin;
     } else {
       xin = xnext;
     }
@@ -231,8 +292,12 @@ int launch(const float* rel, const float* A, const float* Whh, const float* bias
   if (seg2) s2 = *seg2;
   s2.nblk1 = grid;
   const int grid2 = s2.B > 0 ? (s2.B + 63) / 64 : 0;
+  if (act_all) {   // (the dispatch never sends saved-state forwards here)
+    sgg::set_error("sgg_lstm_fwd: the batch-MFMA rollout keeps no saved states");
+    return SGG_E_ARG;
+  }
   hipLaunchKernelGGL(lstm_fwd_mfma_kernel<H>, dim3(grid + grid2), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T,
-                     B, decoder, h_all, c_all, act_all, rel_out, d, s2);
+                     B, decoder, h_all, c_all, rel_out, d, s2);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
 }
 

@@ -31,7 +31,10 @@ def demangle(names):
 
 def resources(src):
     """[{name, vgpr, agpr, sgpr, scratch, vspill, sspill, occ, lds}] of one source file."""
-    r = subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + [src], capture_output=True, text=True)
+    sys.path.insert(0, os.path.join(ROOT, "group-gan-gcn-gat_amd"))
+    from build_native import FILE_FLAGS   # the build's per-source flags
+    extra = FILE_FLAGS.get(os.path.basename(src), [])
+    r = subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + extra + [src], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s" % (src, r.stderr[-2000:]))
     rows, cur = [], None

@@ -44,14 +44,24 @@ def main():
     caps0 = len(bt.buckets)
     t0 = time.perf_counter()
     marks = [t0]
+    mono = [time.monotonic_ns()]   # (CLOCK_MONOTONIC: the clock of rocprofv3's host traces)
+    info = []
     for _ in range(iters):
         sd, sg = next(it), next(it)
         used[bt.bucket_of(dd.layout(sd)[0], dd.layout(sg)[0])] += 1
         bt.step(sd, sg)
         marks.append(time.perf_counter())
+        mono.append(time.monotonic_ns())
+        info.append(bt.last)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     host = np.diff(marks) * 1e3
+    if os.environ.get("SGG_PROBE_MARKS"):   # per-iteration host windows (tools/systrace_stall.py)
+        import json
+        with open(os.environ["SGG_PROBE_MARKS"], "w") as f:
+            json.dump([{"index": i, "start_ns": mono[i], "end_ns": mono[i + 1], "host_ms": float(host[i]),
+                        "bucket": (list(info[i][0]) if info[i][0] is not None else "eager"),
+                        "prior_replays": info[i][1]} for i in range(iters)], f)
     print("host ms per iteration: median %.3f max %.3f; gc collections %d; buckets captured in the loop %d"
           % (np.median(host), host.max(), gcs[0], len(bt.buckets) - caps0))
     print("gran %d pad %d caps %s: %.3f ms / iteration, %.0f D-step scenes/s; buckets used %s"
