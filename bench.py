@@ -258,6 +258,23 @@ def iteration_roofline(agg, ms_step, scenes):
                     "over the measured time (above the fp32 peak because of those de-duplications)"}
 
 
+def host_sched():
+    """(run-queue wait of this thread in ns, the cgroup's throttled time in
+    us) -- None where the kernel does not expose it."""
+    wait = thr = None
+    try:
+        wait = int(open("/proc/thread-self/schedstat").read().split()[1])
+    except (OSError, ValueError, IndexError):
+        pass
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            if line.startswith("throttled_usec"):
+                thr = int(line.split()[1])
+    except (OSError, ValueError):
+        pass
+    return wait, thr
+
+
 def real_data_leg(dev, iters=20, warmup=3, batch=64):
     """configs[1] on REAL data: training iterations over the zara1 train split
     (tests/golden/datasets_group/zara1/train, the reference's datasets_group
@@ -324,11 +341,24 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
         scenes = 0
         marks = [t0]
         steps_info = []
+        # HIP events between the iterations on the launch stream: each
+        # iteration's device-side span (host timings alone cannot tell a host
+        # stall from the host waiting on a device that is behind)
+        evs = [torch.cuda.Event(enable_timing=True)]
+        evs[0].record()
+        # host-side diagnostics per iteration: the thread's run-queue wait
+        # (/proc/thread-self/schedstat: time runnable but not running) and the
+        # cgroup's CPU-quota throttling (cpu.stat throttled_usec) -- a host
+        # stall that is neither Python nor HIP shows up in one of them
+        sched = [host_sched()]
         for _ in range(iters):
             if mode == "graphed":
                 sd, sg = next(it), next(it)
                 bt.step(sd, sg)
                 steps_info.append(bt.last)
+                evs.append(torch.cuda.Event(enable_timing=True))
+                evs[-1].record()
+                sched.append(host_sched())
                 scenes += len(sd)
             else:
                 (bd, scd), (bg, scg) = next(it), next(it)
@@ -354,6 +384,19 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
                                               "bucket": (list(steps_info[k][0]) if steps_info[k][0] is not None
                                                          else "eager"),
                                               "bucket_prior_replays": steps_info[k][1]}
+            dev_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(iters)]
+            kd = max(range(iters), key=lambda i: dev_ms[i])
+            out[mode].update(device_ms_median=round(sorted(dev_ms)[iters // 2], 3), device_ms_max=round(dev_ms[kd], 3),
+                             device_slowest_index=kd, host_ms_per_iteration=[round(x * 1e3, 2) for x in its],
+                             device_ms_per_iteration=[round(x, 3) for x in dev_ms])
+            dq = [(b[0] - a[0]) / 1e6 if a[0] is not None and b[0] is not None else None
+                  for a, b in zip(sched, sched[1:])]
+            dt_ = [(b[1] - a[1]) / 1e3 if a[1] is not None and b[1] is not None else None
+                   for a, b in zip(sched, sched[1:])]
+            out[mode]["slowest_iteration"].update(runqueue_wait_ms=dq[k], cgroup_throttled_ms=dt_[k])
+            out[mode].update(runqueue_wait_ms_total=round(sum(x for x in dq if x is not None), 3),
+                             cgroup_throttled_ms_total=(round(sum(x for x in dt_ if x is not None), 3)
+                                                        if any(x is not None for x in dt_) else None))
         del tr, g, d, bt
     return {"metric": "train-scenes/s on real data (D-step scenes per second; the G-step takes the next loader "
                       "batch)", "split": "zara1 train",

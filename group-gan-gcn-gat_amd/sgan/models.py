@@ -721,13 +721,20 @@ class TrajectoryGenerator(nn.Module):
 
     def pair_ok(self, sc_a, sc_b):
         """context_pair runs its two batches' graph module (GATEncoder or
-        GCNModule, two-block input) in one launch."""
-        if not (self.graph in ("gat", "gcn") and self.pooling_type == "pool_net" and self.num_layers == 1
+        GCNModule, two-block input; sgangat: the GCNModule after each batch's
+        batched GAT) in one launch."""
+        if not (self.graph in ("gat", "gcn", "sgangat") and self.pooling_type == "pool_net" and self.num_layers == 1
                 and self.mlp_decoder_needed() and self.pool_net.fused_ok()):
             return False
         if self.graph == "gat":
             return self.gatencoder.fused_ok(sc_a, False) and self.gatencoder.fused_ok(sc_b, True)
-        fin = self.encoder_h_dim + self.pool_net.bottleneck_dim
+        if self.graph == "sgangat":   # the GCNModule reads the batched GAT's output
+            ps = self.gcn_module.fused_params()
+            if ps is None:
+                return False
+            fin = ps[0].shape[0]
+        else:
+            fin = self.encoder_h_dim + self.pool_net.bottleneck_dim
         return self.gcn_module.fused_ok(sc_a, fin) and self.gcn_module.fused_ok(sc_b, fin)
 
     def context_pair(self, a, b):
@@ -757,12 +764,23 @@ class TrajectoryGenerator(nn.Module):
             with torch.no_grad():
                 h_a, U_a = self.encoder(rel_a, proj_u=u)
             h_b, U_b = self.encoder(rel_b, proj_u=u)
-        link = K.GradLink() if torch.is_grad_enabled() else None
+        # (the two-block graph modules take the pooling's gradient link; the
+        # batched GAT of sgangat reads [h | pool] through its own first layer)
+        link = K.GradLink() if torch.is_grad_enabled() and self.graph != "sgangat" else None
         # both poolings in one launch (sgg_pool_fwd2): a's is held until b's carries it
         with K.pool_pair():
             with torch.no_grad():
                 pool_a = self.pool_net(h_a, sse_a, obs_a[-1], scenes=sc_a, U=U_a)
             pool_b = self.pool_net(h_b, sse_b, obs_b[-1], scenes=sc_b, link=link, U=U_b)
+        if self.graph == "sgangat":
+            # each batch's batched GAT (per-layer launches), then both
+            # GCNModules in one launch
+            with torch.no_grad():
+                x_a = self.gatencoder((h_a.view(-1, H), pool_a), sse_a, scenes=sc_a)
+            x_b = self.gatencoder((h_b.view(-1, H), pool_b), sse_b, scenes=sc_b)
+            comp = K.GcnModCompanion(x_a, g_a[-1], sc_a)
+            y_b = self.gcn_module(x_b, sse_b, obs_b[-1], g_b[-1], scenes=sc_b, companion=comp)
+            return comp.y, y_b
         if self.graph == "gat":
             comp = K.GatEncCompanion(h_a.view(-1, H), g_a[-1], sc_a, x2=pool_a)
             module = self.gatencoder

@@ -409,76 +409,6 @@ def test_no_grad_rollout_mfma_vs_oracle(T, decoder, B):
             close(mod(rel.to(DEV)), ref(rel).numpy(), rtol=1e-5, what="encoder h")
 
 
-@pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (48, 20, False, 37), (32, 12, True, 37),
-                                            (16, 5, True, 37), (64, 3, False, 37),
-                                            # batches that take the MFMA forward (lstm_mfma.hip)
-                                            (32, 8, False, 4133), (32, 12, True, 4133), (48, 20, False, 2085)])
-def test_fused_lstm_vs_oracle(H, T, decoder, B):
-    """sgg_lstm_fwd/bwd (Encoder / Decoder rollout) against the oracle's
-    torch-CPU modules: outputs and every parameter / input gradient."""
-    from oracle import sgan_oracle as O
-    from sgan import models as M
-    torch.manual_seed(H + T)
-    if decoder:
-        ref, mod = O.Decoder(T, 16, H, 64, 1, False), M.Decoder(T, 16, H, 64, 1, False)
-    else:
-        ref, mod = O.Encoder(16, H), M.Encoder(16, H)
-    mod.load_state_dict(ref.state_dict())
-    mod = mod.to(DEV)
-    if decoder:
-        last_pos, last_rel = torch.randn(B, 2), torch.randn(B, 2) * 0.3
-        h0 = (torch.randn(1, B, H) * 0.5).requires_grad_(True)
-        c0 = torch.zeros(1, B, H)
-        y_ref, _ = ref(last_pos, last_rel, (h0, c0), None)
-        h0d = h0.detach().to(DEV).requires_grad_(True)
-        y, _ = mod(last_pos.to(DEV), last_rel.to(DEV), (h0d, c0.to(DEV)), None)
-        dy = torch.randn_like(y_ref)
-        (y_ref * dy).sum().backward()
-        (y * dy.to(DEV)).sum().backward()
-        close(y, y_ref.detach().numpy(), rtol=1e-5, what="decoder out")
-        close(h0d.grad, h0.grad.numpy(), rtol=1e-4, what="decoder dh0")
-    else:
-        rel = (torch.randn(T, B, 2) * 0.3).requires_grad_(True)
-        y_ref = ref(rel)
-        reld = rel.detach().to(DEV).requires_grad_(True)
-        y = mod(reld)
-        dy = torch.randn_like(y_ref)
-        (y_ref * dy).sum().backward()
-        (y * dy.to(DEV)).sum().backward()
-        close(y, y_ref.detach().numpy(), rtol=1e-5, what="encoder h")
-        close(reld.grad, rel.grad.numpy(), rtol=1e-4, what="encoder drel")
-    for (k, p), (_, q) in zip(ref.named_parameters(), mod.named_parameters()):
-        close(q.grad, p.grad.numpy(), rtol=1e-4, floor=1e-6, what="lstm d" + k)
-
-
-@pytest.mark.parametrize("T,decoder,B", [(12, True, 25600), (8, False, 4133), (12, True, 4099)])
-def test_no_grad_rollout_mfma_vs_oracle(T, decoder, B):
-    """The no-grad batch-MFMA forward (lstm_fwd_mfma_kernel: the best-of-20
-    decoder rollout of the training step, 25,600 sequences) against the
-    oracle's modules."""
-    from oracle import sgan_oracle as O
-    from sgan import models as M
-    H = 32
-    torch.manual_seed(T + B)
-    if decoder:
-        ref, mod = O.Decoder(T, 16, H, 64, 1, False), M.Decoder(T, 16, H, 64, 1, False)
-    else:
-        ref, mod = O.Encoder(16, H), M.Encoder(16, H)
-    mod.load_state_dict(ref.state_dict())
-    mod = mod.to(DEV)
-    with torch.no_grad():
-        if decoder:
-            last_pos, last_rel = torch.randn(B, 2), torch.randn(B, 2) * 0.3
-            h0, c0 = torch.randn(1, B, H) * 0.5, torch.zeros(1, B, H)
-            y_ref, h_ref = ref(last_pos, last_rel, (h0, c0), None)
-            y, h = mod(last_pos.to(DEV), last_rel.to(DEV), (h0.to(DEV), c0.to(DEV)), None)
-            close(y, y_ref.numpy(), rtol=1e-5, what="rollout rel")
-            close(h, h_ref.numpy(), rtol=1e-5, what="rollout h_T")
-        else:
-            rel = torch.randn(T, B, 2) * 0.3
-            close(mod(rel.to(DEV)), ref(rel).numpy(), rtol=1e-5, what="encoder h")
-
-
 @pytest.mark.parametrize("H,T,decoder,B", [(32, 8, False, 37), (32, 12, True, 37), (16, 5, True, 21),
                                             (48, 12, True, 37), (64, 3, True, 37), (48, 20, False, 2085)])
 def test_fused_lstm_other_families(H, T, decoder, B, monkeypatch):
@@ -956,7 +886,8 @@ def test_graphed_trainer_overlap_equals_eager(iters):
             assert err <= tol * max(1.0, wa[k].abs().max().item()), (k, err)
 
 
-@pytest.mark.parametrize("graphed,family", [(False, "gat"), (True, "gat"), (False, "gcn"), (True, "gcn")])
+@pytest.mark.parametrize("graphed,family", [(False, "gat"), (True, "gat"), (False, "gcn"), (True, "gcn"),
+                                            (False, "sgangat"), (True, "sgangat")])
 def test_paired_context_step_is_bit_identical(graphed, family, monkeypatch):
     """step() with the G-step's context formed at the D-step beside the
     D-step's own (G.context_pair: one GATEncoder launch for both batches; the

@@ -171,6 +171,10 @@ if __name__ == "__main__":
         for B in (4096, 8192, 16384, 20480, 25600, 32768, 49152):
             lstm(B, 12, 32, True, reps=20)
         sys.exit(0)
+    if what == "rollb":   # the rollout over batch sizes: waves per SIMD 0.5 .. 2
+        for B in (8192, 16384, 20480, 25600, 26880, 32768):
+            lstm(B, 12, 32, True, reps=10)
+        sys.exit(0)
     if what == "roll2":   # one / two waves per SIMD (counter runs: tools/gpu_sq_rollwaves.sh)
         for B in (16384, 25600):
             lstm(B, 12, 32, True, reps=5)
