@@ -221,9 +221,15 @@ __device__ __forceinline__ void gat_attend(const float* Ws, int Fs, const float*
 }
 
 // rows past the last segment (zero-padded group buffers): zero outputs
-__device__ __forceinline__ void gat_zero_pad_rows(int tot, int nrows, int HF, float* y, int ldy, float* hp) {
-  for (size_t e = (size_t)tot * HF + blockIdx.x * kGatThreads + threadIdx.x; e < (size_t)nrows * HF;
-       e += (size_t)gridDim.x * kGatThreads) {
+// (blk / nblk: this workgroup's index among the nblk serving the rows)
+__device__ __forceinline__ void gat_zero_pad_rows(int tot, int nrows, int HF, float* y, int ldy, float* hp,
+                                                  int blk = -1, int nblk = 0) {
+  if (blk < 0) {
+    blk = blockIdx.x;
+    nblk = gridDim.x;
+  }
+  for (size_t e = (size_t)tot * HF + (size_t)blk * kGatThreads + threadIdx.x; e < (size_t)nrows * HF;
+       e += (size_t)nblk * kGatThreads) {
     const size_t r = e / HF, c = e - r * HF;
     y[r * ldy + c] = 0.f;
     if (hp) hp[e] = 0.f;
@@ -290,8 +296,9 @@ struct GatLayerArgs {
 
 __host__ __device__ __forceinline__ int gat_layer_kp(int K) { return (K + 31) & ~31; }
 
+// the layer over one set: workgroups blk = 0 .. nblk - 1 of those serving it
 template <int NM, bool BF16>
-__global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLayerArgs p) {
+__device__ __forceinline__ void gat_layer_fwd_body(const GatLayerArgs& p, int blk, int nblk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int F = p.F, K = p.K1 + p.K2, HF = p.heads * F;
   const int Fs = gat_fs(F);
@@ -300,12 +307,12 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
   const int nmax = gat_r16(p.max_seg);
   GPMARK(0);
   // the first work item's offsets with the total (independent loads)
-  const int gfirst = min((int)blockIdx.x / p.heads, p.nseg);
+  const int gfirst = min(blk / p.heads, p.nseg);
   const int tot = p.seg_off[p.nseg], ofirst = p.seg_off[gfirst], efirst = p.seg_off[min(gfirst + 1, p.nseg)];
-  gat_zero_pad_rows(tot, p.nrows, HF, p.y, p.ldy, p.epi ? p.hp : nullptr);
+  gat_zero_pad_rows(tot, p.nrows, HF, p.y, p.ldy, p.epi ? p.hp : nullptr, blk, nblk);
   if (p.wh) {   // the saved operands too (the backward's products run over all rows)
-    gat_zero_pad_rows(tot, p.nrows, HF, p.wh, HF, nullptr);
-    gat_zero_pad_rows(tot, p.nrows, K, p.xn, K, nullptr);
+    gat_zero_pad_rows(tot, p.nrows, HF, p.wh, HF, nullptr, blk, nblk);
+    gat_zero_pad_rows(tot, p.nrows, K, p.xn, K, nullptr, blk, nblk);
   }
   double(*red)[64] = reinterpret_cast<double(*)[64]>(smem);   // 8 x 64
   float* Xs = reinterpret_cast<float*>(smem + 8 * 64 * sizeof(double));   // nmax x Ks
@@ -318,10 +325,10 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int fl = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  for (int gh = blockIdx.x; gh < p.nseg * p.heads; gh += gridDim.x) {
+  for (int gh = blk; gh < p.nseg * p.heads; gh += nblk) {
     const int g = gh / p.heads, hd = gh - g * p.heads;
-    const int o = gh == (int)blockIdx.x ? ofirst : p.seg_off[g];
-    const int n = min((gh == (int)blockIdx.x ? efirst : p.seg_off[g + 1]) - o, nmax);   // (LDS plan bound)
+    const int o = gh == blk ? ofirst : p.seg_off[g];
+    const int n = min((gh == blk ? efirst : p.seg_off[g + 1]) - o, nmax);   // (LDS plan bound)
     if (n <= 0) continue;
     const int c0 = hd * F;
     const int nr = gat_r16(n);
@@ -433,6 +440,21 @@ __global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLay
     __syncthreads();  // LDS reused by the next segment
     GPMARK(7);
   }
+}
+
+template <int NM, bool BF16>
+__global__ void __launch_bounds__(kGatThreads) gat_layer_fwd_kernel(const GatLayerArgs p) {
+  gat_layer_fwd_body<NM, BF16>(p, blockIdx.x, gridDim.x);
+}
+
+// two sets (batches) through the same layer weights in one launch
+// (sgg_gat_layer_fwd2): workgroups [0, g1) serve set a, [g1, grid) set b
+template <int NM, bool BF16>
+__global__ void __launch_bounds__(kGatThreads) gat_layer_fwd2_kernel(const GatLayerArgs a, const GatLayerArgs b, int g1) {
+  if ((int)blockIdx.x < g1)
+    gat_layer_fwd_body<NM, BF16>(a, blockIdx.x, g1);
+  else
+    gat_layer_fwd_body<NM, BF16>(b, blockIdx.x - g1, gridDim.x - g1);
 }
 
 static size_t gat_layer_lds(int K, int F, int max_seg) {
@@ -835,6 +857,44 @@ extern "C" int sgg_gat_bwd_ex(const float* Wh, int heads, const float* a_src, co
 extern "C" size_t sgg_gat_layer_lds_bytes(int K, int F, int max_seg) {
   if (K < 1 || F < 1 || max_seg < 1) return 0;
   return gat_layer_lds(K, F, max_seg);
+}
+
+static int gat_layer_set_check(const SggGatLayerSet& s, int K, int HF, char which) {
+  SGG_CHECK_ARG(s.x1 && s.seg_off && s.y && s.K1 >= 1 && s.ld1 >= s.K1 && (!s.x2 || (s.K2 >= 1 && s.ld2 >= s.K2)) &&
+                    s.K1 + (s.x2 ? s.K2 : 0) == K && s.ldy >= HF && s.nseg >= 0 && s.n >= 0,
+                "sgg_gat_layer_fwd2: bad set %c", which);
+  SGG_CHECK_ARG(s.max_seg >= 1 && s.max_seg <= SGG_GAT_MAX_NODES, "sgg_gat_layer_fwd2: set %c max segment %d",
+                which, s.max_seg);
+  SGG_CHECK_ARG(!s.wh || (s.xn && s.rstd), "sgg_gat_layer_fwd2: set %c saves without xn / rstd", which);
+  return 0;
+}
+
+extern "C" int sgg_gat_layer_fwd2(const SggGatLayerSet* sa, const SggGatLayerSet* sb, const float* w,
+                                  const float* a_src, const float* a_dst, const float* bias, int heads, int F,
+                                  float alpha, float eps, int epilogue, int bf16, void* stream) {
+  SGG_CHECK_ARG(sa && sb && w && a_src && a_dst, "sgg_gat_layer_fwd2: null pointer");
+  SGG_CHECK_ARG(F >= 1 && F <= 128 && heads >= 1 && heads <= 64, "sgg_gat_layer_fwd2: F=%d heads=%d", F, heads);
+  SGG_CHECK_ARG(epilogue == 0 || epilogue == 1, "sgg_gat_layer_fwd2: epilogue must be 0 or 1");
+  const int K = sa->K1 + (sa->x2 ? sa->K2 : 0);
+  SGG_CHECK_ARG(K >= 1 && K <= 256, "sgg_gat_layer_fwd2: K=%d", K);
+  if (int rc = gat_layer_set_check(*sa, K, heads * F, 'a')) return rc;
+  if (int rc = gat_layer_set_check(*sb, K, heads * F, 'b')) return rc;
+  SGG_CHECK_ARG(epilogue == 0 || (sa->hp && sb->hp), "sgg_gat_layer_fwd2: the ELU epilogue needs hp");
+  // one LDS plan for both sets: the larger segment bound
+  const int max_seg = sa->max_seg > sb->max_seg ? sa->max_seg : sb->max_seg;
+  const size_t lds = gat_layer_lds(K, F, max_seg);
+  SGG_CHECK_ARG(lds <= 160 * 1024, "sgg_gat_layer_fwd2: K %d, F %d, %d nodes need %zu B of LDS", K, F, max_seg, lds);
+  auto args = [&](const SggGatLayerSet& s) {
+    return GatLayerArgs{s.x1, s.x2, s.ld1, s.K1, s.ld2, s.x2 ? s.K2 : 0, w, a_src, a_dst, bias, s.seg_off, s.nseg,
+                        s.n, heads, F, epilogue, max_seg, alpha, eps, s.xn, s.rstd, s.wh, s.hp, s.y, s.ldy};
+  };
+  const int g1 = gat_grid(sa->nseg, heads), g2 = gat_grid(sb->nseg, heads);
+  auto k = bf16 ? (max_seg <= 32 ? gat_layer_fwd2_kernel<8, true> : max_seg <= 64 ? gat_layer_fwd2_kernel<16, true>
+                                                                                   : gat_layer_fwd2_kernel<32, true>)
+                : (max_seg <= 32 ? gat_layer_fwd2_kernel<8, false> : max_seg <= 64 ? gat_layer_fwd2_kernel<16, false>
+                                                                                    : gat_layer_fwd2_kernel<32, false>);
+  hipLaunchKernelGGL(k, dim3(g1 + g2), dim3(kGatThreads), lds, (hipStream_t)stream, args(*sa), args(*sb), g1);
+  SGG_RETURN_LAUNCH("sgg_gat_layer_fwd2");
 }
 
 extern "C" int sgg_gat_layer_fwd(const float* x1, int ld1, int K1, const float* x2, int ld2, int K2, const float* w,

@@ -111,6 +111,13 @@ class PoolBatch(ctypes.Structure):
                 ("gpw", _i), ("B", _i), ("max_n", _i), ("out", _p), ("argmax", _p), ("nchunks_dev", _p)]
 
 
+class GatLayerSet(ctypes.Structure):
+    """SggGatLayerSet (include/sgg.h): one batch of sgg_gat_layer_fwd2."""
+    _fields_ = [("x1", _p), ("ld1", _i), ("K1", _i), ("x2", _p), ("ld2", _i), ("K2", _i), ("seg_off", _p),
+                ("nseg", _i), ("n", _i), ("max_seg", _i), ("xn", _p), ("rstd", _p), ("wh", _p), ("hp", _p), ("y", _p),
+                ("ldy", _i)]
+
+
 class L2Job(ctypes.Structure):
     """SggL2Job (include/sgg.h): an L2 loss value of sgg_grad_finish_losses."""
     _fields_ = [("term", _p), ("S", _i), ("loss", _p)]
@@ -146,6 +153,8 @@ SIGNATURES = {
     "sgg_gat_layer_lds_bytes": (_sz, [_i, _i, _i]),
     "sgg_gat_layer_fwd": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _f, _f, _i, _i, _i, _p, _p,
                                _p, _p, _p, _i, _p]),
+    "sgg_gat_layer_fwd2": (_i, [ctypes.POINTER(GatLayerSet), ctypes.POINTER(GatLayerSet), _p, _p, _p, _p, _i, _i, _f,
+                                _f, _i, _i, _p]),
     "sgg_seg_norm_fwd": (_i, [_p, _i, _i, _p, _i, _f, _p, _i, _p, _p]),
     "sgg_seg_norm_bwd": (_i, [_p, _i, _p, _i, _i, _p, _i, _p, _p, _i, _p]),
     "sgg_group_index_ws": (_sz, [_i, _i]),

@@ -1577,14 +1577,30 @@ class _GatLayer(torch.autograd.Function):
                                           n, H, F, float(alpha), float(eps), epi, max_seg, int(bf16), N.ptr(xn),
                                           N.ptr(rstd), N.ptr(wh), N.ptr(hp), N.ptr(y), HF, N.stream_ptr()),
                     "sgg_gat_layer_fwd")
-        launch()
-        if timer.active and n > 0:
-            # norm 5 nK, transform 2 n K HF, attention 2 n^2 HF (n^2 bounded by
-            # n * max_seg); x in, W, y (+ hp) out, the saved xn / Wh
-            timer.add("sgg::gat_layer_fwd_kernel<%d, %s>" % (8 if max_seg <= 32 else 16 if max_seg <= 64 else 32,
-                                                             "true" if bf16 else "false"),
-                      (n, K, HF, H, max_seg, save), 5.0 * n * K + 2.0 * n * K * HF + 2.0 * n * max_seg * HF,
-                      4.0 * (n * K + H * K * F + n * HF * (2 if epi else 1) + (n * K + n * HF if save else 0)), launch)
+        # norm 5 nK, transform 2 n K HF, attention 2 n^2 HF (n^2 bounded by
+        # n * max_seg); x in, W, y (+ hp) out, the saved xn / Wh
+        work = (5.0 * n * K + 2.0 * n * K * HF + 2.0 * n * max_seg * HF,
+                4.0 * (n * K + n * HF * (2 if epi else 1) + (n * K + n * HF if save else 0)))
+        rider = _GRIDER[0]
+        shape = (H, F, K1, K2, epi, bf16, float(eps), float(alpha))
+        weights = (w, a_src, a_dst, bias)
+        lset = N.GatLayerSet(N.ptr(x1), x1.stride(0), K1, N.ptr(x2), x2.stride(0) if x2 is not None else 0, K2,
+                             N.ptr(seg_off), nseg, n, max_seg, N.ptr(xn), N.ptr(rstd), N.ptr(wh), N.ptr(hp), N.ptr(y), HF)
+        keep = (x1, x2, seg_off, xn, rstd, wh, hp, y)
+        name = "sgg::gat_layer_fwd_kernel<%d, %s>" % (8 if max_seg <= 32 else 16 if max_seg <= 64 else 32,
+                                                      "true" if bf16 else "false")
+        if rider is not None and not save and rider.held is None and n > 0:
+            # the discriminator step's batch: held for the generator step's
+            rider.hold(lset, keep, weights, shape, launch, (name, (n, K, HF, H, max_seg, save)) + work)
+        elif rider is not None and rider.fits(weights, shape) and n > 0:
+            pl, (S2, wk2) = rider.carry(lset, keep, max_seg, work)
+            pl()
+            if timer.active:
+                timer.add(name, (S2, K, HF, H, "pair"), wk2[0], wk2[1] + 4.0 * H * K * F, pl)
+        else:
+            launch()
+            if timer.active and n > 0:
+                timer.add(name, (n, K, HF, H, max_seg, save), work[0], work[1] + 4.0 * H * K * F, launch)
         ctx.meta = (seg_off, nseg, max_seg, float(alpha), epi, H, F, K1, K2, bias is not None)
         ctx.save_for_backward(xn, rstd, wh, hp, y, w, a_src, a_dst)
         return y
@@ -1624,6 +1640,62 @@ class _GatLayer(torch.autograd.Function):
         dx1 = dx[:, :K1] if K2 else dx
         dx2 = dx[:, K1:] if K2 else None
         return dx1, dx2, dw, da_s, da_d, dbias, None, None, None, None, None, None
+
+
+class GatLayerRider:
+    """gat_layer_pair(): a no-grad batched-GAT layer forward (the
+    discriminator step's generator, G.context_pair) is held; the next one of
+    the same layer weights and shape (the generator step's) issues both in
+    ONE launch (sgg_gat_layer_fwd2).  Layer by layer: the held layer's
+    output is written by the carrying launch before the next layer of its
+    batch is held.  A held forward nobody carried is issued on exit."""
+
+    def __init__(self):
+        self.held = None
+
+    def hold(self, lset, keep, weights, shape, launch, timing):
+        self.held = (lset, keep, weights, shape, launch, timing)
+
+    def fits(self, weights, shape):
+        if self.held is None:
+            return False
+        _, _, wh, sh, _, _ = self.held
+        return sh == shape and all(a is b for a, b in zip(wh, weights))
+
+    def carry(self, lset, keep, max_seg, work):
+        """-> (the paired launch, (rows of both, (flop, bytes) of both))."""
+        la, keep_a, (w, a_src, a_dst, bias), (H, F, _, _, epi, bf16, eps, alpha), _, timing = self.held
+        self.held = None
+        lib = _lib()
+
+        def pl(k=(keep_a, keep, w, a_src, a_dst, bias)):
+            N.check(lib.sgg_gat_layer_fwd2(N.ctypes.byref(la), N.ctypes.byref(lset), N.ptr(w), N.ptr(a_src),
+                                           N.ptr(a_dst), N.ptr(bias), H, F, alpha, eps, epi, int(bf16),
+                                           N.stream_ptr()), "sgg_gat_layer_fwd2")
+        return pl, (la.n + lset.n, (timing[2] + work[0], timing[3] + work[1]))
+
+    def flush(self):
+        if self.held is not None:
+            _, _, (w, _, _, _), (H, F, K1, K2, _, _, _, _), launch, timing = self.held
+            self.held = None
+            launch()
+            if timer.active:
+                timer.add(timing[0], timing[1], timing[2], timing[3] + 4.0 * H * (K1 + K2) * F, launch)
+
+
+_GRIDER = [None]
+
+
+@contextlib.contextmanager
+def gat_layer_pair():
+    """Batched-GAT layer forwards of two batches in shared launches (GatLayerRider)."""
+    prev = _GRIDER[0]
+    r = _GRIDER[0] = GatLayerRider()
+    try:
+        yield r
+    finally:
+        _GRIDER[0] = prev
+        r.flush()
 
 
 def gat_layer_ok(K, F, heads, max_seg, epi):

@@ -396,6 +396,30 @@ class BatchGAT(nn.Module):
             x = layer(x, graph, epi)
         return x
 
+    def forward_pair(self, xa, graph_a, xb, graph_b):
+        """forward() of two batches, a without autograd (the discriminator
+        step's) and b (the generator step's): layer by layer, each fused
+        layer of both batches in ONE launch (kernels.gat_layer_pair,
+        sgg_gat_layer_fwd2); each result as forward() computes it."""
+        if self.dropout > 0 and self.training:
+            raise NotImplementedError("dropout between GAT layers is not implemented (dropout1=0)")
+        for i, layer in enumerate(self.layer_stack):
+            epi = 0 if i + 1 == self.n_layer else 1
+            ok = BatchGAT.LAYER_FUSED and all(K.gat_layer_ok(layer.f_in, layer.f_out, layer.n_head, g.max_seg, epi)
+                                              for g in (graph_a, graph_b))
+            if ok:
+                with K.gat_layer_pair():
+                    with torch.no_grad():
+                        xa = K.gat_layer(xa, layer.w, layer.a_src, layer.a_dst, layer.bias, graph_a, epi)
+                    xb = K.gat_layer(xb, layer.w, layer.a_src, layer.a_dst, layer.bias, graph_b, epi)
+                continue
+            with torch.no_grad():
+                xa = layer(K.seg_instance_norm(torch.cat(xa, 1) if isinstance(xa, tuple) else xa, graph_a.seg_off,
+                                               graph_a.nseg), graph_a, epi)
+            xb = layer(K.seg_instance_norm(torch.cat(xb, 1) if isinstance(xb, tuple) else xb, graph_b.seg_off,
+                                           graph_b.nseg), graph_b, epi)
+        return xa, xb
+
     LAYER_FUSED = True
 
 
@@ -414,6 +438,15 @@ class BatchGATEncoder(nn.Module):
         if sc.max_n > 128:
             raise ValueError("GAT kernels hold <= 128 peds per scene (got %d)" % sc.max_n)
         return self.gat_net(h_states, K.SegmentGraph(sc.scene_off, sc.S, sc.max_n, 1, None))
+
+    def forward_pair(self, ha, sca, hb, scb):
+        """forward() of two batches (a without autograd) with each fused layer
+        in one launch for both (BatchGAT.forward_pair)."""
+        for sc in (sca, scb):
+            if sc.max_n > 128:
+                raise ValueError("GAT kernels hold <= 128 peds per scene (got %d)" % sc.max_n)
+        return self.gat_net.forward_pair(ha, K.SegmentGraph(sca.scene_off, sca.S, sca.max_n, 1, None),
+                                         hb, K.SegmentGraph(scb.scene_off, scb.S, scb.max_n, 1, None))
 
 
 # ---------------------------------------------------------------------------
@@ -773,11 +806,9 @@ class TrajectoryGenerator(nn.Module):
                 pool_a = self.pool_net(h_a, sse_a, obs_a[-1], scenes=sc_a, U=U_a)
             pool_b = self.pool_net(h_b, sse_b, obs_b[-1], scenes=sc_b, link=link, U=U_b)
         if self.graph == "sgangat":
-            # each batch's batched GAT (per-layer launches), then both
-            # GCNModules in one launch
-            with torch.no_grad():
-                x_a = self.gatencoder((h_a.view(-1, H), pool_a), sse_a, scenes=sc_a)
-            x_b = self.gatencoder((h_b.view(-1, H), pool_b), sse_b, scenes=sc_b)
+            # both batches' batched-GAT layers, then both GCNModules, in
+            # shared launches
+            x_a, x_b = self.gatencoder.forward_pair((h_a.view(-1, H), pool_a), sc_a, (h_b.view(-1, H), pool_b), sc_b)
             comp = K.GcnModCompanion(x_a, g_a[-1], sc_a)
             y_b = self.gcn_module(x_b, sse_b, obs_b[-1], g_b[-1], scenes=sc_b, companion=comp)
             return comp.y, y_b

@@ -242,6 +242,27 @@ int sgg_gat_layer_fwd(const float* x1, int ld1, int K1, const float* x2, int ld2
                       int n, int heads, int F, float alpha, float eps, int epilogue, int max_seg, int bf16,
                       float* xn, float* rstd, float* wh, float* hp, float* y, int ldy, void* stream);
 
+/* The same layer over TWO batches in one launch (the sgangat generator's two
+ * contexts of one training iteration, G.context_pair: the discriminator
+ * step's, without saved operands, and the generator step's, with them).  A
+ * set is one batch's inputs, segments and outputs, with the fields of
+ * sgg_gat_layer_fwd; the weights and layer shape are shared.  Both sets use
+ * one LDS plan (the larger max_seg); each set's results are those of its
+ * own sgg_gat_layer_fwd launch. */
+typedef struct SggGatLayerSet {
+  const float* x1;
+  int ld1, K1;
+  const float* x2;
+  int ld2, K2;
+  const int32_t* seg_off;
+  int nseg, n, max_seg;
+  float *xn, *rstd, *wh, *hp, *y;
+  int ldy;
+} SggGatLayerSet;
+int sgg_gat_layer_fwd2(const SggGatLayerSet* a, const SggGatLayerSet* b, const float* w, const float* a_src,
+                       const float* a_dst, const float* bias, int heads, int F, float alpha, float eps,
+                       int epilogue, int bf16, void* stream);
+
 /* ------------------------------------------------------------------------
  * Instance normalisation over the rows of each segment (InstanceNorm1d,
  * affine = False, of the sgangat GAT, GAT.py:71-74, 80: each scene's

@@ -1219,6 +1219,49 @@ def test_gcn_module_pair_equals_two_launches(bf16):
         assert torch.equal(g0[k], g1[k]), "d" + k
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_gat_layer_pair_equals_two_launches(prec):
+    """sgg_gat_layer_fwd2 (BatchGAT.forward_pair: each batched-GAT layer of a
+    no-grad batch and a batch with autograd in one launch) == the two
+    batches' own layer launches, bitwise: both outputs, batch b's input and
+    parameter gradients (equal segment bounds: one LDS plan either way)."""
+    from sgan import kernels as K
+    from sgan.models import BatchGATEncoder
+    from sgan.scene import SceneIndex
+    torch.manual_seed(5)
+    enc = BatchGATEncoder([40, 16, 40], [4, 1], 0.0, 0.2).to(DEV)
+    for prm in enc.parameters():
+        torch.nn.init.normal_(prm, std=0.3)
+    sizes_a, sizes_b = [20, 7, 13, 64, 2], [64, 1, 20, 9, 33, 17]
+    sca, scb = (SceneIndex(np.concatenate([[0], np.cumsum(sz)]), DEV) for sz in (sizes_a, sizes_b))
+    Ba, Bb = sum(sizes_a), sum(sizes_b)
+    ha, pa = torch.randn(Ba, 32, device=DEV), torch.randn(Ba, 8, device=DEV)
+    hb, pb = torch.randn(Bb, 32, device=DEV), torch.randn(Bb, 8, device=DEV)
+    dy = torch.randn(Bb, 40, device=DEV)
+    prev = K.precision()
+    K.set_precision(prec)
+    try:
+        res = []
+        for paired in (False, True):
+            enc.zero_grad(set_to_none=True)
+            hbi, pbi = hb.clone().requires_grad_(True), pb.clone().requires_grad_(True)
+            if paired:
+                ya, yb = enc.forward_pair((ha, pa), sca, (hbi, pbi), scb)
+            else:
+                with torch.no_grad():
+                    ya = enc((ha, pa), None, scenes=sca)
+                yb = enc((hbi, pbi), None, scenes=scb)
+            (yb * dy).sum().backward()
+            res.append((ya, yb.detach(), hbi.grad, pbi.grad, {k: q.grad.clone() for k, q in enc.named_parameters()}))
+    finally:
+        K.set_precision(prev)
+    (a0, b0, dh0, dp0, g0), (a1, b1, dh1, dp1, g1) = res
+    assert torch.equal(a0, a1) and torch.equal(b0, b1), "outputs"
+    assert torch.equal(dh0, dh1) and torch.equal(dp0, dp1), "input gradients"
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), "d" + k
+
+
 @pytest.mark.parametrize("bn,prec,sizes_a,sizes_b", [
     (8, "fp32", [20, 7, 13, 20, 2, 33], [20, 1, 20, 9, 33, 17]),
     (48, "fp32", [20, 20, 20, 20], [20, 20, 20, 20]),
