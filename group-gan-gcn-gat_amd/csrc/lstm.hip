@@ -456,11 +456,16 @@ extern "C" int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const floa
   if (act_all && mw)
     return lstm_mw_fwd(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, act_all, rel_out,
                        st, nullptr, 0, nullptr, 0, nullptr, di, rel0_out, to);
-  SGG_CHECK_ARG(!to || (mw && !(lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))),
-                "sgg_lstm_fwd_dec: the discriminator input is written by the four-wave family only (H=%d B=%d)", H, B);
-  if (!act_all && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA"))
+  if (!act_all && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) {
+    if (to) {   // the batch-MFMA family writes the discriminator input as a second segment (alone here)
+      SGG_CHECK_ARG(!h_all, "sgg_lstm_fwd_dec: the batch-MFMA family writes the discriminator input without a "
+                            "final state (h_all NULL)");
+      return lstm_fwd_mfma_dec2(di, di, A, Whh, bias, Wp, bp, T, 0, B, H, nullptr, rel_out, to, st);
+    }
     return lstm_fwd_mfma(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, nullptr, rel_out,
                          st, di);
+  }
+  SGG_CHECK_ARG(!to || mw, "sgg_lstm_fwd_dec: no family writes the discriminator input for H=%d B=%d", H, B);
   if (!act_all && mw)
     return lstm_mw_fwd(nullptr, A, Whh, bias, nullptr, nullptr, Wp, bp, T, B, H, 1, h_all, c_all, nullptr, rel_out, st,
                        nullptr, 0, nullptr, 0, nullptr, di, nullptr, to);

@@ -1561,7 +1561,9 @@ class _GatLayer(torch.autograd.Function):
         bias = bias.contiguous() if bias is not None else None
         HF = H * F
         dev = x1.device
-        save = any(ctx.needs_input_grad[:6])
+        # (under no_grad needs_input_grad still reflects the parameters'
+        # requires_grad: no backward can follow, so nothing is saved)
+        save = torch.is_grad_enabled() and any(ctx.needs_input_grad[:6])
         y = torch.empty(n, HF, device=dev, dtype=torch.float32)
         hp = torch.empty(n, HF, device=dev, dtype=torch.float32) if epi else None
         xn = rstd = wh = None
@@ -2385,9 +2387,10 @@ _RIDER = [None]
 
 
 class DecoderRider:
-    """decoder_pair(): the block's first no-grad four-wave decoder launch
-    with a fused start that writes the discriminator input (the
-    discriminator step's generator decoder) is held; the next no-grad
+    """decoder_pair(): the block's first no-grad decoder launch with a fused
+    start that writes the discriminator input (the discriminator step's
+    generator decoder, four-wave or -- at >= 4096 peds -- batch-MFMA
+    family) is held; the next no-grad
     decoder launch of the same weights on the batch-MFMA family (the
     generator step's best-of-k rollout) issues both (sgg_lstm_fwd_dec2).
     Nothing may read the held launch's outputs before that -- its
@@ -2577,8 +2580,8 @@ class _LSTMSeq(torch.autograd.Function):
                 drider = _DRIDER[0]
                 if drider is not None and not save and not dcarry and h_all is None and Wpc is not None:
                     mfma = "mfma" in lib.sgg_lstm_kernel_name(H, B, 1, 0, 0).decode()
-                    if not mfma and to is not None and drider.held is None and not drider.done:
-                        # the discriminator step's decoder: held for the rollout's launch
+                    if to is not None and drider.held is None and not drider.done:
+                        # the discriminator step's decoder (either family): held for the rollout's launch
                         dheld = True
                     elif mfma and drider.fits(H, T, A, Whh, bias, Wpc, bp):
                         fused = drider.carry(di, A, Whh, bias, Wpc, bp, T, B, H, rel_out, fkeep)

@@ -563,7 +563,9 @@ typedef struct {
  * with b != NULL (NB = 2 ncol) columns ncol .. 2 ncol - 1 hold head again,
  * then b (T steps, stride ldb); with start != NULL, start (1 x NB x 2) gets
  * pos0 (ncol x 2) for either half.  Taken by the four-wave decoder family
- * only (SGG_E_ARG otherwise, as for a start no family takes). */
+ * and, without saved or final states (h_all NULL), by the batch-MFMA family
+ * (its second-segment form of sgg_lstm_fwd_dec2 with an empty first
+ * segment); SGG_E_ARG otherwise, as for a start no family takes. */
 typedef struct {
   float* out;
   int NB;
@@ -584,10 +586,11 @@ int sgg_lstm_fwd_dec(const SggDecInit* di, const float* A, const float* Whh, con
  * the batch-MFMA family (no saved or final states): di's B sequences (the
  * generator step's best-of-k samples, B >= the family's minimum) and di2's
  * B2 (the discriminator step's generator decoder), the latter also writing
- * its discriminator input (to2, may be NULL) as sgg_lstm_fwd_dec would.  The
- * hidden2pos feedback is formed per step (rel_t = Wp h_t + bp) as in the
- * rollout, not folded into the recurrence as in the four-wave family: the
- * same values up to fp32 reassociation. */
+ * its discriminator input (to2, may be NULL) as sgg_lstm_fwd_dec would.  As
+ * in the four-wave family the hidden2pos feedback is folded into the
+ * recurrence from step 1 on (W_hh + A Wp, b + A bp), here with the weights
+ * pre-scaled for v_exp_f32 and the bias as the accumulators' start: the same
+ * values up to fp32 reassociation. */
 int sgg_lstm_fwd_dec2(const SggDecInit* di, const SggDecInit* di2, const float* A, const float* Whh,
                       const float* bias, const float* Wp, const float* bp, int T, int B, int B2, int H,
                       float* rel_out, float* rel_out2, const SggTrajOut* to2, void* stream);

@@ -929,19 +929,23 @@ def test_paired_context_step_is_bit_identical(graphed, family, monkeypatch):
         assert torch.equal(wa[k], wb[k]), k
 
 
-@pytest.mark.parametrize("graphed", [False, True])
-def test_decoder_pair_step_close(graphed, monkeypatch):
+@pytest.mark.parametrize("graphed,big", [(False, False), (True, False), (False, True)])
+def test_decoder_pair_step_close(graphed, big, monkeypatch):
     """The D-step's generator decoder launched with the G-step's best-of-k
     rollout (kernels.decoder_pair, sgg_lstm_fwd_dec2: the batch-MFMA family,
-    whose hidden2pos feedback is formed per step where the four-wave family
-    folds it into the recurrence) against the separate launches: the same
-    iterations up to fp32 reassociation (losses 1e-5, weights within 0.1 lr
-    per step: Adam normalises near-zero gradient elements)."""
+    which folds the hidden2pos feedback into the recurrence with weights
+    pre-scaled for v_exp_f32, where the four-wave family folds it unscaled)
+    against the separate launches: the same iterations up to fp32
+    reassociation (losses 1e-5, weights within 0.1 lr per step: Adam
+    normalises near-zero gradient elements).  big: 4100-ped batches, where
+    the D-step decoder itself is on the batch-MFMA family and writes its
+    discriminator input as a lone second segment when not paired."""
     from sgan import train_step as TS
     from sgan.data.synthetic import synthetic_batch
     from sgan.scene import SceneIndex
-    batch = synthetic_batch([20, 7, 13, 20, 2], seed=3, device=DEV)
-    batch_g = synthetic_batch([20, 7, 13, 20, 2], seed=4, device=DEV)
+    sizes = [20] * 205 if big else [20, 7, 13, 20, 2]
+    batch = synthetic_batch(sizes, seed=3, device=DEV)
+    batch_g = synthetic_batch(sizes, seed=4, device=DEV)
     res = []
     for dec_pair in (False, True):
         monkeypatch.setattr(TS, "DEC_PAIR", dec_pair)
@@ -1220,7 +1224,7 @@ def test_gcn_module_pair_equals_two_launches(bf16):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_gat_layer_pair_equals_two_launches(prec):
+def test_gat_layer_pair_equals_two_launches(prec, monkeypatch):
     """sgg_gat_layer_fwd2 (BatchGAT.forward_pair: each batched-GAT layer of a
     no-grad batch and a batch with autograd in one launch) == the two
     batches' own layer launches, bitwise: both outputs, batch b's input and
@@ -1238,6 +1242,9 @@ def test_gat_layer_pair_equals_two_launches(prec):
     ha, pa = torch.randn(Ba, 32, device=DEV), torch.randn(Ba, 8, device=DEV)
     hb, pb = torch.randn(Bb, 32, device=DEV), torch.randn(Bb, 8, device=DEV)
     dy = torch.randn(Bb, 40, device=DEV)
+    carried = []
+    carry = K.GatLayerRider.carry
+    monkeypatch.setattr(K.GatLayerRider, "carry", lambda self, *a: (carried.append(1), carry(self, *a))[1])
     prev = K.precision()
     K.set_precision(prec)
     try:
@@ -1247,6 +1254,7 @@ def test_gat_layer_pair_equals_two_launches(prec):
             hbi, pbi = hb.clone().requires_grad_(True), pb.clone().requires_grad_(True)
             if paired:
                 ya, yb = enc.forward_pair((ha, pa), sca, (hbi, pbi), scb)
+                assert len(carried) == 2, "each of the two layers must run as ONE paired launch"
             else:
                 with torch.no_grad():
                     ya = enc((ha, pa), None, scenes=sca)
