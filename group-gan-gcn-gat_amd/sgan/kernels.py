@@ -1546,7 +1546,7 @@ class _GatLayer(torch.autograd.Function):
     sgg_seg_norm_bwd."""
 
     @staticmethod
-    def forward(ctx, x1, x2, w, a_src, a_dst, bias, seg_off, nseg, max_seg, eps, alpha, epi):
+    def forward(ctx, x1, x2, w, a_src, a_dst, bias, seg_off, nseg, max_seg, eps, alpha, epi, grad_on=True):
         lib = _lib()
         x1 = _rows(x1, "x1")
         x2 = _rows(x2, "x2") if x2 is not None else None
@@ -1561,9 +1561,10 @@ class _GatLayer(torch.autograd.Function):
         bias = bias.contiguous() if bias is not None else None
         HF = H * F
         dev = x1.device
-        # (under no_grad needs_input_grad still reflects the parameters'
-        # requires_grad: no backward can follow, so nothing is saved)
-        save = torch.is_grad_enabled() and any(ctx.needs_input_grad[:6])
+        # grad_on: the caller's grad mode (forward itself runs with grad off;
+        # under no_grad needs_input_grad still reflects the parameters'
+        # requires_grad, but no backward can follow: nothing is saved)
+        save = grad_on and any(ctx.needs_input_grad[:6])
         y = torch.empty(n, HF, device=dev, dtype=torch.float32)
         hp = torch.empty(n, HF, device=dev, dtype=torch.float32) if epi else None
         xn = rstd = wh = None
@@ -1641,7 +1642,7 @@ class _GatLayer(torch.autograd.Function):
                                       "sgg_seg_norm_bwd"))
         dx1 = dx[:, :K1] if K2 else dx
         dx2 = dx[:, K1:] if K2 else None
-        return dx1, dx2, dw, da_s, da_d, dbias, None, None, None, None, None, None
+        return dx1, dx2, dw, da_s, da_d, dbias, None, None, None, None, None, None, None
 
 
 class GatLayerRider:
@@ -1713,7 +1714,7 @@ def gat_layer(x, w, a_src, a_dst, bias, graph, epilogue, eps=1e-5, alpha=0.2):
     launch (sgg_gat_layer_fwd); the complete graph of each segment."""
     x1, x2 = x if isinstance(x, tuple) else (x, None)
     return _GatLayer.apply(x1, x2, w, a_src, a_dst, bias, graph.seg_off, graph.nseg, graph.max_seg, eps, alpha,
-                           epilogue)
+                           epilogue, torch.is_grad_enabled())
 
 
 def gat_attention(wh, a, alpha, graph, epilogue, heads=1, bias=None):
