@@ -22,6 +22,7 @@
 // by (j, c) bitmasks, thread = hidden unit, W2 column and dW2 partial in
 // registers (see pool_bwd_kernel).
 #include <stdlib.h>
+#include <string.h>
 
 #include "sgg_common.h"
 
@@ -706,6 +707,226 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
 }
 
 
+// ---- bf16 forward, j-block form (scenes of >= 32 peds) ----------------------
+// The pairs of a chunk (i-rows [i0, i1) of one scene, R <= 64 rows) in
+// j-blocks of 16: a 16-pair MFMA group is ONE i-row against 16 consecutive j,
+// so
+//   * a j-block's 16 U rows (16 x 512 fp32, 32 KiB) are staged in LDS ONCE for
+//     all the chunk's rows and all 512 hidden units -- the next block's rows
+//     loaded into registers while this one computes, double-buffered: two
+//     barriers per j-block instead of one per 64-unit k-tile, and a scene's U
+//     crosses L2 -> LDS n / R times per row instead of once per pass of 512
+//     pairs;
+//   * the max over the group's 16 j of each output column is formed in
+//     registers (the D fragment's 4 rows in-lane, then two lane-swap steps over
+//     the four lane quarters on the 64-bit (bits << 32 | ~j) key), so one LDS
+//     atomic max per (row, column) and j-block instead of one per pair;
+//   * rows of a round: 8 waves x GPW groups (rounds for more rows).
+// Hidden units, rounding and ReLU exactly as pool_fwd_bf16_kernel (fp32
+// pre-activation U + A_x r_x + A_y r_y, rounded to bf16 once, ReLU on the
+// bits); the same argmax contract (max over j, smallest j on ties).
+constexpr int kJbRows = 16;             // j per block (the MFMA's 16 pair rows)
+constexpr int kJbUP = kHidden + 4;      // U row pitch (floats; 16-B rows)
+constexpr int kJbUQ = kJbRows * (kHidden / 4) / kBfThreads;   // U float4 per thread per block (4)
+
+template <int BN>
+__host__ __device__ constexpr size_t pool_jb_lds_bytes() {
+  return sizeof(__bf16) * (size_t)16 * PoolCfg<BN>::NT * kBfWP + sizeof(float) * 2 * kHidden +
+         sizeof(float) * 2 * (size_t)kJbRows * kJbUP + sizeof(float2) * SGG_POOL_MAX_PEDS +
+         sizeof(unsigned long long) * (size_t)kBfMaxRows * BN;
+}
+
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+// max of a 64-bit key over the four 16-lane rows of the wave (every lane gets it)
+__device__ __forceinline__ unsigned long long rows_max64(unsigned long long v) {
+  unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+  const auto l1 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h1 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  v = umax64(((unsigned long long)h1[0] << 32) | l1[0], ((unsigned long long)h1[1] << 32) | l1[1]);
+  lo = (unsigned)v;
+  hi = (unsigned)(v >> 32);
+  const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return umax64(((unsigned long long)h2[0] << 32) | l2[0], ((unsigned long long)h2[1] << 32) | l2[1]);
+}
+
+template <int BN, int GPW>
+__global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_jb_kernel(
+    const PoolSet s1, const PoolSet s2, int g1, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2) {
+  constexpr int NT = PoolCfg<BN>::NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __bf16* W2s = reinterpret_cast<__bf16*>(smem);                                // 16 NT rows x kBfWP
+  float* As = reinterpret_cast<float*>(W2s + 16 * NT * kBfWP);                  // 512 units x (A_x, A_y)
+  float* Uj = As + 2 * kHidden;                                                 // 2 x 16 rows x kJbUP
+  float2* ps = reinterpret_cast<float2*>(Uj + 2 * kJbRows * kJbUP);             // scene positions
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // rows x BN
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15, kq = lane >> 4;
+
+  // W2 (rounded to bf16; rows >= BN zero) and A, once per workgroup
+  for (int q = tid; q < 16 * NT * (kHidden / 4); q += kBfThreads) {
+    const int c = q / (kHidden / 4), c4 = q - c * (kHidden / 4);
+    float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < BN) w = *reinterpret_cast<const float4*>(W2 + (size_t)c * kHidden + 4 * c4);
+    __bf16* d = W2s + c * kBfWP + 4 * c4;
+    d[0] = (__bf16)w.x;
+    d[1] = (__bf16)w.y;
+    d[2] = (__bf16)w.z;
+    d[3] = (__bf16)w.w;
+  }
+  for (int q = tid; q < kHidden; q += kBfThreads) {
+    const float2 a = reinterpret_cast<const float2*>(A)[q];
+    As[q] = a.x;
+    As[kHidden + q] = a.y;
+  }
+
+  SGG_POOL_PICK(s1, s2, g1);
+  for (int ch = xb; ch < nch; ch += gstride) {
+    const int4 cd = chunks[ch];
+    const int s = cd.x;
+    if (cd.z <= cd.y) continue;   // an empty padding chunk (fixed-capacity plan), uniform
+    const int o = scene_off[s];
+    const int n = scene_off[s + 1] - o;
+    const int i0 = cd.y, R = min(cd.z - cd.y, kBfMaxRows);
+    const int nj = (n + kJbRows - 1) / kJbRows;
+    __syncthreads();   // (W2s / As staged; the previous chunk's readers of Uj, ps, keys done)
+    for (int q = tid; q < n; q += kBfThreads) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
+    for (int q = tid; q < R * BN; q += kBfThreads) keys[q] = 0ull;
+
+    // U rows of j-block jb: 16 rows x 128 float4, four per thread (rows >= n: zeros)
+    floatx4 ur[kJbUQ];
+    auto load_block = [&](int jb) __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = 0; e < kJbUQ; ++e) {
+        const int q = tid + kBfThreads * e;
+        const int row = q / (kHidden / 4), c4 = q - row * (kHidden / 4);
+        const int j = jb * kJbRows + row;
+        ur[e] = j < n ? *reinterpret_cast<const floatx4*>(U + (size_t)(o + j) * kHidden + 4 * c4)
+                      : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    auto store_block = [&](int buf) __attribute__((always_inline)) {
+      float* d = Uj + buf * kJbRows * kJbUP;
+#pragma unroll
+      for (int e = 0; e < kJbUQ; ++e) {
+        const int q = tid + kBfThreads * e;
+        const int row = q / (kHidden / 4), c4 = q - row * (kHidden / 4);
+        *reinterpret_cast<floatx4*>(d + row * kJbUP + 4 * c4) = ur[e];
+      }
+    };
+    load_block(0);
+    store_block(0);
+    if (nj > 1) load_block(1);
+    __syncthreads();   // ps, keys, block 0 staged
+
+    for (int jb = 0; jb < nj; ++jb) {
+      const float* ut = Uj + (jb & 1) * kJbRows * kJbUP;
+      const int j = jb * kJbRows + c16;                 // this lane's j (pair row c16 of every group)
+      const bool jok = j < n;
+      const float2 pj = ps[jok ? j : 0];
+      for (int r0 = 0; r0 < R; r0 += kBfWaves * GPW) {   // rounds of 8 waves x GPW rows
+        float2v rxy[GPW];
+        floatx4 acc[GPW][NT];
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) {
+          const int il = r0 + wave * GPW + g;
+          const float2 pi = ps[i0 + min(il, R - 1)];
+          rxy[g] = jok ? float2v{pj.x - pi.x, pj.y - pi.y} : float2v{0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        const int ngr = min(GPW, max(0, R - r0 - wave * GPW));   // this wave's rows this round (uniform)
+        const float* urow = ut + c16 * kJbUP + 8 * kq;
+#pragma unroll 2
+        for (int ks = 0; ks < kHidden / 32; ++ks) {
+          const int ku = 32 * ks + 8 * kq;   // the lane's 8 units of this k-step
+          float2v ax[4], ay[4];
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const float4 x = *reinterpret_cast<const float4*>(As + ku + 4 * v);
+            const float4 y = *reinterpret_cast<const float4*>(As + kHidden + ku + 4 * v);
+            ax[2 * v] = float2v{x.x, x.y};
+            ax[2 * v + 1] = float2v{x.z, x.w};
+            ay[2 * v] = float2v{y.x, y.y};
+            ay[2 * v + 1] = float2v{y.z, y.w};
+          }
+          bf16x8_t bfr[NT];
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            bfr[t] = *reinterpret_cast<const bf16x8_t*>(W2s + (16 * t + c16) * kBfWP + ku);
+          const float4 u0 = *reinterpret_cast<const float4*>(urow + 32 * ks);
+          const float4 u1 = *reinterpret_cast<const float4*>(urow + 32 * ks + 4);
+          const float2v uv[4] = {{u0.x, u0.y}, {u0.z, u0.w}, {u1.x, u1.y}, {u1.z, u1.w}};
+#pragma unroll
+          for (int g = 0; g < GPW; ++g) {
+            if (g < ngr) {   // (wave-uniform)
+              const float2v rx2 = rxy[g].xx, ry2 = rxy[g].yy;
+              short2v hi[4];
+#pragma unroll
+              for (int m = 0; m < 4; ++m) {
+                const float2v pre = __builtin_elementwise_fma(ay[m], ry2, __builtin_elementwise_fma(ax[m], rx2, uv[m]));
+                const short2v b = __builtin_bit_cast(short2v, __builtin_convertvector(pre, bf16x2v));
+                hi[m] = __builtin_elementwise_max(b, short2v{0, 0});
+              }
+              const short4v h01 = __builtin_shufflevector(hi[0], hi[1], 0, 1, 2, 3);
+              const short4v h23 = __builtin_shufflevector(hi[2], hi[3], 0, 1, 2, 3);
+              const bf16x8_t hv =
+                  __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(h01, h23, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+              for (int t = 0; t < NT; ++t)
+                acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hv, bfr[t], acc[g][t], 0, 0, 0);
+            }
+          }
+        }
+        // epilogue: bias, ReLU, key (bits << 32 | ~j) per D element (rows 4 kq + r
+        // = j0 + 4 kq + r, column 16 t + c16), max over the group's 16 j, one
+        // LDS atomic per (row, column)
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) {
+          if (g < ngr) {
+            const int il = r0 + wave * GPW + g;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              const int cc = 16 * t + c16;
+              const float bb = cc < BN ? b2[cc] : 0.f;
+              unsigned long long best = 0ull;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int jj = jb * kJbRows + 4 * kq + r;
+                float v = acc[g][t][r] + bb;
+                v = v > 0.f ? v : 0.f;
+                const unsigned long long key =
+                    jj < n ? (((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFull - (unsigned)jj)) : 0ull;
+                best = umax64(best, key);
+              }
+              best = rows_max64(best);
+              if (kq == 0 && cc < BN) atomicMax(&keys[il * BN + cc], best);
+            }
+          }
+        }
+      }
+      // next block: its registers to the other buffer (its last readers were
+      // block jb - 1's, all past the barrier below of that block), then the
+      // block after it into registers
+      if (jb + 1 < nj) {
+        store_block((jb + 1) & 1);
+        if (jb + 2 < nj) load_block(jb + 2);
+      }
+      __syncthreads();
+    }
+    for (int q = tid; q < R * BN; q += kBfThreads) {
+      const unsigned long long key = keys[q];
+      const size_t oi = (size_t)(o + i0) * BN + q;
+      out[oi] = __uint_as_float((unsigned)(key >> 32));
+      argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+    }
+  }
+}
+
+
 // ---- forward, resident form -------------------------------------------------// ---- forward, resident form -------------------------------------------------
 // When the whole W2^T (bn rows x 512, rows padded to 16 NT with zeros) and a
 // scene's U rows fit in LDS beside each other: the workgroup stages W2 and A
@@ -1098,7 +1319,7 @@ static int launch_fwd(const PoolSet& s1, const PoolSet& s2, const float* A, cons
 
 template <int BN>
 static int launch_fwd_bf16(const PoolSet& s1, const PoolSet& s2, const float* A, const float* W2, const float* b2,
-                           int gpw, hipStream_t st) {
+                           int gpw, int max_rows, int max_n, hipStream_t st) {
   // persistent: one 512-thread workgroup per CU (its LDS plan), each batch's
   // range a multiple of 8 (XCD-aware order) sized by its share of the chunks
   const int n1 = s1.nchunks, n2 = s2.chunks ? s2.nchunks : 0;
@@ -1114,6 +1335,22 @@ static int launch_fwd_bf16(const PoolSet& s1, const PoolSet& s2, const float* A,
       g1 = (int)(((long long)grid * n1 / (n1 + n2) + 4) & ~7LL);
       g1 = g1 < 8 ? 8 : (g1 > grid - 8 ? grid - 8 : g1);
     }
+  }
+  // scenes of >= 32 peds: the j-block form (SGG_POOL_JB=0: the pass form)
+  const char* jbe = getenv("SGG_POOL_JB");
+  const bool jb_off = jbe && strcmp(jbe, "0") == 0;
+  if (max_n >= 32 && !jb_off && pool_jb_lds_bytes<BN>() <= 160 * 1024) {
+    const size_t ljb = pool_jb_lds_bytes<BN>();
+#define SGG_POOL_JB(G) \
+  hipLaunchKernelGGL((pool_fwd_bf16_jb_kernel<BN, G>), dim3(grid), dim3(kBfThreads), ljb, st, s1, s2, g1, A, W2, b2)
+    if (max_rows > 16)
+      SGG_POOL_JB(4);
+    else if (max_rows > 8)
+      SGG_POOL_JB(2);
+    else
+      SGG_POOL_JB(1);
+#undef SGG_POOL_JB
+    SGG_RETURN_LAUNCH("sgg_pool_fwd_bf16");
   }
   const size_t lds = pool_bf16_lds_bytes<BN>();
 #define SGG_POOL_BF(G) \
@@ -1276,11 +1513,11 @@ static int pool_fwd_sets(const PoolSet& s1, const PoolSet& s2, const float* A, c
   if (s1.nchunks + (s2.chunks ? s2.nchunks : 0) == 0) return 0;
   if (bf16) {
     switch (bn) {
-      case 8: return launch_fwd_bf16<8>(s1, s2, A, W2, b2, gpw, st);
-      case 16: return launch_fwd_bf16<16>(s1, s2, A, W2, b2, gpw, st);
-      case 32: return launch_fwd_bf16<32>(s1, s2, A, W2, b2, gpw, st);
-      case 48: return launch_fwd_bf16<48>(s1, s2, A, W2, b2, gpw, st);
-      default: return launch_fwd_bf16<64>(s1, s2, A, W2, b2, gpw, st);
+      case 8: return launch_fwd_bf16<8>(s1, s2, A, W2, b2, gpw, max_rows, max_n, st);
+      case 16: return launch_fwd_bf16<16>(s1, s2, A, W2, b2, gpw, max_rows, max_n, st);
+      case 32: return launch_fwd_bf16<32>(s1, s2, A, W2, b2, gpw, max_rows, max_n, st);
+      case 48: return launch_fwd_bf16<48>(s1, s2, A, W2, b2, gpw, max_rows, max_n, st);
+      default: return launch_fwd_bf16<64>(s1, s2, A, W2, b2, gpw, max_rows, max_n, st);
     }
   }
   switch (bn) {
