@@ -1446,15 +1446,17 @@ extern "C" int sgg_pool_plan(const int32_t* host_scene_off, int S, int bn, int t
 extern "C" int sgg_pool_plan_bf16(const int32_t* host_scene_off, int S, int bn, int target_chunks, int32_t* chunks,
                                   int cap, int* max_rows, int* gpw_out) {
   // host helper for pool_fwd_bf16_kernel: chunks of whole i-rows of up to a
-  // pair budget Pb (the largest of 1024 .. 128 that still gives >= target_chunks
-  // chunks), rows spread evenly over a scene's chunks; gpw = the 16-pair groups
-  // per wave that one pass of the widest chunk needs (8 waves per workgroup)
+  // pair budget Pb (the largest of 2048 .. 128 that still gives >= target_chunks
+  // chunks: the j-block form stages a scene's U once per chunk, so the fewer,
+  // larger chunks the better while every CU has one), rows spread evenly over
+  // a scene's chunks; gpw = the 16-pair groups per wave that one pass of the
+  // widest chunk needs (8 waves per workgroup)
   if (!host_scene_off || !chunks || !max_rows || !gpw_out || S < 0 || cap < 0 || !pool_bn_ok(bn)) {
     sgg::set_error("sgg_pool_plan_bf16: bad argument");
     return SGG_E_ARG;
   }
   auto rows_of = [&](int n, int pb) { const int r = pb / n; return r < 1 ? 1 : (r > n ? n : r); };
-  int pb = 1024;
+  int pb = 2048;
   for (; pb > 128; pb >>= 1) {
     long nc = 0;
     for (int s = 0; s < S; ++s) {
