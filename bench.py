@@ -629,6 +629,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         if backend == "nccl":
+            from sgan.train_step import nccl_env
+            nccl_env()
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)

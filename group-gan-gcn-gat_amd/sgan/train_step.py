@@ -86,6 +86,13 @@ def _valid(sc):
     return {"nvalid": nv} if nv is not None else {}
 
 
+def nccl_env():
+    """Settings the RCCL process group must be created with for collectives
+    captured in a HIP graph (see DataParallel): call before
+    dist.init_process_group("nccl")."""
+    os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
+
+
 class DataParallel:
     """Scene-sharded DP context (world 1 = plain single-GPU).
 
@@ -96,7 +103,14 @@ class DataParallel:
     one graph per replay); default on for the nccl (= RCCL) backend, off for
     gloo (a host collective cannot be captured: the graph is then cut into
     segments with the all-reduces run eagerly between them).
-    SGG_CAPTURE_COLLECTIVE=0 forces the segment form."""
+    SGG_CAPTURE_COLLECTIVE=0 forces the segment form.
+
+    Captured collectives need TORCH_NCCL_CUDA_EVENT_CACHE=0 set before the
+    process group is made (nccl_env() does it): with torch's event cache on,
+    an end event last recorded inside a capture is handed to a later eager
+    collective and the process-group watchdog's query of it fails with
+    hipErrorCapturedEvent (seen once in three world-1 runs).
+    Without that setting the default falls back to the segment form."""
 
     def __init__(self, group=None, exercise=False, capture=None):
         self.on = dist.is_available() and dist.is_initialized()
@@ -106,7 +120,8 @@ class DataParallel:
         self.exercise = bool(exercise) and self.on
         if capture is None:
             capture = self.on and dist.get_backend(group) == "nccl" and \
-                os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0"
+                os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0" and \
+                os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") == "0"
         self.capture = bool(capture) and self.on
         self.cut = None   # set by GraphedTrainer while capturing: graph segment boundary
 

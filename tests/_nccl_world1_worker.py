@@ -83,8 +83,11 @@ def allreduce_us(tr, reps=20):
 
 
 def main():
+    from sgan.train_step import DataParallel, nccl_env
     torch.cuda.set_device(0)
+    nccl_env()
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    assert DataParallel(exercise=True).capture, "nccl default is the captured form"
     assert dist.get_world_size() == 1 and dist.get_backend() == "nccl"
     sizes = [20, 7, 13, 20, 2, 9]
     out = {}
