@@ -260,8 +260,15 @@ def iteration_roofline(agg, ms_step, scenes):
 
 def host_sched():
     """(run-queue wait of this thread in ns, the cgroup's throttled time in
-    us) -- None where the kernel does not expose it."""
+    us, this thread's rusage: CPU s, minor / major page faults, voluntary /
+    involuntary context switches) -- None where the kernel does not expose it."""
+    import resource
     wait = thr = None
+    try:
+        ru = resource.getrusage(resource.RUSAGE_THREAD)
+        ru = (ru.ru_utime + ru.ru_stime, ru.ru_minflt, ru.ru_majflt, ru.ru_nvcsw, ru.ru_nivcsw)
+    except (AttributeError, OSError):
+        ru = None
     try:
         wait = int(open("/proc/thread-self/schedstat").read().split()[1])
     except (OSError, ValueError, IndexError):
@@ -272,7 +279,7 @@ def host_sched():
                 thr = int(line.split()[1])
     except (OSError, ValueError):
         pass
-    return wait, thr
+    return wait, thr, ru
 
 
 def real_data_leg(dev, iters=20, warmup=3, batch=64):
@@ -351,10 +358,15 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
         # cgroup's CPU-quota throttling (cpu.stat throttled_usec) -- a host
         # stall that is neither Python nor HIP shows up in one of them
         sched = [host_sched()]
+        phases = []
+        allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc")
         for _ in range(iters):
             if mode == "graphed":
+                tn = time.perf_counter()
                 sd, sg = next(it), next(it)
+                tn = (time.perf_counter() - tn) * 1e3
                 bt.step(sd, sg)
+                phases.append((tn,) + (bt.phase_ms or (None, None, None)))
                 steps_info.append(bt.last)
                 evs.append(torch.cuda.Event(enable_timing=True))
                 evs[-1].record()
@@ -394,6 +406,24 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
             dt_ = [(b[1] - a[1]) / 1e3 if a[1] is not None and b[1] is not None else None
                    for a, b in zip(sched, sched[1:])]
             out[mode]["slowest_iteration"].update(runqueue_wait_ms=dq[k], cgroup_throttled_ms=dt_[k])
+            # where the slowest iteration's host time went: the loader's next
+            # two batches, then BucketedGraphTrainer.step's phases (layout +
+            # bucket, scene-structure uploads, draws + replay); the thread's
+            # CPU time, page faults and context switches over the iteration
+            # (a blocked thread -- a driver call, an allocation -- shows CPU
+            # time far below the wall time and voluntary switches)
+            ru0, ru1 = sched[k][2], sched[k + 1][2]
+            out[mode]["slowest_iteration"].update(
+                phase_ms=dict(zip(("next_batches", "layout_bucket", "scene_upload", "draw_replay"),
+                                  [None if x is None else round(x, 3) for x in phases[k]])),
+                thread_cpu_ms=None if ru0 is None else round((ru1[0] - ru0[0]) * 1e3, 3),
+                minor_faults=None if ru0 is None else ru1[1] - ru0[1],
+                major_faults=None if ru0 is None else ru1[2] - ru0[2],
+                voluntary_switches=None if ru0 is None else ru1[3] - ru0[3],
+                involuntary_switches=None if ru0 is None else ru1[4] - ru0[4])
+            allocs1 = torch.cuda.memory_stats(dev).get("num_device_alloc")
+            out[mode]["device_allocs_timed"] = (None if allocs0 is None or allocs1 is None
+                                                else allocs1 - allocs0)
             out[mode].update(runqueue_wait_ms_total=round(sum(x for x in dq if x is not None), 3),
                              cgroup_throttled_ms_total=(round(sum(x for x in dt_ if x is not None), 3)
                                                         if any(x is not None for x in dt_) else None))

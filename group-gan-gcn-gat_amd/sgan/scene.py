@@ -216,6 +216,11 @@ class PaddedScenes(SceneIndex):
         if self._gpu:
             self._stage = [t.pin_memory() for t in self._stage]
         self._stage_ev = [None, None]
+        # graph staging buffers (load(graph_stage=i) / head_copy(i)); pinned
+        # here: no host allocation may happen while a graph is captured
+        self._gstage = [torch.zeros(self._total, dtype=torch.int32) for _ in range(2)]
+        if self._gpu:
+            self._gstage = [t.pin_memory() for t in self._gstage]
         self._cur = 0
         self.nvalid = self._dev[0:1]
         self.scene_off = self._view("scene_off", self.S + 1)
@@ -318,20 +323,46 @@ class PaddedScenes(SceneIndex):
             out[o + 4:o + 4 + 4 * nc] = tab[:nc].reshape(-1)
         return off
 
-    def load(self, host_off_real, rows_real):
+    def _set_host(self, off, host_off_real, rows_real):
+        self.host_off = off
+        self._host_off_real, self._host_rows = host_off_real, np.asarray(rows_real, dtype=np.int32)
+        for ch in self._children.values():
+            ch.host_off = self._rep_off(self.host_off, ch.k)
+
+    def _graph_stage(self):
+        return self._gstage
+
+    def head_copy(self, i):
+        """The device arrays from graph staging buffer i (load(graph_stage=i)):
+        captured at the head of graph i.  The used length is fixed by then (every
+        pooling plan registers in the warm-up before the capture)."""
+        self._dev[:self._used].copy_(self._graph_stage()[i][:self._used], non_blocking=True)
+
+    def load(self, host_off_real, rows_real, graph_stage=None):
         """Refresh the device arrays for a batch: one asynchronous host-to-
         device copy on the current stream (graph replays issued after it read
-        the new contents)."""
+        the new contents).
+
+        graph_stage=i: only pack the batch into graph staging buffer i; the
+        copy to the device is the head_copy(i) node captured at the start of
+        graph i (BucketedGraphTrainer), and the caller has waited for graph
+        i's previous replay.  No copy is issued from the host: a per-batch
+        hipMemcpyAsync from the host stalled the thread for ~7 ms (4105 minor
+        page faults inside the call) once every ~100 iterations
+        (tools/realdata_stall_probe.py)."""
+        if graph_stage is not None:
+            host_off_real = np.asarray(host_off_real, dtype=np.int64)
+            st = self._graph_stage()[graph_stage].numpy()
+            self._set_host(self.pack(host_off_real, np.asarray(rows_real, dtype=np.int32), st), host_off_real,
+                           rows_real)
+            return
         i = self._cur
         self._cur ^= 1
         if self._stage_ev[i] is not None:
             self._stage_ev[i].synchronize()      # that staging buffer's previous copy has been consumed
         host_off_real = np.asarray(host_off_real, dtype=np.int64)
         st = self._stage[i].numpy()
-        self.host_off = self.pack(host_off_real, np.asarray(rows_real, dtype=np.int32), st)
-        self._host_off_real, self._host_rows = host_off_real, np.asarray(rows_real, dtype=np.int32)
-        for ch in self._children.values():
-            ch.host_off = self._rep_off(self.host_off, ch.k)
+        self._set_host(self.pack(host_off_real, np.asarray(rows_real, dtype=np.int32), st), host_off_real, rows_real)
         self._dev[:self._used].copy_(self._stage[i][:self._used], non_blocking=self._gpu)
         if self._gpu:
             ev = torch.cuda.Event()

@@ -43,6 +43,7 @@ import collections
 import functools
 import os
 import random
+import time
 
 import numpy as np
 import torch
@@ -620,12 +621,16 @@ class GraphedTrainer:
     device)."""
 
     def __init__(self, trainer, batch, sc, S_global=None, B_global=None, shard=(0, None), warmup=2, batch_g=None,
-                 sc_g=None, draw=None, prologue=None, iters=1, overlap=False, draw_ahead=False, draws=None):
+                 sc_g=None, draw=None, prologue=None, iters=1, overlap=False, draw_ahead=False, draws=None,
+                 head=None):
         """draw: () -> (z_d, z_g, y) host tensors of the staging shapes (default:
         trainer.draw_inputs over this rank's span); draws: a DrawSource shared
         with other trainers of the same run (default: one over `draw`);
         prologue: launches captured
-        ahead of the step (the padded real-data path's batch gathers).
+        ahead of the step (the padded real-data path's batch gathers);
+        head: head(i) captured at the start of graph i of the pair, before the
+        prologue -- copies from host staging buffers that the caller fills for
+        graph i after stage_ready() (the padded path's scene structure).
         iters (one rank): iterations per graph -- a replay runs `iters`
         consecutive iterations on the same batches (their host draws made in
         order before it), so the per-replay graph launch is paid once per
@@ -642,6 +647,7 @@ class GraphedTrainer:
         self.iters = iters = max(1, int(iters))
         self.overlap = overlap = bool(overlap) and not trainer.dp.collective
         self.prologue = prologue or (lambda: None)
+        self.head = head
         self.batch, self.sc = batch, sc
         self.batch_g, self.sc_g = batch_g, sc_g
         if batch_g is not None:
@@ -731,6 +737,8 @@ class GraphedTrainer:
                     g = torch.cuda.CUDAGraph()
                     g.capture_begin(pool=torch.cuda.graph_pool_handle())
                     self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
+                    if head is not None:
+                        head(i)
                     for j in range(iters):
                         self.prologue()
                         losses = trainer.step(batch, sc, batch_g, sc_g, inputs=self.inps[j], **self.kw)
@@ -742,6 +750,8 @@ class GraphedTrainer:
             self.done_ev = [None, None]
             self.losses = self.pair[1][1]
             return
+        if head is not None:
+            raise ValueError("GraphedTrainer: head copies need the one-graph pair (no segmented collectives)")
         K.clear_fold_cache()   # every fold the replays need must be a node of the graph
         pool = torch.cuda.graph_pool_handle()   # the segments replay in capture order: one shared pool
         with torch.cuda.stream(cap), K.capture_guard():
@@ -786,6 +796,8 @@ class GraphedTrainer:
                 head = torch.cuda.CUDAGraph()
                 head.capture_begin(pool=pool_a)
                 self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
+                if self.head is not None:
+                    self.head(i)
                 self.prologue()
                 head.capture_end()
                 for j in range(self.iters):
@@ -822,6 +834,15 @@ class GraphedTrainer:
             ga.replay()
             main.wait_stream(self.side)
             gc.replay()
+
+    def stage_ready(self):
+        """Index i of the graph the next step() replays, once graph i's previous
+        replay (which read the staging buffers of its head copies) is done:
+        the caller may then fill those buffers (head)."""
+        i = self.cur
+        if self.done_ev[i] is not None:
+            self.done_ev[i].synchronize()
+        return i
 
     def _load(self, z_d, z_g, y):
         i = self.cur
@@ -967,8 +988,19 @@ class BucketedGraphTrainer:
         self.buckets = {}
         self.eager_steps = 0
         # (diagnostics: the last step's bucket and its replays before it, or
-        # (None, "eager") for a batch pair no bucket holds)
+        # (None, "eager") for a batch pair no bucket holds; the last step's
+        # host time in ms per phase: batch layout + bucket choice, the two
+        # scene-structure uploads, the draws + graph replay)
         self.last = None
+        self.phase_ms = None
+        # replays in flight across buckets: before staging a batch the host
+        # waits for the replay `depth` steps back, so it runs at most that far
+        # ahead of the device.  (Each bucket's graph pair alone would let it
+        # run ahead by two replays PER BUCKET and then wait for all of them
+        # at once: multi-millisecond host iterations that are the queue
+        # draining, not work.)
+        self.depth = 2
+        self._inflight = collections.deque()
 
     def bucket_of(self, off_d, off_g):
         """(B_cap, np_cap) of the bucket holding both batches, or None."""
@@ -992,9 +1024,11 @@ class BucketedGraphTrainer:
     def step(self, scenes_d, scenes_g):
         """One reference iteration: the D-step on the split's scenes scenes_d,
         the G-step on scenes_g (the two consecutive loader batches)."""
+        t0 = time.perf_counter()
         off_d, rows_d = self.dd.layout(scenes_d)
         off_g, rows_g = self.dd.layout(scenes_g)
         key = self.bucket_of(off_d, off_g)
+        self.phase_ms = None
         if key is None:
             self.eager_steps += 1
             self.last = (None, "eager")
@@ -1007,10 +1041,21 @@ class BucketedGraphTrainer:
             ent["replays"] = 0
         self.last = (key, ent["replays"])
         ent["replays"] += 1
-        ent["sc_d"].load(off_d, rows_d)
-        ent["sc_g"].load(off_g, rows_g)
+        t1 = time.perf_counter()
+        # the scene structure into the staging buffers of the graph replayed
+        # next: its head copies them (no host-issued copy per batch)
+        while len(self._inflight) >= self.depth:
+            self._inflight.popleft().synchronize()
+        i = ent["gt"].stage_ready()
+        ent["sc_d"].load(off_d, rows_d, graph_stage=i)
+        ent["sc_g"].load(off_g, rows_g, graph_stage=i)
         ent["state"]["S_real"] = (len(off_d) - 1, len(off_g) - 1)
-        return ent["gt"].step()
+        t2 = time.perf_counter()
+        out = ent["gt"].step()
+        self._inflight.append(ent["gt"].done_ev[i])
+        t3 = time.perf_counter()
+        self.phase_ms = ((t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3)
+        return out
 
     @staticmethod
     def _draw(t, S_cap, state):
@@ -1061,6 +1106,10 @@ class BucketedGraphTrainer:
         def prologue(bufs=bufs, scs=(ent["sc_d"], ent["sc_g"])):   # (no reference to ent: no cycle)
             for b, sc in zip(bufs, scs):
                 dd.gather_into(sc.rows, B_cap, b)
+
+        def head(i, scs=(ent["sc_d"], ent["sc_g"])):
+            for sc in scs:
+                sc.head_copy(i)
         # the warm-up iterations must leave no trace: parameters, optimizer
         # state (created here where missing: zeros == torch Adam's fresh
         # state) and the host RNG streams are restored afterwards
@@ -1069,7 +1118,7 @@ class BucketedGraphTrainer:
         try:
             gt = GraphedTrainer(self.t, batches[0], ent["sc_d"], warmup=2, batch_g=batches[1], sc_g=ent["sc_g"],
                                 draw=functools.partial(self._draw, self.t, self.S_cap, ent["state"]),
-                                prologue=prologue)
+                                prologue=prologue, head=head)
         finally:
             with torch.no_grad():
                 for t in self._state():
