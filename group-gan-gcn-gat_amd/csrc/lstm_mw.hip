@@ -582,6 +582,9 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     int t_stop, int t_sh, int Bsrc) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
   constexpr bool decoder = DEC, wgrad = WGRAD;
+  // encoder with weight gradients: the helper waves also take db, dA and
+  // drel_in (hsum above), so the owners' step is the recurrence alone
+  constexpr bool hacc = wgrad && !decoder;
   // decoder slab rows carry [dWp (2 x H) | dbp (2)] after [dW_hh | db | dA]
   constexpr int NHS = MwCfg<H>::NHS, P0 = MwCfg<H>::P, P = P0 + (DEC ? 2 * H + 2 : 0);
   __shared__ float dgb[2][4][KS][kDgPitch];
@@ -638,6 +641,54 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
       for (int nu = 0; nu < MU; ++nu) dw[mu][nu] = floatx4{0.f, 0.f, 0.f, 0.f};
     // dw[mu][nu] += dG_g^T (units 16 mu..) x h (units 16 nu..) over the 16 peds
+    // encoder: the per-gate sums of the owners' dG image as well, off the
+    // recurrence's critical path -- db and dA (= dG r_in^T) of gate hg for
+    // every slot (lane-accumulated over the steps in the owners' former
+    // order), and gate hg's partial of drel_in = A^T dG (reduced over the
+    // lane quarters here, over the four gates by helper 4 one barrier later)
+    constexpr int KH = hacc ? KS : 1;
+    float ha0[KH], ha1[KH], hdb[KH], hdx[KH], hdy[KH];
+    float hr0 = 0.f, hr1 = 0.f, nr0 = 0.f, nr1 = 0.f;
+    if (hacc) {
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
+        const int u = slot_unit(j, q);
+        ha0[j] = A[2 * (hg * H + u)];
+        ha1[j] = A[2 * (hg * H + u) + 1];
+        hdb[j] = hdx[j] = hdy[j] = 0.f;
+      }
+    }
+    auto rel_load = [&](int t) {
+      const float2 rv = *reinterpret_cast<const float2*>(rel + ((size_t)t * B + pc) * 2);
+      nr0 = rv.x;
+      nr1 = rv.y;
+    };
+    auto hsum = [&](int buf) {
+      float f0 = 0.f, f1 = 0.f;
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
+        const float v = dgb[buf][hg][j][lane];
+        hdb[j] += v;
+        hdx[j] = fmaf(v, hr0, hdx[j]);
+        hdy[j] = fmaf(v, hr1, hdy[j]);
+        f0 = fmaf(ha0[j], v, f0);
+        f1 = fmaf(ha1[j], v, f1);
+      }
+      f0 += __shfl_xor(f0, 16);
+      f0 += __shfl_xor(f0, 32);
+      f1 += __shfl_xor(f1, 16);
+      f1 += __shfl_xor(f1, 32);
+      if (q == 0) fbp[buf][hg][c16] = make_float2(f0, f1);
+    };
+    // drel_in[t] from the four gates' partials of step t (written before the barrier just passed)
+    auto drel_store = [&](int t) {
+      if (hg == 0 && q == 0 && valid) {
+        const int buf = t & 1;
+        const float2 r0 = fbp[buf][0][c16], r1 = fbp[buf][1][c16], r2 = fbp[buf][2][c16], r3 = fbp[buf][3][c16];
+        *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) =
+            make_float2((r0.x + r1.x) + (r2.x + r3.x), (r0.y + r1.y) + (r2.y + r3.y));
+      }
+    };
     auto dw_accum = [&](int buf) {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
@@ -657,14 +708,28 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     stage_load(T - 1);
     stage_store((T - 1) & 1);
     if (T >= 2) stage_load(T - 2);
+    if (hacc) rel_load(T - 1);
     for (int t = T - 1; t >= 0; --t) {
       const int cur = t & 1;
+      if (hacc) {
+        hr0 = nr0;
+        hr1 = nr1;
+        if (t > 0) rel_load(t - 1);
+      }
       lds_barrier();   // (t)
       dw_accum(cur);
+      if (hacc) {
+        if (t < T - 1) drel_store(t + 1);
+        hsum(cur);
+      }
       if (t > 0) {
         stage_store(cur ^ 1);
         if (t > 1) stage_load(t - 2);
       }
+    }
+    if (hacc) {   // the owners' extra barrier: step 0's partials are complete
+      lds_barrier();
+      drel_store(0);
     }
     // slab row of this workgroup: D tile (mu, nu) holds rows hg H + 16 mu + 4 q + r, cols 16 nu + c16
     float* row = wpart + (size_t)blk * P;
@@ -676,6 +741,24 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
         for (int nu = 0; nu < MU; ++nu) row[(size_t)gr * H + 16 * nu + c16] = dw[mu][nu][r];
       }
+    if (hacc) {   // db / dA of gate hg: sums over the 16 peds (lanes c16 of each q)
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
+        const int u = slot_unit(j, q);
+        float a = hdb[j], x = hdx[j], y = hdy[j];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o);
+          x += __shfl_xor(x, o);
+          y += __shfl_xor(y, o);
+        }
+        if (c16 == 0) {
+          row[G4 * H + hg * H + u] = a;
+          row[G4 * H + G4 + 2 * (hg * H + u)] = x;
+          row[G4 * H + G4 + 2 * (hg * H + u) + 1] = y;
+        }
+      }
+    }
     return;
   }
 
@@ -830,19 +913,25 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           dgb[cur][k][j][lane] = vv[k];
-          db[i][k] += vv[k];
-          dax[i][k] = fmaf(vv[k], r0, dax[i][k]);
-          day[i][k] = fmaf(vv[k], r1, day[i][k]);
+          if (!hacc) {
+            db[i][k] += vv[k];
+            dax[i][k] = fmaf(vv[k], r0, dax[i][k]);
+            day[i][k] = fmaf(vv[k], r1, day[i][k]);
+          }
         }
       }
-      f0 = fmaf(aa0[i][3], vv[3], fmaf(aa0[i][2], vv[2], fmaf(aa0[i][1], vv[1], fmaf(aa0[i][0], vv[0], f0))));
-      f1 = fmaf(aa1[i][3], vv[3], fmaf(aa1[i][2], vv[2], fmaf(aa1[i][1], vv[1], fmaf(aa1[i][0], vv[0], f1))));
+      if (!hacc) {
+        f0 = fmaf(aa0[i][3], vv[3], fmaf(aa0[i][2], vv[2], fmaf(aa0[i][1], vv[1], fmaf(aa0[i][0], vv[0], f0))));
+        f1 = fmaf(aa1[i][3], vv[3], fmaf(aa1[i][2], vv[2], fmaf(aa1[i][1], vv[1], fmaf(aa1[i][0], vv[0], f1))));
+      }
     }
-    f0 += __shfl_xor(f0, 16);
-    f0 += __shfl_xor(f0, 32);
-    f1 += __shfl_xor(f1, 16);
-    f1 += __shfl_xor(f1, 32);
-    if (q == 0) fbp[cur][g][c16] = make_float2(f0, f1);
+    if (!hacc) {
+      f0 += __shfl_xor(f0, 16);
+      f0 += __shfl_xor(f0, 32);
+      f1 += __shfl_xor(f1, 16);
+      f1 += __shfl_xor(f1, 32);
+      if (q == 0) fbp[cur][g][c16] = make_float2(f0, f1);
+    }
     // this wave's share of dh_{t-1}: D row 4 q + r of tile mu is unit
     // slot_unit(4 mu + r, q), i.e. slot 4 mu + r of the next step's owners
 #pragma unroll
@@ -850,7 +939,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
       for (int r = 0; r < 4; ++r) part[cur][g][4 * mu + r][lane] = acc[mu][r];
     lds_barrier();
-    if (pgrad || (g == 0 && q == 0)) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
+    if (!hacc && (pgrad || (g == 0 && q == 0))) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
       const float2 r0 = fbp[cur][0][c16], r1 = fbp[cur][1][c16], r2 = fbp[cur][2][c16], r3 = fbp[cur][3][c16];
       const float sx = (r0.x + r1.x) + (r2.x + r3.x), sy = (r0.y + r1.y) + (r2.y + r3.y);
       if (valid && g == 0 && q == 0) {
@@ -861,6 +950,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       din_y = sy;
     }
   }
+  if (hacc) lds_barrier();   // the helpers' last drel_in partials (helper branch)
   if (t_stop > 0 && valid && g == 0 && q == 0) {   // the skipped steps' input gradients are defined as zero
     for (int t = 0; t < t_stop; ++t) *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(0.f, 0.f);
   }
@@ -871,7 +961,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       dh0[(size_t)ped * H + slot_unit(j, q)] = (part[0][0][j][lane] + part[0][1][j][lane]) + (part[0][2][j][lane] + part[0][3][j][lane]);
     }
   }
-  if (wgrad) {
+  if (wgrad && !hacc) {
     float* row = wpart + (size_t)blk * P;
     // db / dA of the owned slots: sum over the 16 peds (lanes c16 of each q)
 #pragma unroll

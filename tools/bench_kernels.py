@@ -123,6 +123,35 @@ def lstm_ab(B, T, H, decoder, reps=20):
         B, T, H, decoder, res[0][0], res[0][1], res[1][0], res[1][1]), flush=True)
 
 
+def lstm_bwd_w(B, T, H, reps=20):
+    """The four-wave backward with in-kernel weight gradients (the
+    discriminator encoder's launch: sgg_lstm_bwd with wpart), after a saving
+    forward; HIP events around back-to-back launches."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    lib = N.load()
+    rel = torch.randn(T, B, 2, device=dev) * 0.3
+    A = torch.randn(4 * H, 2, device=dev) * 0.3
+    Whh = torch.randn(4 * H, H, device=dev) * 0.2
+    bias = torch.randn(4 * H, device=dev) * 0.1
+    h0 = torch.randn(B, H, device=dev) * 0.5
+    h_all = torch.empty(T + 1, B, H, device=dev)
+    c_all = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 1)), device=dev)
+    act = torch.empty(int(lib.sgg_lstm_state_floats(T, B, H, 0)), device=dev)
+    drel_in = torch.empty(T, B, 2, device=dev)
+    dhl = torch.randn(B, H, device=dev)
+    rows = int(lib.sgg_lstm_wpart_rows(H, B))
+    wpart = torch.empty(rows * (4 * H * H + 12 * H + 2 * H + 2), device=dev)
+    N.check(lib.sgg_lstm_fwd(N.ptr(rel), N.ptr(A), N.ptr(Whh), N.ptr(bias), N.ptr(h0), None, None, None, T, B, H, 0,
+                             N.ptr(h_all), N.ptr(c_all), N.ptr(act), None, N.stream_ptr()), "lstm_fwd")
+    bwd = lambda: N.check(lib.sgg_lstm_bwd(N.ptr(A), N.ptr(Whh), None, N.ptr(h_all), N.ptr(c_all), N.ptr(act),
+                                           N.ptr(rel), None, N.ptr(dhl), None, T, B, H, 0, None, None,
+                                           N.ptr(drel_in), None, N.ptr(wpart), N.stream_ptr()), "lstm_bwd")
+    us = timeit(bwd, reps)
+    print("lstm_bwd+w B=%5d T=%2d H=%2d  %7.2f us  (%s)" % (B, T, H, us, os.environ.get("SGG_LIB", "tree")),
+          flush=True)
+
+
 def timeit(call, reps=20):
     for _ in range(3):
         call()
@@ -178,6 +207,10 @@ if __name__ == "__main__":
     if what == "roll2":   # one / two waves per SIMD (counter runs: tools/gpu_sq_rollwaves.sh)
         for B in (16384, 25600):
             lstm(B, 12, 32, True, reps=5)
+        sys.exit(0)
+    if what == "lbwd":    # the discriminator encoder's backward with weight gradients
+        for (B, T, H) in ((2560, 20, 48), (1280, 20, 48), (2560, 12, 32), (8192, 20, 48)):
+            lstm_bwd_w(B, T, H)
         sys.exit(0)
     if what == "lstm":
         for B in (1280, 2560, 4096, 25600):
