@@ -19,6 +19,9 @@
 // same permuted order once.  No LDS, no barriers: waves are independent.
 // Decoder: rel_t = Wp h_t + bp is a lane partial over its H/4 units plus two
 // cross-q shuffles, and feeds the next step's input k-step in registers.
+#include <stdlib.h>
+#include <string.h>
+
 #include "sgg_common.h"
 
 namespace sgg {
@@ -110,6 +113,47 @@ __device__ __forceinline__ void cell2(float2v yi, float2v yf, float2v yg, float2
   h = (one - ec) * rcpv((one + eo) * (one + ec));
 }
 
+// --- the split-bf16 form of the gate GEMM (X3, H = 32) ---------------------
+// An fp32 value x is the exact sum of three bf16 values: hi = x with its low 16
+// bits cleared, mid = the same of x - hi, lo = x - hi - mid (at most 8
+// significant bits left, a bf16 value).  The gate GEMM W h then runs on
+// v_mfma_f32_16x16x32_bf16 (fp32 accumulate, bf16 products exact in fp32) as
+//   W h = Wl hh + Wm hm + Wh hl + Wm hh + Wh hm + Wh hh  (+ O(2^-24) dropped:
+//         Wm hl, Wl hm, Wl hl),
+// six K = 32 MFMAs per 16-row tile (16 cycles each, and an MFMA of this shape
+// leaves half of its cycles to the VALU) instead of eight K = 4 fp32 ones (32
+// cycles each, serialised with the VALU): per step 48 x 16 instead of 64 x 32
+// cycles of the matrix pipe.  The result is the fp32 GEMM to within a few
+// fp32 roundings (not bitwise: the summation differs).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+
+// two bf16 values (the top halves of a and b) in one register, a low
+__device__ __forceinline__ unsigned pack_top(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+__device__ __forceinline__ float2v trunc16(float2v x) {
+  return float2v{__uint_as_float(__float_as_uint(x.x) & 0xffff0000u),
+                 __uint_as_float(__float_as_uint(x.y) & 0xffff0000u)};
+}
+// the three bf16x8 pieces (hi, mid, lo) of eight fp32 values v[0..7], as pairs
+__device__ __forceinline__ void split8(const float2v (&v)[4], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+  uint4v uh, um, ul;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float2v h = trunc16(v[i]);
+    const float2v r = v[i] - h;
+    const float2v m = trunc16(r);
+    const float2v l = r - m;
+    uh[i] = pack_top(h.x, h.y);
+    um[i] = pack_top(m.x, m.y);
+    ul[i] = pack_top(l.x, l.y);
+  }
+  hi = __builtin_bit_cast(bf16x8, uh);
+  mid = __builtin_bit_cast(bf16x8, um);
+  lo = __builtin_bit_cast(bf16x8, ul);
+}
+
 // DEC (runtime, uniform): the decoder's output feedback folded into the
 // recurrence.  The next input is rel_t = Wp h_t + bp, so for t >= 1
 //   W_hh h + A rel + b = (W_hh + A Wp) h + (b + A bp):
@@ -118,7 +162,7 @@ __device__ __forceinline__ void cell2(float2v yi, float2v yf, float2v yg, float2
 // MFMAs with no input k-step.  Step 0 adds A (rel_0 - Wp h_0 - bp) through
 // the input k-step.  The encoder (no feedback) keeps the input k-step
 // [r_x r_y 0 0] every step.
-template <int H>
+template <int H, bool X3>
 __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
@@ -172,7 +216,10 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
   // W' (or W_hh) in registers, columns in the permuted k order; the input
   // column [A_x A_y 0 0] by q; the accumulator start b' (or b) in the D layout
   // (rows 16 mt + 4q + r); all pre-scaled for v_exp_f32
-  float w[MT][KSH + 1];
+  static_assert(!X3 || KSH == 8, "the split-bf16 form takes H = 32 (one K = 32 MFMA per tile)");
+  constexpr int KW = X3 ? 1 : KSH + 1;
+  float w[MT][KW];
+  bf16x8 wb[X3 ? MT : 1][3];   // X3: the A operand (lane: row c16, k = 8q + j <-> k-step j) as hi, mid, lo
   floatx4 b0[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -180,12 +227,20 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     // gate of tile mt: i, f, g, o blocks of MU tiles; g (tanh) takes -2 log2(e)
     const float sc = (mt / MU == 2 ? 2.f : 1.f) * kNegLog2e;
     const float ax = A[2 * row], ay = A[2 * row + 1];
+    float wk[KSH];
 #pragma unroll
     for (int ks = 0; ks < KSH; ++ks) {
       const float wv = Whh[row * H + 16 * (ks >> 2) + 4 * q + (ks & 3)];
-      w[mt][ks] = sc * (decoder ? fmaf(ay, wp1[ks], fmaf(ax, wp0[ks], wv)) : wv);
+      wk[ks] = sc * (decoder ? fmaf(ay, wp1[ks], fmaf(ax, wp0[ks], wv)) : wv);
     }
-    w[mt][KSH] = q == 0 ? sc * ax : q == 1 ? sc * ay : 0.f;
+    if constexpr (X3) {
+      const float2v v[4] = {float2v{wk[0], wk[1]}, float2v{wk[2], wk[3]}, float2v{wk[4], wk[5]}, float2v{wk[6], wk[7]}};
+      split8(v, wb[mt][0], wb[mt][1], wb[mt][2]);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KSH; ++ks) w[mt][ks] = wk[ks];
+    }
+    w[mt][KW - 1] = q == 0 ? sc * ax : q == 1 ? sc * ay : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int brow = 16 * mt + 4 * q + r;
@@ -235,18 +290,33 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
   for (int t = 0; t < T; ++t) {
     const float xnext = (!decoder && t + 1 < T) ? load_in(t + 1) : 0.f;   // prefetch
     floatx4 acc[MT];
+    if constexpr (X3) {
+      // B operand: lane (q, ped) holds k = 8q + j <-> its own h of k-step j
+      bf16x8 hh, hm, hl;
+      split8(h, hh, hm, hl);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][0], h[0].x, b0[mt], 0, 0, 0);
+      for (int mt = 0; mt < MT; ++mt) {
+        floatx4 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][2], hh, b0[mt], 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][1], hm, a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][0], hl, a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][1], hh, a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][0], hm, a, 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][0], hh, a, 0, 0, 0);
+      }
+    } else {
 #pragma unroll
-    for (int ks = 1; ks < KSH; ++ks) {
-      const float hk = (ks & 1) ? h[ks >> 1].y : h[ks >> 1].x;
+      for (int mt = 0; mt < MT; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][0], h[0].x, b0[mt], 0, 0, 0);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][ks], hk, acc[mt], 0, 0, 0);
+      for (int ks = 1; ks < KSH; ++ks) {
+        const float hk = (ks & 1) ? h[ks >> 1].y : h[ks >> 1].x;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][ks], hk, acc[mt], 0, 0, 0);
+      }
     }
     if (!decoder || t == 0) {   // (uniform)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][KSH], xin, acc[mt], 0, 0, 0);
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt][KW - 1], xin, acc[mt], 0, 0, 0);
     }
 
     // gate activations (i, f, o sigmoid; g tanh) and the cell update, two
@@ -296,8 +366,13 @@ int launch(const float* rel, const float* A, const float* Whh, const float* bias
     sgg::set_error("sgg_lstm_fwd: the batch-MFMA rollout keeps no saved states");
     return SGG_E_ARG;
   }
-  hipLaunchKernelGGL(lstm_fwd_mfma_kernel<H>, dim3(grid + grid2), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T,
-                     B, decoder, h_all, c_all, rel_out, d, s2);
+  // the split-bf16 gate GEMM for H = 32 (SGG_LSTM_X3=0: the fp32 MFMA form)
+  const char* x3e = getenv("SGG_LSTM_X3");
+  const bool x3 = H == 32 && !(x3e && strcmp(x3e, "0") == 0);
+  constexpr bool kX3 = H == 32;
+  auto kfn = x3 ? lstm_fwd_mfma_kernel<H, kX3> : lstm_fwd_mfma_kernel<H, false>;
+  hipLaunchKernelGGL(kfn, dim3(grid + grid2), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all,
+                     c_all, rel_out, d, s2);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
 }
 

@@ -90,8 +90,13 @@ def _valid(sc):
 def nccl_env():
     """Settings the RCCL process group must be created with for collectives
     captured in a HIP graph (see DataParallel): call before
-    dist.init_process_group("nccl")."""
+    dist.init_process_group("nccl").  The process group's watchdog thread
+    polls the completion events of its collectives; one polled while a graph
+    is being captured fails with hipErrorCapturedEvent, and by default the
+    watchdog rethrows that and aborts the process: the
+    poll error is left to the next poll instead."""
     os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
+    os.environ["TORCH_NCCL_RETHROW_CUDA_ERRORS"] = "0"
 
 
 class DataParallel:
@@ -106,12 +111,11 @@ class DataParallel:
     segments with the all-reduces run eagerly between them).
     SGG_CAPTURE_COLLECTIVE=0 forces the segment form.
 
-    Captured collectives need TORCH_NCCL_CUDA_EVENT_CACHE=0 set before the
-    process group is made (nccl_env() does it): with torch's event cache on,
-    an end event last recorded inside a capture is handed to a later eager
-    collective and the process-group watchdog's query of it fails with
-    hipErrorCapturedEvent (seen once in three world-1 runs).
-    Without that setting the default falls back to the segment form."""
+    Captured collectives need the settings of nccl_env() before the process
+    group is made: the process-group watchdog's poll of a completion event
+    during a capture fails with hipErrorCapturedEvent, which by default
+    aborts the process (seen in two of five world-1 runs).
+    Without them the default falls back to the segment form."""
 
     def __init__(self, group=None, exercise=False, capture=None):
         self.on = dist.is_available() and dist.is_initialized()
@@ -122,7 +126,8 @@ class DataParallel:
         if capture is None:
             capture = self.on and dist.get_backend(group) == "nccl" and \
                 os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0" and \
-                os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") == "0"
+                os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") == "0" and \
+                os.environ.get("TORCH_NCCL_RETHROW_CUDA_ERRORS") == "0"
         self.capture = bool(capture) and self.on
         self.cut = None   # set by GraphedTrainer while capturing: graph segment boundary
 
