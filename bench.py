@@ -579,14 +579,17 @@ def bucket_allreduce_us(trainer, dev, reps=20):
     iteration's graph (no events there)."""
     nums = [sum(p.numel() for p in ps) + 3 for ps in (trainer.g_params, trainer.d_params)]
     bufs = [torch.zeros(n, device=dev) for n in nums]
+    # the communicator the captured graph uses (sgan.rccl), else the process group's
+    rc = trainer.dp.rccl
+    ar = rc.allreduce_sum_ if rc is not None else dist.all_reduce
     for b in bufs:
-        dist.all_reduce(b)
+        ar(b)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
         for b in bufs:
-            dist.all_reduce(b)
+            ar(b)
     e1.record()
     e1.synchronize()
     return e0.elapsed_time(e1) * 1e3 / reps
@@ -659,8 +662,6 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         if backend == "nccl":
-            from sgan.train_step import nccl_env
-            nccl_env()
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)

@@ -1007,6 +1007,16 @@ def capture_guard():
             gc.enable()
 
 
+def capture_error_mode():
+    """The stream-capture mode of this process's HIP-graph captures:
+    "thread_local" once a torch.distributed process group exists -- its
+    watchdog thread polls collective events while we capture, which the
+    global mode treats as an illegal call and answers by invalidating the
+    capture -- else "global" (the strictest)."""
+    import torch.distributed as dist
+    return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+
+
 @contextlib.contextmanager
 def gc_frozen():
     """Scope in which every object alive at entry (captured graphs and the
@@ -1089,7 +1099,7 @@ class LaunchTimer:
             try:
                 with torch.cuda.stream(side):
                     fn()                          # warm (instruction cache, L2)
-                    graph.capture_begin()
+                    graph.capture_begin(capture_error_mode=capture_error_mode())
                     for _ in range(reps):
                         fn()
                     graph.capture_end()

@@ -87,18 +87,6 @@ def _valid(sc):
     return {"nvalid": nv} if nv is not None else {}
 
 
-def nccl_env():
-    """Settings the RCCL process group must be created with for collectives
-    captured in a HIP graph (see DataParallel): call before
-    dist.init_process_group("nccl").  The process group's watchdog thread
-    polls the completion events of its collectives; one polled while a graph
-    is being captured fails with hipErrorCapturedEvent, and by default the
-    watchdog rethrows that and aborts the process: the
-    poll error is left to the next poll instead."""
-    os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
-    os.environ["TORCH_NCCL_RETHROW_CUDA_ERRORS"] = "0"
-
-
 class DataParallel:
     """Scene-sharded DP context (world 1 = plain single-GPU).
 
@@ -111,11 +99,11 @@ class DataParallel:
     segments with the all-reduces run eagerly between them).
     SGG_CAPTURE_COLLECTIVE=0 forces the segment form.
 
-    Captured collectives need the settings of nccl_env() before the process
-    group is made: the process-group watchdog's poll of a completion event
-    during a capture fails with hipErrorCapturedEvent, which by default
-    aborts the process (seen in two of five world-1 runs).
-    Without them the default falls back to the segment form."""
+    The captured all-reduce goes straight to RCCL (sgan.rccl.RcclComm: a
+    communicator of its own, ncclAllReduce on the capturing stream): torch's
+    process-group watchdog polls the completion event of every collective
+    the process group issues, and a poll during a capture fails with
+    hipErrorCapturedEvent and invalidates the capture."""
 
     def __init__(self, group=None, exercise=False, capture=None):
         self.on = dist.is_available() and dist.is_initialized()
@@ -125,11 +113,16 @@ class DataParallel:
         self.exercise = bool(exercise) and self.on
         if capture is None:
             capture = self.on and dist.get_backend(group) == "nccl" and \
-                os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0" and \
-                os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") == "0" and \
-                os.environ.get("TORCH_NCCL_RETHROW_CUDA_ERRORS") == "0"
+                os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0"
         self.capture = bool(capture) and self.on
         self.cut = None   # set by GraphedTrainer while capturing: graph segment boundary
+        # the captured form's own RCCL communicator (made here: every rank
+        # builds its DataParallel at the same point, the id broadcast is a
+        # collective)
+        self.rccl = None
+        if self.capture and self.collective:
+            from .rccl import RcclComm
+            self.rccl = RcclComm(group)
 
     @property
     def collective(self):
@@ -163,7 +156,10 @@ class DataParallel:
             self.cut(tensors)
             return
         flat = torch.cat([t.reshape(-1) for t in tensors])
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        if self.rccl is not None:
+            self.rccl.allreduce_sum_(flat)
+        else:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
         # unpack with one multi-tensor copy (a copy per tensor would add ~45
         # launches per optimizer step)
         views = flat.split([t.numel() for t in tensors])
@@ -740,7 +736,7 @@ class GraphedTrainer:
                 K.clear_fold_cache()   # every fold the replays need must be a node of this graph
                 with torch.cuda.stream(cap), K.capture_guard():
                     g = torch.cuda.CUDAGraph()
-                    g.capture_begin(pool=torch.cuda.graph_pool_handle())
+                    g.capture_begin(pool=torch.cuda.graph_pool_handle(), capture_error_mode=K.capture_error_mode())
                     self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
                     if head is not None:
                         head(i)
@@ -761,14 +757,14 @@ class GraphedTrainer:
         pool = torch.cuda.graph_pool_handle()   # the segments replay in capture order: one shared pool
         with torch.cuda.stream(cap), K.capture_guard():
             g = torch.cuda.CUDAGraph()
-            g.capture_begin(pool=pool)
+            g.capture_begin(pool=pool, capture_error_mode=K.capture_error_mode())
 
             def cut(tensors):
                 nonlocal g
                 g.capture_end()
                 self.segments.append((g, list(tensors)))
                 g = torch.cuda.CUDAGraph()
-                g.capture_begin(pool=pool)
+                g.capture_begin(pool=pool, capture_error_mode=K.capture_error_mode())
             dp.cut = cut if dp.segmented else None
             try:
                 self.prologue()
@@ -799,7 +795,7 @@ class GraphedTrainer:
             parts = []
             with torch.cuda.stream(cap), K.capture_guard():
                 head = torch.cuda.CUDAGraph()
-                head.capture_begin(pool=pool_a)
+                head.capture_begin(pool=pool_a, capture_error_mode=K.capture_error_mode())
                 self.inp_flat.copy_(self.stage_flat[i], non_blocking=True)
                 if self.head is not None:
                     self.head(i)
@@ -808,16 +804,16 @@ class GraphedTrainer:
                 for j in range(self.iters):
                     K.clear_fold_cache()
                     gb = torch.cuda.CUDAGraph()
-                    gb.capture_begin(pool=pool_b)
+                    gb.capture_begin(pool=pool_b, capture_error_mode=K.capture_error_mode())
                     pre = t.g_prefix(bg, scg, inputs=self.inps[j], **self.kw)
                     gb.capture_end()
                     K.clear_fold_cache()
                     ga = torch.cuda.CUDAGraph()
-                    ga.capture_begin(pool=pool_a)
+                    ga.capture_begin(pool=pool_a, capture_error_mode=K.capture_error_mode())
                     ld = t.d_step(self.batch, self.sc, inputs=self.inps[j], **self.kw)
                     ga.capture_end()
                     gc = torch.cuda.CUDAGraph()
-                    gc.capture_begin(pool=pool_a)
+                    gc.capture_begin(pool=pool_a, capture_error_mode=K.capture_error_mode())
                     lg = t.g_rest(pre)
                     gc.capture_end()
                     del pre

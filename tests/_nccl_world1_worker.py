@@ -5,8 +5,9 @@ one GPU of a lease through RCCL (backend "nccl", device_id bound).
   eager     eager steps, DataParallel(exercise=True): one flat RCCL SUM
             all-reduce per optimizer step, world size 1
   captured  GraphedTrainer, the all-reduces CAPTURED in the HIP graph
-            (DataParallel capture=True: one graph per replay), 1- and
-            2-iteration graphs
+            (DataParallel capture=True: one graph per replay, the
+            all-reduce through sgan.rccl.RcclComm), 1- and 2-iteration
+            graphs
   segmented GraphedTrainer cut at each all-reduce (capture=False: the
             collectives eager between graph segments, the form gloo needs)
 
@@ -83,9 +84,8 @@ def allreduce_us(tr, reps=20):
 
 
 def main():
-    from sgan.train_step import DataParallel, nccl_env
+    from sgan.train_step import DataParallel
     torch.cuda.set_device(0)
-    nccl_env()
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
     assert DataParallel(exercise=True).capture, "nccl default is the captured form"
     assert dist.get_world_size() == 1 and dist.get_backend() == "nccl"
