@@ -113,46 +113,9 @@ __device__ __forceinline__ void cell2(float2v yi, float2v yf, float2v yg, float2
   h = (one - ec) * rcpv((one + eo) * (one + ec));
 }
 
-// --- the split-bf16 form of the gate GEMM (X3, H = 32) ---------------------
-// An fp32 value x is the exact sum of three bf16 values: hi = x with its low 16
-// bits cleared, mid = the same of x - hi, lo = x - hi - mid (at most 8
-// significant bits left, a bf16 value).  The gate GEMM W h then runs on
-// v_mfma_f32_16x16x32_bf16 (fp32 accumulate, bf16 products exact in fp32) as
-//   W h = Wl hh + Wm hm + Wh hl + Wm hh + Wh hm + Wh hh  (+ O(2^-24) dropped:
-//         Wm hl, Wl hm, Wl hl),
-// six K = 32 MFMAs per 16-row tile (16 cycles each, and an MFMA of this shape
-// leaves half of its cycles to the VALU) instead of eight K = 4 fp32 ones (32
-// cycles each, serialised with the VALU): per step 48 x 16 instead of 64 x 32
-// cycles of the matrix pipe.  The result is the fp32 GEMM to within a few
-// fp32 roundings (not bitwise: the summation differs).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned uint4v __attribute__((ext_vector_type(4)));
-
-// two bf16 values (the top halves of a and b) in one register, a low
-__device__ __forceinline__ unsigned pack_top(float a, float b) {
-  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
-}
-__device__ __forceinline__ float2v trunc16(float2v x) {
-  return float2v{__uint_as_float(__float_as_uint(x.x) & 0xffff0000u),
-                 __uint_as_float(__float_as_uint(x.y) & 0xffff0000u)};
-}
-// the three bf16x8 pieces (hi, mid, lo) of eight fp32 values v[0..7], as pairs
-__device__ __forceinline__ void split8(const float2v (&v)[4], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
-  uint4v uh, um, ul;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float2v h = trunc16(v[i]);
-    const float2v r = v[i] - h;
-    const float2v m = trunc16(r);
-    const float2v l = r - m;
-    uh[i] = pack_top(h.x, h.y);
-    um[i] = pack_top(m.x, m.y);
-    ul[i] = pack_top(l.x, l.y);
-  }
-  hi = __builtin_bit_cast(bf16x8, uh);
-  mid = __builtin_bit_cast(bf16x8, um);
-  lo = __builtin_bit_cast(bf16x8, ul);
-}
+// X3 (H = 32): the gate GEMM on split-bf16 MFMAs (sgg_common.h mfma_x3):
+// per step 48 x 16 instead of 64 x 32 cycles of the matrix pipe, within a few
+// fp32 roundings of the fp32 form (not bitwise).
 
 // DEC (runtime, uniform): the decoder's output feedback folded into the
 // recurrence.  The next input is rel_t = Wp h_t + bp, so for t >= 1
@@ -234,8 +197,7 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
       wk[ks] = sc * (decoder ? fmaf(ay, wp1[ks], fmaf(ax, wp0[ks], wv)) : wv);
     }
     if constexpr (X3) {
-      const float2v v[4] = {float2v{wk[0], wk[1]}, float2v{wk[2], wk[3]}, float2v{wk[4], wk[5]}, float2v{wk[6], wk[7]}};
-      split8(v, wb[mt][0], wb[mt][1], wb[mt][2]);
+      split8(wk, wb[mt]);
     } else {
 #pragma unroll
       for (int ks = 0; ks < KSH; ++ks) w[mt][ks] = wk[ks];
@@ -292,17 +254,11 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     floatx4 acc[MT];
     if constexpr (X3) {
       // B operand: lane (q, ped) holds k = 8q + j <-> its own h of k-step j
-      bf16x8 hh, hm, hl;
-      split8(h, hh, hm, hl);
+      const float hv[8] = {h[0].x, h[0].y, h[1].x, h[1].y, h[2].x, h[2].y, h[3].x, h[3].y};
+      bf16x8 hb[3];
+      split8(hv, hb);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        floatx4 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][2], hh, b0[mt], 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][1], hm, a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][0], hl, a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][1], hh, a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][0], hm, a, 0, 0, 0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][0], hh, a, 0, 0, 0);
-      }
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_x3(wb[mt], hb, b0[mt]);
     } else {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)

@@ -157,6 +157,57 @@ __device__ __forceinline__ float keep_if(float v, bool keep) {
   return __int_as_float(__float_as_int(v) & (keep ? -1 : 0));
 }
 
+// --- split-bf16 fp32 products (the LSTM gate GEMMs) ---------------------
+// An fp32 value x is the exact sum of three bf16 values: hi = x with its low
+// 16 bits cleared, mid = the same of x - hi, lo = x - hi - mid (at most 8
+// significant bits remain: a bf16 value).  A K = 32 fp32 dot product then
+// runs on v_mfma_f32_16x16x32_bf16 (bf16 products exact in fp32, fp32
+// accumulation) as the six products of the pieces down to 2^-24:
+//   a.b = al.bh + am.bm + ah.bl + am.bh + ah.bm + ah.bh   (am.bl, al.bm, al.bl
+// dropped), 6 x 16 cycles of the matrix pipe per 16x16 tile against 8 x 32 for
+// the fp32 16x16x4 MFMAs, and this shape leaves half of its cycles to the VALU
+// (MI355X_MICROARCH.md).  Not bitwise the fp32 MFMA's sum: within a few fp32
+// roundings of it.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned sgg_uint4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf16_trunc(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+// two bf16 values (the top halves of a and b) in one register, a in the low half
+__device__ __forceinline__ unsigned bf16_pack_top(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+// the pieces of x as fp32 values whose low 16 bits are zero
+__device__ __forceinline__ void split3(float x, float& h, float& m, float& l) {
+  h = bf16_trunc(x);
+  const float r = x - h;
+  m = bf16_trunc(r);
+  l = r - m;
+}
+// the three bf16x8 operands (hi, mid, lo) of eight fp32 values
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&o)[3]) {
+  sgg_uint4v u[3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float h0, m0, l0, h1, m1, l1;
+    split3(v[2 * i], h0, m0, l0);
+    split3(v[2 * i + 1], h1, m1, l1);
+    u[0][i] = bf16_pack_top(h0, h1);
+    u[1][i] = bf16_pack_top(m0, m1);
+    u[2][i] = bf16_pack_top(l0, l1);
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p) o[p] = __builtin_bit_cast(bf16x8, u[p]);
+}
+// c + a.b over one K = 32 chunk from the pieces (small terms first)
+__device__ __forceinline__ floatx4 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+}
+
 __device__ __forceinline__ float elu(float x) { return x > 0.f ? x : expm1f(x); }
 // derivative of ELU(alpha = 1) from its input
 __device__ __forceinline__ float elu_grad(float x) { return x > 0.f ? 1.f : expf(x); }

@@ -1,4 +1,4 @@
-# split-bf16 rollout: all GPU tests, the rollout over batch sizes (X3 on / off), the headline bench line
+# all GPU tests (not stopping at a failure), the rollout over batch sizes (X3 on / off), the headline bench line
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
