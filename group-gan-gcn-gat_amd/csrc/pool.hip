@@ -461,6 +461,226 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
   }
 }
 
+// ---- forward, split-bf16 layer 2 (fp32 results) -----------------------------
+// pool_fwd_v_kernel's work units, tiles, chunk order and epilogue, with the
+// 512 -> bn contraction on v_mfma_f32_16x16x32_bf16 in the split form of
+// sgg_common.h (mfma_x3: fp32 operands as exact sums of three bf16 pieces,
+// six products per K = 32 chunk; within a few fp32 roundings of the fp32
+// MFMA sum, not bitwise).  Per 64-unit tile a lane consumes two K = 32 chunks:
+// unit 32 c + 8 q + j of the tile is k-element j of lane quarter q in chunk c,
+// stored at column 16 q + 8 c + j, so the lane's 16 units of U and (A_x, A_y)
+// are contiguous as in the v kernel.  Per chunk a lane forms its 8 hidden
+// values per group (2 FMA + max each, fp32), splits them (the A operand) and
+// runs NT x 6 MFMAs against the W2^T pieces, which store_tile splits once
+// into LDS (bf16, 144-byte rows: conflict-free 16-byte reads).  Per chunk
+// and group: 8 x 16 + NT x 96 cycles of the matrix pipe here against
+// 8 NT x 32 for the fp32 16x16x4 form, half of each MFMA's cycles free for
+// the VALU.  The U tile holds the batch's largest scene (umax rows).
+constexpr int kWXP = kKT + 8;    // W2 piece row pitch in bf16 (144 B)
+
+__device__ __forceinline__ int permx(int k) { return ((k >> 3) & 3) * 16 + (k >> 5) * 8 + (k & 7); }
+
+template <int BN>
+__host__ __device__ constexpr int pool_x3_tb_fixed() {   // W2 pieces + A of one tile buffer, in floats
+  return (3 * 16 * PoolCfg<BN>::NT * kWXP) / 2 + 2 * kKT;
+}
+
+template <int BN, int GPW>
+__global__ void __launch_bounds__(256, 2) pool_fwd_x3_kernel(
+    const PoolSet s1, const PoolSet s2, int g1, const float* __restrict__ A,
+    const float* __restrict__ W2 /* BN x 512 */, const float* __restrict__ b2, int umax) {
+  constexpr int NT = PoolCfg<BN>::NT;
+  const int TB = umax * kVP + pool_x3_tb_fixed<BN>();   // one tile buffer: U | W2 pieces | A
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* const tb0 = reinterpret_cast<float*>(smem);
+  float* const tb1 = tb0 + TB;
+  float2* ps = reinterpret_cast<float2*>(tb0 + 2 * TB);                                      // scene positions
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(ps + SGG_POOL_MAX_PEDS);  // rows x BN
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kq = lane >> 4;
+
+  SGG_POOL_PICK(s1, s2, g1);
+  for (int ch = xb; ch < nch; ch += gstride) {
+    const int4 cd = chunks[ch];
+    const int s = cd.x, i0 = cd.y, i1 = cd.z;
+    if (i1 <= i0) continue;   // an empty padding chunk (fixed-capacity plan), uniform over the workgroup
+    const int o = scene_off[s];
+    const int n = scene_off[s + 1] - o;
+    const int rows = i1 - i0;
+    const int npairs = rows * n;
+
+    for (int q = threadIdx.x; q < n; q += blockDim.x) ps[q] = make_float2(pos[2 * (o + q)], pos[2 * (o + q) + 1]);
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) keys[q] = 0ull;
+    __syncthreads();
+
+    int uoff[GPW];
+    float rx[GPW], ry[GPW];
+    floatx4 acc[GPW][NT];
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int p = (wave * GPW + g) * 16 + c16;
+      int il = 0, j = 0;
+      if (p < npairs) { il = p / n; j = p - il * n; }
+      uoff[g] = j * kVP + 16 * kq;
+      const float2 pj = ps[j], pi = ps[i0 + il];
+      rx[g] = p < npairs ? pj.x - pi.x : 0.f;
+      ry[g] = p < npairs ? pj.y - pi.y : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    constexpr int kUQ = (SGG_POOL_MAX_PEDS * (kKT / 4) + 255) / 256;   // float4 of U per thread
+    constexpr int kWQ = (16 * NT * (kKT / 4) + 255) / 256;            // float4 of W2 per thread
+    struct Stage {   // (native vector registers: a HIP float4 struct copied under a guard goes to scratch)
+      floatx4 u[kUQ], w[kWQ];
+      float a;
+    };
+    Stage sx;
+    auto load_tile = [&](Stage& st, int k0) {
+#pragma unroll
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n) st.u[e] = *reinterpret_cast<const floatx4*>(U + (size_t)(o + r) * kHidden + k0 + 4 * c4);
+      }
+#pragma unroll
+      for (int e = 0; e < kWQ; ++e) {   // W2 rows (nn.Linear layout), rows >= BN are zero
+        const int q = threadIdx.x + 256 * e;
+        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
+        st.w[e] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (c < BN) st.w[e] = *reinterpret_cast<const floatx4*>(W2 + (size_t)c * kHidden + k0 + 4 * c4);
+      }
+      if (threadIdx.x < 2 * kKT) st.a = A[2 * k0 + threadIdx.x];
+    };
+    // float4 c4 of a row holds units 4 c4 .. 4 c4 + 3: columns permx(4 c4) .. + 3
+    auto store_tile = [&](const Stage& st, float* tb) {
+      float* Us = tb;
+      unsigned* Wp = reinterpret_cast<unsigned*>(tb + umax * kVP);   // 3 pieces x 16 NT rows x kWXP bf16
+      float* As = tb + umax * kVP + (3 * 16 * NT * kWXP) / 2;
+#pragma unroll
+      for (int e = 0; e < kUQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int r = q / (kKT / 4), c4 = q - r * (kKT / 4);
+        if (r < n && r < umax) *reinterpret_cast<floatx4*>(Us + r * kVP + permx(4 * c4)) = st.u[e];
+      }
+#pragma unroll
+      for (int e = 0; e < kWQ; ++e) {
+        const int q = threadIdx.x + 256 * e;
+        const int c = q / (kKT / 4), c4 = q - c * (kKT / 4);
+        if (c < 16 * NT) {
+          float h[4], m[4], l[4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) split3(st.w[e][x], h[x], m[x], l[x]);
+          const int wo = (c * kWXP + permx(4 * c4)) >> 1;   // in dwords
+          *reinterpret_cast<uint2*>(Wp + wo) = make_uint2(bf16_pack_top(h[0], h[1]), bf16_pack_top(h[2], h[3]));
+          *reinterpret_cast<uint2*>(Wp + (16 * NT * kWXP) / 2 + wo) =
+              make_uint2(bf16_pack_top(m[0], m[1]), bf16_pack_top(m[2], m[3]));
+          *reinterpret_cast<uint2*>(Wp + 16 * NT * kWXP + wo) =
+              make_uint2(bf16_pack_top(l[0], l[1]), bf16_pack_top(l[2], l[3]));
+        }
+      }
+      if (threadIdx.x < 2 * kKT) {   // (A_x, A_y) of unit k at column permx(k)
+        const int k = threadIdx.x >> 1;
+        As[2 * permx(k) + (threadIdx.x & 1)] = st.a;
+      }
+    };
+    // the lane's U and (A_x, A_y) of a tile; the W2 pieces are read per chunk
+    // (compute), which keeps the wave within two per SIMD
+    struct Frag {
+      float uu[GPW][16], aa[32];
+    };
+    auto read_frag = [&](const float* tb, Frag& F) {
+      const float* Us = tb;
+      const float* As = tb + umax * kVP + (3 * 16 * NT * kWXP) / 2;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+#pragma unroll
+        for (int g = 0; g < GPW; ++g)
+          *reinterpret_cast<float4*>(&F.uu[g][4 * v]) = *reinterpret_cast<const float4*>(Us + uoff[g] + 4 * v);
+        *reinterpret_cast<float4*>(&F.aa[8 * v]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v);
+        *reinterpret_cast<float4*>(&F.aa[8 * v + 4]) = *reinterpret_cast<const float4*>(As + 32 * kq + 8 * v + 4);
+      }
+    };
+    auto compute = [&](const float* tb, const Frag& F) {
+      const bf16x8* Wp = reinterpret_cast<const bf16x8*>(tb + umax * kVP);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        bf16x8 wp[NT][3];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int pc = 0; pc < 3; ++pc)
+            wp[t][pc] = Wp[(pc * 16 * NT * kWXP + (16 * t + c16) * kWXP + 16 * kq + 8 * c) >> 3];
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) {
+          float hv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = 8 * c + j;
+            hv[j] = fmaxf(fmaf(F.aa[2 * k + 1], ry[g], fmaf(F.aa[2 * k], rx[g], F.uu[g][k])), 0.f);
+          }
+          bf16x8 hp[3];
+          split8(hv, hp);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] = mfma_x3(hp, wp[t], acc[g][t]);
+        }
+      }
+    };
+    // two LDS tile buffers, one barrier per tile: tile kt's fragments are read
+    // into registers, tile kt + 1 is stored into the other buffer (whose tile
+    // kt - 1 every wave read before the last barrier), tile kt + 2's global
+    // loads go out, then tile kt computes
+    constexpr int NKT = kHidden / kKT;
+    Frag F;
+    load_tile(sx, 0);
+    __syncthreads();  // (ps / keys init visible; previous chunk's readers done)
+    store_tile(sx, tb0);
+    load_tile(sx, kKT);
+    __syncthreads();
+#pragma unroll 1
+    for (int kt = 0; kt < NKT; ++kt) {
+      const float* tb = (kt & 1) ? tb1 : tb0;
+      read_frag(tb, F);
+      if (kt + 1 < NKT) store_tile(sx, (kt & 1) ? tb0 : tb1);
+      if (kt + 2 < NKT) load_tile(sx, (kt + 2) * kKT);
+      compute(tb, F);
+      __syncthreads();
+    }
+
+    // epilogue: bias, ReLU, max over j (as pool_fwd_kernel)
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int grp = wave * GPW + g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = grp * 16 + kq * 4 + r;
+        if (p < npairs) {
+          const int il = p / n, j = p - il * n;
+          const unsigned long long jkey = 0xFFFFFFFFull - (unsigned long long)j;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int cc = 16 * t + c16;
+            if (cc < BN) {
+              float v = acc[g][t][r] + b2[cc];
+              v = v > 0.f ? v : 0.f;
+              atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < rows * BN; q += blockDim.x) {
+      const unsigned long long key = keys[q];
+      const size_t oi = (size_t)(o + i0) * BN + q;
+      out[oi] = __uint_as_float((unsigned)(key >> 32));
+      argmax[oi] = o + (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+    }
+    __syncthreads();
+  }
+}
+
 // ---- forward, bf16 layer 2 ----------------------------------------------------
 // The opt-in bf16 precision (sgg_pool_fwd_bf16; BASELINE configs 3 and 5): the
 // 512 -> bn contraction on v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
@@ -1230,11 +1450,23 @@ static int pool_range(int nchunks) { return nchunks < 32768 ? (nchunks + 7) & ~7
 
 template <int BN, int GPW>
 static void launch_fwd_g(const PoolSet& s1, const PoolSet& s2, const float* A, const float* W2, const float* b2,
-                         int max_rows, hipStream_t st) {
+                         int max_rows, int max_n, hipStream_t st) {
   // one workgroup per chunk (host counts) in each batch's range
   const int g1 = pool_range(s1.nchunks), grid = g1 + (s2.chunks ? pool_range(s2.nchunks) : 0);
   const int nchunks = s1.nchunks + (s2.chunks ? s2.nchunks : 0);
   const size_t lds = pool_fwd_lds<BN>(max_rows);
+  // bn 32 / 48 (the discriminator's pooling): the split-bf16 contraction
+  // (SGG_POOL_X3=0: the fp32 MFMA forms below)
+  if constexpr (GPW <= 2 && BN >= 32 && BN <= 48) {
+    const char* xe = getenv("SGG_POOL_X3");
+    if (!(xe && xe[0] == '0') && max_n >= 1 && max_n <= SGG_POOL_MAX_PEDS) {
+      const int umax = (max_n + 3) & ~3;
+      const size_t lx = sizeof(float) * 2 * ((size_t)umax * kVP + pool_x3_tb_fixed<BN>()) +
+                        sizeof(float2) * SGG_POOL_MAX_PEDS + sizeof(unsigned long long) * (size_t)max_rows * BN;
+      hipLaunchKernelGGL((pool_fwd_x3_kernel<BN, GPW>), dim3(grid), dim3(256), lx, st, s1, s2, g1, A, W2, b2, umax);
+      return;
+    }
+  }
   // small grids (<= 4 chunks per CU, <= 2 pair groups per wave): the
   // fragment-native tiles (measured 1.25-1.45x faster at 64-128 scenes;
   // slower at gpw 4 / >= 1024 scenes, where occupancy hides the LDS latency)
@@ -1309,10 +1541,10 @@ static int launch_fwd(const PoolSet& s1, const PoolSet& s2, const float* A, cons
     SGG_RETURN_LAUNCH("sgg_pool_fwd");
   }
   switch (gpw) {
-    case 1: launch_fwd_g<BN, 1>(s1, s2, A, W2, b2, max_rows, st); break;
-    case 2: launch_fwd_g<BN, 2>(s1, s2, A, W2, b2, max_rows, st); break;
-    case 4: launch_fwd_g<BN, 4>(s1, s2, A, W2, b2, max_rows, st); break;
-    default: launch_fwd_g<BN, 8>(s1, s2, A, W2, b2, max_rows, st); break;
+    case 1: launch_fwd_g<BN, 1>(s1, s2, A, W2, b2, max_rows, max_n, st); break;
+    case 2: launch_fwd_g<BN, 2>(s1, s2, A, W2, b2, max_rows, max_n, st); break;
+    case 4: launch_fwd_g<BN, 4>(s1, s2, A, W2, b2, max_rows, max_n, st); break;
+    default: launch_fwd_g<BN, 8>(s1, s2, A, W2, b2, max_rows, max_n, st); break;
   }
   SGG_RETURN_LAUNCH("sgg_pool_fwd");
 }

@@ -422,13 +422,15 @@ def test_fused_lstm_other_families(H, T, decoder, B, monkeypatch):
 @pytest.mark.parametrize("form", ["SGG_POOL_RESIDENT", "SGG_POOL_V"])
 @pytest.mark.parametrize("bn", [8, 48])
 def test_pool_resident_equals_tiled(bn, form, monkeypatch):
-    """sgg_pool_fwd's alternative forms -- resident (W2^T and the scene's U
-    rows in LDS, used when they fit) and fragment-native k-tiles -- against the
-    k-tiled form on the same chunk table: the same MFMA sequence, so outputs
-    and argmax are bitwise equal."""
+    """sgg_pool_fwd's alternative fp32 forms -- resident (W2^T and the scene's
+    U rows in LDS, used when they fit) and fragment-native k-tiles -- against
+    the k-tiled form on the same chunk table: the same MFMA sequence, so
+    outputs and argmax are bitwise equal.  (The split-bf16 form, the default
+    for bn 32 / 48, is off here: test_pool_x3_vs_fp32.)"""
     from sgan import _native as N
     from sgan import kernels as K
     from sgan.scene import SceneIndex
+    monkeypatch.setenv("SGG_POOL_X3", "0")
     torch.manual_seed(bn)
     sizes = [20, 1, 7, 13, 20, 2, 17] * 3
     B = sum(sizes)
@@ -461,6 +463,55 @@ def test_pool_resident_equals_tiled(bn, form, monkeypatch):
         hid = torch.relu(Uc[s0:s1].unsqueeze(0) + r @ Ac.t())          # (i, j, 512)
         ref[s0:s1] = torch.relu(hid @ Wc.t() + bc).max(1)[0]
     close(res[0][0], ref.numpy(), rtol=1e-5, what="pool resident")
+
+
+@pytest.mark.parametrize("bn", [32, 48])
+@pytest.mark.parametrize("sizes", [[20] * 64, [20, 1, 7, 13, 20, 2, 17, 57, 33] * 4])
+def test_pool_x3_vs_fp32(bn, sizes, monkeypatch):
+    """The split-bf16 pooling forward (pool_fwd_x3_kernel, default for bn 32 /
+    48) is as accurate as the fp32 MFMA form: against an fp64 restatement of
+    the pair MLP on the same inputs, its largest error (relative to the
+    output scale) is within twice the fp32 form's and below 1e-5; every
+    argmax is equal to the fp32 form's or a near tie (the fp64 values at the
+    two j within 1e-5 of the scale)."""
+    from sgan import _native as N
+    from sgan.scene import SceneIndex
+    torch.manual_seed(7 + bn)
+    B = sum(sizes)
+    sc = SceneIndex(np.concatenate([[0], np.cumsum(sizes)]), DEV)
+    U = torch.randn(B, 512, device=DEV) * 0.3
+    pos = torch.rand(B, 2, device=DEV) * 15
+    A = torch.randn(512, 2, device=DEV) * 0.3
+    W2 = torch.randn(bn, 512, device=DEV) * 0.05
+    b2 = torch.randn(bn, device=DEV) * 0.1
+    lib = N.load()
+    chunks, nchunks, max_rows, gpw = sc.pool_plan(bn)
+    res = []
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("SGG_POOL_X3", x3)
+        out = torch.empty(B, bn, device=DEV)
+        am = torch.empty(B, bn, device=DEV, dtype=torch.int32)
+        N.check(lib.sgg_pool_fwd(N.ptr(U), N.ptr(pos), N.ptr(A), N.ptr(W2), N.ptr(b2), N.ptr(sc.scene_off),
+                                 N.ptr(chunks), nchunks, max_rows, gpw, B, bn, sc.max_n, N.ptr(out), N.ptr(am),
+                                 None, N.stream_ptr()), "pool")
+        res.append((out.cpu().double(), am.cpu()))
+    (ox, ax), (of, af) = res
+    Uc, pc, Ac, Wc, bc = (t.cpu().double() for t in (U, pos, A, W2, b2))
+    ref = torch.empty(B, bn, dtype=torch.float64)
+    zs = []
+    for s0, s1 in zip(sc.host_off[:-1], sc.host_off[1:]):
+        r = pc[s0:s1].unsqueeze(0) - pc[s0:s1].unsqueeze(1)          # [i, j] = p_j - p_i
+        z = torch.relu(torch.relu(Uc[s0:s1].unsqueeze(0) + r @ Ac.t()) @ Wc.t() + bc)   # (i, j, bn)
+        ref[s0:s1] = z.max(1)[0]
+        zs.append((int(s0), z))
+    scale = float(ref.abs().max())
+    ex, ef = float((ox - ref).abs().max()) / scale, float((of - ref).abs().max()) / scale
+    assert ex <= 2 * ef + 1e-7 and ex <= 1e-5, (ex, ef)
+    diff = (ax != af).nonzero().tolist()
+    for i, c in diff:
+        s0, z = next((s0, z) for s0, z in reversed(zs) if s0 <= i)
+        a, b = int(ax[i, c]) - s0, int(af[i, c]) - s0
+        assert abs(float(z[i - s0, a, c] - z[i - s0, b, c])) <= 1e-5 * scale, (i, c)
 
 
 def test_xtw_matches_torch():

@@ -208,6 +208,10 @@ if __name__ == "__main__":
         for B in (16384, 25600):
             lstm(B, 12, 32, True, reps=5)
         sys.exit(0)
+    if what == "dpool":   # the discriminator's pooling (bn 48) at the training shapes
+        for (S, n) in ((128, 20), (64, 20), (256, 20), (128, 57)):
+            run(S, n, 48, 48)
+        sys.exit(0)
     if what == "lbwd":    # the discriminator encoder's backward with weight gradients
         for (B, T, H) in ((2560, 20, 48), (1280, 20, 48), (2560, 12, 32), (8192, 20, 48)):
             lstm_bwd_w(B, T, H)
