@@ -34,6 +34,7 @@ constexpr int kRedJobs = SGG_RED_MAX + 2 * SGG_FOLDB_MAX;   // + each fold's (dA
 
 struct FinishArgs {
   SggRed red[kRedJobs];
+  unsigned char vec[kRedJobs];   // job j read as float4 columns (16-byte aligned rows and first column)
   int nred;
   int blk0[kRedJobs + 1];   // first workgroup of red job j (after the loss workgroup, if any); blk0[nred]: end
   SggL2Job l2[SGG_LOSSJOB_MAX];
@@ -56,8 +57,54 @@ __device__ __forceinline__ float phase_sum(const float* __restrict__ src, int ro
   return s;
 }
 
-__device__ void red_job(const SggRed& d, int blk, float (*rpart)[64]) {
+// the same phase sums over four adjacent columns (one 16-byte load per row)
+__device__ __forceinline__ floatx4 phase_sum4(const float* __restrict__ src, int rows, int ld, int col, int ph) {
+  floatx4 s = {0.f, 0.f, 0.f, 0.f};
+  int r = ph;
+  for (; r + 48 < rows; r += 64) {
+    const floatx4 v0 = *reinterpret_cast<const floatx4*>(src + (size_t)r * ld + col);
+    const floatx4 v1 = *reinterpret_cast<const floatx4*>(src + (size_t)(r + 16) * ld + col);
+    const floatx4 v2 = *reinterpret_cast<const floatx4*>(src + (size_t)(r + 32) * ld + col);
+    const floatx4 v3 = *reinterpret_cast<const floatx4*>(src + (size_t)(r + 48) * ld + col);
+    s += v0;
+    s += v1;
+    s += v2;
+    s += v3;
+  }
+  for (; r < rows; r += 16) s += *reinterpret_cast<const floatx4*>(src + (size_t)r * ld + col);
+  return s;
+}
+
+__device__ __forceinline__ void red_store(const SggRed& d, int c, float v) {
+  if (d.map == 0) {
+    d.out[c] = v;
+  } else {
+    const int m = c / d.N, n = c - m * d.N;
+    d.out[d.trans ? (size_t)n * d.ldo + m : (size_t)m * d.ldo + n] = v;
+  }
+}
+
+// a workgroup of 1024 threads = 16 row phases x 64 lanes: 64 columns per
+// workgroup, or 256 when the job's rows are read as float4 (vec) -- a quarter
+// of the workgroups and of the load instructions for the same bytes, and the
+// same per-column order of additions (bit-identical)
+__device__ void red_job(const SggRed& d, bool vec, int blk, float (*rpart)[256]) {
   const int el = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  if (vec) {
+    const int c = blk * 256 + 4 * el;
+    const floatx4 s = c < d.cols ? phase_sum4(d.src + d.col0, d.rows, d.ld, c, ph) : floatx4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<floatx4*>(&rpart[ph][4 * el]) = s;
+    __syncthreads();
+    if (ph == 0 && c < d.cols) {
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < 16; ++p) v += *reinterpret_cast<const floatx4*>(&rpart[p][4 * el]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (c + i < d.cols) red_store(d, c + i, v[i]);
+    }
+    return;
+  }
   const int c = blk * 64 + el;
   const float s = c < d.cols ? phase_sum(d.src + d.col0, d.rows, d.ld, c, ph) : 0.f;
   rpart[ph][el] = s;
@@ -66,12 +113,7 @@ __device__ void red_job(const SggRed& d, int blk, float (*rpart)[64]) {
     float v = 0.f;
 #pragma unroll
     for (int p = 0; p < 16; ++p) v += rpart[p][el];
-    if (d.map == 0) {
-      d.out[c] = v;
-    } else {
-      const int m = c / d.N, n = c - m * d.N;
-      d.out[d.trans ? (size_t)n * d.ldo + m : (size_t)m * d.ldo + n] = v;
-    }
+    red_store(d, c, v);
   }
 }
 
@@ -160,7 +202,7 @@ __device__ void bce_value(const SggBceJob& d, const BceIn& in, float addend, flo
   __syncthreads();
 }
 
-__device__ void loss_workgroup(const FinishArgs& a, float (*rpart)[64]) {
+__device__ void loss_workgroup(const FinishArgs& a, float (*rpart)[256]) {
   __shared__ float lv[SGG_LOSSJOB_MAX];
   BceIn in[SGG_LOSSJOB_MAX];
 #pragma unroll
@@ -191,7 +233,7 @@ __device__ void loss_workgroup(const FinishArgs& a, float (*rpart)[64]) {
 // workgroups = (with loss jobs) the loss workgroup, then the red jobs' 64-column
 // blocks (1024 threads: 64 columns x 16 row phases)
 __global__ void __launch_bounds__(1024) grad_finish_kernel(FinishArgs a) {
-  __shared__ float rpart[16][64];
+  __shared__ __attribute__((aligned(16))) float rpart[16][256];
   const int lw = a.nl2 + a.nbce > 0;   // (the loss workgroup is block 0: dispatched first, beside the row sums)
   const int b = (int)blockIdx.x - lw;
   if (b < 0) {   // the loss values: every L2 job, then every BCE job (an addend may be an L2 loss)
@@ -200,7 +242,7 @@ __global__ void __launch_bounds__(1024) grad_finish_kernel(FinishArgs a) {
   }
   int j = 0;
   while (j + 1 < a.nred && b >= a.blk0[j + 1]) ++j;
-  red_job(a.red[j], b - a.blk0[j], rpart);
+  red_job(a.red[j], a.vec[j] != 0, b - a.blk0[j], rpart);
 }
 
 }  // namespace
@@ -271,8 +313,10 @@ extern "C" int sgg_grad_finish_losses(const SggRed* reds, int nred, const SggFol
   a.nred = nj;
   int blk = 0;
   for (int j = 0; j < nj; ++j) {
+    const SggRed& d = a.red[j];
+    a.vec[j] = d.ld % 4 == 0 && d.col0 % 4 == 0 && (reinterpret_cast<uintptr_t>(d.src) & 15) == 0;
     a.blk0[j] = blk;
-    blk += (a.red[j].cols + 63) / 64;
+    blk += a.vec[j] ? (d.cols + 255) / 256 : (d.cols + 63) / 64;
   }
   a.blk0[nj] = blk;
   for (int j = 0; j < nl2; ++j) a.l2[j] = l2[j];

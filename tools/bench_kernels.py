@@ -208,6 +208,11 @@ if __name__ == "__main__":
         for B in (16384, 25600):
             lstm(B, 12, 32, True, reps=5)
         sys.exit(0)
+    if what == "mwf":     # the four-wave forward of the discriminator's encoder (H 48), saving / not
+        for B in (2560, 1280):
+            for save in (True, False):
+                lstm(B, 12, 48, False, save=save)
+        sys.exit(0)
     if what == "dpool":   # the discriminator's pooling (bn 48) at the training shapes
         for (S, n) in ((128, 20), (64, 20), (256, 20), (128, 57)):
             run(S, n, 48, 48)

@@ -1,4 +1,4 @@
-# split-bf16 pooling forward: all GPU tests, the D pooling microbench (X3 on / off), the headline bench line
+# all GPU tests, the D pooling microbench (X3 on / off), the headline bench line
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
