@@ -572,6 +572,10 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd3_kernel(MwSeg a, MwSeg
     mw_fwd_body<HC, false, SC>(c, blk - nblk_a - nblk_b);
 }
 
+#ifndef SGG_MW_BWD_X3
+#define SGG_MW_BWD_X3 1
+#endif
+
 template <int H, bool DEC, bool WGRAD>
 __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_bwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Whh, const float* __restrict__ Wp,
@@ -582,6 +586,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     int t_stop, int t_sh, int Bsrc) {
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
   constexpr bool decoder = DEC, wgrad = WGRAD;
+  constexpr bool BX3 = SGG_MW_BWD_X3 != 0;   // dh_{t-1} partials on split-bf16 MFMAs (below)
   // encoder with weight gradients: the helper waves also take db, dA and
   // drel_in (hsum above), so the owners' step is the recurrence alone
   constexpr bool hacc = wgrad && !decoder;
@@ -783,6 +788,33 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
         wt[mu][i][r] = decoder ? fmaf(a1, Wp[H + col], fmaf(a0, Wp[col], v)) : v;
       }
     }
+  // X3: P_w on split-bf16 MFMAs (sgg_common.h mfma_x3).  The lane's 4 MU dG
+  // values (slot i, gate r at index 4 i + r) are its k-elements of K = 32
+  // chunks -- k = 32 ch + 8 q + j <-> index 8 ch + j of lane quarter q, zero
+  // past 4 MU -- so the B operand is the lane's own values and the A operand
+  // the same W_hh^T entries as wt (their pieces, built once here; the
+  // decoder's plain set for step 0 beside the folded one while MU <= 2).
+  constexpr int KCH = (4 * MU + 7) / 8;
+  constexpr bool kWq0 = BX3 && DEC && MU <= 2;
+  bf16x8 wq[BX3 ? MU : 1][BX3 ? KCH : 1][3], wq0[kWq0 ? MU : 1][kWq0 ? KCH : 1][3];
+  auto build_wq = [&](const float (&w)[MU][MU][4], bf16x8 (&o)[BX3 ? MU : 1][BX3 ? KCH : 1][3]) {
+    if constexpr (BX3) {
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+        for (int ch = 0; ch < KCH; ++ch) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int x = 8 * ch + j;
+            v[j] = x < 4 * MU ? w[mu][x >> 2][x & 3] : 0.f;
+          }
+          split8(v, o[mu][ch]);
+        }
+    }
+  };
+  build_wq(wt, wq);
+  if constexpr (kWq0) build_wq(wt0, wq0);
   // per owned slot: rows of A for the four gates (A^T dG), Wp columns, dc
   float aa0[MU][4], aa1[MU][4], wp0[MU], wp1[MU], dc[MU], dh[MU];
 #pragma unroll
@@ -880,10 +912,25 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             wt[mu][i][r] = wt0_reg ? wt0[mu][i][r] : Whh[(r * H + slot_unit(g * MU + i, q)) * H + 16 * mu + c16];
+      if constexpr (BX3) {
+        if constexpr (kWq0) {
+#pragma unroll
+          for (int mu = 0; mu < MU; ++mu)
+#pragma unroll
+            for (int ch = 0; ch < KCH; ++ch)
+#pragma unroll
+              for (int pc3 = 0; pc3 < 3; ++pc3) wq[mu][ch][pc3] = wq0[mu][ch][pc3];
+        } else {
+          build_wq(wt, wq);
+        }
+      }
     }
     floatx4 acc[MU];
 #pragma unroll
     for (int mu = 0; mu < MU; ++mu) acc[mu] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float vall[BX3 ? 8 * KCH : 1];   // X3: the lane's dG values in k order, zero padded
+#pragma unroll
+    for (int x = 0; x < (BX3 ? 8 * KCH : 1); ++x) vall[x] = 0.f;
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
       const int j = g * MU + i;
@@ -905,10 +952,26 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       // adds nothing to the weight gradients
       const float vv[4] = {keep_if(dct * gg * ig * (1.f - ig), valid), keep_if(dct * ccp[i] * fg * (1.f - fg), valid),
                            keep_if(dct * ig * (1.f - gg * gg), valid), keep_if(d_o * og * (1.f - og), valid)};
+      if constexpr (BX3) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < 4; ++r) vall[4 * i + r] = vv[r];
+        // a chunk's MFMAs as soon as its 8 values are in (slots 0-1, then 2-3)
+        if ((4 * i + 4) % 8 == 0 || i == MU - 1) {
+          const int ch = (4 * i) / 8;
+          float v8[8];
 #pragma unroll
-        for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[mu][i][r], vv[r], acc[mu], 0, 0, 0);
+          for (int x = 0; x < 8; ++x) v8[x] = vall[8 * ch + x];
+          bf16x8 hp[3];
+          split8(v8, hp);
+#pragma unroll
+          for (int mu = 0; mu < MU; ++mu) acc[mu] = mfma_x3(wq[mu][ch], hp, acc[mu]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[mu][i][r], vv[r], acc[mu], 0, 0, 0);
+      }
       if (wgrad) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {

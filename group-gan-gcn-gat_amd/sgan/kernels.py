@@ -1129,10 +1129,17 @@ def _pool_flops(scenes, bn):
     return float((sz * sz).sum()) * 512.0 * (4 + 2 * bn)
 
 
-def _pool_kname(bn, gpw, nchunks, bf16, dev):
+def _pool_kname(bn, gpw, nchunks, bf16, dev, max_n=None, max_rows=None):
     """The forward kernel the library picks (pool.hip launch_fwd_g / launch_fwd_bf16)."""
     if bf16:
-        return "sgg::pool_fwd_bf16_kernel<%d, %d>" % (bn, 4 if gpw >= 4 and bn <= 48 else (2 if gpw >= 2 else 1))
+        g = 4 if gpw >= 4 and bn <= 48 else (2 if gpw >= 2 else 1)
+        if max_n is not None and max_n >= 32 and os.environ.get("SGG_POOL_JB") != "0":
+            # the j-block form, its wave groups from the plan's rows
+            gj = "*" if max_rows is None else (4 if max_rows > 16 else (2 if max_rows > 8 else 1))
+            return "sgg::pool_fwd_bf16_jb_kernel<%d, %s>" % (bn, gj)
+        return "sgg::pool_fwd_bf16_kernel<%d, %d>" % (bn, g)
+    if gpw <= 2 and 32 <= bn <= 48 and os.environ.get("SGG_POOL_X3", "1")[:1] != "0":
+        return "sgg::pool_fwd_x3_kernel<%d, %d>" % (bn, gpw)
     small = gpw <= 2 and nchunks <= 4 * torch.cuda.get_device_properties(dev).multi_processor_count
     return "sgg::" + ("pool_fwd_v_kernel<%d, %d>" % (bn, gpw) if small else "pool_fwd_kernel<%d, %d, 2>" % (bn, gpw))
 
@@ -1260,14 +1267,14 @@ class _Pool(torch.autograd.Function):
                                                              nchunks, work)
             pl()
             if timer.active:
-                timer.add(_pool_kname(bn, gpw, nch2, bf16, h.device), (S2, B2, "pair"), fl2, nb2 + _pool_wbytes(bn),
-                          pl)
+                timer.add(_pool_kname(bn, gpw, nch2, bf16, h.device, scenes.max_n, max_rows), (S2, B2, "pair"), fl2,
+                          nb2 + _pool_wbytes(bn), pl)
         else:
             if rider is not None:
                 rider.flush()
             launch()
             if timer.active:
-                timer.add(_pool_kname(bn, gpw, nchunks, bf16, h.device), (scenes.S, B), work[2],
+                timer.add(_pool_kname(bn, gpw, nchunks, bf16, h.device, scenes.max_n, max_rows), (scenes.S, B), work[2],
                           nb + _pool_wbytes(bn), launch)
         ctx.scenes = scenes
         ctx.E = E
