@@ -848,8 +848,10 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     float* ginv = reinterpret_cast<float*>(cnt + NP);
     int* Mp = reinterpret_cast<int*>(ginv + NP);
     unsigned long long* gm = reinterpret_cast<unsigned long long*>(lab + gm_offset(NP));
-    const int o = q.scene_off[sc];
-    const int n = q.scene_off[sc + 1] - o;
+    // (the first scene's offsets were read at entry: no second dependent load)
+    const bool first_vs = vs == (int)blockIdx.x;
+    const int o = first_vs ? o0 : q.scene_off[sc];
+    const int n = first_vs ? n0 : q.scene_off[sc + 1] - o;
     if (n <= 0) continue;   // uniform over the workgroup
     PMARK(0);
     const bool first = pre && vs == (int)blockIdx.x;   // uniform

@@ -20,6 +20,7 @@
 // is H register FMAs + a 4-way LDS reduction.  Parameter gradients are sums
 // over (t, ped) of outer products -> the caller's GEMMs on the saved dG.
 #include <stdlib.h>
+#include <string.h>
 
 #include "sgg_common.h"
 
@@ -282,7 +283,11 @@ extern "C" const char* sgg_lstm_kernel_name(int H, int B, int decoder, int save,
     return buf;
   }
   if (save && mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_fwd_kernel<%d, %s, true>", H, tf[decoder != 0]);
-  else if (!save && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) snprintf(buf, sizeof buf, "sgg::lstm_fwd_mfma_kernel<%d>", H);
+  else if (!save && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) {
+    // (lstm_mfma.hip: the split-bf16 gate GEMM for H = 32 unless SGG_LSTM_X3=0)
+    const char* x3e = getenv("SGG_LSTM_X3");
+    snprintf(buf, sizeof buf, "sgg::lstm_fwd_mfma_kernel<%d, %s>", H, tf[H == 32 && !(x3e && strcmp(x3e, "0") == 0)]);
+  }
   else if (mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_fwd_kernel<%d, %s, %s>", H, tf[decoder != 0], tf[save != 0]);
   else if (H <= 32) snprintf(buf, sizeof buf, "sgg::lstm_unit_fwd_kernel<%d>", H);
   else snprintf(buf, sizeof buf, "sgg::lstm_fwd_kernel<%d>", H);
