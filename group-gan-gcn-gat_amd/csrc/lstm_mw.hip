@@ -587,9 +587,12 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   constexpr int MU = MwCfg<H>::MU, KS = MwCfg<H>::KS, G4 = MwCfg<H>::G4, HP = MwCfg<H>::HP;
   constexpr bool decoder = DEC, wgrad = WGRAD;
   constexpr bool BX3 = SGG_MW_BWD_X3 != 0;   // dh_{t-1} partials on split-bf16 MFMAs (below)
-  // encoder with weight gradients: the helper waves also take db, dA and
-  // drel_in (hsum above), so the owners' step is the recurrence alone
-  constexpr bool hacc = wgrad && !decoder;
+  // with weight gradients the helper waves also take the db and dA sums
+  // (hsum below), and for the encoder drel_in too, so the owners' step is the
+  // recurrence alone (the decoder's owners keep drel_in: their dWp / dbp
+  // accumulators read it the next step)
+  constexpr bool hacc = wgrad && !decoder;   // helpers: drel_in
+  constexpr bool hdb = wgrad;                 // helpers: db, dA
   // decoder slab rows carry [dWp (2 x H) | dbp (2)] after [dW_hh | db | dA]
   constexpr int NHS = MwCfg<H>::NHS, P0 = MwCfg<H>::P, P = P0 + (DEC ? 2 * H + 2 : 0);
   __shared__ float dgb[2][4][KS][kDgPitch];
@@ -651,20 +654,24 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     // every slot (lane-accumulated over the steps in the owners' former
     // order), and gate hg's partial of drel_in = A^T dG (reduced over the
     // lane quarters here, over the four gates by helper 4 one barrier later)
-    constexpr int KH = hacc ? KS : 1;
-    float ha0[KH], ha1[KH], hdb[KH], hdx[KH], hdy[KH];
+    constexpr int KH = hdb ? KS : 1, KA = hacc ? KS : 1;
+    float ha0[KA], ha1[KA], sdb[KH], sdx[KH], sdy[KH];
     float hr0 = 0.f, hr1 = 0.f, nr0 = 0.f, nr1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < KH; ++j) sdb[j] = sdx[j] = sdy[j] = 0.f;
     if (hacc) {
 #pragma unroll
       for (int j = 0; j < KS; ++j) {
         const int u = slot_unit(j, q);
         ha0[j] = A[2 * (hg * H + u)];
         ha1[j] = A[2 * (hg * H + u) + 1];
-        hdb[j] = hdx[j] = hdy[j] = 0.f;
       }
     }
+    // r_in(t) of the lane's ped: rel[t] (encoder); rel0, then rel_out[t - 1] (decoder)
     auto rel_load = [&](int t) {
-      const float2 rv = *reinterpret_cast<const float2*>(rel + ((size_t)t * B + pc) * 2);
+      const float* rp = !decoder ? rel + ((size_t)t * B + pc) * 2
+                                 : (t == 0 ? rel + (size_t)pc * 2 : rel_out + ((size_t)(t - 1) * B + pc) * 2);
+      const float2 rv = *reinterpret_cast<const float2*>(rp);
       nr0 = rv.x;
       nr1 = rv.y;
     };
@@ -673,17 +680,21 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
       for (int j = 0; j < KS; ++j) {
         const float v = dgb[buf][hg][j][lane];
-        hdb[j] += v;
-        hdx[j] = fmaf(v, hr0, hdx[j]);
-        hdy[j] = fmaf(v, hr1, hdy[j]);
-        f0 = fmaf(ha0[j], v, f0);
-        f1 = fmaf(ha1[j], v, f1);
+        sdb[j] += v;
+        sdx[j] = fmaf(v, hr0, sdx[j]);
+        sdy[j] = fmaf(v, hr1, sdy[j]);
+        if (hacc) {
+          f0 = fmaf(ha0[j], v, f0);
+          f1 = fmaf(ha1[j], v, f1);
+        }
       }
-      f0 += __shfl_xor(f0, 16);
-      f0 += __shfl_xor(f0, 32);
-      f1 += __shfl_xor(f1, 16);
-      f1 += __shfl_xor(f1, 32);
-      if (q == 0) fbp[buf][hg][c16] = make_float2(f0, f1);
+      if (hacc) {
+        f0 += __shfl_xor(f0, 16);
+        f0 += __shfl_xor(f0, 32);
+        f1 += __shfl_xor(f1, 16);
+        f1 += __shfl_xor(f1, 32);
+        if (q == 0) fbp[buf][hg][c16] = make_float2(f0, f1);
+      }
     };
     // drel_in[t] from the four gates' partials of step t (written before the barrier just passed)
     auto drel_store = [&](int t) {
@@ -713,20 +724,18 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     stage_load(T - 1);
     stage_store((T - 1) & 1);
     if (T >= 2) stage_load(T - 2);
-    if (hacc) rel_load(T - 1);
+    if (hdb) rel_load(T - 1);
     for (int t = T - 1; t >= 0; --t) {
       const int cur = t & 1;
-      if (hacc) {
+      if (hdb) {
         hr0 = nr0;
         hr1 = nr1;
         if (t > 0) rel_load(t - 1);
       }
       lds_barrier();   // (t)
       dw_accum(cur);
-      if (hacc) {
-        if (t < T - 1) drel_store(t + 1);
-        hsum(cur);
-      }
+      if (hacc && t < T - 1) drel_store(t + 1);
+      if (hdb) hsum(cur);
       if (t > 0) {
         stage_store(cur ^ 1);
         if (t > 1) stage_load(t - 2);
@@ -746,11 +755,11 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
         for (int nu = 0; nu < MU; ++nu) row[(size_t)gr * H + 16 * nu + c16] = dw[mu][nu][r];
       }
-    if (hacc) {   // db / dA of gate hg: sums over the 16 peds (lanes c16 of each q)
+    if (hdb) {   // db / dA of gate hg: sums over the 16 peds (lanes c16 of each q)
 #pragma unroll
       for (int j = 0; j < KS; ++j) {
         const int u = slot_unit(j, q);
-        float a = hdb[j], x = hdx[j], y = hdy[j];
+        float a = sdb[j], x = sdx[j], y = sdy[j];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
           a += __shfl_xor(a, o);
@@ -976,7 +985,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           dgb[cur][k][j][lane] = vv[k];
-          if (!hacc) {
+          if (!hdb) {
             db[i][k] += vv[k];
             dax[i][k] = fmaf(vv[k], r0, dax[i][k]);
             day[i][k] = fmaf(vv[k], r1, day[i][k]);
@@ -1024,11 +1033,12 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       dh0[(size_t)ped * H + slot_unit(j, q)] = (part[0][0][j][lane] + part[0][1][j][lane]) + (part[0][2][j][lane] + part[0][3][j][lane]);
     }
   }
-  if (wgrad && !hacc) {
+  if (wgrad) {
     float* row = wpart + (size_t)blk * P;
     // db / dA of the owned slots: sum over the 16 peds (lanes c16 of each q)
+    // (with the helpers' sums, hdb, nothing here)
 #pragma unroll
-    for (int i = 0; i < MU; ++i) {
+    for (int i = 0; i < (hdb ? 0 : MU); ++i) {
       const int u = slot_unit(g * MU + i, q);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
