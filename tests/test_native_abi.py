@@ -108,3 +108,19 @@ def test_pool_plan_covers_every_row_once():
                         assert (s, i) not in seen
                         seen[(s, i)] = 1
                 assert len(seen) == int(off[-1])
+
+
+def test_rccl_binding_symbols():
+    """The captured all-reduce's direct RCCL binding (sgan/rccl.py) resolves
+    its entry points in torch's own librccl.so (no GPU needed to load it)."""
+    import os
+    import torch
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    if not os.path.exists(path):
+        pytest.skip("torch without a bundled librccl.so")
+    from sgan import rccl
+    lib = rccl._rccl()
+    for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy", "ncclGetErrorString"):
+        assert hasattr(lib, f), f
+    assert rccl.NCCL_FLOAT32 == 7 and rccl.NCCL_SUM == 0
+    assert lib.ncclGetErrorString(0) is not None
