@@ -446,6 +446,47 @@ __device__ inline void rows_from_global(float* dst, int ld, const float* __restr
   }
 }
 
+// Several rows x cols global blocks (source row pitch sld, 0: dense) into LDS
+// images (pitch dld, 0: dense) with every block's loads of a round issued
+// before any of its stores: one memory round trip per round of PER x
+// blockDim elements of each block, where a rows_from_global per block waits
+// out one round trip per block (and per element of a thread)
+struct GSeg {
+  float* dst;
+  int dld;
+  const float* src;
+  int sld, rows, cols;
+};
+template <int NS, int PER>
+__device__ __forceinline__ void segs_from_global(const GSeg (&g)[NS]) {
+  int most = 0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) most = max(most, g[s].rows * g[s].cols);
+  for (int base = 0; base < most; base += PER * (int)blockDim.x) {
+    float v[NS][PER];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int m = 0; m < PER; ++m) {
+        const int e = base + (int)threadIdx.x + m * (int)blockDim.x;
+        if (e < g[s].rows * g[s].cols) {
+          const int r = e / g[s].cols, c = e - r * g[s].cols;
+          v[s][m] = g[s].src[(g[s].sld ? r * g[s].sld : r * g[s].cols) + c];
+        }
+      }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int m = 0; m < PER; ++m) {
+        const int e = base + (int)threadIdx.x + m * (int)blockDim.x;
+        if (e < g[s].rows * g[s].cols) {
+          const int r = e / g[s].cols, c = e - r * g[s].cols;
+          g[s].dst[(g[s].dld ? r * g[s].dld : r * g[s].cols) + c] = v[s][m];
+        }
+      }
+  }
+}
+
 __device__ __forceinline__ float lrelu(float x, float a) { return x > 0.f ? x : a * x; }
 
 // ---------------------------------------------------------------------------
@@ -875,32 +916,65 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       }
     }
     const bool preload = BWD && saved && L.WhIs > 0;   // uniform
-    if (BWD && saved) rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
+    if (BWD && saved && !preload) rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
     if (preload) {
       // the backward's whole input in ONE memory round trip: group structure,
       // activations, every layer's Wh / scores (n rows: the group-side rows
       // past M are never read), dy (+ its copies)
-      rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
-      rows_from_global(yI, P16, saved + SL.yI, n, FO);
-      rows_from_global(preI, P16, saved + SL.preI, n, FO);
-      rows_from_global(gin, P16, saved + SL.gin, n, FO);
-      rows_from_global(G1, PH, saved + SL.G1, n, FH * nh);
-      rows_from_global(preG, P16, saved + SL.preG, n, FO);
-      rows_from_global(gout, P16, saved + SL.gout, n, FO);
-      for (int h = 0; h < nh; ++h) {
-        rows_from_global(sm + L.WhIs + h * NP * P72, P72, saved + (SL.Whi[0] + h * SLH), n, FH);
-        rows_from_global(sm + L.stIs + h * 2 * NP, 0, saved + (SL.sti[0] + h * SLH), 1, 2 * NP);
-        rows_from_global(sm + L.WhGs + h * NP * P72, P72, saved + (SL.Whg[0] + h * SLH), n, FH);
-        rows_from_global(sm + L.stGs + h * 2 * NP, 0, saved + (SL.stg[0] + h * SLH), 1, 2 * NP);
+      constexpr int PDY = FE + 1;
+      const float* dyg = p.dy + (size_t)o * p.lddy;
+      const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
+      if constexpr (NH <= 2) {
+        GSeg g[12 + 4 * NH + 1];
+        int ns = 0;
+        g[ns++] = {lab, 0, saved + SL.ints, 0, 1, ints_floats(NP)};
+        g[ns++] = {H1, PH, saved + SL.H1, 0, n, FH * nh};
+        g[ns++] = {yI, P16, saved + SL.yI, 0, n, FO};
+        g[ns++] = {preI, P16, saved + SL.preI, 0, n, FO};
+        g[ns++] = {gin, P16, saved + SL.gin, 0, n, FO};
+        g[ns++] = {G1, PH, saved + SL.G1, 0, n, FH * nh};
+        g[ns++] = {preG, P16, saved + SL.preG, 0, n, FO};
+        g[ns++] = {gout, P16, saved + SL.gout, 0, n, FO};
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          g[ns++] = {sm + L.WhIs + h * NP * P72, P72, saved + (SL.Whi[0] + h * SLH), 0, n, FH};
+          g[ns++] = {sm + L.stIs + h * 2 * NP, 0, saved + (SL.sti[0] + h * SLH), 0, 1, 2 * NP};
+          g[ns++] = {sm + L.WhGs + h * NP * P72, P72, saved + (SL.Whg[0] + h * SLH), 0, n, FH};
+          g[ns++] = {sm + L.stGs + h * 2 * NP, 0, saved + (SL.stg[0] + h * SLH), 0, 1, 2 * NP};
+        }
+        g[ns++] = {sm + L.WhIOs, P16, saved + SL.Whio, 0, n, FO};
+        g[ns++] = {sm + L.stIOs, 0, saved + SL.stio, 0, 1, 2 * NP};
+        g[ns++] = {sm + L.WhGOs, P16, saved + SL.Whgo, 0, n, FO};
+        g[ns++] = {sm + L.stGOs, 0, saved + SL.stgo, 0, 1, 2 * NP};
+        // dy (a single copy: with the rest; else summed below)
+        g[ns++] = {Wh, PDY, dyg, p.lddy, ncp == 1 ? n : 0, FE};
+        segs_from_global<12 + 4 * NH + 1, 2>(g);
+      } else {   // (3 - 4 heads: one block at a time -- all in flight would spill)
+        rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
+        rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
+        rows_from_global(yI, P16, saved + SL.yI, n, FO);
+        rows_from_global(preI, P16, saved + SL.preI, n, FO);
+        rows_from_global(gin, P16, saved + SL.gin, n, FO);
+        rows_from_global(G1, PH, saved + SL.G1, n, FH * nh);
+        rows_from_global(preG, P16, saved + SL.preG, n, FO);
+        rows_from_global(gout, P16, saved + SL.gout, n, FO);
+        for (int h = 0; h < nh; ++h) {
+          rows_from_global(sm + L.WhIs + h * NP * P72, P72, saved + (SL.Whi[0] + h * SLH), n, FH);
+          rows_from_global(sm + L.stIs + h * 2 * NP, 0, saved + (SL.sti[0] + h * SLH), 1, 2 * NP);
+          rows_from_global(sm + L.WhGs + h * NP * P72, P72, saved + (SL.Whg[0] + h * SLH), n, FH);
+          rows_from_global(sm + L.stGs + h * 2 * NP, 0, saved + (SL.stg[0] + h * SLH), 1, 2 * NP);
+        }
+        rows_from_global(sm + L.WhIOs, P16, saved + SL.Whio, n, FO);
+        rows_from_global(sm + L.stIOs, 0, saved + SL.stio, 1, 2 * NP);
+        rows_from_global(sm + L.WhGOs, P16, saved + SL.Whgo, n, FO);
+        rows_from_global(sm + L.stGOs, 0, saved + SL.stgo, 1, 2 * NP);
+        if (ncp == 1)
+          for (int e = tid; e < n * FE; e += blockDim.x) {
+            const int i = e / FE, k = e - i * FE;
+            Wh[i * PDY + k] = dyg[(size_t)i * p.lddy + k];
+          }
       }
-      rows_from_global(sm + L.WhIOs, P16, saved + SL.Whio, n, FO);
-      rows_from_global(sm + L.stIOs, 0, saved + SL.stio, 1, 2 * NP);
-      rows_from_global(sm + L.WhGOs, P16, saved + SL.Whgo, n, FO);
-      rows_from_global(sm + L.stGOs, 0, saved + SL.stgo, 1, 2 * NP);
-      {
-        constexpr int PDY = FE + 1;
-        const float* dyg = p.dy + (size_t)o * p.lddy;
-        const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
+      if (ncp > 1) {
         for (int e = tid; e < n * FE; e += blockDim.x) {
           const int i = e / FE, k = e - i * FE;
           float v = dyg[(size_t)i * p.lddy + k];
