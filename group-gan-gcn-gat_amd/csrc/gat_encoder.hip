@@ -448,42 +448,42 @@ __device__ inline void rows_from_global(float* dst, int ld, const float* __restr
 
 // Several rows x cols global blocks (source row pitch sld, 0: dense) into LDS
 // images (pitch dld, 0: dense) with every block's loads of a round issued
-// before any of its stores: one memory round trip per round of PER x
-// blockDim elements of each block, where a rows_from_global per block waits
-// out one round trip per block (and per element of a thread)
+// before any of its stores: one memory round trip per round of 2 x blockDim
+// elements of each block, where a rows_from_global per block waits out one
+// round trip per block (and per element of a thread).  Element pairs: every
+// block's cols, row pitch and source offset are even (8-byte loads; a pair
+// never crosses a row), so a round is one 8-byte load per thread and block.
+// The loads are clamped, not guarded (a guard's branches break the batch up
+// with waits); lanes past a block reload its last pair and do not store.
 struct GSeg {
   float* dst;
   int dld;
   const float* src;
   int sld, rows, cols;
 };
-template <int NS, int PER>
+template <int NS>
 __device__ __forceinline__ void segs_from_global(const GSeg (&g)[NS]) {
   int most = 0;
 #pragma unroll
   for (int s = 0; s < NS; ++s) most = max(most, g[s].rows * g[s].cols);
-  for (int base = 0; base < most; base += PER * (int)blockDim.x) {
-    float v[NS][PER];
+  for (int base = 0; base < most; base += 2 * (int)blockDim.x) {
+    float2 v[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
+    for (int s = 0; s < NS; ++s) {
+      const int e = max(min(base + 2 * (int)threadIdx.x, g[s].rows * g[s].cols - 2), 0);
+      const int r = e / g[s].cols, c = e - r * g[s].cols;
+      v[s] = *reinterpret_cast<const float2*>(g[s].src + (g[s].sld ? r * g[s].sld : r * g[s].cols) + c);
+    }
 #pragma unroll
-      for (int m = 0; m < PER; ++m) {
-        const int e = base + (int)threadIdx.x + m * (int)blockDim.x;
-        if (e < g[s].rows * g[s].cols) {
-          const int r = e / g[s].cols, c = e - r * g[s].cols;
-          v[s][m] = g[s].src[(g[s].sld ? r * g[s].sld : r * g[s].cols) + c];
-        }
+    for (int s = 0; s < NS; ++s) {
+      const int e = base + 2 * (int)threadIdx.x;
+      if (e < g[s].rows * g[s].cols) {
+        const int r = e / g[s].cols, c = e - r * g[s].cols;
+        float* d = g[s].dst + (g[s].dld ? r * g[s].dld : r * g[s].cols) + c;
+        d[0] = v[s].x;
+        d[1] = v[s].y;
       }
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-      for (int m = 0; m < PER; ++m) {
-        const int e = base + (int)threadIdx.x + m * (int)blockDim.x;
-        if (e < g[s].rows * g[s].cols) {
-          const int r = e / g[s].cols, c = e - r * g[s].cols;
-          g[s].dst[(g[s].dld ? r * g[s].dld : r * g[s].cols) + c] = v[s][m];
-        }
-      }
+    }
   }
 }
 
@@ -742,6 +742,10 @@ __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, 
   }
 }
 
+#ifdef SGG_GATENC_PROF
+__device__ long long g_gatenc_prof[2][64];   // phase timestamps (tools/gatenc_probe.hip)
+#endif
+
 // attention layer backward, s / t / Wh in LDS.  dpre: gradient of the
 // aggregate (rows x F).  Writes dWh (rows x F) and starts the a-gradient
 // (2F, to da) in the last phase WITHOUT a closing barrier: the caller adds
@@ -749,15 +753,21 @@ __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, 
 // rows x npp.
 __device__ __forceinline__ void att_bwd(const float* Wh, int ldw, int rows, int F, const int* gidl, const float* s, const float* t,
                         float alpha, const float* a, const float* dpre, int ldd, float* dWh, int lddw, float* ds,
-                        float* dt, float* attm, float* dz, int npp, float* da) {
+                        float* dt, float* attm, float* dz, int npp, float* da, int mk = 0) {
+#ifdef SGG_GATENC_PROF
+#define AMARK(i) \
+  if (mk && threadIdx.x == 0 && blockIdx.x == 0) g_gatenc_prof[1][mk + (i)] = wall_clock64();
+#else
+#define AMARK(i)
+#endif
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   att_rows(rows, 0, nullptr, nullptr, 0, gidl, alpha, const_cast<float*>(s), const_cast<float*>(t), attm, npp,
            nullptr);
-  lds_barrier();
+  lds_barrier(); AMARK(0);
   // dWh = att^T dpre; datt = dpre Wh^T (to dz)
   wgrad(attm, npp, rows, rows, dpre, ldd, F, dWh, lddw, 0);
   lin_t(dpre, ldd, rows, F, Wh, ldw, rows, dz, npp, false, 8);
-  lds_barrier();
+  lds_barrier(); AMARK(1);
   // softmax + LeakyReLU backward, row i: dz_ij = lrelu'(.) att_ij (datt_ij - sum_k att_ik datt_ik)
   for (int i = threadIdx.x >> 6; i < rows; i += nw) {
     const bool ok = lane < rows;
@@ -769,7 +779,7 @@ __device__ __forceinline__ void att_bwd(const float* Wh, int ldw, int rows, int 
     const float dsum = wsum(z);
     if (lane == 0) ds[i] = dsum;
   }
-  lds_barrier();
+  lds_barrier(); AMARK(2);
   // column j: dt_j = sum_i dz_ij; dWh_j += ds_j a[:F] + dt_j a[F:]
   for (int j = threadIdx.x >> 6; j < rows; j += nw) {
     const float dtj = wsum(lane < rows ? dz[lane * npp + j] : 0.f);
@@ -777,7 +787,7 @@ __device__ __forceinline__ void att_bwd(const float* Wh, int ldw, int rows, int 
     const float dsj = ds[j];
     for (int f = lane; f < F; f += 64) dWh[j * lddw + f] += dsj * a[f] + dtj * a[F + f];
   }
-  lds_barrier();
+  lds_barrier(); AMARK(3);
   // da[f] = sum_i ds_i Wh_i[f], da[F + f] = sum_j dt_j Wh_j[f]
   for (int e = threadIdx.x; e < 2 * F; e += blockDim.x) {
     const int w = e / F, f = e - w * F;
@@ -786,11 +796,12 @@ __device__ __forceinline__ void att_bwd(const float* Wh, int ldw, int rows, int 
     for (int r = 0; r < rows; ++r) acc = fmaf(g[r], Wh[r * ldw + f], acc);
     da[e] = acc;
   }
+  AMARK(4);
+#undef AMARK
 }
 
 // phase timestamps of workgroup 0's first scene (tools/gatenc_probe.hip)
 #ifdef SGG_GATENC_PROF
-__device__ long long g_gatenc_prof[2][64];
 #define PMARK(i) \
   if (threadIdx.x == 0 && blockIdx.x == 0) g_gatenc_prof[BWD][i] = wall_clock64();
 #else
@@ -915,6 +926,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         X[r * P40 + (e - r * FI)] = xval(q, o, e);
       }
     }
+    PMARK(37);
     const bool preload = BWD && saved && L.WhIs > 0;   // uniform
     if (BWD && saved && !preload) rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
     if (preload) {
@@ -924,6 +936,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       constexpr int PDY = FE + 1;
       const float* dyg = p.dy + (size_t)o * p.lddy;
       const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
+      const bool dy_pairs = NH <= 2 && ncp == 1 && (p.lddy & 1) == 0 && (reinterpret_cast<size_t>(p.dy) & 7) == 0;
       if constexpr (NH <= 2) {
         GSeg g[12 + 4 * NH + 1];
         int ns = 0;
@@ -946,9 +959,10 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         g[ns++] = {sm + L.stIOs, 0, saved + SL.stio, 0, 1, 2 * NP};
         g[ns++] = {sm + L.WhGOs, P16, saved + SL.Whgo, 0, n, FO};
         g[ns++] = {sm + L.stGOs, 0, saved + SL.stgo, 0, 1, 2 * NP};
-        // dy (a single copy: with the rest; else summed below)
-        g[ns++] = {Wh, PDY, dyg, p.lddy, ncp == 1 ? n : 0, FE};
-        segs_from_global<12 + 4 * NH + 1, 2>(g);
+        // dy (a single copy at an 8-byte aligned pitch: with the rest; else below)
+        g[ns++] = {Wh, PDY, dy_pairs ? dyg : saved, p.lddy, dy_pairs ? n : 0, FE};
+        segs_from_global<12 + 4 * NH + 1>(g);
+        PMARK(38);
       } else {   // (3 - 4 heads: one block at a time -- all in flight would spill)
         rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
         rows_from_global(H1, PH, saved + SL.H1, n, FH * nh);
@@ -968,13 +982,8 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         rows_from_global(sm + L.stIOs, 0, saved + SL.stio, 1, 2 * NP);
         rows_from_global(sm + L.WhGOs, P16, saved + SL.Whgo, n, FO);
         rows_from_global(sm + L.stGOs, 0, saved + SL.stgo, 1, 2 * NP);
-        if (ncp == 1)
-          for (int e = tid; e < n * FE; e += blockDim.x) {
-            const int i = e / FE, k = e - i * FE;
-            Wh[i * PDY + k] = dyg[(size_t)i * p.lddy + k];
-          }
       }
-      if (ncp > 1) {
+      if (!dy_pairs) {
         for (int e = tid; e < n * FE; e += blockDim.x) {
           const int i = e / FE, k = e - i * FE;
           float v = dyg[(size_t)i * p.lddy + k];
@@ -1328,11 +1337,14 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       }
       lds_barrier(); PMARK(27);
       att_bwd(WhH, P72, n, FH, gidl, sH, tH, p.alpha, (lw.ai[0] + h * SEGI), dH + h * FH, PH, dWh, P72, ds, dt, attm, dz, NPP,
-              slab + (PL.ai[0] + h * PLI));
+              slab + (PL.ai[0] + h * PLI), BWD ? 30 : 0);
       wgrad(X, P40, n, FI, dWh, P72, FH, slab + (PL.Wi[0] + h * PLI), FH, 0);
+      PMARK(35);
       // dX (global) accumulates over heads in a fixed order
       lin_t(dWh, P72, n, FH, (lw.Wi[0] + h * SEGI), PW72, FI, dXo, p.lddx, h > 0, 8, dX2o, p.lddx2, p.kx1);
-      __syncthreads();   // dX read-modify-write by the next head: global ordering PMARK(28);
+      PMARK(36);
+      __syncthreads();   // dX read-modify-write by the next head: global ordering
+      PMARK(28);
     }
   }
 }

@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
     long long prev = pr[bwd][0];
     if (!bwd && pr[0][53] > pr[0][52])
       printf("  shader clock %.2f GHz (F1..F7)\n", (double)(pr[0][51] - pr[0][50]) / ((pr[0][53] - pr[0][52]) * 10.0));
-    for (int i = 1; i < 31; ++i) {
+    for (int i = 1; i < 40; ++i) {
       if (pr[bwd][i] <= 0 || pr[bwd][i] < t0) continue;
       printf("  mark %2d  %7.2f  (+%.2f)\n", i, (pr[bwd][i] - t0) * 0.01, (pr[bwd][i] - prev) * 0.01);
       prev = pr[bwd][i];
