@@ -50,7 +50,7 @@ constexpr int P40 = FI + 1, P72 = FH + 1, P16 = FO + 1;
 // LDS image of the weights: W (K x N) rows at pitch N + 1 (odd: a column walk
 // across rows, lane = row, is bank-conflict free; a row walk is contiguous)
 constexpr int PW72 = FH + 1, PW16 = FO + 1, PWE = 2 * FO + 1;
-__host__ __device__ inline int weights_floats(int nh) {
+__host__ __device__ constexpr int weights_floats(int nh) {
   return nh * (FI * PW72 + 2 * FH) + (FH * nh * PW16 + 2 * FO) + nh * (FO * PW72 + 2 * FH) + (FH * nh * PW16 + 2 * FO) +
          FE * PWE + FE;
 }
@@ -183,9 +183,9 @@ __host__ __device__ constexpr int live_slot(int q) {
          : q < 4 * NH + 2 ? 2 * kGatEncMaxHeads + 2 + (q - 2 * NH - 2)
                           : 4 * kGatEncMaxHeads + 2 + (q - 4 * NH - 2);
 }
+// the weight matrices' / vectors' places in an LDS image at base
 template <int NH>
-__device__ inline void stage_weights_t(float* base, const StageTab& T, LW& lw) {
-  constexpr int NL = 4 * NH + 6;
+__device__ __forceinline__ void set_lw(float* base, const StageTab& T, LW& lw) {
 #pragma unroll
   for (int h = 0; h < NH; ++h) {
     lw.Wi[h] = base + T.dst[2 * h];
@@ -199,6 +199,12 @@ __device__ inline void stage_weights_t(float* base, const StageTab& T, LW& lw) {
   lw.ago = base + T.dst[4 * kGatEncMaxHeads + 3];
   lw.Woe = base + T.dst[4 * kGatEncMaxHeads + 4];
   lw.boe = base + T.dst[4 * kGatEncMaxHeads + 5];
+}
+
+template <int NH>
+__device__ inline void stage_weights_t(float* base, const StageTab& T, LW& lw) {
+  constexpr int NL = 4 * NH + 6;
+  set_lw<NH>(base, T, lw);
   for (int c = threadIdx.x; c < T.nchunks; c += blockDim.x) {
     int q = 0;
 #pragma unroll
@@ -461,29 +467,47 @@ struct GSeg {
   const float* src;
   int sld, rows, cols;
 };
+// (cols are compile-time constants at every call: the lane's row / column
+// per distinct width is one multiply-shift, shared by the blocks of that
+// width; a lane past a block clamps its row, and a block of 0 rows reads
+// its source's first pair)
 template <int NS>
-__device__ __forceinline__ void segs_from_global(const GSeg (&g)[NS]) {
+__device__ __forceinline__ void segs_load(const GSeg (&g)[NS], float2 (&v)[NS], int base) {
+  const int e = base + 2 * (int)threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int r0 = e / g[s].cols, c = e - r0 * g[s].cols;
+    const int r = max(min(r0, g[s].rows - 1), 0);
+    v[s] = *reinterpret_cast<const float2*>(g[s].src + (g[s].sld ? r * g[s].sld : r * g[s].cols) + c);
+  }
+}
+template <int NS>
+__device__ __forceinline__ void segs_store(const GSeg (&g)[NS], const float2 (&v)[NS], int base) {
+  const int e = base + 2 * (int)threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int r = e / g[s].cols, c = e - r * g[s].cols;
+    if (r < g[s].rows) {
+      float* d = g[s].dst + (g[s].dld ? r * g[s].dld : r * g[s].cols) + c;
+      d[0] = v[s].x;
+      d[1] = v[s].y;
+    }
+  }
+}
+template <int NS>
+__device__ __forceinline__ int segs_most(const GSeg (&g)[NS]) {
   int most = 0;
 #pragma unroll
   for (int s = 0; s < NS; ++s) most = max(most, g[s].rows * g[s].cols);
+  return most;
+}
+template <int NS>
+__device__ __forceinline__ void segs_from_global(const GSeg (&g)[NS]) {
+  const int most = segs_most(g);
   for (int base = 0; base < most; base += 2 * (int)blockDim.x) {
     float2 v[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int e = max(min(base + 2 * (int)threadIdx.x, g[s].rows * g[s].cols - 2), 0);
-      const int r = e / g[s].cols, c = e - r * g[s].cols;
-      v[s] = *reinterpret_cast<const float2*>(g[s].src + (g[s].sld ? r * g[s].sld : r * g[s].cols) + c);
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int e = base + 2 * (int)threadIdx.x;
-      if (e < g[s].rows * g[s].cols) {
-        const int r = e / g[s].cols, c = e - r * g[s].cols;
-        float* d = g[s].dst + (g[s].dld ? r * g[s].dld : r * g[s].cols) + c;
-        d[0] = v[s].x;
-        d[1] = v[s].y;
-      }
-    }
+    segs_load(g, v, base);
+    segs_store(g, v, base);
   }
 }
 
@@ -746,6 +770,42 @@ __device__ void epi_bwd(float* d, int ldd, const float* pre, int ldp, int rows, 
 __device__ long long g_gatenc_prof[2][64];   // phase timestamps (tools/gatenc_probe.hip)
 #endif
 
+// The backward's preloaded blocks of one scene (the full plan with every
+// layer's state resident; 1 - 2 heads): group structure, activations, every
+// layer's Wh / scores, and dy when it is one copy at an 8-byte aligned pitch
+// (dy_pairs; else its block is empty and the caller sums the copies)
+template <int NH>
+__device__ __forceinline__ void preload_segs(GSeg (&g)[12 + 4 * NH + 1], float* sm, const Layout& L,
+                                             const SLayout& SL, const float* saved, const float* dyg, int lddy, int n,
+                                             bool dy_pairs) {
+  const int NP = L.NP, PH = L.PH, SLH = NP * FH + 2 * NP;
+  int ns = 0;
+  g[ns++] = {sm + L.ints, 0, saved + SL.ints, 0, ints_floats(NP) / 2, 2};
+  g[ns++] = {sm + L.H1, PH, saved + SL.H1, 0, n, FH * NH};
+  g[ns++] = {sm + L.yI, P16, saved + SL.yI, 0, n, FO};
+  g[ns++] = {sm + L.preI, P16, saved + SL.preI, 0, n, FO};
+  g[ns++] = {sm + L.gin, P16, saved + SL.gin, 0, n, FO};
+  g[ns++] = {sm + L.G1, PH, saved + SL.G1, 0, n, FH * NH};
+  g[ns++] = {sm + L.preG, P16, saved + SL.preG, 0, n, FO};
+  g[ns++] = {sm + L.gout, P16, saved + SL.gout, 0, n, FO};
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    g[ns++] = {sm + L.WhIs + h * NP * P72, P72, saved + (SL.Whi[0] + h * SLH), 0, n, FH};
+    g[ns++] = {sm + L.stIs + h * 2 * NP, 0, saved + (SL.sti[0] + h * SLH), 0, NP, 2};
+    g[ns++] = {sm + L.WhGs + h * NP * P72, P72, saved + (SL.Whg[0] + h * SLH), 0, n, FH};
+    g[ns++] = {sm + L.stGs + h * 2 * NP, 0, saved + (SL.stg[0] + h * SLH), 0, NP, 2};
+  }
+  g[ns++] = {sm + L.WhIOs, P16, saved + SL.Whio, 0, n, FO};
+  g[ns++] = {sm + L.stIOs, 0, saved + SL.stio, 0, NP, 2};
+  g[ns++] = {sm + L.WhGOs, P16, saved + SL.Whgo, 0, n, FO};
+  g[ns++] = {sm + L.stGOs, 0, saved + SL.stgo, 0, NP, 2};
+  g[ns++] = {sm + L.Wh, FE + 1, dy_pairs ? dyg : saved, lddy, dy_pairs ? n : 0, FE};
+}
+
+__device__ __forceinline__ bool dy_pairs_ok(const GatEncArgs& p) {
+  return p.dy_copies <= 1 && (p.lddy & 1) == 0 && (reinterpret_cast<size_t>(p.dy) & 7) == 0;
+}
+
 // attention layer backward, s / t / Wh in LDS.  dpre: gradient of the
 // aggregate (rows x F).  Writes dWh (rows x F) and starts the a-gradient
 // (2F, to da) in the last phase WITHOUT a closing barrier: the caller adds
@@ -804,8 +864,11 @@ __device__ __forceinline__ void att_bwd(const float* Wh, int ldw, int rows, int 
 #ifdef SGG_GATENC_PROF
 #define PMARK(i) \
   if (threadIdx.x == 0 && blockIdx.x == 0) g_gatenc_prof[BWD][i] = wall_clock64();
+#define PMARKW(i) \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_gatenc_prof[BWD][(i) + (threadIdx.x >> 6)] = wall_clock64();
 #else
 #define PMARK(i)
+#define PMARKW(i)
 #endif
 
 // the scene set of virtual scene vs: p's scenes first, then s2's (a
@@ -860,8 +923,45 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     if (tid < n0) lp = q0.labels[o0 + tid];
   }
   PMARK(40);
+  PMARKW(42);
+  // the first scene's backward preload (1 - 2 heads, when one round covers
+  // it): its loads go out with the weight staging's, its stores follow them
+  constexpr int NSEG = 12 + 4 * NH + 1;
+  bool pre0 = false;
+  GSeg g0[NSEG];
+  float2 v0[NSEG];
+  if constexpr (BWD && NH <= 2) {
+    const Layout L0 = make_layout(p.np, NH, BWD);
+    pre0 = p.saved && !L0.compact && L0.WhIs > 0 && n0 > 0 && n0 * FH * NH <= 2 * (int)blockDim.x;   // uniform
+    if (pre0) {
+      const SLayout SL0 = make_slayout(p.np, NH);
+      preload_segs<NH>(g0, sm, L0, SL0, p.saved + (size_t)sc0 * SL0.total, p.dy + (size_t)o0 * p.lddy, p.lddy, n0,
+                       dy_pairs_ok(p));
+      segs_load(g0, v0, 0);
+    }
+  }
+  // The weights' LDS image.  The backward with the forward's saved state
+  // copies the image that forward's workgroup 0 left after the saved blocks
+  // (contiguous, 16-byte loads, no per-element placement); otherwise each
+  // workgroup stages it from the parameters (stage_weights_t)
   LW lw;
-  stage_weights_t<NH>(sm + make_layout(p.np, NH, BWD).wts, tab, lw);
+  float* const wbase = sm + make_layout(p.np, NH, BWD).wts;
+  constexpr int WF4 = (weights_floats(NH) + 3) / 4, WQ = (WF4 + kBwdThreads - 1) / kBwdThreads;
+  const bool wimg = BWD && p.saved != nullptr;   // uniform
+  if (wimg) {
+    set_lw<NH>(wbase, tab, lw);
+    const floatx4* img = reinterpret_cast<const floatx4*>(p.saved + (size_t)p.S * make_slayout(p.np, NH).total);
+    floatx4 wv[WQ];
+#pragma unroll
+    for (int m = 0; m < WQ; ++m) wv[m] = img[min(tid + m * (int)blockDim.x, WF4 - 1)];
+#pragma unroll
+    for (int m = 0; m < WQ; ++m)
+      if (tid + m * (int)blockDim.x < WF4) reinterpret_cast<floatx4*>(wbase)[tid + m * (int)blockDim.x] = wv[m];
+  } else {
+    stage_weights_t<NH>(wbase, tab, lw);
+  }
+  if constexpr (BWD && NH <= 2)
+    if (pre0) segs_store(g0, v0, 0);
   // (the first scene's input stores are followed by a barrier before any use)
   PMARK(41);
 
@@ -936,32 +1036,13 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       constexpr int PDY = FE + 1;
       const float* dyg = p.dy + (size_t)o * p.lddy;
       const int ncp = p.dy_copies > 1 ? p.dy_copies : 1;
-      const bool dy_pairs = NH <= 2 && ncp == 1 && (p.lddy & 1) == 0 && (reinterpret_cast<size_t>(p.dy) & 7) == 0;
+      const bool dy_pairs = NH <= 2 && dy_pairs_ok(p);
       if constexpr (NH <= 2) {
-        GSeg g[12 + 4 * NH + 1];
-        int ns = 0;
-        g[ns++] = {lab, 0, saved + SL.ints, 0, 1, ints_floats(NP)};
-        g[ns++] = {H1, PH, saved + SL.H1, 0, n, FH * nh};
-        g[ns++] = {yI, P16, saved + SL.yI, 0, n, FO};
-        g[ns++] = {preI, P16, saved + SL.preI, 0, n, FO};
-        g[ns++] = {gin, P16, saved + SL.gin, 0, n, FO};
-        g[ns++] = {G1, PH, saved + SL.G1, 0, n, FH * nh};
-        g[ns++] = {preG, P16, saved + SL.preG, 0, n, FO};
-        g[ns++] = {gout, P16, saved + SL.gout, 0, n, FO};
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-          g[ns++] = {sm + L.WhIs + h * NP * P72, P72, saved + (SL.Whi[0] + h * SLH), 0, n, FH};
-          g[ns++] = {sm + L.stIs + h * 2 * NP, 0, saved + (SL.sti[0] + h * SLH), 0, 1, 2 * NP};
-          g[ns++] = {sm + L.WhGs + h * NP * P72, P72, saved + (SL.Whg[0] + h * SLH), 0, n, FH};
-          g[ns++] = {sm + L.stGs + h * 2 * NP, 0, saved + (SL.stg[0] + h * SLH), 0, 1, 2 * NP};
+        if (!(pre0 && first_vs)) {   // (the first scene's came with the weights)
+          GSeg g[NSEG];
+          preload_segs<NH>(g, sm, L, SL, saved, dyg, p.lddy, n, dy_pairs);
+          segs_from_global(g);
         }
-        g[ns++] = {sm + L.WhIOs, P16, saved + SL.Whio, 0, n, FO};
-        g[ns++] = {sm + L.stIOs, 0, saved + SL.stio, 0, 1, 2 * NP};
-        g[ns++] = {sm + L.WhGOs, P16, saved + SL.Whgo, 0, n, FO};
-        g[ns++] = {sm + L.stGOs, 0, saved + SL.stgo, 0, 1, 2 * NP};
-        // dy (a single copy at an 8-byte aligned pitch: with the rest; else below)
-        g[ns++] = {Wh, PDY, dy_pairs ? dyg : saved, p.lddy, dy_pairs ? n : 0, FE};
-        segs_from_global<12 + 4 * NH + 1>(g);
         PMARK(38);
       } else {   // (3 - 4 heads: one block at a time -- all in flight would spill)
         rows_from_global(lab, 0, saved + SL.ints, 1, ints_floats(NP));
@@ -1347,6 +1428,21 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       PMARK(28);
     }
   }
+  if constexpr (!BWD) {
+    // workgroup 0: the staged weight image after the saved blocks of each
+    // batch that keeps its state (the backward copies it contiguously)
+    if (blockIdx.x == 0) {
+      const SLayout SLw = make_slayout(p.np, NH);
+      const floatx4* im = reinterpret_cast<const floatx4*>(wbase);
+      floatx4* d1 = p.saved ? reinterpret_cast<floatx4*>(p.saved + (size_t)p.S * SLw.total) : nullptr;
+      floatx4* d2 = s2.saved ? reinterpret_cast<floatx4*>(s2.saved + (size_t)s2.S * SLw.total) : nullptr;
+      for (int e = tid; e < WF4; e += blockDim.x) {
+        const floatx4 v = im[e];
+        if (d1) d1[e] = v;
+        if (d2) d2[e] = v;
+      }
+    }
+  }
 }
 
 // out[c] = sum_s slab[s][c] in a fixed order (deterministic): block = 64
@@ -1393,7 +1489,8 @@ extern "C" int sgg_gatenc_param_size(int nh) {
 
 extern "C" long long sgg_gatenc_saved_floats(int S, int max_n, int nh) {
   if (S < 0 || max_n < 1 || nh < 1 || nh > kGatEncMaxHeads) return -1;
-  return (long long)S * make_slayout(max_n, nh).total;
+  // S per-scene blocks, then the weights' LDS image (gatenc_kernel)
+  return (long long)S * make_slayout(max_n, nh).total + 4ll * ((weights_floats(nh) + 3) / 4);
 }
 
 extern "C" long long sgg_gatenc_lds_bytes(int max_n, int nh, int bwd) {

@@ -812,7 +812,8 @@ typedef struct {
   float* dX;
   int lddx;
   float* slab;
-  float* saved;   /* may be NULL: S x sgg_gatenc_saved_floats(1, np, nh) floats of forward state */
+  float* saved;   /* may be NULL: sgg_gatenc_saved_floats(S, np, nh) floats of forward state
+                     (S per-scene blocks, then the staged weights the backward copies) */
   /* optional second input block: when X2 != NULL a row of the 40-wide input
    * is [X[r][0 .. kx1) | X2[r][0 .. 40 - kx1)] (the encoder state and the
    * pooled vector without a concatenation copy), and the backward writes the

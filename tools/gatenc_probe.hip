@@ -102,6 +102,11 @@ int main(int argc, char** argv) {
       printf("  mark %2d  %7.2f  (+%.2f)\n", i, (pr[bwd][i] - t0) * 0.01, (pr[bwd][i] - prev) * 0.01);
       prev = pr[bwd][i];
     }
+    if (bwd && pr[1][42] > 0) {   // per-wave arrival after the backward's preload (marks 42 .. 57)
+      printf("  per-wave entry (us from wave 0 entry):");
+      for (int w = 0; w < 16; ++w) printf(" %.2f", (pr[1][42 + w] - t0) * 0.01);
+      printf("\n");
+    }
     CK(hipMemset(pr, 0, 0));
     long long z[2][64] = {};
     CK(hipMemcpyToSymbol(HIP_SYMBOL(sgg::g_gatenc_prof), z, sizeof z));
