@@ -802,6 +802,59 @@ __device__ __forceinline__ void preload_segs(GSeg (&g)[12 + 4 * NH + 1], float* 
   g[ns++] = {sm + L.Wh, FE + 1, dy_pairs ? dyg : saved, lddy, dy_pairs ? n : 0, FE};
 }
 
+// stage_weights_t with the image's blocks at compile-time shapes (1 - 2
+// heads; every parameter 8-byte aligned): one batch of pair loads, then the
+// stores at the matrices' pitches -- a few VALU operations per pair instead of
+// the per-chunk segment search and row walk (the 16 waves of a workgroup share
+// 4 SIMDs, so the staging's VALU count is its time)
+template <int NH>
+__device__ __forceinline__ bool stage_fast_ok(const StageTab& T) {
+  size_t a = 0;
+#pragma unroll
+  for (int k = 0; k < 4 * NH + 6; ++k) a |= reinterpret_cast<size_t>(T.src[live_slot<NH>(k)]);
+  return NH <= 2 && (a & 7) == 0;
+}
+template <int NH>
+__device__ __forceinline__ void stage_weights_fast(float* base, const StageTab& T, LW& lw) {
+  set_lw<NH>(base, T, lw);
+  constexpr int NS = 5 * NH + 6 + (NH > 1 ? 2 : 0);
+  constexpr int HI = FI / 2;   // Wi in two row halves (<= 2 x 1024 floats each)
+  constexpr int RO = NH > 1 ? FH : FH * NH;   // Wio / Wgo row blocks
+  GSeg g[NS];
+  int ns = 0;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int si = live_slot<NH>(2 * h), sa = live_slot<NH>(2 * h + 1);
+    g[ns++] = {base + T.dst[si], PW72, T.src[si], 0, HI, FH};
+    g[ns++] = {base + T.dst[si] + HI * PW72, PW72, T.src[si] + HI * FH, 0, HI, FH};
+    g[ns++] = {base + T.dst[sa], 0, T.src[sa], 0, FH, 2};
+  }
+  {
+    const int so = live_slot<NH>(2 * NH), sa = live_slot<NH>(2 * NH + 1);
+#pragma unroll
+    for (int b = 0; b < (NH > 1 ? 2 : 1); ++b)
+      g[ns++] = {base + T.dst[so] + b * RO * PW16, PW16, T.src[so] + b * RO * FO, 0, NH > 1 ? FH * NH / 2 : RO, FO};
+    g[ns++] = {base + T.dst[sa], 0, T.src[sa], 0, FO, 2};
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int sw = live_slot<NH>(2 * NH + 2 + 2 * h), sa = live_slot<NH>(2 * NH + 3 + 2 * h);
+    g[ns++] = {base + T.dst[sw], PW72, T.src[sw], 0, FO, FH};
+    g[ns++] = {base + T.dst[sa], 0, T.src[sa], 0, FH, 2};
+  }
+  {
+    const int so = live_slot<NH>(4 * NH + 2), sa = live_slot<NH>(4 * NH + 3);
+#pragma unroll
+    for (int b = 0; b < (NH > 1 ? 2 : 1); ++b)
+      g[ns++] = {base + T.dst[so] + b * RO * PW16, PW16, T.src[so] + b * RO * FO, 0, NH > 1 ? FH * NH / 2 : RO, FO};
+    g[ns++] = {base + T.dst[sa], 0, T.src[sa], 0, FO, 2};
+    const int se = live_slot<NH>(4 * NH + 4), sb = live_slot<NH>(4 * NH + 5);
+    g[ns++] = {base + T.dst[se], PWE, T.src[se], 0, FE, 2 * FO};
+    g[ns++] = {base + T.dst[sb], 0, T.src[sb], 0, FE / 2, 2};
+  }
+  segs_from_global(g);
+}
+
 __device__ __forceinline__ bool dy_pairs_ok(const GatEncArgs& p) {
   return p.dy_copies <= 1 && (p.lddy & 1) == 0 && (reinterpret_cast<size_t>(p.dy) & 7) == 0;
 }
@@ -958,7 +1011,14 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     for (int m = 0; m < WQ; ++m)
       if (tid + m * (int)blockDim.x < WF4) reinterpret_cast<floatx4*>(wbase)[tid + m * (int)blockDim.x] = wv[m];
   } else {
-    stage_weights_t<NH>(wbase, tab, lw);
+    // (the forward only: in the backward the dead branch costs the preload's
+    // schedule ~1 us, measured)
+    bool fast = false;
+    if constexpr (!BWD) fast = stage_fast_ok<NH>(tab);
+    if (fast)
+      stage_weights_fast<NH>(wbase, tab, lw);
+    else
+      stage_weights_t<NH>(wbase, tab, lw);
   }
   if constexpr (BWD && NH <= 2)
     if (pre0) segs_store(g0, v0, 0);
