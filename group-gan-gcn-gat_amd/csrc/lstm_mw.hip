@@ -150,6 +150,10 @@ __device__ long long g_lstm_prof[64];
 #define LMARK(i)
 #endif
 
+#ifndef SGG_MW_UPRE
+#define SGG_MW_UPRE 1   // the projection epilogue's Wu fragments fetched in the prologue (0: probe A/B only)
+#endif
+
 namespace {
 
 // DEC / SAVE are compile-time, so the step loop carries no per-store
@@ -291,37 +295,35 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   // the projection epilogue's Wu fragments (see below), fetched now so their
   // latency hides under the recurrence: all of this wave's <= 8 tiles in
   // registers (NU <= 512, H <= 48, 16-byte aligned rows)
-  constexpr bool kUPre = !DEC && H <= 48;
+  constexpr bool kUPre = SGG_MW_UPRE && !DEC && H <= 48;
   constexpr int kUT = 8;
   const float* __restrict__ Wu = sg.Wu;
   const int ldwu = sg.ldwu, NU = sg.NU;
   const bool upre = kUPre && sg.U && NU <= 16 * 4 * kUT &&
                     ((reinterpret_cast<uintptr_t>(Wu) | ((uintptr_t)ldwu * 4)) & 15) == 0;
+  // One tile per recurrence step (tile i at step i, the rest after the
+  // loop): all eight at once in the prologue were ~100 loads per wave behind
+  // the recurrence's operands (a wave tracks <= 63 outstanding), which held
+  // the first step back ~1.7 us (tools/lstm_mw_probe.hip, SGG_MW_UPRE A/B)
   float wu[kUPre ? kUT : 1][KS];
   float cuv[kUPre ? kUT : 1][4];
-  if (upre) {
+  auto load_wu = [&](int i) {   // (called with compile-time i only: wu stays in registers)
     const int ntile = NU >> 4;
+    const float4 v = *reinterpret_cast<const float4*>(sg.cu + 16 * min(g + 4 * i, ntile - 1) + 4 * q);
+    cuv[i][0] = v.x;
+    cuv[i][1] = v.y;
+    cuv[i][2] = v.z;
+    cuv[i][3] = v.w;
+    const float* wr = Wu + (size_t)(min(g + 4 * i, ntile - 1) * 16 + c16) * ldwu;
 #pragma unroll
-    for (int i = 0; i < kUT; ++i) {
-      const float4 v = *reinterpret_cast<const float4*>(sg.cu + 16 * min(g + 4 * i, ntile - 1) + 4 * q);
-      cuv[i][0] = v.x;
-      cuv[i][1] = v.y;
-      cuv[i][2] = v.z;
-      cuv[i][3] = v.w;
+    for (int m = 0; m < KS / 4; ++m) {
+      const float4 w4 = *reinterpret_cast<const float4*>(wr + 16 * m + 4 * q);
+      wu[i][4 * m] = w4.x;
+      wu[i][4 * m + 1] = w4.y;
+      wu[i][4 * m + 2] = w4.z;
+      wu[i][4 * m + 3] = w4.w;
     }
-#pragma unroll
-    for (int i = 0; i < kUT; ++i) {
-      const float* wr = Wu + (size_t)(min(g + 4 * i, ntile - 1) * 16 + c16) * ldwu;
-#pragma unroll
-      for (int m = 0; m < KS / 4; ++m) {
-        const float4 v = *reinterpret_cast<const float4*>(wr + 16 * m + 4 * q);
-        wu[i][4 * m] = v.x;
-        wu[i][4 * m + 1] = v.y;
-        wu[i][4 * m + 2] = v.z;
-        wu[i][4 * m + 3] = v.w;
-      }
-    }
-  }
+  };
 
   if (!decoder) {
 #pragma unroll
@@ -380,6 +382,11 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][ks], hk[ks], acc[mu], 0, 0, 0);
+    if (kUPre && upre) {
+#pragma unroll
+      for (int i = 0; i < kUT; ++i)
+        if (t == i) load_wu(i);
+    }
 
     // activations (r = 2: tanh, else sigmoid) and the cell update of this
     // wave's slots, in registers
@@ -442,6 +449,9 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   const float* __restrict__ cu = sg.cu;
   float* __restrict__ U = sg.U;
   if (kUPre && upre) {
+#pragma unroll
+    for (int i = 0; i < kUT; ++i)
+      if (i >= T) load_wu(i);   // (a recurrence shorter than the tile count)
     // U^T tiles g + 4 i from the prefetched fragments: eight independent
     // accumulation chains
     float hk[KS];
