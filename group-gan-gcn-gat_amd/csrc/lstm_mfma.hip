@@ -125,8 +125,14 @@ __device__ __forceinline__ void cell2(float2v yi, float2v yf, float2v yg, float2
 // MFMAs with no input k-step.  Step 0 adds A (rel_0 - Wp h_0 - bp) through
 // the input k-step.  The encoder (no feedback) keeps the input k-step
 // [r_x r_y 0 0] every step.
+// (H = 32: two waves per SIMD -- the allocator otherwise parks the accumulators
+// in 64 AGPRs on top of 227 VGPRs, 292 in all: one wave per SIMD, so the
+// rollout's 1,680 waves ran in two rounds)
+#ifndef SGG_ROLL_WPE
+#define SGG_ROLL_WPE 2
+#endif
 template <int H, bool X3>
-__global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 32 ? SGG_ROLL_WPE : 1))) lstm_fwd_mfma_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
     const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B1, int decoder,
@@ -205,9 +211,12 @@ __global__ void __launch_bounds__(256) lstm_fwd_mfma_kernel(
     w[mt][KW - 1] = q == 0 ? sc * ax : q == 1 ? sc * ay : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      // (A loaded unconditionally: under the runtime `decoder` branch each
+      // entry's load was followed by its own vmcnt(0) -- 4 MT round trips)
       const int brow = 16 * mt + 4 * q + r;
       const float bv = bias[brow];
-      b0[mt][r] = sc * (decoder ? fmaf(A[2 * brow + 1], bp1, fmaf(A[2 * brow], bp0, bv)) : bv);
+      const float bd = fmaf(A[2 * brow + 1], bp1, fmaf(A[2 * brow], bp0, bv));
+      b0[mt][r] = sc * (decoder ? bd : bv);
     }
   }
 
