@@ -65,14 +65,21 @@ class SceneIndex:
                 self.device, non_blocking=True)
         return self._ped_scene32
 
-    POOL_TARGET_CHUNKS = 512
+    POOL_TARGET_CHUNKS = int(__import__("os").environ.get("SGG_POOL_TARGET_CHUNKS", "512"))
+    # bottlenecks <= 16 (the generator's pooling): two pair groups per wave
+    # already at 256 chunks -- the fp32 fragment kernel then runs its grid in
+    # one round of three workgroups per CU (LDS-bound) instead of 1.2 rounds:
+    # 21.2 -> 18.3 us for the generator step's 2 x 64-scene pair (round 5,
+    # tools/gpu_pool_target.sh; bn 48 keeps 512, where 256 picks 4 groups and
+    # loses 2x)
+    POOL_TARGET_CHUNKS_SMALL = int(__import__("os").environ.get("SGG_POOL_TARGET_CHUNKS_SMALL", "256"))
     POOL_MAX_GPW = int(__import__("os").environ.get("SGG_POOL_MAX_GPW", "0"))
 
     def pool_plan(self, bn, target_chunks=None, bf16=False):
         """Device chunk table for sgg_pool_fwd (built on the host by
         sgg_pool_plan, cached per bottleneck width); bf16: the table of
         sgg_pool_fwd_bf16 (sgg_pool_plan_bf16: big chunks, one per CU)."""
-        target_chunks = target_chunks or self.POOL_TARGET_CHUNKS
+        target_chunks = target_chunks or (self.POOL_TARGET_CHUNKS_SMALL if bn <= 16 else self.POOL_TARGET_CHUNKS)
         plans = self.__dict__.setdefault("_pool_plans", {})
         key = (bn, target_chunks, self.POOL_MAX_GPW, bool(bf16))
         if key not in plans:
