@@ -344,22 +344,25 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
         t_cap = time.perf_counter() - t_cap
         frozen = K.gc_frozen()   # the captured graphs' state out of the collector's scans (scoped)
         frozen.__enter__()
-        t0 = time.perf_counter()
-        scenes = 0
-        marks = [t0]
-        steps_info = []
-        # HIP events between the iterations on the launch stream: each
-        # iteration's device-side span (host timings alone cannot tell a host
-        # stall from the host waiting on a device that is behind)
-        evs = [torch.cuda.Event(enable_timing=True)]
-        evs[0].record()
+        # (the instrumentation's own set-up -- the allocator statistics, the
+        # first scheduler sample -- comes before the clock starts: it was
+        # ~1.2 ms of the first timed iteration)
+        allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc")
         # host-side diagnostics per iteration: the thread's run-queue wait
         # (/proc/thread-self/schedstat: time runnable but not running) and the
         # cgroup's CPU-quota throttling (cpu.stat throttled_usec) -- a host
         # stall that is neither Python nor HIP shows up in one of them
         sched = [host_sched()]
         phases = []
-        allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc")
+        steps_info = []
+        # HIP events between the iterations on the launch stream: each
+        # iteration's device-side span (host timings alone cannot tell a host
+        # stall from the host waiting on a device that is behind)
+        evs = [torch.cuda.Event(enable_timing=True)]
+        t0 = time.perf_counter()
+        scenes = 0
+        marks = [t0]
+        evs[0].record()
         for _ in range(iters):
             if mode == "graphed":
                 tn = time.perf_counter()
