@@ -613,6 +613,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, c16 = lane & 15;
   const int blk = blockIdx.x;
+  LMARK(0);
   const int ped = blk * kMwPeds + c16;
   const bool valid = ped < B;
   const int pc = valid ? ped : B - 1;
@@ -901,7 +902,9 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   // t_stop > 0 (input gradients only, no dh0): the steps below t_stop are
   // skipped -- their input gradients are not wanted (the discriminator's
   // observed part in the generator step)
+  LMARK(1);
   for (int t = T - 1; t >= t_stop; --t) {
+    if (T - 1 - t < 60) LMARK(2 + T - 1 - t);
     const int cur = t & 1;
     const float d0 = nd0, d1 = nd1, r0 = nr0, r1 = nr1;
     float ci[MU], cf[MU], cg[MU], co[MU], cc[MU], ccp[MU];
@@ -1095,6 +1098,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       }
     }
   }
+  LMARK(62);
 }
 
 template <int H>
