@@ -125,9 +125,9 @@ __device__ __forceinline__ void cell2(float2v yi, float2v yf, float2v yg, float2
 // MFMAs with no input k-step.  Step 0 adds A (rel_0 - Wp h_0 - bp) through
 // the input k-step.  The encoder (no feedback) keeps the input k-step
 // [r_x r_y 0 0] every step.
-// (H = 32: two waves per SIMD -- the allocator otherwise parks the accumulators
-// in 64 AGPRs on top of 227 VGPRs, 292 in all: one wave per SIMD, so the
-// rollout's 1,680 waves ran in two rounds)
+// (H = 32: two waves per SIMD, pinned -- the build's -amdgpu-mfma-vgpr-form
+// keeps the accumulators in VGPRs (227); without that flag the allocator
+// parks them in 64 AGPRs, 292 registers in all, one wave per SIMD)
 #ifndef SGG_ROLL_WPE
 #define SGG_ROLL_WPE 2
 #endif
