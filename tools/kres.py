@@ -12,7 +12,12 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-munsafe-fp-ato
 def main():
     src = sys.argv[1]
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
-    r = subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + [src], capture_output=True, text=True)
+    # the build's per-source flags (e.g. lstm_mfma.hip's -amdgpu-mfma-vgpr-form), as kernel_resources.py does
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "group-gan-gcn-gat_amd"))
+    from build_native import FILE_FLAGS
+    extra = FILE_FLAGS.get(os.path.basename(src), [])
+    r = subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + extra + [src], capture_output=True, text=True)
     rows, cur = [], None
     for line in r.stderr.splitlines():
         m = re.search(r"remark:\s+(.*?)\s*\[-Rpass", line)
