@@ -834,7 +834,10 @@ int sgg_gatenc_param_size(int nh);
 /* Forward state kept for the backward: when args->saved != NULL the forward
  * writes every scene's layer inputs / activations and group structure there
  * and the backward reads them instead of recomputing the forward (it must
- * then be called with the same saved buffer, np and nh). */
+ * then be called with the same saved buffer, np, nh and weights: after the S
+ * scene blocks the buffer holds the weights' LDS image, written by the
+ * forward's workgroup 0 and copied by the backward instead of restaging the
+ * parameters). */
 long long sgg_gatenc_saved_floats(int S, int max_n, int nh);
 /* LDS bytes of a launch's plan (<= 160 KiB to run): bwd 0 the forward, 1 the
  * backward with the forward's saved state (scenes past the full plan, e.g.
