@@ -343,3 +343,23 @@ def test_draw_source_orders_draws_across_trainers():
     assert (seq, items) == (1, [1, 2, 3])
     src.pop(3)
     assert src.take() == 4 and src.seq == 5 and not src.pending
+
+
+def test_pool_plan_targets_by_bottleneck(monkeypatch):
+    """SceneIndex.pool_plan's chunk target (round 5): the generator's bn-8
+    pooling of a configs[1] batch (64 scenes of 20) runs two pair groups per
+    wave (256 chunks: one round of the fragment kernel), the discriminator's
+    bn-48 pooling keeps the 512 target (its 128-scene D-step batch at two
+    groups, its 64-scene G-step batch at one)."""
+    from sgan import _native
+    if not os.path.exists(_native.lib_path()):
+        pytest.skip("libsgg.so not built")
+    from sgan import scene
+    from sgan.scene import SceneIndex
+    # (the plan is host code of the C ABI: no device needed)
+    real_load = _native.load
+    monkeypatch.setattr(scene.N, "load", lambda require_gpu=True: real_load(require_gpu=False))
+    for S, bn, want_gpw, want_nc in ((64, 8, 2, 256), (128, 48, 2, 512), (64, 48, 1, 448)):
+        sc = SceneIndex(np.arange(0, 20 * S + 1, 20, dtype=np.int64), "cpu")
+        _, nc, mr, gpw = sc.pool_plan(bn)[:4]
+        assert (gpw, nc) == (want_gpw, want_nc), (S, bn, gpw, nc)
