@@ -124,3 +124,19 @@ def test_rccl_binding_symbols():
         assert hasattr(lib, f), f
     assert rccl.NCCL_FLOAT32 == 7 and rccl.NCCL_SUM == 0
     assert lib.ncclGetErrorString(0) is not None
+
+
+def test_gatenc_saved_floats_carries_the_weight_image():
+    """sgg_gatenc_saved_floats(S, np, nh) = S per-scene blocks + the weights'
+    staged LDS image (round 5: the backward copies it instead of restaging the
+    parameters) -- a fixed tail independent of S, growing with the heads."""
+    from sgan import _native
+    if not os.path.exists(_native.lib_path()):
+        pytest.skip("libsgg.so not built")
+    lib = _native.load(require_gpu=False)
+    for nh in (1, 2, 4):
+        tail = lib.sgg_gatenc_saved_floats(0, 20, nh)
+        per = lib.sgg_gatenc_saved_floats(1, 20, nh) - tail
+        assert tail > 0 and tail % 4 == 0 and per > 0
+        assert lib.sgg_gatenc_saved_floats(64, 20, nh) == 64 * per + tail
+    assert lib.sgg_gatenc_saved_floats(0, 20, 2) > lib.sgg_gatenc_saved_floats(0, 20, 1)
