@@ -1134,37 +1134,39 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       }
     } else if (!(BWD && saved)) {
       // group structure (models.py:263-278) in ONE wave, lane = ped (n <= 64),
-      // from the labels in global memory (no barrier after the X stores):
-      // the lowest ungrouped ped leads the next group, its members are the
-      // peds with its non-zero label (a zero label: itself alone); groups are
-      // ranked by their first member, as the reference's unique rows
+      // from the labels in global memory (no barrier after the X stores): a
+      // ped's group is every ped with its non-zero label (a zero label: itself
+      // alone), led by its lowest member; groups are ranked by their leaders,
+      // as the reference's unique rows.  Each lane builds its own member mask
+      // over the n labels (broadcast by readlane, no dependence between the
+      // steps) -- the former walk over the groups was a serial chain of
+      // ballots, ~1.5 us of the forward's first phase
       if (tid < 64) {
         const int i = tid;
         const bool in = i < n;
         const float li = !in ? 0.f : first ? lp : q.labels[o + i];
         if (in) lab[i] = li;
-        unsigned long long rem = __ballot(in);
-        int g = i, r = 0, c = 1, m = 0;
-        while (rem) {   // wave-uniform
-          const int lead = __ffsll((long long)rem) - 1;
-          const float ll = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(li), lead));   // (lead: uniform)
-          const unsigned long long same = ll != 0.f ? __ballot(in && li == ll) : (1ull << lead);
-          if ((same >> i) & 1ull) {
-            g = lead;
-            r = m;
-            c = __popcll(same);
-          }
-          if (i == 0) gm[m] = same;
-          ++m;
-          rem &= ~same;
+        unsigned long long same = 0ull;
+        for (int j = 0; j < n; ++j) {   // (n: uniform)
+          const float lj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(li), j));
+          if (lj == li) same |= 1ull << j;
         }
+        if (li == 0.f || !in) same = 1ull << i;
+        same |= 1ull << i;   // (a label that equals nothing, e.g. NaN: itself alone)
+        const int g = __ffsll((long long)same) - 1;   // the leader (in lanes: same has bit i)
+        const unsigned long long leaders = __ballot(in && g == i);
+        const int r = __popcll(leaders & ((1ull << g) - 1ull));
+        const int c = __popcll(same);
         if (in) {
           gidl[i] = g;
           grank[i] = r;
           ginv[i] = 1.f / (float)c;
-          if (g == i) cnt[r] = c;
+          if (g == i) {
+            cnt[r] = c;
+            gm[r] = same;
+          }
         }
-        if (i == 0) *Mp = m;
+        if (i == 0) *Mp = __popcll(leaders);
       }
     }
     lds_barrier(); PMARK(1); PMARK(2);
