@@ -55,6 +55,7 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 dense (vector == f32 MFMA), MI355X_MICR
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0  # MI355X bf16 dense MFMA (no sparsity), MI355X_MICROARCH.md
 RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)   # FLOP / byte
+TRANSPORT = ["rccl"]       # DataParallel transport of the N > 1 runs (main)
 CONFIG4_GLOBAL = 4096      # BASELINE configs[3]: synthetic 20-ped, batch 4096, 8 x MI355X
 GRAPH_ITERS = int(os.environ.get("SGG_GRAPH_ITERS", "4"))   # iterations per HIP-graph replay (one rank)
 # one rank: the G-step's prefix graph beside the D-step graph on a second
@@ -194,32 +195,66 @@ def main_launch(a):
     return max(a["shapes"], key=lambda s: (s[2] * s[1]["bytes"], s[2] * s[1]["flop"]))
 
 
+def _steps_of(name, key):
+    """Serial recurrence steps of one launch of a sequence kernel (the LSTM
+    families: the launch key's first field is the step count T), else None."""
+    if "lstm" in name and len(key) > 1 and isinstance(key[1], int):
+        return key[1]
+    return None
+
+
 def roofline_of(name, a):
-    us = a["us_per_iter"]
-    ai = a["flop"] / max(a["bytes"], 1.0)
+    """The kernel against its roof, per launch of its MAIN launch shape (the
+    one the PMC passes re-issue, main_launch): achieved = that launch's
+    algorithmic FLOP (or bytes) / its average device time, traffic = PMC
+    bytes of that same launch -- so traffic / algorithmic_bytes is a re-read
+    factor of one launch.
+
+    bound: the roof the launch's arithmetic intensity points at ("mfma"
+    above the ridge, "hbm" below) -- unless the launch runs far from both
+    roofs because its time is a dependency chain: "latency" when the time
+    per launch stays > 4x its roofline time and either (a) it is a serial
+    recurrence (T dependent steps: the LSTM families; `latency.us_per_step`)
+    or (b) another launch shape of the kernel with at most 2/3 of the work
+    takes > 0.8x the time (the time does not follow the work).  frac is
+    then roofline time / measured time: max(FLOP / FLOP peak, bytes / HBM
+    peak) over the launch's duration, i.e. achieved / peak of the nearer
+    roof."""
+    key, r, per_it = main_launch(a)
+    us = r["ms"] * 1e3
+    fl, by = r["flop"], r["bytes"]
+    ai = fl / max(by, 1.0)
     # a bf16-MFMA kernel (the opt-in precision) is priced at the dense bf16 peak
     bf16 = "bf16" in name or ("gcnmod" in name and "<true>" in name)
     fpeak = BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
-    if ai >= fpeak * 1e12 / (HBM_PEAK_GBS * 1e9):
-        achieved, peak, unit, bound = a["flop"] / (us * 1e-6) / 1e12, fpeak, "TFLOP/s", "mfma"
+    t_f, t_b = fl / (fpeak * 1e12), by / (HBM_PEAK_GBS * 1e9)
+    t_roof = max(t_f, t_b)
+    steps = _steps_of(name, key)
+    evidence = None
+    for k2, r2, _ in a["shapes"]:
+        w1, w2 = max(fl / fpeak / 1e3, by / HBM_PEAK_GBS), max(r2["flop"] / fpeak / 1e3, r2["bytes"] / HBM_PEAK_GBS)
+        if k2 != key and w2 <= w1 * 2.0 / 3.0 and r2["ms"] * 1e3 > 0.8 * us:
+            evidence = "%s %s: %.2fx the work in %.2fx the time" % (name, list(k2[1:]), w2 / w1, r2["ms"] * 1e3 / us)
+    latency = us * 1e-6 > 4.0 * t_roof and (steps is not None or evidence is not None)
+    if t_f >= t_b:
+        achieved, peak, unit = fl / (us * 1e-6) / 1e12, fpeak, "TFLOP/s"
     else:
-        achieved, peak, unit, bound = a["bytes"] / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
-    # the launch shape carrying most of the kernel's time: its PMC traffic
-    key, r, per_it = main_launch(a)
+        achieved, peak, unit = by / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
+    bound = "latency" if latency else ("mfma" if t_f >= t_b else "hbm")
     traffic = traffic_lookup(name, key)
-    return {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": traffic[0], "traffic_source": traffic[1],
-            "kernel": name, "launches_per_iteration": round(a["launches_per_iter"], 2),
-            "avg_launch_us": round(us / a["launches_per_iter"], 2), "us_per_iteration": round(us, 1),
-            "flop_per_launch": a["flop"] / a["launches_per_iter"],
-            "algorithmic_bytes_per_launch": a["bytes"] / a["launches_per_iter"],
-            "arithmetic_intensity": round(ai, 2), "ridge": round(RIDGE, 2),
-            "traffic_launch": "%s %s (avg %.2f us, %.3g algorithmic B)" % (name, list(key[1:]), r["ms"] * 1e3,
-                                                                          r["bytes"]),
-            "note": ("bf16 MFMA (dense peak)" if bf16 else "fp32 (f32 MFMA, same peak as VALU FMA)") +
-                    "; achieved = algorithmic work of the kernel's launches "
-                    "in one iteration / their summed device time (HIP events around a HIP-graph replay of back-to-back "
-                    "re-issues of each launch on its stream); traffic = PMC HBM bytes of the named launch (null if not profiled)"}
+    out = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+           "frac": round(achieved / peak, 4), "traffic": traffic[0],
+           "kernel": name, "launch": list(key[1:]), "avg_launch_us": round(us, 2),
+           "launches_per_iteration": round(a["launches_per_iter"], 2), "us_per_iteration": round(a["us_per_iter"], 1),
+           "flop_per_launch": fl, "algorithmic_bytes_per_launch": by,
+           "traffic_over_algorithmic": round(traffic[0] / by, 3) if traffic[0] else None,
+           "traffic_source": traffic[1], "arithmetic_intensity": round(ai, 2), "ridge": round(RIDGE, 2)}
+    if latency:
+        out["latency"] = {"roofline_us": round(t_roof * 1e6, 3), "us_per_step": round(us / steps, 3) if steps else None,
+                          "steps": steps, "time_vs_work": evidence,
+                          "note": "a dependency chain, not bandwidth or MFMA throughput: frac = roofline time / "
+                                  "measured time (achieved / peak of the nearer roof)"}
+    return out
 
 
 # SURVEY.md section 8(d): the reference's work per 20-ped scene and training
@@ -342,48 +377,48 @@ def real_data_leg(dev, iters=20, warmup=3, batch=64):
                 K.GATENC_FUSED = True
         torch.cuda.synchronize()
         t_cap = time.perf_counter() - t_cap
-        frozen = K.gc_frozen()   # the captured graphs' state out of the collector's scans (scoped)
-        frozen.__enter__()
-        # (the instrumentation's own set-up -- the allocator statistics, the
-        # first scheduler sample -- comes before the clock starts: it was
-        # ~1.2 ms of the first timed iteration)
-        allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc")
-        # host-side diagnostics per iteration: the thread's run-queue wait
-        # (/proc/thread-self/schedstat: time runnable but not running) and the
-        # cgroup's CPU-quota throttling (cpu.stat throttled_usec) -- a host
-        # stall that is neither Python nor HIP shows up in one of them
-        sched = [host_sched()]
-        phases = []
-        steps_info = []
-        # HIP events between the iterations on the launch stream: each
-        # iteration's device-side span (host timings alone cannot tell a host
-        # stall from the host waiting on a device that is behind)
-        evs = [torch.cuda.Event(enable_timing=True)]
-        t0 = time.perf_counter()
-        scenes = 0
-        marks = [t0]
-        evs[0].record()
-        for _ in range(iters):
-            if mode == "graphed":
-                tn = time.perf_counter()
-                sd, sg = next(it), next(it)
-                tn = (time.perf_counter() - tn) * 1e3
-                bt.step(sd, sg)
-                phases.append((tn,) + (bt.phase_ms or (None, None, None)))
-                steps_info.append(bt.last)
-                evs.append(torch.cuda.Event(enable_timing=True))
-                evs[-1].record()
-                sched.append(host_sched())
-                scenes += len(sd)
-            else:
-                (bd, scd), (bg, scg) = next(it), next(it)
-                tr.d_step(bd, scd)
-                tr.g_step(bg, scg)
-                scenes += scd.S
-            marks.append(time.perf_counter())
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        frozen.__exit__(None, None, None)
+        # the captured graphs' state out of the collector's scans, scoped to the
+        # timed loop (unfrozen on any exit, kernels.gc_frozen)
+        with K.gc_frozen():
+            # (the instrumentation's own set-up -- the allocator statistics, the
+            # first scheduler sample -- comes before the clock starts: it was
+            # ~1.2 ms of the first timed iteration)
+            allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc")
+            # host-side diagnostics per iteration: the thread's run-queue wait
+            # (/proc/thread-self/schedstat: time runnable but not running) and the
+            # cgroup's CPU-quota throttling (cpu.stat throttled_usec) -- a host
+            # stall that is neither Python nor HIP shows up in one of them
+            sched = [host_sched()]
+            phases = []
+            steps_info = []
+            # HIP events between the iterations on the launch stream: each
+            # iteration's device-side span (host timings alone cannot tell a host
+            # stall from the host waiting on a device that is behind)
+            evs = [torch.cuda.Event(enable_timing=True)]
+            t0 = time.perf_counter()
+            scenes = 0
+            marks = [t0]
+            evs[0].record()
+            for _ in range(iters):
+                if mode == "graphed":
+                    tn = time.perf_counter()
+                    sd, sg = next(it), next(it)
+                    tn = (time.perf_counter() - tn) * 1e3
+                    bt.step(sd, sg)
+                    phases.append((tn,) + (bt.phase_ms or (None, None, None)))
+                    steps_info.append(bt.last)
+                    evs.append(torch.cuda.Event(enable_timing=True))
+                    evs[-1].record()
+                    sched.append(host_sched())
+                    scenes += len(sd)
+                else:
+                    (bd, scd), (bg, scg) = next(it), next(it)
+                    tr.d_step(bd, scd)
+                    tr.g_step(bg, scg)
+                    scenes += scd.S
+                marks.append(time.perf_counter())
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
         # host-side iteration times (eager issue is host-bound; a first-use
         # stall -- a kernel's code object loaded at its first launch -- is an outlier)
         per = sorted(b - a for a, b in zip(marks, marks[1:]))
@@ -513,8 +548,8 @@ def timed_run(run, steps, warmup, world, dev, on_start=None):
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
+    if world > 1:   # (host control over gloo: a CPU tensor)
+        t = torch.tensor([elapsed])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     return elapsed
@@ -526,7 +561,7 @@ def setup(per_gpu, peds, rank, world, dev, graph_kind):
     from sgan.train_step import DataParallel, GanTrainer
     g, d = build_models(0, graph_kind)
     g, d = g.to(dev), d.to(dev)
-    trainer = GanTrainer(g, d, dp=DataParallel(), capturable=True)
+    trainer = GanTrainer(g, d, dp=DataParallel(transport=TRANSPORT[0]), capturable=True)
     # the reference feeds consecutive loader batches to the D-step and the
     # G-step (scripts/train.py:279-297): two distinct synthetic batches
     batch = synthetic_batch([peds] * per_gpu, seed=1000 + rank, device=dev)
@@ -560,7 +595,7 @@ def measure(spec, steps, warmup, rank, world, dev, graph_on, n_it=3):
         elif world > 1:
             ar_us = bucket_allreduce_us(trainer, dev)
         if ar_us is not None:
-            t = torch.tensor([ar_us], device=dev)
+            t = torch.tensor([ar_us])
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ar_us = float(t)
         n_it = max(1, min(steps, n_it))
@@ -572,7 +607,8 @@ def measure(spec, steps, warmup, rank, world, dev, graph_on, n_it=3):
     finally:
         K.set_precision("fp32")
     return dict(elapsed=elapsed, graphed=graphed, agg=kernel_table(timed, n_it), recs=recs, n_it=n_it,
-                allreduce_us=ar_us, captured=bool(graphed and world > 1 and not trainer.dp.segmented))
+                allreduce_us=ar_us, captured=bool(graphed and world > 1 and not trainer.dp.segmented),
+                transport=trainer.dp.transport)
 
 
 def bucket_allreduce_us(trainer, dev, reps=20):
@@ -582,7 +618,7 @@ def bucket_allreduce_us(trainer, dev, reps=20):
     iteration's graph (no events there)."""
     nums = [sum(p.numel() for p in ps) + 3 for ps in (trainer.g_params, trainer.d_params)]
     bufs = [torch.zeros(n, device=dev) for n in nums]
-    # the communicator the captured graph uses (sgan.rccl), else the process group's
+    # the communicator the steps use (sgan.rccl), else the process group's
     rc = trainer.dp.rccl
     ar = rc.allreduce_sum_ if rc is not None else dist.all_reduce
     for b in bufs:
@@ -656,22 +692,24 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    # one process per GPU; SGG_BENCH_BACKEND=gloo (and more ranks than GPUs,
-    # ranks sharing a device) is only for rehearsing the multi-rank path on a
-    # one-GPU box -- the driver's runs use nccl (RCCL over xGMI)
+    # one process per GPU.  The process group is gloo and carries host
+    # control only (barriers, the max over ranks); the gradient all-reduces
+    # go through RCCL on sgan.rccl's own communicator (DataParallel transport
+    # "rccl", the unique id exchanged through the rendezvous store) -- no
+    # ProcessGroupNCCL exists, so no watchdog thread polls events while the
+    # step is captured.  SGG_BENCH_BACKEND=gloo (more
+    # ranks than GPUs, ranks sharing a device) is only for rehearsing the
+    # multi-rank path on a one-GPU box: the all-reduces then go through gloo.
     backend = os.environ.get("SGG_BENCH_BACKEND", "nccl")
+    TRANSPORT[0] = "rccl" if backend == "nccl" else "pg"
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-        # the collective library must see exactly the N ranks the line reports
-        if dist.get_world_size() != args.gpus or dist.get_backend() != backend:
-            raise SystemExit("bench: %s process group reports world size %d (backend %s), expected %d"
-                             % (backend, dist.get_world_size(), dist.get_backend(), args.gpus))
+        dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("bench: the process group reports world size %d, expected %d"
+                             % (dist.get_world_size(), args.gpus))
 
     if args.leg:
         head = dict(LEGS[args.leg])
@@ -737,7 +775,7 @@ def main():
         top = sorted(agg.items(), key=lambda kv: -kv[1]["us_per_iter"])
         dom_name, dom = top[0]
         roofline = roofline_of(dom_name, dom)
-        roofline["iteration"] = iteration_roofline(agg, elapsed / args.steps * 1e3, per_gpu)
+        it_roof = iteration_roofline(agg, elapsed / args.steps * 1e3, per_gpu)
         launches = sorted(((r["launches"] / n_it * r["ms"] * 1e3, n, r, k) for n, a in agg.items()
                            for k, r, _ in a["shapes"]), key=lambda x: -x[0])
         # every instrumented launch with its work model: the iteration's
@@ -762,24 +800,24 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(per_gpu, head["peds"], iters=args.cpu_iters)
         is_c1 = world == 1 and (per_gpu, head["peds"], head["graph"], head["prec"]) == (64, 20, "gat", "fp32")
+        # everything beyond the driver's fields goes to a side file named in
+        # the line: the stdout line stays a few KB
+        detail_path = os.environ.get("SGG_BENCH_DETAIL") or os.path.join(
+            ROOT, "gpurun_out", "bench_detail_n%d_%d.json" % (world, os.getpid()))
+        detail = {"roofline": roofline, "iteration_roofline": it_roof, "kernels": top_kernels(agg, 24),
+                  "launch_table": launch_table, "cpu_baseline": cpu, "legs": legs, "scaling_reference": scaling_ref,
+                  "real_data": real, "pmc_target": pmc_target}
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "scenes/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak" if world == 1 else "strong",
             "vs_baseline": round(value / REFERENCE_CPU_SCENES_S, 1) if is_c1 else None,
-            "vs_baseline_basis": "value / 13.9 scenes/s: the reference's own CPU path on this workload (train "
-                                 "iteration, batch 64, 8 threads of the SURVEY container's Xeon -- another machine), "
-                                 "BASELINE.md section 2; the reference publishes no throughput; vs_cpu_same_box is "
-                                 "the ratio on this box" if is_c1 else None,
-            # the same box: the GPU rate over the CPU baseline timed above on
-            # this machine's host cores, beside vs_baseline
+            "vs_baseline_basis": "value / 13.9 scenes/s, the reference's CPU path on this workload in the survey "
+                                 "container (BASELINE.md 2); no published throughput" if is_c1 else None,
             "vs_cpu_same_box": round(value / cpu["value"], 1) if cpu else None,
-            "vs_cpu_same_box_basis": ("value / cpu_baseline.value: the oracle's reference formulation on %d host "
-                                      "cores of this box (%s)" % (cpu["cores"], cpu["cpu_model"])) if cpu else None,
             "dtype": head["prec"],
             "data": "synthetic (random-init weights, SURVEY.md 8d recipe)",
-            "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam) of the %s generator "
-                                   "(scripts/train.py defaults)%s" % (
+            "config": {"workload": "train iteration = D-step + G-step (best_k=20, Adam), %s generator%s" % (
                                        head["graph"].upper(),
                                        "; BASELINE configs[1] shape (batch 64)" if is_c1 else
                                        "; BASELINE configs[3] (4096-scene global batch)"
@@ -788,33 +826,61 @@ def main():
                        "scenes_per_gpu": per_gpu, "global_batch": per_gpu * world, "peds_per_scene": head["peds"],
                        "obs_len": 8, "pred_len": 12, "generator": head["graph"], "hip_graph": res["graphed"],
                        "parallelism": "dp%d" % world},
-            "roofline": roofline, "kernels": top_kernels(agg, 10), "cpu_baseline": cpu,
+            "roofline": {k: roofline[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                                  "launch", "avg_launch_us", "flop_per_launch",
+                                                  "algorithmic_bytes_per_launch", "traffic_over_algorithmic")},
+            "cpu_baseline": None if cpu is None else {k: cpu[k] for k in ("value", "unit", "cores", "kind", "cpu_model")}
+            | {"sample": "%d train iterations on %d x %d-ped synthetic scenes, oracle reference formulation, torch CPU "
+                         "fp32" % (args.cpu_iters, per_gpu, head["peds"])},
             "instrumented_us_per_iter": round(total_launch_us, 1),
-            "instrumented_launches_per_iter": round(sum(a["launches_per_iter"] for a in agg.values()), 1),
-            "launch_table": launch_table,
+            "detail": os.path.relpath(detail_path, ROOT),
         }
+        if "latency" in roofline:
+            line["roofline"]["latency"] = {k: roofline["latency"][k] for k in ("us_per_step", "steps", "roofline_us")}
+        line["roofline"]["iteration_frac"] = it_roof["frac"]
         if legs:
-            line["legs"] = legs
+            line["legs"] = [{"config": l["config"], "value": l["value"], "ms_per_step": l["ms_per_step"],
+                             "dtype": l["dtype"], "roofline": {k: l["roofline"][k] for k in ("kernel", "bound", "frac")}}
+                            for l in legs]
         if scaling_ref is not None:
-            line["scaling_reference"] = scaling_ref
+            line["scaling_reference"] = {k: scaling_ref[k] for k in ("global_batch", "value", "ms_per_step")}
         if real is not None:
-            line["real_data"] = real
+            gd = real["graphed_device_data_path"]
+            line["real_data"] = {"split": real["split"], "batch": real["batch"],
+                                 "graphed": {k: gd.get(k) for k in ("value", "ms_per_iteration", "host_ms_median",
+                                                                    "host_ms_max", "device_ms_median")},
+                                 "device_data_path": real["device_data_path"]["value"],
+                                 "host_data_path": real["host_data_path"]["value"]}
         if pmc_target is not None:
             line["pmc_target"] = pmc_target
         if world > 1:
             ar = res["allreduce_us"]
             line["communication"] = {
-                "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                "transport": res["transport"], "control": dist.get_backend(), "world_size": dist.get_world_size(),
                 "allreduce_us_per_iter": round(ar, 1) if ar is not None else None,
                 "compute_us_per_iter": round(ms_step * 1e3 - ar, 1) if ar is not None else None,
                 "allreduces_per_iter": 2,
-                "collectives": "captured in the HIP graph" if res.get("captured") else "eager between graph segments",
-                "note": "one flat SUM bucket per optimizer step; captured: the two buckets all-reduced eagerly "
-                        "between HIP events after the timed run; segmented: HIP events around each eager "
-                        "all-reduce between the graph segments; per iteration, max over ranks; compute = "
-                        "ms_per_step - all-reduce time"}
+                "collectives": "captured in the HIP graph" if res.get("captured") else "eager between graph segments"}
+            detail["communication_note"] = (
+                "one flat SUM bucket per optimizer step; transport rccl = ncclAllReduce on sgan.rccl's communicator "
+                "(no ProcessGroupNCCL; gloo carries host control), pg = the gloo process group's all_reduce; "
+                "captured: the two buckets all-reduced eagerly between HIP events after the timed run; segmented: "
+                "HIP events around each eager all-reduce between the graph segments; per iteration, max over ranks; "
+                "compute = ms_per_step - all-reduce time")
+        try:
+            os.makedirs(os.path.dirname(detail_path), exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(dict(line=line, **detail), f, indent=1, default=str)
+        except OSError as e:
+            line["detail"] = "unwritten (%s)" % e
         print(json.dumps(line), flush=True)
     if world > 1:
+        import gc
+        from sgan import rccl
+        gc.collect()   # the captured graphs are gone before their communicator
+        torch.cuda.synchronize()
+        dist.barrier()
+        rccl.release()
         dist.destroy_process_group()
 
 

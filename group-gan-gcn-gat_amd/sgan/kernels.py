@@ -79,6 +79,41 @@ def precision():
 # ---------------------------------------------------------------------------
 # dense node transform
 # ---------------------------------------------------------------------------
+_private = {}   # (tag, device index) -> torch.cuda.ExternalStream
+_hiprt = None
+
+
+def private_stream(tag, device=None):
+    """A HIP stream of this package's own as a torch.cuda.ExternalStream --
+    hipStreamCreateWithFlags(hipStreamNonBlocking) through the HIP runtime
+    torch loaded, one per (tag, device), kept for the process.  It lies
+    outside torch's stream pool (32 pooled streams handed out round-robin),
+    so it can never be the stream of a torch.distributed process group or of
+    other torch code: the graph captures (GraphedTrainer, tag "capture"), the
+    weight-gradient side stream ("side"), the overlap plan's second stream
+    ("overlap") and the launch timer ("timer") run on such streams."""
+    global _hiprt
+    import ctypes
+    dev = torch.cuda.current_device() if device is None else torch.device(device).index
+    if dev is None:
+        dev = torch.cuda.current_device()
+    key = (tag, dev)
+    st = _private.get(key)
+    if st is None:
+        if _hiprt is None:
+            lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+            lib.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            lib.hipStreamCreateWithFlags.restype = ctypes.c_int
+            _hiprt = lib
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            rc = _hiprt.hipStreamCreateWithFlags(ctypes.byref(h), 1)   # hipStreamNonBlocking
+        if rc != 0 or not h.value:
+            raise N.NativeError("hipStreamCreateWithFlags failed (%d)" % rc)
+        st = _private[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", dev))
+    return st
+
+
 class _Side:
     stream = None
     origin = None   # the stream that must wait for the side work
@@ -97,7 +132,7 @@ def side(*keep):
         return
     cur = torch.cuda.current_stream()
     if _Side.stream is None or _Side.stream.device != cur.device:
-        _Side.stream = torch.cuda.Stream(device=cur.device)
+        _Side.stream = private_stream("side", cur.device)
     st = _Side.stream
     st.wait_stream(cur)
     _Side.keep.extend(t for t in keep if t is not None)
@@ -1093,7 +1128,7 @@ class LaunchTimer:
             # the re-issues are captured into a HIP graph and replayed, so the
             # events bracket device work only (an eager loop of ctypes launches
             # is host-bound for the few-us kernels)
-            side = torch.cuda.Stream()
+            side = private_stream("timer")
             side.wait_stream(cur)
             graph = torch.cuda.CUDAGraph()
             try:

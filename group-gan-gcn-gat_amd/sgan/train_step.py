@@ -90,39 +90,58 @@ def _valid(sc):
 class DataParallel:
     """Scene-sharded DP context (world 1 = plain single-GPU).
 
+    transport: how the gradient all-reduce travels --
+      "rccl"  ncclAllReduce on a communicator of sgan.rccl (one per process
+              group, its id exchanged through the rendezvous store): eager,
+              or captured inside GraphedTrainer's HIP graph (capture=True,
+              the default for this transport: one graph per replay);
+      "pg"    the process group's own all_reduce (gloo: host collectives,
+              CPU tensors or ranks sharing one GPU) -- never captured: the
+              graph is cut into segments with the all-reduces run eagerly
+              between them.
+    Default: "rccl" for a process group whose backend includes nccl, else
+    "pg"; SGG_DP_TRANSPORT overrides it, SGG_CAPTURE_COLLECTIVE=0 forces the
+    segment form.  No transport issues a collective of torch's
+    ProcessGroupNCCL: its watchdog thread polls the events of the
+    collectives it issued, and a poll that meets a capturing stream aborts
+    the process (sgan/rccl.py).
+
     exercise: run the gradient all-reduce even at world size 1 (the DP code
     path on one GPU: an RCCL SUM over one rank is the identity, so the step
-    must stay bitwise equal to the non-DP one).  capture: the all-reduces are
-    captured INSIDE GraphedTrainer's HIP graph (RCCL is stream-capturable:
-    one graph per replay); default on for the nccl (= RCCL) backend, off for
-    gloo (a host collective cannot be captured: the graph is then cut into
-    segments with the all-reduces run eagerly between them).
-    SGG_CAPTURE_COLLECTIVE=0 forces the segment form.
+    must stay bitwise equal to the non-DP one)."""
 
-    The captured all-reduce goes straight to RCCL (sgan.rccl.RcclComm: a
-    communicator of its own, ncclAllReduce on the capturing stream): torch's
-    process-group watchdog polls the completion event of every collective
-    the process group issues, and a poll during a capture fails with
-    hipErrorCapturedEvent and invalidates the capture."""
-
-    def __init__(self, group=None, exercise=False, capture=None):
+    def __init__(self, group=None, exercise=False, capture=None, transport=None):
         self.on = dist.is_available() and dist.is_initialized()
         self.group = group
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
         self.exercise = bool(exercise) and self.on
+        if transport is None:
+            transport = os.environ.get("SGG_DP_TRANSPORT") or (
+                "rccl" if self.on and "nccl" in str(dist.get_backend(group)) else "pg")
+        if transport not in ("rccl", "pg"):
+            raise ValueError("DataParallel: transport %r (rccl | pg)" % (transport,))
+        self.transport = transport
         if capture is None:
-            capture = self.on and dist.get_backend(group) == "nccl" and \
-                os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0"
+            capture = transport == "rccl" and os.environ.get("SGG_CAPTURE_COLLECTIVE", "1") != "0"
+        if capture and transport != "rccl":
+            raise ValueError("DataParallel: only the rccl transport's all-reduce can be captured in a graph")
         self.capture = bool(capture) and self.on
         self.cut = None   # set by GraphedTrainer while capturing: graph segment boundary
-        # the captured form's own RCCL communicator (made here: every rank
-        # builds its DataParallel at the same point, the id broadcast is a
-        # collective)
-        self.rccl = None
-        if self.capture and self.collective:
-            from .rccl import RcclComm
-            self.rccl = RcclComm(group)
+
+    @property
+    def rccl(self):
+        """The RCCL communicator of the rccl transport (sgan.rccl.comm_for:
+        made at the first use, one per process group), else None."""
+        if self.transport != "rccl" or not self.collective:
+            return None
+        from .rccl import comm_for
+        return comm_for(self.group)
+
+    def prepare(self):
+        """Make the communicator now (a collective point of every rank):
+        before any graph capture, which must not create it."""
+        self.rccl
 
     @property
     def collective(self):
@@ -156,7 +175,7 @@ class DataParallel:
             self.cut(tensors)
             return
         flat = torch.cat([t.reshape(-1) for t in tensors])
-        if self.rccl is not None:
+        if self.transport == "rccl":
             self.rccl.allreduce_sum_(flat)
         else:
             dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
@@ -696,8 +715,11 @@ class GraphedTrainer:
                              "capture=True: nccl) or one rank -- segmented collectives cut the graph")
         # warm-up and capture on the same side stream: the parameters'
         # AccumulateGrad nodes (created by the first backward, kept alive by
-        # the captured graph) are bound to the stream that created them
-        cap = torch.cuda.Stream()
+        # the captured graph) are bound to the stream that created them.  A
+        # stream of our own, outside torch's pool (kernels.private_stream):
+        # never a process group's stream
+        cap = K.private_stream("capture")
+        trainer.dp.prepare()   # the RCCL communicator (if any) exists before the capture
         cap.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(cap):
             for _ in range(warmup):
@@ -789,7 +811,7 @@ class GraphedTrainer:
         on the other stream."""
         t = self.t
         bg, scg = (self.batch, self.sc) if self.batch_g is None else (self.batch_g, self.sc_g)
-        self.side = torch.cuda.Stream()
+        self.side = K.private_stream("overlap")
         for i in range(2):
             pool_b, pool_a = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
             parts = []

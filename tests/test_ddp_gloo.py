@@ -190,3 +190,72 @@ def test_shard_covers_scenes():
         dp.rank = r
         spans.append(dp.shard(8))
     assert spans == [(0, 3), (3, 6), (6, 8)]
+
+
+def test_rccl_uid_round_trip_keeps_nul_bytes():
+    """the RCCL unique id is 128 raw bytes whose sockaddr
+    part holds zeros; packing must not cut it at the first NUL."""
+    from sgan import rccl
+    raw = bytes([0x11, 0x22, 0, 0, 2, 0, 0x1f, 0x90] + [i % 7 for i in range(120)])
+    assert len(raw) == rccl.UID_BYTES and raw.count(0) > 10
+    uid = rccl.unpack_uid(raw)
+    assert rccl.pack_uid(uid) == raw
+    assert bytes(uid.internal) != raw    # (what the round-5 code sent: cut at byte 2)
+    with pytest.raises(ValueError):
+        rccl.unpack_uid(raw[:9])
+
+
+def _uid_rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sgan import rccl
+    from sgan.train_step import DataParallel
+    got = []
+    for n in range(3):   # repeated exchanges of one group use distinct keys
+        made = bytes([n, 0, 0, 2] + [rank] * 124)
+        got.append(rccl.exchange_uid(lambda: made, None))
+    dp = DataParallel()
+    torch.save({"got": got, "transport": dp.transport, "capture": dp.capture, "collective": dp.collective},
+               "%s.%d" % (out, rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_uid_exchange_through_store_world2():
+    """The id travels through the rendezvous store (no collective of any
+    process group): every rank receives rank 0's 128 bytes exactly, for each
+    of several exchanges in order; a gloo group's DataParallel picks the pg
+    transport (never captured)."""
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "uid")
+        mp.spawn(_uid_rank, args=(2, _free_port(), out), nprocs=2, join=True)
+        r0 = torch.load(out + ".0", weights_only=True)
+        r1 = torch.load(out + ".1", weights_only=True)
+    assert r0["got"] == r1["got"]
+    for n, g in enumerate(r0["got"]):
+        assert g == bytes([n, 0, 0, 2] + [0] * 124)
+    for r in (r0, r1):
+        assert r["transport"] == "pg" and not r["capture"] and r["collective"]
+
+
+def test_dataparallel_transport_choice(monkeypatch):
+    from sgan.train_step import DataParallel
+    dp = DataParallel()   # no process group: one rank, nothing to reduce
+    assert not dp.on and not dp.collective and dp.rccl is None and dp.transport == "pg"
+    with pytest.raises(ValueError):
+        DataParallel(transport="mpi")
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda g=None: 2)
+    monkeypatch.setattr(dist, "get_rank", lambda g=None: 0)
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "nccl")
+    dp = DataParallel()
+    assert dp.transport == "rccl" and dp.capture and not dp.segmented
+    monkeypatch.setenv("SGG_CAPTURE_COLLECTIVE", "0")
+    assert DataParallel().segmented
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "gloo")
+    dp = DataParallel()
+    assert dp.transport == "pg" and dp.segmented
+    with pytest.raises(ValueError):
+        DataParallel(capture=True)          # a host collective cannot be captured
+    monkeypatch.setenv("SGG_DP_TRANSPORT", "rccl")
+    assert DataParallel().transport == "rccl"

@@ -1760,27 +1760,6 @@ def test_clip_adam_matches_torch(max_norm):
             close(sb["exp_avg_sq"], sa["exp_avg_sq"].cpu(), rtol=2e-6, floor=1e-9, what="v %d it %d" % (i, it))
 
 
-def test_graphed_trainer_two_ranks():
-    """Scene-sharded DP with the segmented graph replay (GraphedTrainer cuts
-    the capture at each gradient all-reduce): 2 ranks on this GPU over gloo
-    (tests/_dp_graph_worker.py), graph replay == eager step on every rank."""
-    import socket
-    import subprocess
-    import sys
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, OMP_NUM_THREADS="1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port),
-                        os.path.join(here, "_dp_graph_worker.py")],
-                       capture_output=True, text=True, timeout=110, env=env)
-    out = r.stdout + r.stderr
-    assert r.returncode == 0 and out.count(" OK") == 2, out[-3000:]
-
-
 @pytest.mark.parametrize("bn,H,sizes", [(48, 48, [20] * 12 + [64, 3]), (8, 32, [20] * 40 + [57, 1])])
 def test_pool_backward_one_launch_equals_two(bn, H, sizes):
     """The pooling backward's dh = dU W1h and h^T dU partials in one launch

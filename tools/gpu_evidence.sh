@@ -4,7 +4,7 @@
 # WRITE_SIZE; separate runs, eager) re-issuing the dominant kernel's main launch
 # of the headline and of every leg -> the traffic table.  Each GPU step has its
 # own time limit; the script stops at the first failure.
-# usage: bash tools/gpu_evidence.sh TAG
+# usage: [PMC=0] [LEGS="head ..."] bash tools/gpu_evidence.sh TAG   (PMC=0: no PMC passes)
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -12,14 +12,14 @@ tag=$1
 O=$R/gpurun_out/$tag
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS_FAIL; tail -40 $O/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS_FAIL; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $O/smoke.log; exit 1; }
 tail -3 $O/smoke.log
-timeout -k 10 400 python bench.py --steps 100 --warmup 10 > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
+SGG_BENCH_DETAIL=$O/bench_detail.json timeout -k 10 400 python bench.py --steps 100 --warmup 10 > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-real-data --no-scaling-reference --no-legs > $O/prof_bench.json 2> $O/prof.err || { echo PROF_FAIL; tail -20 $O/prof.err; exit 1; }
-for leg in head configs3_shard512 configs2_gcn_fp32 configs2_gcn_bf16 configs4_sgangat_bf16; do
+[ "${PMC:-1}" = 1 ] && for leg in ${LEGS:-head configs3_shard512 configs2_gcn_fp32 configs2_gcn_bf16 configs4_sgangat_bf16}; do
   K=$(python -c "
 import json; d = json.loads(open('$O/bench.json').read().strip().splitlines()[-1])
 legs = {l['config']: l for l in d.get('legs', [])}
