@@ -120,6 +120,19 @@ __device__ __forceinline__ void load_vec(const float* p, float (&v)[MU]) {
 // unit held by slot j of lane quarter q
 __device__ __forceinline__ int slot_unit(int j, int q) { return 16 * (j >> 2) + 4 * q + (j & 3); }
 
+// c + a.b over two K = 32 chunks from the pieces (sgg_common.h mfma_x3): the
+// six product kinds smallest first, each over both chunks, on one
+// accumulator (16x16x32 bf16 MFMAs issue back to back on one chain)
+__device__ __forceinline__ floatx4 mfma_x3x2(const bf16x8 (&a)[2][3], const bf16x8 (&b)[2][3], floatx4 c) {
+  constexpr int pa[6] = {2, 1, 0, 1, 0, 0}, pb[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][pa[k]], b[0][pb[k]], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][pa[k]], b[1][pb[k]], c, 0, 0, 0);
+  }
+  return c;
+}
+
 // h staging pitch: q * pitch mod 64 in {0, 16, 32, 48} keeps the B-operand
 // read (4 peds x 16 consecutive units) on distinct banks
 template <int H>
@@ -143,15 +156,28 @@ struct MwCfg {
 
 #ifdef SGG_LSTM_PROF
 // phase timestamps of workgroup 0 (tools/lstm_mw_probe.hip; diagnostic builds only)
-__device__ long long g_lstm_prof[64];
+__device__ long long g_lstm_prof[256];
 #define LMARK(i) \
   if (threadIdx.x == 0 && blk == 0) g_lstm_prof[i] = wall_clock64();
+// sub-phases of step 4, lane 0 of every wave: [64 + 8 wave + k]
+#define LSUB(k) \
+  if ((threadIdx.x & 63) == 0 && blk == 0 && t == 4) g_lstm_prof[64 + 8 * (threadIdx.x >> 6) + (k)] = wall_clock64();
+#define LUSE(x) __asm__ volatile("" ::"v"(x));
+// backward: sub-phases of the 5th step from the end, lane 0 of every wave: [96 + 8 wave + k]
+#define LSUBB(k) \
+  if ((threadIdx.x & 63) == 0 && blk == 0 && t == T - 5) g_lstm_prof[96 + 8 * (threadIdx.x >> 6) + (k)] = wall_clock64();
 #else
+#define LSUBB(k)
 #define LMARK(i)
+#define LSUB(k)
+#define LUSE(x)
 #endif
 
 #ifndef SGG_MW_UPRE
 #define SGG_MW_UPRE 1   // the projection epilogue's Wu fragments fetched in the prologue (0: probe A/B only)
+#endif
+#ifndef SGG_MW_FWD_X3
+#define SGG_MW_FWD_X3 1   // the encoders' gate GEMM on split-bf16 MFMAs (0: the fp32 16x16x4 form; A/B builds)
 #endif
 
 namespace {
@@ -175,7 +201,22 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   float* __restrict__ act_tile = sg.act_tile;
   float* __restrict__ rel_out = sg.rel_out;
   const int T = sg.T, B = sg.B, Bl = sg.Bl, t0 = sg.t0, Tl = sg.Tl;
-  __shared__ float hb[2][KS][64];
+  // X3 (encoders, H 32 / 48): the gate GEMM on split-bf16 MFMAs (section
+  // 4a of DESIGN.md).  h_{t-1} is exchanged as its three bf16 pieces in the
+  // B-operand layout of v_mfma_f32_16x16x32_bf16: lane (q, c16) holds, per
+  // chunk c and piece p, the 8 values of K slots s = 8 c + i of quarter q,
+  // ped c16, one 16-byte LDS read each (hx[buf][p][c][lane]).  Slot s = 4 w + m
+  // is h of unit slot_unit(w MU + m, q) -- written by lane (q, c16) of wave w,
+  // its m-th slot -- for m < MU, and the step input for m = 3 (w = 0: r_x,
+  // 1: r_y, 2: the bias' 1, 3: 0; the weights read it in quarter 0 only);
+  // each producer lane writes its 4 slots of a piece as one 8-byte store.
+  // The fp32 gate tiles of the MFMA output are those of the fp32 form (the
+  // same A rows), so activations, saved states and the backward are
+  // unchanged.  36 MFMAs of 16 cycles per wave and step at H = 48 (fp32:
+  // 39 of 32), and this MFMA shape leaves VALU issue slots beside it.
+  constexpr bool X3 = !DEC && SGG_MW_FWD_X3 && (H == 32 || H == 48);
+  __shared__ float hb[X3 ? 1 : 2][KS][64];        // fp32 form: h_{t-1}; X3: h_T for the epilogue
+  __shared__ sgg_uint4v hx[X3 ? 2 : 1][3][2][64];  // X3: the pieces of h_{t-1} and the step input
   __shared__ float2 rpart[2][4][kMwPeds];
   __shared__ float relseq[kMwMaxT][kMwPeds][2];
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -190,8 +231,33 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   // permuted k order (slot_unit(4 m + i, q) = 16 m + 4 q + i: one 16-byte load
   // per block m)
   float w[MU][KS + 1], ak0[MU], ak1[MU];
+  bf16x8 wx[X3 ? MU : 1][2][3];
+  if constexpr (X3) {
+    // A operand of the split form: lane (q, c16) holds row c16 (gate c16 & 3
+    // of unit slot_unit(g MU + mu, c16 >> 2)) at the K slots of quarter q
 #pragma unroll
-  for (int mu = 0; mu < MU; ++mu) {
+    for (int mu = 0; mu < MU; ++mu) {
+      const int row = (c16 & 3) * H + slot_unit(g * MU + mu, c16 >> 2);
+      const float a0 = A[2 * row], a1 = A[2 * row + 1], bi = bias[row];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int w2 = (8 * c + i) >> 2, m2 = (8 * c + i) & 3;
+          if (m2 < MU)
+            v[i] = Whh[row * H + slot_unit(w2 * MU + m2, q)];
+          else if (m2 == 3)
+            v[i] = q != 0 ? 0.f : w2 == 0 ? a0 : w2 == 1 ? a1 : w2 == 2 ? bi : 0.f;
+          else
+            v[i] = 0.f;
+        }
+        split8(v, wx[mu][c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int mu = 0; mu < (X3 ? 0 : MU); ++mu) {
     const int row = (c16 & 3) * H + slot_unit(g * MU + mu, c16 >> 2);
 #pragma unroll
     for (int m = 0; m < KS / 4; ++m) {
@@ -205,7 +271,7 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
     ak1[mu] = A[2 * row + 1];
     w[mu][KS] = q == 0 ? ak0[mu] : q == 1 ? ak1[mu] : q == 2 ? bias[row] : 0.f;
   }
-  float c[MU], wp0[MU], wp1[MU];
+  float c[MU], wp0[MU], wp1[MU], hv0[MU];
   // t0 > 0: the source block / row of the state entering step t0
   const int nsrc = (sg.Bsrc + kMwPeds - 1) / kMwPeds;
   const int sblk = t0 > 0 ? blk % nsrc : blk;
@@ -226,7 +292,8 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
       }
     }
     c[i] = cv;
-    hb[0][j][lane] = hv;
+    hv0[i] = hv;
+    if constexpr (!X3) hb[0][j][lane] = hv;
     wp0[i] = decoder ? Wp[u] : 0.f;
     wp1[i] = decoder ? Wp[H + u] : 0.f;
   }
@@ -337,6 +404,30 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
     for (int m = 0; m < kTo; ++m)
       if (tod[m]) *tod[m] = tov[m];
   }
+  // the split image of h_{-1} and the step-0 input (this wave's slots)
+  auto put_x3 = [&](int buf, const float (&hv)[MU], float inv) {
+    float v[4] = {0.f, 0.f, 0.f, inv};
+#pragma unroll
+    for (int i = 0; i < MU; ++i) v[i] = hv[i];
+    unsigned wd[3][2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float h0, m0, l0, h1, m1, l1;
+      split3(v[2 * k], h0, m0, l0);
+      split3(v[2 * k + 1], h1, m1, l1);
+      wd[0][k] = bf16_pack_top(h0, h1);
+      wd[1][k] = bf16_pack_top(m0, m1);
+      wd[2][k] = bf16_pack_top(l0, l1);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      reinterpret_cast<uint2*>(&hx[buf][p][g >> 1][lane])[g & 1] = make_uint2(wd[p][0], wd[p][1]);
+  };
+  // the step input of this wave's slot 3 (r_x, r_y, 1, 0)
+  auto in_x3 = [&](int t) -> float {
+    return g < 2 ? rel[((size_t)(t0 + t) * B + pc) * 2 + g] : (g == 2 ? 1.f : 0.f);
+  };
+  if constexpr (X3) put_x3(0, hv0, in_x3(0));
   // LDS only: the prologue's global stores (saved initial state) need not
   // complete before the recurrence
   lds_barrier();
@@ -354,6 +445,7 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
   const SggTrajOut& to = sg.to;
   const int tcol = pc - to.col0;   // this lane's column of the discriminator input
   const bool tlive = decoder && to.out != nullptr && tcol >= 0 && tcol < to.ncol;
+  float hl[MU];   // X3: h of the last step
   for (int t = 0; t < T; ++t) {
     if (decoder && t == 1) {
       // fold the hidden2pos feedback into the recurrence (see header)
@@ -369,19 +461,72 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
         if (q == 2) w[mu][KS] = fmaf(ak1[mu], bp1, fmaf(ak0[mu], bp0, w[mu][KS]));
       xin = q == 2 ? 1.f : 0.f;
     }
-    const int rb = t & 1;   // h_{t-1} is in hb[rb]; h_t goes to hb[rb ^ 1]
+    const int rb = t & 1;   // h_{t-1} is in hb[rb] (hx[rb]); h_t goes to hb[rb ^ 1] (hx[rb ^ 1])
+    if constexpr (X3) {
+      // the split-bf16 step: tile mu + 1's MFMA chain is issued before tile
+      // mu's activations, so the VALU work of one tile runs in the issue
+      // slots the 16x16x32 bf16 MFMAs of the next leave free
+      LSUB(0);
+      bf16x8 hbx[2][3];
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) hbx[cc][p] = __builtin_bit_cast(bf16x8, hx[rb][p][cc][lane]);
+      const float xnext = g < 2 ? relseq[min(t + 1, T - 1)][c16][g] : (g == 2 ? 1.f : 0.f);
+      LUSE(__builtin_bit_cast(sgg_uint4v, hbx[1][2])[0]);
+      LSUB(1);
+      if (kUPre && upre) {
+#pragma unroll
+        for (int i = 0; i < kUT; ++i)
+          if (t == i) load_wu(i);
+      }
+      floatx4 acc[MU];
+      acc[0] = mfma_x3x2(wx[0], hbx, floatx4{0.f, 0.f, 0.f, 0.f});
+      LSUB(2);
+      float hn[MU];
+#pragma unroll
+      for (int mu = 0; mu < MU; ++mu) {
+        if (mu + 1 < MU) acc[mu + 1] = mfma_x3x2(wx[mu + 1], hbx, floatx4{0.f, 0.f, 0.f, 0.f});
+        const int j = g * MU + mu;
+        float a[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float s = r == 2 ? 2.f : 1.f;
+          a[r] = gate_act(acc[mu][r], s, s * kNegLog2e);
+        }
+        if (save)
+          reinterpret_cast<float4*>(act_tile)[(((size_t)blk * Tl + t0 + t) * KS + j) * 64 + lane] =
+              make_float4(a[0], a[1], a[2], a[3]);
+        c[mu] = fmaf(a[1], c[mu], a[0] * a[2]);
+        hn[mu] = a[3] * tanh_m(c[mu]);
+        hl[mu] = hn[mu];
+        if (save) h_all[((size_t)(t0 + t + 1) * Bl + pc) * H + slot_unit(j, q)] = hn[mu];
+      }
+      if (save)
+        store_vec<MU>(c_tile + ((((size_t)blk * (Tl + 1) + t0 + t + 1) * 4 + g) * 64 + lane) * MU, c);
+      LSUB(3);
+      put_x3(rb ^ 1, hn, xnext);
+      LSUB(4);
+      lds_barrier();
+      LSUB(5);
+      if (t < 60) LMARK(t + 2);
+      continue;
+    }
     floatx4 acc[MU];
+    {
 #pragma unroll
-    for (int mu = 0; mu < MU; ++mu)
-      acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][KS], xin, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    float hk[KS];
+      for (int mu = 0; mu < MU; ++mu)
+        acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][KS], xin, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      float hk[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[rb][ks][lane];
-    if (!decoder && t + 1 < T) xin = input(t + 1);
+      for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[rb][ks][lane];
+      if (!decoder && t + 1 < T) xin = input(t + 1);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+      for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int mu = 0; mu < MU; ++mu) acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][ks], hk[ks], acc[mu], 0, 0, 0);
+        for (int mu = 0; mu < MU; ++mu)
+          acc[mu] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mu][ks], hk[ks], acc[mu], 0, 0, 0);
+    }
     if (kUPre && upre) {
 #pragma unroll
       for (int i = 0; i < kUT; ++i)
@@ -436,6 +581,14 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
       }
     }
   }
+  if constexpr (X3) {   // h_T: the projection epilogue's operand (fp32, permuted k order), the output row
+#pragma unroll
+    for (int mu = 0; mu < MU; ++mu) {
+      hb[0][g * MU + mu][lane] = hl[mu];
+      if (!save && h_all) h_all[((size_t)(t0 + T) * Bl + pc) * H + slot_unit(g * MU + mu, q)] = hl[mu];
+    }
+    lds_barrier();
+  }
   if (DEC && to.out != nullptr && T <= kMwMaxT) {   // the generated steps of the discriminator input
     lds_barrier();
     for (int e = threadIdx.x; e < T * kMwPeds; e += kMwThreads) {
@@ -456,7 +609,7 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
     // accumulation chains
     float hk[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[T & 1][ks][lane];
+    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[X3 ? 0 : T & 1][ks][lane];
     const int ntile = NU >> 4;
     floatx4 acc[kUT];
 #pragma unroll
@@ -480,7 +633,7 @@ __device__ __forceinline__ void mw_fwd_body(const MwSeg& sg, int blk) {
     // takes tiles g, g + 4, ...
     float hk[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[T & 1][ks][lane];
+    for (int ks = 0; ks < KS; ++ks) hk[ks] = hb[X3 ? 0 : T & 1][ks][lane];
     const int ntile = NU >> 4;
     // tiles in pairs (two independent accumulation chains); the next pair's
     // Wu fragments are in flight during the current pair's MFMAs
@@ -744,13 +897,18 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
         if (t > 0) rel_load(t - 1);
       }
       lds_barrier();   // (t)
+      LSUBB(0);
       dw_accum(cur);
+      LUSE(dw[0][0][0]);
+      LSUBB(1);
       if (hacc && t < T - 1) drel_store(t + 1);
       if (hdb) hsum(cur);
+      LSUBB(2);
       if (t > 0) {
         stage_store(cur ^ 1);
         if (t > 1) stage_load(t - 2);
       }
+      LSUBB(3);
     }
     if (hacc) {   // the owners' extra barrier: step 0's partials are complete
       lds_barrier();
@@ -854,7 +1012,13 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   // saved activations and cells of the owned slots (and the decoder's output
   // gradient, the step input of the weight gradient), one step ahead;
   // tile-native, lane-linear
-  float ni[MU], nf[MU], ng[MU], no[MU], nc[MU], ncp[MU], nd0 = 0.f, nd1 = 0.f, nr0 = 0.f, nr1 = 0.f;
+  // (the activations stay one 16-byte vector per slot from the load to the
+  // use: split into scalars, the loop-carried copies did not line up with the
+  // dwordx4 load's registers and the compiler moved two lanes of the FRESH
+  // load right after issuing it -- a wait for a whole memory round trip at
+  // the head of every step, ~1 us; tools/lstm_bwd_probe.hip)
+  floatx4 na[MU];
+  float nc[MU], ncp[MU], nd0 = 0.f, nd1 = 0.f, nr0 = 0.f, nr1 = 0.f;
   auto load_step = [&](int t) {
     if (wgrad) {   // r_in(t): rel[t] (encoder); rel0, then rel_out[t - 1] (decoder)
       const float* rp = !decoder ? rel + ((size_t)t * B + pc) * 2
@@ -865,13 +1029,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
     }
     const float4* ab = reinterpret_cast<const float4*>(act_tile) + ((size_t)sblk(t < t_sh) * T + t) * KS * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < MU; ++i) {
-      const float4 v = ab[(g * MU + i) * 64];
-      ni[i] = v.x;
-      nf[i] = v.y;
-      ng[i] = v.z;
-      no[i] = v.w;
-    }
+    for (int i = 0; i < MU; ++i) na[i] = *reinterpret_cast<const floatx4*>(ab + (g * MU + i) * 64);
     load_vec<MU>(c_tile + ((((size_t)sblk(t + 1 <= t_sh) * (T + 1) + t + 1) * 4 + g) * 64 + lane) * MU, nc);
     load_vec<MU>(c_tile + ((((size_t)sblk(t <= t_sh) * (T + 1) + t) * 4 + g) * 64 + lane) * MU, ncp);
     if (decoder) {
@@ -906,14 +1064,13 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   for (int t = T - 1; t >= t_stop; --t) {
     if (T - 1 - t < 60) LMARK(2 + T - 1 - t);
     const int cur = t & 1;
+    LSUBB(0);
     const float d0 = nd0, d1 = nd1, r0 = nr0, r1 = nr1;
-    float ci[MU], cf[MU], cg[MU], co[MU], cc[MU], ccp[MU];
+    floatx4 ca[MU];
+    float cc[MU], ccp[MU];
 #pragma unroll
     for (int i = 0; i < MU; ++i) {
-      ci[i] = ni[i];
-      cf[i] = nf[i];
-      cg[i] = ng[i];
-      co[i] = no[i];
+      ca[i] = na[i];
       cc[i] = nc[i];
       ccp[i] = ncp[i];
     }
@@ -959,8 +1116,12 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       float dhv = dh[i];
       if (t < T - 1)
         dhv = (part[cur ^ 1][0][j][lane] + part[cur ^ 1][1][j][lane]) + (part[cur ^ 1][2][j][lane] + part[cur ^ 1][3][j][lane]);
+      if (i == 0) {
+        LUSE(dhv);
+        LSUBB(1);
+      }
       if (decoder) dhv = fmaf(wp0[i], d0, fmaf(wp1[i], d1, dhv));
-      const float ig = ci[i], fg = cf[i], gg = cg[i], og = co[i];
+      const float ig = ca[i][0], fg = ca[i][1], gg = ca[i][2], og = ca[i][3];
       const float tc = tanh_m(cc[i]);
       if (pgrad) {   // h_{t+1} of the slot = o_t tanh(c_t)
         const float hn = og * tc;
@@ -1017,13 +1178,17 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       f1 += __shfl_xor(f1, 32);
       if (q == 0) fbp[cur][g][c16] = make_float2(f0, f1);
     }
+    LUSE(acc[MU - 1][0]);
+    LSUBB(2);
     // this wave's share of dh_{t-1}: D row 4 q + r of tile mu is unit
     // slot_unit(4 mu + r, q), i.e. slot 4 mu + r of the next step's owners
 #pragma unroll
     for (int mu = 0; mu < MU; ++mu)
 #pragma unroll
       for (int r = 0; r < 4; ++r) part[cur][g][4 * mu + r][lane] = acc[mu][r];
+    LSUBB(3);
     lds_barrier();
+    LSUBB(4);
     if (!hacc && (pgrad || (g == 0 && q == 0))) {   // drel_in[t] = A^T dG_t; decoder: drel_tot[t] = dout[t] + drel_in[t + 1]
       const float2 r0 = fbp[cur][0][c16], r1 = fbp[cur][1][c16], r2 = fbp[cur][2][c16], r3 = fbp[cur][3][c16];
       const float sx = (r0.x + r1.x) + (r2.x + r3.x), sy = (r0.y + r1.y) + (r2.y + r3.y);

@@ -176,8 +176,14 @@ __device__ __forceinline__ float bf16_trunc(float x) { return __uint_as_float(__
 __device__ __forceinline__ unsigned bf16_pack_top(float a, float b) {
   return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
 }
-// the pieces of x as fp32 values whose low 16 bits are zero
+// the pieces of x as fp32 values whose low 16 bits are zero.  No FMA
+// contraction here: with x = a * b inlined from the caller, -ffp-contract=fast
+// would form x - h as fma(a, b, -h) from the UNROUNDED product, so the pieces
+// would sum to a * b rather than to the fp32 value x that the caller stores --
+// and a recurrence restarted from the stored x (a segment from step t0)
+// would see other pieces than the one that continued in registers
 __device__ __forceinline__ void split3(float x, float& h, float& m, float& l) {
+#pragma clang fp contract(off)
   h = bf16_trunc(x);
   const float r = x - h;
   m = bf16_trunc(r);

@@ -7,7 +7,7 @@
 #include "../group-gan-gcn-gat_amd/csrc/lstm_mw.hip"
 #include "../group-gan-gcn-gat_amd/csrc/runtime.hip"
 #ifndef SGG_LSTM_PROF
-namespace sgg { __device__ long long g_lstm_prof[64]; }
+namespace sgg { __device__ long long g_lstm_prof[256]; }
 #endif
 
 #include <cstdio>
@@ -61,12 +61,20 @@ int main(int argc, char** argv) {
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
-  long long pr[64];
+  long long pr[256];
   CK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(sgg::g_lstm_prof), sizeof pr));
   printf("bwd B=%d T=%d: %.2f us/launch; workgroup 0 owner wave 0 (us from entry):\n", B, T, ms * 1e3 / 50);
   printf("  prologue %.2f\n", (pr[1] - pr[0]) * 0.01);
   for (int s = 0; s < T && s < 60; ++s) printf("  step %2d %.2f (+%.2f)\n", T - 1 - s, (pr[s + 2] - pr[0]) * 0.01,
                                                (pr[s + 2] - (s ? pr[s + 1] : pr[1])) * 0.01);
   printf("  end %.2f (+%.2f)\n", (pr[62] - pr[0]) * 0.01, (pr[62] - pr[T + 1]) * 0.01);
+  printf("  step %d sub-phases (us after its start mark; owners: start, dh read, MFMAs done, part written, barrier; "
+         "helpers: barrier, dW MFMAs, sums, staged):\n", T - 5);
+  const long long b0 = pr[2 + 4];
+  for (int w = 0; w < 8; ++w) {
+    printf("   wave %d", w);
+    for (int k = 0; k < (w < 4 ? 5 : 4); ++k) printf(" %6.3f", (pr[96 + 8 * w + k] - b0) * 0.01);
+    printf("\n");
+  }
   return 0;
 }

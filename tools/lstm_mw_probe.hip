@@ -7,7 +7,7 @@
 #include "../group-gan-gcn-gat_amd/csrc/lstm_mw.hip"
 #include "../group-gan-gcn-gat_amd/csrc/runtime.hip"
 #ifndef SGG_LSTM_PROF
-namespace sgg { __device__ long long g_lstm_prof[64]; }   // (the un-instrumented build: launch times only)
+namespace sgg { __device__ long long g_lstm_prof[256]; }   // (the un-instrumented build: launch times only)
 #endif
 
 #include <cstdio>
@@ -53,12 +53,21 @@ int main(int argc, char** argv) {
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
-  long long pr[64];
+  long long pr[256];
   CK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(sgg::g_lstm_prof), sizeof pr));
   printf("B=%d T=%d U=%d save=%d: %.2f us/launch; workgroup 0 (us from entry):\n", B, T, withu, save, ms * 1e3 / 50);
   printf("  staged %.2f\n", (pr[1] - pr[0]) * 0.01);
   for (int t = 0; t < T && t < 60; ++t) printf("  step %2d %.2f (+%.2f)\n", t, (pr[t + 2] - pr[0]) * 0.01,
                                               (pr[t + 2] - (t ? pr[t + 1] : pr[1])) * 0.01);
   printf("  end %.2f (+%.2f)\n", (pr[63] - pr[0]) * 0.01, (pr[63] - pr[T + 1]) * 0.01);
+  if (T > 4) {
+    printf("  step 4 sub-phases (us after step 3's mark; wave: start, B loaded, MFMAs done, activations, h written, "
+           "barrier passed):\n");
+    for (int w = 0; w < 4; ++w) {
+      printf("   wave %d", w);
+      for (int k = 0; k < 6; ++k) printf(" %6.3f", (pr[64 + 8 * w + k] - pr[5]) * 0.01);
+      printf("\n");
+    }
+  }
   return 0;
 }
