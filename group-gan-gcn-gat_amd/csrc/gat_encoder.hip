@@ -562,6 +562,9 @@ __device__ __forceinline__ float wmax(float v) {
 // 4], B[k = lane >> 4][j = lane & 15]; the D lane holds rows 4 (lane >> 4) + r,
 // column lane & 15.  Rows / columns past the edge read a clamped (valid)
 // element and are not stored; a reduction over rows masks them to zero.
+// k-steps per operand batch of lin / lin_t / wgrad (template NB): the forward
+// kernel batches 4 (its 1024-thread workgroups leave it registers); the
+// backward sits at the 128-VGPR cap and keeps the plain loop (NB = 1)
 __device__ __forceinline__ int mm_wave(int first) {
   const int nw = blockDim.x >> 6;
   return ((int)(threadIdx.x >> 6) + nw - first % nw) % nw;
@@ -571,6 +574,7 @@ __device__ __forceinline__ int mm_wave(int first) {
 // With a (2N: a_src | a_dst), also the attention score partials of the tile:
 // sp[tile column][r] = sum over its 16 columns of out[r][c] a[c], tp the same
 // with a[N + c] (att_rows sums the column tiles).
+template <int kMmB = 1>
 __device__ __forceinline__ void lin(const float* in, int ldi, int rows, int K, const float* W, int ldw, int N, float* out, int ldo,
                     int first = 0, const float* a = nullptr, float* sp = nullptr, float* tp = nullptr, int np = 0) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
@@ -580,8 +584,24 @@ __device__ __forceinline__ void lin(const float* in, int ldi, int rows, int K, c
     const float* pa = in + min(r0 + i, rows - 1) * ldi + kq;
     const float* pb = W + kq * ldw + min(c0 + i, N - 1);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    // batches of kMmB k-steps: the batch's LDS operands are read before its
+    // MFMAs (one LDS latency per batch, not per k-step); k-steps past K
+    // multiply zeros (the sum is unchanged, bit for bit)
+    if constexpr (kMmB == 1) {
 #pragma unroll 2
-    for (int k = 0; k < K; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k], pb[k * ldw], acc, 0, 0, 0);
+      for (int k = 0; k < K; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k], pb[k * ldw], acc, 0, 0, 0);
+    } else
+    for (int k = 0; k < K; k += 4 * kMmB) {
+      float av[kMmB], bv[kMmB];
+#pragma unroll
+      for (int u = 0; u < kMmB; ++u) {
+        const int kk = min(k + 4 * u, K - 4);
+        av[u] = k + 4 * u < K ? pa[kk] : 0.f;
+        bv[u] = k + 4 * u < K ? pb[kk * ldw] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kMmB; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    }
     const int col = c0 + i;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -606,6 +626,7 @@ __device__ __forceinline__ void lin(const float* in, int ldi, int rows, int K, c
 // out[r][k] (+)= sum_c d[r][c] W[k][c]   (input gradient of lin; N % 4 == 0;
 // out may be global memory)
 // (out2: columns >= ksplit go to out2 at pitch ldo2 instead)
+template <int kMmB = 1>
 __device__ __forceinline__ void lin_t(const float* d, int ldd, int rows, int N, const float* W, int ldw, int K, float* out, int ldo,
                       bool accum, int first = 0, float* out2 = nullptr, int ldo2 = 0, int ksplit = 0) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
@@ -615,8 +636,21 @@ __device__ __forceinline__ void lin_t(const float* d, int ldd, int rows, int N, 
     const float* pa = d + min(r0 + i, rows - 1) * ldd + kq;
     const float* pb = W + min(k0 + i, K - 1) * ldw + kq;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (kMmB == 1) {
 #pragma unroll 2
-    for (int c = 0; c < N; c += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[c], pb[c], acc, 0, 0, 0);
+      for (int c = 0; c < N; c += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[c], pb[c], acc, 0, 0, 0);
+    } else
+    for (int c = 0; c < N; c += 4 * kMmB) {   // batched as in lin
+      float av[kMmB], bv[kMmB];
+#pragma unroll
+      for (int u = 0; u < kMmB; ++u) {
+        const int cc = min(c + 4 * u, N - 4);
+        av[u] = c + 4 * u < N ? pa[cc] : 0.f;
+        bv[u] = c + 4 * u < N ? pb[cc] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kMmB; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    }
     const int col = k0 + i;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -631,6 +665,7 @@ __device__ __forceinline__ void lin_t(const float* d, int ldd, int rows, int N, 
 
 // dst[k][c] = sum_r x[r][k] d[r][c]  (weight gradient of lin: to the slab,
 // ldo = N; or an LDS image)
+template <int kMmB = 1>
 __device__ __forceinline__ void wgrad(const float* x, int ldx, int rows, int K, const float* d, int ldd, int N, float* dst, int ldo,
                       int first = 0) {
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, i = lane & 15, kq = lane >> 4;
@@ -640,10 +675,26 @@ __device__ __forceinline__ void wgrad(const float* x, int ldx, int rows, int K, 
     const float* pa = x + min(k0 + i, K - 1);
     const float* pb = d + min(c0 + i, N - 1);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int r = kq; r < rows + kq; r += 4) {   // the lane's row r; the step covers rows r - kq .. r - kq + 3
-      const bool ok = r < rows;
-      const float av = ok ? pa[r * ldx] : 0.f, bv = ok ? pb[r * ldd] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    // the lane's row r; a step covers rows r - kq .. r - kq + 3; batched as in lin
+    if constexpr (kMmB == 1) {
+      for (int r = kq; r < rows + kq; r += 4) {
+        const bool ok = r < rows;
+        const float av = ok ? pa[r * ldx] : 0.f, bv = ok ? pb[r * ldd] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+      }
+    } else
+    for (int r = kq; r < rows + kq; r += 4 * kMmB) {
+      float av[kMmB], bv[kMmB];
+#pragma unroll
+      for (int u = 0; u < kMmB; ++u) {
+        const int rr = r + 4 * u;
+        const bool ok = rr < rows;
+        av[u] = ok ? pa[rr * ldx] : 0.f;
+        bv[u] = ok ? pb[rr * ldd] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kMmB; ++u)
+        if (r + 4 * u < rows + kq) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
     }
     const int col = c0 + i;
 #pragma unroll
@@ -901,13 +952,20 @@ __device__ __forceinline__ void att_bwd(const float* Wh, int ldw, int rows, int 
     for (int f = lane; f < F; f += 64) dWh[j * lddw + f] += dsj * a[f] + dtj * a[F + f];
   }
   lds_barrier(); AMARK(3);
-  // da[f] = sum_i ds_i Wh_i[f], da[F + f] = sum_j dt_j Wh_j[f]
+  // da[f] = sum_i ds_i Wh_i[f], da[F + f] = sum_j dt_j Wh_j[f]: four
+  // interleaved partial sums per output (one chain over the rows waited an
+  // LDS latency per row: ~1 us at F = 72, 20 rows)
   for (int e = threadIdx.x; e < 2 * F; e += blockDim.x) {
     const int w = e / F, f = e - w * F;
     const float* g = w ? dt : ds;
-    float acc = 0.f;
-    for (int r = 0; r < rows; ++r) acc = fmaf(g[r], Wh[r * ldw + f], acc);
-    da[e] = acc;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int r = 0;
+    for (; r + 4 <= rows; r += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = fmaf(g[r + u], Wh[(r + u) * ldw + f], acc[u]);
+    }
+    for (; r < rows; ++r) acc[0] = fmaf(g[r], Wh[r * ldw + f], acc[0]);
+    da[e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
   AMARK(4);
 #undef AMARK
@@ -1175,7 +1233,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
     if (!BWD || !saved) {
       // ---- intra GAT: heads (40 -> 72, ELU), out (72 nh -> 16, ELU, log_softmax)
       for (int h = 0; h < nh; ++h) {   // per-head offsets are strides (no indexed arrays)
-        lin(X, P40, n, FI, (lw.Wi[0] + h * SEGI), PW72, FH, Wh, P72, 0, (lw.ai[0] + h * SEGI), sp, tp, NP);
+        lin<BWD ? 1 : 4>(X, P40, n, FI, (lw.Wi[0] + h * SEGI), PW72, FH, Wh, P72, 0, (lw.ai[0] + h * SEGI), sp, tp, NP);
         lds_barrier(); PMARK(3);
         att_rows(n, kScoreTiles, sp, tp, NP, gidl, p.alpha, s, t, attm, NPP, saved ? saved + (SL.sti[0] + h * SLH) : nullptr);
         if (saved) rows_to_global(saved + (SL.Whi[0] + h * SLH), Wh, P72, n, FH);
@@ -1183,7 +1241,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         att_agg(attm, NPP, n, Wh, P72, FH, 1, H1 + h * FH, PH, nullptr, 0);
         lds_barrier(); PMARK(5);
       }
-      lin(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72, 0, lw.aio, sp, tp, NP);
+      lin<BWD ? 1 : 4>(H1, PH, n, FH * nh, lw.Wio, PW16, FO, Wh, P72, 0, lw.aio, sp, tp, NP);
       lds_barrier(); PMARK(6);
       att_rows(n, 1, sp, tp, NP, gidl, p.alpha, s, t, attm, NPP, saved ? saved + SL.stio : nullptr);
       if (saved) rows_to_global(saved + SL.Whio, Wh, P72, n, FO);
@@ -1205,7 +1263,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
       lds_barrier(); PMARK(9);
       // ---- inter GAT on the complete graph of the M groups ----------------
       for (int h = 0; h < nh; ++h) {   // per-head offsets are strides (no indexed arrays)
-        lin(gin, P16, M, FO, (lw.Wg[0] + h * SEGG), PW72, FH, Wh, P72, 0, (lw.ag[0] + h * SEGG), sp, tp, NP);
+        lin<BWD ? 1 : 4>(gin, P16, M, FO, (lw.Wg[0] + h * SEGG), PW72, FH, Wh, P72, 0, (lw.ag[0] + h * SEGG), sp, tp, NP);
         lds_barrier(); PMARK(10);
         att_rows(M, kScoreTiles, sp, tp, NP, nullptr, p.alpha, s, t, attm, NPP, saved ? saved + (SL.stg[0] + h * SLH) : nullptr);
         if (saved) rows_to_global(saved + (SL.Whg[0] + h * SLH), Wh, P72, M, FH);
@@ -1213,7 +1271,7 @@ __global__ void __launch_bounds__(BWD ? kBwdThreads : kFwdThreads) gatenc_kernel
         att_agg(attm, NPP, M, Wh, P72, FH, 1, G1 + h * FH, PH, nullptr, 0);
         lds_barrier(); PMARK(12);
       }
-      lin(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72, 0, lw.ago, sp, tp, NP);
+      lin<BWD ? 1 : 4>(G1, PH, M, FH * nh, lw.Wgo, PW16, FO, Wh, P72, 0, lw.ago, sp, tp, NP);
       lds_barrier(); PMARK(13);
       att_rows(M, 1, sp, tp, NP, nullptr, p.alpha, s, t, attm, NPP, saved ? saved + SL.stgo : nullptr);
       if (saved) rows_to_global(saved + SL.Whgo, Wh, P72, M, FO);
