@@ -235,7 +235,7 @@ def roofline_of(name, a):
         w1, w2 = max(fl / fpeak / 1e3, by / HBM_PEAK_GBS), max(r2["flop"] / fpeak / 1e3, r2["bytes"] / HBM_PEAK_GBS)
         if k2 != key and w2 <= w1 * 2.0 / 3.0 and r2["ms"] * 1e3 > 0.8 * us:
             evidence = "%s %s: %.2fx the work in %.2fx the time" % (name, list(k2[1:]), w2 / w1, r2["ms"] * 1e3 / us)
-    latency = us * 1e-6 > 4.0 * t_roof and (steps is not None or evidence is not None)
+    latency = us * 1e-6 > 2.0 * t_roof and (steps is not None or evidence is not None)
     if t_f >= t_b:
         achieved, peak, unit = fl / (us * 1e-6) / 1e12, fpeak, "TFLOP/s"
     else:
