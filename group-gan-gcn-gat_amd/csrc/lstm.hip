@@ -286,7 +286,8 @@ extern "C" const char* sgg_lstm_kernel_name(int H, int B, int decoder, int save,
   else if (!save && lstm_fwd_mfma_ok(H, B) && !getenv("SGG_LSTM_NO_MFMA")) {
     // (lstm_mfma.hip: the split-bf16 gate GEMM for H = 32 unless SGG_LSTM_X3=0)
     const char* x3e = getenv("SGG_LSTM_X3");
-    snprintf(buf, sizeof buf, "sgg::lstm_fwd_mfma_kernel<%d, %s>", H, tf[H == 32 && !(x3e && strcmp(x3e, "0") == 0)]);
+    const bool x3 = H == 32 && !(x3e && strcmp(x3e, "0") == 0);
+    snprintf(buf, sizeof buf, "sgg::lstm_fwd_mfma_kernel<%d, %s, %s>", H, tf[x3], tf[decoder != 0]);
   }
   else if (mw) snprintf(buf, sizeof buf, "sgg::lstm_mw_fwd_kernel<%d, %s, %s>", H, tf[decoder != 0], tf[save != 0]);
   else if (H <= 32) snprintf(buf, sizeof buf, "sgg::lstm_unit_fwd_kernel<%d>", H);

@@ -16,7 +16,8 @@
 // The k order of the next step's GEMM is permuted so that k-step ks, lane q
 // supplies unit 16 (ks >> 2) + 4q + (ks & 3) -- exactly the h value that lane
 // just produced (h[ks]); W_ext's columns are loaded into registers in the
-// same permuted order once.  No LDS, no barriers: waves are independent.
+// same permuted order once (staged through LDS by the workgroup, one barrier
+// in the prologue); the steps need no LDS and no barriers.
 // Decoder: rel_t = Wp h_t + bp is a lane partial over its H/4 units plus two
 // cross-q shuffles, and feeds the next step's input k-step in registers.
 #include <stdlib.h>
@@ -128,15 +129,37 @@ __device__ __forceinline__ void cell2(float2v yi, float2v yf, float2v yg, float2
 // (H = 32: two waves per SIMD, pinned -- the build's -amdgpu-mfma-vgpr-form
 // keeps the accumulators in VGPRs (227); without that flag the allocator
 // parks them in 64 AGPRs, 292 registers in all, one wave per SIMD)
+// phase probe (tools/lstm_roll_probe.hip builds its own copy with
+// SGG_ROLL_PROF): wall-clock marks per step of workgroups 0 and 300, shader
+// cycle marks of step 4's phases; nothing in the library build
+#ifdef SGG_ROLL_PROF
+__device__ long long g_roll_prof[8192 + 512];
+#define RMARK(t)                                                                                      \
+  if (threadIdx.x == 0 && blockIdx.x < 512 && (t) < 16) g_roll_prof[16 * blockIdx.x + (t)] = wall_clock64();
+#define RSUB(k)                                                                                       \
+  if ((threadIdx.x & 63) == 0 && (blockIdx.x == 0 || blockIdx.x == 300) && t == 4)                   \
+    g_roll_prof[8192 + (blockIdx.x ? 64 : 0) + 8 * (threadIdx.x >> 6) + (k)] = clock64();
+#define RUSE(x) __asm__ volatile("" ::"v"(x));
+#else
+#define RMARK(t)
+#define RSUB(k)
+#define RUSE(x)
+#endif
+
 #ifndef SGG_ROLL_WPE
 #define SGG_ROLL_WPE 2
 #endif
-template <int H, bool X3>
+// (DEC a template parameter: with one step loop for both forms, the encoder's
+// prefetch load made the compiler wait vmcnt(0) at the loop's back edge --
+// and on gfx9 vmcnt counts stores too, so every decoder step waited for the
+// acknowledgement of its own output stores)
+template <int H, bool X3, bool DEC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 32 ? SGG_ROLL_WPE : 1))) lstm_fwd_mfma_kernel(
     const float* __restrict__ rel, const float* __restrict__ A, const float* __restrict__ Whh,
     const float* __restrict__ bias, const float* __restrict__ h0, const float* __restrict__ c0,
-    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B1, int decoder,
+    const float* __restrict__ Wp, const float* __restrict__ bp, int T, int B1,
     float* __restrict__ h_all, float* __restrict__ c_all, float* __restrict__ rel_out1, SggDecInit di1, RollSeg2 s2) {
+  constexpr bool decoder = DEC;
   constexpr int G4 = 4 * H;
   constexpr int MT = G4 / 16;     // gate-row tiles
   constexpr int MU = H / 16;      // unit tiles (i/f/g/o blocks are MU tiles apart)
@@ -156,21 +179,68 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
   const SggTrajOut& to = s2.to;
   const int tcol = ped - to.col0;
   const bool tlive = two && valid && to.out != nullptr && tcol >= 0 && tcol < to.ncol;
-  if (tlive && q == 0) {
+  // (entries e = T0 head steps, T b steps, the start: the ped's four q lanes
+  // take every fourth, all loads of a chunk in flight before its stores -- a
+  // load-store loop per entry was a memory round trip each, ~20 in a row
+  // before these workgroups' first step)
+  if (tlive) {
     float2* o2 = reinterpret_cast<float2*>(to.out);
-    const int dup = to.b ? 2 : 1;
-    for (int t = 0; t < to.T0; ++t) {
-      const float2 v = reinterpret_cast<const float2*>(to.head + (size_t)t * to.ldh)[tcol];
-      for (int hf = 0; hf < dup; ++hf) o2[(size_t)t * to.NB + tcol + hf * to.ncol] = v;
-    }
-    if (to.b)
-      for (int t = 0; t < T; ++t)
-        o2[(size_t)(to.T0 + t) * to.NB + to.ncol + tcol] = reinterpret_cast<const float2*>(to.b + (size_t)t * to.ldb)[tcol];
-    if (to.start) {
-      const float2 p0 = reinterpret_cast<const float2*>(to.pos0)[tcol];
-      for (int hf = 0; hf < dup; ++hf) reinterpret_cast<float2*>(to.start)[tcol + hf * to.ncol] = p0;
+    const int dup = to.b ? 2 : 1;   // (SggTrajOut: b != NULL <-> NB = 2 ncol)
+    const int nh = to.T0, nb = to.b ? T : 0, n = nh + nb + (to.start ? 1 : 0);
+    constexpr int kJ = 8;
+    for (int base = 0; base < n; base += 4 * kJ) {
+      float2 v[kJ];
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const int e = base + 4 * j + q;
+        const float2* src = e < nh ? reinterpret_cast<const float2*>(to.head + (size_t)e * to.ldh)
+                            : e < nh + nb ? reinterpret_cast<const float2*>(to.b + (size_t)(e - nh) * to.ldb)
+                            : e < n       ? reinterpret_cast<const float2*>(to.pos0)
+                                          : reinterpret_cast<const float2*>(to.head);
+        v[j] = src[tcol];
+      }
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const int e = base + 4 * j + q;
+        float2* dst = e < nh ? o2 + (size_t)e * to.NB + tcol
+                      : e < nh + nb ? o2 + (size_t)(to.T0 + e - nh) * to.NB + to.ncol + tcol
+                                    : reinterpret_cast<float2*>(to.start) + tcol;
+        if (e < n) dst[0] = v[j];
+        if (e < n && dup == 2 && (e < nh || e >= nh + nb)) dst[to.ncol] = v[j];   // (the head / start copy of the b half)
+      }
     }
   }
+
+  RMARK(15);   // (probe: workgroup start)
+  // the weights through LDS, once per workgroup: coalesced 16-byte loads
+  // (read per lane they were ~50 row gathers of 16 cache lines each per wave,
+  // with every workgroup of the launch in its prologue at once -- the first
+  // step of a late workgroup took ~9 us, tools/lstm_roll_probe.hip)
+  constexpr int WP = H + 4;   // row pitch: the lanes' 16-byte reads of 16 rows spread over the banks
+  __shared__ __attribute__((aligned(16))) float sW[G4 * WP];
+  __shared__ __attribute__((aligned(16))) float sA[2 * G4];
+  __shared__ __attribute__((aligned(16))) float sBias[G4];
+  __shared__ float sWp[2 * H];
+  {
+    const bool al = ((reinterpret_cast<uintptr_t>(Whh) | reinterpret_cast<uintptr_t>(A) |
+                      reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
+    if (al) {
+      for (int e = threadIdx.x; e < G4 * H / 4; e += 256) {
+        const int r = e / (H / 4), c4 = e - r * (H / 4);
+        *reinterpret_cast<float4*>(&sW[r * WP + 4 * c4]) = reinterpret_cast<const float4*>(Whh)[e];
+      }
+      for (int e = threadIdx.x; e < G4 / 2; e += 256) reinterpret_cast<float4*>(sA)[e] = reinterpret_cast<const float4*>(A)[e];
+      for (int e = threadIdx.x; e < G4 / 4; e += 256)
+        reinterpret_cast<float4*>(sBias)[e] = reinterpret_cast<const float4*>(bias)[e];
+    } else {
+      for (int e = threadIdx.x; e < G4 * H; e += 256) sW[(e / H) * WP + e % H] = Whh[e];
+      for (int e = threadIdx.x; e < 2 * G4; e += 256) sA[e] = A[e];
+      for (int e = threadIdx.x; e < G4; e += 256) sBias[e] = bias[e];
+    }
+    if (decoder)
+      for (int e = threadIdx.x; e < 2 * H; e += 256) sWp[e] = Wp[e];
+  }
+  __syncthreads();
 
   // the lane's k-step units (k = 4 mu + r  <->  unit 16 mu + 4q + r, the
   // permuted k order) and the decoder's Wp columns of them
@@ -178,8 +248,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
 #pragma unroll
   for (int k = 0; k < NU; ++k) {
     const int u = 16 * (k >> 2) + 4 * q + (k & 3);
-    wp0[k] = decoder ? Wp[u] : 0.f;
-    wp1[k] = decoder ? Wp[H + u] : 0.f;
+    wp0[k] = decoder ? sWp[u] : 0.f;
+    wp1[k] = decoder ? sWp[H + u] : 0.f;
   }
   const float bp0 = decoder ? bp[0] : 0.f, bp1 = decoder ? bp[1] : 0.f;
   // W' (or W_hh) in registers, columns in the permuted k order; the input
@@ -195,11 +265,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
     const int row = 16 * mt + c16;
     // gate of tile mt: i, f, g, o blocks of MU tiles; g (tanh) takes -2 log2(e)
     const float sc = (mt / MU == 2 ? 2.f : 1.f) * kNegLog2e;
-    const float ax = A[2 * row], ay = A[2 * row + 1];
+    const float ax = sA[2 * row], ay = sA[2 * row + 1];
     float wk[KSH];
 #pragma unroll
     for (int ks = 0; ks < KSH; ++ks) {
-      const float wv = Whh[row * H + 16 * (ks >> 2) + 4 * q + (ks & 3)];
+      const float wv = sW[row * WP + 16 * (ks >> 2) + 4 * q + (ks & 3)];
       wk[ks] = sc * (decoder ? fmaf(ay, wp1[ks], fmaf(ax, wp0[ks], wv)) : wv);
     }
     if constexpr (X3) {
@@ -214,8 +284,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
       // (A loaded unconditionally: under the runtime `decoder` branch each
       // entry's load was followed by its own vmcnt(0) -- 4 MT round trips)
       const int brow = 16 * mt + 4 * q + r;
-      const float bv = bias[brow];
-      const float bd = fmaf(A[2 * brow + 1], bp1, fmaf(A[2 * brow], bp0, bv));
+      const float bv = sBias[brow];
+      const float bd = fmaf(sA[2 * brow + 1], bp1, fmaf(sA[2 * brow], bp0, bv));
       b0[mt][r] = sc * (decoder ? bd : bv);
     }
   }
@@ -258,7 +328,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
     xin = q == 0 ? xin - px : q == 1 ? xin - py : 0.f;
   }
 
+  RMARK(0);
   for (int t = 0; t < T; ++t) {
+    RSUB(0);
     const float xnext = (!decoder && t + 1 < T) ? load_in(t + 1) : 0.f;   // prefetch
     floatx4 acc[MT];
     if constexpr (X3) {
@@ -266,8 +338,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
       const float hv[8] = {h[0].x, h[0].y, h[1].x, h[1].y, h[2].x, h[2].y, h[3].x, h[3].y};
       bf16x8 hb[3];
       split8(hv, hb);
+      RUSE(hb[2]);
+      RSUB(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_x3(wb[mt], hb, b0[mt]);
+      RUSE(acc[MT - 1]);
+      RSUB(2);
     } else {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -304,6 +380,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
         *reinterpret_cast<float4*>(c_all + o) = make_float4(c[2 * mu].x, c[2 * mu].y, c[2 * mu + 1].x, c[2 * mu + 1].y);
       }
     }
+    RUSE(h[NU / 2 - 1]);
+    RSUB(3);
     if (decoder) {   // rel_t = Wp h_t + bp: sum the 4 q-lanes of the ped
       px = rows_sum(px) + bp0;
       py = rows_sum(py) + bp1;
@@ -313,6 +391,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H <= 3
     } else {
       xin = xnext;
     }
+    RSUB(4);
+    RMARK(t + 1);
   }
 }
 
@@ -320,13 +400,6 @@ template <int H>
 int launch(const float* rel, const float* A, const float* Whh, const float* bias, const float* h0, const float* c0,
            const float* Wp, const float* bp, int T, int B, int decoder, float* h_all, float* c_all, float* act_all,
            float* rel_out, hipStream_t st, const SggDecInit* di, const RollSeg2* seg2 = nullptr) {
-  const int grid = (B + 63) / 64;
-  SggDecInit d = {};
-  if (di) d = *di;
-  RollSeg2 s2 = {};
-  if (seg2) s2 = *seg2;
-  s2.nblk1 = grid;
-  const int grid2 = s2.B > 0 ? (s2.B + 63) / 64 : 0;
   if (act_all) {   // (the dispatch never sends saved-state forwards here)
     sgg::set_error("sgg_lstm_fwd: the batch-MFMA rollout keeps no saved states");
     return SGG_E_ARG;
@@ -335,9 +408,17 @@ int launch(const float* rel, const float* A, const float* Whh, const float* bias
   const char* x3e = getenv("SGG_LSTM_X3");
   const bool x3 = H == 32 && !(x3e && strcmp(x3e, "0") == 0);
   constexpr bool kX3 = H == 32;
-  auto kfn = x3 ? lstm_fwd_mfma_kernel<H, kX3> : lstm_fwd_mfma_kernel<H, false>;
-  hipLaunchKernelGGL(kfn, dim3(grid + grid2), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B, decoder, h_all,
-                     c_all, rel_out, d, s2);
+  const int grid = (B + 63) / 64;
+  SggDecInit d = {};
+  if (di) d = *di;
+  RollSeg2 s2 = {};
+  if (seg2) s2 = *seg2;
+  s2.nblk1 = grid;
+  const int grid2 = s2.B > 0 ? (s2.B + 63) / 64 : 0;
+  auto kfn = decoder ? (x3 ? lstm_fwd_mfma_kernel<H, kX3, true> : lstm_fwd_mfma_kernel<H, false, true>)
+                     : (x3 ? lstm_fwd_mfma_kernel<H, kX3, false> : lstm_fwd_mfma_kernel<H, false, false>);
+  hipLaunchKernelGGL(kfn, dim3(grid + grid2), dim3(256), 0, st, rel, A, Whh, bias, h0, c0, Wp, bp, T, B, h_all, c_all,
+                     rel_out, d, s2);
   SGG_RETURN_LAUNCH("sgg_lstm_fwd");
 }
 

@@ -102,6 +102,11 @@ __attribute__((amdgpu_waves_per_eu(BN == 8 && GPW == 1 ? 5 : 1))) pool_fwd_kerne
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
+  // b2 of the lane's columns, loaded once: read in the epilogue's guarded
+  // branches each load was a memory round trip of its own (NT x 4 x GPW per chunk)
+  float bv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bv[t] = b2[min(16 * t + c16, BN - 1)];
 
   // XCD-aware chunk order: the grid is a multiple of 8 and blocks b, b + 8,
   // b + 16, ... share an XCD (round-robin dispatch; speed only, never
@@ -232,7 +237,7 @@ __attribute__((amdgpu_waves_per_eu(BN == 8 && GPW == 1 ? 5 : 1))) pool_fwd_kerne
           for (int t = 0; t < NT; ++t) {
             const int cc = 16 * t + c16;
             if (cc < BN) {
-              float v = acc[g][t][r] + b2[cc];
+              float v = acc[g][t][r] + bv[t];
               v = v > 0.f ? v : 0.f;
               atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
             }
@@ -277,6 +282,11 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
+  // b2 of the lane's columns, loaded once: read in the epilogue's guarded
+  // branches each load was a memory round trip of its own (NT x 4 x GPW per chunk)
+  float bv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bv[t] = b2[min(16 * t + c16, BN - 1)];
 
   SGG_POOL_PICK(s1, s2, g1);
   for (int ch = xb; ch < nch; ch += gstride) {
@@ -442,7 +452,7 @@ __global__ void __launch_bounds__(256) pool_fwd_v_kernel(
           for (int t = 0; t < NT; ++t) {
             const int cc = 16 * t + c16;
             if (cc < BN) {
-              float v = acc[g][t][r] + b2[cc];
+              float v = acc[g][t][r] + bv[t];
               v = v > 0.f ? v : 0.f;
               atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
             }
@@ -499,6 +509,11 @@ __global__ void __launch_bounds__(256, 2) pool_fwd_x3_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
+  // b2 of the lane's columns, loaded once: read in the epilogue's guarded
+  // branches each load was a memory round trip of its own (NT x 4 x GPW per chunk)
+  float bv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bv[t] = b2[min(16 * t + c16, BN - 1)];
 
   SGG_POOL_PICK(s1, s2, g1);
   for (int ch = xb; ch < nch; ch += gstride) {
@@ -662,7 +677,7 @@ __global__ void __launch_bounds__(256, 2) pool_fwd_x3_kernel(
           for (int t = 0; t < NT; ++t) {
             const int cc = 16 * t + c16;
             if (cc < BN) {
-              float v = acc[g][t][r] + b2[cc];
+              float v = acc[g][t][r] + bv[t];
               v = v > 0.f ? v : 0.f;
               atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
             }
@@ -735,6 +750,11 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
+  // b2 of the lane's columns, loaded once: read in the epilogue's guarded
+  // branches each load was a memory round trip of its own (NT x 4 x GPW per chunk)
+  float bv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bv[t] = b2[min(16 * t + c16, BN - 1)];
 
   // W2 (rounded to bf16; rows >= BN zero) and A, once per workgroup
   for (int q = tid; q < 16 * NT * (kHidden / 4); q += kBfThreads) {
@@ -907,7 +927,7 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_kernel(
             for (int t = 0; t < NT; ++t) {
               const int cc = 16 * t + c16;
               if (cc < BN) {
-                float v = acc[g][t][r] + b2[cc];
+                float v = acc[g][t][r] + bv[t];
                 v = v > 0.f ? v : 0.f;
                 atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
               }
@@ -985,6 +1005,11 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_jb_kernel(
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
+  // b2 of the lane's columns, loaded once: read in the epilogue's guarded
+  // branches each load was a memory round trip of its own (NT x 4 x GPW per chunk)
+  float bv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bv[t] = b2[min(16 * t + c16, BN - 1)];
 
   // W2 (rounded to bf16; rows >= BN zero) and A, once per workgroup
   for (int q = tid; q < 16 * NT * (kHidden / 4); q += kBfThreads) {
@@ -1111,7 +1136,7 @@ __global__ void __launch_bounds__(kBfThreads) pool_fwd_bf16_jb_kernel(
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
               const int cc = 16 * t + c16;
-              const float bb = cc < BN ? b2[cc] : 0.f;
+              const float bb = cc < BN ? bv[t] : 0.f;
               unsigned long long best = 0ull;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
@@ -1199,6 +1224,11 @@ __global__ void __launch_bounds__(256) pool_fwd_res_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kq = lane >> 4;
+  // b2 of the lane's columns, loaded once: read in the epilogue's guarded
+  // branches each load was a memory round trip of its own (NT x 4 x GPW per chunk)
+  float bv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bv[t] = b2[min(16 * t + c16, BN - 1)];
 
   stage_rows512(W2s, W2, 16 * NT, BN);
   for (int e = threadIdx.x; e < 2 * kHidden; e += 256) As[e] = A[e];
@@ -1281,7 +1311,7 @@ __global__ void __launch_bounds__(256) pool_fwd_res_kernel(
           for (int t = 0; t < NT; ++t) {
             const int cc = 16 * t + c16;
             if (cc < BN) {
-              float v = acc[g][t][r] + b2[cc];
+              float v = acc[g][t][r] + bv[t];
               v = v > 0.f ? v : 0.f;
               atomicMax(&keys[il * BN + cc], ((unsigned long long)__float_as_uint(v) << 32) | jkey);
             }

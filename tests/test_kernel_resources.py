@@ -33,7 +33,7 @@ def test_no_kernel_uses_scratch():
     rows = KR.collect()
     names = [r["name"] for r in rows]
     # the hot kernels of round 4's verdict are among those checked
-    for must in ("pool_fwd_bf16_kernel<48, 4>", "gatenc_kernel<true, 1>", "lstm_fwd_mfma_kernel<32, true>",
+    for must in ("pool_fwd_bf16_kernel<48, 4>", "gatenc_kernel<true, 1>", "lstm_fwd_mfma_kernel<32, true, true>",
                  "pool_fwd_kernel<48, 4, 2>", "lstm_mw_bwd_kernel<48, false, true>", "pool_fwd_x3_kernel<48, 2>"):
         assert any(must in n for n in names), must
     bad = []
