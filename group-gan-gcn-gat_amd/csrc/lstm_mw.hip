@@ -57,6 +57,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "sgg_common.h"
 
 namespace sgg {
@@ -760,6 +762,9 @@ __global__ void __launch_bounds__(kMwThreads) lstm_mw_fwd3_kernel(MwSeg a, MwSeg
     mw_fwd_body<HC, false, SC>(c, blk - nblk_a - nblk_b);
 }
 
+#ifndef SGG_MW_BWD_DB
+#define SGG_MW_BWD_DB 1
+#endif
 #ifndef SGG_MW_BWD_X3
 #define SGG_MW_BWD_X3 1
 #endif
@@ -1042,28 +1047,50 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   // dwordx4 load's registers and the compiler moved two lanes of the FRESH
   // load right after issuing it -- a wait for a whole memory round trip at
   // the head of every step, ~1 us; tools/lstm_bwd_probe.hip)
-  floatx4 na[MU];
-  float nc[MU], ncp[MU], nd0 = 0.f, nd1 = 0.f, nr0 = 0.f, nr1 = 0.f;
-  auto load_step = [&](int t) {
+  // (the two-set form keeps the cells as one native vector each: as float
+  // arrays their copies were v_movs placed right after the fresh loads, and
+  // each step waited vmcnt(0) for its own prefetch before its barrier)
+  typedef float fvmu __attribute__((ext_vector_type(MU)));
+  struct FArr {   // the one-set form's cells: plain arrays (its measured code)
+    float v[MU];
+    __device__ float operator[](int i) const { return v[i]; }
+  };
+  constexpr bool kDB = SGG_MW_BWD_DB && !(WGRAD && !DEC);
+  typedef typename std::conditional<kDB, fvmu, FArr>::type CellV;
+  struct StepIn {
+    floatx4 a[MU];
+    CellV c, cp;
+    float d0, d1, r0, r1;
+  };
+  StepIn sa, sb;
+  sa.d0 = sa.d1 = sa.r0 = sa.r1 = sb.d0 = sb.d1 = sb.r0 = sb.r1 = 0.f;
+  auto load_step = [&](int t, StepIn& s) {
     if (wgrad) {   // r_in(t): rel[t] (encoder); rel0, then rel_out[t - 1] (decoder)
       const float* rp = !decoder ? rel + ((size_t)t * B + pc) * 2
                                  : (t == 0 ? rel + (size_t)pc * 2 : rel_out + ((size_t)(t - 1) * B + pc) * 2);
       const float2 rv = *reinterpret_cast<const float2*>(rp);
-      nr0 = rv.x;
-      nr1 = rv.y;
+      s.r0 = rv.x;
+      s.r1 = rv.y;
     }
     const float4* ab = reinterpret_cast<const float4*>(act_tile) + ((size_t)sblk(t < t_sh) * T + t) * KS * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < MU; ++i) na[i] = *reinterpret_cast<const floatx4*>(ab + (g * MU + i) * 64);
-    load_vec<MU>(c_tile + ((((size_t)sblk(t + 1 <= t_sh) * (T + 1) + t + 1) * 4 + g) * 64 + lane) * MU, nc);
-    load_vec<MU>(c_tile + ((((size_t)sblk(t <= t_sh) * (T + 1) + t) * 4 + g) * 64 + lane) * MU, ncp);
+    for (int i = 0; i < MU; ++i) s.a[i] = *reinterpret_cast<const floatx4*>(ab + (g * MU + i) * 64);
+    const float* pc1 = c_tile + ((((size_t)sblk(t + 1 <= t_sh) * (T + 1) + t + 1) * 4 + g) * 64 + lane) * MU;
+    const float* pc0 = c_tile + ((((size_t)sblk(t <= t_sh) * (T + 1) + t) * 4 + g) * 64 + lane) * MU;
+    if constexpr (kDB) {
+      __builtin_memcpy(&s.c, pc1, MU * sizeof(float));
+      __builtin_memcpy(&s.cp, pc0, MU * sizeof(float));
+    } else {
+      load_vec<MU>(pc1, s.c.v);
+      load_vec<MU>(pc0, s.cp.v);
+    }
     if (decoder) {
       // dout2: the output gradient of peds >= bsplit is a separate (T x (B - bsplit) x 2) block
       const float* dp = (dout2 && pc >= bsplit) ? dout2 + ((size_t)t * (B - bsplit) + (pc - bsplit)) * 2
                                                 : dout + ((size_t)t * (dout2 ? bsplit : B) + pc) * 2;
       const float2 dv = *reinterpret_cast<const float2*>(dp);
-      nd0 = dv.x;
-      nd1 = dv.y;
+      s.d0 = dv.x;
+      s.d1 = dv.y;
     }
   };
 
@@ -1073,7 +1100,7 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
 #pragma unroll
     for (int k = 0; k < 4; ++k) db[i][k] = dax[i][k] = day[i][k] = 0.f;
 
-  load_step(T - 1);
+  load_step(T - 1, sa);
   float din_x = 0.f, din_y = 0.f;   // drel_in[t + 1] (wave 0, q = 0 lanes; every lane for the decoder's dWp)
   // decoder weight gradients of hidden2pos, lane-accumulated over the steps:
   // dWp += drel_tot[t] h_{t+1}^T (the lane's slots), dbp += drel_tot[t]
@@ -1086,20 +1113,29 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
   // skipped -- their input gradients are not wanted (the discriminator's
   // observed part in the generator step)
   LMARK(1);
-  for (int t = T - 1; t >= t_stop; --t) {
+  // (two sets (kDB, above) where the owners are the step's long pole; with
+  // the encoders' weight gradients the helpers are, and the owners' earlier
+  // start only took issue slots from them -- H = 48: 38.5 -> 42.8 us; the
+  // G-step's H = 48 input-gradient form 18.0 -> 16.8 us, the decoder's
+  // 19.1 -> 18.7 us)
+  // the step's loaded operands in two register sets used in turn (the loop
+  // runs two steps per iteration): a set is loaded one step ahead and read
+  // where it was loaded, no loop-carried copy -- a copy of a fresh load had
+  // the compiler wait for the prefetch inside the step that issued it
+  auto step = [&](int t, const StepIn& si, StepIn& so) {
     if (T - 1 - t < 60) LMARK(2 + T - 1 - t);
     const int cur = t & 1;
     LSUBB(0);
-    const float d0 = nd0, d1 = nd1, r0 = nr0, r1 = nr1;
+    const float d0 = si.d0, d1 = si.d1, r0 = si.r0, r1 = si.r1;
     floatx4 ca[MU];
-    float cc[MU], ccp[MU];
 #pragma unroll
-    for (int i = 0; i < MU; ++i) {
-      ca[i] = na[i];
-      cc[i] = nc[i];
-      ccp[i] = ncp[i];
-    }
-    if (t > t_stop) load_step(t - 1);   // in flight while this step computes
+    for (int i = 0; i < MU; ++i) ca[i] = si.a[i];
+    const CellV cc = si.c, ccp = si.cp;
+    // in flight while this step computes; with two sets unconditional (the
+    // last step re-reads a valid step): under a branch the compiler's wait
+    // counts at the join assumed the loads absent and waited for them inside
+    // this step
+    if (kDB || t > t_stop) load_step(t > 0 ? t - 1 : 0, so);
 
     float f0 = 0.f, f1 = 0.f;
     // drel_tot[t] = dout[t] + drel_in[t + 1] of this lane's ped (zero for a padded ped)
@@ -1224,7 +1260,20 @@ __global__ void __launch_bounds__(WGRAD ? 2 * kMwThreads : kMwThreads) lstm_mw_b
       din_x = sx;
       din_y = sy;
     }
+    };
+  if constexpr (kDB) {
+    for (int t = T - 1; t >= t_stop; t -= 2) {
+      step(t, sa, sb);
+      if (t - 1 < t_stop) break;
+      step(t - 1, sb, sa);
+    }
+  } else {
+    for (int t = T - 1; t >= t_stop; --t) {
+      const StepIn si = sa;
+      step(t, si, sa);
+    }
   }
+
   if (hacc) lds_barrier();   // the helpers' last drel_in partials (helper branch)
   if (t_stop > 0 && valid && g == 0 && q == 0) {   // the skipped steps' input gradients are defined as zero
     for (int t = 0; t < t_stop; ++t) *reinterpret_cast<float2*>(drel_in + ((size_t)t * B + ped) * 2) = make_float2(0.f, 0.f);
