@@ -499,9 +499,10 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
     one-iteration graph for the remainder, so run(k) does exactly k."""
     from sgan.train_step import GraphedTrainer
     if graph:
+        g1 = gk = None
+        err = None
         try:
             g1 = GraphedTrainer(trainer, batch, sc, warmup=2, batch_g=batch_g, sc_g=sc_g, overlap=OVERLAP, **kw)
-            gk = None
             if GRAPH_ITERS > 1 and not trainer.dp.segmented:
                 # (the timed trainer draws each replay's host RNG numbers
                 # while the previous replay runs: GraphedTrainer draw_ahead;
@@ -511,7 +512,21 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
                 gk = GraphedTrainer(trainer, batch, sc, warmup=0, batch_g=batch_g, sc_g=sc_g, iters=GRAPH_ITERS,
                                     draw_ahead=True, draws=g1.draws,
                                     overlap=OVERLAP, **kw)
-
+        except Exception as e:  # capture unsupported (e.g. a collective): eager
+            err = e
+        # every rank takes the same form: a rank that ran eager while the
+        # others replayed graphs would issue a different number of
+        # collectives before the timed run (the graphs' first replays below)
+        # and the job would hang in them.  Captures execute no collective, so
+        # up to here every rank ran the same warm-up iterations.
+        ok = err is None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            f = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)   # (the host-control group: gloo)
+            if ok and int(f.item()) == 0:
+                err = RuntimeError("graph capture failed on another rank")
+            ok = int(f.item()) == 1
+        if ok:
             if gk is not None:   # both graphs replayed once before any timing (first-replay costs)
                 gk.step()
                 g1.step()
@@ -524,9 +539,9 @@ def make_step(trainer, batch, sc, batch_g, sc_g, kw, graph, world=1):
                 for _ in range(k):
                     g1.step()
             return run, True, g1
-        except Exception as e:  # capture unsupported (e.g. a collective): eager
-            print("bench: graph capture failed (%s: %s); running eager" % (type(e).__name__, e), file=sys.stderr)
-            torch.cuda.synchronize()
+        print("bench: graph capture failed (%s: %s); running eager" % (type(err).__name__, err), file=sys.stderr)
+        g1 = gk = None
+        torch.cuda.synchronize()
     def eager(k):
         for _ in range(k):
             trainer.step(batch, sc, batch_g, sc_g, **kw)
